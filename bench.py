@@ -1,0 +1,232 @@
+#!/usr/bin/env python3
+"""Headline benchmark: training iterations/s of the reference's synthetic MLP (+ all-reduce bus GB/s).
+
+Metric (BASELINE.json): "iters/sec + allreduce bus GB/s, synthetic MLP at 1/2/4/8 MI355X".
+Config: the reference workload exactly — SimpleNet Linear(20,64)-ReLU-Linear(64,1), fp32,
+micro-batch 4 per rank, BCE-with-logits, Adam(lr=1e-3), DistributedSampler over the 2000x20
+synthetic dataset (seed 42), data-parallel over N ranks with a gradient all-reduce every step
+(weak scaling: per-rank work is fixed).  Every timed step does the full forward, loss, backward,
+cross-rank gradient reduction and optimizer update; nothing is cached or skipped.
+
+    python bench.py                                  # 1 GPU
+    torchrun --nproc-per-node N bench.py --gpus N    # N GPUs, one rank per GPU (RCCL/xGMI)
+
+``value`` is the whole-job aggregate: optimizer iterations per second summed over ranks
+(= N x global steps/s).  ``allreduce_busbw_GBps`` is the peak RCCL all-reduce bus bandwidth of a
+short size sweep run after the timed region (rccl-tests convention, busbw = algbw x 2(n-1)/n).
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+METRIC = "iters/sec + allreduce bus GB/s, synthetic MLP at 1/2/4/8 MI355X"
+
+
+def parse_args(argv=None):
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20000, help="timed optimizer steps")
+    ap.add_argument("--warmup", type=int, default=2000, help="untimed warmup steps")
+    ap.add_argument("--impl", default="fused", choices=["fused", "stepwise", "engine"],
+                    help="fused: one-launch HIP training kernel; stepwise: per-step HIP kernels + RCCL; "
+                         "engine: PyTorch eager + RCCL (the reference-equivalent stack)")
+    ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce bus bandwidth sweep")
+    ap.add_argument("--sweep-max-mb", type=int, default=256)
+    return ap.parse_known_args(argv)[0]
+
+
+def build_plan(trainer, n_steps: int):
+    plans, counts, e = [], [], 1
+    total = 0
+    while total < n_steps:
+        p, c = trainer.epoch_plan(e)
+        plans.append(p)
+        counts.append(c)
+        total += p.shape[0]
+        e += 1
+    return torch.cat(plans)[:n_steps].contiguous(), torch.cat(counts)[:n_steps].contiguous()
+
+
+def allreduce_sweep(device, max_mb: int, world: int):
+    """RCCL all-reduce bus bandwidth over message sizes (rccl-tests all_reduce_perf columns)."""
+    results = []
+    if world < 2:
+        return results
+    size = 8
+    while size <= max_mb * 1024 * 1024:
+        n = max(1, size // 4)
+        t = torch.ones(n, dtype=torch.float32, device=device)
+        iters = 20 if size <= (1 << 22) else 5
+        for _ in range(3):
+            dist.all_reduce(t)
+        torch.cuda.synchronize()
+        dist.barrier()
+        t0 = time.perf_counter()
+        for _ in range(iters):
+            dist.all_reduce(t)
+        torch.cuda.synchronize()
+        dt = (time.perf_counter() - t0) / iters
+        algbw = n * 4 / dt / 1e9
+        results.append({"bytes": n * 4, "us": dt * 1e6, "algbw_GBps": algbw,
+                        "busbw_GBps": algbw * 2 * (world - 1) / world})
+        size *= 4
+    return results
+
+
+def main(argv=None):
+    args = parse_args(argv)
+    from distributed_gpu_test_amd.data import make_synthetic_data
+    from distributed_gpu_test_amd.models import SimpleNet
+    from distributed_gpu_test_amd.parallel import comm
+    from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
+
+    info = comm.init_distributed()
+    world, rank = comm.get_world_size(), comm.get_rank()
+    if args.gpus != world:
+        print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
+    device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+
+    torch.manual_seed(42)
+    x, y = make_synthetic_data(2000, 20, 42)
+    model = SimpleNet(20, 64)
+    B = 4
+    if args.impl == "engine":
+        trainer = EngineBench(model, x, y, B, device)
+    else:
+        trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=args.impl if device.type == "cuda" else "torch",
+                                 device=device)
+    plan, counts = build_plan(trainer, args.warmup + args.steps)
+
+    # ---- warmup (untimed)
+    if args.warmup:
+        trainer.run_plan(plan[: args.warmup], counts[: args.warmup])
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    # ---- timed: exactly args.steps optimizer steps
+    trainer.loss_acc.zero_()
+    t0 = time.perf_counter()
+    trainer.run_plan(plan[args.warmup:], counts[args.warmup:])
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    trainer.check()
+    mean_loss = float(trainer.loss_acc.item()) / max(1, args.steps)
+    elapsed_max = comm.all_reduce_max(elapsed)
+
+    # every rank must hold identical parameters after DP training
+    consistent = True
+    if world > 1:
+        p = trainer.params.detach().clone()
+        ref = p.clone()
+        dist.broadcast(ref, 0)
+        flag = torch.tensor([0.0 if torch.equal(p, ref) else 1.0], device=p.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        consistent = flag.item() == 0.0
+
+    sweep = [] if (args.no_sweep or device.type != "cuda") else allreduce_sweep(device, args.sweep_max_mb, world)
+    peak_busbw = max((r["busbw_GBps"] for r in sweep), default=None)
+    small = min(sweep, key=lambda r: abs(r["bytes"] - 5632)) if sweep else None
+
+    ms = elapsed_max / args.steps * 1e3
+    global_steps_per_s = args.steps / elapsed_max
+    out = {
+        "metric": METRIC,
+        "value": round(world * global_steps_per_s, 2),
+        "unit": "iters/s (sum over ranks)",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(ms, 6),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "fp32",
+        "data": "synthetic (2000x20 N(0,1), seed 42; random-init SimpleNet)",
+        "config": {"model": "SimpleNet Linear(20,64)-ReLU-Linear(64,1) + BCEWithLogits + Adam(1e-3)",
+                   "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
+                   "micro_batch_per_gpu": B, "impl": trainer.impl, "exchange": trainer.exchange},
+        "global_steps_per_sec": round(global_steps_per_s, 2),
+        "samples_per_sec": round(global_steps_per_s * B * world, 2),
+        "mean_loss": round(mean_loss, 6),
+        "params_consistent_across_ranks": consistent,
+        "allreduce_busbw_GBps": None if peak_busbw is None else round(peak_busbw, 2),
+        "allreduce_5KB_us": None if small is None else round(small["us"], 2),
+        "allreduce_sweep": [{k: round(v, 3) for k, v in r.items()} for r in sweep],
+    }
+    if rank == 0:
+        print(json.dumps(out), flush=True)
+    trainer.close()
+    comm.destroy()
+
+
+class EngineBench:
+    """The reference-equivalent stack: nn.Module eager + autograd + RCCL all-reduce + torch Adam."""
+
+    impl = "engine"
+
+    def __init__(self, model, x, y, B, device):
+        from distributed_gpu_test_amd import data as dgt_data
+        from distributed_gpu_test_amd.parallel import comm
+        self.model = model.to(device)
+        self.device = device
+        self.x, self.y = x.to(device), y.to(device).reshape(-1, 1)
+        self.B = B
+        self.world = comm.get_world_size()
+        self.rank = comm.get_rank()
+        self._data = dgt_data
+        if self.world > 1:
+            for p in self.model.parameters():
+                dist.broadcast(p.data, 0)
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=1e-3)
+        self.crit = torch.nn.BCEWithLogitsLoss()
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=device)
+        self.params = torch.nn.utils.parameters_to_vector(self.model.parameters())
+        self.exchange = f"{comm.backend_name()}-allreduce" if self.world > 1 else "none"
+
+    def epoch_plan(self, epoch):
+        idx = self._data.shard_indices(self.x.shape[0], self.world, self.rank, epoch)
+        plan = self._data.batch_plan(idx, self.B)
+        return plan, (plan >= 0).sum(1).to(torch.int32)
+
+    def run_plan(self, plan, counts):
+        plan_d = plan.to(self.device).long()
+        for s in range(plan.shape[0]):
+            rows = plan_d[s, : int(counts[s])]
+            loss = self.crit(self.model(self.x[rows]), self.y[rows])
+            self.opt.zero_grad(set_to_none=True)
+            loss.backward()
+            if self.world > 1:
+                flat = torch.cat([p.grad.reshape(-1) for p in self.model.parameters()])
+                dist.all_reduce(flat)
+                flat.div_(self.world)
+                torch.nn.utils.vector_to_parameters(flat, [p.grad for p in self.model.parameters()])
+            self.opt.step()
+            self.loss_acc += loss.item()  # the reference's per-step host sync (train.py:115)
+        self.params = torch.nn.utils.parameters_to_vector(self.model.parameters()).detach()
+
+    def check(self):
+        pass
+
+    def close(self):
+        pass
+
+
+if __name__ == "__main__":
+    main()

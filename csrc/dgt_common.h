@@ -1,0 +1,110 @@
+// Shared device helpers for the MI355X (gfx950 / CDNA4) kernels of distributed_gpu_test_amd.
+// Wave64 everywhere: every cross-lane helper assumes 64 lanes.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#define DGT_HOST_DEVICE __host__ __device__ __forceinline__
+#define DGT_DEVICE __device__ __forceinline__
+
+namespace dgt {
+
+constexpr int kWave = 64;
+constexpr int kMaxRanks = 8;
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// ---- status words written by kernels (read by the host after a sync)
+enum Status : int {
+  kOk = 0,
+  kTimeout = 1,       // a cross-GPU spin exceeded its bound
+  kBadShape = 2,      // launch arguments disagree with what the kernel was built for
+};
+
+// Scalars are rounded to fp32 on the host from double, the way torch passes python floats to
+// its foreach kernels (1 - beta1 is computed in double, THEN rounded).
+struct AdamHyper {
+  float lr;
+  float beta2;
+  float one_minus_beta1;
+  float one_minus_beta2;
+  float eps;
+  float weight_decay;
+  float decay;  // 1 - lr * weight_decay (AdamW)
+  int adamw;    // 1: decoupled weight decay (AdamW); 0: L2 added to the gradient (torch.optim.Adam)
+};
+
+// Cross-GPU exchange arguments for the IPC one-shot gradient exchange.  Every rank owns one
+// "mailbox" allocation (uncached device memory, IPC-exported); peers write into it over xGMI.
+//   data  : float [2 parity][kMaxRanks src][stride]
+//   flags : uint32 [2 parity][kMaxRanks src]   (monotonic sequence numbers, never reset)
+struct Exchange {
+  int rank;
+  int world_size;
+  int stride;                       // floats per (parity, src) slot
+  long long seq_base;               // sequence number of the first exchange of this launch (0-based)
+  long long timeout_ticks;          // bound on every spin, in s_memrealtime ticks (100 MHz)
+  float* data[kMaxRanks];           // each rank's data region (index rank = local)
+  unsigned* flags[kMaxRanks];       // each rank's flag region
+};
+
+DGT_DEVICE float wave_sum16(float v) {  // sum over the 16 lanes sharing lane>>4
+  v += __shfl_xor(v, 1, 64);
+  v += __shfl_xor(v, 2, 64);
+  v += __shfl_xor(v, 4, 64);
+  v += __shfl_xor(v, 8, 64);
+  return v;
+}
+
+DGT_DEVICE float wave_sum_groups(float v) {  // sum over the 4 lane groups (lane, lane^16, lane^32, ...)
+  v += __shfl_xor(v, 16, 64);
+  v += __shfl_xor(v, 32, 64);
+  return v;
+}
+
+DGT_DEVICE float wave_sum(float v) {
+  return wave_sum_groups(wave_sum16(v));
+}
+
+DGT_DEVICE unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
+
+DGT_DEVICE void store_release_system(unsigned* p, unsigned v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+DGT_DEVICE unsigned load_relaxed_system(unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// Bounded spin until *p >= want (wrap-safe compare).  Returns false on timeout.
+DGT_DEVICE bool spin_geq(unsigned* p, unsigned want, long long timeout_ticks) {
+  const unsigned long long t0 = realtime();
+  while (true) {
+    unsigned cur = load_relaxed_system(p);
+    if ((int)(cur - want) >= 0) return true;
+    if ((long long)(realtime() - t0) > timeout_ticks) return false;
+    __builtin_amdgcn_s_sleep(1);
+  }
+}
+
+// torch.lerp for weight < 0.5 (what Adam's exp_avg.lerp_(grad, 1 - beta1) evaluates)
+DGT_DEVICE float lerp_torch(float self, float end, float w) {
+  return (fabsf(w) < 0.5f) ? fmaf(w, end - self, self) : end - (end - self) * (1.0f - w);
+}
+
+// One Adam/AdamW update of a single element, in the op order of torch's foreach Adam
+// (torch/optim/adam.py _multi_tensor_adam: lerp_, mul_, addcmul_, sqrt, div_, add_, addcdiv_).
+DGT_DEVICE float adam_update(float p, float g, float& m, float& v, const AdamHyper& h,
+                             float step_size_neg, float bc2_sqrt) {
+  if (h.weight_decay != 0.f) {
+    if (h.adamw) p = p * h.decay;
+    else g = fmaf(h.weight_decay, p, g);
+  }
+  m = lerp_torch(m, g, h.one_minus_beta1);
+  v = v * h.beta2;
+  v = v + h.one_minus_beta2 * g * g;
+  const float denom = sqrtf(v) / bc2_sqrt + h.eps;
+  return p + step_size_neg * (m / denom);
+}
+
+}  // namespace dgt

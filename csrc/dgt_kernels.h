@@ -1,0 +1,77 @@
+// Host-side launch API of the HIP kernels (no torch headers: the .hip translation units compile fast
+// and the torch binding layer in bindings.cpp only sees these declarations).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "dgt_common.h"
+
+namespace dgt {
+
+// ---------------------------------------------------------------- tiny MLP (reference model)
+// Which (n_features, hidden) pairs have a compiled fused kernel.
+bool tiny_mlp_supported(int n_features, int hidden);
+int tiny_mlp_padded_numel(int n_features, int hidden);  // flat length incl. float4 padding
+
+struct TinyTrainArgs {
+  const float* X;        // [n_samples, F]
+  const float* Y;        // [n_samples]
+  const int* plan;       // [n_steps, bmax] sample indices, -1 = padding
+  const int* counts;     // [n_steps] valid rows per step
+  int n_steps;
+  int bmax;              // <= 16
+  float* params;         // [padded numel] flat: W1[H,F], b1[H], W2[H], b2
+  float* exp_avg;        // [padded numel]
+  float* exp_avg_sq;     // [padded numel]
+  AdamHyper hp;
+  double lr;             // python-double lr (bias-corrected step size is formed in double)
+  double beta1, beta2;
+  long long adam_step0;  // optimizer steps already taken before this launch
+  double* loss_acc;      // += sum over steps of the step's mean loss
+  int* status;           // Status
+  Exchange ex;           // world_size 1 -> no exchange
+};
+
+hipError_t tiny_mlp_train(int n_features, int hidden, const TinyTrainArgs& a, hipStream_t stream);
+
+struct TinyGradArgs {
+  const float* X;
+  const float* Y;
+  const int* plan;       // [n_steps, bmax]
+  const int* counts;     // [n_steps]
+  int step;              // which row of the plan
+  int bmax;
+  const float* params;   // flat (padded)
+  float* grad;           // flat (padded), overwritten
+  double* loss_acc;      // += this step's mean loss
+};
+
+hipError_t tiny_mlp_grad(int n_features, int hidden, const TinyGradArgs& a, hipStream_t stream);
+
+// ---------------------------------------------------------------- flat fused Adam
+enum DType : int { kF32 = 0, kBF16 = 1, kF16 = 2 };
+
+struct AdamFlatArgs {
+  float* master;         // fp32 master params [n]
+  void* param_lp;        // optional low-precision copy (nullptr = none)
+  int lp_dtype;          // DType of param_lp
+  const void* grad;      // [n]
+  int grad_dtype;        // DType
+  float* exp_avg;
+  float* exp_avg_sq;
+  long long n;           // multiple of 4
+  AdamHyper hp;
+  float step_size_neg;   // -lr / (1 - beta1^t)
+  float bc2_sqrt;        // sqrt(1 - beta2^t)
+  float grad_scale;      // multiplies the gradient (1/world_size, 1/loss_scale ...)
+  const float* grad_scale_dev;  // optional extra device-side multiplier (clip coefficient)
+};
+
+hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream);
+
+// ---------------------------------------------------------------- IPC one-shot all-reduce
+// in[n] (fp32) from every rank -> out[n] = scale * sum over ranks (rank order, identical bits on
+// every rank).  Uses the Exchange mailboxes; n <= ex.stride.
+hipError_t oneshot_allreduce(const float* in, float* out, long long n, float scale, const Exchange& ex,
+                             int* status, hipStream_t stream);
+
+}  // namespace dgt

@@ -1,0 +1,52 @@
+"""Loader for the in-tree native extension ``distributed_gpu_test_amd/_C.so``.
+
+The extension registers ``torch.ops.dgt.*`` (HIP kernels for gfx950 + the IPC runtime).  It is
+built by ``python tools/build_ext.py`` (or ``__graft_entry__.build()``).  On a machine with a GPU a
+missing extension is an error, never a silent fallback: ``require()`` raises.
+"""
+from __future__ import annotations
+
+import os
+import threading
+
+import torch
+
+_PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(_PKG, "_C.so")
+_lock = threading.Lock()
+_loaded = False
+_error: Exception | None = None
+
+
+def load() -> bool:
+    """Load the extension if it exists; returns whether ``torch.ops.dgt`` is usable."""
+    global _loaded, _error
+    with _lock:
+        if _loaded:
+            return True
+        if not os.path.exists(LIB_PATH):
+            _error = FileNotFoundError(
+                f"native extension not built: {LIB_PATH} missing (run `python tools/build_ext.py`)")
+            return False
+        try:
+            torch.ops.load_library(LIB_PATH)
+            _loaded = True
+        except Exception as e:  # pragma: no cover - only on a broken build
+            _error = e
+            return False
+        return True
+
+
+def available() -> bool:
+    return load()
+
+
+def require():
+    """Return ``torch.ops.dgt``; raise if the extension cannot be loaded."""
+    if not load():
+        raise RuntimeError(f"distributed_gpu_test_amd native extension unavailable: {_error}")
+    return torch.ops.dgt
+
+
+def gpu_available() -> bool:
+    return torch.cuda.is_available()

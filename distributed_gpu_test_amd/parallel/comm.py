@@ -1,0 +1,116 @@
+"""Process-group setup and thin collective helpers.
+
+Replaces ``deepspeed.init_distributed()`` + ``get_accelerator().set_device`` (``train.py:59-61``;
+SURVEY X2/X3).  Backend choice: ``nccl`` — which IS RCCL on ROCm, riding xGMI between the GPUs of
+a node — whenever a GPU is present, ``gloo`` otherwise (the CPU plumbing config of BASELINE.json).
+No MPI discovery: rank info comes from ``launch.resolve_rank_info`` (torchrun env, SLURM env or a
+bare single process).
+"""
+from __future__ import annotations
+
+import datetime
+import os
+from dataclasses import replace
+from typing import Any, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..launch import RankInfo, free_port, resolve_rank_info
+
+_RANK_INFO: Optional[RankInfo] = None
+
+
+def default_backend() -> str:
+    return "nccl" if torch.cuda.is_available() else "gloo"
+
+
+def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
+                     rank_info: Optional[RankInfo] = None, set_device: bool = True) -> RankInfo:
+    """Create the default process group (idempotent) and bind this rank's GPU."""
+    global _RANK_INFO
+    info = rank_info or resolve_rank_info()
+    if info.source == "bare" and not info.master_port:
+        info = replace(info, master_port=free_port(info.master_addr))
+    info.export()
+    backend = backend or default_backend()
+    if backend == "nccl":
+        if not torch.cuda.is_available():
+            raise RuntimeError("backend 'nccl' (RCCL) requested but no GPU is visible")
+        if set_device:
+            torch.cuda.set_device(info.local_rank % max(torch.cuda.device_count(), 1))
+        # hangs become errors instead of silent stalls
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+    if not dist.is_initialized():
+        dist.init_process_group(backend=backend, init_method="env://", rank=info.rank,
+                                world_size=info.world_size,
+                                timeout=datetime.timedelta(seconds=timeout_s))
+    _RANK_INFO = info
+    return info
+
+
+def rank_info() -> RankInfo:
+    if _RANK_INFO is not None:
+        return _RANK_INFO
+    return resolve_rank_info()
+
+
+def is_initialized() -> bool:
+    return dist.is_available() and dist.is_initialized()
+
+
+def get_rank() -> int:
+    return dist.get_rank() if is_initialized() else 0
+
+
+def get_world_size() -> int:
+    return dist.get_world_size() if is_initialized() else 1
+
+
+def backend_name() -> str:
+    return dist.get_backend() if is_initialized() else "none"
+
+
+def barrier() -> None:
+    if is_initialized() and get_world_size() > 1:
+        if backend_name() == "nccl":
+            dist.barrier(device_ids=[torch.cuda.current_device()])
+        else:
+            dist.barrier()
+
+
+def all_gather_object(obj: Any) -> List[Any]:
+    if not is_initialized() or get_world_size() == 1:
+        return [obj]
+    out: List[Any] = [None] * get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
+def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
+    if is_initialized() and get_world_size() > 1:
+        dist.broadcast(t, src)
+    return t
+
+
+def all_reduce_max(value: float, device: Optional[torch.device] = None) -> float:
+    if not is_initialized() or get_world_size() == 1:
+        return float(value)
+    dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
+                                             if backend_name() == "nccl" else torch.device("cpu"))
+    t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def destroy() -> None:
+    """Reference teardown (``train.py:131-140``): barrier, destroy, swallow errors of dead peers."""
+    try:
+        barrier()
+    except Exception:
+        pass
+    try:
+        if is_initialized():
+            dist.destroy_process_group()
+    except Exception:
+        pass

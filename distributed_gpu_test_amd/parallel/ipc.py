@@ -1,0 +1,147 @@
+"""IPC mailboxes for the one-shot xGMI exchange (``csrc/comm.hip``, ``csrc/tiny_mlp.hip``).
+
+Each rank allocates ONE uncached device buffer (``hipExtMallocWithFlags(hipDeviceMallocUncached)``:
+peers' writes land in HBM and are read without stale cache lines), exports it with
+``hipIpcGetMemHandle``, and every rank maps every peer's buffer (``hipIpcOpenMemHandle``).  The
+handles travel over the already-initialised process group (``all_gather_object``), so no extra
+rendezvous is needed.
+
+Buffer layout (bytes):  [ data : float[2][8][stride] ][ flags : uint32[64 blocks][2][8] ]
+
+A channel carries a monotonically increasing sequence number per exchange; the kernels poll
+``flag >= seq + 1`` so buffers are zeroed only once, at creation.
+
+Before the channel is trusted, ``selftest`` runs a one-shot all-reduce with a bounded spin and
+compares it against the process group's own all-reduce (RCCL).  Any mismatch or timeout on any
+rank disables the channel everywhere and callers fall back to RCCL.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..ops._ext import require
+from . import comm
+
+MAX_RANKS = 8
+MAX_BLOCKS = 64
+TICKS_PER_SECOND = 100_000_000  # s_memrealtime runs at 100 MHz
+
+
+class IpcChannel:
+    def __init__(self, stride_floats: int, device: Optional[torch.device] = None, timeout_s: float = 30.0,
+                 group=None):
+        if not torch.cuda.is_available():
+            raise RuntimeError("IpcChannel needs a GPU")
+        self.ops = require()
+        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.rank = comm.get_rank()
+        self.world_size = comm.get_world_size()
+        if self.world_size > MAX_RANKS:
+            raise ValueError(f"one-shot exchange supports up to {MAX_RANKS} ranks (one xGMI hop)")
+        self.stride = (int(stride_floats) + 63) // 64 * 64
+        self.data_bytes = 2 * MAX_RANKS * self.stride * 4
+        self.flag_bytes = MAX_BLOCKS * 2 * MAX_RANKS * 4
+        self.nbytes = self.data_bytes + self.flag_bytes
+        self.timeout_ticks = int(timeout_s * TICKS_PER_SECOND)
+        self.seq = 0
+        self.local_ptr = 0
+        self.base_ptrs: List[int] = []
+        self._opened: List[int] = []
+        self.error: Optional[BaseException] = None
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        handle = b""
+        try:
+            self.local_ptr = self.ops.ipc_alloc(self.nbytes, True, self.device.index)
+            handle = bytes(self.ops.ipc_handle(self.local_ptr).numpy().tobytes())
+        except Exception as e:  # IPC not supported here: every rank must learn it below
+            self.error = e
+        handles = comm.all_gather_object(handle)
+        if self.error is None:
+            try:
+                for r, h in enumerate(handles):
+                    if r == self.rank:
+                        self.base_ptrs.append(self.local_ptr)
+                    elif not h:
+                        raise RuntimeError(f"rank {r} could not export its mailbox")
+                    else:
+                        t = torch.frombuffer(bytearray(h), dtype=torch.uint8)
+                        p = self.ops.ipc_open(t, self.device.index)
+                        self._opened.append(p)
+                        self.base_ptrs.append(p)
+            except Exception as e:
+                self.error = e
+        # every rank agrees on usability before anybody launches a kernel that waits on peers
+        bad = torch.tensor([0.0 if self.error is None else 1.0], device=self.device)
+        if self.world_size > 1:
+            dist.all_reduce(bad, op=dist.ReduceOp.MAX)
+        self.healthy = bad.item() == 0.0
+        self.data_ptrs = list(self.base_ptrs) if self.healthy else []
+        self.flag_ptrs = [p + self.data_bytes for p in self.base_ptrs] if self.healthy else []
+
+    # ------------------------------------------------------------------ one-shot all-reduce
+    def next_seq(self, n: int = 1) -> int:
+        s = self.seq
+        self.seq += n
+        return s
+
+    def allreduce(self, inp: torch.Tensor, out: Optional[torch.Tensor] = None, scale: float = 1.0) -> torch.Tensor:
+        out = inp if out is None else out
+        self.ops.oneshot_allreduce(inp, out, float(scale), self.data_ptrs, self.flag_ptrs, self.rank,
+                                   self.world_size, self.stride, self.next_seq(), self.timeout_ticks, self.status)
+        return out
+
+    def check_status(self) -> int:
+        return int(self.status.item())
+
+    def selftest(self, n: int = 4096, timeout_s: float = 10.0) -> bool:
+        """Compare one-shot results with the process group's all-reduce; agree across ranks."""
+        if not self.healthy:
+            return False
+        ok = True
+        saved = self.timeout_ticks
+        self.timeout_ticks = int(timeout_s * TICKS_PER_SECOND)
+        n = min(n, self.stride) // 4 * 4
+        g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
+        x = torch.randn(n, generator=g).to(self.device)
+        ref = x.clone()
+        dist.all_reduce(ref)  # unconditional: every rank issues the same collectives
+        try:
+            got = torch.empty_like(x)
+            for _ in range(3):  # both parities + a wrap of the first
+                self.allreduce(x, got, 1.0)
+            torch.cuda.synchronize(self.device)
+            if self.check_status() != 0:
+                ok = False
+            if ok and not torch.allclose(got, ref, rtol=1e-5, atol=1e-5):
+                ok = False
+        except Exception:
+            ok = False
+        finally:
+            self.timeout_ticks = saved
+        flag = torch.tensor([0.0 if ok else 1.0], device=self.device)
+        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+        self.healthy = flag.item() == 0.0
+        self.status.zero_()
+        return self.healthy
+
+    def close(self) -> None:
+        for p in self._opened:
+            try:
+                self.ops.ipc_close(p)
+            except Exception:
+                pass
+        self._opened = []
+        if self.local_ptr:
+            try:
+                self.ops.ipc_free(self.local_ptr)
+            except Exception:
+                pass
+            self.local_ptr = 0
+
+
+def ipc_disabled_by_env() -> bool:
+    return os.environ.get("DGT_DISABLE_IPC", "0") not in ("", "0", "false", "False")

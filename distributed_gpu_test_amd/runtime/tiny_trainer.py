@@ -1,0 +1,231 @@
+"""Device-resident trainer for the reference model (the fused HIP path of ``train.py``).
+
+The reference's hot loop (``train.py:99-117``) does, per step: DataLoader collate on the CPU, two
+H2D copies, ~30 ATen/cuBLAS launches, a DeepSpeed flatten -> NCCL all-reduce -> unflatten, seven
+foreach-Adam launches and a blocking ``loss.item()``.  This trainer keeps the whole problem on the
+GPU instead:
+
+* dataset, parameters and Adam moments live in HBM for the whole run; the sampler's per-epoch
+  index plan (bit-exact ``DistributedSampler``) is uploaded once per epoch;
+* ``impl="fused"``: ONE kernel launch per epoch runs every step (``csrc/tiny_mlp.hip``),
+  exchanging gradients with the peers through the IPC mailboxes over xGMI when world_size > 1;
+* ``impl="stepwise"``: per step a fused fwd+bwd kernel -> RCCL all-reduce -> fused flat Adam
+  (the path used when IPC is unavailable; also the A/B baseline for the fused kernel);
+* ``impl="torch"``: the same math in plain PyTorch (CPU / gloo, and the numerics reference).
+
+The epoch's mean loss is accumulated on the device and read once per epoch, giving the same
+printed value as the reference's per-step ``loss.item()`` sum.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional
+
+import torch
+import torch.distributed as dist
+
+from .. import data as dgt_data
+from ..models.simple_net import SimpleNet, pack_simple_net, simple_net_layout, simple_net_numel
+from ..ops import _ext
+from ..ops.adam import adam_flat_
+from ..ops.reference import adam_flat_reference_, tiny_mlp_step_reference
+from ..parallel import comm
+from . import checkpoint as ckpt
+from .optim_state import adam_state_to_flat, flat_to_adam_state
+
+IMPLS = ("auto", "fused", "stepwise", "torch")
+
+
+def fused_supported(n_features: int, hidden: int, batch_size: int) -> bool:
+    if not (torch.cuda.is_available() and _ext.available()):
+        return False
+    return bool(_ext.require().tiny_mlp_supported(n_features, hidden)) and batch_size <= 16
+
+
+class TinyMLPTrainer:
+    def __init__(self, model: SimpleNet, x: torch.Tensor, y: torch.Tensor, batch_size: int = 4,
+                 lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
+                 adamw: bool = False, device: Optional[torch.device] = None, impl: str = "auto",
+                 sampler_seed: int = 0, ds_config: Optional[Dict[str, Any]] = None, use_ipc: bool = True,
+                 exchange_timeout_s: float = 60.0):
+        if impl not in IMPLS:
+            raise ValueError(f"impl must be one of {IMPLS}")
+        self.F = model.n_features
+        self.H = model.hidden
+        self.B = batch_size
+        self.device = device or (torch.device("cuda", torch.cuda.current_device())
+                                 if torch.cuda.is_available() else torch.device("cpu"))
+        self.rank = comm.get_rank()
+        self.world_size = comm.get_world_size()
+        self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
+        self.weight_decay, self.adamw = float(weight_decay), bool(adamw)
+        self.sampler_seed = sampler_seed
+        self.ds_config = ds_config or {}
+        self.global_steps = 0
+        self.global_samples = 0
+        self.channel = None
+
+        if impl == "auto":
+            impl = "fused" if (self.device.type == "cuda" and fused_supported(self.F, self.H, self.B)) else (
+                "torch" if self.device.type == "cpu" else "stepwise")
+        if impl in ("fused", "stepwise"):
+            if self.device.type != "cuda":
+                raise RuntimeError(f"impl={impl!r} needs a GPU")
+            if not fused_supported(self.F, self.H, self.B):
+                raise RuntimeError(f"no fused kernel for F={self.F} H={self.H} B={self.B}")
+        self.impl = impl
+
+        self.numel = simple_net_numel(self.F, self.H)
+        self.padded = (self.numel + 3) // 4 * 4
+        self.segments = [(off, shp) for _, shp, off in simple_net_layout(self.F, self.H)]
+        flat = torch.zeros(self.padded, dtype=torch.float32)
+        flat[: self.numel] = pack_simple_net(model)
+        self.params = flat.to(self.device)
+        if self.world_size > 1:  # DeepSpeed broadcasts the model from rank 0 at initialize
+            dist.broadcast(self.params, 0)
+        self.exp_avg = torch.zeros_like(self.params)
+        self.exp_avg_sq = torch.zeros_like(self.params)
+        self.grad = torch.zeros_like(self.params)
+        self.model = model
+        self.x = x.to(self.device, torch.float32).contiguous()
+        self.y = y.to(self.device, torch.float32).reshape(-1).contiguous()
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        self.exchange_timeout_s = exchange_timeout_s
+
+        if self.impl == "fused" and self.world_size > 1:
+            self.channel = self._open_channel() if use_ipc else None
+            if self.channel is None:
+                self.impl = "stepwise"
+
+    # ------------------------------------------------------------------ setup helpers
+    def _open_channel(self):
+        from ..parallel.ipc import IpcChannel, ipc_disabled_by_env
+        if ipc_disabled_by_env() or self.world_size > 8:
+            return None
+        try:
+            ch = IpcChannel(self.padded, self.device, timeout_s=self.exchange_timeout_s)
+        except Exception:
+            return None
+        if not ch.selftest():
+            ch.close()
+            return None
+        return ch
+
+    @property
+    def exchange(self) -> str:
+        if self.world_size == 1:
+            return "none"
+        if self.impl == "fused":
+            return "ipc-oneshot-xgmi"
+        return f"{comm.backend_name()}-allreduce"
+
+    def steps_per_epoch(self) -> int:
+        return dgt_data.steps_per_epoch(self.x.shape[0], self.world_size, self.B)
+
+    def epoch_plan(self, epoch: int):
+        idx = dgt_data.shard_indices(self.x.shape[0], self.world_size, self.rank, epoch, self.sampler_seed)
+        plan = dgt_data.batch_plan(idx, self.B)
+        counts = (plan >= 0).sum(1).to(torch.int32)
+        return plan.to(self.device), counts.to(self.device)
+
+    # ------------------------------------------------------------------ training
+    def run_plan(self, plan: torch.Tensor, counts: torch.Tensor) -> None:
+        """Run len(plan) optimizer steps (asynchronously on GPU); loss accumulates into loss_acc."""
+        n = int(plan.shape[0])
+        if n == 0:
+            return
+        if self.impl == "fused":
+            ops = _ext.require()
+            ch = self.channel
+            seq = ch.next_seq(n) if ch is not None else 0
+            ops.tiny_mlp_train(self.x, self.y, plan, counts, self.params, self.exp_avg, self.exp_avg_sq,
+                               self.loss_acc, self.status, self.F, self.H, self.lr, self.betas[0], self.betas[1],
+                               self.eps, self.weight_decay, self.adamw, self.global_steps,
+                               ch.data_ptrs if ch else [], ch.flag_ptrs if ch else [], self.rank,
+                               self.world_size, ch.stride if ch else 0, seq,
+                               ch.timeout_ticks if ch else 0)
+            self.global_steps += n
+        elif self.impl == "stepwise":
+            ops = _ext.require()
+            for s in range(n):
+                ops.tiny_mlp_grad(self.x, self.y, plan, counts, s, self.params, self.grad, self.loss_acc,
+                                  self.F, self.H)
+                if self.world_size > 1:
+                    dist.all_reduce(self.grad)
+                self.global_steps += 1
+                adam_flat_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, self.global_steps, self.lr,
+                           self.betas[0], self.betas[1], self.eps, self.weight_decay, self.adamw,
+                           grad_scale=1.0 / self.world_size)
+        else:
+            plan_c, counts_c = plan.cpu(), counts.cpu()
+            for s in range(n):
+                rows = plan_c[s, : int(counts_c[s])].long().to(self.device)
+                loss, g = tiny_mlp_step_reference(self.params, self.x[rows], self.y[rows], self.F, self.H,
+                                                  grad_out=self.grad)
+                self.loss_acc += loss
+                if self.world_size > 1:
+                    dist.all_reduce(self.grad)
+                self.global_steps += 1
+                adam_flat_reference_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, self.global_steps,
+                                     self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay,
+                                     self.adamw, grad_scale=1.0 / self.world_size)
+        self.global_samples += n * self.B * self.world_size
+
+    def check(self) -> None:
+        """Raise if a kernel reported a failure (cross-GPU timeout, bad shape)."""
+        if self.device.type == "cuda":
+            st = int(self.status.item())
+            if st != 0:
+                raise RuntimeError(f"fused training kernel failed with status {st} "
+                                   f"({'cross-GPU exchange timeout' if st == 1 else 'bad launch shape'})")
+
+    def run_epoch(self, epoch: int) -> float:
+        plan, counts = self.epoch_plan(epoch)
+        self.loss_acc.zero_()
+        self.run_plan(plan, counts)
+        loss_sum = float(self.loss_acc.item())  # the epoch's single host sync
+        self.check()
+        return loss_sum / max(1, int(plan.shape[0]))
+
+    # ------------------------------------------------------------------ state
+    def sync_model(self) -> SimpleNet:
+        flat = self.params[: self.numel].detach().cpu()
+        with torch.no_grad():
+            off = 0
+            for p in self.model.parameters():
+                n = p.numel()
+                p.copy_(flat[off:off + n].view_as(p))
+                off += n
+        return self.model
+
+    def optimizer_state_dict(self) -> Dict[str, Any]:
+        return flat_to_adam_state(self.exp_avg, self.exp_avg_sq, self.segments, self.global_steps, self.lr,
+                                  self.betas, self.eps, self.weight_decay, self.adamw)
+
+    def save_checkpoint(self, save_dir: str, tag: Optional[str] = None, client_state: Optional[dict] = None) -> str:
+        self.sync_model()
+        return ckpt.save(save_dir, tag, self.global_steps,
+                         {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()},
+                         self.optimizer_state_dict(),
+                         {"global_samples": self.global_samples, "dp_world_size": self.world_size,
+                          "client_state": client_state or {}},
+                         self.ds_config)
+
+    def load_checkpoint(self, load_dir: str, tag: Optional[str] = None, load_optimizer_states: bool = True):
+        path, states, _ = ckpt.load(load_dir, tag)
+        if states is None:
+            return None, None
+        self.model.load_state_dict(states["module"])
+        self.params[: self.numel].copy_(pack_simple_net(self.model).to(self.device))
+        if load_optimizer_states and states.get("optimizer"):
+            step = adam_state_to_flat(states["optimizer"], self.exp_avg, self.exp_avg_sq, self.segments)
+            self.global_steps = int(states.get("global_steps", step))
+        else:
+            self.global_steps = int(states.get("global_steps", 0))
+        self.global_samples = int(states.get("global_samples", 0))
+        return path, states.get("client_state", {})
+
+    def close(self) -> None:
+        if self.channel is not None:
+            self.channel.close()
+            self.channel = None

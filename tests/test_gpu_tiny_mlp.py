@@ -1,0 +1,96 @@
+"""GPU numerics of the fused tiny-MLP kernels vs plain-PyTorch fp32 references."""
+import pytest
+import torch
+
+from distributed_gpu_test_amd.data import make_synthetic_data
+from distributed_gpu_test_amd.models import SimpleNet
+from distributed_gpu_test_amd.ops import _ext, adam_flat_, adam_flat_reference_, tiny_mlp_step_reference
+from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
+
+pytestmark = pytest.mark.gpu
+
+ORACLE_WS1 = [0.4301, 0.1461, 0.0865, 0.0637, 0.0516]
+
+
+def _setup(F=20, H=64, n=2000, seed=42):
+    torch.manual_seed(seed)
+    x, y = make_synthetic_data(n, F, seed)
+    return x, y, SimpleNet(F, H)
+
+
+def test_extension_loaded_on_gpu():
+    assert _ext.available(), "native extension must load on a GPU box"
+    assert torch.ops.dgt.tiny_mlp_supported(20, 64)
+
+
+@pytest.mark.parametrize("F,H,B", [(20, 64, 4), (20, 64, 3), (32, 64, 16), (8, 16, 1), (20, 128, 7)])
+def test_grad_kernel_matches_reference(F, H, B):
+    dev = torch.device("cuda")
+    x, y, m = _setup(F, H, 64)
+    tr = TinyMLPTrainer(m, x, y, batch_size=B, impl="stepwise")
+    plan, counts = tr.epoch_plan(1)
+    ops = _ext.require()
+    g = torch.zeros_like(tr.params)
+    loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
+    ops.tiny_mlp_grad(tr.x, tr.y, plan, counts, 0, tr.params, g, loss_acc, F, H)
+    rows = plan[0, : int(counts[0])].long()
+    ref_loss, ref_g = tiny_mlp_step_reference(tr.params.double(), tr.x[rows].double(), tr.y[rows].double(), F, H)
+    torch.cuda.synchronize()
+    assert abs(loss_acc.item() - ref_loss) < 1e-5
+    torch.testing.assert_close(g.double(), ref_g, rtol=1e-4, atol=1e-6)
+
+
+def test_fused_epoch_matches_torch_reference():
+    x, y, m = _setup()
+    _, _, m_ref = _setup()  # same seed -> identical init
+    ref = TinyMLPTrainer(m_ref, x, y, 4, impl="torch", device=torch.device("cuda"))
+    fused = TinyMLPTrainer(m, x, y, 4, impl="fused")
+    torch.testing.assert_close(fused.params, ref.params)
+    l_ref = ref.run_epoch(1)
+    l_fused = fused.run_epoch(1)
+    assert abs(l_ref - l_fused) < 1e-5
+    torch.testing.assert_close(fused.params, ref.params, rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(fused.exp_avg_sq, ref.exp_avg_sq, rtol=1e-3, atol=1e-9)
+
+
+def test_fused_reproduces_reference_oracle_ws1():
+    x, y, m = _setup()
+    tr = TinyMLPTrainer(m, x, y, 4, impl="fused")
+    losses = [round(tr.run_epoch(e), 4) for e in range(1, 6)]
+    assert losses == ORACLE_WS1
+
+
+def test_stepwise_matches_fused():
+    x, y, m1 = _setup()
+    _, _, m2 = _setup()
+    a = TinyMLPTrainer(m1, x, y, 4, impl="fused")
+    b = TinyMLPTrainer(m2, x, y, 4, impl="stepwise")
+    for e in (1, 2):
+        la, lb = a.run_epoch(e), b.run_epoch(e)
+        assert abs(la - lb) < 1e-5
+    torch.testing.assert_close(a.params, b.params, rtol=1e-4, atol=1e-6)
+
+
+@pytest.mark.parametrize("gdt,lpdt", [(torch.float32, None), (torch.bfloat16, torch.bfloat16),
+                                       (torch.float16, torch.float16), (torch.float32, torch.bfloat16)])
+@pytest.mark.parametrize("wd,adamw", [(0.0, False), (0.01, False), (0.01, True)])
+def test_adam_flat_matches_reference(gdt, lpdt, wd, adamw):
+    n = 4096 * 3 + 8
+    g = torch.Generator().manual_seed(0)
+    p = torch.randn(n, generator=g).cuda()
+    grads = [torch.randn(n, generator=g).cuda().to(gdt) for _ in range(3)]
+    m = torch.zeros(n, device="cuda")
+    v = torch.zeros(n, device="cuda")
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    lp = torch.empty(n, device="cuda", dtype=lpdt) if lpdt else None
+    scale = torch.tensor([0.5], device="cuda")
+    for step, gr in enumerate(grads, 1):
+        adam_flat_(p, gr, m, v, step, 1e-3, 0.9, 0.999, 1e-8, wd, adamw, grad_scale=0.25, grad_scale_dev=scale,
+                   param_lp=lp)
+        adam_flat_reference_(p2, gr, m2, v2, step, 1e-3, 0.9, 0.999, 1e-8, wd, adamw, grad_scale=0.25,
+                             grad_scale_dev=scale)
+    torch.testing.assert_close(p, p2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m, m2, rtol=1e-5, atol=1e-7)
+    torch.testing.assert_close(v, v2, rtol=1e-5, atol=1e-9)
+    if lp is not None:
+        torch.testing.assert_close(lp, p2.to(lpdt))
