@@ -2,8 +2,8 @@
 // Host-only translation unit: validates shapes/devices, picks the current HIP stream, and calls
 // the launch functions declared in dgt_kernels.h.  Every op fails loudly on a non-GPU tensor.
 #include <ATen/ATen.h>
-#include <c10/hip/HIPStream.h>
-#include <c10/hip/HIPGuard.h>
+#include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
+#include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
 #include <cstring>
@@ -26,7 +26,7 @@ void check_gpu(const at::Tensor& t, const char* name, at::ScalarType dt) {
 }
 
 hipStream_t stream_of(const at::Tensor& t) {
-  return c10::hip::getCurrentHIPStream(t.device().index()).stream();
+  return at::hip::getCurrentHIPStreamMasqueradingAsCUDA(t.device().index()).stream();
 }
 
 dgt::AdamHyper make_hyper(double lr, double beta1, double beta2, double eps, double wd, bool adamw) {
@@ -102,7 +102,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   TORCH_CHECK(Y.numel() == X.size(0), "dgt: Y must have one label per row of X");
   TORCH_CHECK(plan.dim() == 2 && plan.size(1) >= 1 && plan.size(1) <= 16, "dgt: plan must be [steps, bmax<=16]");
   TORCH_CHECK(counts.numel() == plan.size(0), "dgt: counts must have one entry per plan row");
-  c10::hip::HIPGuard guard(X.device());
+  c10::DeviceGuard guard(X.device());
   dgt::TinyTrainArgs a;
   a.X = X.data_ptr<float>();
   a.Y = Y.data_ptr<float>();
@@ -142,7 +142,7 @@ void tiny_mlp_grad(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& p
   TORCH_CHECK(params.numel() >= pp && grad.numel() >= pp, "dgt: flat buffers need ", pp, " elements");
   TORCH_CHECK(plan.dim() == 2 && plan.size(1) <= 16 && step >= 0 && step < plan.size(0), "dgt: bad plan/step");
   TORCH_CHECK(X.dim() == 2 && X.size(1) == n_features, "dgt: X must be [N, ", n_features, "]");
-  c10::hip::HIPGuard guard(X.device());
+  c10::DeviceGuard guard(X.device());
   dgt::TinyGradArgs a;
   a.X = X.data_ptr<float>();
   a.Y = Y.data_ptr<float>();
@@ -169,7 +169,7 @@ void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_
   TORCH_CHECK(n % 4 == 0, "dgt: flat buffers must be padded to a multiple of 4 elements");
   TORCH_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "dgt: flat size mismatch");
   TORCH_CHECK(step >= 1, "dgt: adam step must be >= 1");
-  c10::hip::HIPGuard guard(master.device());
+  c10::DeviceGuard guard(master.device());
   dgt::AdamFlatArgs a;
   a.master = master.data_ptr<float>();
   a.param_lp = nullptr;
@@ -207,7 +207,7 @@ void oneshot_allreduce(const at::Tensor& inp, const at::Tensor& out, double scal
   check_gpu(status, "status", at::kInt);
   TORCH_CHECK(inp.numel() == out.numel() && inp.numel() % 4 == 0 && inp.numel() <= stride,
               "dgt: one-shot all-reduce needs equal sizes, a multiple of 4 and <= mailbox stride");
-  c10::hip::HIPGuard guard(inp.device());
+  c10::DeviceGuard guard(inp.device());
   dgt::Exchange ex = make_exchange(data_ptrs, flag_ptrs, rank, world_size, stride, seq, timeout_ticks);
   DGT_CHECK_HIP(dgt::oneshot_allreduce(inp.data_ptr<float>(), out.data_ptr<float>(), inp.numel(), (float)scale, ex,
                                        status.data_ptr<int>(), stream_of(inp)));
@@ -216,7 +216,7 @@ void oneshot_allreduce(const at::Tensor& inp, const at::Tensor& out, double scal
 // ------------------------------------------------------------------------------ IPC runtime
 int64_t ipc_alloc(int64_t nbytes, bool uncached, int64_t device) {
   TORCH_CHECK(nbytes > 0, "dgt: ipc_alloc needs a positive size");
-  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
   void* p = nullptr;
   if (uncached) {
     DGT_CHECK_HIP(hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocUncached));
@@ -239,7 +239,7 @@ at::Tensor ipc_handle(int64_t ptr) {
 int64_t ipc_open(const at::Tensor& handle, int64_t device) {
   TORCH_CHECK(!handle.is_cuda() && handle.scalar_type() == at::kByte && handle.numel() == sizeof(hipIpcMemHandle_t),
               "dgt: ipc_open needs a CPU uint8 tensor of ", sizeof(hipIpcMemHandle_t), " bytes");
-  c10::hip::HIPGuard guard((c10::DeviceIndex)device);
+  c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
   hipIpcMemHandle_t h;
   std::memcpy(&h, handle.contiguous().data_ptr(), sizeof(h));
   void* p = nullptr;

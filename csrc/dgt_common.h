@@ -48,18 +48,29 @@ struct Exchange {
   unsigned* flags[kMaxRanks];       // each rank's flag region
 };
 
-DGT_DEVICE float wave_sum16(float v) {  // sum over the 16 lanes sharing lane>>4
-  v += __shfl_xor(v, 1, 64);
-  v += __shfl_xor(v, 2, 64);
-  v += __shfl_xor(v, 4, 64);
-  v += __shfl_xor(v, 8, 64);
+template <int CTRL>
+DGT_DEVICE float dpp_mov(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+}
+
+// Sum over the 16 lanes of a DPP row (lanes sharing lane>>4), result in every lane of the row.
+// DPP quad permutes + row (half-)mirrors: 4 v_add_f32_dpp, no LDS traffic (ds_bpermute costs an
+// LDS round trip per step).  Every lane ends with the bitwise-same value.
+DGT_DEVICE float wave_sum16(float v) {
+  v += dpp_mov<0xB1>(v);   // quad_perm [1,0,3,2]
+  v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
+  v += dpp_mov<0x141>(v);  // row_half_mirror
+  v += dpp_mov<0x140>(v);  // row_mirror
   return v;
 }
 
-DGT_DEVICE float wave_sum_groups(float v) {  // sum over the 4 lane groups (lane, lane^16, lane^32, ...)
-  v += __shfl_xor(v, 16, 64);
-  v += __shfl_xor(v, 32, 64);
-  return v;
+// Sum over the 4 rows of the wave (lane, lane^16, lane^32, lane^48) with the gfx950
+// v_permlane16_swap / v_permlane32_swap half-exchanges.
+DGT_DEVICE float wave_sum_groups(float v) {
+  auto a = __builtin_amdgcn_permlane16_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  v = __uint_as_float(a[0]) + __uint_as_float(a[1]);
+  auto b = __builtin_amdgcn_permlane32_swap(__float_as_uint(v), __float_as_uint(v), false, false);
+  return __uint_as_float(b[0]) + __uint_as_float(b[1]);
 }
 
 DGT_DEVICE float wave_sum(float v) {

@@ -2,22 +2,25 @@
 // BCE-with-logits, Adam; reference train.py:26-36, 96, 107-115).
 //
 // Design (MI355X-first, not a translation of the reference's ~30 ATen/cuBLAS launches per step):
-//   * ONE workgroup of 4*H threads (H/16 waves) owns the whole model.  Parameters and gradients
-//     live in LDS for the entire launch; Adam moments live in registers (each thread owns fixed
-//     float4 chunks of the flat parameter vector).  A launch runs many optimizer steps.
+//   * ONE workgroup of H/16 waves trains the model; a launch runs many optimizer steps.
+//   * Each wave OWNS 16 hidden units end to end: its rows of W1, its slice of b1 and W2, their
+//     gradients, their Adam moments (registers) and a private copy of the minibatch.  The only
+//     cross-wave dependency of a step is the sum of the per-wave partial logits, so a step has
+//     ONE workgroup barrier (the partial-logit buffer is double-buffered by step parity).
+//     The shared scalar b2 is updated redundantly (bit-identically) by every wave.
 //   * Both GEMM-shaped products run on the matrix cores with exact-fp32 MFMA
-//     (v_mfma_f32_16x16x4_f32): the forward x.W1^T (M = batch, N = hidden, K = features) and the
-//     weight gradient dh^T.x (M = hidden, N = features, K = batch).  Each wave owns one 16-wide
-//     hidden tile, so the hidden tile is the MFMA N (fwd) / M (wgrad) dimension.  Operands are
-//     staged through LDS with padded strides (no 16-way bank conflicts on the strided reads).
-//   * The minibatch rows are gathered from the device-resident dataset by sampler index, with
-//     the next step's rows prefetched into registers while the current step computes
-//     (no per-step H2D copy, no host sync: SURVEY K1/K2/K24).
-//   * World size > 1: after the local gradient is complete, the workgroup pushes it into every
-//     peer's IPC mailbox over xGMI, raises a per-peer sequence flag (system-scope release), waits
-//     for its own flags, and sums the world_size contributions in rank order, so every rank
-//     applies bit-identical updates.  This replaces DeepSpeed's flatten -> NCCL all_reduce ->
-//     scale -> unflatten with one latency-bound exchange inside the kernel.
+//     (v_mfma_f32_16x16x4_f32): the forward x.W1^T (M = batch, N = the wave's 16 hidden units,
+//     K = features) and the weight gradient dh^T.x (M = hidden, N = features, K = batch).
+//     Operands are staged through LDS with padded strides.
+//   * Row reductions use DPP (v_add_f32_dpp) and the gfx950 v_permlane{16,32}_swap exchanges,
+//     never ds_bpermute.
+//   * Minibatch rows are gathered from the device-resident dataset by sampler index; the next
+//     step's rows are prefetched into registers while the current step computes (no per-step H2D,
+//     no host sync: SURVEY K1/K2/K24).
+//   * World size > 1: each wave pushes its gradient slice into every peer's IPC mailbox over
+//     xGMI, raises a per-(wave, rank) sequence flag (system-scope release), waits for its own flags
+//     and sums the contributions in rank order, so every rank applies bit-identical updates.  This
+//     replaces DeepSpeed's flatten -> NCCL all_reduce -> scale -> unflatten.
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 
@@ -29,103 +32,119 @@ struct TinyCfg {
   static constexpr int T = 64 * NW;              // threads
   static constexpr int FP = (F + 3) / 4 * 4;     // K of the forward GEMM, padded for 16x16x4
   static constexpr int NKT = (F + 15) / 16;      // 16-wide feature tiles of the weight gradient
-  static constexpr int SX = NKT * 16 + 1;        // LDS row stride of the batch (padded: no 16-way conflict)
-  static constexpr int SD = H + 1;               // LDS row stride of dh
+  static constexpr int SX = NKT * 16 + 1;        // LDS row stride of the batch (+1: no 16-way conflict)
   static constexpr int BM = 16;                  // max micro-batch (MFMA M of the forward)
-  static constexpr int P = H * F + 2 * H + 1;
+  static constexpr int P = H * F + 2 * H + 1;    // global flat parameter count
   static constexpr int PP = (P + 3) / 4 * 4;
-  static constexpr int NCH = PP / 4;             // float4 chunks
-  static constexpr int CPT = (NCH + T - 1) / T;  // chunks per thread
+  // a wave's local parameter vector: [W1 rows 16 x F][b1 16][W2 16][b2]
+  static constexpr int L_B1 = 16 * F, L_W2 = 16 * F + 16, L_B2 = 16 * F + 32;
+  static constexpr int WP = 16 * F + 33;
+  static constexpr int NPL = (WP + 63) / 64;     // owned elements per lane
+  static constexpr int WPP = NPL * 64;
   static constexpr int XE = BM * F;
-  static constexpr int XPT = (XE + T - 1) / T;   // batch elements loaded per thread per step
-  static constexpr int OFF_B1 = H * F, OFF_W2 = H * F + H, OFF_B2 = H * F + 2 * H;
+  static constexpr int XPL = (XE + 63) / 64;     // batch elements each lane stages
+  static constexpr int G_B1 = H * F, G_W2 = H * F + H, G_B2 = H * F + 2 * H;
   static_assert(H % 16 == 0 && H >= 16 && H <= 256, "hidden must be a multiple of 16 in [16, 256]");
   static_assert(F >= 1 && F <= 64, "n_features must be in [1, 64]");
+
+  // local element e of wave w -> index in the global flat vector
+  static DGT_HOST_DEVICE int global_index(int w, int e) {
+    if (e < L_B1) return 16 * w * F + e;
+    if (e < L_W2) return G_B1 + 16 * w + (e - L_B1);
+    if (e < L_B2) return G_W2 + 16 * w + (e - L_W2);
+    return G_B2;
+  }
+};
+
+template <int F, int H>
+struct __attribute__((aligned(16))) WaveSmem {
+  using C = TinyCfg<F, H>;
+  float P[C::WPP];           // this wave's parameters
+  float G[C::WPP];           // their gradient for the current step
+  float X[C::BM * C::SX];    // private copy of the minibatch (rows >= batch, cols >= F are zero)
+  float DH[C::BM * 17];      // dL/d(pre-activation) of this wave's 16 hidden units
+  float Y[C::BM];
+  int idx[C::BM];            // sample indices of the NEXT step (prefetch pipeline)
 };
 
 template <int F, int H>
 struct __attribute__((aligned(16))) TinySmem {
   using C = TinyCfg<F, H>;
-  float P[C::PP];          // parameters
-  float G[C::PP];          // gradient of the current step
-  float X[C::BM * C::SX];  // current minibatch, rows >= batch and cols >= F are zero
-  float Y[C::BM];
-  float Z[C::NW * 16];     // per-wave partial logits
-  float DH[C::BM * C::SD]; // dL/d(pre-activation)
-  int idx[C::BM];          // sample indices of the NEXT step (prefetch pipeline)
+  WaveSmem<F, H> w[C::NW];
+  float Z[2][C::NW * 16];    // per-wave partial logits, double-buffered by step parity
   int err;
 };
 
-// Forward + BCE + backward of one step; the gradient lands in sm.G.  Returns the step's mean loss
-// (identical in every lane).  Contains two workgroup barriers; the caller provides the others.
-template <int F, int H>
-DGT_DEVICE float tiny_fwd_bwd(TinySmem<F, H>& sm, int Bt) {
-  using C = TinyCfg<F, H>;
-  const int t = threadIdx.x, w = t >> 6, l = t & 63, lr = l & 15, lq = l >> 4;
-  const int j0 = 16 * w, j = j0 + lr;
+// ------------------------------------------------------------------ per-wave step pieces
 
-  // ---- forward GEMM on MFMA: D[b][j] = sum_k x[b][k] * W1[j][k]
+// Forward GEMM on MFMA + bias + ReLU; publishes this wave's partial logits into Zbuf.
+template <int F, int H>
+DGT_DEVICE void wave_forward(WaveSmem<F, H>& ws, float* Zbuf, int w, int l, float (&h)[4]) {
+  using C = TinyCfg<F, H>;
+  const int lr = l & 15, lq = l >> 4;
   // 16x16x4 f32 operand maps: A[i = l&15][k = l>>4], B[k = l>>4][j = l&15];
-  // D: col = l&15 (hidden j), row = 4*(l>>4) + r (batch b).
+  // D: col = l&15 (hidden unit), row = 4*(l>>4) + r (batch row).
   f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int ks = 0; ks < C::FP / 4; ++ks) {
     const int k = 4 * ks + lq;
-    const float a = sm.X[lr * C::SX + k];
-    const float b = (F % 4 == 0 || k < F) ? sm.P[j * F + k] : 0.f;
+    const float a = ws.X[lr * C::SX + k];
+    const float b = (F % 4 == 0 || k < F) ? ws.P[lr * F + k] : 0.f;
     acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
   }
-  const float b1 = sm.P[C::OFF_B1 + j];
-  const float w2 = sm.P[C::OFF_W2 + j];
-  float h[4];
+  const float b1 = ws.P[C::L_B1 + lr];
+  const float w2 = ws.P[C::L_W2 + lr];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     h[r] = fmaxf(acc[r] + b1, 0.f);
-    const float pz = wave_sum16(h[r] * w2);  // partial logit over this wave's 16 hidden units
-    if (lr == 0) sm.Z[w * 16 + 4 * lq + r] = pz;
+    const float pz = wave_sum16(h[r] * w2);
+    if (lr == 0) Zbuf[w * 16 + 4 * lq + r] = pz;
   }
-  __syncthreads();
+}
 
-  // ---- logits, BCE-with-logits (torch: (1-y)*z - log_sigmoid(z)), dL/dz = (sigmoid(z)-y)/B
-  const float b2 = sm.P[C::OFF_B2];
-  const float invB = 1.0f / (float)Bt;
-  float dz[4];
-  float lsum = 0.f, db2 = 0.f, dw2 = 0.f, db1 = 0.f;
+// After the barrier: logits, loss, backward into ws.G.  Returns the step's mean loss (every lane).
+template <int F, int H, bool WANT_LOSS>
+DGT_DEVICE float wave_backward(WaveSmem<F, H>& ws, const float* Zbuf, int l, const float (&h)[4], int Bt,
+                               float invB) {
+  using C = TinyCfg<F, H>;
+  const int lr = l & 15, lq = l >> 4;
+  const float b2 = ws.P[C::L_B2];
+  const float w2 = ws.P[C::L_W2 + lr];
+  float lsum = 0.f, dw2 = 0.f, db1 = 0.f, db2 = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     const int b = 4 * lq + r;
     float s = 0.f;
 #pragma unroll
-    for (int ww = 0; ww < C::NW; ++ww) s += sm.Z[ww * 16 + b];
+    for (int ww = 0; ww < C::NW; ++ww) s += Zbuf[ww * 16 + b];
     const float z = s + b2;
-    const float y = sm.Y[b];
+    const float y = ws.Y[b];
     const bool valid = b < Bt;
+    // BCE-with-logits (torch: (1-y)*z - log_sigmoid(z)); d/dz = sigmoid(z) - y, times 1/B (mean)
     const float e = __expf(-fabsf(z));
-    const float log_sig = fminf(z, 0.f) - log1pf(e);
-    const float sig = (z >= 0.f) ? 1.f / (1.f + e) : e / (1.f + e);
-    dz[r] = valid ? (sig - y) * invB : 0.f;
-    lsum += valid ? (1.f - y) * z - log_sig : 0.f;
-    // backward through Linear(H,1) and ReLU
-    dw2 = fmaf(dz[r], h[r], dw2);
-    const float dh = (h[r] > 0.f) ? dz[r] * w2 : 0.f;
-    sm.DH[b * C::SD + j] = dh;
+    const float rinv = __builtin_amdgcn_rcpf(1.f + e);
+    const float sig = (z >= 0.f) ? rinv : e * rinv;
+    const float dz = valid ? (sig - y) * invB : 0.f;
+    if (WANT_LOSS) lsum += valid ? (1.f - y) * z - (fminf(z, 0.f) - __logf(1.f + e)) : 0.f;
+    dw2 = fmaf(dz, h[r], dw2);
+    const float dh = (h[r] > 0.f) ? dz * w2 : 0.f;
+    ws.DH[b * 17 + lr] = dh;
     db1 += dh;
-    db2 += dz[r];
+    db2 += dz;
   }
   dw2 = wave_sum_groups(dw2);
   db1 = wave_sum_groups(db1);
   db2 = wave_sum_groups(db2);
-  lsum = wave_sum_groups(lsum);
   if (lq == 0) {
-    sm.G[C::OFF_W2 + j] = dw2;
-    sm.G[C::OFF_B1 + j] = db1;
+    ws.G[C::L_W2 + lr] = dw2;
+    ws.G[C::L_B1 + lr] = db1;
   }
-  if (t == 0) sm.G[C::OFF_B2] = db2;
-  __syncthreads();
+  if (l == 0) ws.G[C::L_B2] = db2;
+  __builtin_amdgcn_wave_barrier();
 
-  // ---- weight gradient on MFMA: dW1[j][k] = sum_b dh[b][j] * x[b][k]
+  // weight gradient on MFMA: dW1[jj][k] = sum_b dh[b][jj] * x[b][k]
   // A[i = hidden (l&15)][kk = batch (l>>4)], B[kk = batch][col = feature (l&15)];
-  // D: col = feature 16*ct + (l&15), row = hidden j0 + 4*(l>>4) + r.
+  // D: col = feature 16*ct + (l&15), row = hidden 4*(l>>4) + r.
   const int nks = (Bt + 3) >> 2;
 #pragma unroll
   for (int ct = 0; ct < C::NKT; ++ct) {
@@ -134,53 +153,50 @@ DGT_DEVICE float tiny_fwd_bwd(TinySmem<F, H>& sm, int Bt) {
     for (int ks = 0; ks < C::BM / 4; ++ks) {
       if (ks < nks) {  // wave-uniform
         const int b = 4 * ks + lq;
-        const float a = sm.DH[b * C::SD + j0 + lr];
-        const float xb = sm.X[b * C::SX + 16 * ct + lr];
-        g = __builtin_amdgcn_mfma_f32_16x16x4f32(a, xb, g, 0, 0, 0);
+        g = __builtin_amdgcn_mfma_f32_16x16x4f32(ws.DH[b * 17 + lr], ws.X[b * C::SX + 16 * ct + lr], g, 0, 0, 0);
       }
     }
     const int k = 16 * ct + lr;
     if (k < F) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) sm.G[(j0 + 4 * lq + r) * F + k] = g[r];
+      for (int r = 0; r < 4; ++r) ws.G[(4 * lq + r) * F + k] = g[r];
     }
   }
-  return lsum / (float)Bt;
+  __builtin_amdgcn_wave_barrier();
+  return WANT_LOSS ? wave_sum_groups(lsum) * invB : 0.f;
 }
 
-// Gather the x / y values this thread stages for one step (rows from sm.idx).
+// Gather the x / y values this lane stages for one step (rows from ws.idx).
 template <int F, int H>
-DGT_DEVICE void gather_rows(const TinySmem<F, H>& sm, const float* __restrict__ X, const float* __restrict__ Y,
-                            float (&xv)[TinyCfg<F, H>::XPT], float& yv) {
+DGT_DEVICE void gather_rows(const WaveSmem<F, H>& ws, const float* __restrict__ X, const float* __restrict__ Y,
+                            int l, float (&xv)[TinyCfg<F, H>::XPL], float& yv) {
   using C = TinyCfg<F, H>;
-  const int t = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < C::XPT; ++q) {
-    const int e = t + q * C::T;
+  for (int q = 0; q < C::XPL; ++q) {
+    const int e = l + 64 * q;
     float v = 0.f;
     if (e < C::XE) {
-      const int id = sm.idx[e / F];
+      const int id = ws.idx[e / F];
       if (id >= 0) v = X[(long long)id * F + (e % F)];
     }
     xv[q] = v;
   }
   yv = 0.f;
-  if (t < C::BM) {
-    const int id = sm.idx[t];
+  if (l < C::BM) {
+    const int id = ws.idx[l];
     if (id >= 0) yv = Y[id];
   }
 }
 
 template <int F, int H>
-DGT_DEVICE void stage_rows(TinySmem<F, H>& sm, const float (&xv)[TinyCfg<F, H>::XPT], float yv) {
+DGT_DEVICE void stage_rows(WaveSmem<F, H>& ws, int l, const float (&xv)[TinyCfg<F, H>::XPL], float yv) {
   using C = TinyCfg<F, H>;
-  const int t = threadIdx.x;
 #pragma unroll
-  for (int q = 0; q < C::XPT; ++q) {
-    const int e = t + q * C::T;
-    if (e < C::XE) sm.X[(e / F) * C::SX + (e % F)] = xv[q];
+  for (int q = 0; q < C::XPL; ++q) {
+    const int e = l + 64 * q;
+    if (e < C::XE) ws.X[(e / F) * C::SX + (e % F)] = xv[q];
   }
-  if (t < C::BM) sm.Y[t] = yv;
+  if (l < C::BM) ws.Y[l] = yv;
 }
 
 DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row) {
@@ -188,11 +204,24 @@ DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row
 }
 
 template <int F, int H>
+DGT_DEVICE void wave_init(WaveSmem<F, H>& ws, const float* __restrict__ params, int w, int l) {
+  using C = TinyCfg<F, H>;
+  for (int e = l; e < C::WPP; e += 64) {
+    ws.P[e] = (e < C::WP) ? params[C::global_index(w, e)] : 0.f;
+    ws.G[e] = 0.f;
+  }
+  for (int i = l; i < C::BM * C::SX; i += 64) ws.X[i] = 0.f;
+  for (int i = l; i < C::BM * 17; i += 64) ws.DH[i] = 0.f;
+}
+
+// ------------------------------------------------------------------ persistent training kernel
+template <int F, int H>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
   __shared__ TinySmem<F, H> sm;
-  const int t = threadIdx.x;
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
   const Exchange& ex = a.ex;
+  WaveSmem<F, H>& ws = sm.w[w];
 
   if (a.bmax > C::BM || a.bmax < 1 || ex.world_size < 1 || ex.world_size > kMaxRanks ||
       (ex.world_size > 1 && ex.stride < C::PP)) {
@@ -200,106 +229,94 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     return;
   }
 
-  // ---- prologue: parameters -> LDS, moments -> registers, batch 0 staged, batch 1 in flight
-  for (int i = t; i < C::PP; i += C::T) {
-    sm.P[i] = (i < C::P) ? a.params[i] : 0.f;
-    sm.G[i] = 0.f;
-  }
-  for (int i = t; i < C::BM * C::SX; i += C::T) sm.X[i] = 0.f;
+  // ---- prologue: parameters -> LDS, moments -> registers, batch 0 staged, batch 1 indices ready
+  wave_init<F, H>(ws, a.params, w, l);
   if (t == 0) sm.err = 0;
-  f32x4 m[C::CPT], v[C::CPT];
+  float m[C::NPL], v[C::NPL];
 #pragma unroll
-  for (int c = 0; c < C::CPT; ++c) {
-    const int ch = t + c * C::T;
-    if (ch < C::NCH) {
-      m[c] = *reinterpret_cast<const f32x4*>(a.exp_avg + 4 * ch);
-      v[c] = *reinterpret_cast<const f32x4*>(a.exp_avg_sq + 4 * ch);
-    } else {
-      m[c] = f32x4{0.f, 0.f, 0.f, 0.f};
-      v[c] = m[c];
+  for (int i = 0; i < C::NPL; ++i) {
+    const int e = l + 64 * i;
+    m[i] = v[i] = 0.f;
+    if (e < C::WP) {
+      const int gi = C::global_index(w, e);
+      m[i] = a.exp_avg[gi];
+      v[i] = a.exp_avg_sq[gi];
     }
   }
-  if (t < C::BM) sm.idx[t] = plan_at(a.plan, a.n_steps, a.bmax, 0, t);
-  __syncthreads();
-  float xv[C::XPT], yv;
-  gather_rows<F, H>(sm, a.X, a.Y, xv, yv);
-  __syncthreads();  // every thread has read sm.idx (step 0)
-  stage_rows<F, H>(sm, xv, yv);
-  if (t < C::BM) sm.idx[t] = plan_at(a.plan, a.n_steps, a.bmax, 1, t);
-  int idx_reg = (t < C::BM) ? plan_at(a.plan, a.n_steps, a.bmax, 2, t) : -1;
+  if (l < C::BM) ws.idx[l] = plan_at(a.plan, a.n_steps, a.bmax, 0, l);
+  __builtin_amdgcn_wave_barrier();
+  float xv[C::XPL], yv;
+  gather_rows<F, H>(ws, a.X, a.Y, l, xv, yv);
+  __builtin_amdgcn_wave_barrier();
+  stage_rows<F, H>(ws, l, xv, yv);
+  if (l < C::BM) ws.idx[l] = plan_at(a.plan, a.n_steps, a.bmax, 1, l);
+  int idx_reg = (l < C::BM) ? plan_at(a.plan, a.n_steps, a.bmax, 2, l) : -1;
   __syncthreads();
 
   double b1p = pow(a.beta1, (double)a.adam_step0);
   double b2p = pow(a.beta2, (double)a.adam_step0);
   double loss_total = 0.0;
   const float inv_ws = 1.0f / (float)ex.world_size;
-  int s = 0;
-  for (; s < a.n_steps; ++s) {
+  for (int s = 0; s < a.n_steps; ++s) {
     const int Bt = a.counts[s];
-    // prefetch step s+1 rows (indices already in sm.idx); consumed after this step's last barrier
-    if (s + 1 < a.n_steps) gather_rows<F, H>(sm, a.X, a.Y, xv, yv);
+    const float invB = 1.0f / (float)Bt;
+    // prefetch step s+1 rows (indices already in ws.idx); consumed after this step's wgrad
+    if (s + 1 < a.n_steps) gather_rows<F, H>(ws, a.X, a.Y, l, xv, yv);
 
-    const float step_loss = tiny_fwd_bwd<F, H>(sm, Bt);
-    __syncthreads();  // gradient complete in sm.G; nobody reads sm.X / sm.idx / sm.P any more
+    float h[4];
+    float* Zb = sm.Z[s & 1];
+    wave_forward<F, H>(ws, Zb, w, l, h);
+    __syncthreads();  // the step's only workgroup barrier: all partial logits published
+    if (sm.err) break;
+    const float step_loss = (w == 0) ? wave_backward<F, H, true>(ws, Zb, l, h, Bt, invB)
+                                     : wave_backward<F, H, false>(ws, Zb, l, h, Bt, invB);
 
-    if (s + 1 < a.n_steps) stage_rows<F, H>(sm, xv, yv);
-    if (t < C::BM) {
-      sm.idx[t] = idx_reg;
-      idx_reg = plan_at(a.plan, a.n_steps, a.bmax, s + 3, t);
+    // this wave is done reading its batch copy: stage the next one
+    if (s + 1 < a.n_steps) stage_rows<F, H>(ws, l, xv, yv);
+    if (l < C::BM) {
+      ws.idx[l] = idx_reg;
+      idx_reg = plan_at(a.plan, a.n_steps, a.bmax, s + 3, l);
     }
 
-    f32x4 g[C::CPT];
+    float g[C::NPL];
 #pragma unroll
-    for (int c = 0; c < C::CPT; ++c) {
-      const int ch = t + c * C::T;
-      g[c] = (ch < C::NCH) ? *reinterpret_cast<const f32x4*>(&sm.G[4 * ch]) : f32x4{0.f, 0.f, 0.f, 0.f};
-    }
+    for (int i = 0; i < C::NPL; ++i) g[i] = ws.G[l + 64 * i];
 
     if (ex.world_size > 1) {
-      // ---- one-shot exchange over xGMI: push to every peer, flag, wait, sum in rank order
+      // ---- one-shot exchange of this wave's slice over xGMI: push, flag, wait, sum in rank order
       const long long seq = ex.seq_base + s;
       const int parity = (int)(seq & 1);
       const unsigned val = (unsigned)(seq + 1);
 #pragma unroll
-      for (int c = 0; c < C::CPT; ++c) {
-        const int ch = t + c * C::T;
-        if (ch < C::NCH) {
+      for (int i = 0; i < C::NPL; ++i) {
+        const int e = l + 64 * i;
+        if (e < C::WP) {
+          const long long gi = C::global_index(w, e);
           for (int p = 0; p < ex.world_size; ++p) {
             if (p == ex.rank) continue;
-            float* dst = ex.data[p] + (long long)(parity * kMaxRanks + ex.rank) * ex.stride + 4 * ch;
-            *reinterpret_cast<f32x4*>(dst) = g[c];
+            ex.data[p][(long long)(parity * kMaxRanks + ex.rank) * ex.stride + gi] = g[i];
           }
         }
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      __syncthreads();
-      if (t < ex.world_size && t != ex.rank) {
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        store_release_system(ex.flags[t] + parity * kMaxRanks + ex.rank, val);
-        if (!spin_geq(ex.flags[ex.rank] + parity * kMaxRanks + t, val, ex.timeout_ticks)) sm.err = 1;
+      if (l < ex.world_size && l != ex.rank) {
+        const int fo = (w * 2 + parity) * kMaxRanks;
+        store_release_system(ex.flags[l] + fo + ex.rank, val);
+        if (!spin_geq(ex.flags[ex.rank] + fo + l, val, ex.timeout_ticks)) sm.err = 1;
         __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
-      __syncthreads();
-      if (sm.err) break;
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
-      for (int c = 0; c < C::CPT; ++c) {
-        const int ch = t + c * C::T;
-        if (ch < C::NCH) {
-          f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-          for (int p = 0; p < ex.world_size; ++p) {
-            f32x4 gp;
-            if (p == ex.rank) {
-              gp = g[c];
-            } else {
-              const float* src = ex.data[ex.rank] + (long long)(parity * kMaxRanks + p) * ex.stride + 4 * ch;
-              gp = *reinterpret_cast<const f32x4*>(src);
-            }
-            sum += gp;
-          }
-          g[c] = sum * inv_ws;
+      for (int i = 0; i < C::NPL; ++i) {
+        const int e = l + 64 * i;
+        if (e < C::WP) {
+          const long long gi = C::global_index(w, e);
+          float sum = 0.f;
+          for (int p = 0; p < ex.world_size; ++p)
+            sum += (p == ex.rank) ? g[i] : ex.data[ex.rank][(long long)(parity * kMaxRanks + p) * ex.stride + gi];
+          g[i] = sum * inv_ws;
         }
       }
     }
@@ -310,34 +327,26 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     const float step_size_neg = (float)(-(a.lr / (1.0 - b1p)));
     const float bc2_sqrt = (float)sqrt(1.0 - b2p);
 #pragma unroll
-    for (int c = 0; c < C::CPT; ++c) {
-      const int ch = t + c * C::T;
-      if (ch < C::NCH) {
-        f32x4 p4 = *reinterpret_cast<const f32x4*>(&sm.P[4 * ch]);
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float mm = m[c][e], vv = v[c][e];
-          p4[e] = adam_update(p4[e], g[c][e], mm, vv, a.hp, step_size_neg, bc2_sqrt);
-          m[c][e] = mm;
-          v[c][e] = vv;
-        }
-        *reinterpret_cast<f32x4*>(&sm.P[4 * ch]) = p4;
-      }
+    for (int i = 0; i < C::NPL; ++i) {
+      const int e = l + 64 * i;
+      if (e < C::WP) ws.P[e] = adam_update(ws.P[e], g[i], m[i], v[i], a.hp, step_size_neg, bc2_sqrt);
     }
+    __builtin_amdgcn_wave_barrier();
     loss_total += (double)step_loss;
-    __syncthreads();
   }
 
-  // ---- epilogue: state back to HBM
-  for (int i = t; i < C::P; i += C::T) a.params[i] = sm.P[i];
+  // ---- epilogue: state back to HBM (b2 belongs to wave 0)
 #pragma unroll
-  for (int c = 0; c < C::CPT; ++c) {
-    const int ch = t + c * C::T;
-    if (ch < C::NCH) {
-      *reinterpret_cast<f32x4*>(a.exp_avg + 4 * ch) = m[c];
-      *reinterpret_cast<f32x4*>(a.exp_avg_sq + 4 * ch) = v[c];
+  for (int i = 0; i < C::NPL; ++i) {
+    const int e = l + 64 * i;
+    if (e < C::WP && (e != C::L_B2 || w == 0)) {
+      const int gi = C::global_index(w, e);
+      a.params[gi] = ws.P[e];
+      a.exp_avg[gi] = m[i];
+      a.exp_avg_sq[gi] = v[i];
     }
   }
+  __syncthreads();
   if (t == 0) {
     *a.loss_acc += loss_total;
     *a.status = sm.err ? kTimeout : kOk;
@@ -349,21 +358,24 @@ template <int F, int H>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_grad_kernel(TinyGradArgs a) {
   using C = TinyCfg<F, H>;
   __shared__ TinySmem<F, H> sm;
-  const int t = threadIdx.x;
-  for (int i = t; i < C::PP; i += C::T) {
-    sm.P[i] = (i < C::P) ? a.params[i] : 0.f;
-    sm.G[i] = 0.f;
+  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  WaveSmem<F, H>& ws = sm.w[w];
+  wave_init<F, H>(ws, a.params, w, l);
+  if (l < C::BM) ws.idx[l] = (l < a.bmax) ? a.plan[(long long)a.step * a.bmax + l] : -1;
+  __builtin_amdgcn_wave_barrier();
+  float xv[C::XPL], yv;
+  gather_rows<F, H>(ws, a.X, a.Y, l, xv, yv);
+  stage_rows<F, H>(ws, l, xv, yv);
+  __builtin_amdgcn_wave_barrier();
+  const int Bt = a.counts[a.step];
+  const float invB = 1.0f / (float)Bt;
+  float h[4];
+  wave_forward<F, H>(ws, sm.Z[0], w, l, h);
+  __syncthreads();
+  const float loss = wave_backward<F, H, true>(ws, sm.Z[0], l, h, Bt, invB);
+  for (int e = l; e < C::WP; e += 64) {
+    if (e != C::L_B2 || w == 0) a.grad[C::global_index(w, e)] = ws.G[e];
   }
-  for (int i = t; i < C::BM * C::SX; i += C::T) sm.X[i] = 0.f;
-  if (t < C::BM) sm.idx[t] = (t < a.bmax) ? a.plan[(long long)a.step * a.bmax + t] : -1;
-  __syncthreads();
-  float xv[C::XPT], yv;
-  gather_rows<F, H>(sm, a.X, a.Y, xv, yv);
-  stage_rows<F, H>(sm, xv, yv);
-  __syncthreads();
-  const float loss = tiny_fwd_bwd<F, H>(sm, a.counts[a.step]);
-  __syncthreads();
-  for (int i = t; i < C::PP; i += C::T) a.grad[i] = sm.G[i];
   if (t == 0) *a.loss_acc += (double)loss;
 }
 
@@ -380,11 +392,11 @@ bool tiny_mlp_supported(int f, int h) {
 int tiny_mlp_padded_numel(int f, int h) { return (h * f + 2 * h + 1 + 3) / 4 * 4; }
 
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
-#define X_(F_, H_)                                                                        \
-  if (f == F_ && h == H_) {                                                               \
+#define X_(F_, H_)                                                                            \
+  if (f == F_ && h == H_) {                                                                   \
     hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_>), dim3(1), dim3(TinyCfg<F_, H_>::T), 0, \
-                       stream, a);                                                        \
-    return hipGetLastError();                                                             \
+                       stream, a);                                                            \
+    return hipGetLastError();                                                                 \
   }
   DGT_TINY_SHAPES(X_)
 #undef X_
@@ -392,11 +404,11 @@ hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stre
 }
 
 hipError_t tiny_mlp_grad(int f, int h, const TinyGradArgs& a, hipStream_t stream) {
-#define X_(F_, H_)                                                                        \
-  if (f == F_ && h == H_) {                                                               \
+#define X_(F_, H_)                                                                           \
+  if (f == F_ && h == H_) {                                                                  \
     hipLaunchKernelGGL((tiny_mlp_grad_kernel<F_, H_>), dim3(1), dim3(TinyCfg<F_, H_>::T), 0, \
-                       stream, a);                                                        \
-    return hipGetLastError();                                                             \
+                       stream, a);                                                           \
+    return hipGetLastError();                                                                \
   }
   DGT_TINY_SHAPES(X_)
 #undef X_

@@ -1,0 +1,432 @@
+"""The training engine: a native replacement for the slice of DeepSpeed the reference uses.
+
+Reference call sites (``train.py``): ``deepspeed.initialize`` (87-93), ``engine(x)`` (107),
+``engine.backward(loss)`` (113), ``engine.step()`` (114), ``engine.save_checkpoint`` (125),
+``engine.train()`` (100) and ``engine.device`` (94).  Semantics kept:
+
+* batch-size derivation + assertion from the JSON config (``config.parse_config``);
+* parameters broadcast from rank 0 at construction;
+* ``backward`` scales the loss by 1/gradient_accumulation_steps and, at the accumulation boundary,
+  reduces gradients across data-parallel ranks (mean);
+* ``step`` applies the optimizer at the boundary, zeroes gradients, advances ``global_steps`` and
+  logs every ``steps_per_print`` steps;
+* DeepSpeed checkpoint layout (``runtime/checkpoint.py``) — plus ``load_checkpoint``.
+
+MI355X-first mechanics (not DeepSpeed's): parameters and gradients are views into flat,
+bucket-aligned buffers (``runtime/flat.py``); gradient buckets are reduced by RCCL over xGMI *while
+backward runs* (``parallel/reducer.py``); the optimizer is one fused HIP Adam launch over the flat
+fp32 master buffer with the 1/world_size average, loss-scale and clip coefficient folded in
+(``ops.adam_flat_``); ZeRO-1/2 reduce-scatter gradients into a contiguous shard, update only the
+shard, then all-gather parameters per bucket.
+"""
+from __future__ import annotations
+
+import math
+import os
+import time
+from typing import Any, Dict, Iterable, Optional, Tuple
+
+import torch
+import torch.distributed as dist
+
+from .config import DSConfig, parse_config
+from .ops.adam import adam_flat_
+from .parallel import comm
+from .parallel.reducer import GradReducer
+from .runtime import checkpoint as ckpt
+from .runtime.flat import FlatLayout, FlatParamStore
+from .runtime.optim_state import adam_hparams, adam_state_to_flat, flat_to_adam_state
+from .runtime.schedules import LossScaler, build_scheduler
+from .utils.fault import FaultInjector
+from .utils.metrics import MetricsSink, ThroughputTimer
+
+_DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
+
+
+class FlatAdamOptimizer:
+    """Optimizer facade handed back by ``initialize`` (the engine drives the actual update)."""
+
+    def __init__(self, lr: float, betas, eps: float, weight_decay: float, adamw: bool):
+        self.param_groups = [{"lr": lr, "betas": tuple(betas), "eps": eps, "weight_decay": weight_decay,
+                              "adamw": adamw}]
+        self.engine: Optional["Engine"] = None
+
+    @property
+    def lr(self) -> float:
+        return self.param_groups[0]["lr"]
+
+    def zero_grad(self, set_to_none: bool = False) -> None:
+        if self.engine is not None:
+            self.engine.zero_grad()
+
+    def state_dict(self) -> Dict[str, Any]:
+        return self.engine.optimizer_state_dict() if self.engine else {}
+
+    def step(self, closure=None):  # DeepSpeed's engine.step() is the supported entry point
+        if self.engine is not None:
+            self.engine.step()
+
+
+class Engine:
+    def __init__(self, model: torch.nn.Module, config: DSConfig, optimizer=None, lr_scheduler=None,
+                 device: Optional[torch.device] = None, model_parameters: Optional[Iterable] = None):
+        self.config = config
+        self.rank = comm.get_rank()
+        self.world_size = comm.get_world_size()
+        self.local_rank = comm.rank_info().local_rank
+        if device is None:
+            device = (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
+                      else torch.device("cpu"))
+        self.device = device
+        self.dtype = _DTYPES[config.compute_dtype]
+        self.module = model.to(device=device, dtype=self.dtype)
+        self.stage = config.zero_stage
+        self.gas = config.gradient_accumulation_steps
+        self.micro_batch = config.train_micro_batch_size_per_gpu
+        self.global_steps = 0
+        self.global_samples = 0
+        self.micro_steps = 0
+        self.skipped_steps = 0
+
+        # ---- optimizer hyper-parameters: client torch optimizer, else config, else Adam defaults
+        self.client_optimizer = optimizer
+        if optimizer is not None and not isinstance(optimizer, FlatAdamOptimizer):
+            hp = adam_hparams(optimizer)
+        elif config.optimizer is not None:
+            o = config.optimizer
+            hp = {"lr": o.lr, "betas": o.betas, "eps": o.eps, "weight_decay": o.weight_decay, "adamw": o.adamw}
+        else:
+            hp = {"lr": 1e-3, "betas": (0.9, 0.999), "eps": 1e-8, "weight_decay": 0.0, "adamw": False}
+        self.optimizer = FlatAdamOptimizer(hp["lr"], hp["betas"], hp["eps"], hp["weight_decay"], hp["adamw"])
+        self.optimizer.engine = self
+
+        # ---- flat, bucket-aligned parameter / gradient storage
+        params = [p for p in (model_parameters if model_parameters is not None else self.module.parameters())
+                  if p.requires_grad]
+        self.params = list(params)
+        self.param_names = self._names(self.params)
+        bucket_elems = max(int(config.zero.reduce_bucket_size), 1024)
+        self.layout = FlatLayout([tuple(p.shape) for p in self.params], bucket_elems, self.world_size,
+                                 shard=self.stage >= 1)
+        self.store = FlatParamStore(self.params, self.layout, device, self.dtype)
+        if self.world_size > 1:
+            dist.broadcast(self.store.param_buf, 0)  # DeepSpeed _broadcast_model
+
+        # ---- fp32 master + moments (full for stage 0, this rank's shard for stage >= 1)
+        if self.stage == 0:
+            self.master = (self.store.param_buf if self.dtype == torch.float32
+                           else self.store.param_buf.float())
+            self.param_lp = None if self.dtype == torch.float32 else self.store.param_buf
+        else:
+            pieces = [self.store.param_buf[s:s + n].float() for s, n in self.layout.shard_ranges(self.rank)]
+            self.master = torch.cat(pieces).contiguous()
+            self.param_lp = (None if self.dtype == torch.float32
+                             else torch.empty(self.master.numel(), dtype=self.dtype, device=device))
+        self.exp_avg = torch.zeros_like(self.master)
+        self.exp_avg_sq = torch.zeros_like(self.master)
+
+        # ---- communication
+        comm_dtype = None
+        if config.communication_data_type:
+            comm_dtype = _DTYPES.get(str(config.communication_data_type).replace("float", "fp"), None)
+        self.oneshot = None
+        if (self.world_size > 1 and device.type == "cuda" and self.stage == 0
+                and config.amd.allreduce in ("auto", "oneshot")):
+            self.oneshot = self._maybe_oneshot()
+        self.reducer = GradReducer(self.store.grad_buf, self.layout, self.stage, self.world_size, self.rank,
+                                   comm_dtype=comm_dtype, oneshot=self.oneshot,
+                                   oneshot_max_bytes=config.amd.oneshot_max_bytes,
+                                   debug_sync=config.amd.debug_sync_streams)
+        self._hooks = []
+        for i, p in enumerate(self.params):
+            self._hooks.append(p.register_post_accumulate_grad_hook(
+                lambda _p, i=i: self.reducer.on_grad_ready(i)))
+
+        # ---- schedules, loss scaling, logging, fault injection
+        self.lr_scheduler = lr_scheduler
+        self.ds_scheduler = build_scheduler(config.scheduler.type, config.scheduler.params)
+        if self.ds_scheduler is not None:
+            self.optimizer.param_groups[0]["lr"] = self.ds_scheduler.step()
+        self.loss_scaler = LossScaler(config.loss_scale, config.initial_scale_power) if config.fp16_enabled else None
+        self.tput = ThroughputTimer(self.micro_batch * self.world_size, config.steps_per_print)
+        self.metrics = MetricsSink.from_env(self.rank)
+        self.faults = FaultInjector.from_env(self.rank)
+        self._timers: Dict[str, float] = {}
+        self._grad_norm: Optional[torch.Tensor] = None
+        self._boundary_pending = False
+        self.training = True
+
+    # ------------------------------------------------------------------ helpers
+    def _names(self, params):
+        lookup = {id(p): n for n, p in self.module.named_parameters()}
+        return [lookup.get(id(p), f"param{i}") for i, p in enumerate(params)]
+
+    def _maybe_oneshot(self):
+        from .parallel.ipc import IpcChannel, ipc_disabled_by_env
+        if ipc_disabled_by_env() or self.world_size > 8:
+            return None
+        biggest = max(b.numel for b in self.layout.buckets)
+        stride = min(biggest, self.config.amd.oneshot_max_bytes // 4)
+        try:
+            ch = IpcChannel(stride, self.device)
+        except Exception:
+            return None
+        if not ch.selftest():
+            ch.close()
+            return None
+        return ch
+
+    def is_gradient_accumulation_boundary(self) -> bool:
+        return (self.micro_steps + 1) % self.gas == 0
+
+    @property
+    def lr(self) -> float:
+        return self.optimizer.param_groups[0]["lr"]
+
+    def get_lr(self):
+        return [self.lr]
+
+    def train(self, mode: bool = True):
+        self.training = mode
+        self.module.train(mode)
+        return self
+
+    def eval(self):
+        return self.train(False)
+
+    def zero_grad(self) -> None:
+        self.store.zero_grad()
+
+    # ------------------------------------------------------------------ forward / backward / step
+    def forward(self, *args, **kwargs):
+        if self.dtype != torch.float32:
+            args = tuple(a.to(self.dtype) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)
+        self.tput.start()
+        return self.module(*args, **kwargs)
+
+    __call__ = forward
+
+    def backward(self, loss: torch.Tensor, retain_graph: bool = False) -> torch.Tensor:
+        loss = self.faults.maybe_corrupt_loss(loss, self.global_steps)
+        boundary = self.is_gradient_accumulation_boundary()
+        self.store.rebind_grads()
+        self.reducer.arm(boundary and self.training)
+        scaled = loss.float()
+        if self.gas > 1:
+            scaled = scaled / self.gas
+        if self.loss_scaler is not None:
+            scaled = scaled * self.loss_scaler.scale
+        t0 = time.perf_counter() if self.config.wall_clock_breakdown else 0.0
+        scaled.backward(retain_graph=retain_graph)
+        if boundary:
+            self.reducer.finish()
+            self._boundary_pending = True
+        if self.config.wall_clock_breakdown:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            self._timers["backward_ms"] = (time.perf_counter() - t0) * 1e3
+        return loss
+
+    def _clip_coef(self, grads: torch.Tensor, scale: float) -> Optional[torch.Tensor]:
+        clip = self.config.gradient_clipping
+        if clip <= 0:
+            self._grad_norm = None
+            return None
+        sq = grads.float().pow(2).sum() * (scale * scale)
+        if self.stage >= 1 and self.world_size > 1:
+            dist.all_reduce(sq)
+        norm = sq.sqrt()
+        self._grad_norm = norm
+        return torch.clamp(clip / (norm + 1e-6), max=1.0).reshape(1).float()
+
+    def step(self, lr_kwargs=None) -> None:
+        self.micro_steps += 1
+        if not self._boundary_pending:
+            return
+        self._boundary_pending = False
+        t0 = time.perf_counter() if self.config.wall_clock_breakdown else 0.0
+        grads = self.reducer.reduced
+        scale = 1.0 / self.world_size
+        if self.loss_scaler is not None:
+            scale /= self.loss_scaler.scale
+            overflow = not bool(torch.isfinite(grads).all().item())
+            if self.stage >= 1 and self.world_size > 1:
+                overflow = comm.all_reduce_max(float(overflow), self.device) > 0
+            self.loss_scaler.update(overflow)
+            if overflow:
+                self.skipped_steps += 1
+                self._finish_step(skipped=True)
+                return
+        if self.client_optimizer is not None and not isinstance(self.client_optimizer, FlatAdamOptimizer):
+            self.optimizer.param_groups[0]["lr"] = float(self.client_optimizer.param_groups[0]["lr"])
+        coef = self._clip_coef(grads, scale)
+        g = self.optimizer.param_groups[0]
+        adam_flat_(self.master, grads, self.exp_avg, self.exp_avg_sq, self.global_steps + 1 - self.skipped_steps,
+                   g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], g["adamw"],
+                   grad_scale=scale, grad_scale_dev=coef, param_lp=self.param_lp)
+        if self.stage >= 1:
+            self._allgather_params()
+        self._finish_step(skipped=False)
+        if self.config.wall_clock_breakdown:
+            if self.device.type == "cuda":
+                torch.cuda.synchronize()
+            self._timers["step_ms"] = (time.perf_counter() - t0) * 1e3
+
+    def _allgather_params(self) -> None:
+        src = self.param_lp if self.param_lp is not None else self.master
+        works = []
+        off = 0
+        for b in self.layout.buckets:
+            n = b.numel // self.world_size
+            out = self.store.param_buf[b.start:b.start + b.numel]
+            piece = src[off:off + n]
+            if self.world_size > 1:
+                works.append(dist.all_gather_into_tensor(out, piece, async_op=True))
+            else:
+                out.copy_(piece)
+            off += n
+        for w in works:
+            w.wait()
+
+    def _finish_step(self, skipped: bool) -> None:
+        self.store.zero_grad()
+        self.global_steps += 1
+        self.global_samples += self.config.train_batch_size
+        if self.lr_scheduler is not None and not skipped:
+            self.lr_scheduler.step()
+        if self.ds_scheduler is not None and not skipped:
+            self.optimizer.param_groups[0]["lr"] = self.ds_scheduler.step()
+        self.tput.stop(self.global_steps)
+        if self.global_steps % self.config.steps_per_print == 0 and self.rank == 0:
+            g = self.optimizer.param_groups[0]
+            msg = (f"[Rank 0] step={self.global_steps}, skipped={self.skipped_steps}, lr={[g['lr']]}, "
+                   f"mom={[tuple(g['betas'])]}")
+            sps = self.tput.samples_per_sec()
+            if sps:
+                msg += f", samples/sec={sps:.1f}"
+            if self._timers:
+                msg += ", " + ", ".join(f"{k}={v:.3f}" for k, v in self._timers.items())
+            if os.environ.get("DGT_QUIET", "0") == "0":
+                print(msg, flush=True)
+        self.metrics.log({"step": self.global_steps, "lr": self.lr, "skipped": int(skipped),
+                          "samples_per_sec": self.tput.samples_per_sec(),
+                          "comm_bytes": self.reducer.bytes_reduced, **self._timers})
+        self.faults.maybe_fire(self.global_steps)
+
+    # ------------------------------------------------------------------ state
+    def module_state_dict(self) -> Dict[str, torch.Tensor]:
+        return {k: v.detach().cpu().clone() for k, v in self.module.state_dict().items()}
+
+    def optimizer_state_dict(self) -> Dict[str, Any]:
+        g = self.optimizer.param_groups[0]
+        if self.stage >= 1:
+            raise RuntimeError("ZeRO optimizer state is sharded; see the zero_pp_rank_* checkpoint files")
+        return flat_to_adam_state(self.exp_avg, self.exp_avg_sq, self.layout.segments(), self.global_steps
+                                  - self.skipped_steps, g["lr"], g["betas"], g["eps"], g["weight_decay"], g["adamw"])
+
+    def _zero_shard_state(self) -> Dict[str, Any]:
+        g = self.optimizer.param_groups[0]
+        return {
+            "zero_stage": self.stage,
+            "partition_rank": self.rank,
+            "partition_world_size": self.world_size,
+            "buckets": [[b.start, b.numel] for b in self.layout.buckets],
+            "offsets": list(self.layout.offsets),
+            "shapes": [list(s) for s in self.layout.shapes],
+            "names": list(self.param_names),
+            "total": self.layout.total,
+            "fp32_flat": self.master.detach().cpu().clone(),
+            "exp_avg": self.exp_avg.detach().cpu().clone(),
+            "exp_avg_sq": self.exp_avg_sq.detach().cpu().clone(),
+            "step": self.global_steps - self.skipped_steps,
+            "param_groups": [{"lr": g["lr"], "betas": list(g["betas"]), "eps": g["eps"],
+                              "weight_decay": g["weight_decay"], "adamw": g["adamw"]}],
+        }
+
+    def save_checkpoint(self, save_dir: str, tag: Optional[str] = None, client_state: Optional[dict] = None,
+                        save_latest: bool = True) -> str:
+        extra = {"global_samples": self.global_samples, "skipped_steps": self.skipped_steps,
+                 "dp_world_size": self.world_size, "client_state": client_state or {},
+                 "lr_scheduler": (self.ds_scheduler.state_dict() if self.ds_scheduler is not None else
+                                  (self.lr_scheduler.state_dict() if self.lr_scheduler is not None else None))}
+        if self.loss_scaler is not None:
+            extra["client_state"] = dict(extra["client_state"], _loss_scaler=self.loss_scaler.state_dict())
+        return ckpt.save(save_dir, tag, self.global_steps, self.module_state_dict(),
+                         None if self.stage >= 1 else self.optimizer_state_dict(), extra, self.config.to_dict(),
+                         zero_shard=self._zero_shard_state() if self.stage >= 1 else None,
+                         save_latest=save_latest)
+
+    def load_checkpoint(self, load_dir: str, tag: Optional[str] = None, load_optimizer_states: bool = True,
+                        load_lr_scheduler_states: bool = True) -> Tuple[Optional[str], Optional[dict]]:
+        path, states, shard = ckpt.load(load_dir, tag)
+        if states is None:
+            return None, None
+        sd = states["module"]
+        self.module.load_state_dict({k: v.to(self.dtype) if v.is_floating_point() else v for k, v in sd.items()})
+        self.global_steps = int(states.get("global_steps", 0))
+        self.global_samples = int(states.get("global_samples", 0))
+        self.skipped_steps = int(states.get("skipped_steps", 0))
+        if self.stage == 0:
+            if self.master.data_ptr() != self.store.param_buf.data_ptr():
+                self.master.copy_(self.store.param_buf.float())
+            if load_optimizer_states and states.get("optimizer"):
+                adam_state_to_flat(states["optimizer"], self.exp_avg, self.exp_avg_sq, self.layout.segments())
+        else:
+            if shard is None:
+                raise FileNotFoundError(f"missing ZeRO shard for rank {self.rank} under {path}")
+            if int(shard["partition_world_size"]) != self.world_size or int(shard["total"]) != self.layout.total:
+                raise RuntimeError("ZeRO checkpoint was written with a different world size / layout; "
+                                   "consolidate it with zero_to_fp32.py and load the fp32 weights instead")
+            self.master.copy_(shard["fp32_flat"].to(self.master))
+            if load_optimizer_states:
+                self.exp_avg.copy_(shard["exp_avg"].to(self.exp_avg))
+                self.exp_avg_sq.copy_(shard["exp_avg_sq"].to(self.exp_avg_sq))
+            if self.param_lp is not None:
+                self.param_lp.copy_(self.master)
+            self._allgather_params()
+        if load_lr_scheduler_states and states.get("lr_scheduler") is not None:
+            if self.ds_scheduler is not None:
+                self.ds_scheduler.load_state_dict(states["lr_scheduler"])
+                self.optimizer.param_groups[0]["lr"] = self.ds_scheduler.get_lr()
+            elif self.lr_scheduler is not None:
+                self.lr_scheduler.load_state_dict(states["lr_scheduler"])
+        cs = dict(states.get("client_state") or {})
+        if self.loss_scaler is not None and "_loss_scaler" in cs:
+            self.loss_scaler.load_state_dict(cs.pop("_loss_scaler"))
+        return path, cs
+
+    def close(self) -> None:
+        for h in self._hooks:
+            h.remove()
+        self._hooks = []
+        if self.oneshot is not None:
+            self.oneshot.close()
+            self.oneshot = None
+        self.metrics.close()
+
+
+def initialize(args=None, model: Optional[torch.nn.Module] = None, optimizer=None, model_parameters=None,
+               training_data=None, lr_scheduler=None, config=None, config_params=None, collate_fn=None,
+               dist_init_required: Optional[bool] = None):
+    """DeepSpeed-compatible ``initialize`` -> ``(engine, optimizer, training_dataloader, lr_scheduler)``.
+
+    ``config`` (or ``config_params``) is a dict or a JSON path.  ``args`` is accepted for call
+    compatibility (the reference passes its config dict there too) and is otherwise
+    used only for ``args.deepspeed_config``.
+    """
+    if model is None:
+        raise ValueError("initialize() needs a model")
+    cfg_src = config if config is not None else config_params
+    if cfg_src is None and args is not None and getattr(args, "deepspeed_config", None):
+        cfg_src = args.deepspeed_config
+    if not comm.is_initialized() and dist_init_required is not False:
+        comm.init_distributed()
+    cfg = parse_config(cfg_src, comm.get_world_size())
+    engine = Engine(model, cfg, optimizer=optimizer, lr_scheduler=lr_scheduler, model_parameters=model_parameters)
+    loader = None
+    if training_data is not None:
+        from torch.utils.data import DataLoader, DistributedSampler
+        sampler = DistributedSampler(training_data, num_replicas=comm.get_world_size(), rank=comm.get_rank())
+        loader = DataLoader(training_data, batch_size=cfg.train_micro_batch_size_per_gpu, sampler=sampler,
+                            collate_fn=collate_fn)
+    return engine, engine.optimizer, loader, (engine.ds_scheduler or lr_scheduler)

@@ -1,0 +1,125 @@
+"""Bucketed gradient reduction overlapped with backward.
+
+DeepSpeed stage 0 reduces ALL gradients after backward finishes (one 5e8-element bucket, SURVEY
+X6): communication never overlaps compute.  Here each bucket (a contiguous slice of the flat
+gradient buffer, ``runtime/flat.py``) is launched the moment autograd has accumulated the last
+gradient that belongs to it (``register_post_accumulate_grad_hook``), so RCCL moves bucket k over
+xGMI while backward computes bucket k-1.  ProcessGroupNCCL runs the collective on its own HIP
+stream, ordered after the producing kernels; ``finish()`` joins all of them before the optimizer.
+
+* stage 0: in-place ``all_reduce(SUM)`` of the bucket (or the IPC one-shot kernel for buckets up
+  to ``oneshot_max_bytes`` when a validated channel exists: one xGMI hop instead of a ring);
+* stage 1/2: ``reduce_scatter_tensor`` of the bucket into this rank's contiguous shard buffer.
+
+The 1/world_size averaging is NOT applied here; it is folded into the fused Adam kernel's
+``grad_scale`` (no extra pass over the gradients).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+from ..runtime.flat import FlatLayout
+
+
+class GradReducer:
+    def __init__(self, grad_buf: torch.Tensor, layout: FlatLayout, stage: int, world_size: int, rank: int,
+                 comm_dtype: Optional[torch.dtype] = None, oneshot=None, oneshot_max_bytes: int = 0,
+                 debug_sync: bool = False):
+        self.grad_buf = grad_buf
+        self.layout = layout
+        self.stage = stage
+        self.world_size = world_size
+        self.rank = rank
+        self.comm_dtype = comm_dtype or grad_buf.dtype
+        self.oneshot = oneshot
+        self.oneshot_max_bytes = oneshot_max_bytes
+        self.debug_sync = debug_sync
+        nb = len(layout.buckets)
+        self._param_count = [len(b.params) for b in layout.buckets]
+        self._remaining = list(self._param_count)
+        self._launched = [False] * nb
+        self._works: List = []
+        self.armed = False
+        # staging buffer when the wire dtype differs from the gradient dtype (e.g. bf16 grads, fp32 comm)
+        self.comm_buf = (torch.zeros(layout.total, dtype=self.comm_dtype, device=grad_buf.device)
+                         if self.comm_dtype != grad_buf.dtype else None)
+        if stage >= 1:
+            self.shard_offsets = []
+            off = 0
+            for b in layout.buckets:
+                self.shard_offsets.append(off)
+                off += b.numel // world_size
+            self.shard_grad = torch.zeros(off, dtype=self.comm_dtype, device=grad_buf.device)
+        else:
+            self.shard_offsets = []
+            self.shard_grad = None
+        self.bytes_reduced = 0
+
+    # the buffer the optimizer reads after finish()
+    @property
+    def reduced(self) -> torch.Tensor:
+        if self.stage >= 1:
+            return self.shard_grad
+        return self.comm_buf if self.comm_buf is not None else self.grad_buf
+
+    def arm(self, boundary: bool) -> None:
+        """Called before backward: only the accumulation-boundary micro-step communicates."""
+        self.armed = boundary
+        self._remaining = list(self._param_count)
+        self._launched = [False] * len(self._launched)
+        self._works = []
+
+    def on_grad_ready(self, param_index: int) -> None:
+        if not self.armed:
+            return
+        b = self.layout.param_bucket[param_index]
+        self._remaining[b] -= 1
+        if self._remaining[b] == 0:
+            self._launch(b)
+
+    def _launch(self, bi: int) -> None:
+        if self._launched[bi]:
+            return
+        self._launched[bi] = True
+        b = self.layout.buckets[bi]
+        src = self.grad_buf[b.start:b.start + b.numel]
+        if self.comm_buf is not None:
+            view = self.comm_buf[b.start:b.start + b.numel]
+            view.copy_(src)
+        else:
+            view = src
+        self.bytes_reduced += view.numel() * view.element_size()
+        if self.world_size == 1:
+            if self.stage >= 1:
+                self.shard_grad[self.shard_offsets[bi]:self.shard_offsets[bi] + b.numel].copy_(view)
+            return
+        if self.debug_sync and view.is_cuda:
+            torch.cuda.synchronize()
+        if self.stage == 0:
+            nbytes = view.numel() * view.element_size()
+            if (self.oneshot is not None and view.dtype == torch.float32 and nbytes <= self.oneshot_max_bytes
+                    and view.numel() <= self.oneshot.stride):
+                self.oneshot.allreduce(view, view, 1.0)
+            else:
+                self._works.append(dist.all_reduce(view, async_op=True))
+        else:
+            n = b.numel // self.world_size
+            out = self.shard_grad[self.shard_offsets[bi]:self.shard_offsets[bi] + n]
+            self._works.append(dist.reduce_scatter_tensor(out, view, async_op=True))
+
+    def finish(self) -> None:
+        """Launch buckets that received no gradient (unused params), then join all collectives."""
+        if not self.armed:
+            return
+        for bi in reversed(range(len(self._launched))):
+            if not self._launched[bi]:
+                self._launch(bi)
+        for w in self._works:
+            w.wait()
+        self._works = []
+        if self.debug_sync and self.grad_buf.is_cuda:
+            torch.cuda.synchronize()
+        self.armed = False

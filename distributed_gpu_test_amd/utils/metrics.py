@@ -1,0 +1,76 @@
+"""Structured metrics: a JSONL sink and a throughput timer.
+
+DeepSpeed's ``ThroughputTimer`` derives samples/sec from ``train_batch_size`` (which the reference
+hard-codes to 64 while the real global batch is 4 x world_size), so it over-reports.
+``ThroughputTimer`` here counts the samples actually processed.  ``MetricsSink`` writes one JSON
+object per optimizer step when ``DGT_METRICS_JSONL`` names a file (``{rank}`` is substituted).
+"""
+from __future__ import annotations
+
+import json
+import os
+import time
+from typing import Any, Dict, Optional
+
+
+class ThroughputTimer:
+    def __init__(self, samples_per_step: int, window: int = 10):
+        self.samples_per_step = samples_per_step
+        self.window = max(1, window)
+        self._t_start: Optional[float] = None
+        self._window_t0: Optional[float] = None
+        self._window_steps = 0
+        self._last_sps: Optional[float] = None
+        self.total_steps = 0
+        self.total_time = 0.0
+
+    def start(self) -> None:
+        if self._t_start is None:
+            self._t_start = time.perf_counter()
+        if self._window_t0 is None:
+            self._window_t0 = time.perf_counter()
+
+    def stop(self, global_step: int) -> None:
+        self._window_steps += 1
+        self.total_steps += 1
+        if self._window_steps >= self.window and self._window_t0 is not None:
+            dt = time.perf_counter() - self._window_t0
+            if dt > 0:
+                self._last_sps = self._window_steps * self.samples_per_step / dt
+                self.total_time += dt
+            self._window_t0 = time.perf_counter()
+            self._window_steps = 0
+
+    def samples_per_sec(self) -> Optional[float]:
+        return self._last_sps
+
+
+class MetricsSink:
+    def __init__(self, path: Optional[str]):
+        self.path = path
+        self._fh = open(path, "a") if path else None
+
+    @classmethod
+    def from_env(cls, rank: int) -> "MetricsSink":
+        p = os.environ.get("DGT_METRICS_JSONL")
+        if not p:
+            return cls(None)
+        p = p.replace("{rank}", str(rank))
+        if "{rank}" not in os.environ.get("DGT_METRICS_JSONL", "") and rank != 0:
+            return cls(None)  # one shared file: rank 0 only
+        d = os.path.dirname(p)
+        if d:
+            os.makedirs(d, exist_ok=True)
+        return cls(p)
+
+    def log(self, record: Dict[str, Any]) -> None:
+        if self._fh is None:
+            return
+        rec = {"ts": time.time(), **{k: v for k, v in record.items() if v is not None}}
+        self._fh.write(json.dumps(rec) + "\n")
+        self._fh.flush()
+
+    def close(self) -> None:
+        if self._fh is not None:
+            self._fh.close()
+            self._fh = None
