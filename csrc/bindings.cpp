@@ -86,6 +86,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
                     int64_t rank, int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks) {
   TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
               " H=", hidden);
+  TORCH_CHECK(beta1 > 0.5 && beta1 < 1.0 && beta2 > 0.0 && beta2 < 1.0, "dgt: fused kernel needs 0.5 < beta1 < 1");
   check_gpu(X, "X", at::kFloat);
   check_gpu(Y, "Y", at::kFloat);
   check_gpu(plan, "plan", at::kInt);
@@ -121,6 +122,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   a.loss_acc = loss_acc.data_ptr<double>();
   a.status = status.data_ptr<int>();
   a.ex = make_exchange(data_ptrs, flag_ptrs, rank, world_size, stride, seq_base, timeout_ticks);
+  a.stamps = nullptr;
   if (world_size > 1) TORCH_CHECK(stride >= pp, "dgt: mailbox stride ", stride, " < ", pp);
   if (a.n_steps == 0) return;
   DGT_CHECK_HIP(dgt::tiny_mlp_train((int)n_features, (int)hidden, a, stream_of(X)));

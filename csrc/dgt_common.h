@@ -118,4 +118,20 @@ DGT_DEVICE float adam_update(float p, float g, float& m, float& v, const AdamHyp
   return p + step_size_neg * (m / denom);
 }
 
+// Latency-optimised variant for the persistent tiny-model kernel: hardware v_sqrt_f32 / v_rcp_f32
+// (<= 1 ulp) instead of the IEEE division sequences, and the 1/sqrt(1 - beta2^t) factor as a
+// multiply.  Differs from adam_update by a few ulp per step; exact-formula Adam stays in adam_flat.
+DGT_DEVICE float adam_update_fast(float p, float g, float& m, float& v, const AdamHyper& h,
+                                  float step_size_neg, float inv_bc2_sqrt) {
+  if (h.weight_decay != 0.f) {
+    if (h.adamw) p = p * h.decay;
+    else g = fmaf(h.weight_decay, p, g);
+  }
+  m = fmaf(h.one_minus_beta1, g - m, m);  // torch.lerp, weight < 0.5 branch (host checks beta1 > 0.5)
+  v = v * h.beta2;
+  v = v + h.one_minus_beta2 * g * g;
+  const float denom = fmaf(__builtin_amdgcn_sqrtf(v), inv_bc2_sqrt, h.eps);
+  return fmaf(step_size_neg, m * __builtin_amdgcn_rcpf(denom), p);
+}
+
 }  // namespace dgt

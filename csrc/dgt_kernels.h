@@ -29,6 +29,7 @@ struct TinyTrainArgs {
   double* loss_acc;      // += sum over steps of the step's mean loss
   int* status;           // Status
   Exchange ex;           // world_size 1 -> no exchange
+  unsigned long long* stamps;  // diagnostic builds only (-DDGT_TINY_STAMPS); nullptr otherwise
 };
 
 hipError_t tiny_mlp_train(int n_features, int hidden, const TinyTrainArgs& a, hipStream_t stream);

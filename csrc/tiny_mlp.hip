@@ -4,14 +4,21 @@
 // Design (MI355X-first, not a translation of the reference's ~30 ATen/cuBLAS launches per step):
 //   * ONE workgroup of H/16 waves trains the model; a launch runs many optimizer steps.
 //   * Each wave OWNS 16 hidden units end to end: its rows of W1, its slice of b1 and W2, their
-//     gradients, their Adam moments (registers) and a private copy of the minibatch.  The only
-//     cross-wave dependency of a step is the sum of the per-wave partial logits, so a step has
-//     ONE workgroup barrier (the partial-logit buffer is double-buffered by step parity).
-//     The shared scalar b2 is updated redundantly (bit-identically) by every wave.
+//     gradients and Adam moments — all in VGPRs for the whole launch.  The only cross-wave
+//     dependency of a step is the sum of the per-wave partial logits, so a step has ONE workgroup
+//     barrier (the partial-logit buffer is double-buffered by step parity).  The shared scalar b2
+//     is updated redundantly (bit-identically) by every wave.
 //   * Both GEMM-shaped products run on the matrix cores with exact-fp32 MFMA
-//     (v_mfma_f32_16x16x4_f32): the forward x.W1^T (M = batch, N = the wave's 16 hidden units,
-//     K = features) and the weight gradient dh^T.x (M = hidden, N = features, K = batch).
-//     Operands are staged through LDS with padded strides.
+//     (v_mfma_f32_16x16x4_f32).  The weight gradient is computed transposed,
+//     dW1^T[k][j] = sum_b x[b][k] dh[b][j], so lane (l&15, l>>4) receives dW1[j = l&15][k] for
+//     k = 16ct + 4(l>>4) + r.  The forward H^T = W1 . X^T walks its K dimension in exactly that
+//     permuted order, so the lane that receives a weight's gradient is the lane that owns the
+//     weight, updates it with Adam and feeds it to the next forward MFMA — no LDS round trip for
+//     parameters or gradients.  The forward's x operand comes straight from HBM/L2 as float4
+//     rows; LDS only stages the two transposed operands of the weight-gradient MFMA.
+//   * b1 is folded into the GEMMs as an augmented weight column: x carries a constant 1 at feature
+//     index F, so the forward MFMA adds the bias and the weight-gradient MFMA produces db1 in the
+//     same registers as dW1.  W2 is owned by 4 lanes per DPP row and broadcast with row_newbcast.
 //   * Row reductions use DPP (v_add_f32_dpp) and the gfx950 v_permlane{16,32}_swap exchanges,
 //     never ds_bpermute.
 //   * Minibatch rows are gathered from the device-resident dataset by sampler index; the next
@@ -26,45 +33,56 @@
 
 namespace dgt {
 
+// Diagnostic build only (-DDGT_TINY_STAMPS): per-section s_memtime cycle sums of wave 0 / wave 1
+// written to TinyTrainArgs::stamps.  The shipped kernel executes no stamp.
+#ifdef DGT_TINY_STAMPS
+#define DGT_STAMP(i)                                                                    \
+  do {                                                                                  \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    unsigned long long t_;                                                              \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t_)::"memory");         \
+    __builtin_amdgcn_sched_barrier(0);                                                  \
+    if ((i) > 0) st_acc[(i)-1] += t_ - st_last;                                         \
+    st_last = t_;                                                                       \
+  } while (0)
+#else
+#define DGT_STAMP(i) do {} while (0)
+#endif
+
 template <int F, int H>
 struct TinyCfg {
   static constexpr int NW = H / 16;              // waves; wave w owns hidden units [16w, 16w+16)
   static constexpr int T = 64 * NW;              // threads
-  static constexpr int FP = (F + 3) / 4 * 4;     // K of the forward GEMM, padded for 16x16x4
-  static constexpr int NKT = (F + 15) / 16;      // 16-wide feature tiles of the weight gradient
-  static constexpr int SX = NKT * 16 + 1;        // LDS row stride of the batch (+1: no 16-way conflict)
-  static constexpr int BM = 16;                  // max micro-batch (MFMA M of the forward)
+  static constexpr int NKT = (F + 1 + 15) / 16;  // 16-wide tiles of the augmented features [x, 1]
+  static constexpr int NS = 4 * NKT;             // W1 slots per lane: (ct, r) -> k = 16ct + 4(l>>4) + r
+  static constexpr int SX = NKT * 16 + 1;        // LDS row stride of the staged batch (+1: conflict-free)
+  static constexpr int BM = 16;                  // max micro-batch (MFMA N of the forward)
   static constexpr int P = H * F + 2 * H + 1;    // global flat parameter count
   static constexpr int PP = (P + 3) / 4 * 4;
-  // a wave's local parameter vector: [W1 rows 16 x F][b1 16][W2 16][b2]
-  static constexpr int L_B1 = 16 * F, L_W2 = 16 * F + 16, L_B2 = 16 * F + 32;
-  static constexpr int WP = 16 * F + 33;
-  static constexpr int NPL = (WP + 63) / 64;     // owned elements per lane
-  static constexpr int WPP = NPL * 64;
-  static constexpr int XE = BM * F;
-  static constexpr int XPL = (XE + 63) / 64;     // batch elements each lane stages
   static constexpr int G_B1 = H * F, G_W2 = H * F + H, G_B2 = H * F + 2 * H;
   static_assert(H % 16 == 0 && H >= 16 && H <= 256, "hidden must be a multiple of 16 in [16, 256]");
-  static_assert(F >= 1 && F <= 64, "n_features must be in [1, 64]");
+  static_assert(F % 4 == 0 && F >= 4 && F <= 64, "n_features must be a multiple of 4 in [4, 64]");
 
-  // local element e of wave w -> index in the global flat vector
-  static DGT_HOST_DEVICE int global_index(int w, int e) {
-    if (e < L_B1) return 16 * w * F + e;
-    if (e < L_W2) return G_B1 + 16 * w + (e - L_B1);
-    if (e < L_B2) return G_W2 + 16 * w + (e - L_W2);
-    return G_B2;
+  // feature index of W1 slot i (= 4ct + r) in lane-row lq
+  static DGT_HOST_DEVICE int slot_k(int i, int lq) { return 16 * (i >> 2) + 4 * lq + (i & 3); }
+  // global index of W1 slot i of lane (lr, lq) in wave w: W1 column k < F, b1 at k == F, else -1
+  static DGT_HOST_DEVICE int slot_index(int w, int lr, int lq, int i) {
+    const int k = slot_k(i, lq);
+    if (k < F) return (16 * w + lr) * F + k;
+    if (k == F) return G_B1 + 16 * w + lr;
+    return -1;
+  }
+  // global index of the W2 element owned by lane (lr < 4, lq) of wave w; -1 if none
+  static DGT_HOST_DEVICE int bw_index(int w, int lr, int lq) {
+    return lr < 4 ? G_W2 + 16 * w + 4 * lq + lr : -1;
   }
 };
 
 template <int F, int H>
 struct __attribute__((aligned(16))) WaveSmem {
   using C = TinyCfg<F, H>;
-  float P[C::WPP];           // this wave's parameters
-  float G[C::WPP];           // their gradient for the current step
-  float X[C::BM * C::SX];    // private copy of the minibatch (rows >= batch, cols >= F are zero)
-  float DH[C::BM * 17];      // dL/d(pre-activation) of this wave's 16 hidden units
-  float Y[C::BM];
-  int idx[C::BM];            // sample indices of the NEXT step (prefetch pipeline)
+  float X[C::BM * C::SX];    // this step's minibatch, row-major (A operand of the weight gradient)
+  float DH[C::BM * 17];      // dL/d(pre-activation) [batch][hidden] (B operand of the weight gradient)
 };
 
 template <int F, int H>
@@ -75,76 +93,124 @@ struct __attribute__((aligned(16))) TinySmem {
   int err;
 };
 
-// ------------------------------------------------------------------ per-wave step pieces
-
-// Forward GEMM on MFMA + bias + ReLU; publishes this wave's partial logits into Zbuf.
+// Register-resident per-lane training state of one wave.
 template <int F, int H>
-DGT_DEVICE void wave_forward(WaveSmem<F, H>& ws, float* Zbuf, int w, int l, float (&h)[4]) {
+struct LaneState {
   using C = TinyCfg<F, H>;
-  const int lr = l & 15, lq = l >> 4;
-  // 16x16x4 f32 operand maps: A[i = l&15][k = l>>4], B[k = l>>4][j = l&15];
-  // D: col = l&15 (hidden unit), row = 4*(l>>4) + r (batch row).
-  f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+  float w1[C::NS], m1[C::NS], v1[C::NS];  // [W1 | b1][16w + (l&15)][slot_k(i, l>>4)]
+  float bw, mbw, vbw;                      // W2 element (lanes 0-3 of each DPP row)
+  float b2, mb2, vb2;                      // replicated in every lane
+};
+
+template <int F, int H>
+DGT_DEVICE void load_state(LaneState<F, H>& st, const float* __restrict__ p, const float* __restrict__ m,
+                           const float* __restrict__ v, int w, int lr, int lq) {
+  using C = TinyCfg<F, H>;
 #pragma unroll
-  for (int ks = 0; ks < C::FP / 4; ++ks) {
-    const int k = 4 * ks + lq;
-    const float a = ws.X[lr * C::SX + k];
-    const float b = (F % 4 == 0 || k < F) ? ws.P[lr * F + k] : 0.f;
-    acc = __builtin_amdgcn_mfma_f32_16x16x4f32(a, b, acc, 0, 0, 0);
+  for (int i = 0; i < C::NS; ++i) {
+    const int gi = C::slot_index(w, lr, lq, i);
+    const bool ok = gi >= 0;
+    st.w1[i] = ok ? p[gi] : 0.f;
+    st.m1[i] = (ok && m) ? m[gi] : 0.f;
+    st.v1[i] = (ok && v) ? v[gi] : 0.f;
   }
-  const float b1 = ws.P[C::L_B1 + lr];
-  const float w2 = ws.P[C::L_W2 + lr];
-#pragma unroll
-  for (int r = 0; r < 4; ++r) {
-    h[r] = fmaxf(acc[r] + b1, 0.f);
-    const float pz = wave_sum16(h[r] * w2);
-    if (lr == 0) Zbuf[w * 16 + 4 * lq + r] = pz;
-  }
+  const int bi = C::bw_index(w, lr, lq);
+  st.bw = bi >= 0 ? p[bi] : 0.f;
+  st.mbw = (bi >= 0 && m) ? m[bi] : 0.f;
+  st.vbw = (bi >= 0 && v) ? v[bi] : 0.f;
+  st.b2 = p[C::G_B2];
+  st.mb2 = m ? m[C::G_B2] : 0.f;
+  st.vb2 = v ? v[C::G_B2] : 0.f;
 }
 
-// After the barrier: logits, loss, backward into ws.G.  Returns the step's mean loss (every lane).
-template <int F, int H, bool WANT_LOSS>
-DGT_DEVICE float wave_backward(WaveSmem<F, H>& ws, const float* Zbuf, int l, const float (&h)[4], int Bt,
-                               float invB) {
+// Minibatch values for the lane's row b = l&15: x[b][slot_k(i, l>>4)] and y[b] (0 when padding).
+template <int F, int H>
+DGT_DEVICE void load_rows(const float* __restrict__ X, const float* __restrict__ Y, int id, int lq,
+                          float (&x)[TinyCfg<F, H>::NS], float& y) {
   using C = TinyCfg<F, H>;
-  const int lr = l & 15, lq = l >> 4;
-  const float b2 = ws.P[C::L_B2];
-  const float w2 = ws.P[C::L_W2 + lr];
-  float lsum = 0.f, dw2 = 0.f, db1 = 0.f, db2 = 0.f;
+#pragma unroll
+  for (int ct = 0; ct < C::NKT; ++ct) {
+    f32x4 q = {0.f, 0.f, 0.f, 0.f};
+    const int k0 = 16 * ct + 4 * lq;
+    if (id >= 0 && k0 < F) q = *reinterpret_cast<const f32x4*>(X + (long long)id * F + k0);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) x[4 * ct + r] = (id >= 0 && k0 + r == F) ? 1.f : q[r];  // bias feature
+  }
+  y = id >= 0 ? Y[id] : 0.f;
+}
+
+// Forward (MFMA) + bias + ReLU; publishes the wave's partial logits; stages x for the wgrad.
+// H^T = W1 . X^T with K visited in slot order: A[i = l&15][kk = l>>4] = W1[j = l&15][slot_k],
+// B[kk = l>>4][col = l&15] = x[b = l&15][slot_k]; D: col = batch row b = l&15,
+// row = hidden 4*(l>>4) + r.
+template <int F, int H>
+DGT_DEVICE void wave_forward(const LaneState<F, H>& st, WaveSmem<F, H>& ws, float* Zbuf, int w, int lr, int lq,
+                             const float (&x)[TinyCfg<F, H>::NS], float (&h)[4], float (&w2v)[4]) {
+  using C = TinyCfg<F, H>;
+  // two independent accumulation chains halve the dependent-MFMA latency
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < C::NS; i += 2) {
+    acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(st.w1[i], x[i], acc0, 0, 0, 0);
+    if (i + 1 < C::NS) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(st.w1[i + 1], x[i + 1], acc1, 0, 0, 0);
+  }
+  const f32x4 acc = acc0 + acc1;
+  // stage this step's rows for the weight-gradient MFMA (row-major, conflict-free stride)
+#pragma unroll
+  for (int i = 0; i < C::NS; ++i) ws.X[lr * C::SX + 16 * (i >> 2) + 4 * lq + (i & 3)] = x[i];
+  w2v[0] = dpp_mov<0x150>(st.bw);  // row_newbcast: W2[4lq + r] from lane r of the DPP row
+  w2v[1] = dpp_mov<0x151>(st.bw);
+  w2v[2] = dpp_mov<0x152>(st.bw);
+  w2v[3] = dpp_mov<0x153>(st.bw);
+  float pz = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
-    const int b = 4 * lq + r;
-    float s = 0.f;
-#pragma unroll
-    for (int ww = 0; ww < C::NW; ++ww) s += Zbuf[ww * 16 + b];
-    const float z = s + b2;
-    const float y = ws.Y[b];
-    const bool valid = b < Bt;
-    // BCE-with-logits (torch: (1-y)*z - log_sigmoid(z)); d/dz = sigmoid(z) - y, times 1/B (mean)
-    const float e = __expf(-fabsf(z));
-    const float rinv = __builtin_amdgcn_rcpf(1.f + e);
-    const float sig = (z >= 0.f) ? rinv : e * rinv;
-    const float dz = valid ? (sig - y) * invB : 0.f;
-    if (WANT_LOSS) lsum += valid ? (1.f - y) * z - (fminf(z, 0.f) - __logf(1.f + e)) : 0.f;
-    dw2 = fmaf(dz, h[r], dw2);
-    const float dh = (h[r] > 0.f) ? dz * w2 : 0.f;
-    ws.DH[b * 17 + lr] = dh;
-    db1 += dh;
-    db2 += dz;
+    h[r] = fmaxf(acc[r], 0.f);  // bias already added by the augmented column
+    pz = fmaf(h[r], w2v[r], pz);
   }
-  dw2 = wave_sum_groups(dw2);
-  db1 = wave_sum_groups(db1);
-  db2 = wave_sum_groups(db2);
-  if (lq == 0) {
-    ws.G[C::L_W2 + lr] = dw2;
-    ws.G[C::L_B1 + lr] = db1;
-  }
-  if (l == 0) ws.G[C::L_B2] = db2;
-  __builtin_amdgcn_wave_barrier();
+  pz = wave_sum_groups(pz);  // over the wave's 16 hidden units, for row b = l&15
+  if (lq == 0) Zbuf[w * 16 + lr] = pz;
+}
 
-  // weight gradient on MFMA: dW1[jj][k] = sum_b dh[b][jj] * x[b][k]
-  // A[i = hidden (l&15)][kk = batch (l>>4)], B[kk = batch][col = feature (l&15)];
-  // D: col = feature 16*ct + (l&15), row = hidden 4*(l>>4) + r.
+struct StepGrads {
+  float bw, b2, loss;
+};
+
+// After the barrier: logits, BCE, backward.  W1 gradients land in gw1 (slot layout).
+template <int F, int H, bool WANT_LOSS>
+DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws, const float* Zbuf, int lr,
+                                   int lq, const float (&h)[4], const float (&w2v)[4], float y, int Bt,
+                                   float invB, float (&gw1)[TinyCfg<F, H>::NS]) {
+  using C = TinyCfg<F, H>;
+  float s = 0.f;
+#pragma unroll
+  for (int ww = 0; ww < C::NW; ++ww) s += Zbuf[ww * 16 + lr];
+  const float z = s + st.b2;
+  const bool valid = lr < Bt;
+  // BCE-with-logits (torch: (1-y)*z - log_sigmoid(z)); d/dz = sigmoid(z) - y, times 1/B (mean)
+  const float e = __expf(-fabsf(z));
+  const float rinv = __builtin_amdgcn_rcpf(1.f + e);
+  const float sig = (z >= 0.f) ? rinv : e * rinv;
+  const float dz = valid ? (sig - y) * invB : 0.f;
+  StepGrads out;
+  out.loss = 0.f;
+  if (WANT_LOSS) out.loss = wave_sum16(valid ? (1.f - y) * z - (fminf(z, 0.f) - __logf(1.f + e)) : 0.f) * invB;
+  float dw2[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    ws.DH[lr * 17 + 4 * lq + r] = (h[r] > 0.f) ? dz * w2v[r] : 0.f;
+    dw2[r] = wave_sum16(dz * h[r]);  // over the 16 batch rows: W2[4lq + r]
+  }
+  out.b2 = wave_sum16(dz);
+  // the lane's own W2 element (lanes 0-3 of each row); db1 comes out of the wgrad MFMA
+  float gbw = 0.f;
+#pragma unroll
+  for (int r = 0; r < 4; ++r) gbw = (lr == r) ? dw2[r] : gbw;
+  out.bw = gbw;
+  __builtin_amdgcn_wave_barrier();
+  // weight gradient on MFMA, transposed: dW1^T[k][j] = sum_b x[b][k] dh[b][j]
+  // A[i = k (l&15)][kk = b (l>>4)] = x[b][16ct + (l&15)], B[kk = b][col = j (l&15)] = dh[b][j];
+  // D: lane (lr, lq) gets dW1[j = lr][k = 16ct + 4lq + r] = W1 slot 4ct + r.
   const int nks = (Bt + 3) >> 2;
 #pragma unroll
   for (int ct = 0; ct < C::NKT; ++ct) {
@@ -153,65 +219,18 @@ DGT_DEVICE float wave_backward(WaveSmem<F, H>& ws, const float* Zbuf, int l, con
     for (int ks = 0; ks < C::BM / 4; ++ks) {
       if (ks < nks) {  // wave-uniform
         const int b = 4 * ks + lq;
-        g = __builtin_amdgcn_mfma_f32_16x16x4f32(ws.DH[b * 17 + lr], ws.X[b * C::SX + 16 * ct + lr], g, 0, 0, 0);
+        g = __builtin_amdgcn_mfma_f32_16x16x4f32(ws.X[b * C::SX + 16 * ct + lr], ws.DH[b * 17 + lr], g, 0, 0, 0);
       }
     }
-    const int k = 16 * ct + lr;
-    if (k < F) {
 #pragma unroll
-      for (int r = 0; r < 4; ++r) ws.G[(4 * lq + r) * F + k] = g[r];
-    }
+    for (int r = 0; r < 4; ++r) gw1[4 * ct + r] = g[r];
   }
   __builtin_amdgcn_wave_barrier();
-  return WANT_LOSS ? wave_sum_groups(lsum) * invB : 0.f;
-}
-
-// Gather the x / y values this lane stages for one step (rows from ws.idx).
-template <int F, int H>
-DGT_DEVICE void gather_rows(const WaveSmem<F, H>& ws, const float* __restrict__ X, const float* __restrict__ Y,
-                            int l, float (&xv)[TinyCfg<F, H>::XPL], float& yv) {
-  using C = TinyCfg<F, H>;
-#pragma unroll
-  for (int q = 0; q < C::XPL; ++q) {
-    const int e = l + 64 * q;
-    float v = 0.f;
-    if (e < C::XE) {
-      const int id = ws.idx[e / F];
-      if (id >= 0) v = X[(long long)id * F + (e % F)];
-    }
-    xv[q] = v;
-  }
-  yv = 0.f;
-  if (l < C::BM) {
-    const int id = ws.idx[l];
-    if (id >= 0) yv = Y[id];
-  }
-}
-
-template <int F, int H>
-DGT_DEVICE void stage_rows(WaveSmem<F, H>& ws, int l, const float (&xv)[TinyCfg<F, H>::XPL], float yv) {
-  using C = TinyCfg<F, H>;
-#pragma unroll
-  for (int q = 0; q < C::XPL; ++q) {
-    const int e = l + 64 * q;
-    if (e < C::XE) ws.X[(e / F) * C::SX + (e % F)] = xv[q];
-  }
-  if (l < C::BM) ws.Y[l] = yv;
+  return out;
 }
 
 DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row) {
   return (step < n_steps && row < bmax) ? plan[(long long)step * bmax + row] : -1;
-}
-
-template <int F, int H>
-DGT_DEVICE void wave_init(WaveSmem<F, H>& ws, const float* __restrict__ params, int w, int l) {
-  using C = TinyCfg<F, H>;
-  for (int e = l; e < C::WPP; e += 64) {
-    ws.P[e] = (e < C::WP) ? params[C::global_index(w, e)] : 0.f;
-    ws.G[e] = 0.f;
-  }
-  for (int i = l; i < C::BM * C::SX; i += 64) ws.X[i] = 0.f;
-  for (int i = l; i < C::BM * 17; i += 64) ws.DH[i] = 0.f;
 }
 
 // ------------------------------------------------------------------ persistent training kernel
@@ -219,7 +238,7 @@ template <int F, int H>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
   __shared__ TinySmem<F, H> sm;
-  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, lr = l & 15, lq = l >> 4;
   const Exchange& ex = a.ex;
   WaveSmem<F, H>& ws = sm.w[w];
 
@@ -229,74 +248,62 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     return;
   }
 
-  // ---- prologue: parameters -> LDS, moments -> registers, batch 0 staged, batch 1 indices ready
-  wave_init<F, H>(ws, a.params, w, l);
+  // ---- prologue: state -> registers, LDS zeroed, batch 0 loaded, indices of steps 1 and 2 in flight
+  LaneState<F, H> st;
+  load_state<F, H>(st, a.params, a.exp_avg, a.exp_avg_sq, w, lr, lq);
+  for (int i = l; i < C::BM * C::SX; i += 64) ws.X[i] = 0.f;
+  for (int i = l; i < C::BM * 17; i += 64) ws.DH[i] = 0.f;
   if (t == 0) sm.err = 0;
-  float m[C::NPL], v[C::NPL];
-#pragma unroll
-  for (int i = 0; i < C::NPL; ++i) {
-    const int e = l + 64 * i;
-    m[i] = v[i] = 0.f;
-    if (e < C::WP) {
-      const int gi = C::global_index(w, e);
-      m[i] = a.exp_avg[gi];
-      v[i] = a.exp_avg_sq[gi];
-    }
-  }
-  if (l < C::BM) ws.idx[l] = plan_at(a.plan, a.n_steps, a.bmax, 0, l);
-  __builtin_amdgcn_wave_barrier();
-  float xv[C::XPL], yv;
-  gather_rows<F, H>(ws, a.X, a.Y, l, xv, yv);
-  __builtin_amdgcn_wave_barrier();
-  stage_rows<F, H>(ws, l, xv, yv);
-  if (l < C::BM) ws.idx[l] = plan_at(a.plan, a.n_steps, a.bmax, 1, l);
-  int idx_reg = (l < C::BM) ? plan_at(a.plan, a.n_steps, a.bmax, 2, l) : -1;
+  float x[C::NS], y, xn[C::NS], yn;
+  load_rows<F, H>(a.X, a.Y, plan_at(a.plan, a.n_steps, a.bmax, 0, lr), lq, x, y);
+  int idx_next = plan_at(a.plan, a.n_steps, a.bmax, 1, lr);
+  int idx_next2 = plan_at(a.plan, a.n_steps, a.bmax, 2, lr);
   __syncthreads();
 
   double b1p = pow(a.beta1, (double)a.adam_step0);
   double b2p = pow(a.beta2, (double)a.adam_step0);
   double loss_total = 0.0;
   const float inv_ws = 1.0f / (float)ex.world_size;
+#ifdef DGT_TINY_STAMPS
+  unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0;
+#endif
   for (int s = 0; s < a.n_steps; ++s) {
+    DGT_STAMP(0);
     const int Bt = a.counts[s];
-    const float invB = 1.0f / (float)Bt;
-    // prefetch step s+1 rows (indices already in ws.idx); consumed after this step's wgrad
-    if (s + 1 < a.n_steps) gather_rows<F, H>(ws, a.X, a.Y, l, xv, yv);
+    const float invB = __builtin_amdgcn_rcpf((float)Bt);
+    // prefetch step s+1 rows into registers; consumed by the next step's forward
+    load_rows<F, H>(a.X, a.Y, idx_next, lq, xn, yn);
 
-    float h[4];
+    float h[4], w2v[4];
     float* Zb = sm.Z[s & 1];
-    wave_forward<F, H>(ws, Zb, w, l, h);
+    wave_forward<F, H>(st, ws, Zb, w, lr, lq, x, h, w2v);
+    DGT_STAMP(1);
     __syncthreads();  // the step's only workgroup barrier: all partial logits published
+    DGT_STAMP(2);
     if (sm.err) break;
-    const float step_loss = (w == 0) ? wave_backward<F, H, true>(ws, Zb, l, h, Bt, invB)
-                                     : wave_backward<F, H, false>(ws, Zb, l, h, Bt, invB);
-
-    // this wave is done reading its batch copy: stage the next one
-    if (s + 1 < a.n_steps) stage_rows<F, H>(ws, l, xv, yv);
-    if (l < C::BM) {
-      ws.idx[l] = idx_reg;
-      idx_reg = plan_at(a.plan, a.n_steps, a.bmax, s + 3, l);
-    }
-
-    float g[C::NPL];
-#pragma unroll
-    for (int i = 0; i < C::NPL; ++i) g[i] = ws.G[l + 64 * i];
+    float gw1[C::NS];
+    const StepGrads sg = (w == 0) ? wave_backward<F, H, true>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1)
+                                  : wave_backward<F, H, false>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
+    float gbw = sg.bw, gb2 = sg.b2;
+    DGT_STAMP(3);
 
     if (ex.world_size > 1) {
-      // ---- one-shot exchange of this wave's slice over xGMI: push, flag, wait, sum in rank order
+      // ---- one-shot exchange of this wave's gradients over xGMI: push, flag, wait, sum in rank order
       const long long seq = ex.seq_base + s;
       const int parity = (int)(seq & 1);
       const unsigned val = (unsigned)(seq + 1);
+      const long long mine = (long long)(parity * kMaxRanks + ex.rank) * ex.stride;
+      const int bi = C::bw_index(w, lr, lq);
+      for (int p = 0; p < ex.world_size; ++p) {
+        if (p == ex.rank) continue;
+        float* dst = ex.data[p] + mine;
 #pragma unroll
-      for (int i = 0; i < C::NPL; ++i) {
-        const int e = l + 64 * i;
-        if (e < C::WP) {
-          const long long gi = C::global_index(w, e);
-          for (int p = 0; p < ex.world_size; ++p) {
-            if (p == ex.rank) continue;
-            ex.data[p][(long long)(parity * kMaxRanks + ex.rank) * ex.stride + gi] = g[i];
-          }
+        for (int i = 0; i < C::NS; ++i) {
+          const int gi = C::slot_index(w, lr, lq, i);
+          if (gi >= 0) dst[gi] = gw1[i];
         }
+        if (bi >= 0) dst[bi] = gbw;
+        if (l == 0) dst[C::G_B2] = gb2;
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -308,43 +315,71 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_wave_barrier();
+      float sw1[C::NS], sbw = 0.f, sb2 = 0.f;
 #pragma unroll
-      for (int i = 0; i < C::NPL; ++i) {
-        const int e = l + 64 * i;
-        if (e < C::WP) {
-          const long long gi = C::global_index(w, e);
-          float sum = 0.f;
-          for (int p = 0; p < ex.world_size; ++p)
-            sum += (p == ex.rank) ? g[i] : ex.data[ex.rank][(long long)(parity * kMaxRanks + p) * ex.stride + gi];
-          g[i] = sum * inv_ws;
+      for (int i = 0; i < C::NS; ++i) sw1[i] = 0.f;
+      for (int p = 0; p < ex.world_size; ++p) {
+        const float* src = ex.data[ex.rank] + (long long)(parity * kMaxRanks + p) * ex.stride;
+        const bool own = p == ex.rank;
+#pragma unroll
+        for (int i = 0; i < C::NS; ++i) {
+          const int gi = C::slot_index(w, lr, lq, i);
+          if (gi >= 0) sw1[i] += own ? gw1[i] : src[gi];
         }
+        if (bi >= 0) sbw += own ? gbw : src[bi];
+        sb2 += own ? gb2 : src[C::G_B2];
       }
+#pragma unroll
+      for (int i = 0; i < C::NS; ++i) gw1[i] = sw1[i] * inv_ws;
+      gbw = sbw * inv_ws;
+      gb2 = sb2 * inv_ws;
     }
+    DGT_STAMP(4);
 
-    // ---- Adam (torch foreach op order); bias correction formed in double like torch does on host
+    // ---- Adam; bias corrections from double running powers (torch forms them in double on host)
     b1p *= a.beta1;
     b2p *= a.beta2;
-    const float step_size_neg = (float)(-(a.lr / (1.0 - b1p)));
-    const float bc2_sqrt = (float)sqrt(1.0 - b2p);
+    const float step_size_neg = -a.hp.lr * __builtin_amdgcn_rcpf((float)(1.0 - b1p));
+    const float inv_bc2_sqrt = __builtin_amdgcn_rsqf((float)(1.0 - b2p));
 #pragma unroll
-    for (int i = 0; i < C::NPL; ++i) {
-      const int e = l + 64 * i;
-      if (e < C::WP) ws.P[e] = adam_update(ws.P[e], g[i], m[i], v[i], a.hp, step_size_neg, bc2_sqrt);
-    }
-    __builtin_amdgcn_wave_barrier();
-    loss_total += (double)step_loss;
+    for (int i = 0; i < C::NS; ++i)
+      st.w1[i] = adam_update_fast(st.w1[i], gw1[i], st.m1[i], st.v1[i], a.hp, step_size_neg, inv_bc2_sqrt);
+    st.bw = adam_update_fast(st.bw, gbw, st.mbw, st.vbw, a.hp, step_size_neg, inv_bc2_sqrt);
+    st.b2 = adam_update_fast(st.b2, gb2, st.mb2, st.vb2, a.hp, step_size_neg, inv_bc2_sqrt);
+    loss_total += (double)sg.loss;
+    // rotate the prefetch pipeline
+#pragma unroll
+    for (int i = 0; i < C::NS; ++i) x[i] = xn[i];
+    y = yn;
+    idx_next = idx_next2;
+    idx_next2 = plan_at(a.plan, a.n_steps, a.bmax, s + 3, lr);
+    DGT_STAMP(5);
   }
+#ifdef DGT_TINY_STAMPS
+  if (a.stamps && l == 0 && w < 2)
+    for (int i = 0; i < 5; ++i) a.stamps[w * 8 + i] = st_acc[i];
+#endif
 
-  // ---- epilogue: state back to HBM (b2 belongs to wave 0)
+  // ---- epilogue: state back to HBM (b2 belongs to wave 0, lane 0)
 #pragma unroll
-  for (int i = 0; i < C::NPL; ++i) {
-    const int e = l + 64 * i;
-    if (e < C::WP && (e != C::L_B2 || w == 0)) {
-      const int gi = C::global_index(w, e);
-      a.params[gi] = ws.P[e];
-      a.exp_avg[gi] = m[i];
-      a.exp_avg_sq[gi] = v[i];
+  for (int i = 0; i < C::NS; ++i) {
+    const int gi = C::slot_index(w, lr, lq, i);
+    if (gi >= 0) {
+      a.params[gi] = st.w1[i];
+      a.exp_avg[gi] = st.m1[i];
+      a.exp_avg_sq[gi] = st.v1[i];
     }
+  }
+  const int bi = C::bw_index(w, lr, lq);
+  if (bi >= 0) {
+    a.params[bi] = st.bw;
+    a.exp_avg[bi] = st.mbw;
+    a.exp_avg_sq[bi] = st.vbw;
+  }
+  if (t == 0) {
+    a.params[C::G_B2] = st.b2;
+    a.exp_avg[C::G_B2] = st.mb2;
+    a.exp_avg_sq[C::G_B2] = st.vb2;
   }
   __syncthreads();
   if (t == 0) {
@@ -358,25 +393,33 @@ template <int F, int H>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_grad_kernel(TinyGradArgs a) {
   using C = TinyCfg<F, H>;
   __shared__ TinySmem<F, H> sm;
-  const int t = threadIdx.x, w = t >> 6, l = t & 63;
+  const int t = threadIdx.x, w = t >> 6, l = t & 63, lr = l & 15, lq = l >> 4;
   WaveSmem<F, H>& ws = sm.w[w];
-  wave_init<F, H>(ws, a.params, w, l);
-  if (l < C::BM) ws.idx[l] = (l < a.bmax) ? a.plan[(long long)a.step * a.bmax + l] : -1;
-  __builtin_amdgcn_wave_barrier();
-  float xv[C::XPL], yv;
-  gather_rows<F, H>(ws, a.X, a.Y, l, xv, yv);
-  stage_rows<F, H>(ws, l, xv, yv);
-  __builtin_amdgcn_wave_barrier();
+  LaneState<F, H> st;
+  load_state<F, H>(st, a.params, nullptr, nullptr, w, lr, lq);
+  for (int i = l; i < C::BM * C::SX; i += 64) ws.X[i] = 0.f;
+  for (int i = l; i < C::BM * 17; i += 64) ws.DH[i] = 0.f;
+  float x[C::NS], y;
+  const int id = (lr < a.bmax) ? a.plan[(long long)a.step * a.bmax + lr] : -1;
+  load_rows<F, H>(a.X, a.Y, id, lq, x, y);
   const int Bt = a.counts[a.step];
-  const float invB = 1.0f / (float)Bt;
-  float h[4];
-  wave_forward<F, H>(ws, sm.Z[0], w, l, h);
+  const float invB = __builtin_amdgcn_rcpf((float)Bt);
+  float h[4], w2v[4], gw1[C::NS];
+  __builtin_amdgcn_wave_barrier();
+  wave_forward<F, H>(st, ws, sm.Z[0], w, lr, lq, x, h, w2v);
   __syncthreads();
-  const float loss = wave_backward<F, H, true>(ws, sm.Z[0], l, h, Bt, invB);
-  for (int e = l; e < C::WP; e += 64) {
-    if (e != C::L_B2 || w == 0) a.grad[C::global_index(w, e)] = ws.G[e];
+  const StepGrads sg = wave_backward<F, H, true>(st, ws, sm.Z[0], lr, lq, h, w2v, y, Bt, invB, gw1);
+#pragma unroll
+  for (int i = 0; i < C::NS; ++i) {
+    const int gi = C::slot_index(w, lr, lq, i);
+    if (gi >= 0) a.grad[gi] = gw1[i];
   }
-  if (t == 0) *a.loss_acc += (double)loss;
+  const int bi = C::bw_index(w, lr, lq);
+  if (bi >= 0) a.grad[bi] = sg.bw;
+  if (t == 0) {
+    a.grad[C::G_B2] = sg.b2;
+    *a.loss_acc += (double)sg.loss;
+  }
 }
 
 // ------------------------------------------------------------------ dispatch
