@@ -22,6 +22,10 @@ _RANK_INFO: Optional[RankInfo] = None
 
 
 def default_backend() -> str:
+    """``DGT_BACKEND`` overrides; else nccl (= RCCL) with a GPU, gloo without."""
+    env = os.environ.get("DGT_BACKEND")
+    if env:
+        return env
     return "nccl" if torch.cuda.is_available() else "gloo"
 
 
@@ -87,17 +91,37 @@ def all_gather_object(obj: Any) -> List[Any]:
     return out
 
 
+def needs_host_staging(t: torch.Tensor) -> bool:
+    """gloo cannot reduce HIP tensors: stage them through host memory (tests / 1-GPU rehearsals)."""
+    return t.is_cuda and backend_name() == "gloo"
+
+
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
     if is_initialized() and get_world_size() > 1:
-        dist.broadcast(t, src)
+        if needs_host_staging(t):
+            c = t.detach().cpu()
+            dist.broadcast(c, src)
+            t.copy_(c)
+        else:
+            dist.broadcast(t, src)
+    return t
+
+
+def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
+    if is_initialized() and get_world_size() > 1:
+        if needs_host_staging(t):
+            c = t.detach().cpu()
+            dist.all_reduce(c, op=op)
+            t.copy_(c)
+        else:
+            dist.all_reduce(t, op=op)
     return t
 
 
 def all_reduce_max(value: float, device: Optional[torch.device] = None) -> float:
     if not is_initialized() or get_world_size() == 1:
         return float(value)
-    dev = device if device is not None else (torch.device("cuda", torch.cuda.current_device())
-                                             if backend_name() == "nccl" else torch.device("cpu"))
+    dev = torch.device("cuda", torch.cuda.current_device()) if backend_name() == "nccl" else torch.device("cpu")
     t = torch.tensor([float(value)], dtype=torch.float64, device=dev)
     dist.all_reduce(t, op=dist.ReduceOp.MAX)
     return float(t.item())

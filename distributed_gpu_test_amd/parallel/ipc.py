@@ -21,7 +21,6 @@ import os
 from typing import List, Optional
 
 import torch
-import torch.distributed as dist
 
 from ..ops._ext import require
 from . import comm
@@ -75,10 +74,7 @@ class IpcChannel:
             except Exception as e:
                 self.error = e
         # every rank agrees on usability before anybody launches a kernel that waits on peers
-        bad = torch.tensor([0.0 if self.error is None else 1.0], device=self.device)
-        if self.world_size > 1:
-            dist.all_reduce(bad, op=dist.ReduceOp.MAX)
-        self.healthy = bad.item() == 0.0
+        self.healthy = comm.all_reduce_max(0.0 if self.error is None else 1.0) == 0.0
         self.data_ptrs = list(self.base_ptrs) if self.healthy else []
         self.flag_ptrs = [p + self.data_bytes for p in self.base_ptrs] if self.healthy else []
 
@@ -107,8 +103,7 @@ class IpcChannel:
         n = min(n, self.stride) // 4 * 4
         g = torch.Generator(device="cpu").manual_seed(1234 + self.rank)
         x = torch.randn(n, generator=g).to(self.device)
-        ref = x.clone()
-        dist.all_reduce(ref)  # unconditional: every rank issues the same collectives
+        ref = comm.all_reduce_(x.clone())  # unconditional: every rank issues the same collectives
         try:
             got = torch.empty_like(x)
             for _ in range(3):  # both parities + a wrap of the first
@@ -122,9 +117,7 @@ class IpcChannel:
             ok = False
         finally:
             self.timeout_ticks = saved
-        flag = torch.tensor([0.0 if ok else 1.0], device=self.device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-        self.healthy = flag.item() == 0.0
+        self.healthy = comm.all_reduce_max(0.0 if ok else 1.0) == 0.0
         self.status.zero_()
         return self.healthy
 

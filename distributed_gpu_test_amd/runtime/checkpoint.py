@@ -90,7 +90,7 @@ def save(save_dir: str, tag: Optional[str], global_steps: int, model_state: Dict
         if save_latest:
             with open(os.path.join(save_dir, "latest"), "w") as fh:
                 fh.write(tag)
-        script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools_zero_to_fp32.py")
+        script = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "utils", "zero_to_fp32.py")
         if os.path.exists(script):
             shutil.copyfile(script, os.path.join(save_dir, "zero_to_fp32.py"))
     comm.barrier()

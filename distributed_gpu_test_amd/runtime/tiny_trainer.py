@@ -21,7 +21,6 @@ from __future__ import annotations
 from typing import Any, Dict, List, Optional
 
 import torch
-import torch.distributed as dist
 
 from .. import data as dgt_data
 from ..models.simple_net import SimpleNet, pack_simple_net, simple_net_layout, simple_net_numel
@@ -30,6 +29,7 @@ from ..ops.adam import adam_flat_
 from ..ops.reference import adam_flat_reference_, tiny_mlp_step_reference
 from ..parallel import comm
 from . import checkpoint as ckpt
+from ..utils.fault import FaultInjector
 from .optim_state import adam_state_to_flat, flat_to_adam_state
 
 IMPLS = ("auto", "fused", "stepwise", "torch")
@@ -81,7 +81,7 @@ class TinyMLPTrainer:
         flat[: self.numel] = pack_simple_net(model)
         self.params = flat.to(self.device)
         if self.world_size > 1:  # DeepSpeed broadcasts the model from rank 0 at initialize
-            dist.broadcast(self.params, 0)
+            comm.broadcast_(self.params, 0)
         self.exp_avg = torch.zeros_like(self.params)
         self.exp_avg_sq = torch.zeros_like(self.params)
         self.grad = torch.zeros_like(self.params)
@@ -91,6 +91,7 @@ class TinyMLPTrainer:
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         self.exchange_timeout_s = exchange_timeout_s
+        self.faults = FaultInjector.from_env(self.rank)
 
         if self.impl == "fused" and self.world_size > 1:
             self.channel = self._open_channel() if use_ipc else None
@@ -151,7 +152,7 @@ class TinyMLPTrainer:
                 ops.tiny_mlp_grad(self.x, self.y, plan, counts, s, self.params, self.grad, self.loss_acc,
                                   self.F, self.H)
                 if self.world_size > 1:
-                    dist.all_reduce(self.grad)
+                    comm.all_reduce_(self.grad)
                 self.global_steps += 1
                 adam_flat_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, self.global_steps, self.lr,
                            self.betas[0], self.betas[1], self.eps, self.weight_decay, self.adamw,
@@ -164,12 +165,13 @@ class TinyMLPTrainer:
                                                   grad_out=self.grad)
                 self.loss_acc += loss
                 if self.world_size > 1:
-                    dist.all_reduce(self.grad)
+                    comm.all_reduce_(self.grad)
                 self.global_steps += 1
                 adam_flat_reference_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, self.global_steps,
                                      self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay,
                                      self.adamw, grad_scale=1.0 / self.world_size)
         self.global_samples += n * self.B * self.world_size
+        self.faults.maybe_fire(self.global_steps)
 
     def check(self) -> None:
         """Raise if a kernel reported a failure (cross-GPU timeout, bad shape)."""

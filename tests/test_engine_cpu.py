@@ -1,0 +1,173 @@
+"""T1: the engine (DeepSpeed replacement) vs plain PyTorch fp32 references, single process (gloo)."""
+import copy
+import os
+
+import pytest
+import torch
+
+os.environ.setdefault("DGT_QUIET", "1")
+
+import distributed_gpu_test_amd as dgt  # noqa: E402
+from distributed_gpu_test_amd.data import make_synthetic_data  # noqa: E402
+from distributed_gpu_test_amd.models import SimpleNet  # noqa: E402
+from distributed_gpu_test_amd.runtime.flat import FlatLayout  # noqa: E402
+from distributed_gpu_test_amd.runtime.schedules import LossScaler, WarmupDecayLR, WarmupLR  # noqa: E402
+
+
+def _mlp(seed=0):
+    torch.manual_seed(seed)
+    return torch.nn.Sequential(torch.nn.Linear(12, 32), torch.nn.ReLU(), torch.nn.Linear(32, 16), torch.nn.Tanh(),
+                               torch.nn.Linear(16, 1))
+
+
+def _batches(n, seed=1, bs=8):
+    g = torch.Generator().manual_seed(seed)
+    return [(torch.randn(bs, 12, generator=g), (torch.rand(bs, 1, generator=g) > 0.5).float()) for _ in range(n)]
+
+
+def _reference_run(model, batches, lr=1e-3, gas=1, clip=0.0, wd=0.0, adamw=False, betas=(0.9, 0.999)):
+    opt = (torch.optim.AdamW if adamw else torch.optim.Adam)(model.parameters(), lr=lr, weight_decay=wd, betas=betas)
+    crit = torch.nn.BCEWithLogitsLoss()
+    for i, (x, y) in enumerate(batches):
+        loss = crit(model(x), y) / gas
+        loss.backward()
+        if (i + 1) % gas == 0:
+            if clip > 0:
+                torch.nn.utils.clip_grad_norm_(model.parameters(), clip)
+            opt.step()
+            opt.zero_grad()
+    return torch.nn.utils.parameters_to_vector(model.parameters()).detach()
+
+
+def _engine_run(model, batches, config, optimizer=None):
+    engine, _, _, _ = dgt.initialize(model=model, optimizer=optimizer, config=config)
+    crit = torch.nn.BCEWithLogitsLoss()
+    for x, y in batches:
+        loss = crit(engine(x).float(), y)
+        engine.backward(loss)
+        engine.step()
+    out = torch.nn.utils.parameters_to_vector(engine.module.parameters()).detach().float()
+    return engine, out
+
+
+@pytest.mark.parametrize("bucket", [64, 10_000_000])
+def test_stage0_matches_torch_adam(bucket):
+    m = _mlp()
+    ref = _reference_run(copy.deepcopy(m), _batches(12))
+    cfg = {"train_batch_size": 8, "zero_optimization": {"stage": 0, "reduce_bucket_size": bucket}}
+    engine, got = _engine_run(m, _batches(12), cfg, torch.optim.Adam(m.parameters(), lr=1e-3))
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    assert engine.global_steps == 12
+    engine.close()
+
+
+def test_gradient_accumulation_and_clipping_and_adamw():
+    m = _mlp(3)
+    ref = _reference_run(copy.deepcopy(m), _batches(12, 5), lr=5e-3, gas=3, clip=0.05, wd=0.1, adamw=True)
+    cfg = {"train_micro_batch_size_per_gpu": 8, "gradient_accumulation_steps": 3, "gradient_clipping": 0.05,
+           "optimizer": {"type": "AdamW", "params": {"lr": 5e-3, "weight_decay": 0.1}}}
+    engine, got = _engine_run(m, _batches(12, 5), cfg)
+    torch.testing.assert_close(got, ref, rtol=1e-5, atol=1e-6)
+    assert engine.global_steps == 4
+    engine.close()
+
+
+def test_stage1_single_rank_matches_stage0():
+    m = _mlp(4)
+    cfg0 = {"train_batch_size": 8, "zero_optimization": {"stage": 0}}
+    cfg1 = {"train_batch_size": 8, "zero_optimization": {"stage": 1, "reduce_bucket_size": 100}}
+    e0, p0 = _engine_run(copy.deepcopy(m), _batches(6), cfg0)
+    e1, p1 = _engine_run(copy.deepcopy(m), _batches(6), cfg1)
+    torch.testing.assert_close(p0, p1, rtol=1e-6, atol=1e-7)
+    e0.close()
+    e1.close()
+
+
+def test_bf16_engine_runs_with_fp32_master():
+    m = _mlp(5)
+    cfg = {"train_batch_size": 8, "bf16": {"enabled": True}}
+    engine, got = _engine_run(m, _batches(4), cfg)
+    assert next(engine.module.parameters()).dtype == torch.bfloat16
+    assert engine.master.dtype == torch.float32
+    torch.testing.assert_close(engine.master.to(torch.bfloat16), engine.store.param_buf)
+    engine.close()
+
+
+def test_checkpoint_round_trip(tmp_path):
+    cfg = {"train_batch_size": 8, "scheduler": {"type": "WarmupLR", "params": {"warmup_num_steps": 5,
+                                                                               "warmup_max_lr": 0.01}}}
+    m = _mlp(6)
+    engine, _ = _engine_run(copy.deepcopy(m), _batches(4), cfg)
+    path = engine.save_checkpoint(str(tmp_path), client_state={"epoch": 3})
+    assert os.path.exists(os.path.join(tmp_path, "latest"))
+    assert open(os.path.join(tmp_path, "latest")).read() == "global_step4"
+    assert os.path.exists(os.path.join(path, "mp_rank_00_model_states.pt"))
+    crit = torch.nn.BCEWithLogitsLoss()
+    for x, y in _batches(3, 9):
+        engine.backward(crit(engine(x), y))
+        engine.step()
+    a = torch.nn.utils.parameters_to_vector(engine.module.parameters()).detach().clone()
+    engine.close()
+
+    e2, _, _, _ = dgt.initialize(model=_mlp(99), config=cfg)
+    _, client = e2.load_checkpoint(str(tmp_path))
+    assert client == {"epoch": 3} and e2.global_steps == 4
+    for x, y in _batches(3, 9):
+        e2.backward(crit(e2(x), y))
+        e2.step()
+    b = torch.nn.utils.parameters_to_vector(e2.module.parameters()).detach()
+    torch.testing.assert_close(a, b)
+    # the optimizer state is torch.optim.Adam's format
+    sd = torch.load(os.path.join(path, "mp_rank_00_model_states.pt"), weights_only=True)
+    opt = torch.optim.Adam(_mlp().parameters())
+    opt.load_state_dict(sd["optimizer"])
+    assert sd["global_steps"] == 4 and sd["dp_world_size"] == 1
+    e2.close()
+
+
+def test_flat_layout_buckets_and_shards():
+    shapes = [(64, 20), (64,), (1, 64), (1,)]
+    lay = FlatLayout(shapes, bucket_elems=100, world_size=4, shard=True)
+    assert all(o % 16 == 0 for o in lay.offsets)
+    assert all(b.numel % (16 * 4) == 0 for b in lay.buckets)
+    assert lay.buckets[-1].params == [3] or 3 in lay.buckets[-1].params  # last layer reduced first
+    covered = sorted(i for b in lay.buckets for i in b.params)
+    assert covered == [0, 1, 2, 3]
+    assert sum(n for _, n in lay.shard_ranges(2)) == lay.shard_numel()
+
+
+def test_schedules_and_loss_scaler():
+    s = WarmupLR(warmup_min_lr=0.0, warmup_max_lr=1.0, warmup_num_steps=10, warmup_type="linear")
+    vals = [s.step() for _ in range(12)]
+    assert vals[0] == 0.0 and abs(vals[5] - 0.5) < 1e-9 and vals[11] == 1.0
+    d = WarmupDecayLR(total_num_steps=20, warmup_min_lr=0.0, warmup_max_lr=1.0, warmup_num_steps=10,
+                      warmup_type="linear")
+    vals = [d.step() for _ in range(21)]
+    assert vals[10] == 1.0 and abs(vals[15] - 0.5) < 1e-9 and vals[20] == 0.0
+    ls = LossScaler(0.0, initial_scale_power=4, scale_window=2, hysteresis=1)
+    ls.update(True)
+    assert ls.scale == 8.0
+    ls.update(False)
+    ls.update(False)
+    assert ls.scale == 16.0
+
+
+def test_simplenet_engine_reproduces_reference_epoch_loss():
+    torch.manual_seed(42)
+    x, y = make_synthetic_data(2000, 20, 42)
+    model = SimpleNet(20, 64)
+    from distributed_gpu_test_amd.config import REFERENCE_DS_CONFIG
+    from distributed_gpu_test_amd.data import SyntheticDataset
+    engine, _, _, _ = dgt.initialize(model=model, optimizer=torch.optim.Adam(model.parameters(), lr=1e-3),
+                                     config=REFERENCE_DS_CONFIG)
+    data = SyntheticDataset(x, y, 4)
+    data.set_epoch(1)
+    crit = torch.nn.BCEWithLogitsLoss()
+    tot = 0.0
+    for bx, by in data:
+        loss = crit(engine(bx), by)
+        engine.backward(loss)
+        engine.step()
+        tot += loss.item()
+    assert round(tot / len(data), 4) == 0.4301  # SURVEY §6.2 oracle, ws=1 epoch 1
+    engine.close()

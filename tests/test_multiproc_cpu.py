@@ -1,0 +1,93 @@
+"""T2: end-to-end train.py under torchrun with the gloo backend (SURVEY §4 tier T2)."""
+import json
+import os
+import re
+import subprocess
+import sys
+
+import pytest
+
+from distributed_gpu_test_amd.launch import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+ORACLE = {  # SURVEY §6.2 / BASELINE.md: rank-0 "Avg loss" per epoch
+    1: [0.4301, 0.1461, 0.0865, 0.0637, 0.0516],
+    2: [0.5126, 0.2219, 0.1250, 0.0857, 0.0741],
+    4: [0.5857, 0.3375, 0.1943, 0.1321, 0.0969],
+}
+pytestmark = pytest.mark.slow
+
+
+def run(nproc, *args, env=None, timeout=300, script="train.py"):
+    e = dict(os.environ)
+    e.update({"DGT_QUIET": "1", "OMP_NUM_THREADS": "1", "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+    e.update(env or {})
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
+           "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, script), *args]
+    return subprocess.run(cmd, cwd=ROOT, env=e, capture_output=True, text=True, timeout=timeout)
+
+
+def epoch_losses(stdout):
+    return [float(m) for m in re.findall(r"Epoch\s+\d+ finished\. Avg loss: ([0-9.]+)", stdout)]
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_train_py_matches_oracle(ws, tmp_path):
+    r = run(ws, "--save-dir", str(tmp_path), "--deepspeed", "--distributed-backend", "nccl")
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert epoch_losses(r.stdout) == ORACLE[ws]
+    assert r.stdout.count("Training completed.") == 1  # printed by local_rank 0 only
+    steps = {2: 250, 4: 125}[ws]
+    for e in range(1, 6):
+        d = tmp_path / f"epoch{e}"
+        assert (d / "latest").read_text() == f"global_step{steps * e}"
+        assert (d / f"global_step{steps * e}" / "mp_rank_00_model_states.pt").exists()
+
+
+def test_tiny_trainer_torch_impl_matches_oracle(tmp_path):
+    r = run(2, "--impl", "torch", "--epochs", "3", "--save-dir", str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert epoch_losses(r.stdout) == ORACLE[2][:3]
+
+
+def test_zero1_equals_zero0_and_writes_shards(tmp_path):
+    r = run(2, "--deepspeed_config", os.path.join(ROOT, "configs", "ds_zero1.json"), "--epochs", "2",
+            "--save-dir", str(tmp_path))
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert epoch_losses(r.stdout) == ORACLE[2][:2]
+    tag = tmp_path / "epoch2" / "global_step500"
+    assert (tag / "mp_rank_00_model_states.pt").exists()
+    assert (tag / "zero_pp_rank_0_mp_rank_00_optim_states.pt").exists()
+    assert (tag / "zero_pp_rank_1_mp_rank_00_optim_states.pt").exists()
+    # the consolidation script reproduces the module weights from the shards
+    out = tmp_path / "fp32.pt"
+    c = subprocess.run([sys.executable, str(tmp_path / "epoch2" / "zero_to_fp32.py"), str(tmp_path / "epoch2"),
+                        str(out)], capture_output=True, text=True, timeout=120)
+    assert c.returncode == 0, c.stderr
+    import torch
+    full = torch.load(out, weights_only=True)
+    mod = torch.load(tag / "mp_rank_00_model_states.pt", weights_only=True)["module"]
+    for k, v in mod.items():
+        torch.testing.assert_close(full[k], v.float())
+
+
+def test_resume_continues_identically(tmp_path):
+    full = run(2, "--epochs", "3", "--save-dir", str(tmp_path / "a"))
+    assert full.returncode == 0, full.stderr[-2000:]
+    part = run(2, "--epochs", "2", "--save-dir", str(tmp_path / "b"))
+    assert part.returncode == 0
+    res = run(2, "--epochs", "3", "--resume", "--save-dir", str(tmp_path / "b"))
+    assert res.returncode == 0, res.stderr[-2000:]
+    assert epoch_losses(res.stdout) == epoch_losses(full.stdout)[2:]
+
+
+@pytest.mark.parametrize("spec", ["1:end", "0:3:exit", "*:2:abort"])
+def test_fault_injection_fails_the_job(spec, tmp_path):
+    r = run(2, "--epochs", "1", "--fail-at", spec, "--no-save", timeout=180)
+    assert r.returncode != 0
+
+
+def test_world_size_3_fails_batch_assertion():
+    r = run(3, "--epochs", "1", "--no-save")
+    assert r.returncode != 0
+    assert "train_batch_size" in r.stderr

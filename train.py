@@ -1,0 +1,157 @@
+#!/usr/bin/env python3
+"""train.py — the distributed acceptance-test training job, MI355X-native.
+
+Same CLI, stdout and checkpoint layout as the reference ``train.py`` (dashabalashova/
+distributed-gpu-test): a 2-layer MLP trained data-parallel on 2000 synthetic samples for
+``--epochs`` epochs, printing ``Epoch  e finished. Avg loss: x.xxxx`` per epoch and
+``Training completed.`` at the end, and saving ``<save-dir>/epoch{e}/global_step{N}/...``
+after every epoch (``train.py:42-129``).  Unknown flags (``--deepspeed``,
+``--distributed-backend nccl``, ``--local-rank=N``) are ignored, as in the reference.
+
+Differences by design:
+* world_size 1 works (the reference crashes in ``sampler.set_epoch``);
+* on a GPU the default ``--impl auto`` runs the fused HIP training kernel (one launch per epoch,
+  gradient exchange over xGMI inside the kernel); ``--impl engine`` runs the generic
+  DeepSpeed-style engine (PyTorch modules + bucketed RCCL all-reduce + fused Adam);
+* extra flags: ``--deepspeed_config``, ``--impl``, ``--backend``, ``--fail-at``, ``--resume``,
+  ``--no-save``, ``--dist-timeout``.
+"""
+from __future__ import annotations
+
+import argparse
+import glob
+import json
+import os
+import re
+import sys
+
+import torch
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+import distributed_gpu_test_amd as dgt  # noqa: E402
+from distributed_gpu_test_amd.config import REFERENCE_DS_CONFIG, parse_config  # noqa: E402
+from distributed_gpu_test_amd.data import SyntheticDataset, make_synthetic_data  # noqa: E402
+from distributed_gpu_test_amd.models import SimpleNet  # noqa: E402
+from distributed_gpu_test_amd.parallel import comm  # noqa: E402
+from distributed_gpu_test_amd.utils.fault import FaultInjector  # noqa: E402
+
+N_SAMPLES, N_FEATURES, HIDDEN, MICRO_BATCH = 2000, 20, 64, 4
+
+
+def parse_args(argv=None):
+    p = argparse.ArgumentParser(allow_abbrev=False)  # "--deepspeed" must not match --deepspeed_config
+    p.add_argument("--train-batch-size", type=int, default=64)  # parsed, unused (reference Q2)
+    p.add_argument("--epochs", type=int, default=5)
+    p.add_argument("--lr", type=float, default=1e-3)
+    p.add_argument("--seed", type=int, default=42)
+    p.add_argument("--save-dir", type=str, default="ds_checkpoints")
+    # additions
+    p.add_argument("--deepspeed_config", "--deepspeed-config", dest="deepspeed_config", default=None)
+    p.add_argument("--impl", default="auto", choices=["auto", "fused", "stepwise", "engine", "torch"])
+    p.add_argument("--backend", default=None, choices=["nccl", "gloo"])
+    p.add_argument("--fail-at", default=None, help="RANK:STEP[:exit|abort|hang|nan] (STEP 'end' = after training)")
+    p.add_argument("--resume", action="store_true", help="continue from the newest checkpoint in --save-dir")
+    p.add_argument("--no-save", action="store_true")
+    p.add_argument("--dist-timeout", type=float, default=1800.0)
+    return p.parse_known_args(argv)[0]
+
+
+def newest_checkpoint(save_dir: str):
+    best = None
+    for d in glob.glob(os.path.join(save_dir, "epoch*")):
+        m = re.fullmatch(r"epoch(\d+)", os.path.basename(d))
+        if m and os.path.exists(os.path.join(d, "latest")):
+            e = int(m.group(1))
+            if best is None or e > best[0]:
+                best = (e, d)
+    return best
+
+
+def main(argv=None) -> int:
+    args = parse_args(argv)
+    torch.manual_seed(args.seed)
+    info = comm.init_distributed(backend=args.backend, timeout_s=args.dist_timeout)
+    local_rank, world = info.local_rank, comm.get_world_size()
+    faults = FaultInjector.from_env(comm.get_rank(), args.fail_at)
+    if args.fail_at:
+        os.environ["DGT_FAIL_AT"] = args.fail_at
+
+    ds_config = REFERENCE_DS_CONFIG if args.deepspeed_config is None else json.load(open(args.deepspeed_config))
+    cfg = parse_config(ds_config, world)  # DeepSpeed's batch assertion on every path
+
+    x, y = make_synthetic_data(n_samples=N_SAMPLES, n_features=N_FEATURES, seed=args.seed)
+    model = SimpleNet(n_features=x.shape[1], hidden=HIDDEN)
+    optimizer = torch.optim.Adam(model.parameters(), lr=args.lr)
+
+    gpu = torch.cuda.is_available()
+    impl = args.impl
+    if impl == "auto":
+        from distributed_gpu_test_amd.runtime.tiny_trainer import fused_supported
+        fused_ok = gpu and cfg.zero_stage == 0 and cfg.gradient_accumulation_steps == 1 and \
+            cfg.compute_dtype == "fp32" and fused_supported(N_FEATURES, HIDDEN, MICRO_BATCH)
+        impl = "fused" if fused_ok else "engine"
+
+    start_epoch = 1
+    if impl in ("fused", "stepwise", "torch"):
+        from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
+        trainer = TinyMLPTrainer(model, x, y, MICRO_BATCH, lr=args.lr, impl=impl, ds_config=cfg.to_dict(),
+                                 device=None if impl != "torch" else torch.device("cpu"))
+        if args.resume:
+            found = newest_checkpoint(args.save_dir)
+            if found:
+                trainer.load_checkpoint(found[1])
+                start_epoch = found[0] + 1
+        for epoch in range(start_epoch, args.epochs + 1):
+            avg_loss = trainer.run_epoch(epoch)
+            if local_rank == 0:
+                print(f"Epoch {epoch:2d} finished. Avg loss: {avg_loss:.4f}", flush=True)
+            if not args.no_save:
+                save_dir = os.path.join(args.save_dir, f"epoch{epoch}")
+                os.makedirs(save_dir, exist_ok=True)
+                trainer.save_checkpoint(save_dir)
+        trainer.close()
+    else:
+        engine, optimizer, _, _ = dgt.initialize(args=ds_config, model=model, optimizer=optimizer,
+                                                 model_parameters=model.parameters(), config=ds_config)
+        device = engine.device
+        data = SyntheticDataset(x, y, MICRO_BATCH, world, comm.get_rank()).to(device)
+        criterion = torch.nn.BCEWithLogitsLoss()
+        if args.resume:
+            found = newest_checkpoint(args.save_dir)
+            if found:
+                engine.load_checkpoint(found[1])
+                start_epoch = found[0] + 1
+        for epoch in range(start_epoch, args.epochs + 1):
+            engine.train()
+            data.set_epoch(epoch)
+            loss_acc = torch.zeros((), dtype=torch.float64, device=device)
+            steps = 0
+            for batch_x, batch_y in data:
+                logits = engine(batch_x)
+                loss = criterion(logits.float(), batch_y)
+                engine.backward(loss)
+                engine.step()
+                loss_acc += loss.detach().double()  # on device: no per-step host sync
+                steps += 1
+            avg_loss = float(loss_acc.item()) / max(1, steps)
+            if local_rank == 0:
+                print(f"Epoch {epoch:2d} finished. Avg loss: {avg_loss:.4f}", flush=True)
+            if not args.no_save:
+                save_dir = os.path.join(args.save_dir, f"epoch{epoch}")
+                os.makedirs(save_dir, exist_ok=True)
+                engine.save_checkpoint(save_dir)
+        engine.close()
+
+    if local_rank == 0:
+        print("Training completed.", flush=True)
+    faults.maybe_fire_end()  # the reference's commented-out sys.exit(1) (train.py:129), as a flag
+    return 0
+
+
+if __name__ == "__main__":
+    rc = main()
+    comm.destroy()
+    sys.exit(rc)
