@@ -110,7 +110,7 @@ class Engine:
                                  shard=self.stage >= 1)
         self.store = FlatParamStore(self.params, self.layout, device, self.dtype)
         if self.world_size > 1:
-            dist.broadcast(self.store.param_buf, 0)  # DeepSpeed _broadcast_model
+            comm.broadcast_(self.store.param_buf, 0)  # DeepSpeed _broadcast_model
 
         # ---- fp32 master + moments (full for stage 0, this rank's shard for stage >= 1)
         if self.stage == 0:
@@ -234,7 +234,7 @@ class Engine:
             return None
         sq = grads.float().pow(2).sum() * (scale * scale)
         if self.stage >= 1 and self.world_size > 1:
-            dist.all_reduce(sq)
+            comm.all_reduce_(sq)
         norm = sq.sqrt()
         self._grad_norm = norm
         return torch.clamp(clip / (norm + 1e-6), max=1.0).reshape(1).float()
@@ -280,7 +280,11 @@ class Engine:
             n = b.numel // self.world_size
             out = self.store.param_buf[b.start:b.start + b.numel]
             piece = src[off:off + n]
-            if self.world_size > 1:
+            if self.world_size > 1 and comm.needs_host_staging(out):
+                host = torch.empty(b.numel, dtype=piece.dtype)
+                dist.all_gather_into_tensor(host, piece.detach().cpu())
+                out.copy_(host)
+            elif self.world_size > 1:
                 works.append(dist.all_gather_into_tensor(out, piece, async_op=True))
             else:
                 out.copy_(piece)

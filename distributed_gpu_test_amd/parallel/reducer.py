@@ -22,6 +22,7 @@ import torch
 import torch.distributed as dist
 
 from ..runtime.flat import FlatLayout
+from . import comm
 
 
 class GradReducer:
@@ -98,6 +99,16 @@ class GradReducer:
             return
         if self.debug_sync and view.is_cuda:
             torch.cuda.synchronize()
+        if comm.needs_host_staging(view):  # gloo rehearsal of a GPU run: synchronous, via host memory
+            if self.stage == 0:
+                comm.all_reduce_(view)
+            else:
+                n = b.numel // self.world_size
+                host = view.detach().cpu()
+                out = torch.empty(n, dtype=host.dtype)
+                dist.reduce_scatter_tensor(out, host)
+                self.shard_grad[self.shard_offsets[bi]:self.shard_offsets[bi] + n].copy_(out)
+            return
         if self.stage == 0:
             nbytes = view.numel() * view.element_size()
             if (self.oneshot is not None and view.dtype == torch.float32 and nbytes <= self.oneshot_max_bytes

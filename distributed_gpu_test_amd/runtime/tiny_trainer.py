@@ -18,6 +18,7 @@ printed value as the reference's per-step ``loss.item()`` sum.
 """
 from __future__ import annotations
 
+import os
 from typing import Any, Dict, List, Optional
 
 import torch
@@ -46,7 +47,7 @@ class TinyMLPTrainer:
                  lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  adamw: bool = False, device: Optional[torch.device] = None, impl: str = "auto",
                  sampler_seed: int = 0, ds_config: Optional[Dict[str, Any]] = None, use_ipc: bool = True,
-                 exchange_timeout_s: float = 60.0):
+                 exchange_timeout_s: Optional[float] = None):
         if impl not in IMPLS:
             raise ValueError(f"impl must be one of {IMPLS}")
         self.F = model.n_features
@@ -90,7 +91,8 @@ class TinyMLPTrainer:
         self.y = y.to(self.device, torch.float32).reshape(-1).contiguous()
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.device)
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
-        self.exchange_timeout_s = exchange_timeout_s
+        self.exchange_timeout_s = float(exchange_timeout_s if exchange_timeout_s is not None
+                                        else os.environ.get("DGT_EXCHANGE_TIMEOUT_S", 60.0))
         self.faults = FaultInjector.from_env(self.rank)
 
         if self.impl == "fused" and self.world_size > 1:

@@ -99,6 +99,9 @@ def main(argv=None) -> int:
         from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
         trainer = TinyMLPTrainer(model, x, y, MICRO_BATCH, lr=args.lr, impl=impl, ds_config=cfg.to_dict(),
                                  device=None if impl != "torch" else torch.device("cpu"))
+        if comm.get_rank() == 0:
+            print(f"[dgt] impl={trainer.impl} exchange={trainer.exchange} world_size={world}", file=sys.stderr,
+                  flush=True)
         if args.resume:
             found = newest_checkpoint(args.save_dir)
             if found:
@@ -117,6 +120,10 @@ def main(argv=None) -> int:
         engine, optimizer, _, _ = dgt.initialize(args=ds_config, model=model, optimizer=optimizer,
                                                  model_parameters=model.parameters(), config=ds_config)
         device = engine.device
+        if comm.get_rank() == 0:
+            print(f"[dgt] impl=engine zero_stage={cfg.zero_stage} dtype={cfg.compute_dtype} "
+                  f"oneshot={'yes' if engine.oneshot is not None else 'no'} backend={comm.backend_name()} "
+                  f"world_size={world}", file=sys.stderr, flush=True)
         data = SyntheticDataset(x, y, MICRO_BATCH, world, comm.get_rank()).to(device)
         criterion = torch.nn.BCEWithLogitsLoss()
         if args.resume:
