@@ -41,6 +41,12 @@ def parse_args(argv=None):
     ap.add_argument("--impl", default="fused", choices=["fused", "stepwise", "engine"],
                     help="fused: one-launch HIP training kernel; stepwise: per-step HIP kernels + RCCL; "
                          "engine: PyTorch eager + RCCL (the reference-equivalent stack)")
+    ap.add_argument("--model", default="simple", choices=["simple", "mlp"],
+                    help="simple: the reference SimpleNet (headline); mlp: bench-size bf16 synthetic MLP on the "
+                         "HIP MFMA GEMMs (BASELINE config #2)")
+    ap.add_argument("--width", type=int, default=4096)
+    ap.add_argument("--depth", type=int, default=4)
+    ap.add_argument("--batch", type=int, default=1024, help="mlp: per-GPU micro-batch")
     ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce bus bandwidth sweep")
     ap.add_argument("--sweep-max-mb", type=int, default=256)
     return ap.parse_known_args(argv)[0]
@@ -101,7 +107,13 @@ def main(argv=None):
     x, y = make_synthetic_data(2000, 20, 42)
     model = SimpleNet(20, 64)
     B = 4
-    if args.impl == "engine":
+    if args.model == "mlp":
+        from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+        from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
+        model = SyntheticMLP(args.width, args.depth)
+        B = args.batch
+        trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device)
+    elif args.impl == "engine":
         trainer = EngineBench(model, x, y, B, device)
     else:
         trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=args.impl if device.type == "cuda" else "torch",
@@ -146,6 +158,15 @@ def main(argv=None):
 
     ms = elapsed_max / args.steps * 1e3
     global_steps_per_s = args.steps / elapsed_max
+    if args.model == "mlp":
+        tflops = trainer.flops_per_step() * world * global_steps_per_s / 1e12
+        model_desc = (f"SyntheticMLP {args.depth}x[Linear({args.width},{args.width})+ReLU] + Linear({args.width},1) "
+                      f"+ BCEWithLogits + Adam, bf16 MFMA")
+        dtype = "bf16"
+    else:
+        tflops = None
+        model_desc = "SimpleNet Linear(20,64)-ReLU-Linear(64,1) + BCEWithLogits + Adam(1e-3)"
+        dtype = "fp32"
     out = {
         "metric": METRIC,
         "value": round(world * global_steps_per_s, 2),
@@ -157,14 +178,16 @@ def main(argv=None):
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "fp32",
-        "data": "synthetic (2000x20 N(0,1), seed 42; random-init SimpleNet)",
-        "config": {"model": "SimpleNet Linear(20,64)-ReLU-Linear(64,1) + BCEWithLogits + Adam(1e-3)",
+        "dtype": dtype,
+        "data": ("synthetic (2000x20 N(0,1), seed 42; random-init SimpleNet)" if args.model == "simple" else
+                 "synthetic N(0,1) batches, random-init weights"),
+        "config": {"model": model_desc,
                    "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
                    "micro_batch_per_gpu": B, "impl": trainer.impl, "exchange": trainer.exchange},
         "global_steps_per_sec": round(global_steps_per_s, 2),
         "samples_per_sec": round(global_steps_per_s * B * world, 2),
         "mean_loss": round(mean_loss, 6),
+        "model_tflops": None if tflops is None else round(tflops, 2),
         "params_consistent_across_ranks": consistent,
         "allreduce_busbw_GBps": None if peak_busbw is None else round(peak_busbw, 2),
         "allreduce_5KB_us": None if small is None else round(small["us"], 2),

@@ -215,6 +215,116 @@ void oneshot_allreduce(const at::Tensor& inp, const at::Tensor& out, double scal
                                        status.data_ptr<int>(), stream_of(inp)));
 }
 
+// ------------------------------------------------------------------------------ bf16 GEMM + MLP helpers
+void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t r, int64_t c) {
+  check_gpu(t, name, dt);
+  TORCH_CHECK(t.dim() == 2 && t.size(0) == r && t.size(1) == c, "dgt: ", name, " must be [", r, ", ", c, "], got ",
+              t.sizes());
+}
+
+void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
+             const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
+             const std::optional<at::Tensor>& mask, int64_t epi, double alpha) {
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt needs A[M,K], B[N,K]");
+  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+  for (const at::Tensor* t : {&A, &B}) {  // rows may be strided (column blocks of a wider matrix)
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16, "dgt: gemm_nt operands must be bf16 GPU tensors");
+    TORCH_CHECK(t->stride(1) == 1 && t->stride(0) >= t->size(1) && t->stride(0) % 8 == 0,
+                "dgt: gemm_nt operand rows must be unit-stride with a 16-byte aligned row stride");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "dgt: gemm_nt operand must be 16-byte aligned");
+  }
+  TORCH_CHECK(M % 128 == 0 && N % 128 == 0 && K % 64 == 0, "dgt: gemm_nt needs M, N % 128 == 0 and K % 64 == 0 (got ",
+              M, "x", N, "x", K, ")");
+  dgt::GemmArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.A = A.data_ptr();
+  g.B = B.data_ptr();
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.lda = (int)A.stride(0);
+  g.ldb = (int)B.stride(0);
+  g.alpha = (float)alpha;
+  if (C.has_value() && C->defined()) {
+    check_2d(*C, "C", (epi & dgt::kEpiOutF32) ? at::kFloat : at::kBFloat16, M, N);
+    g.C = C->data_ptr();
+    g.ldc = (int)N;
+  } else {
+    TORCH_CHECK(!(epi & dgt::kEpiOutF32) && (epi & dgt::kEpiStoreT), "dgt: gemm_nt without C must store C^T");
+  }
+  if (epi & dgt::kEpiStoreT) {
+    TORCH_CHECK(CT.has_value() && CT->defined(), "dgt: kEpiStoreT needs CT");
+    check_2d(*CT, "CT", at::kBFloat16, N, M);
+    g.CT = CT->data_ptr();
+    g.ldct = (int)M;
+  }
+  if (epi & dgt::kEpiBias) {
+    TORCH_CHECK(bias.has_value() && bias->defined() && bias->numel() == N, "dgt: bias must have N elements");
+    check_gpu(*bias, "bias", at::kFloat);
+    g.bias = bias->data_ptr<float>();
+  }
+  if (epi & dgt::kEpiMask) {
+    TORCH_CHECK(mask.has_value() && mask->defined(), "dgt: kEpiMask needs mask");
+    check_2d(*mask, "mask", at::kBFloat16, M, N);
+    g.mask = mask->data_ptr();
+    g.ldmask = (int)N;
+  }
+  c10::DeviceGuard guard(A.device());
+  DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A)));
+}
+
+void transpose_bf16(const at::Tensor& in, const at::Tensor& out) {
+  TORCH_CHECK(in.dim() == 2, "dgt: transpose needs a 2-d tensor");
+  check_2d(in, "in", at::kBFloat16, in.size(0), in.size(1));
+  check_2d(out, "out", at::kBFloat16, in.size(1), in.size(0));
+  c10::DeviceGuard guard(in.device());
+  DGT_CHECK_HIP(dgt::transpose_bf16(in.data_ptr(), out.data_ptr(), (int)in.size(0), (int)in.size(1), stream_of(in)));
+}
+
+void rowsum_bf16(const at::Tensor& in, const at::Tensor& out, bool accumulate) {
+  TORCH_CHECK(in.dim() == 2 && in.size(1) % 8 == 0, "dgt: rowsum needs [rows, cols % 8 == 0]");
+  check_2d(in, "in", at::kBFloat16, in.size(0), in.size(1));
+  check_gpu(out, "out", at::kFloat);
+  TORCH_CHECK(out.numel() == in.size(0), "dgt: rowsum out must have one entry per row");
+  c10::DeviceGuard guard(in.device());
+  DGT_CHECK_HIP(dgt::rowsum_bf16(in.data_ptr(), out.data_ptr<float>(), (int)in.size(0), (int)in.size(1),
+                                 accumulate ? 1 : 0, stream_of(in)));
+}
+
+void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& y,
+              const at::Tensor& dz, const at::Tensor& dw, const at::Tensor& db, const at::Tensor& loss_acc,
+              const at::Tensor& g, const at::Tensor& gT) {
+  TORCH_CHECK(a.dim() == 2, "dgt: head activation must be 2-d");
+  const int64_t B = a.size(0), D = a.size(1);
+  TORCH_CHECK(B % 64 == 0 && D % 64 == 0, "dgt: head needs B, D % 64 == 0");
+  check_2d(a, "a", at::kBFloat16, B, D);
+  check_gpu(w, "w", at::kFloat);
+  check_gpu(b0, "b0", at::kFloat);
+  check_gpu(y, "y", at::kFloat);
+  check_gpu(dz, "dz", at::kFloat);
+  check_gpu(dw, "dw", at::kFloat);
+  check_gpu(db, "db", at::kFloat);
+  check_gpu(loss_acc, "loss_acc", at::kDouble);
+  TORCH_CHECK(w.numel() == D && dw.numel() == D && y.numel() == B && dz.numel() == B, "dgt: head size mismatch");
+  check_2d(g, "g", at::kBFloat16, B, D);
+  check_2d(gT, "gT", at::kBFloat16, D, B);
+  dgt::HeadArgs h;
+  h.a = a.data_ptr();
+  h.w = w.data_ptr<float>();
+  h.b0 = b0.data_ptr<float>();
+  h.y = y.data_ptr<float>();
+  h.B = (int)B;
+  h.D = (int)D;
+  h.dz = dz.data_ptr<float>();
+  h.dw = dw.data_ptr<float>();
+  h.db = db.data_ptr<float>();
+  h.loss_acc = loss_acc.data_ptr<double>();
+  h.g = g.data_ptr();
+  h.gT = gT.data_ptr();
+  c10::DeviceGuard guard(a.device());
+  DGT_CHECK_HIP(dgt::mlp_head(h, stream_of(a)));
+}
+
 // ------------------------------------------------------------------------------ IPC runtime
 int64_t ipc_alloc(int64_t nbytes, bool uncached, int64_t device) {
   TORCH_CHECK(nbytes > 0, "dgt: ipc_alloc needs a positive size");
@@ -286,6 +396,16 @@ TORCH_LIBRARY(dgt, m) {
       "oneshot_allreduce(Tensor inp, Tensor(a!) out, float scale, int[] data_ptrs, int[] flag_ptrs, int rank, "
       "int world_size, int stride, int seq, int timeout_ticks, Tensor(b!) status) -> ()",
       &oneshot_allreduce);
+  m.def(
+      "gemm_nt(Tensor A, Tensor B, Tensor(a!)? C, Tensor(b!)? CT, Tensor? bias, Tensor? mask, int epi, "
+      "float alpha) -> ()",
+      &gemm_nt);
+  m.def("transpose_bf16(Tensor inp, Tensor(a!) out) -> ()", &transpose_bf16);
+  m.def("rowsum_bf16(Tensor inp, Tensor(a!) out, bool accumulate) -> ()", &rowsum_bf16);
+  m.def(
+      "mlp_head(Tensor a, Tensor w, Tensor b0, Tensor y, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!) db, "
+      "Tensor(d!) loss_acc, Tensor(e!) g, Tensor(f!) gT) -> ()",
+      &mlp_head);
   m.def("ipc_alloc(int nbytes, bool uncached, int device) -> int", &ipc_alloc);
   m.def("ipc_handle(int ptr) -> Tensor", &ipc_handle);
   m.def("ipc_open(Tensor handle, int device) -> int", &ipc_open);

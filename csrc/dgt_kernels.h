@@ -75,4 +75,46 @@ hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream);
 hipError_t oneshot_allreduce(const float* in, float* out, long long n, float scale, const Exchange& ex,
                              int* status, hipStream_t stream);
 
+// ---------------------------------------------------------------- bf16 MFMA GEMM (gemm.hip)
+enum GemmEpilogue : int {
+  kEpiBias = 1,        // + bias[n] (fp32)
+  kEpiRelu = 2,        // max(., 0)
+  kEpiMask = 4,        // * 1[mask[m][n] > 0]   (mask: bf16 [M, N], row stride ldmask)
+  kEpiStoreT = 8,      // also write C^T (bf16, row stride ldct)
+  kEpiOutF32 = 16,     // C is fp32 (else bf16)
+  kEpiAccumulate = 32, // C += result (fp32 only)
+};
+
+struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 A/B, fp32 accumulate
+  const void* A;
+  const void* B;
+  void* C;             // bf16 or fp32 [M, ldc]; may be null when only C^T is wanted
+  void* CT;            // bf16 [N, ldct]
+  const float* bias;
+  const void* mask;
+  int M, N, K;
+  int lda, ldb, ldc, ldct, ldmask;
+  float alpha;
+};
+
+hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream);
+hipError_t transpose_bf16(const void* in, void* out, int rows, int cols, hipStream_t stream);
+hipError_t rowsum_bf16(const void* in, float* out, int rows, int cols, int accumulate, hipStream_t stream);
+
+struct HeadArgs {      // binary head of the synthetic MLP: Linear(D, 1) + BCE-with-logits (mean)
+  const void* a;       // bf16 [B, D] last hidden activation
+  const float* w;      // fp32 [D]
+  const float* b0;     // fp32 [1]
+  const float* y;      // fp32 [B]
+  int B, D;
+  float* dz;           // fp32 [B]
+  float* dw;           // fp32 [D]  (+=)
+  float* db;           // fp32 [1]  (+=)
+  double* loss_acc;    // += mean loss
+  void* g;             // bf16 [B, D] gradient wrt the last pre-activation
+  void* gT;            // bf16 [D, B]
+};
+
+hipError_t mlp_head(const HeadArgs& h, hipStream_t stream);
+
 }  // namespace dgt

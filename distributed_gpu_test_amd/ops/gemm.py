@@ -1,0 +1,80 @@
+"""bf16 MFMA GEMM + MLP helper ops (``csrc/gemm.hip``) with plain-PyTorch references.
+
+``gemm_nt`` computes ``C = alpha * A @ B.T`` (A[M,K], B[N,K], both bf16, fp32 accumulation) with
+optional fused epilogue: ``+ bias``, ``relu``, ``* 1[mask > 0]``, a transposed bf16 copy ``CT``,
+fp32 output / accumulation.  On GPU tensors it runs the HIP kernel (and raises if the extension
+is missing); on CPU tensors it runs the reference, which is also the numerics oracle in tests.
+"""
+from __future__ import annotations
+
+from typing import Optional
+
+import torch
+
+from ._ext import require
+
+EPI_BIAS, EPI_RELU, EPI_MASK, EPI_STORE_T, EPI_OUT_F32, EPI_ACCUMULATE = 1, 2, 4, 8, 16, 32
+
+
+def gemm_nt_reference(A, B, C=None, CT=None, bias=None, mask=None, relu=False, out_f32=False,
+                      accumulate=False, alpha=1.0):
+    r = (A.float() @ B.float().t()) * alpha
+    if bias is not None:
+        r = r + bias.float()
+    if relu:
+        r = torch.relu(r)
+    if mask is not None:
+        r = torch.where(mask.float() > 0, r, torch.zeros_like(r))
+    if C is not None:
+        if out_f32 and accumulate:
+            C.add_(r)
+        else:
+            C.copy_(r.to(C.dtype))
+    if CT is not None:
+        CT.copy_(r.t().to(CT.dtype))
+    return r
+
+
+def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, CT: Optional[torch.Tensor] = None,
+            bias: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, relu: bool = False,
+            out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0) -> None:
+    if not A.is_cuda:
+        gemm_nt_reference(A, B, C, CT, bias, mask, relu, out_f32, accumulate, alpha)
+        return
+    epi = ((EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | (EPI_MASK if mask is not None else 0)
+           | (EPI_STORE_T if CT is not None else 0) | (EPI_OUT_F32 if out_f32 else 0)
+           | (EPI_ACCUMULATE if accumulate else 0))
+    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha))
+
+
+def transpose_bf16(inp: torch.Tensor, out: torch.Tensor) -> None:
+    if inp.is_cuda:
+        require().transpose_bf16(inp, out)
+    else:
+        out.copy_(inp.t())
+
+
+def rowsum_bf16(inp: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> None:
+    if inp.is_cuda:
+        require().rowsum_bf16(inp, out, accumulate)
+    else:
+        s = inp.float().sum(1)
+        out.add_(s) if accumulate else out.copy_(s)
+
+
+def mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT) -> None:
+    """Linear(D,1) + BCE-with-logits (mean) forward and backward; dw/db/loss_acc accumulate."""
+    if a.is_cuda:
+        require().mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT)
+        return
+    af = a.float()
+    z = af @ w + b0
+    loss = torch.nn.functional.binary_cross_entropy_with_logits(z, y)
+    d = (torch.sigmoid(z) - y) / a.shape[0]
+    dz.copy_(d)
+    dw.add_(d @ af)
+    db.add_(d.sum())
+    loss_acc.add_(float(loss))
+    gg = torch.outer(d, w) * (af > 0)
+    g.copy_(gg.to(g.dtype))
+    gT.copy_(gg.t().to(gT.dtype))

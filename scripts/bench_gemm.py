@@ -1,0 +1,47 @@
+#!/usr/bin/env python3
+"""GEMM micro-benchmark: the HIP MFMA gemm_nt kernel vs torch.matmul (hipBLASLt) on the MLP's
+shapes, bf16 in / fp32 accumulate, random N(0,1) data (cdna_hip_programming.md rule 25).
+Prints one JSON line per shape."""
+import json
+import sys
+import os
+import time
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_gpu_test_amd.ops.gemm import gemm_nt  # noqa: E402
+
+
+def bench(fn, iters=50, warmup=10):
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(iters):
+        fn()
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / iters * 1e-3
+
+
+def main():
+    shapes = [(4096, 4096, 4096), (8192, 8192, 8192), (1024, 4096, 4096), (4096, 4096, 1024), (2048, 8192, 8192)]
+    for M, N, K in shapes:
+        A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+        B = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+        C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+        Cf = torch.empty(M, N, device="cuda", dtype=torch.float32)
+        flops = 2.0 * M * N * K
+        t_ours = bench(lambda: gemm_nt(A, B, C=C))
+        t_ours32 = bench(lambda: gemm_nt(A, B, C=Cf, out_f32=True))
+        t_torch = bench(lambda: torch.matmul(A, B.t(), out=C))
+        print(json.dumps({"M": M, "N": N, "K": K, "dgt_TFLOPs": round(flops / t_ours / 1e12, 1),
+                          "dgt_f32out_TFLOPs": round(flops / t_ours32 / 1e12, 1),
+                          "torch_hipblaslt_TFLOPs": round(flops / t_torch / 1e12, 1),
+                          "dgt_us": round(t_ours * 1e6, 1), "torch_us": round(t_torch * 1e6, 1)}), flush=True)
+
+
+if __name__ == "__main__":
+    main()

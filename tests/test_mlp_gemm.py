@@ -1,0 +1,127 @@
+"""bf16 MFMA GEMM + synthetic-MLP trainer vs plain PyTorch fp32 references.
+
+CPU runs check the trainer's math through the reference ops; GPU runs (marker ``gpu``) check the
+HIP kernels against the same references."""
+import copy
+
+import pytest
+import torch
+
+from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+from distributed_gpu_test_amd.ops.gemm import gemm_nt, gemm_nt_reference, mlp_head, rowsum_bf16, transpose_bf16
+from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
+
+
+def _trainer_vs_torch(device):
+    """One step of the trainer vs torch autograd on the same bf16-rounded weights and inputs:
+    returns (trainer gradient, reference gradient, trainer loss, reference loss)."""
+    torch.manual_seed(0)
+    model = SyntheticMLP(width=128, depth=2)
+    ref = copy.deepcopy(model)
+    tr = MLPTrainer(model, batch_size=128, n_batches=2, lr=1e-3, device=device)
+    x = tr.X[:128].float().cpu()
+    y = tr.Y[:128].float().cpu()
+    with torch.no_grad():
+        for name, p in ref.named_parameters():
+            if "layers" in name and "weight" in name:
+                p.copy_(p.to(torch.bfloat16).float())
+    ref_loss = torch.nn.functional.binary_cross_entropy_with_logits(ref(x).view(-1), y)
+    ref_loss.backward()
+    tr.step(0)
+    got = torch.cat([tr.grads[o:o + p.numel()].cpu() for (_, _, o), p in zip(tr.segments, ref.parameters())])
+    want = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
+    return got, want, float(tr.loss_acc.item()), float(ref_loss)
+
+
+def _check(device):
+    got, want, loss, ref_loss = _trainer_vs_torch(device)
+    assert abs(loss - ref_loss) < 1e-2 * max(1.0, abs(ref_loss))
+    scale = want.abs().max()
+    torch.testing.assert_close(got / scale, want / scale, rtol=0, atol=3e-2)  # bf16 activations
+    cos = torch.nn.functional.cosine_similarity(got, want, dim=0)
+    assert cos > 0.999, float(cos)
+
+
+def test_trainer_cpu_reference_path():
+    _check(torch.device("cpu"))
+
+
+gpu = pytest.mark.gpu
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 128), (512, 256, 1024)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "mask_T", "f32", "f32_acc"])
+def test_gemm_nt_matches_reference(M, N, K, epi):
+    g = torch.Generator().manual_seed(M + N + K)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
+    bias = torch.randn(N, generator=g).cuda()
+    mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).cuda()
+    kw = {}
+    if epi == "bias_relu_T":
+        kw = dict(bias=bias, relu=True)
+    elif epi == "mask_T":
+        kw = dict(mask=mask)
+    f32 = epi.startswith("f32")
+    C = (torch.randn(M, N, generator=g) if f32 else torch.zeros(M, N)).cuda().to(torch.float32 if f32 else torch.bfloat16)
+    C0 = C.clone()
+    CT = torch.zeros(N, M, dtype=torch.bfloat16).cuda() if epi.endswith("_T") else None
+    gemm_nt(A, B, C=C, CT=CT, out_f32=f32, accumulate=epi == "f32_acc", **kw)
+    ref = gemm_nt_reference(A.cpu(), B.cpu(), **{k: (v.cpu() if torch.is_tensor(v) else v)
+                                                  for k, v in kw.items()}).cuda()
+    if epi == "f32_acc":
+        ref = ref + C0
+    tol = dict(rtol=2e-2, atol=2e-2 * K ** 0.5) if not f32 else dict(rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(C.float(), ref if f32 else ref.to(torch.bfloat16).float(), **tol)
+    if CT is not None:
+        torch.testing.assert_close(CT.float(), ref.t().to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2 * K ** 0.5)
+
+
+@gpu
+def test_gemm_identity_with_asymmetric_operand():
+    # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
+    M = N = K = 128
+    A = torch.eye(M, dtype=torch.bfloat16).cuda()
+    B = torch.arange(N * K, dtype=torch.float32).remainder(251).reshape(N, K).to(torch.bfloat16).cuda()
+    C = torch.empty(M, N, dtype=torch.float32).cuda()
+    gemm_nt(A, B, C=C, out_f32=True)
+    torch.testing.assert_close(C, B.float().t())
+
+
+@gpu
+def test_gemm_strided_operand():
+    A = torch.randn(128, 64).to(torch.bfloat16).cuda()
+    wide = torch.randn(128, 256).to(torch.bfloat16).cuda()
+    Bv = wide[:, 64:128]  # row stride 256
+    C = torch.empty(128, 128, dtype=torch.float32).cuda()
+    gemm_nt(A, Bv, C=C, out_f32=True)
+    torch.testing.assert_close(C, A.float() @ Bv.float().t(), rtol=1e-4, atol=1e-3)
+
+
+@gpu
+def test_transpose_rowsum_head():
+    x = torch.randn(192, 320).to(torch.bfloat16).cuda()
+    xt = torch.empty(320, 192, dtype=torch.bfloat16).cuda()
+    transpose_bf16(x, xt)
+    assert torch.equal(xt, x.t().contiguous())
+    out = torch.empty(192).cuda()
+    rowsum_bf16(x, out)
+    torch.testing.assert_close(out, x.float().sum(1), rtol=1e-4, atol=1e-3)
+    B, D = 128, 256
+    a = torch.relu(torch.randn(B, D)).to(torch.bfloat16)
+    w, b0, y = torch.randn(D) * 0.1, torch.tensor([0.05]), (torch.rand(B) > 0.5).float()
+    bufs = lambda dev: [torch.zeros(B, device=dev), torch.zeros(D, device=dev), torch.zeros(1, device=dev),
+                        torch.zeros(1, dtype=torch.float64, device=dev),
+                        torch.zeros(B, D, dtype=torch.bfloat16, device=dev),
+                        torch.zeros(D, B, dtype=torch.bfloat16, device=dev)]
+    ref, got = bufs("cpu"), bufs("cuda")
+    mlp_head(a, w, b0, y, *ref)
+    mlp_head(a.cuda(), w.cuda(), b0.cuda(), y.cuda(), *got)
+    for r, g_ in zip(ref, got):
+        torch.testing.assert_close(g_.cpu().float(), r.float(), rtol=2e-2, atol=1e-4)
+
+
+@gpu
+def test_trainer_gpu_matches_torch():
+    _check(torch.device("cuda"))
