@@ -38,9 +38,10 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20000, help="timed optimizer steps")
     ap.add_argument("--warmup", type=int, default=2000, help="untimed warmup steps")
-    ap.add_argument("--impl", default="fused", choices=["fused", "stepwise", "engine"],
-                    help="fused: one-launch HIP training kernel; stepwise: per-step HIP kernels + RCCL; "
-                         "engine: PyTorch eager + RCCL (the reference-equivalent stack)")
+    ap.add_argument("--impl", default="fused", choices=["fused", "graph", "stepwise", "engine"],
+                    help="fused: one-launch HIP training kernel (IPC exchange over xGMI); graph: per-step HIP "
+                         "kernels + native RCCL captured in a HIP graph; stepwise: the same launched eagerly with "
+                         "ProcessGroupNCCL; engine: PyTorch eager + RCCL (the reference-equivalent stack)")
     ap.add_argument("--model", default="simple", choices=["simple", "mlp"],
                     help="simple: the reference SimpleNet (headline); mlp: bench-size bf16 synthetic MLP on the "
                          "HIP MFMA GEMMs (BASELINE config #2)")
@@ -90,6 +91,44 @@ def allreduce_sweep(device, max_mb: int, world: int):
     return results
 
 
+def timed_run(trainer, plan, counts, args, device, comm):
+    """W untimed warmup steps, then exactly K timed steps between barrier + device syncs.
+    Returns (max elapsed over ranks, mean loss over the timed steps).  Raises on every rank if the
+    fused kernel failed on any rank."""
+    if args.warmup:
+        trainer.run_plan(plan[: args.warmup], counts[: args.warmup])
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    failed = _failed(trainer)
+    if comm.all_reduce_max(float(failed)) > 0:
+        raise RuntimeError("warmup failed on some rank")
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    trainer.loss_acc.zero_()
+    t0 = time.perf_counter()
+    trainer.run_plan(plan[args.warmup:], counts[args.warmup:])
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    comm.barrier()
+    if device.type == "cuda":
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    if comm.all_reduce_max(float(_failed(trainer))) > 0:
+        raise RuntimeError("timed run failed on some rank")
+    mean_loss = float(trainer.loss_acc.item()) / max(1, args.steps)
+    return comm.all_reduce_max(elapsed), mean_loss
+
+
+def _failed(trainer) -> bool:
+    try:
+        trainer.check()
+        return False
+    except RuntimeError as e:
+        print(f"[bench] rank failure: {e}", file=sys.stderr, flush=True)
+        return True
+
+
 def main(argv=None):
     args = parse_args(argv)
     from distributed_gpu_test_amd.data import make_synthetic_data
@@ -119,28 +158,19 @@ def main(argv=None):
         trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=args.impl if device.type == "cuda" else "torch",
                                  device=device)
     plan, counts = build_plan(trainer, args.warmup + args.steps)
-
-    # ---- warmup (untimed)
-    if args.warmup:
-        trainer.run_plan(plan[: args.warmup], counts[: args.warmup])
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    comm.barrier()
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    # ---- timed: exactly args.steps optimizer steps
-    trainer.loss_acc.zero_()
-    t0 = time.perf_counter()
-    trainer.run_plan(plan[args.warmup:], counts[args.warmup:])
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    comm.barrier()
-    if device.type == "cuda":
-        torch.cuda.synchronize()
-    elapsed = time.perf_counter() - t0
-    trainer.check()
-    mean_loss = float(trainer.loss_acc.item()) / max(1, args.steps)
-    elapsed_max = comm.all_reduce_max(elapsed)
+    try:
+        elapsed_max, mean_loss = timed_run(trainer, plan, counts, args, device, comm)
+    except RuntimeError as e:
+        # the fused kernel reports a cross-GPU exchange timeout through its status word; every rank
+        # learns about it here and the whole job re-runs on the RCCL path instead of dying
+        if getattr(trainer, "impl", "") != "fused":
+            raise
+        fallback = "graph" if comm.backend_name() == "nccl" else "stepwise"
+        print(f"[bench] fused path failed ({e}); falling back to {fallback} (RCCL)", file=sys.stderr, flush=True)
+        trainer.close()
+        trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=fallback, device=device)
+        plan, counts = build_plan(trainer, args.warmup + args.steps)
+        elapsed_max, mean_loss = timed_run(trainer, plan, counts, args, device, comm)
 
     # every rank must hold identical parameters after DP training
     consistent = True

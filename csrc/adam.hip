@@ -51,6 +51,18 @@ template <> struct Vec4<__half> {
 template <typename GT, typename LT>
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   const long long n4 = a.n >> 2;
+  float step_size_neg = a.step_size_neg, bc2_sqrt = a.bc2_sqrt;
+  if (a.step_dev) {  // graph replay: bias corrections from the device step counter, in double
+    __shared__ float sc[2];
+    if (threadIdx.x == 0) {
+      const double t = (double)*a.step_dev;
+      sc[0] = (float)(-(a.lr_d / (1.0 - pow(a.beta1_d, t))));
+      sc[1] = (float)sqrt(1.0 - pow(a.beta2_d, t));
+    }
+    __syncthreads();
+    step_size_neg = sc[0];
+    bc2_sqrt = sc[1];
+  }
   float scale = a.grad_scale;
   if (a.grad_scale_dev) scale *= *a.grad_scale_dev;
   const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
@@ -65,7 +77,7 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
       float mm = m[e], vv = v[e];
-      p[e] = adam_update(p[e], g[e] * scale, mm, vv, a.hp, a.step_size_neg, a.bc2_sqrt);
+      p[e] = adam_update(p[e], g[e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
       m[e] = mm;
       v[e] = vv;
     }
@@ -87,6 +99,13 @@ static hipError_t launch_adam_g(const AdamFlatArgs& a, hipStream_t s, int grid) 
       hipLaunchKernelGGL((adam_flat_kernel<GT, float>), dim3(grid), dim3(256), 0, s, b);
     }
   }
+  return hipGetLastError();
+}
+
+__global__ void step_increment_kernel(long long* c) { *c += 1; }
+
+hipError_t step_increment(long long* counter, hipStream_t stream) {
+  hipLaunchKernelGGL(step_increment_kernel, dim3(1), dim3(1), 0, stream, counter);
   return hipGetLastError();
 }
 

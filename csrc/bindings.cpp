@@ -162,7 +162,7 @@ void tiny_mlp_grad(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& p
 void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_lp, const at::Tensor& grad,
                const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq, double lr, double beta1, double beta2,
                double eps, double weight_decay, bool adamw, int64_t step, double grad_scale,
-               const std::optional<at::Tensor>& grad_scale_dev) {
+               const std::optional<at::Tensor>& grad_scale_dev, const std::optional<at::Tensor>& step_dev) {
   check_gpu(master, "master", at::kFloat);
   check_gpu(exp_avg, "exp_avg", at::kFloat);
   check_gpu(exp_avg_sq, "exp_avg_sq", at::kFloat);
@@ -170,7 +170,8 @@ void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_
   const int64_t n = master.numel();
   TORCH_CHECK(n % 4 == 0, "dgt: flat buffers must be padded to a multiple of 4 elements");
   TORCH_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "dgt: flat size mismatch");
-  TORCH_CHECK(step >= 1, "dgt: adam step must be >= 1");
+  const bool dev_step = step_dev.has_value() && step_dev->defined();
+  TORCH_CHECK(dev_step || step >= 1, "dgt: adam step must be >= 1");
   c10::DeviceGuard guard(master.device());
   dgt::AdamFlatArgs a;
   a.master = master.data_ptr<float>();
@@ -187,8 +188,8 @@ void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_
   a.exp_avg_sq = exp_avg_sq.data_ptr<float>();
   a.n = n;
   a.hp = make_hyper(lr, beta1, beta2, eps, weight_decay, adamw);
-  const double bc1 = 1.0 - std::pow(beta1, (double)step);
-  const double bc2 = 1.0 - std::pow(beta2, (double)step);
+  const double bc1 = 1.0 - std::pow(beta1, (double)std::max<int64_t>(step, 1));
+  const double bc2 = 1.0 - std::pow(beta2, (double)std::max<int64_t>(step, 1));
   a.step_size_neg = (float)(-(lr / bc1));
   a.bc2_sqrt = (float)std::sqrt(bc2);
   a.grad_scale = (float)grad_scale;
@@ -197,7 +198,21 @@ void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_
     check_gpu(*grad_scale_dev, "grad_scale_dev", at::kFloat);
     a.grad_scale_dev = grad_scale_dev->data_ptr<float>();
   }
+  a.step_dev = nullptr;
+  a.lr_d = lr;
+  a.beta1_d = beta1;
+  a.beta2_d = beta2;
+  if (dev_step) {
+    check_gpu(*step_dev, "step_dev", at::kLong);
+    a.step_dev = reinterpret_cast<const long long*>(step_dev->data_ptr<int64_t>());
+  }
   DGT_CHECK_HIP(dgt::adam_flat(a, stream_of(master)));
+}
+
+void step_increment(const at::Tensor& counter) {
+  check_gpu(counter, "counter", at::kLong);
+  c10::DeviceGuard guard(counter.device());
+  DGT_CHECK_HIP(dgt::step_increment(reinterpret_cast<long long*>(counter.data_ptr<int64_t>()), stream_of(counter)));
 }
 
 // ------------------------------------------------------------------------------ one-shot all-reduce
@@ -390,8 +405,9 @@ TORCH_LIBRARY(dgt, m) {
   m.def(
       "adam_flat(Tensor(a!) master, Tensor(b!)? param_lp, Tensor grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
       "float lr, float beta1, float beta2, float eps, float weight_decay, bool adamw, int step, float grad_scale, "
-      "Tensor? grad_scale_dev) -> ()",
+      "Tensor? grad_scale_dev, Tensor? step_dev=None) -> ()",
       &adam_flat);
+  m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def(
       "oneshot_allreduce(Tensor inp, Tensor(a!) out, float scale, int[] data_ptrs, int[] flag_ptrs, int rank, "
       "int world_size, int stride, int seq, int timeout_ticks, Tensor(b!) status) -> ()",

@@ -65,7 +65,14 @@ struct AdamFlatArgs {
   float bc2_sqrt;        // sqrt(1 - beta2^t)
   float grad_scale;      // multiplies the gradient (1/world_size, 1/loss_scale ...)
   const float* grad_scale_dev;  // optional extra device-side multiplier (clip coefficient)
+  // optional device-resident step counter (graph replay): when set, the kernel forms the bias
+  // corrections from *step_dev (the 1-based step of THIS update) instead of the host scalars
+  const long long* step_dev;
+  double lr_d, beta1_d, beta2_d;
 };
+
+// *counter += 1 on the stream (advances the device-side Adam step inside a captured graph)
+hipError_t step_increment(long long* counter, hipStream_t stream);
 
 hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream);
 

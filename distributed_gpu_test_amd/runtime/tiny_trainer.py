@@ -9,8 +9,11 @@ GPU instead:
   index plan (bit-exact ``DistributedSampler``) is uploaded once per epoch;
 * ``impl="fused"``: ONE kernel launch per epoch runs every step (``csrc/tiny_mlp.hip``),
   exchanging gradients with the peers through the IPC mailboxes over xGMI when world_size > 1;
-* ``impl="stepwise"``: per step a fused fwd+bwd kernel -> RCCL all-reduce -> fused flat Adam
-  (the path used when IPC is unavailable; also the A/B baseline for the fused kernel);
+* ``impl="graph"``: per step a fused fwd+bwd kernel -> native RCCL all-reduce -> fused flat Adam
+  with a device-resident step counter, one epoch of steps captured in a HIP graph and replayed
+  (the multi-GPU path when IPC mailboxes are unavailable);
+* ``impl="stepwise"``: the same kernels launched eagerly with ProcessGroupNCCL (RCCL) in between
+  (the A/B baseline for the fused kernel);
 * ``impl="torch"``: the same math in plain PyTorch (CPU / gloo, and the numerics reference).
 
 The epoch's mean loss is accumulated on the device and read once per epoch, giving the same
@@ -33,7 +36,7 @@ from . import checkpoint as ckpt
 from ..utils.fault import FaultInjector
 from .optim_state import adam_state_to_flat, flat_to_adam_state
 
-IMPLS = ("auto", "fused", "stepwise", "torch")
+IMPLS = ("auto", "fused", "graph", "stepwise", "torch")
 
 
 def fused_supported(n_features: int, hidden: int, batch_size: int) -> bool:
@@ -68,7 +71,7 @@ class TinyMLPTrainer:
         if impl == "auto":
             impl = "fused" if (self.device.type == "cuda" and fused_supported(self.F, self.H, self.B)) else (
                 "torch" if self.device.type == "cpu" else "stepwise")
-        if impl in ("fused", "stepwise"):
+        if impl in ("fused", "stepwise", "graph"):
             if self.device.type != "cuda":
                 raise RuntimeError(f"impl={impl!r} needs a GPU")
             if not fused_supported(self.F, self.H, self.B):
@@ -98,7 +101,11 @@ class TinyMLPTrainer:
         if self.impl == "fused" and self.world_size > 1:
             self.channel = self._open_channel() if use_ipc else None
             if self.channel is None:
-                self.impl = "stepwise"
+                self.impl = "graph" if comm.backend_name() == "nccl" else "stepwise"
+        self._graph = None
+        self.rccl = None
+        if self.impl == "graph":
+            self._setup_graph()
 
     # ------------------------------------------------------------------ setup helpers
     def _open_channel(self):
@@ -114,12 +121,47 @@ class TinyMLPTrainer:
             return None
         return ch
 
+    def _setup_graph(self) -> None:
+        if self.world_size > 1:
+            if comm.backend_name() != "nccl":
+                raise RuntimeError("impl='graph' needs RCCL (one GPU per rank)")
+            from ..parallel.rccl import RcclComm
+            self.rccl = RcclComm(self.device)
+        self.step_dev = torch.zeros((), dtype=torch.int64, device=self.device)
+        self._gsteps = self.steps_per_epoch()
+        self._gplan = torch.full((self._gsteps, self.B), -1, dtype=torch.int32, device=self.device)
+        self._gcounts = torch.ones(self._gsteps, dtype=torch.int32, device=self.device)
+
+    def _graph_step(self, plan, counts, s: int) -> None:
+        ops = _ext.require()
+        ops.tiny_mlp_grad(self.x, self.y, plan, counts, s, self.params, self.grad, self.loss_acc, self.F, self.H)
+        if self.rccl is not None:
+            self.rccl.all_reduce(self.grad)
+        ops.step_increment(self.step_dev)
+        adam_flat_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, 1, self.lr, self.betas[0], self.betas[1],
+                   self.eps, self.weight_decay, self.adamw, grad_scale=1.0 / self.world_size, step_dev=self.step_dev)
+
+    def _capture(self) -> None:
+        # warm the kernels once outside capture, then restore the state they touched
+        saved = [t.clone() for t in (self.params, self.exp_avg, self.exp_avg_sq, self.loss_acc, self.step_dev)]
+        self._graph_step(self._gplan, self._gcounts, 0)
+        torch.cuda.synchronize(self.device)
+        for t, v in zip((self.params, self.exp_avg, self.exp_avg_sq, self.loss_acc, self.step_dev), saved):
+            t.copy_(v)
+        g = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(g):
+            for s in range(self._gsteps):
+                self._graph_step(self._gplan, self._gcounts, s)
+        self._graph = g
+
     @property
     def exchange(self) -> str:
         if self.world_size == 1:
             return "none"
         if self.impl == "fused":
             return "ipc-oneshot-xgmi"
+        if self.impl == "graph":
+            return "rccl-native-in-hipgraph"
         return f"{comm.backend_name()}-allreduce"
 
     def steps_per_epoch(self) -> int:
@@ -147,6 +189,19 @@ class TinyMLPTrainer:
                                ch.data_ptrs if ch else [], ch.flag_ptrs if ch else [], self.rank,
                                self.world_size, ch.stride if ch else 0, seq,
                                ch.timeout_ticks if ch else 0)
+            self.global_steps += n
+        elif self.impl == "graph":
+            self.step_dev.fill_(self.global_steps)
+            s = 0
+            while n - s >= self._gsteps:
+                if self._graph is None:
+                    self._capture()
+                self._gplan.copy_(plan[s:s + self._gsteps])
+                self._gcounts.copy_(counts[s:s + self._gsteps])
+                self._graph.replay()
+                s += self._gsteps
+            for r in range(s, n):  # tail shorter than one captured epoch: eager launches
+                self._graph_step(plan, counts, r)
             self.global_steps += n
         elif self.impl == "stepwise":
             ops = _ext.require()
@@ -233,3 +288,7 @@ class TinyMLPTrainer:
         if self.channel is not None:
             self.channel.close()
             self.channel = None
+        if self.rccl is not None:
+            self.rccl.close()
+            self.rccl = None
+        self._graph = None

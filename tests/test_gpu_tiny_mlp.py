@@ -94,3 +94,36 @@ def test_adam_flat_matches_reference(gdt, lpdt, wd, adamw):
     torch.testing.assert_close(v, v2, rtol=1e-5, atol=1e-9)
     if lp is not None:
         torch.testing.assert_close(lp, p2.to(lpdt))
+
+
+def test_graph_impl_matches_oracle_and_stepwise():
+    x, y, m1 = _setup()
+    _, _, m2 = _setup()
+    g = TinyMLPTrainer(m1, x, y, 4, impl="graph")
+    s = TinyMLPTrainer(m2, x, y, 4, impl="stepwise")
+    losses = [round(g.run_epoch(e), 4) for e in range(1, 4)]
+    assert losses == ORACLE_WS1[:3]
+    for e in range(1, 4):
+        s.run_epoch(e)
+    torch.testing.assert_close(g.params, s.params, rtol=1e-5, atol=1e-7)
+    assert int(g.step_dev.item()) == g.global_steps == 1500
+    # a plan that is not a multiple of the captured epoch: graph replays + eager tail
+    plan, counts = g.epoch_plan(4)
+    g.run_plan(plan[:300], counts[:300])
+    s.run_plan(plan[:300], counts[:300])
+    torch.testing.assert_close(g.params, s.params, rtol=1e-5, atol=1e-7)
+
+
+def test_native_rccl_comm_single_rank():
+    from distributed_gpu_test_amd.parallel import comm
+    from distributed_gpu_test_amd.parallel.rccl import RcclComm
+    comm.init_distributed()
+    c = RcclComm()
+    t = torch.arange(1024, dtype=torch.float32, device="cuda")
+    c.all_reduce(t)
+    torch.testing.assert_close(t, torch.arange(1024, dtype=torch.float32, device="cuda"))
+    out = torch.empty(1024, device="cuda")
+    c.all_gather(out, t)
+    torch.testing.assert_close(out, t)
+    assert RcclComm.version() >= 22000
+    c.close()

@@ -69,18 +69,19 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 8) -> str:
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
             jobs_list.append([HIPCC, f"--offload-arch={ARCH}", *common, "-c", src, "-o", obj])
-    bsrc = os.path.join(CSRC, "bindings.cpp")
-    bobj = os.path.join(BUILD, "bindings.cpp.o")
-    objs.append(bobj)
-    if force or _newer(bobj, [bsrc] + headers):
-        jobs_list.append([HIPCC, *common, f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
-                          *[f"-I{p}" for p in inc], f"-I{sysconfig.get_paths()['include']}",
-                          "-c", bsrc, "-o", bobj])
+    # host translation units against the torch headers (op bindings, RCCL communicator)
+    for bsrc in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
+        bobj = os.path.join(BUILD, os.path.basename(bsrc) + ".o")
+        objs.append(bobj)
+        if force or _newer(bobj, [bsrc] + headers):
+            jobs_list.append([HIPCC, *common, f"-D_GLIBCXX_USE_CXX11_ABI={abi}", "-DUSE_ROCM=1",
+                              *[f"-I{p}" for p in inc], f"-I{sysconfig.get_paths()['include']}",
+                              "-c", bsrc, "-o", bobj])
     with cf.ThreadPoolExecutor(max_workers=max(1, jobs)) as ex:
         list(ex.map(lambda c: _run(c, verbose), jobs_list))
     if force or jobs_list or _newer(OUT, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", OUT,
-              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch",
+              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lrccl",
               f"-Wl,-rpath,{tlib}"], verbose)
 
     # standalone native tools (no torch): link straight against ROCm's HIP + RCCL

@@ -50,7 +50,7 @@ def parse_args(argv=None):
     p.add_argument("--save-dir", type=str, default="ds_checkpoints")
     # additions
     p.add_argument("--deepspeed_config", "--deepspeed-config", dest="deepspeed_config", default=None)
-    p.add_argument("--impl", default="auto", choices=["auto", "fused", "stepwise", "engine", "torch"])
+    p.add_argument("--impl", default="auto", choices=["auto", "fused", "graph", "stepwise", "engine", "torch"])
     p.add_argument("--backend", default=None, choices=["nccl", "gloo"])
     p.add_argument("--fail-at", default=None, help="RANK:STEP[:exit|abort|hang|nan] (STEP 'end' = after training)")
     p.add_argument("--resume", action="store_true", help="continue from the newest checkpoint in --save-dir")
@@ -95,7 +95,7 @@ def main(argv=None) -> int:
         impl = "fused" if fused_ok else "engine"
 
     start_epoch = 1
-    if impl in ("fused", "stepwise", "torch"):
+    if impl in ("fused", "graph", "stepwise", "torch"):
         from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
         trainer = TinyMLPTrainer(model, x, y, MICRO_BATCH, lr=args.lr, impl=impl, ds_config=cfg.to_dict(),
                                  device=None if impl != "torch" else torch.device("cpu"))
