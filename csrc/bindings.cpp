@@ -77,6 +77,7 @@ int dtype_code(at::ScalarType t) {
 // ------------------------------------------------------------------------------ tiny MLP
 bool tiny_mlp_supported(int64_t f, int64_t h) { return dgt::tiny_mlp_supported((int)f, (int)h); }
 int64_t tiny_mlp_padded_numel(int64_t f, int64_t h) { return dgt::tiny_mlp_padded_numel((int)f, (int)h); }
+int64_t tiny_mlp_exchange_floats(int64_t f, int64_t h) { return dgt::tiny_mlp_exchange_floats((int)f, (int)h); }
 
 void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& plan, const at::Tensor& counts,
                     const at::Tensor& params, const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq,
@@ -123,7 +124,10 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   a.status = status.data_ptr<int>();
   a.ex = make_exchange(data_ptrs, flag_ptrs, rank, world_size, stride, seq_base, timeout_ticks);
   a.stamps = nullptr;
-  if (world_size > 1) TORCH_CHECK(stride >= pp, "dgt: mailbox stride ", stride, " < ", pp);
+  if (world_size > 1) {
+    const int64_t need = dgt::tiny_mlp_exchange_floats((int)n_features, (int)hidden);
+    TORCH_CHECK(stride >= need && stride % 4 == 0, "dgt: mailbox stride ", stride, " < ", need);
+  }
   if (a.n_steps == 0) return;
   DGT_CHECK_HIP(dgt::tiny_mlp_train((int)n_features, (int)hidden, a, stream_of(X)));
 }
@@ -392,6 +396,7 @@ bool can_access_peer(int64_t dev, int64_t peer) {
 TORCH_LIBRARY(dgt, m) {
   m.def("tiny_mlp_supported(int f, int h) -> bool", &tiny_mlp_supported);
   m.def("tiny_mlp_padded_numel(int f, int h) -> int", &tiny_mlp_padded_numel);
+  m.def("tiny_mlp_exchange_floats(int f, int h) -> int", &tiny_mlp_exchange_floats);
   m.def(
       "tiny_mlp_train(Tensor X, Tensor Y, Tensor plan, Tensor counts, Tensor(a!) params, Tensor(b!) exp_avg, "
       "Tensor(c!) exp_avg_sq, Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, "

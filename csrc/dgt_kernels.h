@@ -11,6 +11,7 @@ namespace dgt {
 // Which (n_features, hidden) pairs have a compiled fused kernel.
 bool tiny_mlp_supported(int n_features, int hidden);
 int tiny_mlp_padded_numel(int n_features, int hidden);  // flat length incl. float4 padding
+int tiny_mlp_exchange_floats(int n_features, int hidden);  // IPC mailbox floats per (parity, rank)
 
 struct TinyTrainArgs {
   const float* X;        // [n_samples, F]

@@ -55,6 +55,8 @@ struct TinyCfg {
   static constexpr int T = 64 * NW;              // threads
   static constexpr int NKT = (F + 1 + 15) / 16;  // 16-wide tiles of the augmented features [x, 1]
   static constexpr int NS = 4 * NKT;             // W1 slots per lane: (ct, r) -> k = 16ct + 4(l>>4) + r
+  static constexpr int NQ = (NS + 2 + 3) / 4;    // float4s per lane in the exchange (W1 slots, W2, b2)
+  static constexpr int XCH = NW * NQ * 256;      // exchange floats per (parity, rank) mailbox slot
   static constexpr int SX = NKT * 16 + 1;        // LDS row stride of the staged batch (+1: conflict-free)
   static constexpr int BM = 16;                  // max micro-batch (MFMA N of the forward)
   static constexpr int P = H * F + 2 * H + 1;    // global flat parameter count
@@ -243,7 +245,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   WaveSmem<F, H>& ws = sm.w[w];
 
   if (a.bmax > C::BM || a.bmax < 1 || ex.world_size < 1 || ex.world_size > kMaxRanks ||
-      (ex.world_size > 1 && ex.stride < C::PP)) {
+      (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3)))) {
     if (t == 0) *a.status = kBadShape;
     return;
   }
@@ -288,22 +290,28 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(3);
 
     if (ex.world_size > 1) {
-      // ---- one-shot exchange of this wave's gradients over xGMI: push, flag, wait, sum in rank order
+      // ---- one-shot exchange of this wave's gradients over xGMI: push, flag, wait, sum in rank order.
+      // Every rank maps lanes to parameters identically, so the mailbox is lane-linear: lane l of
+      // wave w packs its slots into NQ float4s at [w][q][l]; each store instruction writes 1 KiB
+      // contiguous, and the receiver adds the peers' float4s slot by slot.
       const long long seq = ex.seq_base + s;
       const int parity = (int)(seq & 1);
       const unsigned val = (unsigned)(seq + 1);
-      const long long mine = (long long)(parity * kMaxRanks + ex.rank) * ex.stride;
-      const int bi = C::bw_index(w, lr, lq);
+      f32x4 pk[C::NQ];
+#pragma unroll
+      for (int q = 0; q < C::NQ; ++q) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * q + e;
+          pk[q][e] = i < C::NS ? gw1[i] : (i == C::NS ? gbw : (i == C::NS + 1 ? gb2 : 0.f));
+        }
+      }
+      const long long mine = (long long)(parity * kMaxRanks + ex.rank) * ex.stride + (long long)w * C::NQ * 256;
       for (int p = 0; p < ex.world_size; ++p) {
         if (p == ex.rank) continue;
         float* dst = ex.data[p] + mine;
 #pragma unroll
-        for (int i = 0; i < C::NS; ++i) {
-          const int gi = C::slot_index(w, lr, lq, i);
-          if (gi >= 0) dst[gi] = gw1[i];
-        }
-        if (bi >= 0) dst[bi] = gbw;
-        if (l == 0) dst[C::G_B2] = gb2;
+        for (int q = 0; q < C::NQ; ++q) *reinterpret_cast<f32x4*>(dst + (q * 64 + l) * 4) = pk[q];
       }
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -315,24 +323,26 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       }
       __builtin_amdgcn_wave_barrier();
-      float sw1[C::NS], sbw = 0.f, sb2 = 0.f;
+      f32x4 sum[C::NQ];
 #pragma unroll
-      for (int i = 0; i < C::NS; ++i) sw1[i] = 0.f;
+      for (int q = 0; q < C::NQ; ++q) sum[q] = f32x4{0.f, 0.f, 0.f, 0.f};
       for (int p = 0; p < ex.world_size; ++p) {
-        const float* src = ex.data[ex.rank] + (long long)(parity * kMaxRanks + p) * ex.stride;
-        const bool own = p == ex.rank;
+        const float* src = ex.data[ex.rank] + (long long)(parity * kMaxRanks + p) * ex.stride + (long long)w * C::NQ * 256;
 #pragma unroll
-        for (int i = 0; i < C::NS; ++i) {
-          const int gi = C::slot_index(w, lr, lq, i);
-          if (gi >= 0) sw1[i] += own ? gw1[i] : src[gi];
-        }
-        if (bi >= 0) sbw += own ? gbw : src[bi];
-        sb2 += own ? gb2 : src[C::G_B2];
+        for (int q = 0; q < C::NQ; ++q)
+          sum[q] += (p == ex.rank) ? pk[q] : *reinterpret_cast<const f32x4*>(src + (q * 64 + l) * 4);
       }
 #pragma unroll
-      for (int i = 0; i < C::NS; ++i) gw1[i] = sw1[i] * inv_ws;
-      gbw = sbw * inv_ws;
-      gb2 = sb2 * inv_ws;
+      for (int q = 0; q < C::NQ; ++q) {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int i = 4 * q + e;
+          const float v = sum[q][e] * inv_ws;
+          if (i < C::NS) gw1[i] = v;
+          else if (i == C::NS) gbw = v;
+          else if (i == C::NS + 1) gb2 = v;
+        }
+      }
     }
     DGT_STAMP(4);
 
@@ -433,6 +443,13 @@ bool tiny_mlp_supported(int f, int h) {
 }
 
 int tiny_mlp_padded_numel(int f, int h) { return (h * f + 2 * h + 1 + 3) / 4 * 4; }
+
+int tiny_mlp_exchange_floats(int f, int h) {
+#define X_(F_, H_) if (f == F_ && h == H_) return TinyCfg<F_, H_>::XCH;
+  DGT_TINY_SHAPES(X_)
+#undef X_
+  return 0;
+}
 
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
 #define X_(F_, H_)                                                                            \

@@ -113,7 +113,8 @@ class TinyMLPTrainer:
         if ipc_disabled_by_env() or self.world_size > 8:
             return None
         try:
-            ch = IpcChannel(self.padded, self.device, timeout_s=self.exchange_timeout_s)
+            need = int(_ext.require().tiny_mlp_exchange_floats(self.F, self.H))
+            ch = IpcChannel(max(need, self.padded), self.device, timeout_s=self.exchange_timeout_s)
         except Exception:
             return None
         if not ch.selftest():
