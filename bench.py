@@ -65,6 +65,41 @@ def build_plan(trainer, n_steps: int):
     return torch.cat(plans)[:n_steps].contiguous(), torch.cat(counts)[:n_steps].contiguous()
 
 
+def oneshot_sweep(device, world: int, max_bytes: int = 256 * 1024):
+    """The IPC one-shot all-reduce over xGMI (csrc/comm.hip) on the small sizes where latency rules."""
+    from distributed_gpu_test_amd.parallel.ipc import IpcChannel
+    if world < 2:
+        return []
+    ch = IpcChannel(max_bytes // 4, device, timeout_s=10.0)
+    try:
+        if not ch.selftest():
+            return []
+        out = []
+        size = 64
+        while size <= max_bytes:
+            n = size // 4
+            t = torch.ones(n, dtype=torch.float32, device=device)
+            o = torch.empty_like(t)
+            iters = 50
+            for _ in range(5):
+                ch.allreduce(t, o)
+            torch.cuda.synchronize()
+            dist.barrier()
+            t0 = time.perf_counter()
+            for _ in range(iters):
+                ch.allreduce(t, o)
+            torch.cuda.synchronize()
+            dt = (time.perf_counter() - t0) / iters
+            ok = ch.check_status() == 0 and bool(torch.all(o == float(world)).item())
+            algbw = n * 4 / dt / 1e9
+            out.append({"bytes": n * 4, "us": dt * 1e6, "algbw_GBps": algbw,
+                        "busbw_GBps": algbw * 2 * (world - 1) / world, "correct": ok})
+            size *= 4
+        return out
+    finally:
+        ch.close()
+
+
 def allreduce_sweep(device, max_mb: int, world: int):
     """RCCL all-reduce bus bandwidth over message sizes (rccl-tests all_reduce_perf columns)."""
     results = []
@@ -183,6 +218,13 @@ def main(argv=None):
         consistent = flag.item() == 0.0
 
     sweep = [] if (args.no_sweep or device.type != "cuda") else allreduce_sweep(device, args.sweep_max_mb, world)
+    oneshot = []
+    if sweep and comm.backend_name() == "nccl":
+        try:
+            oneshot = oneshot_sweep(device, world)
+        except Exception as e:  # the sweep is informational; never lose the headline number to it
+            print(f"[bench] one-shot sweep skipped: {e}", file=sys.stderr)
+    small_os = min(oneshot, key=lambda r: abs(r["bytes"] - 5632)) if oneshot else None
     peak_busbw = max((r["busbw_GBps"] for r in sweep), default=None)
     small = min(sweep, key=lambda r: abs(r["bytes"] - 5632)) if sweep else None
 
@@ -221,7 +263,10 @@ def main(argv=None):
         "params_consistent_across_ranks": consistent,
         "allreduce_busbw_GBps": None if peak_busbw is None else round(peak_busbw, 2),
         "allreduce_5KB_us": None if small is None else round(small["us"], 2),
+        "oneshot_xgmi_5KB_us": None if small_os is None else round(small_os["us"], 2),
         "allreduce_sweep": [{k: round(v, 3) for k, v in r.items()} for r in sweep],
+        "oneshot_xgmi_sweep": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
+                               for r in oneshot],
     }
     if rank == 0:
         print(json.dumps(out), flush=True)

@@ -38,6 +38,7 @@ from .runtime.flat import FlatLayout, FlatParamStore
 from .runtime.optim_state import adam_hparams, adam_state_to_flat, flat_to_adam_state
 from .runtime.schedules import LossScaler, build_scheduler
 from .utils.fault import FaultInjector
+from .utils import tracing
 from .utils.metrics import MetricsSink, ThroughputTimer
 
 _DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
@@ -202,7 +203,8 @@ class Engine:
         if self.dtype != torch.float32:
             args = tuple(a.to(self.dtype) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)
         self.tput.start()
-        return self.module(*args, **kwargs)
+        with tracing.range("dgt.forward"):
+            return self.module(*args, **kwargs)
 
     __call__ = forward
 
@@ -217,9 +219,11 @@ class Engine:
         if self.loss_scaler is not None:
             scaled = scaled * self.loss_scaler.scale
         t0 = time.perf_counter() if self.config.wall_clock_breakdown else 0.0
-        scaled.backward(retain_graph=retain_graph)
+        with tracing.range("dgt.backward"):
+            scaled.backward(retain_graph=retain_graph)
         if boundary:
-            self.reducer.finish()
+            with tracing.range("dgt.allreduce_wait"):
+                self.reducer.finish()
             self._boundary_pending = True
         if self.config.wall_clock_breakdown:
             if self.device.type == "cuda":
@@ -261,9 +265,10 @@ class Engine:
             self.optimizer.param_groups[0]["lr"] = float(self.client_optimizer.param_groups[0]["lr"])
         coef = self._clip_coef(grads, scale)
         g = self.optimizer.param_groups[0]
-        adam_flat_(self.master, grads, self.exp_avg, self.exp_avg_sq, self.global_steps + 1 - self.skipped_steps,
-                   g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], g["adamw"],
-                   grad_scale=scale, grad_scale_dev=coef, param_lp=self.param_lp)
+        with tracing.range("dgt.adam"):
+            adam_flat_(self.master, grads, self.exp_avg, self.exp_avg_sq, self.global_steps + 1 - self.skipped_steps,
+                       g["lr"], g["betas"][0], g["betas"][1], g["eps"], g["weight_decay"], g["adamw"],
+                       grad_scale=scale, grad_scale_dev=coef, param_lp=self.param_lp)
         if self.stage >= 1:
             self._allgather_params()
         self._finish_step(skipped=False)

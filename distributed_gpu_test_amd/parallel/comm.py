@@ -46,9 +46,20 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
         # hangs become errors instead of silent stalls
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
-        dist.init_process_group(backend=backend, init_method="env://", rank=info.rank,
-                                world_size=info.world_size,
-                                timeout=datetime.timedelta(seconds=timeout_s))
+        timeout = datetime.timedelta(seconds=timeout_s)
+        restart = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0)
+        if restart > 0 and info.world_size > 1:
+            # elastic restart (torchrun --max-restarts): the agent's store still holds the previous
+            # attempt's keys (dead peers' addresses); rendezvous under a per-attempt prefix instead
+            agent_store = os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
+            store = dist.TCPStore(info.master_addr, info.master_port, info.world_size,
+                                  is_master=(info.rank == 0 and not agent_store), timeout=timeout)
+            store = dist.PrefixStore(f"/dgt/attempt_{restart}", store)
+            dist.init_process_group(backend=backend, store=store, rank=info.rank, world_size=info.world_size,
+                                    timeout=timeout)
+        else:
+            dist.init_process_group(backend=backend, init_method="env://", rank=info.rank,
+                                    world_size=info.world_size, timeout=timeout)
     _RANK_INFO = info
     return info
 

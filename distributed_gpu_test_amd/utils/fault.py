@@ -13,6 +13,10 @@ RANK may be ``*`` (every rank).  STEP is the global optimizer step after which t
 * ``abort`` — ``os.abort()``: a crash (signal), like a segfaulting worker;
 * ``hang``  — sleep forever: exercises the process-group / CI timeouts;
 * ``nan``   — poison the loss with NaN from that step on (the training must notice / skip).
+
+``DGT_FAIL_ONCE=<path>`` makes the fault fire only while ``<path>`` does not exist (it is created
+just before firing): a restarted job (torchrun ``--max-restarts``) then runs through, which is how
+elastic recovery + ``--resume`` is exercised.
 """
 from __future__ import annotations
 
@@ -61,6 +65,12 @@ class FaultInjector:
         return self.spec is not None and (self.spec.rank is None or self.spec.rank == self.rank)
 
     def fire(self) -> None:
+        once = os.environ.get("DGT_FAIL_ONCE")
+        if once:
+            if os.path.exists(once):
+                return
+            with open(once, "w") as fh:
+                fh.write(f"rank {self.rank}\n")
         mode = self.spec.mode
         print(f"[dgt] fault injection on rank {self.rank}: {mode}", file=sys.stderr, flush=True)
         if mode == "exit":

@@ -81,6 +81,26 @@ def test_resume_continues_identically(tmp_path):
     assert epoch_losses(res.stdout) == epoch_losses(full.stdout)[2:]
 
 
+def test_elastic_restart_resumes_from_checkpoint(tmp_path):
+    clean = run(2, "--epochs", "3", "--save-dir", str(tmp_path / "clean"))
+    assert clean.returncode == 0
+    e = dict(os.environ)
+    cmd_env = {"DGT_FAIL_ONCE": str(tmp_path / "fired")}
+    # elastic restarts need the c10d rendezvous (static rendezvous keeps stale peer addresses)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2",
+                        "--max-restarts=1", "--rdzv-backend=c10d", f"--rdzv-endpoint=127.0.0.1:{free_port()}",
+                        "--rdzv-id=elastic-test",
+                        os.path.join(ROOT, "train.py"), "--epochs", "3", "--resume", "--fail-at", "0:300",
+                        "--save-dir", str(tmp_path / "elastic")],
+                       cwd=ROOT, env={**e, "DGT_QUIET": "1", "OMP_NUM_THREADS": "1", "CUDA_VISIBLE_DEVICES": "",
+                                      "HIP_VISIBLE_DEVICES": "", **cmd_env},
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert (tmp_path / "fired").exists()
+    # first attempt printed epoch 1 and died in epoch 2; the restart resumed at epoch 2
+    assert epoch_losses(r.stdout) == epoch_losses(clean.stdout)[:1] + epoch_losses(clean.stdout)[1:]
+
+
 @pytest.mark.parametrize("spec", ["1:end", "0:3:exit", "*:2:abort"])
 def test_fault_injection_fails_the_job(spec, tmp_path):
     r = run(2, "--epochs", "1", "--fail-at", spec, "--no-save", timeout=180)

@@ -56,6 +56,9 @@ def parse_args(argv=None):
     p.add_argument("--resume", action="store_true", help="continue from the newest checkpoint in --save-dir")
     p.add_argument("--no-save", action="store_true")
     p.add_argument("--dist-timeout", type=float, default=1800.0)
+    p.add_argument("--profile", default=None, help="write a torch.profiler (kineto) trace per rank to this dir")
+    p.add_argument("--debug-sync", action="store_true",
+                   help="serialize kernels (AMD_SERIALIZE_KERNEL=3) and sync comm/compute streams: race hunting")
     return p.parse_known_args(argv)[0]
 
 
@@ -72,6 +75,9 @@ def newest_checkpoint(save_dir: str):
 
 def main(argv=None) -> int:
     args = parse_args(argv)
+    if args.debug_sync:  # serialize to bisect ordering bugs between streams
+        os.environ.setdefault("AMD_SERIALIZE_KERNEL", "3")
+        os.environ.setdefault("AMD_SERIALIZE_COPY", "3")
     torch.manual_seed(args.seed)
     info = comm.init_distributed(backend=args.backend, timeout_s=args.dist_timeout)
     local_rank, world = info.local_rank, comm.get_world_size()
@@ -80,6 +86,8 @@ def main(argv=None) -> int:
         os.environ["DGT_FAIL_AT"] = args.fail_at
 
     ds_config = REFERENCE_DS_CONFIG if args.deepspeed_config is None else json.load(open(args.deepspeed_config))
+    if args.debug_sync:
+        ds_config = dict(ds_config, amd=dict(ds_config.get("amd", {}), debug_sync_streams=True))
     cfg = parse_config(ds_config, world)  # DeepSpeed's batch assertion on every path
 
     x, y = make_synthetic_data(n_samples=N_SAMPLES, n_features=N_FEATURES, seed=args.seed)
@@ -131,25 +139,29 @@ def main(argv=None) -> int:
             if found:
                 engine.load_checkpoint(found[1])
                 start_epoch = found[0] + 1
-        for epoch in range(start_epoch, args.epochs + 1):
-            engine.train()
-            data.set_epoch(epoch)
-            loss_acc = torch.zeros((), dtype=torch.float64, device=device)
-            steps = 0
-            for batch_x, batch_y in data:
-                logits = engine(batch_x)
-                loss = criterion(logits.float(), batch_y)
-                engine.backward(loss)
-                engine.step()
-                loss_acc += loss.detach().double()  # on device: no per-step host sync
-                steps += 1
-            avg_loss = float(loss_acc.item()) / max(1, steps)
-            if local_rank == 0:
-                print(f"Epoch {epoch:2d} finished. Avg loss: {avg_loss:.4f}", flush=True)
-            if not args.no_save:
-                save_dir = os.path.join(args.save_dir, f"epoch{epoch}")
-                os.makedirs(save_dir, exist_ok=True)
-                engine.save_checkpoint(save_dir)
+        from distributed_gpu_test_amd.utils.tracing import Profiler
+        prof = Profiler(args.profile, comm.get_rank())
+        with prof:
+            for epoch in range(start_epoch, args.epochs + 1):
+                engine.train()
+                data.set_epoch(epoch)
+                loss_acc = torch.zeros((), dtype=torch.float64, device=device)
+                steps = 0
+                for batch_x, batch_y in data:
+                    logits = engine(batch_x)
+                    loss = criterion(logits.float(), batch_y)
+                    engine.backward(loss)
+                    engine.step()
+                    prof.step()
+                    loss_acc += loss.detach().double()  # on device: no per-step host sync
+                    steps += 1
+                avg_loss = float(loss_acc.item()) / max(1, steps)
+                if local_rank == 0:
+                    print(f"Epoch {epoch:2d} finished. Avg loss: {avg_loss:.4f}", flush=True)
+                if not args.no_save:
+                    save_dir = os.path.join(args.save_dir, f"epoch{epoch}")
+                    os.makedirs(save_dir, exist_ok=True)
+                    engine.save_checkpoint(save_dir)
         engine.close()
 
     if local_rank == 0:
