@@ -67,24 +67,44 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   if (a.grad_scale_dev) scale *= *a.grad_scale_dev;
   const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
   LT* __restrict__ lp = static_cast<LT*>(a.param_lp);
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long o = 4 * i;
-    f32x4 p = Vec4<float>::load(a.master + o);
-    f32x4 g = Vec4<GT>::load(grad + o);
-    f32x4 m = Vec4<float>::load(a.exp_avg + o);
-    f32x4 v = Vec4<float>::load(a.exp_avg_sq + o);
+  // two float4 groups per thread per iteration: 8 independent 16-byte loads in flight per lane
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += 2 * stride) {
+    const bool two = i + stride < n4;
+    const long long o0 = 4 * i, o1 = 4 * (i + stride);
+    f32x4 p0 = Vec4<float>::load(a.master + o0), g0 = Vec4<GT>::load(grad + o0);
+    f32x4 m0 = Vec4<float>::load(a.exp_avg + o0), v0 = Vec4<float>::load(a.exp_avg_sq + o0);
+    f32x4 p1, g1, m1, v1;
+    if (two) {
+      p1 = Vec4<float>::load(a.master + o1);
+      g1 = Vec4<GT>::load(grad + o1);
+      m1 = Vec4<float>::load(a.exp_avg + o1);
+      v1 = Vec4<float>::load(a.exp_avg_sq + o1);
+    }
 #pragma unroll
     for (int e = 0; e < 4; ++e) {
-      float mm = m[e], vv = v[e];
-      p[e] = adam_update(p[e], g[e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
-      m[e] = mm;
-      v[e] = vv;
+      float mm = m0[e], vv = v0[e];
+      p0[e] = adam_update(p0[e], g0[e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
+      m0[e] = mm;
+      v0[e] = vv;
     }
-    Vec4<float>::store(a.master + o, p);
-    Vec4<float>::store(a.exp_avg + o, m);
-    Vec4<float>::store(a.exp_avg_sq + o, v);
-    if (lp) Vec4<LT>::store(lp + o, p);
+    Vec4<float>::store(a.master + o0, p0);
+    Vec4<float>::store(a.exp_avg + o0, m0);
+    Vec4<float>::store(a.exp_avg_sq + o0, v0);
+    if (lp) Vec4<LT>::store(lp + o0, p0);
+    if (two) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float mm = m1[e], vv = v1[e];
+        p1[e] = adam_update(p1[e], g1[e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
+        m1[e] = mm;
+        v1[e] = vv;
+      }
+      Vec4<float>::store(a.master + o1, p1);
+      Vec4<float>::store(a.exp_avg + o1, m1);
+      Vec4<float>::store(a.exp_avg_sq + o1, v1);
+      if (lp) Vec4<LT>::store(lp + o1, p1);
+    }
   }
 }
 
@@ -112,8 +132,8 @@ hipError_t step_increment(long long* counter, hipStream_t stream) {
 hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream) {
   if (a.n % 4 != 0) return hipErrorInvalidValue;
   const long long n4 = a.n / 4;
-  long long grid = (n4 + 255) / 256;
-  if (grid > 2048) grid = 2048;
+  long long grid = (n4 + 511) / 512;
+  if (grid > 4096) grid = 4096;  // 16 blocks per CU: enough loads in flight to stream HBM
   if (grid < 1) grid = 1;
   switch (a.grad_dtype) {
     case kBF16: return launch_adam_g<__hip_bfloat16>(a, stream, (int)grid);

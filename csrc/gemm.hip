@@ -172,21 +172,48 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream) {
 }
 
 // ------------------------------------------------------------------ transpose (bf16, 64x64 tiles)
+// 16-byte global loads and stores: a thread moves one 8-element row chunk in and one 8-element
+// column chunk out; the tile sits in LDS with a 2-element pad per row (no 32-way column conflicts).
 __global__ __launch_bounds__(256) void transpose_bf16_kernel(const u16* __restrict__ in, u16* __restrict__ out,
                                                              int rows, int cols) {
-  __shared__ u16 tile[64][65];
+  __shared__ u16 tile[64][66];
   const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64;
   const int t = threadIdx.x;
+  const bool full = (r0 + 64 <= rows) && (c0 + 64 <= cols) && (cols % 8 == 0) && (rows % 8 == 0);
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int rr = i * 4 + (t >> 6), cc = t & 63;
-    if (r0 + rr < rows && c0 + cc < cols) tile[rr][cc] = in[(long long)(r0 + rr) * cols + c0 + cc];
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i;          // 512 chunks of 8 elements
+    const int rr = idx >> 3, cc = (idx & 7) * 8;
+    if (full) {
+      const uint4 v = *reinterpret_cast<const uint4*>(in + (long long)(r0 + rr) * cols + c0 + cc);
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        tile[rr][cc + 2 * e] = (u16)(w[e] & 0xffff);
+        tile[rr][cc + 2 * e + 1] = (u16)(w[e] >> 16);
+      }
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (r0 + rr < rows && c0 + cc + e < cols) tile[rr][cc + e] = in[(long long)(r0 + rr) * cols + c0 + cc + e];
+    }
   }
   __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int cc = i * 4 + (t >> 6), rr = t & 63;
-    if (c0 + cc < cols && r0 + rr < rows) out[(long long)(c0 + cc) * rows + r0 + rr] = tile[rr][cc];
+  for (int i = 0; i < 2; ++i) {
+    const int idx = t + 256 * i;
+    const int oc = idx >> 3, orr = (idx & 7) * 8;  // output row = input column oc, 8 input rows orr..
+    if (full) {
+      unsigned w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        w[e] = (unsigned)tile[orr + 2 * e][oc] | ((unsigned)tile[orr + 2 * e + 1][oc] << 16);
+      *reinterpret_cast<uint4*>(out + (long long)(c0 + oc) * rows + r0 + orr) = make_uint4(w[0], w[1], w[2], w[3]);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 8; ++e)
+        if (c0 + oc < cols && r0 + orr + e < rows) out[(long long)(c0 + oc) * rows + r0 + orr + e] = tile[orr + e][oc];
+    }
   }
 }
 
