@@ -65,7 +65,7 @@ def build_plan(trainer, n_steps: int):
     return torch.cat(plans)[:n_steps].contiguous(), torch.cat(counts)[:n_steps].contiguous()
 
 
-def oneshot_sweep(device, world: int, max_bytes: int = 256 * 1024):
+def oneshot_sweep(device, world: int, max_bytes: int = 1024 * 1024):
     """The IPC one-shot all-reduce over xGMI (csrc/comm.hip) on the small sizes where latency rules."""
     from distributed_gpu_test_amd.parallel.ipc import IpcChannel
     if world < 2:
@@ -76,12 +76,13 @@ def oneshot_sweep(device, world: int, max_bytes: int = 256 * 1024):
             return []
         out = []
         size = 64
+        reps = 200
         while size <= max_bytes:
             n = size // 4
             t = torch.ones(n, dtype=torch.float32, device=device)
             o = torch.empty_like(t)
-            iters = 50
-            for _ in range(5):
+            iters = 20
+            for _ in range(3):
                 ch.allreduce(t, o)
             torch.cuda.synchronize()
             dist.barrier()
@@ -90,9 +91,15 @@ def oneshot_sweep(device, world: int, max_bytes: int = 256 * 1024):
                 ch.allreduce(t, o)
             torch.cuda.synchronize()
             dt = (time.perf_counter() - t0) / iters
+            # device latency: `reps` back-to-back all-reduces inside one launch (no host gaps)
+            dist.barrier()
+            t0 = time.perf_counter()
+            ch.allreduce(t, o, reps=reps)
+            torch.cuda.synchronize()
+            dt_dev = (time.perf_counter() - t0) / reps
             ok = ch.check_status() == 0 and bool(torch.all(o == float(world)).item())
-            algbw = n * 4 / dt / 1e9
-            out.append({"bytes": n * 4, "us": dt * 1e6, "algbw_GBps": algbw,
+            algbw = n * 4 / dt_dev / 1e9
+            out.append({"bytes": n * 4, "us": dt_dev * 1e6, "us_per_launch": dt * 1e6, "algbw_GBps": algbw,
                         "busbw_GBps": algbw * 2 * (world - 1) / world, "correct": ok})
             size *= 4
         return out
@@ -217,9 +224,10 @@ def main(argv=None):
         dist.all_reduce(flag, op=dist.ReduceOp.MAX)
         consistent = flag.item() == 0.0
 
-    sweep = [] if (args.no_sweep or device.type != "cuda") else allreduce_sweep(device, args.sweep_max_mb, world)
+    gpu_sweeps = not args.no_sweep and device.type == "cuda" and world > 1
+    sweep = allreduce_sweep(device, args.sweep_max_mb, world) if gpu_sweeps and comm.backend_name() == "nccl" else []
     oneshot = []
-    if sweep and comm.backend_name() == "nccl":
+    if gpu_sweeps:
         try:
             oneshot = oneshot_sweep(device, world)
         except Exception as e:  # the sweep is informational; never lose the headline number to it

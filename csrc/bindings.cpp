@@ -42,7 +42,7 @@ dgt::AdamHyper make_hyper(double lr, double beta1, double beta2, double eps, dou
   return h;
 }
 
-dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, c10::ArrayRef<int64_t> flag_ptrs, int64_t rank,
+dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank,
                             int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks) {
   dgt::Exchange ex;
   std::memset(&ex, 0, sizeof(ex));
@@ -54,12 +54,11 @@ dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, c10::ArrayRef<int6
   ex.seq_base = seq_base;
   ex.timeout_ticks = timeout_ticks;
   if (world_size > 1) {
-    TORCH_CHECK((int64_t)data_ptrs.size() == world_size && (int64_t)flag_ptrs.size() == world_size,
-                "dgt: need one mailbox pointer per rank");
+    TORCH_CHECK((int64_t)data_ptrs.size() == world_size, "dgt: need one mailbox pointer per rank");
+    TORCH_CHECK(stride > 0 && stride % 256 == 0, "dgt: mailbox stride must be a positive multiple of 256 floats");
     for (int64_t i = 0; i < world_size; ++i) {
-      TORCH_CHECK(data_ptrs[i] != 0 && flag_ptrs[i] != 0, "dgt: null mailbox pointer for rank ", i);
-      ex.data[i] = reinterpret_cast<float*>(data_ptrs[i]);
-      ex.flags[i] = reinterpret_cast<unsigned*>(flag_ptrs[i]);
+      TORCH_CHECK(data_ptrs[i] != 0, "dgt: null mailbox pointer for rank ", i);
+      ex.data[i] = reinterpret_cast<unsigned*>(data_ptrs[i]);
     }
   }
   return ex;
@@ -83,7 +82,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
                     const at::Tensor& params, const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq,
                     const at::Tensor& loss_acc, const at::Tensor& status, int64_t n_features, int64_t hidden,
                     double lr, double beta1, double beta2, double eps, double weight_decay, bool adamw,
-                    int64_t adam_step0, c10::ArrayRef<int64_t> data_ptrs, c10::ArrayRef<int64_t> flag_ptrs,
+                    int64_t adam_step0, c10::ArrayRef<int64_t> data_ptrs,
                     int64_t rank, int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks) {
   TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
               " H=", hidden);
@@ -122,7 +121,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   a.adam_step0 = adam_step0;
   a.loss_acc = loss_acc.data_ptr<double>();
   a.status = status.data_ptr<int>();
-  a.ex = make_exchange(data_ptrs, flag_ptrs, rank, world_size, stride, seq_base, timeout_ticks);
+  a.ex = make_exchange(data_ptrs, rank, world_size, stride, seq_base, timeout_ticks);
   a.stamps = nullptr;
   if (world_size > 1) {
     const int64_t need = dgt::tiny_mlp_exchange_floats((int)n_features, (int)hidden);
@@ -221,17 +220,17 @@ void step_increment(const at::Tensor& counter) {
 
 // ------------------------------------------------------------------------------ one-shot all-reduce
 void oneshot_allreduce(const at::Tensor& inp, const at::Tensor& out, double scale, c10::ArrayRef<int64_t> data_ptrs,
-                       c10::ArrayRef<int64_t> flag_ptrs, int64_t rank, int64_t world_size, int64_t stride,
-                       int64_t seq, int64_t timeout_ticks, const at::Tensor& status) {
+                       int64_t rank, int64_t world_size, int64_t stride,
+                       int64_t seq, int64_t timeout_ticks, const at::Tensor& status, int64_t reps) {
   check_gpu(inp, "inp", at::kFloat);
   check_gpu(out, "out", at::kFloat);
   check_gpu(status, "status", at::kInt);
   TORCH_CHECK(inp.numel() == out.numel() && inp.numel() % 4 == 0 && inp.numel() <= stride,
               "dgt: one-shot all-reduce needs equal sizes, a multiple of 4 and <= mailbox stride");
   c10::DeviceGuard guard(inp.device());
-  dgt::Exchange ex = make_exchange(data_ptrs, flag_ptrs, rank, world_size, stride, seq, timeout_ticks);
+  dgt::Exchange ex = make_exchange(data_ptrs, rank, world_size, stride, seq, timeout_ticks);
   DGT_CHECK_HIP(dgt::oneshot_allreduce(inp.data_ptr<float>(), out.data_ptr<float>(), inp.numel(), (float)scale, ex,
-                                       status.data_ptr<int>(), stream_of(inp)));
+                                       status.data_ptr<int>(), stream_of(inp), (int)reps));
 }
 
 // ------------------------------------------------------------------------------ bf16 GEMM + MLP helpers
@@ -401,7 +400,7 @@ TORCH_LIBRARY(dgt, m) {
       "tiny_mlp_train(Tensor X, Tensor Y, Tensor plan, Tensor counts, Tensor(a!) params, Tensor(b!) exp_avg, "
       "Tensor(c!) exp_avg_sq, Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, "
       "float beta1, float beta2, float eps, float weight_decay, bool adamw, int adam_step0, int[] data_ptrs, "
-      "int[] flag_ptrs, int rank, int world_size, int stride, int seq_base, int timeout_ticks) -> ()",
+      "int rank, int world_size, int stride, int seq_base, int timeout_ticks) -> ()",
       &tiny_mlp_train);
   m.def(
       "tiny_mlp_grad(Tensor X, Tensor Y, Tensor plan, Tensor counts, int step, Tensor params, Tensor(a!) grad, "
@@ -414,8 +413,8 @@ TORCH_LIBRARY(dgt, m) {
       &adam_flat);
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def(
-      "oneshot_allreduce(Tensor inp, Tensor(a!) out, float scale, int[] data_ptrs, int[] flag_ptrs, int rank, "
-      "int world_size, int stride, int seq, int timeout_ticks, Tensor(b!) status) -> ()",
+      "oneshot_allreduce(Tensor inp, Tensor(a!) out, float scale, int[] data_ptrs, int rank, "
+      "int world_size, int stride, int seq, int timeout_ticks, Tensor(b!) status, int reps=1) -> ()",
       &oneshot_allreduce);
   m.def(
       "gemm_nt(Tensor A, Tensor B, Tensor(a!)? C, Tensor(b!)? CT, Tensor? bias, Tensor? mask, int epi, "

@@ -1,85 +1,100 @@
-// Cross-GPU one-shot all-reduce over xGMI for latency-bound (small) buckets, plus the IPC
-// mailbox runtime it runs on.
+// Cross-GPU one-shot all-reduce over xGMI for latency-bound (small) buckets.
 //
 // Why: the reference's only per-step collective is a 5.6 KB gradient all-reduce.
 // A ring all-reduce (RCCL) crosses 2(n-1) = 14 hops at n = 8; on MI355X every GPU has a direct
 // xGMI link to each of its 7 peers, so a push-based one-shot exchange costs ONE link latency:
-// every rank writes its buffer into each peer's mailbox (7 links in parallel), raises a
-// per-(block, rank) sequence flag with a system-scope release, waits for its own flags and sums
-// the contributions locally in rank order (bit-identical results on every rank).
+// every rank streams its buffer into each peer's mailbox as low-latency (LL) lines (payload and
+// sequence tag in every 8-byte pair, dgt_common.h), then polls its own mailbox until every peer's
+// lines carry this call's tag and sums the contributions locally in rank order (bit-identical
+// results on every rank).  No fences, no flags, no inter-block synchronisation: every block owns
+// a disjoint range of the buffer, so the grid can be as wide as the payload.
 //
-// Mailbox layout (one uncached, IPC-exported allocation per rank):
-//   data  : float [2 parity][kMaxRanks src][stride]
-//   flags : uint32 [kMaxBlocks][2 parity][kMaxRanks src] (monotonic sequence numbers)
-// Sequence numbers come from the host (one per call), so no memset is needed between calls.
+// Mailbox slot layout (words): float4 i -> LL lines 2*(i/64) and 2*(i/64)+1, lane i%64 -> every
+// wave-instruction writes or reads 1 KiB contiguous.
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 
 namespace dgt {
 
-constexpr int kMaxBlocks = 64;
+constexpr int kMaxBlocks = 256;
+
+DGT_DEVICE long long os_word(long long i) { return (2 * (i >> 6)) * 256 + (i & 63) * 4; }
 
 __global__ __launch_bounds__(256) void oneshot_allreduce_kernel(const float* __restrict__ in,
                                                                 float* __restrict__ out, long long n,
-                                                                float scale, Exchange ex, int* status) {
-  __shared__ int err;
-  const int t = threadIdx.x;
-  if (t == 0) err = 0;
+                                                                float scale, Exchange ex, int* status,
+                                                                int reps) {
   const long long n4 = n >> 2;
-  const long long per = (n4 + gridDim.x - 1) / gridDim.x;
-  const long long lo = blockIdx.x * per;
-  const long long hi = lo + per < n4 ? lo + per : n4;
-  const long long seq = ex.seq_base;
-  const int parity = (int)(seq & 1);
-  const unsigned val = (unsigned)(seq + 1);
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  const long long first = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  bool late = false;
+  // reps > 1 runs back-to-back all-reduces of the same input (latency measurement without launch
+  // gaps).  Safe without grid synchronisation: every rank gives thread t the same elements, and a
+  // sender reaches rep r+2 (same parity slot) only after reading the peer's rep r+1, which the
+  // peer pushes only after it has read rep r.
+  for (int r = 0; r < reps && !late; ++r) {
+    const long long seq = ex.seq_base + r;
+    const int parity = (int)(seq & 1);
+    const unsigned tag = (unsigned)(seq + 1);
+    const long long mine = ll_slot(ex, parity, ex.rank);
 
-  for (long long i = lo + t; i < hi; i += blockDim.x) {
-    const f32x4 v = *reinterpret_cast<const f32x4*>(in + 4 * i);
-    for (int p = 0; p < ex.world_size; ++p) {
-      if (p == ex.rank) continue;
-      *reinterpret_cast<f32x4*>(ex.data[p] + (long long)(parity * kMaxRanks + ex.rank) * ex.stride + 4 * i) = v;
+    for (long long i = first; i < n4; i += stride) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(in + 4 * i);
+      const long long o = mine + os_word(i);
+      for (int p = 0; p < ex.world_size; ++p) {
+        if (p == ex.rank) continue;
+        ll_put(ex.data[p] + o, v[0], v[1], tag);
+        ll_put(ex.data[p] + o + 256, v[2], v[3], tag);
+      }
+    }
+
+    const unsigned long long t0 = realtime();
+    for (long long i = first; i < n4; i += stride) {
+      const long long o = os_word(i);
+      unsigned long long v[kMaxRanks][4];
+      bool ready;
+      do {  // re-read every peer's lines per retry: one round trip per poll
+        ready = true;
+#pragma unroll
+        for (int p = 0; p < kMaxRanks; ++p) {
+          if (p < ex.world_size && p != ex.rank) {
+            const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, p) + o;
+#pragma unroll
+            for (int k = 0; k < 4; ++k) v[p][k] = ll_get(src + (k >> 1) * 256 + (k & 1) * 2);
+          }
+        }
+#pragma unroll
+        for (int p = 0; p < kMaxRanks; ++p) {
+          if (p < ex.world_size && p != ex.rank) {
+#pragma unroll
+            for (int k = 0; k < 4; ++k) ready = ready && ll_ok(v[p][k], tag);
+          }
+        }
+        if (!ready && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
+      } while (!ready && !late);
+      f32x4 sum = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int p = 0; p < kMaxRanks; ++p) {
+        if (p >= ex.world_size) continue;
+        if (p == ex.rank) sum += *reinterpret_cast<const f32x4*>(in + 4 * i);
+        else sum += f32x4{ll_val(v[p][0]), ll_val(v[p][1]), ll_val(v[p][2]), ll_val(v[p][3])};
+      }
+      *reinterpret_cast<f32x4*>(out + 4 * i) = sum * scale;
     }
   }
-  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  if (t < ex.world_size && t != ex.rank) {
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    unsigned* peer_flags = ex.flags[t] + (blockIdx.x * 2 + parity) * kMaxRanks;
-    store_release_system(peer_flags + ex.rank, val);
-    unsigned* my_flags = ex.flags[ex.rank] + (blockIdx.x * 2 + parity) * kMaxRanks;
-    if (!spin_geq(my_flags + t, val, ex.timeout_ticks)) err = 1;
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  }
-  __syncthreads();
-  if (err) {
-    if (t == 0) atomicExch(status, (int)kTimeout);
-    return;
-  }
-  for (long long i = lo + t; i < hi; i += blockDim.x) {
-    f32x4 sum = {0.f, 0.f, 0.f, 0.f};
-    for (int p = 0; p < ex.world_size; ++p) {
-      f32x4 v;
-      if (p == ex.rank) v = *reinterpret_cast<const f32x4*>(in + 4 * i);
-      else v = *reinterpret_cast<const f32x4*>(ex.data[ex.rank] + (long long)(parity * kMaxRanks + p) * ex.stride + 4 * i);
-      sum += v;
-    }
-    *reinterpret_cast<f32x4*>(out + 4 * i) = sum * scale;
-  }
+  if (late) atomicExch(status, (int)kTimeout);
 }
 
 hipError_t oneshot_allreduce(const float* in, float* out, long long n, float scale, const Exchange& ex,
-                             int* status, hipStream_t stream) {
-  if (n % 4 != 0 || n > ex.stride || ex.world_size < 1 || ex.world_size > kMaxRanks) return hipErrorInvalidValue;
+                             int* status, hipStream_t stream, int reps) {
+  if (reps < 1 || n % 4 != 0 || n > ex.stride || (ex.stride & 255) || ex.world_size < 1 || ex.world_size > kMaxRanks)
+    return hipErrorInvalidValue;
   const long long n4 = n / 4;
-  // one block per 64 KB of payload keeps all 7 outgoing links fed without flag overhead dominating
-  long long blocks = (n4 * 16 + 65535) / 65536;
+  long long blocks = (n4 + 255) / 256;  // one float4 per thread up to 256 blocks (1 MiB)
   if (blocks < 1) blocks = 1;
   if (blocks > kMaxBlocks) blocks = kMaxBlocks;
   hipLaunchKernelGGL(oneshot_allreduce_kernel, dim3((int)blocks), dim3(256), 0, stream, in, out, n, scale, ex,
-                     status);
+                     status, reps);
   return hipGetLastError();
 }
 

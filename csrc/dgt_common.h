@@ -36,17 +36,42 @@ struct AdamHyper {
 
 // Cross-GPU exchange arguments for the IPC one-shot gradient exchange.  Every rank owns one
 // "mailbox" allocation (uncached device memory, IPC-exported); peers write into it over xGMI.
-//   data  : float [2 parity][kMaxRanks src][stride]
-//   flags : uint32 [2 parity][kMaxRanks src]   (monotonic sequence numbers, never reset)
+//   data : LL lines [2 parity][kMaxRanks src][stride / 2]     (stride = payload floats per slot)
+// A low-latency (LL) line is 16 bytes = two {payload float, tag} pairs; the tag is the exchange's
+// sequence number + 1.  Each aligned 8-byte pair lands atomically, so a reader that sees both
+// tags of a line has both payloads: no release fence, no separate flag, no acquire fence, and
+// the reader's polls return the data itself (one xGMI latency per exchange).  Tags increase
+// monotonically per channel, so mailboxes are zeroed once, at creation.
 struct Exchange {
   int rank;
   int world_size;
-  int stride;                       // floats per (parity, src) slot
+  int stride;                       // payload floats per (parity, src) slot; the slot is 2*stride words
   long long seq_base;               // sequence number of the first exchange of this launch (0-based)
   long long timeout_ticks;          // bound on every spin, in s_memrealtime ticks (100 MHz)
-  float* data[kMaxRanks];           // each rank's data region (index rank = local)
-  unsigned* flags[kMaxRanks];       // each rank's flag region
+  unsigned* data[kMaxRanks];        // each rank's mailbox (index rank = local)
 };
+
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+
+// word offset of (parity, src)'s slot in a mailbox
+DGT_DEVICE long long ll_slot(const Exchange& ex, int parity, int src) {
+  return (long long)(parity * kMaxRanks + src) * ex.stride * 2;
+}
+
+// push one LL line (two payload floats) into a peer's mailbox: one 16-byte streaming store
+DGT_DEVICE void ll_put(unsigned* dst, float a, float b, unsigned tag) {
+  u32x4 v = {__float_as_uint(a), tag, __float_as_uint(b), tag};
+  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+}
+
+// one {payload, tag} pair from the local mailbox: a relaxed system-scope 64-bit load (sc0 sc1,
+// never served from a stale cache line; many can be in flight, unlike volatile accesses)
+DGT_DEVICE unsigned long long ll_get(const unsigned* src) {
+  return __hip_atomic_load(reinterpret_cast<const unsigned long long*>(src), __ATOMIC_RELAXED,
+                           __HIP_MEMORY_SCOPE_SYSTEM);
+}
+DGT_DEVICE bool ll_ok(unsigned long long pair, unsigned tag) { return (unsigned)(pair >> 32) == tag; }
+DGT_DEVICE float ll_val(unsigned long long pair) { return __uint_as_float((unsigned)pair); }
 
 template <int CTRL>
 DGT_DEVICE float dpp_mov(float v) {
@@ -78,25 +103,6 @@ DGT_DEVICE float wave_sum(float v) {
 }
 
 DGT_DEVICE unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
-
-DGT_DEVICE void store_release_system(unsigned* p, unsigned v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-DGT_DEVICE unsigned load_relaxed_system(unsigned* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
-
-// Bounded spin until *p >= want (wrap-safe compare).  Returns false on timeout.
-DGT_DEVICE bool spin_geq(unsigned* p, unsigned want, long long timeout_ticks) {
-  const unsigned long long t0 = realtime();
-  while (true) {
-    unsigned cur = load_relaxed_system(p);
-    if ((int)(cur - want) >= 0) return true;
-    if ((long long)(realtime() - t0) > timeout_ticks) return false;
-    __builtin_amdgcn_s_sleep(1);
-  }
-}
 
 // torch.lerp for weight < 0.5 (what Adam's exp_avg.lerp_(grad, 1 - beta1) evaluates)
 DGT_DEVICE float lerp_torch(float self, float end, float w) {

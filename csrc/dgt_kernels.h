@@ -81,7 +81,7 @@ hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream);
 // in[n] (fp32) from every rank -> out[n] = scale * sum over ranks (rank order, identical bits on
 // every rank).  Uses the Exchange mailboxes; n <= ex.stride.
 hipError_t oneshot_allreduce(const float* in, float* out, long long n, float scale, const Exchange& ex,
-                             int* status, hipStream_t stream);
+                             int* status, hipStream_t stream, int reps = 1);
 
 // ---------------------------------------------------------------- bf16 MFMA GEMM (gemm.hip)
 enum GemmEpilogue : int {

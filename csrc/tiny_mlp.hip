@@ -290,13 +290,13 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(3);
 
     if (ex.world_size > 1) {
-      // ---- one-shot exchange of this wave's gradients over xGMI: push, flag, wait, sum in rank order.
+      // ---- one-shot LL exchange of this wave's gradients over xGMI: push, poll, sum in rank order.
       // Every rank maps lanes to parameters identically, so the mailbox is lane-linear: lane l of
-      // wave w packs its slots into NQ float4s at [w][q][l]; each store instruction writes 1 KiB
-      // contiguous, and the receiver adds the peers' float4s slot by slot.
+      // wave w packs its slots into NQ float4s = 2*NQ LL lines at [w][line][l]; every store
+      // instruction writes 1 KiB contiguous into a peer, every poll reads the local mailbox.
       const long long seq = ex.seq_base + s;
       const int parity = (int)(seq & 1);
-      const unsigned val = (unsigned)(seq + 1);
+      const unsigned tag = (unsigned)(seq + 1);
       f32x4 pk[C::NQ];
 #pragma unroll
       for (int q = 0; q < C::NQ; ++q) {
@@ -306,32 +306,62 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
           pk[q][e] = i < C::NS ? gw1[i] : (i == C::NS ? gbw : (i == C::NS + 1 ? gb2 : 0.f));
         }
       }
-      const long long mine = (long long)(parity * kMaxRanks + ex.rank) * ex.stride + (long long)w * C::NQ * 256;
+      const long long wofs = (long long)w * C::NQ * 512 + l * 4;
+      const long long mine = ll_slot(ex, parity, ex.rank) + wofs;
       for (int p = 0; p < ex.world_size; ++p) {
         if (p == ex.rank) continue;
-        float* dst = ex.data[p] + mine;
+        unsigned* dst = ex.data[p] + mine;
 #pragma unroll
-        for (int q = 0; q < C::NQ; ++q) *reinterpret_cast<f32x4*>(dst + (q * 64 + l) * 4) = pk[q];
+        for (int q = 0; q < C::NQ; ++q) {
+          ll_put(dst + (2 * q) * 256, pk[q][0], pk[q][1], tag);
+          ll_put(dst + (2 * q + 1) * 256, pk[q][2], pk[q][3], tag);
+        }
       }
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "");
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      if (l < ex.world_size && l != ex.rank) {
-        const int fo = (w * 2 + parity) * kMaxRanks;
-        store_release_system(ex.flags[l] + fo + ex.rank, val);
-        if (!spin_geq(ex.flags[ex.rank] + fo + l, val, ex.timeout_ticks)) sm.err = 1;
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-      }
-      __builtin_amdgcn_wave_barrier();
       f32x4 sum[C::NQ];
 #pragma unroll
       for (int q = 0; q < C::NQ; ++q) sum[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      for (int p = 0; p < ex.world_size; ++p) {
-        const float* src = ex.data[ex.rank] + (long long)(parity * kMaxRanks + p) * ex.stride + (long long)w * C::NQ * 256;
+      const unsigned long long t0 = realtime();
+      bool late = false;
+      for (int p0 = 0; p0 < ex.world_size; p0 += 4) {  // 4 peers' lines in flight at a time
+        unsigned long long v[4][4 * C::NQ];
+        bool ready;
+        do {  // every retry re-reads the whole batch: one round trip per poll, not one per line
+          ready = true;
 #pragma unroll
-        for (int q = 0; q < C::NQ; ++q)
-          sum[q] += (p == ex.rank) ? pk[q] : *reinterpret_cast<const f32x4*>(src + (q * 64 + l) * 4);
+          for (int j = 0; j < 4; ++j) {
+            const int p = p0 + j;
+            if (p < ex.world_size && p != ex.rank) {
+              const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, p) + wofs;
+#pragma unroll
+              for (int k = 0; k < 4 * C::NQ; ++k) v[j][k] = ll_get(src + (k >> 1) * 256 + (k & 1) * 2);
+            }
+          }
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int p = p0 + j;
+            if (p < ex.world_size && p != ex.rank) {
+#pragma unroll
+              for (int k = 0; k < 4 * C::NQ; ++k) ready = ready && ll_ok(v[j][k], tag);
+            }
+          }
+          if (!ready && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
+        } while (!ready && !late);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int p = p0 + j;
+          if (p >= ex.world_size) continue;
+          if (p == ex.rank) {
+#pragma unroll
+            for (int q = 0; q < C::NQ; ++q) sum[q] += pk[q];
+          } else {
+#pragma unroll
+            for (int q = 0; q < C::NQ; ++q)
+              sum[q] += f32x4{ll_val(v[j][4 * q]), ll_val(v[j][4 * q + 1]), ll_val(v[j][4 * q + 2]),
+                              ll_val(v[j][4 * q + 3])};
+          }
+        }
       }
+      if (late) sm.err = 1;
 #pragma unroll
       for (int q = 0; q < C::NQ; ++q) {
 #pragma unroll

@@ -6,10 +6,11 @@ peers' writes land in HBM and are read without stale cache lines), exports it wi
 handles travel over the already-initialised process group (``all_gather_object``), so no extra
 rendezvous is needed.
 
-Buffer layout (bytes):  [ data : float[2][8][stride] ][ flags : uint32[64 blocks][2][8] ]
-
-A channel carries a monotonically increasing sequence number per exchange; the kernels poll
-``flag >= seq + 1`` so buffers are zeroed only once, at creation.
+Buffer layout: LL lines ``[2 parity][8 src ranks][stride / 2]`` of 16 bytes; a line carries two
+``{payload float, tag}`` pairs (``csrc/dgt_common.h``), so ``stride`` payload floats take
+``8 * stride`` bytes per slot.  A channel carries a monotonically increasing sequence number per
+exchange and the tag of exchange ``seq`` is ``seq + 1``; a reader polls its own mailbox until
+every line carries the expected tag.  No flags and no fences: the tag travels with the data.
 
 Before the channel is trusted, ``selftest`` runs a one-shot all-reduce with a bounded spin and
 compares it against the process group's own all-reduce (RCCL).  Any mismatch or timeout on any
@@ -26,7 +27,6 @@ from ..ops._ext import require
 from . import comm
 
 MAX_RANKS = 8
-MAX_BLOCKS = 64
 TICKS_PER_SECOND = 100_000_000  # s_memrealtime runs at 100 MHz
 
 
@@ -41,10 +41,8 @@ class IpcChannel:
         self.world_size = comm.get_world_size()
         if self.world_size > MAX_RANKS:
             raise ValueError(f"one-shot exchange supports up to {MAX_RANKS} ranks (one xGMI hop)")
-        self.stride = (int(stride_floats) + 63) // 64 * 64
-        self.data_bytes = 2 * MAX_RANKS * self.stride * 4
-        self.flag_bytes = MAX_BLOCKS * 2 * MAX_RANKS * 4
-        self.nbytes = self.data_bytes + self.flag_bytes
+        self.stride = (int(stride_floats) + 255) // 256 * 256
+        self.nbytes = 2 * MAX_RANKS * self.stride * 8
         self.timeout_ticks = int(timeout_s * TICKS_PER_SECOND)
         self.seq = 0
         self.local_ptr = 0
@@ -76,7 +74,6 @@ class IpcChannel:
         # every rank agrees on usability before anybody launches a kernel that waits on peers
         self.healthy = comm.all_reduce_max(0.0 if self.error is None else 1.0) == 0.0
         self.data_ptrs = list(self.base_ptrs) if self.healthy else []
-        self.flag_ptrs = [p + self.data_bytes for p in self.base_ptrs] if self.healthy else []
 
     # ------------------------------------------------------------------ one-shot all-reduce
     def next_seq(self, n: int = 1) -> int:
@@ -84,10 +81,15 @@ class IpcChannel:
         self.seq += n
         return s
 
-    def allreduce(self, inp: torch.Tensor, out: Optional[torch.Tensor] = None, scale: float = 1.0) -> torch.Tensor:
+    def allreduce(self, inp: torch.Tensor, out: Optional[torch.Tensor] = None, scale: float = 1.0,
+                  reps: int = 1) -> torch.Tensor:
+        """out = scale * sum over ranks of inp.  ``reps > 1`` repeats the all-reduce back to back
+        inside one launch (latency measurement; needs ``out`` distinct from ``inp``)."""
         out = inp if out is None else out
-        self.ops.oneshot_allreduce(inp, out, float(scale), self.data_ptrs, self.flag_ptrs, self.rank,
-                                   self.world_size, self.stride, self.next_seq(), self.timeout_ticks, self.status)
+        if reps > 1 and out.data_ptr() == inp.data_ptr():
+            raise ValueError("repeated one-shot all-reduce needs out != inp")
+        self.ops.oneshot_allreduce(inp, out, float(scale), self.data_ptrs, self.rank, self.world_size,
+                                   self.stride, self.next_seq(reps), self.timeout_ticks, self.status, int(reps))
         return out
 
     def check_status(self) -> int:

@@ -187,7 +187,7 @@ class TinyMLPTrainer:
             ops.tiny_mlp_train(self.x, self.y, plan, counts, self.params, self.exp_avg, self.exp_avg_sq,
                                self.loss_acc, self.status, self.F, self.H, self.lr, self.betas[0], self.betas[1],
                                self.eps, self.weight_decay, self.adamw, self.global_steps,
-                               ch.data_ptrs if ch else [], ch.flag_ptrs if ch else [], self.rank,
+                               ch.data_ptrs if ch else [], self.rank,
                                self.world_size, ch.stride if ch else 0, seq,
                                ch.timeout_ticks if ch else 0)
             self.global_steps += n

@@ -1,7 +1,7 @@
 """GPU multi-rank rehearsal on ONE MI355X: 2 ranks share the card over gloo, exercising the IPC
 mailboxes (hipIpcGetMemHandle / hipIpcOpenMemHandle across processes) and the in-kernel one-shot
 gradient exchange of the fused trainer.  The 8-GPU xGMI run happens only in the driver's scaling
-bench; these tests pin the protocol (flags, parities, rank-order sums) on real hardware."""
+bench; these tests pin the protocol (LL tags, parities, rank-order sums) on real hardware."""
 import os
 import re
 import subprocess
@@ -58,3 +58,15 @@ def test_bench_two_ranks_one_gpu():
     assert out["n_gpus"] == 2 and out["params_consistent_across_ranks"] is True
     assert out["config"]["exchange"] == "ipc-oneshot-xgmi"
     print(line)
+
+
+def test_oneshot_sweep_two_ranks_one_gpu():
+    """The standalone LL one-shot all-reduce at every sweep size (64 B .. 1 MiB) gives exact sums."""
+    r = run(2, "bench.py", "--gpus", "2", "--steps", "200", "--warmup", "20")
+    assert r.returncode == 0, r.stderr[-4000:]
+    import json
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    sweep = out["oneshot_xgmi_sweep"]
+    assert sweep and sweep[-1]["bytes"] == 1024 * 1024
+    assert all(row["correct"] for row in sweep), sweep
+    print(json.dumps(sweep))
