@@ -242,7 +242,8 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
 
 void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
-             const std::optional<at::Tensor>& mask, int64_t epi, double alpha) {
+             const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant) {
+  TORCH_CHECK(variant >= 0 && variant <= 2, "dgt: gemm_nt variant must be 0 (auto), 1 (128x128) or 2 (256x256)");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {  // rows may be strided (column blocks of a wider matrix)
@@ -288,7 +289,9 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
     g.ldmask = (int)N;
   }
   c10::DeviceGuard guard(A.device());
-  DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A)));
+  if (variant == 2)
+    TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
+  DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A), (int)variant));
 }
 
 void transpose_bf16(const at::Tensor& in, const at::Tensor& out) {
@@ -418,7 +421,7 @@ TORCH_LIBRARY(dgt, m) {
       &oneshot_allreduce);
   m.def(
       "gemm_nt(Tensor A, Tensor B, Tensor(a!)? C, Tensor(b!)? CT, Tensor? bias, Tensor? mask, int epi, "
-      "float alpha) -> ()",
+      "float alpha, int variant=0) -> ()",
       &gemm_nt);
   m.def("transpose_bf16(Tensor inp, Tensor(a!) out) -> ()", &transpose_bf16);
   m.def("rowsum_bf16(Tensor inp, Tensor(a!) out, bool accumulate) -> ()", &rowsum_bf16);

@@ -105,7 +105,7 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   float alpha;
 };
 
-hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream);
+hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream, int variant = 0);
 hipError_t transpose_bf16(const void* in, void* out, int rows, int cols, hipStream_t stream);
 hipError_t rowsum_bf16(const void* in, float* out, int rows, int cols, int accumulate, hipStream_t stream);
 

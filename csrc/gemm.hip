@@ -53,19 +53,58 @@ DGT_DEVICE bf16x8 read_frag(const u16* lds, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds + row * GBK + p * 8);
 }
 
+// One MFMA accumulator (rows mb..mb+3 of column n) through the fused epilogue.
+template <int EPI>
+DGT_DEVICE void epi_store(const GemmArgs& g, const f32x4& acc, int mb, int n) {
+  const float bn = (EPI & kEpiBias) ? g.bias[n] : 0.f;
+  const u16* mask = static_cast<const u16*>(g.mask);
+  float v[4];
+#pragma unroll
+  for (int rr = 0; rr < 4; ++rr) {
+    float x = acc[rr] * g.alpha + bn;
+    if (EPI & kEpiRelu) x = fmaxf(x, 0.f);
+    if (EPI & kEpiMask) x = bf2f(mask[(long long)(mb + rr) * g.ldmask + n]) > 0.f ? x : 0.f;
+    v[rr] = x;
+  }
+  if (EPI & kEpiOutF32) {
+    float* C = static_cast<float*>(g.C);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) {
+      float* p = C + (long long)(mb + rr) * g.ldc + n;
+      *p = (EPI & kEpiAccumulate) ? *p + v[rr] : v[rr];
+    }
+  } else if (g.C) {
+    u16* C = static_cast<u16*>(g.C);
+#pragma unroll
+    for (int rr = 0; rr < 4; ++rr) C[(long long)(mb + rr) * g.ldc + n] = f2bf(v[rr]);
+  }
+  if (EPI & kEpiStoreT) {  // C^T[n][m..m+3]: 4 consecutive bf16 per lane
+    u16* CT = static_cast<u16*>(g.CT);
+    uint2 packed;
+    packed.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
+    packed.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
+    *reinterpret_cast<uint2*>(CT + (long long)n * g.ldct + mb) = packed;
+  }
+}
+
+// XCD-aware bijective block remap (T1): blocks b and b+8 share an XCD; give each XCD a contiguous
+// range of tile ids, then group GROUP block-rows so consecutive ids reuse the same B panel in L2.
+DGT_DEVICE void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
+  const int nwg = nbm * nbn, xcd = bid % 8, q = nwg / 8, r = nwg % 8;
+  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
+  const int GROUP = 8;
+  const int group = wgid / (GROUP * nbn), first_m = group * GROUP;
+  const int gsize = min(nbm - first_m, GROUP);
+  tm = first_m + (wgid % (GROUP * nbn)) % gsize;
+  tn = (wgid % (GROUP * nbn)) / gsize;
+}
+
 template <int EPI>
 __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) u16 lds[2][2][GBM * GBK];  // [stage][A|B] = 64 KiB
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
-  const int nbm = g.M / GBM, nbn = g.N / GBN, nwg = nbm * nbn;
-  // XCD-aware bijective remap: blocks b and b+8 share an XCD; give each XCD a contiguous range
-  const int bid = blockIdx.x, xcd = bid % 8, q = nwg / 8, r = nwg % 8;
-  const int wgid = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
-  // group 8 block-rows together so consecutive wgids reuse the same B panel from L2
-  const int GROUP = 8;
-  const int group = wgid / (GROUP * nbn), first_m = group * GROUP;
-  const int gsize = min(nbm - first_m, GROUP);
-  const int tm = first_m + (wgid % (GROUP * nbn)) % gsize, tn = (wgid % (GROUP * nbn)) / gsize;
+  int tm, tn;
+  tile_of_block(blockIdx.x, g.M / GBM, g.N / GBN, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int wr = w >> 1, wc = w & 1;
   const u16* A = static_cast<const u16*>(g.A);
@@ -109,52 +148,234 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
   }
 
   // ---- epilogue: D col = l&15 (n), row = 4*(l>>4) + r (m)
-  const float* bias = g.bias;
-  const u16* mask = static_cast<const u16*>(g.mask);
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int n = n0 + wc * 64 + j * 16 + (l & 15);
-      const int mb = m0 + wr * 64 + i * 16 + 4 * (l >> 4);
-      const float bn = (EPI & kEpiBias) ? bias[n] : 0.f;
-      float v[4];
-#pragma unroll
-      for (int rr = 0; rr < 4; ++rr) {
-        float x = acc[i][j][rr] * g.alpha + bn;
-        if (EPI & kEpiRelu) x = fmaxf(x, 0.f);
-        if (EPI & kEpiMask) x = bf2f(mask[(long long)(mb + rr) * g.ldmask + n]) > 0.f ? x : 0.f;
-        v[rr] = x;
-      }
-      if (EPI & kEpiOutF32) {
-        float* C = static_cast<float*>(g.C);
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) {
-          float* p = C + (long long)(mb + rr) * g.ldc + n;
-          *p = (EPI & kEpiAccumulate) ? *p + v[rr] : v[rr];
-        }
-      } else if (g.C) {
-        u16* C = static_cast<u16*>(g.C);
-#pragma unroll
-        for (int rr = 0; rr < 4; ++rr) C[(long long)(mb + rr) * g.ldc + n] = f2bf(v[rr]);
-      }
-      if (EPI & kEpiStoreT) {  // C^T[n][m..m+3]: 4 consecutive bf16 per lane
-        u16* CT = static_cast<u16*>(g.CT);
-        uint2 packed;
-        packed.x = (unsigned)f2bf(v[0]) | ((unsigned)f2bf(v[1]) << 16);
-        packed.y = (unsigned)f2bf(v[2]) | ((unsigned)f2bf(v[3]) << 16);
-        *reinterpret_cast<uint2*>(CT + (long long)n * g.ldct + mb) = packed;
-      }
-    }
-  }
+    for (int j = 0; j < 4; ++j)
+      epi_store<EPI>(g, acc[i][j], m0 + wr * 64 + i * 16 + 4 * (l >> 4), n0 + wc * 64 + j * 16 + (l & 15));
 }
 
-hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream) {
+// ------------------------------------------------------------------ 256 x 256 tile, 8-phase pipeline
+// For large M x N (>= ~200 tiles): 512 threads = 8 waves in 2 (M) x 4 (N), each wave 128 x 64 =
+// 8 x 4 accumulators of 16x16 (128 VGPRs).  A K-tile (BK = 64) of A and of B is staged as four
+// 16 KiB "units" of 128 rows, split so that each unit is read in exactly ONE phase:
+//   A_lo: block rows with (row % 128) < 64    read in phase q0 (rows 0..63 of every wave)
+//   A_hi: block rows with (row % 128) >= 64   read in phase q2
+//   B_lo: block cols with (col % 64) < 32     read in phase q0
+//   B_hi: block cols with (col % 64) >= 32    read in phase q1
+// A K-tile is consumed in four phases, one output quadrant (64 x 32 per wave, 16 MFMAs) each:
+//   q0: A_lo x B_lo (reads A_lo, B_lo)   q1: A_lo x B_hi (reads B_hi)
+//   q2: A_hi x B_hi (reads A_hi)         q3: A_hi x B_lo (no reads)
+// Two LDS buffers (even / odd K-tile) = 128 KiB; one loop iteration = 8 phases = 2 K-tiles.  Each
+// phase issues ONE unit of staging (2 global_load_lds per thread), its LDS reads, then
+// `s_waitcnt vmcnt(10)` (every unit but the 5 newest has landed), barrier, MFMAs, barrier.  The
+// unit order below restages a unit at least one phase after its last read (WAR) and reads it at
+// least one phase after the wait that retires it (RAW), so loads stay in flight across 5 phases
+// and never drain in the main loop (cdna_hip_programming.md §5, "8-phase template").
+namespace g256 {
+constexpr int BM = 256, BN = 256, BK = 64, UNIT = 128 * BK;  // elements per unit
+enum Unit { kALo = 0, kAHi = 1, kBLo = 2, kBHi = 3 };
+
+// LDS row u of a unit holds global chunk c at slot c ^ ((u >> 1) & 7): a 16-lane group reading 16
+// consecutive rows at one chunk then touches 16 distinct 16-byte bank slots (conflict-free).
+DGT_DEVICE int swz(int u, int c) { return c ^ ((u >> 1) & 7); }
+
+// Per-lane staging offsets (elements, 32-bit) for the two glds of a unit; the unit/tile part of
+// the address is wave-uniform and added to the base pointer, so each glds needs one VGPR.
+//   A units: unit row u -> block row (u >> 6) * 128 + (u & 63) (+64 for A_hi)
+//   B units: unit row u -> block col (u >> 5) * 64 + (u & 31)  (+32 for B_hi)
+DGT_DEVICE int lane_off(bool is_a, int ld, int w, int i, int l) {
+  const int u = (w * 2 + i) * 8 + (l >> 3);
+  const int row = is_a ? (u >> 6) * 128 + (u & 63) : (u >> 5) * 64 + (u & 31);
+  return row * ld + swz(u, l & 7) * 8;
+}
+
+DGT_DEVICE void stage(const u16* ubase, const int (&off)[2], u16* unit_lds, int w) {
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(ubase + off[i]),
+                                     reinterpret_cast<int*>(unit_lds + (w * 2 + i) * 8 * BK), 16, 0, 0);
+}
+
+DGT_DEVICE bf16x8 frag(const u16* unit_lds, int u, int c) {
+  return *reinterpret_cast<const bf16x8*>(unit_lds + u * BK + swz(u, c) * 8);
+}
+
+// s_waitcnt with only the vector-memory count constrained (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4]
+// << 14, expcnt[6:4] = 7 and lgkmcnt[11:8] = 15 mean "don't wait")
+template <int N>
+DGT_DEVICE void wait_vm() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+DGT_DEVICE void wait_lgkm0() { __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4)); }
+
+struct Frags {
+  bf16x8 a[4][2];    // the wave's current 64 A rows x K 64 (lo or hi half)
+  bf16x8 blo[2][2];  // 32 B columns x K 64
+  bf16x8 bhi[2][2];
+};
+
+struct Ctx {
+  const u16* A;      // block's A panel: A + m0 * lda
+  const u16* B;      // block's B panel: B + n0 * ldb
+  int lda, ldb, w, l, wr, wc;
+  int offa[2], offb[2];
+  u16* lds;
+};
+
+template <int U>
+DGT_DEVICE void stage_unit(const Ctx& c, int kt, int buf) {
+  const bool is_a = (U == kALo || U == kAHi);
+  const u16* ubase = is_a ? c.A + (U == kAHi ? 64 * c.lda : 0) + kt * BK
+                          : c.B + (U == kBHi ? 32 * c.ldb : 0) + kt * BK;
+  stage(ubase, is_a ? c.offa : c.offb, c.lds + (buf * 4 + U) * UNIT, c.w);
+}
+
+// unit staged in phase P (1..8) of an iteration: ph1 -> the odd tile's A_hi; ph2..5 -> the next
+// even tile; ph6..8 -> the next odd tile's A_lo, B_lo, B_hi
+template <int P>
+DGT_DEVICE void stage_phase(const Ctx& c, int it) {
+  constexpr int unit = P == 1 ? kAHi : P == 2 ? kALo : P == 3 ? kBLo : P == 4 ? kBHi : P == 5 ? kAHi
+                     : P == 6 ? kALo : P == 7 ? kBLo : kBHi;
+  constexpr int buf = (P == 1 || P >= 6) ? 1 : 0;
+  const int kt = P == 1 ? 2 * it + 1 : (P <= 5 ? 2 * it + 2 : 2 * it + 3);
+  stage_unit<unit>(c, kt, buf);
+}
+
+template <int P, bool LAST>
+DGT_DEVICE void phase(const Ctx& c, int it, Frags& f, f32x4 (&acc)[8][4]) {
+  constexpr int buf = P <= 4 ? 0 : 1;
+  constexpr int q = (P - 1) & 3;
+  const u16* base = c.lds + buf * 4 * UNIT;
+  const int lr = c.l & 15, lc = c.l >> 4;
+  if (!LAST || P == 1) stage_phase<P>(c, it);
+  if (q == 0 || q == 2) {
+    const u16* ul = base + (q == 0 ? kALo : kAHi) * UNIT;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) f.a[i][kk] = frag(ul, c.wr * 64 + i * 16 + lr, kk * 4 + lc);
+  }
+  if (q == 0 || q == 1) {
+    const u16* ul = base + (q == 0 ? kBLo : kBHi) * UNIT;
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        const bf16x8 v = frag(ul, c.wc * 32 + j * 16 + lr, kk * 4 + lc);
+        if (q == 0) f.blo[j][kk] = v;
+        else f.bhi[j][kk] = v;
+      }
+  }
+  // retire the unit read next phase (see the schedule above); the last iteration stages nothing
+  // after phase 1, so its counts shrink as the pipeline drains
+  if (!LAST) wait_vm<10>();
+  else wait_vm<P == 1 ? 10 : P == 2 ? 8 : P == 3 ? 6 : P == 4 ? 4 : P == 5 ? 2 : 0>();
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  wait_lgkm0();
+  __builtin_amdgcn_s_setprio(1);
+  constexpr int i0 = (q == 0 || q == 1) ? 0 : 4;
+  constexpr bool hi_b = (q == 1 || q == 2);
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 2; ++j)
+        acc[i0 + i][(hi_b ? 2 : 0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+            f.a[i][kk], hi_b ? f.bhi[j][kk] : f.blo[j][kk], acc[i0 + i][(hi_b ? 2 : 0) + j], 0, 0, 0);
+  __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool LAST>
+DGT_DEVICE void iteration(const Ctx& c, int it, Frags& f, f32x4 (&acc)[8][4]) {
+  phase<1, LAST>(c, it, f, acc);
+  phase<2, LAST>(c, it, f, acc);
+  phase<3, LAST>(c, it, f, acc);
+  phase<4, LAST>(c, it, f, acc);
+  phase<5, LAST>(c, it, f, acc);
+  phase<6, LAST>(c, it, f, acc);
+  phase<7, LAST>(c, it, f, acc);
+  phase<8, LAST>(c, it, f, acc);
+}
+}  // namespace g256
+
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
+  using namespace g256;
+  __shared__ __attribute__((aligned(16))) u16 lds[2 * 4 * UNIT];  // ONE array (no extra vmcnt(0) waits)
+  const int tid = threadIdx.x;
+  int tm, tn;
+  tile_of_block(blockIdx.x, g.M / BM, g.N / BN, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  Ctx c;
+  c.A = static_cast<const u16*>(g.A) + (long long)m0 * g.lda;
+  c.B = static_cast<const u16*>(g.B) + (long long)n0 * g.ldb;
+  c.lda = g.lda;
+  c.ldb = g.ldb;
+  c.w = tid >> 6;
+  c.l = tid & 63;
+  c.wr = c.w >> 2;
+  c.wc = c.w & 3;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    c.offa[i] = lane_off(true, g.lda, c.w, i, c.l);
+    c.offb[i] = lane_off(false, g.ldb, c.w, i, c.l);
+  }
+  c.lds = lds;
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  Frags f;
+
+  // prologue: the 7 units phases 2..8 of iteration "-1" would have staged (tile 0 whole, tile 1
+  // without A_hi), then the wait phase 8 would have done
+  stage_unit<kALo>(c, 0, 0);
+  stage_unit<kBLo>(c, 0, 0);
+  stage_unit<kBHi>(c, 0, 0);
+  stage_unit<kAHi>(c, 0, 0);
+  stage_unit<kALo>(c, 1, 1);
+  stage_unit<kBLo>(c, 1, 1);
+  stage_unit<kBHi>(c, 1, 1);
+  wait_vm<10>();
+  __builtin_amdgcn_s_barrier();
+
+  const int nit = g.K / (2 * BK);
+  for (int it = 0; it + 1 < nit; ++it) iteration<false>(c, it, f, acc);
+  iteration<true>(c, nit - 1, f, acc);
+
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      epi_store<EPI>(g, acc[i][j], m0 + c.wr * 128 + i * 16 + 4 * (c.l >> 4), n0 + c.wc * 64 + j * 16 + (c.l & 15));
+}
+
+// variant: 0 = pick by shape, 1 = 128x128 kernel, 2 = 256x256 8-phase kernel
+hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  const int grid = (g.M / GBM) * (g.N / GBN);
-#define DGT_EPI_CASE(E)                                                                   \
-  case E:                                                                                 \
-    hipLaunchKernelGGL((gemm_nt_kernel<E>), dim3(grid), dim3(256), 0, stream, g);         \
+  const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0;
+  // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks,
+  // 2 blocks per CU) wins
+  bool big = fits256 && (g.M / 256) * (g.N / 256) >= 200;
+  if (variant == 1) big = false;
+  if (variant == 2) {
+    if (!fits256) return hipErrorInvalidValue;
+    big = true;
+  }
+  const int grid = big ? (g.M / 256) * (g.N / 256) : (g.M / GBM) * (g.N / GBN);
+#define DGT_EPI_CASE(E)                                                                        \
+  case E:                                                                                      \
+    if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g); \
+    else hipLaunchKernelGGL((gemm_nt_kernel<E>), dim3(grid), dim3(256), 0, stream, g);         \
     break;
   switch (epi) {
     DGT_EPI_CASE(0)

@@ -33,6 +33,14 @@ def make_synthetic_data(n_samples: int = 200, n_features: int = 20, seed: int = 
     return x, y
 
 
+def get_dataloader(x: torch.Tensor, y: torch.Tensor, batch_size: int = 32, shuffle: bool = True):
+    """Plain host-side ``DataLoader`` over ``(x, y)``.  The reference defines this helper but never
+    calls it (``train.py:38-40``); it is kept for API parity.  The training paths use the
+    device-resident dataset and sampler plans below instead."""
+    from torch.utils.data import DataLoader, TensorDataset
+    return DataLoader(TensorDataset(x, y), batch_size=batch_size, shuffle=shuffle)
+
+
 def shard_indices(n: int, world_size: int, rank: int, epoch: int, seed: int = 0,
                   shuffle: bool = True, drop_last: bool = False) -> List[int]:
     """Indices rank ``rank`` sees in ``epoch`` — ``torch.utils.data.DistributedSampler``'s algorithm."""

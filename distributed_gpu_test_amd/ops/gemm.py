@@ -37,14 +37,15 @@ def gemm_nt_reference(A, B, C=None, CT=None, bias=None, mask=None, relu=False, o
 
 def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, CT: Optional[torch.Tensor] = None,
             bias: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, relu: bool = False,
-            out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0) -> None:
+            out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0) -> None:
+    """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles, 2 = 256x256 8-phase pipeline."""
     if not A.is_cuda:
         gemm_nt_reference(A, B, C, CT, bias, mask, relu, out_f32, accumulate, alpha)
         return
     epi = ((EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | (EPI_MASK if mask is not None else 0)
            | (EPI_STORE_T if CT is not None else 0) | (EPI_OUT_F32 if out_f32 else 0)
            | (EPI_ACCUMULATE if accumulate else 0))
-    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha))
+    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant))
 
 
 def transpose_bf16(inp: torch.Tensor, out: torch.Tensor) -> None:

@@ -36,9 +36,14 @@ def main():
         flops = 2.0 * M * N * K
         t_ours = bench(lambda: gemm_nt(A, B, C=C))
         t_ours32 = bench(lambda: gemm_nt(A, B, C=Cf, out_f32=True))
+        t_128 = bench(lambda: gemm_nt(A, B, C=C, variant=1))
+        fits256 = M % 256 == 0 and N % 256 == 0 and K % 128 == 0
+        t_256 = bench(lambda: gemm_nt(A, B, C=C, variant=2)) if fits256 else None
         t_torch = bench(lambda: torch.matmul(A, B.t(), out=C))
         print(json.dumps({"M": M, "N": N, "K": K, "dgt_TFLOPs": round(flops / t_ours / 1e12, 1),
                           "dgt_f32out_TFLOPs": round(flops / t_ours32 / 1e12, 1),
+                          "dgt_tile128_TFLOPs": round(flops / t_128 / 1e12, 1),
+                          "dgt_tile256_TFLOPs": round(flops / t_256 / 1e12, 1) if t_256 else None,
                           "torch_hipblaslt_TFLOPs": round(flops / t_torch / 1e12, 1),
                           "dgt_us": round(t_ours * 1e6, 1), "torch_us": round(t_torch * 1e6, 1)}), flush=True)
 

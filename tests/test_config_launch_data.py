@@ -140,3 +140,13 @@ def test_dataset_iteration():
     assert len(batches) == len(ds) == 7
     idx = shard_indices(50, 2, 1, 2)
     assert torch.equal(torch.cat([b[0] for b in batches]), x[idx])
+
+
+def test_get_dataloader_helper():
+    from distributed_gpu_test_amd.data import get_dataloader, make_synthetic_data
+    x, y = make_synthetic_data(100, 20, 42)
+    dl = get_dataloader(x, y, batch_size=32, shuffle=False)
+    bx, by = next(iter(dl))
+    assert bx.shape == (32, 20) and by.shape == (32, 1)
+    assert torch.equal(bx, x[:32])
+    assert sum(b[0].shape[0] for b in dl) == 100

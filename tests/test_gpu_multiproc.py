@@ -70,3 +70,13 @@ def test_oneshot_sweep_two_ranks_one_gpu():
     assert sweep and sweep[-1]["bytes"] == 1024 * 1024
     assert all(row["correct"] for row in sweep), sweep
     print(json.dumps(sweep))
+
+
+def test_engine_zero1_two_ranks_one_gpu(tmp_path):
+    """ZeRO-1 on HIP tensors: reduce-scatter into the shard, fused Adam on the shard, all-gather."""
+    r = run(2, "train.py", "--impl", "engine", "--deepspeed_config", os.path.join(ROOT, "configs", "ds_zero1.json"),
+            "--epochs", "2", "--save-dir", str(tmp_path))
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert losses(r.stdout) == ORACLE2[:2]
+    tag = tmp_path / "epoch2" / "global_step500"
+    assert (tag / "zero_pp_rank_1_mp_rank_00_optim_states.pt").exists()

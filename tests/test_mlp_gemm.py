@@ -50,9 +50,10 @@ gpu = pytest.mark.gpu
 
 
 @gpu
-@pytest.mark.parametrize("M,N,K", [(128, 128, 64), (256, 384, 128), (512, 256, 1024)])
+@pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 1), (512, 256, 1024, 1),
+                                           (256, 256, 128, 2), (512, 768, 256, 2), (768, 512, 1152, 2)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "mask_T", "f32", "f32_acc"])
-def test_gemm_nt_matches_reference(M, N, K, epi):
+def test_gemm_nt_matches_reference(M, N, K, variant, epi):
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
     B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
@@ -67,7 +68,7 @@ def test_gemm_nt_matches_reference(M, N, K, epi):
     C = (torch.randn(M, N, generator=g) if f32 else torch.zeros(M, N)).cuda().to(torch.float32 if f32 else torch.bfloat16)
     C0 = C.clone()
     CT = torch.zeros(N, M, dtype=torch.bfloat16).cuda() if epi.endswith("_T") else None
-    gemm_nt(A, B, C=C, CT=CT, out_f32=f32, accumulate=epi == "f32_acc", **kw)
+    gemm_nt(A, B, C=C, CT=CT, out_f32=f32, accumulate=epi == "f32_acc", variant=variant, **kw)
     ref = gemm_nt_reference(A.cpu(), B.cpu(), **{k: (v.cpu() if torch.is_tensor(v) else v)
                                                   for k, v in kw.items()}).cuda()
     if epi == "f32_acc":
@@ -79,14 +80,31 @@ def test_gemm_nt_matches_reference(M, N, K, epi):
 
 
 @gpu
-def test_gemm_identity_with_asymmetric_operand():
+@pytest.mark.parametrize("n,variant", [(128, 1), (256, 2)])
+def test_gemm_identity_with_asymmetric_operand(n, variant):
     # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
-    M = N = K = 128
+    M = N = K = n
     A = torch.eye(M, dtype=torch.bfloat16).cuda()
     B = torch.arange(N * K, dtype=torch.float32).remainder(251).reshape(N, K).to(torch.bfloat16).cuda()
     C = torch.empty(M, N, dtype=torch.float32).cuda()
-    gemm_nt(A, B, C=C, out_f32=True)
+    gemm_nt(A, B, C=C, out_f32=True, variant=variant)
     torch.testing.assert_close(C, B.float().t())
+
+
+@gpu
+def test_gemm_256_large_k_repeated():
+    """The pipelined kernel over many K-tiles and a full wave of blocks, several launches: staging
+    races show up as rare wrong tiles, so compare every launch with an fp32 reference."""
+    M, N, K = 2048, 4096, 2048
+    g = torch.Generator().manual_seed(7)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
+    ref = A.float() @ B.float().t()
+    C = torch.empty(M, N, dtype=torch.float32).cuda()
+    for _ in range(5):
+        C.fill_(float("nan"))
+        gemm_nt(A, B, C=C, out_f32=True, variant=2)
+        torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
 
 
 @gpu
