@@ -1,22 +1,40 @@
 // Flat fused Adam/AdamW: ONE launch over the engine's flat fp32 master buffer replaces torch's
 // seven _foreach_* multi-tensor launches plus the DeepSpeed 1/world_size scale and the host-side
 // bias-correction .item() syncs.  Memory-bound: 16-byte vector accesses on
-// every stream (Guideline 13), grid capped near 8 blocks/CU with a grid-stride loop.
+// every stream (Guideline 13), nontemporal hints (each byte is touched once), one float4 group per
+// thread over a full grid: 6.1 TB/s on the bench MLP's 67M parameters (scripts/bench_adam.py).
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include "dgt_common.h"
 #include "dgt_kernels.h"
+#include <algorithm>
+#include <cstdlib>
 
 namespace dgt {
 
-template <typename T> struct Vec4;
-template <> struct Vec4<float> {
-  static DGT_DEVICE f32x4 load(const float* p) { return *reinterpret_cast<const f32x4*>(p); }
-  static DGT_DEVICE void store(float* p, f32x4 v) { *reinterpret_cast<f32x4*>(p) = v; }
+typedef unsigned u32x2 __attribute__((ext_vector_type(2)));
+
+// 16-byte (fp32) / 8-byte (16-bit) vector accesses; NT = streaming (nontemporal) hint: every
+// element is touched exactly once, so nothing is worth keeping in L2 / MALL.
+template <bool NT, typename V>
+DGT_DEVICE V vload(const V* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(p);
+  else return *p;
+}
+template <bool NT, typename V>
+DGT_DEVICE void vstore(V* p, V v) {
+  if constexpr (NT) __builtin_nontemporal_store(v, p);
+  else *p = v;
+}
+
+template <typename T, bool NT> struct Vec4;
+template <bool NT> struct Vec4<float, NT> {
+  static DGT_DEVICE f32x4 load(const float* p) { return vload<NT>(reinterpret_cast<const f32x4*>(p)); }
+  static DGT_DEVICE void store(float* p, f32x4 v) { vstore<NT>(reinterpret_cast<f32x4*>(p), v); }
 };
-template <> struct Vec4<__hip_bfloat16> {
+template <bool NT> struct Vec4<__hip_bfloat16, NT> {
   static DGT_DEVICE f32x4 load(const __hip_bfloat16* p) {
-    const uint2 raw = *reinterpret_cast<const uint2*>(p);
+    const u32x2 raw = vload<NT>(reinterpret_cast<const u32x2*>(p));
     f32x4 r;
     r[0] = __uint_as_float(raw.x << 16);
     r[1] = __uint_as_float(raw.x & 0xffff0000u);
@@ -28,12 +46,12 @@ template <> struct Vec4<__hip_bfloat16> {
     __hip_bfloat16 b[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = __float2bfloat16(v[i]);
-    *reinterpret_cast<uint2*>(p) = *reinterpret_cast<uint2*>(b);
+    vstore<NT>(reinterpret_cast<u32x2*>(p), *reinterpret_cast<u32x2*>(b));
   }
 };
-template <> struct Vec4<__half> {
+template <bool NT> struct Vec4<__half, NT> {
   static DGT_DEVICE f32x4 load(const __half* p) {
-    const uint2 raw = *reinterpret_cast<const uint2*>(p);
+    const u32x2 raw = vload<NT>(reinterpret_cast<const u32x2*>(p));
     const __half* h = reinterpret_cast<const __half*>(&raw);
     f32x4 r;
 #pragma unroll
@@ -44,11 +62,30 @@ template <> struct Vec4<__half> {
     __half b[4];
 #pragma unroll
     for (int i = 0; i < 4; ++i) b[i] = __float2half(v[i]);
-    *reinterpret_cast<uint2*>(p) = *reinterpret_cast<uint2*>(b);
+    vstore<NT>(reinterpret_cast<u32x2*>(p), *reinterpret_cast<u32x2*>(b));
   }
 };
 
-template <typename GT, typename LT>
+template <typename GT, typename LT, bool NT>
+DGT_DEVICE void adam_group(const AdamFlatArgs& a, const GT* __restrict__ grad, LT* __restrict__ lp, long long o,
+                           float scale, float step_size_neg, float bc2_sqrt) {
+  f32x4 p = Vec4<float, NT>::load(a.master + o), g = Vec4<GT, NT>::load(grad + o);
+  f32x4 m = Vec4<float, NT>::load(a.exp_avg + o), v = Vec4<float, NT>::load(a.exp_avg_sq + o);
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    float mm = m[e], vv = v[e];
+    p[e] = adam_update(p[e], g[e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
+    m[e] = mm;
+    v[e] = vv;
+  }
+  Vec4<float, NT>::store(a.master + o, p);
+  Vec4<float, NT>::store(a.exp_avg + o, m);
+  Vec4<float, NT>::store(a.exp_avg_sq + o, v);
+  if (lp) Vec4<LT, NT>::store(lp + o, p);
+}
+
+// GROUPS float4 groups per thread per grid-stride iteration
+template <typename GT, typename LT, bool NT, int GROUPS>
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   const long long n4 = a.n >> 2;
   float step_size_neg = a.step_size_neg, bc2_sqrt = a.bc2_sqrt;
@@ -67,56 +104,53 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   if (a.grad_scale_dev) scale *= *a.grad_scale_dev;
   const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
   LT* __restrict__ lp = static_cast<LT*>(a.param_lp);
-  // two float4 groups per thread per iteration: 8 independent 16-byte loads in flight per lane
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += 2 * stride) {
-    const bool two = i + stride < n4;
-    const long long o0 = 4 * i, o1 = 4 * (i + stride);
-    f32x4 p0 = Vec4<float>::load(a.master + o0), g0 = Vec4<GT>::load(grad + o0);
-    f32x4 m0 = Vec4<float>::load(a.exp_avg + o0), v0 = Vec4<float>::load(a.exp_avg_sq + o0);
-    f32x4 p1, g1, m1, v1;
-    if (two) {
-      p1 = Vec4<float>::load(a.master + o1);
-      g1 = Vec4<GT>::load(grad + o1);
-      m1 = Vec4<float>::load(a.exp_avg + o1);
-      v1 = Vec4<float>::load(a.exp_avg_sq + o1);
-    }
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += GROUPS * stride) {
 #pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float mm = m0[e], vv = v0[e];
-      p0[e] = adam_update(p0[e], g0[e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
-      m0[e] = mm;
-      v0[e] = vv;
-    }
-    Vec4<float>::store(a.master + o0, p0);
-    Vec4<float>::store(a.exp_avg + o0, m0);
-    Vec4<float>::store(a.exp_avg_sq + o0, v0);
-    if (lp) Vec4<LT>::store(lp + o0, p0);
-    if (two) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        float mm = m1[e], vv = v1[e];
-        p1[e] = adam_update(p1[e], g1[e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
-        m1[e] = mm;
-        v1[e] = vv;
-      }
-      Vec4<float>::store(a.master + o1, p1);
-      Vec4<float>::store(a.exp_avg + o1, m1);
-      Vec4<float>::store(a.exp_avg_sq + o1, v1);
-      if (lp) Vec4<LT>::store(lp + o1, p1);
-    }
+    for (int gi = 0; gi < GROUPS; ++gi)
+      if (gi == 0 || i + gi * stride < n4)
+        adam_group<GT, LT, NT>(a, grad, lp, 4 * (i + gi * stride), scale, step_size_neg, bc2_sqrt);
+  }
+}
+
+// loop shape chosen by measurement (scripts/bench_adam.py); DGT_ADAM_VARIANT overrides it for A/B runs
+static int adam_variant() {
+  const char* e = getenv("DGT_ADAM_VARIANT");
+  return e ? atoi(e) : 0;
+}
+
+template <typename GT, typename LT>
+static void launch_adam_v(const AdamFlatArgs& a, hipStream_t s) {
+  const long long n4 = a.n / 4;
+  long long grid;
+  switch (adam_variant()) {
+    case 1:  // two groups per thread, plain, capped grid
+      grid = std::min<long long>(std::max<long long>((n4 + 511) / 512, 1), 4096);
+      hipLaunchKernelGGL((adam_flat_kernel<GT, LT, false, 2>), dim3((int)grid), dim3(256), 0, s, a);
+      break;
+    case 2:  // two groups, streaming hints, capped grid
+      grid = std::min<long long>(std::max<long long>((n4 + 511) / 512, 1), 4096);
+      hipLaunchKernelGGL((adam_flat_kernel<GT, LT, true, 2>), dim3((int)grid), dim3(256), 0, s, a);
+      break;
+    case 3:  // one group per thread, plain, full grid
+      grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);
+      hipLaunchKernelGGL((adam_flat_kernel<GT, LT, false, 1>), dim3((int)grid), dim3(256), 0, s, a);
+      break;
+    default:  // one group per thread, streaming hints, full grid: 6.1 TB/s at 67M params
+      grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);
+      hipLaunchKernelGGL((adam_flat_kernel<GT, LT, true, 1>), dim3((int)grid), dim3(256), 0, s, a);
   }
 }
 
 template <typename GT>
-static hipError_t launch_adam_g(const AdamFlatArgs& a, hipStream_t s, int grid) {
+static hipError_t launch_adam_g(const AdamFlatArgs& a, hipStream_t s) {
   switch (a.param_lp ? a.lp_dtype : kF32) {
-    case kBF16: hipLaunchKernelGGL((adam_flat_kernel<GT, __hip_bfloat16>), dim3(grid), dim3(256), 0, s, a); break;
-    case kF16: hipLaunchKernelGGL((adam_flat_kernel<GT, __half>), dim3(grid), dim3(256), 0, s, a); break;
+    case kBF16: launch_adam_v<GT, __hip_bfloat16>(a, s); break;
+    case kF16: launch_adam_v<GT, __half>(a, s); break;
     default: {
       AdamFlatArgs b = a;
       b.param_lp = nullptr;  // fp32 params are the master buffer itself
-      hipLaunchKernelGGL((adam_flat_kernel<GT, float>), dim3(grid), dim3(256), 0, s, b);
+      launch_adam_v<GT, float>(b, s);
     }
   }
   return hipGetLastError();
@@ -131,14 +165,10 @@ hipError_t step_increment(long long* counter, hipStream_t stream) {
 
 hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream) {
   if (a.n % 4 != 0) return hipErrorInvalidValue;
-  const long long n4 = a.n / 4;
-  long long grid = (n4 + 511) / 512;
-  if (grid > 4096) grid = 4096;  // 16 blocks per CU: enough loads in flight to stream HBM
-  if (grid < 1) grid = 1;
   switch (a.grad_dtype) {
-    case kBF16: return launch_adam_g<__hip_bfloat16>(a, stream, (int)grid);
-    case kF16: return launch_adam_g<__half>(a, stream, (int)grid);
-    default: return launch_adam_g<float>(a, stream, (int)grid);
+    case kBF16: return launch_adam_g<__hip_bfloat16>(a, stream);
+    case kF16: return launch_adam_g<__half>(a, stream);
+    default: return launch_adam_g<float>(a, stream);
   }
 }
 

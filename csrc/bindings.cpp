@@ -238,12 +238,15 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
   check_gpu(t, name, dt);
   TORCH_CHECK(t.dim() == 2 && t.size(0) == r && t.size(1) == c, "dgt: ", name, " must be [", r, ", ", c, "], got ",
               t.sizes());
+  // the kernels move whole 16-byte rows pieces (staged GEMM epilogue, vector loads)
+  TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "dgt: ", name, " must be 16-byte aligned");
 }
 
 void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant) {
-  TORCH_CHECK(variant >= 0 && variant <= 2, "dgt: gemm_nt variant must be 0 (auto), 1 (128x128) or 2 (256x256)");
+  TORCH_CHECK(variant >= 0 && variant <= 3,
+              "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256) or 3 (128x128, 4 stages)");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {  // rows may be strided (column blocks of a wider matrix)

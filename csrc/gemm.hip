@@ -99,9 +99,85 @@ DGT_DEVICE void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
   tn = (wgid % (GROUP * nbn)) / gsize;
 }
 
+// bf16-output epilogue of the 128 x 128 kernel, staged through the (then idle) operand LDS: the
+// MFMA layout gives each lane 4 rows of ONE column, so direct stores are 2-byte scatters; staged,
+// every global access (C rows, C^T rows, mask rows) is a 16-byte vector and 16 lanes cover one
+// 256-byte row piece.  The tile's 16-byte chunks are XOR-swizzled by row / 8, so both the row reads
+// (C) and the column reads (C^T: 16 lanes at rows 8k + e of one column) hit 16 distinct bank groups.
+// Values are rounded to bf16 once (after bias / ReLU) and masked after rounding (identical results:
+// the mask only zeroes).
+DGT_DEVICE int etile(int r, int n) { return r * 128 + ((((n >> 3) ^ (r >> 3)) & 15) << 3) + (n & 7); }
+
 template <int EPI>
-__global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) u16 lds[2][2][GBM * GBK];  // [stage][A|B] = 64 KiB
+DGT_DEVICE void epilogue_staged_128(const GemmArgs& g, const f32x4 (&acc)[4][4], u16* tile, int m0, int n0, int wr,
+                                    int wc, int l, int tid) {
+  __syncthreads();  // every wave has finished reading the operand stages
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int nl = wc * 64 + j * 16 + (l & 15);
+    const float bn = (EPI & kEpiBias) ? g.bias[n0 + nl] : 0.f;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int ml = wr * 64 + i * 16 + 4 * (l >> 4);
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr) {
+        float x = acc[i][j][rr] * g.alpha + bn;
+        if (EPI & kEpiRelu) x = fmaxf(x, 0.f);
+        tile[etile(ml + rr, nl)] = f2bf(x);
+      }
+    }
+  }
+  __syncthreads();
+  const u16* mask = static_cast<const u16*>(g.mask);
+  u16* C = static_cast<u16*>(g.C);
+  if ((EPI & kEpiMask) || C) {
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {  // 128 rows x 16 chunks of 8
+      const int idx = tid + 256 * it, r = idx >> 4, c = (idx & 15) * 8;
+      uint4 v = *reinterpret_cast<const uint4*>(tile + etile(r, c));
+      if (EPI & kEpiMask) {
+        const uint4 mk = *reinterpret_cast<const uint4*>(mask + (long long)(m0 + r) * g.ldmask + n0 + c);
+        unsigned* vw = reinterpret_cast<unsigned*>(&v);
+        const unsigned* mw = reinterpret_cast<const unsigned*>(&mk);
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const unsigned lo = bf2f(mw[e] & 0xffff) > 0.f ? 0x0000ffffu : 0u;
+          const unsigned hi = __uint_as_float(mw[e] & 0xffff0000u) > 0.f ? 0xffff0000u : 0u;
+          vw[e] &= lo | hi;
+        }
+        if (EPI & kEpiStoreT) *reinterpret_cast<uint4*>(tile + etile(r, c)) = v;
+      }
+      if (C) *reinterpret_cast<uint4*>(C + (long long)(m0 + r) * g.ldc + n0 + c) = v;
+    }
+  }
+  if (EPI & kEpiStoreT) {
+    if (EPI & kEpiMask) __syncthreads();
+    u16* CT = static_cast<u16*>(g.CT);
+#pragma unroll
+    for (int it = 0; it < 8; ++it) {  // 128 columns x 16 chunks of 8 rows
+      const int idx = tid + 256 * it, n = idx >> 4, mc = (idx & 15) * 8;
+      unsigned w[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e)
+        w[e] = (unsigned)tile[etile(mc + 2 * e, n)] | ((unsigned)tile[etile(mc + 2 * e + 1, n)] << 16);
+      *reinterpret_cast<uint4*>(CT + (long long)(n0 + n) * g.ldct + m0 + mc) = make_uint4(w[0], w[1], w[2], w[3]);
+    }
+  }
+}
+
+// S = 2: two stages (64 KiB), two blocks per CU, plain vmcnt(0) + barrier per K-step.
+// S > 2: S stages (S x 32 KiB), one block per CU, S-1 K-tiles in flight: the wait before K-tile kt
+// is a counted vmcnt (every glds but the newest (S-2) tiles' 8 per thread) and the barrier is a raw
+// s_barrier, so the prefetches stay in flight across it (a __syncthreads would drain them).  For
+// grids that fit the chip in one wave of blocks this hides HBM latency the 2-stage loop exposes.
+template <int N>
+DGT_DEVICE void wait_vmcnt() {
+  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
+}
+
+template <int EPI, int S>
+__global__ __launch_bounds__(256, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) u16 lds[S][2][GBM * GBK];  // [stage][A|B], 32 KiB per stage
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   int tm, tn;
   tile_of_block(blockIdx.x, g.M / GBM, g.N / GBN, tm, tn);
@@ -117,18 +193,9 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
     for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / GBK;
-  stage_tile(A, g.lda, m0, 0, lds[0][0], w, l);
-  stage_tile(B, g.ldb, n0, 0, lds[0][1], w, l);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  for (int kt = 0; kt < nk; ++kt) {
-    const int cur = kt & 1;
-    if (kt + 1 < nk) {
-      stage_tile(A, g.lda, m0, (kt + 1) * GBK, lds[cur ^ 1][0], w, l);
-      stage_tile(B, g.ldb, n0, (kt + 1) * GBK, lds[cur ^ 1][1], w, l);
-    }
-    const u16* As = lds[cur][0];
-    const u16* Bs = lds[cur][1];
+  auto compute = [&](int buf) {
+    const u16* As = lds[buf][0];
+    const u16* Bs = lds[buf][1];
 #pragma unroll
     for (int kk = 0; kk < GBK / 32; ++kk) {
       const int chunk = kk * 4 + (l >> 4);
@@ -143,16 +210,62 @@ __global__ __launch_bounds__(256, 2) void gemm_nt_kernel(GemmArgs g) {
         for (int j = 0; j < 4; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
+  };
+  if constexpr (S == 2) {
+    stage_tile(A, g.lda, m0, 0, lds[0][0], w, l);
+    stage_tile(B, g.ldb, n0, 0, lds[0][1], w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    for (int kt = 0; kt < nk; ++kt) {
+      const int cur = kt & 1;
+      if (kt + 1 < nk) {
+        stage_tile(A, g.lda, m0, (kt + 1) * GBK, lds[cur ^ 1][0], w, l);
+        stage_tile(B, g.ldb, n0, (kt + 1) * GBK, lds[cur ^ 1][1], w, l);
+      }
+      compute(cur);
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  } else {
+    constexpr int PER_TILE = 8;  // glds per thread per K-tile (A and B: 4 each)
+#pragma unroll
+    for (int p = 0; p < S - 1; ++p) {
+      if (p < nk) {
+        stage_tile(A, g.lda, m0, p * GBK, lds[p][0], w, l);
+        stage_tile(B, g.ldb, n0, p * GBK, lds[p][1], w, l);
+      }
+    }
+    int buf = 0;
+    for (int kt = 0; kt < nk; ++kt) {
+      // tiles kt .. min(kt + S - 2, nk - 1) are in flight; retire tile kt
+      const int ahead = min(S - 2, nk - 1 - kt);
+      if (ahead >= S - 2) wait_vmcnt<(S - 2) * PER_TILE>();
+      else if (S > 3 && ahead == 1) wait_vmcnt<PER_TILE>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // tile kt visible to all waves; buffer of kt-1 free for reuse
+      __builtin_amdgcn_sched_barrier(0);
+      if (kt + S - 1 < nk) {
+        const int nb = (buf + S - 1) % S;
+        stage_tile(A, g.lda, m0, (kt + S - 1) * GBK, lds[nb][0], w, l);
+        stage_tile(B, g.ldb, n0, (kt + S - 1) * GBK, lds[nb][1], w, l);
+      }
+      compute(buf);
+      buf = (buf + 1 == S) ? 0 : buf + 1;
+    }
+    __builtin_amdgcn_s_barrier();
   }
 
   // ---- epilogue: D col = l&15 (n), row = 4*(l>>4) + r (m)
+  if constexpr (!(EPI & kEpiOutF32)) {
+    epilogue_staged_128<EPI>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
+  } else {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      epi_store<EPI>(g, acc[i][j], m0 + wr * 64 + i * 16 + 4 * (l >> 4), n0 + wc * 64 + j * 16 + (l & 15));
+      for (int j = 0; j < 4; ++j)
+        epi_store<EPI>(g, acc[i][j], m0 + wr * 64 + i * 16 + 4 * (l >> 4), n0 + wc * 64 + j * 16 + (l & 15));
+  }
 }
 
 // ------------------------------------------------------------------ 256 x 256 tile, 8-phase pipeline
@@ -359,23 +472,27 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
       epi_store<EPI>(g, acc[i][j], m0 + c.wr * 128 + i * 16 + 4 * (c.l >> 4), n0 + c.wc * 64 + j * 16 + (c.l & 15));
 }
 
-// variant: 0 = pick by shape, 1 = 128x128 kernel, 2 = 256x256 8-phase kernel
+// variant: 0 = pick by shape, 1 = 128x128 2-stage, 2 = 256x256 8-phase, 3 = 128x128 4-stage
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0;
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks,
   // 2 blocks per CU) wins
   bool big = fits256 && (g.M / 256) * (g.N / 256) >= 200;
-  if (variant == 1) big = false;
+  if (variant == 1 || variant == 3) big = false;
   if (variant == 2) {
     if (!fits256) return hipErrorInvalidValue;
     big = true;
   }
   const int grid = big ? (g.M / 256) * (g.N / 256) : (g.M / GBM) * (g.N / GBN);
-#define DGT_EPI_CASE(E)                                                                        \
-  case E:                                                                                      \
-    if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g); \
-    else hipLaunchKernelGGL((gemm_nt_kernel<E>), dim3(grid), dim3(256), 0, stream, g);         \
+  // a grid that fits the chip at one block per CU gains nothing from 2 blocks/CU: spend the LDS on
+  // a deep (4-stage) pipeline instead
+  const bool deep = !big && (variant == 3 || (variant == 0 && grid <= 256));
+#define DGT_EPI_CASE(E)                                                                           \
+  case E:                                                                                         \
+    if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
+    else if (deep) hipLaunchKernelGGL((gemm_nt_kernel<E, 4>), dim3(grid), dim3(256), 0, stream, g); \
+    else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;
   switch (epi) {
     DGT_EPI_CASE(0)

@@ -8,3 +8,4 @@ echo "== gemm bench"; timeout -k 10 300 python scripts/bench_gemm.py > gpurun_ou
 cat gpurun_out/bench_gemm.jsonl
 echo "== mlp bench"; timeout -k 10 300 python bench.py --model mlp --steps 30 --warmup 5 --no-sweep > gpurun_out/bench_mlp.json 2> gpurun_out/bench_mlp.err || { tail -20 gpurun_out/bench_mlp.err; exit 1; }
 cat gpurun_out/bench_mlp.json
+echo "== rocprof mlp"; cd /tmp && timeout -k 10 300 rocprofv3 --kernel-trace --stats -d $GRAFT_REPO_ROOT/gpurun_out/prof_mlp -o run --output-format csv -- python3 $GRAFT_REPO_ROOT/bench.py --model mlp --steps 10 --warmup 2 --no-sweep > $GRAFT_REPO_ROOT/gpurun_out/prof_mlp.log 2>&1; echo "rocprof rc=$?"
