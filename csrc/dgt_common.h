@@ -140,4 +140,24 @@ DGT_DEVICE float adam_update_fast(float p, float g, float& m, float& v, const Ad
   return fmaf(step_size_neg, m * __builtin_amdgcn_rcpf(denom), p);
 }
 
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// adam_update_fast on two elements: the non-transcendental math runs as packed fp32
+// (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth per instruction, same IEEE result
+// per element as the scalar form); sqrt and rcp stay per element.
+DGT_DEVICE f32x2 adam_update_fast2(f32x2 p, f32x2 g, f32x2& m, f32x2& v, const AdamHyper& h, float step_size_neg,
+                                   float inv_bc2_sqrt) {
+  if (h.weight_decay != 0.f) {
+    if (h.adamw) p = p * h.decay;
+    else g = __builtin_elementwise_fma(f32x2(h.weight_decay), p, g);
+  }
+  m = __builtin_elementwise_fma(f32x2(h.one_minus_beta1), g - m, m);
+  v = v * h.beta2;
+  v = __builtin_elementwise_fma(f32x2(h.one_minus_beta2) * g, g, v);
+  f32x2 r;
+  r.x = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(v.x), inv_bc2_sqrt, h.eps));
+  r.y = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(v.y), inv_bc2_sqrt, h.eps));
+  return __builtin_elementwise_fma(f32x2(step_size_neg), m * r, p);
+}
+
 }  // namespace dgt

@@ -27,6 +27,7 @@ struct TinyTrainArgs {
   double lr;             // python-double lr (bias-corrected step size is formed in double)
   double beta1, beta2;
   long long adam_step0;  // optimizer steps already taken before this launch
+  float* bc;             // [n_steps][2] workspace: per-step bias corrections (filled by tiny_mlp_train)
   double* loss_acc;      // += sum over steps of the step's mean loss
   int* status;           // Status
   Exchange ex;           // world_size 1 -> no exchange

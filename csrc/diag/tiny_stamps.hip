@@ -69,6 +69,9 @@ int main(int argc, char** argv) {
   a.loss_acc = dLoss; a.status = dStatus;
   a.ex.rank = 0; a.ex.world_size = 1;
   a.stamps = dStamps;
+  float* dBc;
+  CK(hipMalloc(&dBc, (size_t)steps * 2 * sizeof(float)));
+  a.bc = dBc;
   CK(dgt::tiny_mlp_train(F, H, a, 0));
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;
@@ -84,7 +87,7 @@ int main(int argc, char** argv) {
   unsigned long long st[16];
   CK(hipMemcpy(st, dStamps, sizeof(st), hipMemcpyDeviceToHost));
   const char* names[5] = {"prefetch+fwd GEMM+partial z", "barrier wait", "loss+bwd+wgrad MFMA",
-                          "stage next batch+grad regs", "Adam (+double bias corr)"};
+                          "stage next batch+grad regs", "Adam (packed fp32)"};
   printf("stamped build: %.3f us/step (%d steps)\n", ms * 1e3 / steps, steps);
   for (int w = 0; w < 2; ++w) {
     unsigned long long tot = 0;

@@ -10,12 +10,14 @@
 //     is updated redundantly (bit-identically) by every wave.
 //   * Both GEMM-shaped products run on the matrix cores with exact-fp32 MFMA
 //     (v_mfma_f32_16x16x4_f32).  The weight gradient is computed transposed,
-//     dW1^T[k][j] = sum_b x[b][k] dh[b][j], so lane (l&15, l>>4) receives dW1[j = l&15][k] for
-//     k = 16ct + 4(l>>4) + r.  The forward H^T = W1 . X^T walks its K dimension in exactly that
-//     permuted order, so the lane that receives a weight's gradient is the lane that owns the
-//     weight, updates it with Adam and feeds it to the next forward MFMA — no LDS round trip for
-//     parameters or gradients.  The forward's x operand comes straight from HBM/L2 as float4
-//     rows; LDS only stages the two transposed operands of the weight-gradient MFMA.
+//     dW1^T[k][j] = sum_b x[b][k] dh[b][j], with the MFMA's A rows permuted so that lane
+//     (l&15, l>>4) receives dW1[j = l&15][k] for k = 16ct + (l>>4) + 4r ("slot" 4ct + r).  The
+//     forward H^T = W1 . X^T walks its K dimension in exactly that slot order, so the lane that
+//     receives a weight's gradient is the lane that owns the weight, updates it with Adam and
+//     feeds it to the next forward MFMA — no LDS round trip for parameters or gradients.  The
+//     stride-4 slot order packs the padding of the last K tile (K = F + 1 is rarely a multiple of
+//     16) into whole slots that are skipped: F = 20 runs 6 of 8 slots (6 forward MFMAs, 8 Adam
+//     updates per lane).  LDS only stages the two transposed operands of the weight gradient.
 //   * b1 is folded into the GEMMs as an augmented weight column: x carries a constant 1 at feature
 //     index F, so the forward MFMA adds the bias and the weight-gradient MFMA produces db1 in the
 //     same registers as dW1.  W2 is owned by 4 lanes per DPP row and broadcast with row_newbcast.
@@ -25,9 +27,12 @@
 //     step's rows are prefetched into registers while the current step computes (no per-step H2D,
 //     no host sync: SURVEY K1/K2/K24).
 //   * World size > 1: each wave pushes its gradient slice into every peer's IPC mailbox over
-//     xGMI, raises a per-(wave, rank) sequence flag (system-scope release), waits for its own flags
-//     and sums the contributions in rank order, so every rank applies bit-identical updates.  This
-//     replaces DeepSpeed's flatten -> NCCL all_reduce -> scale -> unflatten.
+//     xGMI as LL lines (payload + sequence tag per 8 bytes, dgt_common.h), polls its own mailbox
+//     until every peer's tags match and sums the contributions in rank order, so every rank
+//     applies bit-identical updates.  This replaces DeepSpeed's flatten -> NCCL all_reduce ->
+//     scale -> unflatten.
+//   * Adam's bias corrections come from a per-step table (torch's double-precision formula,
+//     filled by a one-thread-per-step kernel before the launch): no double math in the loop.
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 
@@ -54,8 +59,11 @@ struct TinyCfg {
   static constexpr int NW = H / 16;              // waves; wave w owns hidden units [16w, 16w+16)
   static constexpr int T = 64 * NW;              // threads
   static constexpr int NKT = (F + 1 + 15) / 16;  // 16-wide tiles of the augmented features [x, 1]
-  static constexpr int NS = 4 * NKT;             // W1 slots per lane: (ct, r) -> k = 16ct + 4(l>>4) + r
-  static constexpr int NQ = (NS + 2 + 3) / 4;    // float4s per lane in the exchange (W1 slots, W2, b2)
+  static constexpr int NS = 4 * NKT;             // W1 slots per lane: (ct, r) -> k = 16ct + (l>>4) + 4r
+  static constexpr int REM = F + 1 - 16 * (NKT - 1);      // live k in the last tile (1..16)
+  static constexpr int NSL = 4 * (NKT - 1) + (REM + 3) / 4;  // slots holding any live k
+  static constexpr int NSP = NSL + (NSL & 1);    // rounded up to packed-fp32 pairs (extra slot stays 0)
+  static constexpr int NQ = (NSL + 2 + 3) / 4;   // float4s per lane in the exchange (W1 slots, W2, b2)
   static constexpr int XCH = NW * NQ * 256;      // exchange floats per (parity, rank) mailbox slot
   static constexpr int SX = NKT * 16 + 1;        // LDS row stride of the staged batch (+1: conflict-free)
   static constexpr int BM = 16;                  // max micro-batch (MFMA N of the forward)
@@ -66,7 +74,7 @@ struct TinyCfg {
   static_assert(F % 4 == 0 && F >= 4 && F <= 64, "n_features must be a multiple of 4 in [4, 64]");
 
   // feature index of W1 slot i (= 4ct + r) in lane-row lq
-  static DGT_HOST_DEVICE int slot_k(int i, int lq) { return 16 * (i >> 2) + 4 * lq + (i & 3); }
+  static DGT_HOST_DEVICE int slot_k(int i, int lq) { return 16 * (i >> 2) + lq + 4 * (i & 3); }
   // global index of W1 slot i of lane (lr, lq) in wave w: W1 column k < F, b1 at k == F, else -1
   static DGT_HOST_DEVICE int slot_index(int w, int lr, int lq, int i) {
     const int k = slot_k(i, lq);
@@ -99,7 +107,7 @@ struct __attribute__((aligned(16))) TinySmem {
 template <int F, int H>
 struct LaneState {
   using C = TinyCfg<F, H>;
-  float w1[C::NS], m1[C::NS], v1[C::NS];  // [W1 | b1][16w + (l&15)][slot_k(i, l>>4)]
+  float w1[C::NSP], m1[C::NSP], v1[C::NSP];  // [W1 | b1][16w + (l&15)][slot_k(i, l>>4)]
   float bw, mbw, vbw;                      // W2 element (lanes 0-3 of each DPP row)
   float b2, mb2, vb2;                      // replicated in every lane
 };
@@ -109,8 +117,8 @@ DGT_DEVICE void load_state(LaneState<F, H>& st, const float* __restrict__ p, con
                            const float* __restrict__ v, int w, int lr, int lq) {
   using C = TinyCfg<F, H>;
 #pragma unroll
-  for (int i = 0; i < C::NS; ++i) {
-    const int gi = C::slot_index(w, lr, lq, i);
+  for (int i = 0; i < C::NSP; ++i) {
+    const int gi = i < C::NSL ? C::slot_index(w, lr, lq, i) : -1;
     const bool ok = gi >= 0;
     st.w1[i] = ok ? p[gi] : 0.f;
     st.m1[i] = (ok && m) ? m[gi] : 0.f;
@@ -126,17 +134,21 @@ DGT_DEVICE void load_state(LaneState<F, H>& st, const float* __restrict__ p, con
 }
 
 // Minibatch values for the lane's row b = l&15: x[b][slot_k(i, l>>4)] and y[b] (0 when padding).
+// Slot k's are stride-4 (k = 16ct + lq + 4r): scalar loads, issued a step ahead of their use.
 template <int F, int H>
 DGT_DEVICE void load_rows(const float* __restrict__ X, const float* __restrict__ Y, int id, int lq,
-                          float (&x)[TinyCfg<F, H>::NS], float& y) {
+                          float (&x)[TinyCfg<F, H>::NSP], float& y) {
   using C = TinyCfg<F, H>;
+  const float* row = X + (long long)(id >= 0 ? id : 0) * F;
 #pragma unroll
-  for (int ct = 0; ct < C::NKT; ++ct) {
-    f32x4 q = {0.f, 0.f, 0.f, 0.f};
-    const int k0 = 16 * ct + 4 * lq;
-    if (id >= 0 && k0 < F) q = *reinterpret_cast<const f32x4*>(X + (long long)id * F + k0);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) x[4 * ct + r] = (id >= 0 && k0 + r == F) ? 1.f : q[r];  // bias feature
+  for (int i = 0; i < C::NSP; ++i) {
+    const int k = C::slot_k(i, lq);
+    float v = 0.f;
+    if (i < C::NSL) {
+      if (16 * (i >> 2) + 15 < F) v = row[k];  // full tile: every k is a feature
+      else v = k < F ? row[k] : (k == F ? 1.f : 0.f);
+    }
+    x[i] = id >= 0 ? v : 0.f;
   }
   y = id >= 0 ? Y[id] : 0.f;
 }
@@ -147,19 +159,19 @@ DGT_DEVICE void load_rows(const float* __restrict__ X, const float* __restrict__
 // row = hidden 4*(l>>4) + r.
 template <int F, int H>
 DGT_DEVICE void wave_forward(const LaneState<F, H>& st, WaveSmem<F, H>& ws, float* Zbuf, int w, int lr, int lq,
-                             const float (&x)[TinyCfg<F, H>::NS], float (&h)[4], float (&w2v)[4]) {
+                             const float (&x)[TinyCfg<F, H>::NSP], float (&h)[4], float (&w2v)[4]) {
   using C = TinyCfg<F, H>;
   // two independent accumulation chains halve the dependent-MFMA latency
   f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < C::NS; i += 2) {
+  for (int i = 0; i < C::NSL; i += 2) {
     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(st.w1[i], x[i], acc0, 0, 0, 0);
-    if (i + 1 < C::NS) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(st.w1[i + 1], x[i + 1], acc1, 0, 0, 0);
+    if (i + 1 < C::NSL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(st.w1[i + 1], x[i + 1], acc1, 0, 0, 0);
   }
   const f32x4 acc = acc0 + acc1;
   // stage this step's rows for the weight-gradient MFMA (row-major, conflict-free stride)
 #pragma unroll
-  for (int i = 0; i < C::NS; ++i) ws.X[lr * C::SX + 16 * (i >> 2) + 4 * lq + (i & 3)] = x[i];
+  for (int i = 0; i < C::NSL; ++i) ws.X[lr * C::SX + C::slot_k(i, lq)] = x[i];
   w2v[0] = dpp_mov<0x150>(st.bw);  // row_newbcast: W2[4lq + r] from lane r of the DPP row
   w2v[1] = dpp_mov<0x151>(st.bw);
   w2v[2] = dpp_mov<0x152>(st.bw);
@@ -182,7 +194,7 @@ struct StepGrads {
 template <int F, int H, bool WANT_LOSS>
 DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws, const float* Zbuf, int lr,
                                    int lq, const float (&h)[4], const float (&w2v)[4], float y, int Bt,
-                                   float invB, float (&gw1)[TinyCfg<F, H>::NS]) {
+                                   float invB, float (&gw1)[TinyCfg<F, H>::NSP]) {
   using C = TinyCfg<F, H>;
   float s = 0.f;
 #pragma unroll
@@ -211,9 +223,10 @@ DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws
   out.bw = gbw;
   __builtin_amdgcn_wave_barrier();
   // weight gradient on MFMA, transposed: dW1^T[k][j] = sum_b x[b][k] dh[b][j]
-  // A[i = k (l&15)][kk = b (l>>4)] = x[b][16ct + (l&15)], B[kk = b][col = j (l&15)] = dh[b][j];
-  // D: lane (lr, lq) gets dW1[j = lr][k = 16ct + 4lq + r] = W1 slot 4ct + r.
+  // A[i (l&15)][kk = b (l>>4)] = x[b][16ct + (i>>2) + 4(i&3)], B[kk = b][col = j (l&15)] = dh[b][j];
+  // D row i = 4lq + r lands in lane (lr, lq): dW1[j = lr][k = 16ct + lq + 4r] = W1 slot 4ct + r.
   const int nks = (Bt + 3) >> 2;
+  const int arow = (lr >> 2) + 4 * (lr & 3);
 #pragma unroll
   for (int ct = 0; ct < C::NKT; ++ct) {
     f32x4 g = {0.f, 0.f, 0.f, 0.f};
@@ -221,11 +234,12 @@ DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws
     for (int ks = 0; ks < C::BM / 4; ++ks) {
       if (ks < nks) {  // wave-uniform
         const int b = 4 * ks + lq;
-        g = __builtin_amdgcn_mfma_f32_16x16x4f32(ws.X[b * C::SX + 16 * ct + lr], ws.DH[b * 17 + lr], g, 0, 0, 0);
+        g = __builtin_amdgcn_mfma_f32_16x16x4f32(ws.X[b * C::SX + 16 * ct + arow], ws.DH[b * 17 + lr], g, 0, 0, 0);
       }
     }
 #pragma unroll
-    for (int r = 0; r < 4; ++r) gw1[4 * ct + r] = g[r];
+    for (int r = 0; r < 4; ++r)
+      if (4 * ct + r < C::NSP) gw1[4 * ct + r] = (4 * ct + r < C::NSL) ? g[r] : 0.f;
   }
   __builtin_amdgcn_wave_barrier();
   return out;
@@ -256,14 +270,12 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   for (int i = l; i < C::BM * C::SX; i += 64) ws.X[i] = 0.f;
   for (int i = l; i < C::BM * 17; i += 64) ws.DH[i] = 0.f;
   if (t == 0) sm.err = 0;
-  float x[C::NS], y, xn[C::NS], yn;
+  float x[C::NSP], y, xn[C::NSP], yn;
   load_rows<F, H>(a.X, a.Y, plan_at(a.plan, a.n_steps, a.bmax, 0, lr), lq, x, y);
   int idx_next = plan_at(a.plan, a.n_steps, a.bmax, 1, lr);
   int idx_next2 = plan_at(a.plan, a.n_steps, a.bmax, 2, lr);
   __syncthreads();
 
-  double b1p = pow(a.beta1, (double)a.adam_step0);
-  double b2p = pow(a.beta2, (double)a.adam_step0);
   double loss_total = 0.0;
   const float inv_ws = 1.0f / (float)ex.world_size;
 #ifdef DGT_TINY_STAMPS
@@ -283,7 +295,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     __syncthreads();  // the step's only workgroup barrier: all partial logits published
     DGT_STAMP(2);
     if (sm.err) break;
-    float gw1[C::NS];
+    float gw1[C::NSP];
     const StepGrads sg = (w == 0) ? wave_backward<F, H, true>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1)
                                   : wave_backward<F, H, false>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
     float gbw = sg.bw, gb2 = sg.b2;
@@ -303,7 +315,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * q + e;
-          pk[q][e] = i < C::NS ? gw1[i] : (i == C::NS ? gbw : (i == C::NS + 1 ? gb2 : 0.f));
+          pk[q][e] = i < C::NSL ? gw1[i] : (i == C::NSL ? gbw : (i == C::NSL + 1 ? gb2 : 0.f));
         }
       }
       const long long wofs = (long long)w * C::NQ * 512 + l * 4;
@@ -368,28 +380,44 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
         for (int e = 0; e < 4; ++e) {
           const int i = 4 * q + e;
           const float v = sum[q][e] * inv_ws;
-          if (i < C::NS) gw1[i] = v;
-          else if (i == C::NS) gbw = v;
-          else if (i == C::NS + 1) gb2 = v;
+          if (i < C::NSL) gw1[i] = v;
+          else if (i == C::NSL) gbw = v;
+          else if (i == C::NSL + 1) gb2 = v;
         }
       }
     }
     DGT_STAMP(4);
 
-    // ---- Adam; bias corrections from double running powers (torch forms them in double on host)
-    b1p *= a.beta1;
-    b2p *= a.beta2;
-    const float step_size_neg = -a.hp.lr * __builtin_amdgcn_rcpf((float)(1.0 - b1p));
-    const float inv_bc2_sqrt = __builtin_amdgcn_rsqf((float)(1.0 - b2p));
+    // ---- Adam; bias corrections of this step from the table (wave-uniform scalar loads)
+    const float step_size_neg = a.bc[2 * s], inv_bc2_sqrt = a.bc[2 * s + 1];
+    // two parameters per packed-fp32 update (W2 and b2 form the last pair)
 #pragma unroll
-    for (int i = 0; i < C::NS; ++i)
-      st.w1[i] = adam_update_fast(st.w1[i], gw1[i], st.m1[i], st.v1[i], a.hp, step_size_neg, inv_bc2_sqrt);
-    st.bw = adam_update_fast(st.bw, gbw, st.mbw, st.vbw, a.hp, step_size_neg, inv_bc2_sqrt);
-    st.b2 = adam_update_fast(st.b2, gb2, st.mb2, st.vb2, a.hp, step_size_neg, inv_bc2_sqrt);
+    for (int i = 0; i < C::NSP; i += 2) {
+      f32x2 m = {st.m1[i], st.m1[i + 1]}, v = {st.v1[i], st.v1[i + 1]};
+      const f32x2 pn = adam_update_fast2(f32x2{st.w1[i], st.w1[i + 1]}, f32x2{gw1[i], gw1[i + 1]}, m, v, a.hp,
+                                         step_size_neg, inv_bc2_sqrt);
+      st.w1[i] = pn.x;
+      st.w1[i + 1] = pn.y;
+      st.m1[i] = m.x;
+      st.m1[i + 1] = m.y;
+      st.v1[i] = v.x;
+      st.v1[i + 1] = v.y;
+    }
+    {
+      f32x2 m = {st.mbw, st.mb2}, v = {st.vbw, st.vb2};
+      const f32x2 pn = adam_update_fast2(f32x2{st.bw, st.b2}, f32x2{gbw, gb2}, m, v, a.hp, step_size_neg,
+                                         inv_bc2_sqrt);
+      st.bw = pn.x;
+      st.b2 = pn.y;
+      st.mbw = m.x;
+      st.mb2 = m.y;
+      st.vbw = v.x;
+      st.vb2 = v.y;
+    }
     loss_total += (double)sg.loss;
     // rotate the prefetch pipeline
 #pragma unroll
-    for (int i = 0; i < C::NS; ++i) x[i] = xn[i];
+    for (int i = 0; i < C::NSP; ++i) x[i] = xn[i];
     y = yn;
     idx_next = idx_next2;
     idx_next2 = plan_at(a.plan, a.n_steps, a.bmax, s + 3, lr);
@@ -402,7 +430,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
 
   // ---- epilogue: state back to HBM (b2 belongs to wave 0, lane 0)
 #pragma unroll
-  for (int i = 0; i < C::NS; ++i) {
+  for (int i = 0; i < C::NSL; ++i) {
     const int gi = C::slot_index(w, lr, lq, i);
     if (gi >= 0) {
       a.params[gi] = st.w1[i];
@@ -439,18 +467,18 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_grad_kernel(TinyG
   load_state<F, H>(st, a.params, nullptr, nullptr, w, lr, lq);
   for (int i = l; i < C::BM * C::SX; i += 64) ws.X[i] = 0.f;
   for (int i = l; i < C::BM * 17; i += 64) ws.DH[i] = 0.f;
-  float x[C::NS], y;
+  float x[C::NSP], y;
   const int id = (lr < a.bmax) ? a.plan[(long long)a.step * a.bmax + lr] : -1;
   load_rows<F, H>(a.X, a.Y, id, lq, x, y);
   const int Bt = a.counts[a.step];
   const float invB = __builtin_amdgcn_rcpf((float)Bt);
-  float h[4], w2v[4], gw1[C::NS];
+  float h[4], w2v[4], gw1[C::NSP];
   __builtin_amdgcn_wave_barrier();
   wave_forward<F, H>(st, ws, sm.Z[0], w, lr, lq, x, h, w2v);
   __syncthreads();
   const StepGrads sg = wave_backward<F, H, true>(st, ws, sm.Z[0], lr, lq, h, w2v, y, Bt, invB, gw1);
 #pragma unroll
-  for (int i = 0; i < C::NS; ++i) {
+  for (int i = 0; i < C::NSL; ++i) {
     const int gi = C::slot_index(w, lr, lq, i);
     if (gi >= 0) a.grad[gi] = gw1[i];
   }
@@ -481,7 +509,20 @@ int tiny_mlp_exchange_floats(int f, int h) {
   return 0;
 }
 
+// Per-step Adam bias corrections for a launch, in double exactly as torch's (non-capturable)
+// foreach Adam forms them on the host: step_size = -(lr / (1 - beta1^t)), 1 / sqrt(1 - beta2^t).
+__global__ void adam_bias_table_kernel(float* bc, int n, long long step0, double lr, double beta1, double beta2) {
+  const int s = blockIdx.x * blockDim.x + threadIdx.x;
+  if (s >= n) return;
+  const double t = (double)(step0 + s + 1);
+  bc[2 * s] = (float)(-(lr / (1.0 - pow(beta1, t))));
+  bc[2 * s + 1] = (float)(1.0 / sqrt(1.0 - pow(beta2, t)));
+}
+
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
+  if (!a.bc) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(adam_bias_table_kernel, dim3((a.n_steps + 255) / 256), dim3(256), 0, stream, a.bc, a.n_steps,
+                     a.adam_step0, a.lr, a.beta1, a.beta2);
 #define X_(F_, H_)                                                                            \
   if (f == F_ && h == H_) {                                                                   \
     hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_>), dim3(1), dim3(TinyCfg<F_, H_>::T), 0, \
