@@ -73,9 +73,11 @@ DGT_DEVICE unsigned long long ll_get(const unsigned* src) {
 DGT_DEVICE bool ll_ok(unsigned long long pair, unsigned tag) { return (unsigned)(pair >> 32) == tag; }
 DGT_DEVICE float ll_val(unsigned long long pair) { return __uint_as_float((unsigned)pair); }
 
+// Full-row DPP permutations (quad_perm, row mirrors, row_newbcast) have a source lane for every
+// lane, so bound_ctrl = true: no "old" value has to be materialised and an add can fold the move.
 template <int CTRL>
 DGT_DEVICE float dpp_mov(float v) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xF, 0xF, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), CTRL, 0xF, 0xF, true));
 }
 
 // Sum over the 16 lanes of a DPP row (lanes sharing lane>>4), result in every lane of the row.
@@ -86,6 +88,14 @@ DGT_DEVICE float wave_sum16(float v) {
   v += dpp_mov<0x4E>(v);   // quad_perm [2,3,0,1]
   v += dpp_mov<0x141>(v);  // row_half_mirror
   v += dpp_mov<0x140>(v);  // row_mirror
+  return v;
+}
+
+// Sum over each quad (lanes 4q..4q+3): enough for a row reduction when only lanes 0..3 of each DPP
+// row can be non-zero (micro-batch <= 4); the result is in every lane of the quad.
+DGT_DEVICE float quad_sum(float v) {
+  v += dpp_mov<0xB1>(v);
+  v += dpp_mov<0x4E>(v);
   return v;
 }
 

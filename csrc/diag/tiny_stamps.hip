@@ -1,7 +1,8 @@
 // Diagnostic harness (not part of the extension): where does one fused training step spend its
 // cycles?  Builds the training kernel with per-section s_memtime stamps and reports cycles/step per
 // section for waves 0 and 1.  Read the SHARES, not the total: stamps serialize the schedule.
-//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc csrc/diag/tiny_stamps.hip -o build/bin/tiny_stamps
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -mllvm -amdgpu-mfma-vgpr-form -Icsrc csrc/diag/tiny_stamps.hip \
+//         -o build/bin/tiny_stamps
 #define DGT_TINY_STAMPS 1
 #include "../tiny_mlp.hip"
 

@@ -191,7 +191,9 @@ struct StepGrads {
 };
 
 // After the barrier: logits, BCE, backward.  W1 gradients land in gw1 (slot layout).
-template <int F, int H, bool WANT_LOSS>
+// SMALLB: micro-batch <= 4 (the reference's 4 per rank): only lanes 0..3 of a DPP row carry
+// batch rows, so row reductions are quad reductions and the weight gradient is one MFMA per tile.
+template <int F, int H, bool WANT_LOSS, bool SMALLB>
 DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws, const float* Zbuf, int lr,
                                    int lq, const float (&h)[4], const float (&w2v)[4], float y, int Bt,
                                    float invB, float (&gw1)[TinyCfg<F, H>::NSP]) {
@@ -208,14 +210,20 @@ DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws
   const float dz = valid ? (sig - y) * invB : 0.f;
   StepGrads out;
   out.loss = 0.f;
-  if (WANT_LOSS) out.loss = wave_sum16(valid ? (1.f - y) * z - (fminf(z, 0.f) - __logf(1.f + e)) : 0.f) * invB;
+  if (WANT_LOSS) {
+    // 1 + e is in [1, 2]: the raw v_log_f32 (log2) needs no denormal range fix-up
+    const float l1pe = __builtin_amdgcn_logf(1.f + e) * 0.6931471805599453f;
+    const float term = valid ? (1.f - y) * z - (fminf(z, 0.f) - l1pe) : 0.f;
+    out.loss = (SMALLB ? quad_sum(term) : wave_sum16(term)) * invB;
+  }
   float dw2[4];
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     ws.DH[lr * 17 + 4 * lq + r] = (h[r] > 0.f) ? dz * w2v[r] : 0.f;
-    dw2[r] = wave_sum16(dz * h[r]);  // over the 16 batch rows: W2[4lq + r]
+    dw2[r] = SMALLB ? quad_sum(dz * h[r]) : wave_sum16(dz * h[r]);  // over the batch rows: W2[4lq + r]
   }
-  out.b2 = wave_sum16(dz);
+  // b2 is replicated in every lane: a quad sum is broadcast from lane 0 of each row
+  out.b2 = SMALLB ? dpp_mov<0x150>(quad_sum(dz)) : wave_sum16(dz);
   // the lane's own W2 element (lanes 0-3 of each row); db1 comes out of the wgrad MFMA
   float gbw = 0.f;
 #pragma unroll
@@ -225,14 +233,14 @@ DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws
   // weight gradient on MFMA, transposed: dW1^T[k][j] = sum_b x[b][k] dh[b][j]
   // A[i (l&15)][kk = b (l>>4)] = x[b][16ct + (i>>2) + 4(i&3)], B[kk = b][col = j (l&15)] = dh[b][j];
   // D row i = 4lq + r lands in lane (lr, lq): dW1[j = lr][k = 16ct + lq + 4r] = W1 slot 4ct + r.
-  const int nks = (Bt + 3) >> 2;
+  const int nks = SMALLB ? 1 : (Bt + 3) >> 2;
   const int arow = (lr >> 2) + 4 * (lr & 3);
 #pragma unroll
   for (int ct = 0; ct < C::NKT; ++ct) {
     f32x4 g = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ks = 0; ks < C::BM / 4; ++ks) {
-      if (ks < nks) {  // wave-uniform
+    for (int ks = 0; ks < (SMALLB ? 1 : C::BM / 4); ++ks) {
+      if (SMALLB || ks < nks) {  // wave-uniform
         const int b = 4 * ks + lq;
         g = __builtin_amdgcn_mfma_f32_16x16x4f32(ws.X[b * C::SX + 16 * ct + arow], ws.DH[b * 17 + lr], g, 0, 0, 0);
       }
@@ -250,15 +258,16 @@ DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row
 }
 
 // ------------------------------------------------------------------ persistent training kernel
-template <int F, int H>
+template <int F, int H, bool SMALLB>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
   __shared__ TinySmem<F, H> sm;
-  const int t = threadIdx.x, w = t >> 6, l = t & 63, lr = l & 15, lq = l >> 4;
+  const int t = threadIdx.x, l = t & 63, lr = l & 15, lq = l >> 4;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar branches on w
   const Exchange& ex = a.ex;
   WaveSmem<F, H>& ws = sm.w[w];
 
-  if (a.bmax > C::BM || a.bmax < 1 || ex.world_size < 1 || ex.world_size > kMaxRanks ||
+  if (a.bmax > (SMALLB ? 4 : C::BM) || a.bmax < 1 || ex.world_size < 1 || ex.world_size > kMaxRanks ||
       (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3)))) {
     if (t == 0) *a.status = kBadShape;
     return;
@@ -296,8 +305,8 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(2);
     if (sm.err) break;
     float gw1[C::NSP];
-    const StepGrads sg = (w == 0) ? wave_backward<F, H, true>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1)
-                                  : wave_backward<F, H, false>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
+    const StepGrads sg = (w == 0) ? wave_backward<F, H, true, SMALLB>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1)
+                                  : wave_backward<F, H, false, SMALLB>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
     float gbw = sg.bw, gb2 = sg.b2;
     DGT_STAMP(3);
 
@@ -476,7 +485,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_grad_kernel(TinyG
   __builtin_amdgcn_wave_barrier();
   wave_forward<F, H>(st, ws, sm.Z[0], w, lr, lq, x, h, w2v);
   __syncthreads();
-  const StepGrads sg = wave_backward<F, H, true>(st, ws, sm.Z[0], lr, lq, h, w2v, y, Bt, invB, gw1);
+  const StepGrads sg = wave_backward<F, H, true, false>(st, ws, sm.Z[0], lr, lq, h, w2v, y, Bt, invB, gw1);
 #pragma unroll
   for (int i = 0; i < C::NSL; ++i) {
     const int gi = C::slot_index(w, lr, lq, i);
@@ -525,8 +534,12 @@ hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stre
                      a.adam_step0, a.lr, a.beta1, a.beta2);
 #define X_(F_, H_)                                                                            \
   if (f == F_ && h == H_) {                                                                   \
-    hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_>), dim3(1), dim3(TinyCfg<F_, H_>::T), 0, \
-                       stream, a);                                                            \
+    if (a.bmax <= 4)                                                                          \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, true>), dim3(1), dim3(TinyCfg<F_, H_>::T), 0, \
+                         stream, a);                                                          \
+    else                                                                                      \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, false>), dim3(1), dim3(TinyCfg<F_, H_>::T), 0, \
+                         stream, a);                                                          \
     return hipGetLastError();                                                                 \
   }
   DGT_TINY_SHAPES(X_)

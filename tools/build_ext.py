@@ -55,6 +55,11 @@ def _run(cmd, verbose):
     return r.stdout
 
 
+# the fused tiny kernel reads every MFMA result straight back into VALU math: accumulators in
+# VGPRs save the v_accvgpr_read round trips (the GEMMs keep the compiler's AGPR choice)
+PER_FILE_FLAGS = {"tiny_mlp.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+
+
 def build(verbose: bool = False, force: bool = False, jobs: int = 8) -> str:
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(BIN, exist_ok=True)
@@ -68,7 +73,8 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 8) -> str:
         obj = os.path.join(BUILD, os.path.basename(src) + ".o")
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
-            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", *common, "-c", src, "-o", obj])
+            jobs_list.append([HIPCC, f"--offload-arch={ARCH}", *common, *PER_FILE_FLAGS.get(os.path.basename(src), []),
+                              "-c", src, "-o", obj])
     # host translation units against the torch headers (op bindings, RCCL communicator)
     for bsrc in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
         bobj = os.path.join(BUILD, os.path.basename(bsrc) + ".o")
