@@ -114,6 +114,14 @@ DGT_DEVICE float wave_sum(float v) {
 
 DGT_DEVICE unsigned long long realtime() { return __builtin_amdgcn_s_memrealtime(); }
 
+// Wave-uniform read of memory that no kernel writes during the launch, through the constant
+// address space: the compiler emits a scalar s_load (lgkmcnt) instead of a vector load, so
+// waiting for it does not also wait for every older vector load (vmcnt retires in order).
+template <typename T>
+DGT_DEVICE T load_uniform(const T* p) {
+  return *reinterpret_cast<const __attribute__((address_space(4))) T*>(reinterpret_cast<uintptr_t>(p));
+}
+
 // torch.lerp for weight < 0.5 (what Adam's exp_avg.lerp_(grad, 1 - beta1) evaluates)
 DGT_DEVICE float lerp_torch(float self, float end, float w) {
   return (fabsf(w) < 0.5f) ? fmaf(w, end - self, self) : end - (end - self) * (1.0f - w);

@@ -292,10 +292,12 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
 #endif
   for (int s = 0; s < a.n_steps; ++s) {
     DGT_STAMP(0);
-    const int Bt = a.counts[s];
+    const int Bt = load_uniform(a.counts + s);
     const float invB = __builtin_amdgcn_rcpf((float)Bt);
     // prefetch step s+1 rows into registers; consumed by the next step's forward
     load_rows<F, H>(a.X, a.Y, idx_next, lq, xn, yn);
+    // sampler index of step s+3, issued now so the end-of-step rotation never waits on it
+    const int idx_next3 = plan_at(a.plan, a.n_steps, a.bmax, s + 3, lr);
 
     float h[4], w2v[4];
     float* Zb = sm.Z[s & 1];
@@ -398,7 +400,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(4);
 
     // ---- Adam; bias corrections of this step from the table (wave-uniform scalar loads)
-    const float step_size_neg = a.bc[2 * s], inv_bc2_sqrt = a.bc[2 * s + 1];
+    const float step_size_neg = load_uniform(a.bc + 2 * s), inv_bc2_sqrt = load_uniform(a.bc + 2 * s + 1);
     // two parameters per packed-fp32 update (W2 and b2 form the last pair)
 #pragma unroll
     for (int i = 0; i < C::NSP; i += 2) {
@@ -429,7 +431,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     for (int i = 0; i < C::NSP; ++i) x[i] = xn[i];
     y = yn;
     idx_next = idx_next2;
-    idx_next2 = plan_at(a.plan, a.n_steps, a.bmax, s + 3, lr);
+    idx_next2 = idx_next3;
     DGT_STAMP(5);
   }
 #ifdef DGT_TINY_STAMPS
