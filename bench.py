@@ -38,10 +38,14 @@ def parse_args(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20000, help="timed optimizer steps")
     ap.add_argument("--warmup", type=int, default=2000, help="untimed warmup steps")
-    ap.add_argument("--impl", default="fused", choices=["fused", "graph", "stepwise", "engine"],
+    ap.add_argument("--impl", default="fused", choices=["fused", "graph", "stepwise", "engine", "dgt-engine"],
                     help="fused: one-launch HIP training kernel (IPC exchange over xGMI); graph: per-step HIP "
                          "kernels + native RCCL captured in a HIP graph; stepwise: the same launched eagerly with "
-                         "ProcessGroupNCCL; engine: PyTorch eager + RCCL (the reference-equivalent stack)")
+                         "ProcessGroupNCCL; engine: PyTorch eager + RCCL (the reference-equivalent stack); "
+                         "dgt-engine: this framework's DeepSpeed-style engine on the nn.Module "
+                         "(--deepspeed-config, e.g. configs/ds_graph.json for whole-step HIP graphs)")
+    ap.add_argument("--deepspeed-config", "--deepspeed_config", dest="ds_config", default=None,
+                    help="dgt-engine: DeepSpeed JSON config (default: the reference's in-code dict)")
     ap.add_argument("--model", default="simple", choices=["simple", "mlp"],
                     help="simple: the reference SimpleNet (headline); mlp: bench-size bf16 synthetic MLP on the "
                          "HIP MFMA GEMMs (BASELINE config #2)")
@@ -173,6 +177,7 @@ def _failed(trainer) -> bool:
 
 def main(argv=None):
     args = parse_args(argv)
+    os.environ.setdefault("DGT_QUIET", "1")  # the engine's steps_per_print lines would be timed too
     from distributed_gpu_test_amd.data import make_synthetic_data
     from distributed_gpu_test_amd.models import SimpleNet
     from distributed_gpu_test_amd.parallel import comm
@@ -196,6 +201,8 @@ def main(argv=None):
         trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device)
     elif args.impl == "engine":
         trainer = EngineBench(model, x, y, B, device)
+    elif args.impl == "dgt-engine":
+        trainer = DgtEngineBench(model, x, y, B, device, args.ds_config)
     else:
         trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=args.impl if device.type == "cuda" else "torch",
                                  device=device)
@@ -332,6 +339,61 @@ class EngineBench:
 
     def close(self):
         pass
+
+
+class DgtEngineBench(EngineBench):
+    """This framework's engine (``initialize`` + DeepSpeed JSON) on the reference nn.Module: flat
+    bucketed gradients, fused HIP Adam, ZeRO-0/1, and with ``"amd": {"hip_graph": true}`` the whole
+    step (forward, backward, RCCL collective, Adam) replayed from a HIP graph."""
+
+    impl = "dgt-engine"
+
+    def __init__(self, model, x, y, B, device, config_path=None):
+        import json
+        from distributed_gpu_test_amd.config import REFERENCE_DS_CONFIG
+        from distributed_gpu_test_amd.engine import initialize
+        from distributed_gpu_test_amd.parallel import comm
+        from distributed_gpu_test_amd import data as dgt_data
+        cfg = json.load(open(config_path)) if config_path else dict(REFERENCE_DS_CONFIG)
+        self._data = dgt_data
+        self.device = device
+        self.world, self.rank = comm.get_world_size(), comm.get_rank()
+        self.x, self.y = x.to(device), y.to(device).reshape(-1, 1)
+        self.B = B
+        opt = torch.optim.Adam(model.parameters(), lr=1e-3)
+        self.engine, _, _, _ = initialize(model=model, optimizer=opt, model_parameters=model.parameters(), config=cfg)
+        crit = torch.nn.BCEWithLogitsLoss()
+        if self.engine.config.amd.hip_graph:
+            self.step = self.engine.graph_step(lambda bx, by: crit(self.engine(bx).float(), by))
+        else:
+            def step(bx, by):
+                loss = crit(self.engine(bx).float(), by)
+                self.engine.backward(loss)
+                self.engine.step()
+                return loss.detach()
+            self.step = step
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=device)
+        graphed = self.engine.graphed is not None
+        self.exchange = ("none" if self.world == 1 else
+                         ("rccl-native-in-hipgraph" if graphed else f"{comm.backend_name()}-bucketed"))
+        self.impl = "dgt-engine" + ("+hipgraph" if graphed else "") + f"+zero{self.engine.stage}"
+
+    def run_plan(self, plan, counts):
+        plan_d = plan.to(self.device).long()
+        for s in range(plan.shape[0]):
+            rows = plan_d[s, : int(counts[s])]
+            self.loss_acc += self.step(self.x[rows], self.y[rows]).double()
+
+    @property
+    def params(self):
+        return self.engine.store.param_buf.detach()
+
+    @params.setter
+    def params(self, value):
+        pass
+
+    def close(self):
+        self.engine.close()
 
 
 if __name__ == "__main__":

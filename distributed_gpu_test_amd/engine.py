@@ -156,6 +156,8 @@ class Engine:
         self._grad_norm: Optional[torch.Tensor] = None
         self._boundary_pending = False
         self.training = True
+        self.graphed = None
+        self.graph_fallback_reason = ""
 
     # ------------------------------------------------------------------ helpers
     def _names(self, params):
@@ -200,6 +202,9 @@ class Engine:
 
     # ------------------------------------------------------------------ forward / backward / step
     def forward(self, *args, **kwargs):
+        if args and torch.is_tensor(args[0]) and args[0].dim() > 0:
+            # throughput from the REAL micro-batch (DeepSpeed uses the configured one: SURVEY X9)
+            self.tput.samples_per_step = int(args[0].shape[0]) * self.world_size
         if self.dtype != torch.float32:
             args = tuple(a.to(self.dtype) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)
         self.tput.start()
@@ -297,8 +302,33 @@ class Engine:
         for w in works:
             w.wait()
 
-    def _finish_step(self, skipped: bool) -> None:
-        self.store.zero_grad()
+    # ------------------------------------------------------------------ whole-step HIP graphs
+    def graph_step(self, loss_fn, warmup: int = 2):
+        """A callable ``step(*batch) -> loss`` running forward + backward + gradient collective +
+        optimizer as one replayed HIP graph per input shape (``runtime/graph_step.py``).  Where a
+        graph cannot represent the configuration it returns the equivalent eager closure."""
+        from .runtime.graph_step import GraphedStep, supported
+        ok, why = supported(self)
+        if ok:
+            self.graphed = GraphedStep(self, loss_fn, warmup=warmup)
+            return self.graphed
+        self.graph_fallback_reason = why
+
+        def eager(*args):
+            loss = loss_fn(*args)
+            self.backward(loss)
+            self.step()
+            return loss.detach()
+        return eager
+
+    def _finish_graph_step(self) -> None:
+        self.micro_steps += 1
+        self.tput.start()
+        self._finish_step(skipped=False, zero=False)
+
+    def _finish_step(self, skipped: bool, zero: bool = True) -> None:
+        if zero:
+            self.store.zero_grad()
         self.global_steps += 1
         self.global_samples += self.config.train_batch_size
         if self.lr_scheduler is not None and not skipped:
@@ -405,6 +435,9 @@ class Engine:
         return path, cs
 
     def close(self) -> None:
+        if self.graphed is not None:
+            self.graphed.close()
+            self.graphed = None
         for h in self._hooks:
             h.remove()
         self._hooks = []

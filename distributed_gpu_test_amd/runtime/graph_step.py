@@ -1,0 +1,184 @@
+"""Whole-training-step HIP graphs for the engine (DeepSpeed JSON ``"amd": {"hip_graph": true}``).
+
+A data-parallel step of a small model is launch-bound: eager PyTorch issues tens of kernels for
+forward + autograd backward, then the gradient collective, the optimizer and the host bookkeeping
+(~30 launches + a host sync per step of the reference).  MI355X-first, the step is
+captured ONCE per input shape into a HIP graph and replayed:
+
+    zero grads -> loss_fn(*batch) -> autograd backward (grads land in the flat bucket) ->
+    [world > 1] gradient collective on the native RCCL communicator, on the capture stream
+                (stage 0: all_reduce per bucket; ZeRO-1: reduce_scatter into the shard) ->
+    [clipping]  device-side global norm -> clip coefficient (never read on the host) ->
+    step counter += 1 on the device -> fused flat Adam (bias corrections from the device counter) ->
+    [ZeRO-1]    all_gather of the updated parameter shards
+
+Everything the step reads or writes lives in static buffers (the engine's flat param / grad /
+moment buffers, the copied-in batch, the loss output), so a replay is one graph launch.  This is
+the HIP-graph replacement for a tracing compiler: no retracing, no Python in the replayed step.
+
+Limits (checked in ``supported``; the engine falls back to eager steps otherwise): CUDA device,
+``gradient_accumulation_steps == 1``, no fp16 dynamic loss scaling (its overflow skip is a host
+decision), no learning-rate schedule (the lr is baked into the captured Adam launch), and for
+``world_size > 1`` the ``nccl`` (RCCL) backend.  Every new input shape first runs ``warmup`` eager
+steps of the same body (allocator / library warm-up before capture), then is captured.
+"""
+from __future__ import annotations
+
+from typing import Callable, Dict, Optional, Tuple
+
+import torch
+
+from ..ops.adam import adam_flat_
+from ..parallel import comm
+
+
+def supported(engine) -> Tuple[bool, str]:
+    if engine.device.type != "cuda":
+        return False, "HIP graphs need a GPU"
+    if engine.gas != 1:
+        return False, "gradient_accumulation_steps > 1"
+    if engine.loss_scaler is not None:
+        return False, "fp16 dynamic loss scaling decides on the host"
+    if engine.ds_scheduler is not None or engine.lr_scheduler is not None:
+        return False, "a learning-rate schedule changes the captured lr"
+    if engine.world_size > 1 and comm.backend_name() != "nccl":
+        return False, f"collectives in a graph need RCCL (backend is {comm.backend_name()})"
+    return True, ""
+
+
+class GraphedStep:
+    def __init__(self, engine, loss_fn: Callable[..., torch.Tensor], warmup: int = 2, max_graphs: int = 4):
+        ok, why = supported(engine)
+        if not ok:
+            raise RuntimeError(f"hip_graph step unavailable: {why}")
+        self.e = engine
+        self.loss_fn = loss_fn
+        self.warmup = warmup
+        self.max_graphs = max_graphs
+        self.rccl = None
+        if engine.world_size > 1:
+            from ..parallel.rccl import RcclComm
+            self.rccl = RcclComm(engine.device)
+        # the Adam step counter the captured launch reads (the step number of THIS update, 1-based)
+        self.step_dev = torch.full((), engine.global_steps - engine.skipped_steps, dtype=torch.int64,
+                                   device=engine.device)
+        self.pool = torch.cuda.graph_pool_handle()
+        self.graphs: Dict[tuple, tuple] = {}  # shape key -> (graph, static inputs, static loss)
+        self.seen: Dict[tuple, int] = {}
+        self.replays = 0
+        self.eager_steps = 0
+        self.failed = ""
+        engine.reducer.arm(False)  # the hooks stay silent: the step issues its own collectives
+
+    # ------------------------------------------------------------------ the step body
+    def _reduce(self) -> torch.Tensor:
+        """What GradReducer does at the boundary, on the capture stream: the optimizer then reads
+        ``reducer.reduced`` (the flat bucket, its wire-dtype copy, or the ZeRO shard)."""
+        e = self.e
+        red = e.reducer
+        src = red.grad_buf
+        if red.comm_buf is not None:
+            red.comm_buf.copy_(src)
+            src = red.comm_buf
+        for bi, b in enumerate(e.layout.buckets):
+            view = src[b.start:b.start + b.numel]
+            if e.stage >= 1:
+                n = b.numel // e.world_size
+                out = red.shard_grad[red.shard_offsets[bi]:red.shard_offsets[bi] + n]
+                if self.rccl is not None:
+                    self.rccl.reduce_scatter(out, view)
+                else:
+                    out.copy_(view)
+            elif self.rccl is not None:
+                self.rccl.all_reduce(view)
+        return red.reduced
+
+    def _clip(self, grads: torch.Tensor, scale: float) -> Optional[torch.Tensor]:
+        clip = self.e.config.gradient_clipping
+        if clip <= 0:
+            return None
+        sq = grads.float().pow(2).sum() * (scale * scale)
+        if self.e.stage >= 1 and self.e.world_size > 1:
+            self.rccl.all_reduce(sq.reshape(1))
+        return torch.clamp(clip / (sq.sqrt() + 1e-6), max=1.0).reshape(1).float()
+
+    def _allgather(self) -> None:
+        e = self.e
+        src = e.param_lp if e.param_lp is not None else e.master
+        off = 0
+        for b in e.layout.buckets:
+            n = b.numel // e.world_size
+            out = e.store.param_buf[b.start:b.start + b.numel]
+            if self.rccl is not None:
+                self.rccl.all_gather(out, src[off:off + n])
+            else:
+                out.copy_(src[off:off + n])
+            off += n
+
+    def _body(self, *args) -> torch.Tensor:
+        e = self.e
+        e.store.rebind_grads()  # .grad views into the flat bucket (host-side binding, no kernel)
+        e.store.grad_buf.zero_()
+        loss = self.loss_fn(*args)
+        loss.float().backward()
+        grads = self._reduce()
+        scale = 1.0 / e.world_size
+        coef = self._clip(grads, scale)
+        g = e.optimizer.param_groups[0]
+        self.step_dev.add_(1)
+        adam_flat_(e.master, grads, e.exp_avg, e.exp_avg_sq, 1, g["lr"], g["betas"][0], g["betas"][1], g["eps"],
+                   g["weight_decay"], g["adamw"], grad_scale=scale, grad_scale_dev=coef, param_lp=e.param_lp,
+                   step_dev=self.step_dev)
+        if e.stage >= 1:
+            self._allgather()
+        return loss.detach()
+
+    # ------------------------------------------------------------------ public
+    def __call__(self, *args) -> torch.Tensor:
+        e = self.e
+        key = tuple((tuple(a.shape), a.dtype) if torch.is_tensor(a) else ("py", a) for a in args)
+        entry = self.graphs.get(key)
+        if entry is None:
+            n = self.seen.get(key, 0)
+            if n < self.warmup or len(self.graphs) >= self.max_graphs:
+                self.seen[key] = n + 1
+                loss = self._body(*args)
+                self.eager_steps += 1
+                e._finish_graph_step()
+                return loss
+            try:
+                entry = self._capture(key, args)
+            except Exception as err:  # never lose a step to a capture problem: run it eagerly
+                self.failed = f"{type(err).__name__}: {err}"
+                self.max_graphs = len(self.graphs)
+                torch.cuda.synchronize(e.device)
+                loss = self._body(*args)
+                self.eager_steps += 1
+                e._finish_graph_step()
+                return loss
+        graph, static_in, static_loss = entry
+        for dst, src in zip(static_in, args):
+            if torch.is_tensor(dst):
+                dst.copy_(src, non_blocking=True)
+        graph.replay()
+        self.replays += 1
+        e._finish_graph_step()
+        return static_loss
+
+    def _capture(self, key, args):
+        static_in = tuple(a.detach().clone() if torch.is_tensor(a) else a for a in args)
+        torch.cuda.synchronize(self.e.device)
+        graph = torch.cuda.CUDAGraph()
+        # capture records the launches without running them: the step counter advance is replayed,
+        # not double-counted
+        with torch.cuda.graph(graph, pool=self.pool):
+            static_loss = self._body(*static_in)
+        entry = (graph, static_in, static_loss)
+        self.graphs[key] = entry
+        return entry
+
+    def close(self) -> None:
+        self.graphs.clear()
+        if self.rccl is not None:
+            self.rccl.close()
+            self.rccl = None

@@ -171,3 +171,19 @@ def test_simplenet_engine_reproduces_reference_epoch_loss():
         tot += loss.item()
     assert round(tot / len(data), 4) == 0.4301  # SURVEY §6.2 oracle, ws=1 epoch 1
     engine.close()
+
+
+def test_hip_graph_config_falls_back_to_eager_on_cpu():
+    import distributed_gpu_test_amd as dgt
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 1))
+    engine, _, _, _ = dgt.initialize(model=m, config={"train_batch_size": 4, "amd": {"hip_graph": True}})
+    crit = torch.nn.BCEWithLogitsLoss()
+    step = engine.graph_step(lambda bx, by: crit(engine(bx), by))
+    assert engine.graphed is None and "GPU" in engine.graph_fallback_reason
+    x, y = torch.randn(4, 8), (torch.rand(4, 1) > 0.5).float()
+    l0 = float(step(x, y))
+    for _ in range(20):
+        loss = float(step(x, y))
+    assert loss < l0 and engine.global_steps == 21
+    engine.close()

@@ -57,3 +57,40 @@ def test_engine_gpu_bf16():
     assert float(loss) < first
     torch.testing.assert_close(engine.master.to(torch.bfloat16), engine.store.param_buf)
     engine.close()
+
+
+def _run_engine(cfg, batches, seed=4, graph=False):
+    m = _mlp(seed)
+    engine, _, _, _ = dgt.initialize(model=m, optimizer=torch.optim.Adam(m.parameters(), lr=1e-3), config=cfg)
+    crit = torch.nn.BCEWithLogitsLoss()
+    losses = []
+    if graph:
+        step = engine.graph_step(lambda bx, by: crit(engine(bx).float(), by))
+        assert engine.graphed is not None, engine.graph_fallback_reason
+        for x, y in batches:
+            losses.append(float(step(x, y)))  # the static loss must be read before the next replay
+    else:
+        for x, y in batches:
+            loss = crit(engine(x).float(), y)
+            engine.backward(loss)
+            engine.step()
+            losses.append(float(loss))
+    params = engine.store.param_buf.detach().clone()
+    return engine, losses, params
+
+
+@pytest.mark.parametrize("extra", [{}, {"gradient_clipping": 0.5}, {"zero_optimization": {"stage": 1}}])
+def test_engine_hip_graph_matches_eager(extra):
+    """Whole-step HIP-graph replay (forward + backward + Adam from a device step counter) gives the
+    eager engine's trajectory, including a second captured shape (a short batch)."""
+    batches = _batches(12, 5) + _batches(1, 6, bs=8) + _batches(12, 7) + _batches(4, 8, bs=8)
+    cfg = {"train_batch_size": 32, **extra}
+    e1, l1, p1 = _run_engine(dict(cfg), batches)
+    e2, l2, p2 = _run_engine(dict(cfg, amd={"hip_graph": True}), batches, graph=True)
+    assert e2.graphed.replays >= 20 and not e2.graphed.failed, (e2.graphed.replays, e2.graphed.failed)
+    assert len(e2.graphed.graphs) == 2  # one per input shape
+    assert e2.global_steps == len(batches)
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
+    e1.close()
+    e2.close()

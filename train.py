@@ -139,6 +139,13 @@ def main(argv=None) -> int:
             if found:
                 engine.load_checkpoint(found[1])
                 start_epoch = found[0] + 1
+        train_step = None
+        if cfg.amd.hip_graph:
+            train_step = engine.graph_step(lambda bx, by: criterion(engine(bx).float(), by))
+            if comm.get_rank() == 0:
+                why = engine.graph_fallback_reason
+                print(f"[dgt] hip_graph={'on' if engine.graphed is not None else 'off (' + why + ')'}",
+                      file=sys.stderr, flush=True)
         from distributed_gpu_test_amd.utils.tracing import Profiler
         prof = Profiler(args.profile, comm.get_rank())
         with prof:
@@ -148,10 +155,13 @@ def main(argv=None) -> int:
                 loss_acc = torch.zeros((), dtype=torch.float64, device=device)
                 steps = 0
                 for batch_x, batch_y in data:
-                    logits = engine(batch_x)
-                    loss = criterion(logits.float(), batch_y)
-                    engine.backward(loss)
-                    engine.step()
+                    if train_step is not None:  # whole step replayed from a HIP graph
+                        loss = train_step(batch_x, batch_y)
+                    else:
+                        logits = engine(batch_x)
+                        loss = criterion(logits.float(), batch_y)
+                        engine.backward(loss)
+                        engine.step()
                     prof.step()
                     loss_acc += loss.detach().double()  # on device: no per-step host sync
                     steps += 1
