@@ -1,6 +1,7 @@
 # distributed-gpu-test for AMD Instinct MI355X: ROCm PyTorch base, no CUDA image, no CUDA shims,
 # no Triton on the compute path.  The HIP extension and the rccl_perf tool are compiled for gfx950
 # at build time (hipcc cross-compiles; no GPU needed during `docker build`).
+# Reference: Dockerfile:2-16 (nvcr CUDA 12.8 base + pip torch/deepspeed) -> rocm/pytorch + in-tree HIP build.
 ARG BASE_IMAGE=rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.7.1
 FROM ${BASE_IMAGE}
 

@@ -3,6 +3,7 @@
 // bias-correction .item() syncs.  Memory-bound: 16-byte vector accesses on
 // every stream (Guideline 13), nontemporal hints (each byte is touched once), one float4 group per
 // thread over a full grid: 6.1 TB/s on the bench MLP's 67M parameters (scripts/bench_adam.py).
+// Reference: torch.optim.Adam created at train.py:85, stepped by model_engine.step() at train.py:114.
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include "dgt_common.h"

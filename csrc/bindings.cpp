@@ -1,6 +1,7 @@
 // torch.ops.dgt.* bindings for the MI355X kernels and the IPC runtime.
 // Host-only translation unit: validates shapes/devices, picks the current HIP stream, and calls
 // the launch functions declared in dgt_kernels.h.  Every op fails loudly on a non-GPU tensor.
+// Reference: the ops that replace train.py:85 (Adam), train.py:107/113 (forward/backward), train.py:113 (all-reduce).
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>

@@ -11,6 +11,7 @@
 //
 // Mailbox slot layout (words): float4 i -> LL lines 2*(i/64) and 2*(i/64)+1, lane i%64 -> every
 // wave-instruction writes or reads 1 KiB contiguous.
+// Reference: the gradient all-reduce of model_engine.backward, train.py:113.
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 

@@ -17,6 +17,7 @@
 // LDS-DMA writes base + 16*lane), so the bank-conflict XOR swizzle (chunk ^= row & 7 on 128-B rows)
 // is applied to the per-lane GLOBAL source address and undone on the ds_read_b128 side (rule 21).
 // Block ids are remapped so blocks sharing an XCD (id % 8) get neighbouring tiles (T1).
+// Reference: Linear(20,64) / Linear(64,1) of train.py:29-33, forward train.py:107, backward train.py:113.
 #include <hip/hip_bf16.h>
 #include "dgt_common.h"
 #include "dgt_kernels.h"

@@ -6,6 +6,7 @@
 //
 // Links against the librccl.so that PyTorch-ROCm already loads (same soname), so RCCL state is
 // shared with ProcessGroupNCCL's copy of the library rather than duplicated.
+// Reference: deepspeed.init_distributed() at train.py:59 and the all-reduce inside backward at train.py:113.
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>

@@ -33,6 +33,7 @@
 //     scale -> unflatten.
 //   * Adam's bias corrections come from a per-step table (torch's double-precision formula,
 //     filled by a one-thread-per-step kernel before the launch): no double math in the loop.
+// Reference: train.py:26-36 (model), 96 (loss), 98-117 (loop), 113 (all-reduce), 114 (Adam step).
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 

@@ -1,5 +1,7 @@
 """distributed_gpu_test_amd — an MI355X-native distributed GPU acceptance-test framework.
 
+Reference: ``train.py:10-12`` (deepspeed / get_accelerator imports) and ``train.py:59-94`` (init + initialize).
+
 Same capabilities as ``dashabalashova/distributed-gpu-test`` (train.py CLI, DeepSpeed-style JSON
 config, ZeRO-0/1 data parallelism, SLURM + Pyxis launch, CI), built for AMD Instinct MI355X:
 PyTorch-ROCm + hand-written HIP/CDNA4 kernels + RCCL over xGMI.

@@ -1,5 +1,7 @@
 """Bench-size synthetic MLP (BASELINE config #2: "1x MI355X single-process bf16 synthetic MLP").
 
+Reference: ``SimpleNet`` (``train.py:26-36``), widened and deepened.
+
 The reference trains Linear(20,64)-ReLU-Linear(64,1); that workload is launch/latency bound, so
 it cannot exercise the matrix cores.  This is the same architecture family scaled up:
 ``depth`` x [Linear(width, width) + ReLU] followed by Linear(width, 1) + BCE-with-logits, on

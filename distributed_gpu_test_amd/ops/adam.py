@@ -1,4 +1,7 @@
-"""Flat fused Adam dispatch: HIP kernel on GPU tensors, torch reference on CPU tensors."""
+"""Flat fused Adam dispatch: HIP kernel on GPU tensors, torch reference on CPU tensors.
+
+Reference: ``train.py:85`` (torch.optim.Adam) stepped at ``train.py:114``; SURVEY K15-K22.
+"""
 from __future__ import annotations
 
 from typing import Optional

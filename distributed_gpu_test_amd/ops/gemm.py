@@ -1,5 +1,7 @@
 """bf16 MFMA GEMM + MLP helper ops (``csrc/gemm.hip``) with plain-PyTorch references.
 
+Reference: the Linear layers of ``train.py:29-33`` (forward ``train.py:107``, backward ``train.py:113``), scaled up.
+
 ``gemm_nt`` computes ``C = alpha * A @ B.T`` (A[M,K], B[N,K], both bf16, fp32 accumulation) with
 optional fused epilogue: ``+ bias``, ``relu``, ``* 1[mask > 0]``, a transposed bf16 copy ``CT``,
 fp32 output / accumulation.  On GPU tensors it runs the HIP kernel (and raises if the extension

@@ -1,5 +1,7 @@
 """Native RCCL communicator (``csrc/rccl_comm.cpp``) for stream-ordered, graph-capturable collectives.
 
+Reference: the NCCL communicator behind ``deepspeed.init_distributed()`` (``train.py:59``) and ``train.py:113``.
+
 ``ProcessGroupNCCL`` (the ``nccl`` backend = RCCL on ROCm) is the general path.  This thin native
 communicator exists for the places where a collective must sit INSIDE a captured HIP graph next to
 the kernels that produce and consume its buffer (``TinyMLPTrainer(impl="graph")``): the collective

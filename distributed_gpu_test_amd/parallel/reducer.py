@@ -1,5 +1,7 @@
 """Bucketed gradient reduction overlapped with backward.
 
+Reference: the gradient all-reduce inside ``model_engine.backward`` (``train.py:113``); SURVEY X6/HC1.
+
 DeepSpeed stage 0 reduces ALL gradients after backward finishes (one 5e8-element bucket, SURVEY
 X6): communication never overlaps compute.  Here each bucket (a contiguous slice of the flat
 gradient buffer, ``runtime/flat.py``) is launched the moment autograd has accumulated the last

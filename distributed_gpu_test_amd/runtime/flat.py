@@ -1,5 +1,7 @@
 """Flat, bucket-aligned parameter and gradient storage.
 
+Reference: parameters moved/broadcast by ``deepspeed.initialize`` (``train.py:87-93``), grads reduced at ``train.py:113``.
+
 DeepSpeed (stage 0) keeps per-tensor ``.grad``s and, at the accumulation boundary, flattens them
 into a bucket, all-reduces, scales and unflattens back.  Here every parameter and
 gradient is a VIEW into one contiguous buffer from the start, so:

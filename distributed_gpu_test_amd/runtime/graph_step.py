@@ -1,5 +1,7 @@
 """Whole-training-step HIP graphs for the engine (DeepSpeed JSON ``"amd": {"hip_graph": true}``).
 
+Reference: one iteration of the loop ``train.py:103-115`` (forward, backward, step).
+
 A data-parallel step of a small model is launch-bound: eager PyTorch issues tens of kernels for
 forward + autograd backward, then the gradient collective, the optimizer and the host bookkeeping
 (~30 launches + a host sync per step of the reference).  MI355X-first, the step is

@@ -1,5 +1,7 @@
 """bf16 trainer for the bench-size synthetic MLP on the HIP MFMA GEMM (``csrc/gemm.hip``).
 
+Reference: the loop of ``train.py:98-117`` on a bench-size ``SimpleNet`` (``train.py:26-36``).
+
 One optimizer step, all on the GPU, no host sync:
 
     forward   a_l = relu(a_{l-1} W_l^T + b_l)   gemm_nt epilogue: bias + ReLU + bf16 a_l and a_l^T

@@ -1,5 +1,7 @@
 """Conversion between flat Adam buffers and ``torch.optim.Adam.state_dict()`` format.
 
+Reference: the optimizer state DeepSpeed writes with ``save_checkpoint`` (``train.py:125``).
+
 Checkpoints store optimizer state in torch's own per-parameter format so a checkpoint written by
 the fused HIP path can be loaded into a plain ``torch.optim.Adam`` (and vice versa).
 """

@@ -1,4 +1,7 @@
-"""DeepSpeed-compatible LR schedules (``scheduler.type`` in the JSON config) and the fp16 loss scaler."""
+"""DeepSpeed-compatible LR schedules (``scheduler.type`` in the JSON config) and the fp16 loss scaler.
+
+Reference: the DeepSpeed JSON dict of ``train.py:78-83`` (``fp16`` key) and the DS ``scheduler`` schema it accepts.
+"""
 from __future__ import annotations
 
 import math

@@ -1,5 +1,7 @@
 """Structured metrics: a JSONL sink and a throughput timer.
 
+Reference: ``train.py:119-121`` (epoch loss print) and DeepSpeed's ``steps_per_print`` progress lines.
+
 DeepSpeed's ``ThroughputTimer`` derives samples/sec from ``train_batch_size`` (which the reference
 hard-codes to 64 while the real global batch is 4 x world_size), so it over-reports.
 ``ThroughputTimer`` here counts the samples actually processed.  ``MetricsSink`` writes one JSON

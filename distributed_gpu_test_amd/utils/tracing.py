@@ -1,5 +1,7 @@
 """Tracing: roctx ranges and an optional torch.profiler session.
 
+Reference: the training loop ``train.py:98-117`` (no tracing there).
+
 The reference has no profiling.  Here every engine phase is wrapped in a named range (roctx on
 ROCm through ``torch.cuda.nvtx``, visible in ``rocprofv3 --marker-trace`` timelines), and
 ``train.py --profile DIR`` records a kineto trace of the first steps (Chrome-trace JSON per rank).

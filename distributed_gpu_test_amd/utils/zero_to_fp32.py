@@ -1,6 +1,8 @@
 #!/usr/bin/env python3
 """Consolidate a ZeRO-1/2 checkpoint into one fp32 state_dict (DeepSpeed's zero_to_fp32.py role).
 
+Reference: the script DeepSpeed copies next to checkpoints written at ``train.py:125``.
+
     python zero_to_fp32.py <checkpoint_dir> <output.pt> [--tag global_stepN]
 
 <checkpoint_dir> is the directory holding ``latest`` (e.g. ds_checkpoints/epoch5).  Each rank's
