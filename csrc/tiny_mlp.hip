@@ -259,7 +259,9 @@ DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row
 }
 
 // ------------------------------------------------------------------ persistent training kernel
-template <int F, int H, bool SMALLB>
+// XCH: world size > 1 (the exchange is compiled in).  The single-rank kernel has no exchange
+// branch, so backward and Adam form one basic block the scheduler can interleave.
+template <int F, int H, bool SMALLB, bool XCH>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
   __shared__ TinySmem<F, H> sm;
@@ -268,7 +270,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   const Exchange& ex = a.ex;
   WaveSmem<F, H>& ws = sm.w[w];
 
-  if (a.bmax > (SMALLB ? 4 : C::BM) || a.bmax < 1 || ex.world_size < 1 || ex.world_size > kMaxRanks ||
+  if (a.bmax > (SMALLB ? 4 : C::BM) || a.bmax < 1 || (ex.world_size > 1) != XCH || ex.world_size > kMaxRanks ||
       (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3)))) {
     if (t == 0) *a.status = kBadShape;
     return;
@@ -313,7 +315,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     float gbw = sg.bw, gb2 = sg.b2;
     DGT_STAMP(3);
 
-    if (ex.world_size > 1) {
+    if constexpr (XCH) {
       // ---- one-shot LL exchange of this wave's gradients over xGMI: push, poll, sum in rank order.
       // Every rank maps lanes to parameters identically, so the mailbox is lane-linear: lane l of
       // wave w packs its slots into NQ float4s = 2*NQ LL lines at [w][line][l]; every store
@@ -537,12 +539,16 @@ hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stre
                      a.adam_step0, a.lr, a.beta1, a.beta2);
 #define X_(F_, H_)                                                                            \
   if (f == F_ && h == H_) {                                                                   \
-    if (a.bmax <= 4)                                                                          \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, true>), dim3(1), dim3(TinyCfg<F_, H_>::T), 0, \
-                         stream, a);                                                          \
+    const dim3 blk(TinyCfg<F_, H_>::T);                                                       \
+    const bool xch = a.ex.world_size > 1;                                                     \
+    if (a.bmax <= 4 && !xch)                                                                  \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, true, false>), dim3(1), blk, 0, stream, a); \
+    else if (a.bmax <= 4)                                                                     \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, true, true>), dim3(1), blk, 0, stream, a); \
+    else if (!xch)                                                                            \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, false, false>), dim3(1), blk, 0, stream, a); \
     else                                                                                      \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, false>), dim3(1), dim3(TinyCfg<F_, H_>::T), 0, \
-                         stream, a);                                                          \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, false, true>), dim3(1), blk, 0, stream, a); \
     return hipGetLastError();                                                                 \
   }
   DGT_TINY_SHAPES(X_)
