@@ -100,42 +100,47 @@ DGT_DEVICE void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
   tn = (wgid % (GROUP * nbn)) / gsize;
 }
 
-// bf16-output epilogue of the 128 x 128 kernel, staged through the (then idle) operand LDS: the
-// MFMA layout gives each lane 4 rows of ONE column, so direct stores are 2-byte scatters; staged,
-// every global access (C rows, C^T rows, mask rows) is a 16-byte vector and 16 lanes cover one
-// 256-byte row piece.  The tile's 16-byte chunks are XOR-swizzled by row / 8, so both the row reads
-// (C) and the column reads (C^T: 16 lanes at rows 8k + e of one column) hit 16 distinct bank groups.
-// Values are rounded to bf16 once (after bias / ReLU) and masked after rounding (identical results:
-// the mask only zeroes).
-DGT_DEVICE int etile(int r, int n) { return r * 128 + ((((n >> 3) ^ (r >> 3)) & 15) << 3) + (n & 7); }
+// bf16-output epilogue staged through the (then idle) operand LDS, for a TM x TN block tile of NT
+// threads whose waves own WM x WN sub-tiles: the MFMA layout gives each lane 4 rows of ONE column,
+// so direct stores are 2-byte scatters; staged, every global access (C rows, C^T rows, mask rows)
+// is a 16-byte vector and 16 lanes cover one 256-byte row piece.  The low 4 bits of a row's
+// 16-byte chunk index are XOR-swizzled by row / 8, so both the row reads (C) and the column reads
+// (C^T: 16 lanes at rows 8k + e of one column) hit 16 distinct bank groups.  Values are rounded to
+// bf16 once (after bias / ReLU) and masked after rounding (identical results: the mask only zeroes).
+template <int TN>
+DGT_DEVICE int etile(int r, int n) {
+  const int c = n >> 3;
+  return r * TN + ((((c ^ (r >> 3)) & 15) | (c & ~15)) << 3) + (n & 7);
+}
 
-template <int EPI>
-DGT_DEVICE void epilogue_staged_128(const GemmArgs& g, const f32x4 (&acc)[4][4], u16* tile, int m0, int n0, int wr,
-                                    int wc, int l, int tid) {
+template <int EPI, int TM, int TN, int WM, int WN, int NT>
+DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN / 16], u16* tile, int m0, int n0,
+                                int wr, int wc, int l, int tid) {
   __syncthreads();  // every wave has finished reading the operand stages
 #pragma unroll
-  for (int j = 0; j < 4; ++j) {
-    const int nl = wc * 64 + j * 16 + (l & 15);
+  for (int j = 0; j < WN / 16; ++j) {
+    const int nl = wc * WN + j * 16 + (l & 15);
     const float bn = (EPI & kEpiBias) ? g.bias[n0 + nl] : 0.f;
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int ml = wr * 64 + i * 16 + 4 * (l >> 4);
+    for (int i = 0; i < WM / 16; ++i) {
+      const int ml = wr * WM + i * 16 + 4 * (l >> 4);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
         float x = acc[i][j][rr] * g.alpha + bn;
         if (EPI & kEpiRelu) x = fmaxf(x, 0.f);
-        tile[etile(ml + rr, nl)] = f2bf(x);
+        tile[etile<TN>(ml + rr, nl)] = f2bf(x);
       }
     }
   }
   __syncthreads();
   const u16* mask = static_cast<const u16*>(g.mask);
   u16* C = static_cast<u16*>(g.C);
+  constexpr int CPR = TN / 8;  // 16-byte chunks per row
   if ((EPI & kEpiMask) || C) {
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {  // 128 rows x 16 chunks of 8
-      const int idx = tid + 256 * it, r = idx >> 4, c = (idx & 15) * 8;
-      uint4 v = *reinterpret_cast<const uint4*>(tile + etile(r, c));
+    for (int it = 0; it < TM * CPR / NT; ++it) {
+      const int idx = tid + NT * it, r = idx / CPR, c = (idx % CPR) * 8;
+      uint4 v = *reinterpret_cast<const uint4*>(tile + etile<TN>(r, c));
       if (EPI & kEpiMask) {
         const uint4 mk = *reinterpret_cast<const uint4*>(mask + (long long)(m0 + r) * g.ldmask + n0 + c);
         unsigned* vw = reinterpret_cast<unsigned*>(&v);
@@ -146,7 +151,7 @@ DGT_DEVICE void epilogue_staged_128(const GemmArgs& g, const f32x4 (&acc)[4][4],
           const unsigned hi = __uint_as_float(mw[e] & 0xffff0000u) > 0.f ? 0xffff0000u : 0u;
           vw[e] &= lo | hi;
         }
-        if (EPI & kEpiStoreT) *reinterpret_cast<uint4*>(tile + etile(r, c)) = v;
+        if (EPI & kEpiStoreT) *reinterpret_cast<uint4*>(tile + etile<TN>(r, c)) = v;
       }
       if (C) *reinterpret_cast<uint4*>(C + (long long)(m0 + r) * g.ldc + n0 + c) = v;
     }
@@ -154,13 +159,14 @@ DGT_DEVICE void epilogue_staged_128(const GemmArgs& g, const f32x4 (&acc)[4][4],
   if (EPI & kEpiStoreT) {
     if (EPI & kEpiMask) __syncthreads();
     u16* CT = static_cast<u16*>(g.CT);
+    constexpr int CPC = TM / 8;  // 8-row chunks per column
 #pragma unroll
-    for (int it = 0; it < 8; ++it) {  // 128 columns x 16 chunks of 8 rows
-      const int idx = tid + 256 * it, n = idx >> 4, mc = (idx & 15) * 8;
+    for (int it = 0; it < TN * CPC / NT; ++it) {
+      const int idx = tid + NT * it, n = idx / CPC, mc = (idx % CPC) * 8;
       unsigned w[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
-        w[e] = (unsigned)tile[etile(mc + 2 * e, n)] | ((unsigned)tile[etile(mc + 2 * e + 1, n)] << 16);
+        w[e] = (unsigned)tile[etile<TN>(mc + 2 * e, n)] | ((unsigned)tile[etile<TN>(mc + 2 * e + 1, n)] << 16);
       *reinterpret_cast<uint4*>(CT + (long long)(n0 + n) * g.ldct + m0 + mc) = make_uint4(w[0], w[1], w[2], w[3]);
     }
   }
@@ -259,7 +265,7 @@ __global__ __launch_bounds__(256, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g
 
   // ---- epilogue: D col = l&15 (n), row = 4*(l>>4) + r (m)
   if constexpr (!(EPI & kEpiOutF32)) {
-    epilogue_staged_128<EPI>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
+    epilogue_staged<EPI, GBM, GBN, 64, 64, 256>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -466,11 +472,15 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   for (int it = 0; it + 1 < nit; ++it) iteration<false>(c, it, f, acc);
   iteration<true>(c, nit - 1, f, acc);
 
+  if constexpr (!(EPI & kEpiOutF32)) {
+    epilogue_staged<EPI, BM, BN, 128, 64, 512>(g, acc, lds, m0, n0, c.wr, c.wc, c.l, tid);
+  } else {
 #pragma unroll
-  for (int i = 0; i < 8; ++i)
+    for (int i = 0; i < 8; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j)
-      epi_store<EPI>(g, acc[i][j], m0 + c.wr * 128 + i * 16 + 4 * (c.l >> 4), n0 + c.wc * 64 + j * 16 + (c.l & 15));
+      for (int j = 0; j < 4; ++j)
+        epi_store<EPI>(g, acc[i][j], m0 + c.wr * 128 + i * 16 + 4 * (c.l >> 4), n0 + c.wc * 64 + j * 16 + (c.l & 15));
+  }
 }
 
 // variant: 0 = pick by shape, 1 = 128x128 2-stage, 2 = 256x256 8-phase, 3 = 128x128 4-stage

@@ -1,0 +1,23 @@
+#!/usr/bin/env python3
+"""Run one gemm_nt shape a few times (a compact target for rocprofv3 counter collection).
+
+    python scripts/gemm_one.py M N K [variant] [iters]
+"""
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_gpu_test_amd.ops.gemm import gemm_nt  # noqa: E402
+
+M, N, K = (int(a) for a in sys.argv[1:4])
+variant = int(sys.argv[4]) if len(sys.argv) > 4 else 0
+iters = int(sys.argv[5]) if len(sys.argv) > 5 else 10
+A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
+B = torch.randn(N, K, device="cuda").to(torch.bfloat16)
+C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+for _ in range(iters):
+    gemm_nt(A, B, C=C, variant=variant)
+torch.cuda.synchronize()
+print("ok", M, N, K, variant)
