@@ -33,6 +33,13 @@ REFERENCE_DS_CONFIG: Dict[str, Any] = {
     "zero_optimization": {"stage": 0},
 }
 
+# Default gradient bucket: 32 MiB (8M fp32 elements).  DeepSpeed's default (5e8 elements = 2 GB)
+# puts the whole model in one bucket, so nothing overlaps backward.  On an 8 x MI355X node a ring
+# all-reduce is bound by ONE xGMI link per hop (~153 GB/s) and RCCL splits a message
+# across its channels: 32 MiB gives every channel multi-MB pieces (near the bus-bandwidth plateau of
+# the rccl_perf sweep) while the first bucket still leaves backward after ~1/N of its work, so the
+# remaining buckets overlap the rest of backward.  Buckets at or below ``amd.oneshot_max_bytes``
+# (256 KiB) take the one-hop IPC exchange instead, where latency, not link bandwidth, rules.
 DEFAULT_BUCKET_BYTES = 32 * 1024 * 1024
 
 
