@@ -52,6 +52,9 @@ def parse_args(argv=None):
     ap.add_argument("--width", type=int, default=4096)
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--batch", type=int, default=1024, help="mlp: per-GPU micro-batch")
+    ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
+                    help="mlp: 0 = all-reduce the weight gradients; 1 = reduce-scatter them, shard Adam, "
+                         "all-gather bf16 weights (ZeRO-1/2)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce bus bandwidth sweep")
     ap.add_argument("--sweep-max-mb", type=int, default=256)
     return ap.parse_known_args(argv)[0]
@@ -198,7 +201,7 @@ def main(argv=None):
         from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
         model = SyntheticMLP(args.width, args.depth)
         B = args.batch
-        trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device)
+        trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device, zero_stage=args.zero_stage)
     elif args.impl == "engine":
         trainer = EngineBench(model, x, y, B, device)
     elif args.impl == "dgt-engine":

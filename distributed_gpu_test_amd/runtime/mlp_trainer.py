@@ -9,17 +9,28 @@ One optimizer step, all on the GPU, no host sync:
     backward  dW_l = g_l^T a_{l-1}   -> fp32 gradient buffer                           (gemm_nt)
               db_l = row sums of g_l^T                                              (rowsum_bf16)
               g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0] (+ g_{l-1}^T)   epilogue: mask      (gemm_nt)
-              each layer's gradient slice is all-reduced (RCCL over xGMI) as soon as its
-              wgrad is enqueued: the collective overlaps the remaining backward GEMMs
-    update    one fused Adam launch over the flat fp32 master (1/world_size folded in) that also
-              writes the bf16 compute copy; W_l^T refreshed by a tiled transpose
+              each layer's weight gradient leaves for its collective as soon as its wgrad is
+              enqueued (RCCL over xGMI on the process group's stream): the collective overlaps
+              the remaining backward GEMMs
+    update    fused Adam launches over flat fp32 masters that also write the bf16 compute copy;
+              W_l^T refreshed by a tiled transpose
 
-Parameters live in one flat fp32 buffer (+ a bf16 mirror); per-layer segments are 64-element
-aligned, so every GEMM operand and every gradient bucket is a contiguous, 16-byte aligned view.
+Parameters live in two flat regions:
+
+* the big region — the L weight matrices, bf16 for compute + fp32 gradients, each matrix padded to
+  a multiple of 64 * world_size elements (a per-layer communication bucket);
+* the small region — biases and the head, fp32 (the GEMM epilogues read fp32 biases), replicated
+  on every rank and all-reduced as one bucket.
+
+``zero_stage=0``: every rank keeps the full fp32 master of the big region; its buckets are
+all-reduced and one Adam launch updates everything.  ``zero_stage=1`` (DeepSpeed ZeRO-1/2 for the
+matrices): each bucket is REDUCE-SCATTERED into this rank's fp32 gradient shard, Adam updates
+only the 1/N master shard (N x less optimizer traffic and memory), and the bf16 parameter shards
+are ALL-GATHERED back: 4 + 2 bytes on the wire per parameter instead of an fp32 all-reduce's 8.
 """
 from __future__ import annotations
 
-from typing import List, Optional, Tuple
+from typing import Dict, List, Optional
 
 import torch
 import torch.distributed as dist
@@ -41,55 +52,82 @@ class MLPTrainer:
 
     def __init__(self, model: SyntheticMLP, batch_size: int = 1024, n_batches: int = 8, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 1234,
-                 device: Optional[torch.device] = None):
+                 device: Optional[torch.device] = None, zero_stage: int = 0):
+        if zero_stage not in (0, 1):
+            raise ValueError("MLPTrainer supports zero_stage 0 or 1")
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.model = model
         self.B, self.D, self.L, self.Din = batch_size, model.width, model.depth, model.in_features
         self.rank, self.world_size = comm.get_rank(), comm.get_world_size()
+        self.zero_stage = zero_stage if self.world_size > 1 else 0
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.global_steps = 0
-        dev = self.device
+        dev, ws = self.device, self.world_size
+        named = dict(model.named_parameters())
 
-        # ---- flat parameter layout: [W_l, b_l]*, head.w, head.b
-        self.segments: List[Tuple[str, Tuple[int, ...], int]] = []
+        # ---- big region: W_l, each padded to a multiple of ALIGN * world_size (one bucket each)
+        self.w_off: List[int] = []
+        self.w_len: List[int] = []
         off = 0
-        for name, p in model.named_parameters():
-            self.segments.append((name, tuple(p.shape), off))
-            off = _round(off + p.numel())
-        self.total = off
-        master = torch.zeros(self.total, dtype=torch.float32)
-        for (name, shape, o), p in zip(self.segments, model.parameters()):
-            master[o:o + p.numel()] = p.detach().reshape(-1).float()
-        self.master = master.to(dev)
-        comm.broadcast_(self.master, 0)
-        self.params_bf16 = self.master.to(torch.bfloat16)
-        self.grads = torch.zeros_like(self.master)
-        self.exp_avg = torch.zeros_like(self.master)
-        self.exp_avg_sq = torch.zeros_like(self.master)
-        seg = {n: (s, o) for n, s, o in self.segments}
-
-        def view(buf, name):
-            shape, o = seg[name]
-            n = 1
-            for d in shape:
-                n *= d
-            return buf[o:o + n].view(shape)
-
-        self.W = [view(self.params_bf16, f"layers.{i}.weight") for i in range(self.L)]
-        self.b = [view(self.master, f"layers.{i}.bias") for i in range(self.L)]
-        self.gW = [view(self.grads, f"layers.{i}.weight") for i in range(self.L)]
-        self.gb = [view(self.grads, f"layers.{i}.bias") for i in range(self.L)]
-        self.hw = view(self.master, "head.weight").view(-1)
-        self.hb = view(self.master, "head.bias").view(-1)
-        self.ghw = view(self.grads, "head.weight").view(-1)
-        self.ghb = view(self.grads, "head.bias").view(-1)
-        self.layer_slices = []  # contiguous gradient bucket per layer (W_l, b_l)
         for i in range(self.L):
-            _, o_w = seg[f"layers.{i}.weight"]
-            shape_b, o_b = seg[f"layers.{i}.bias"]
-            self.layer_slices.append((o_w, _round(o_b + shape_b[0])))
-        _, o_h = seg["head.weight"]
-        self.layer_slices.append((o_h, self.total))
+            self.w_off.append(off)
+            self.w_len.append(_round(named[f"layers.{i}.weight"].numel(), ALIGN * ws))
+            off += self.w_len[-1]
+        self.total_w = off
+        w_full = torch.zeros(self.total_w, dtype=torch.float32)
+        for i in range(self.L):
+            p = named[f"layers.{i}.weight"]
+            w_full[self.w_off[i]:self.w_off[i] + p.numel()] = p.detach().reshape(-1).float()
+        # ---- small region: b_l, head.weight, head.bias (fp32, replicated)
+        self.s_off: Dict[str, int] = {}
+        off = 0
+        for name in [f"layers.{i}.bias" for i in range(self.L)] + ["head.weight", "head.bias"]:
+            self.s_off[name] = off
+            off = _round(off + named[name].numel())
+        self.total_s = off
+        s_full = torch.zeros(self.total_s, dtype=torch.float32)
+        for name, o in self.s_off.items():
+            s_full[o:o + named[name].numel()] = named[name].detach().reshape(-1).float()
+        w_full, s_full = w_full.to(dev), s_full.to(dev)
+        comm.broadcast_(w_full, 0)  # DeepSpeed _broadcast_model
+        comm.broadcast_(s_full, 0)
+
+        self.params_bf16 = w_full.to(torch.bfloat16)  # compute copy of every W_l
+        self.grads_w = torch.zeros(self.total_w, dtype=torch.float32, device=dev)
+        self.master_s = s_full
+        self.grads_s = torch.zeros_like(self.master_s)
+        self.m_s, self.v_s = torch.zeros_like(self.master_s), torch.zeros_like(self.master_s)
+        if self.zero_stage == 0:
+            self.master_w = w_full
+            self.lp_w = self.params_bf16
+            self.shard_grad = None
+            self.shard_len = list(self.w_len)
+            self.shard_off = list(self.w_off)
+        else:  # this rank's 1/N of every bucket, concatenated
+            self.shard_len = [n // ws for n in self.w_len]
+            self.shard_off = [sum(self.shard_len[:i]) for i in range(self.L)]
+            pieces = [w_full[self.w_off[i] + self.rank * n:self.w_off[i] + (self.rank + 1) * n]
+                      for i, n in enumerate(self.shard_len)]
+            self.master_w = torch.cat(pieces).contiguous()
+            self.lp_w = torch.empty(self.master_w.numel(), dtype=torch.bfloat16, device=dev)
+            self.shard_grad = torch.zeros_like(self.master_w)
+            del w_full
+        self.m_w, self.v_w = torch.zeros_like(self.master_w), torch.zeros_like(self.master_w)
+
+        def wview(buf, i):
+            shape = named[f"layers.{i}.weight"].shape
+            return buf[self.w_off[i]:self.w_off[i] + shape[0] * shape[1]].view(shape)
+
+        def sview(buf, name):
+            o = self.s_off[name]
+            return buf[o:o + named[name].numel()]
+
+        self.W = [wview(self.params_bf16, i) for i in range(self.L)]
+        self.gW = [wview(self.grads_w, i) for i in range(self.L)]
+        self.b = [sview(self.master_s, f"layers.{i}.bias") for i in range(self.L)]
+        self.gb = [sview(self.grads_s, f"layers.{i}.bias") for i in range(self.L)]
+        self.hw, self.hb = sview(self.master_s, "head.weight"), sview(self.master_s, "head.bias")
+        self.ghw, self.ghb = sview(self.grads_s, "head.weight"), sview(self.grads_s, "head.bias")
         self.WT = [torch.empty(w.shape[1], w.shape[0], dtype=torch.bfloat16, device=dev) for w in self.W]
         self._refresh_transposes()
 
@@ -110,7 +148,8 @@ class MLPTrainer:
         transpose_bf16(self.X, self.XT)
         self.Y = y.to(dev)
         self.n_batches = n_batches
-        self.exchange = f"{comm.backend_name()}-allreduce-per-layer" if self.world_size > 1 else "none"
+        kind = "allreduce" if self.zero_stage == 0 else "reducescatter+allgather"
+        self.exchange = f"{comm.backend_name()}-{kind}-per-layer" if self.world_size > 1 else "none"
 
     # ------------------------------------------------------------------ helpers
     def _refresh_transposes(self):
@@ -120,15 +159,41 @@ class MLPTrainer:
     def flops_per_step(self) -> int:
         return self.model.flops_per_sample() * self.B
 
-    def _reduce_async(self, li: int, works: list):
+    def grad_of(self, name: str) -> torch.Tensor:
+        """This rank's local (pre-reduction) gradient of a model parameter, in its shape."""
+        p = dict(self.model.named_parameters())[name]
+        if name.startswith("layers.") and name.endswith("weight"):
+            return self.gW[int(name.split(".")[1])].reshape(p.shape)
+        o = self.s_off[name]
+        return self.grads_s[o:o + p.numel()].reshape(p.shape)
+
+    @staticmethod
+    def _collective(fn, out: torch.Tensor, *inp: torch.Tensor, works: list) -> None:
+        if comm.needs_host_staging(out):  # gloo rehearsal with GPU tensors: via host memory
+            host_out = out.detach().cpu()
+            fn(host_out, *[t.detach().cpu() for t in inp])
+            out.copy_(host_out)
+        else:
+            works.append(fn(out, *inp, async_op=True))
+
+    def _reduce_layer(self, i: int, works: list) -> None:
         if self.world_size == 1:
             return
-        lo, hi = self.layer_slices[li]
-        view = self.grads[lo:hi]
-        if comm.needs_host_staging(view):
-            comm.all_reduce_(view)
+        bucket = self.grads_w[self.w_off[i]:self.w_off[i] + self.w_len[i]]
+        if self.zero_stage == 0:
+            self._collective(dist.all_reduce, bucket, works=works)
         else:
-            works.append(dist.all_reduce(view, async_op=True))
+            out = self.shard_grad[self.shard_off[i]:self.shard_off[i] + self.shard_len[i]]
+            self._collective(dist.reduce_scatter_tensor, out, bucket, works=works)
+
+    def _allgather_params(self) -> None:
+        works: list = []
+        for i in range(self.L):
+            out = self.params_bf16[self.w_off[i]:self.w_off[i] + self.w_len[i]]
+            piece = self.lp_w[self.shard_off[i]:self.shard_off[i] + self.shard_len[i]]
+            self._collective(dist.all_gather_into_tensor, out, piece, works=works)
+        for w in works:
+            w.wait()
 
     # ------------------------------------------------------------------ one step
     def step(self, s: int) -> None:
@@ -149,22 +214,28 @@ class MLPTrainer:
         mlp_head(self.a[self.L], self.hw, self.hb, y, self.dz, self.ghw, self.ghb, self.loss_acc, self.g[cur],
                  self.gT[cur])
         works: list = []
-        self._reduce_async(self.L, works)
-        # backward, last layer first; each layer's gradient bucket leaves as soon as it is enqueued
+        # backward, last layer first; each weight bucket leaves as soon as its wgrad is enqueued
         for i in reversed(range(self.L)):
             a_prevT = xT if i == 0 else self.aT[i]
             gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=True)
             rowsum_bf16(self.gT[cur], self.gb[i])
-            self._reduce_async(i, works)
+            self._reduce_layer(i, works)
             if i > 0:
                 gemm_nt(self.g[cur], self.WT[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i])
                 cur ^= 1
+        if self.world_size > 1:  # biases + head: one small replicated bucket
+            self._collective(dist.all_reduce, self.grads_s, works=works)
         for w in works:
             w.wait()
         self.global_steps += 1
-        adam_flat_(self.master, self.grads, self.exp_avg, self.exp_avg_sq, self.global_steps, self.lr,
-                   self.betas[0], self.betas[1], self.eps, self.weight_decay, False,
-                   grad_scale=1.0 / self.world_size, param_lp=self.params_bf16)
+        scale = 1.0 / self.world_size
+        grads_w = self.grads_w if self.zero_stage == 0 else self.shard_grad
+        adam_flat_(self.master_w, grads_w, self.m_w, self.v_w, self.global_steps, self.lr, self.betas[0],
+                   self.betas[1], self.eps, self.weight_decay, False, grad_scale=scale, param_lp=self.lp_w)
+        adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, self.global_steps, self.lr, self.betas[0],
+                   self.betas[1], self.eps, self.weight_decay, False, grad_scale=scale)
+        if self.zero_stage == 1:
+            self._allgather_params()
         self._refresh_transposes()
 
     # bench.py adapter (same surface as TinyMLPTrainer)
@@ -178,7 +249,8 @@ class MLPTrainer:
 
     @property
     def params(self) -> torch.Tensor:
-        return self.master
+        """Every parameter as this rank sees it (bf16 matrices + fp32 small params), for checks."""
+        return torch.cat([self.params_bf16.float(), self.master_s])
 
     def check(self) -> None:
         pass

@@ -80,3 +80,14 @@ def test_engine_zero1_two_ranks_one_gpu(tmp_path):
     assert losses(r.stdout) == ORACLE2[:2]
     tag = tmp_path / "epoch2" / "global_step500"
     assert (tag / "zero_pp_rank_1_mp_rank_00_optim_states.pt").exists()
+
+
+def test_bench_mlp_zero1_two_ranks_one_gpu():
+    """bf16 MLP with ZeRO-1 (reduce-scatter, shard Adam, all-gather) on HIP tensors: ranks agree."""
+    r = run(2, "bench.py", "--gpus", "2", "--model", "mlp", "--width", "512", "--depth", "2", "--batch", "256",
+            "--zero-stage", "1", "--steps", "20", "--warmup", "2", "--no-sweep")
+    assert r.returncode == 0, r.stderr[-4000:]
+    import json
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["params_consistent_across_ranks"] is True
+    assert "reducescatter+allgather" in out["config"]["exchange"]

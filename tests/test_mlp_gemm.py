@@ -28,7 +28,7 @@ def _trainer_vs_torch(device):
     ref_loss = torch.nn.functional.binary_cross_entropy_with_logits(ref(x).view(-1), y)
     ref_loss.backward()
     tr.step(0)
-    got = torch.cat([tr.grads[o:o + p.numel()].cpu() for (_, _, o), p in zip(tr.segments, ref.parameters())])
+    got = torch.cat([tr.grad_of(n).reshape(-1).cpu() for n, _ in ref.named_parameters()])
     want = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
     return got, want, float(tr.loss_acc.item()), float(ref_loss)
 

@@ -111,3 +111,14 @@ def test_world_size_3_fails_batch_assertion():
     r = run(3, "--epochs", "1", "--no-save")
     assert r.returncode != 0
     assert "train_batch_size" in r.stderr
+
+
+def test_mlp_trainer_zero1_matches_zero0():
+    """bf16 MLP trainer: reduce-scatter + sharded Adam + all-gather == all-reduce + full Adam."""
+    r = run(2, script=os.path.join("tests", "mlp_zero_worker.py"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    m = re.search(r"RESULT diff=(\S+) rank_diff=(\S+) shard=(\d+) full=(\d+) exchange=(\S+)", r.stdout)
+    assert m, r.stdout[-2000:]
+    assert float(m.group(1)) == 0.0 and float(m.group(2)) == 0.0
+    assert int(m.group(3)) * 2 == int(m.group(4))
+    assert "reducescatter+allgather" in m.group(5)
