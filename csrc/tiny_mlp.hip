@@ -188,8 +188,16 @@ DGT_DEVICE void wave_forward(const LaneState<F, H>& st, WaveSmem<F, H>& ws, floa
 }
 
 struct StepGrads {
-  float bw, b2, loss;
+  float bw, b2, loss, z;  // z: the lane's logit (row l&15), for the deferred loss
 };
+
+// BCE-with-logits of one row, torch's form (1-y)*z - log_sigmoid(z); 1 + e^-|z| is in [1, 2], so
+// the raw v_log_f32 (log2) needs no denormal range fix-up.
+DGT_DEVICE float bce_term(float z, float y) {
+  const float e = __expf(-fabsf(z));
+  const float l1pe = __builtin_amdgcn_logf(1.f + e) * 0.6931471805599453f;
+  return (1.f - y) * z - (fminf(z, 0.f) - l1pe);
+}
 
 // After the barrier: logits, BCE, backward.  W1 gradients land in gw1 (slot layout).
 // SMALLB: micro-batch <= 4 (the reference's 4 per rank): only lanes 0..3 of a DPP row carry
@@ -211,10 +219,9 @@ DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws
   const float dz = valid ? (sig - y) * invB : 0.f;
   StepGrads out;
   out.loss = 0.f;
+  out.z = z;
   if (WANT_LOSS) {
-    // 1 + e is in [1, 2]: the raw v_log_f32 (log2) needs no denormal range fix-up
-    const float l1pe = __builtin_amdgcn_logf(1.f + e) * 0.6931471805599453f;
-    const float term = valid ? (1.f - y) * z - (fminf(z, 0.f) - l1pe) : 0.f;
+    const float term = valid ? bce_term(z, y) : 0.f;
     out.loss = (SMALLB ? quad_sum(term) : wave_sum16(term)) * invB;
   }
   float dw2[4];
@@ -254,6 +261,11 @@ DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws
   return out;
 }
 
+// sum over the wave of the ring's (row, step) terms, each weighted 1/B of its step (0 = empty)
+DGT_DEVICE float deferred_loss(float zs, float ys, float ibs) {
+  return wave_sum(ibs != 0.f ? bce_term(zs, ys) * ibs : 0.f);
+}
+
 DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row) {
   return (step < n_steps && row < bmax) ? plan[(long long)step * bmax + row] : -1;
 }
@@ -289,6 +301,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   __syncthreads();
 
   double loss_total = 0.0;
+  float zs = 0.f, ys = 0.f, ibs = 0.f;  // deferred-loss ring (wave 0)
   const float inv_ws = 1.0f / (float)ex.world_size;
 #ifdef DGT_TINY_STAMPS
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0;
@@ -310,9 +323,23 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(2);
     if (sm.err) break;
     float gw1[C::NSP];
-    const StepGrads sg = (w == 0) ? wave_backward<F, H, true, SMALLB>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1)
-                                  : wave_backward<F, H, false, SMALLB>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
+    const StepGrads sg = wave_backward<F, H, false, SMALLB>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
     float gbw = sg.bw, gb2 = sg.b2;
+    // Deferred loss (reporting only, off the per-step critical path): wave 0's lane row lq keeps
+    // step s's logits when s % 4 == lq; every 4th step one wave-wide reduction folds 4 steps in.
+    // (Logging the logits to memory for a follow-up kernel measured slower: the store joins the
+    // in-order vmcnt queue the row prefetch waits on.)
+    if (w == 0) {
+      if (lq == (s & 3)) {
+        zs = sg.z;
+        ys = y;
+        ibs = lr < Bt ? invB : 0.f;
+      }
+      if ((s & 3) == 3) {
+        loss_total += (double)deferred_loss(zs, ys, ibs);
+        ibs = 0.f;
+      }
+    }
     DGT_STAMP(3);
 
     if constexpr (XCH) {
@@ -428,7 +455,6 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
       st.vbw = v.x;
       st.vb2 = v.y;
     }
-    loss_total += (double)sg.loss;
     // rotate the prefetch pipeline
 #pragma unroll
     for (int i = 0; i < C::NSP; ++i) x[i] = xn[i];
@@ -437,6 +463,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     idx_next2 = idx_next3;
     DGT_STAMP(5);
   }
+  if (w == 0) loss_total += (double)deferred_loss(zs, ys, ibs);  // the partial last ring
 #ifdef DGT_TINY_STAMPS
   if (a.stamps && l == 0 && w < 2)
     for (int i = 0; i < 5; ++i) a.stamps[w * 8 + i] = st_acc[i];
