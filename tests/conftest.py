@@ -21,3 +21,13 @@ def pytest_collection_modifyitems(config, items):
     for item in items:
         if "gpu" in item.keywords:
             item.add_marker(skip)
+
+
+@pytest.fixture(scope="session", autouse=True)
+def _teardown_process_group():
+    """Tests that initialise the default process group in-process (engine, graph impl, native RCCL)
+    share it; tear it down once at the end, as the reference's train.py:138 does."""
+    yield
+    import torch.distributed as dist
+    if dist.is_available() and dist.is_initialized():
+        dist.destroy_process_group()
