@@ -7,14 +7,15 @@ DeepSpeed's ``init_distributed`` to find ``RANK`` / ``MASTER_ADDR`` /
 ``scontrol show hostnames`` and hard-codes ``MASTER_PORT=12345``
 (``slurm_train.sbatch:14-15``).
 
-Here one resolver handles three launch modes, in priority order:
+Here one resolver handles four launch modes, in priority order:
 
 1. torchrun / ``torch.distributed.launch`` env (``RANK``, ``WORLD_SIZE`` ...);
 2. ``srun`` with one task per GPU (``SLURM_PROCID`` / ``SLURM_NTASKS`` ...);
    ``MASTER_ADDR`` is the first host of ``SLURM_JOB_NODELIST`` (parsed here,
    no ``scontrol`` needed) and the port is derived from ``SLURM_JOB_ID`` so two
    jobs on one head node do not collide (SURVEY Q16);
-3. bare ``python train.py``: a single rank on 127.0.0.1 (SURVEY Q1/Q9 fixed).
+3. ``mpirun`` (Open MPI ``OMPI_COMM_WORLD_*`` / MPICH ``PMI_*``), DeepSpeed's MPI discovery;
+4. bare ``python train.py``: a single rank on 127.0.0.1 (SURVEY Q1/Q9 fixed).
 """
 from __future__ import annotations
 
@@ -36,7 +37,7 @@ class RankInfo:
     node_rank: int
     master_addr: str
     master_port: int
-    source: str  # "torchrun" | "slurm" | "bare"
+    source: str  # "torchrun" | "slurm" | "mpi" | "bare"
 
     @property
     def is_distributed(self) -> bool:
@@ -166,6 +167,23 @@ def resolve_rank_info(env: Optional[Mapping[str, str]] = None) -> RankInfo:
         port = int(env["MASTER_PORT"]) if "MASTER_PORT" in env else slurm_master_port(
             env.get("SLURM_JOB_ID") or env.get("SLURM_JOBID"))
         return RankInfo(rank, local_rank, ws, lws, node_rank, master, port, "slurm")
+
+    # mpirun-launched ranks (DeepSpeed's init_distributed falls back to MPI discovery when the
+    # torchrun variables are missing): Open MPI, then MPICH / Intel MPI (PMI).  The
+    # rendezvous address comes from MASTER_ADDR / MASTER_PORT (exported to every rank, e.g.
+    # `mpirun -x MASTER_ADDR -x MASTER_PORT`); no mpi4py needed.
+    mpi = None
+    if "OMPI_COMM_WORLD_RANK" in env and "OMPI_COMM_WORLD_SIZE" in env:
+        mpi = ("OMPI_COMM_WORLD_RANK", "OMPI_COMM_WORLD_SIZE", "OMPI_COMM_WORLD_LOCAL_RANK",
+               "OMPI_COMM_WORLD_LOCAL_SIZE")
+    elif "PMI_RANK" in env and "PMI_SIZE" in env:
+        mpi = ("PMI_RANK", "PMI_SIZE", "MPI_LOCALRANKID", "MPI_LOCALNRANKS")
+    if mpi is not None:
+        rank, ws = int(env[mpi[0]]), int(env[mpi[1]])
+        local_rank = int(env.get(mpi[2], rank))
+        lws = int(env.get(mpi[3], ws))
+        return RankInfo(rank, local_rank, ws, lws, rank // max(lws, 1), env.get("MASTER_ADDR", "127.0.0.1"),
+                        int(env.get("MASTER_PORT", DEFAULT_PORT)), "mpi")
 
     return RankInfo(0, int(env.get("LOCAL_RANK", 0)), 1, 1, 0,
                     env.get("MASTER_ADDR", "127.0.0.1"),

@@ -150,3 +150,17 @@ def test_get_dataloader_helper():
     assert bx.shape == (32, 20) and by.shape == (32, 1)
     assert torch.equal(bx, x[:32])
     assert sum(b[0].shape[0] for b in dl) == 100
+
+
+def test_rank_info_mpi():
+    ompi = {"OMPI_COMM_WORLD_RANK": "5", "OMPI_COMM_WORLD_SIZE": "16", "OMPI_COMM_WORLD_LOCAL_RANK": "5",
+            "OMPI_COMM_WORLD_LOCAL_SIZE": "8", "MASTER_ADDR": "10.0.0.1", "MASTER_PORT": "29600"}
+    ri = resolve_rank_info(ompi)
+    assert (ri.rank, ri.world_size, ri.local_rank, ri.local_world_size, ri.node_rank, ri.source) == \
+        (5, 16, 5, 8, 0, "mpi")
+    assert (ri.master_addr, ri.master_port) == ("10.0.0.1", 29600)
+    pmi = {"PMI_RANK": "9", "PMI_SIZE": "16", "MPI_LOCALRANKID": "1", "MPI_LOCALNRANKS": "8"}
+    ri = resolve_rank_info(pmi)
+    assert (ri.rank, ri.local_rank, ri.node_rank, ri.master_addr) == (9, 1, 1, "127.0.0.1")
+    # torchrun variables win when both are present
+    assert resolve_rank_info({**ompi, "RANK": "0", "WORLD_SIZE": "1"}).source == "torchrun"
