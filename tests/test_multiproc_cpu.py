@@ -122,3 +122,20 @@ def test_mlp_trainer_zero1_matches_zero0():
     assert float(m.group(1)) == 0.0 and float(m.group(2)) == 0.0
     assert int(m.group(3)) * 2 == int(m.group(4))
     assert "reducescatter+allgather" in m.group(5)
+
+
+def test_mpirun_style_launch_matches_oracle(tmp_path):
+    """Ranks started the way mpirun starts them (only OMPI_COMM_WORLD_* + MASTER_* set)."""
+    port = free_port()
+    procs = []
+    for r in range(2):
+        e = {k: v for k, v in os.environ.items() if k not in ("RANK", "WORLD_SIZE", "LOCAL_RANK")}
+        e.update({"DGT_QUIET": "1", "OMPI_COMM_WORLD_RANK": str(r), "OMPI_COMM_WORLD_SIZE": "2",
+                  "OMPI_COMM_WORLD_LOCAL_RANK": str(r), "OMPI_COMM_WORLD_LOCAL_SIZE": "2",
+                  "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "OMP_NUM_THREADS": "1",
+                  "CUDA_VISIBLE_DEVICES": "", "HIP_VISIBLE_DEVICES": ""})
+        procs.append(subprocess.Popen([sys.executable, os.path.join(ROOT, "train.py"), "--epochs", "2", "--no-save"],
+                                      cwd=ROOT, env=e, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    outs = [p.communicate(timeout=300) for p in procs]
+    assert all(p.returncode == 0 for p in procs), outs[0][1][-2000:] + outs[1][1][-2000:]
+    assert epoch_losses(outs[0][0]) == ORACLE[2][:2]
