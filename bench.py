@@ -201,7 +201,10 @@ def main(argv=None):
         from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
         model = SyntheticMLP(args.width, args.depth)
         B = args.batch
-        trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device, zero_stage=args.zero_stage)
+        if args.impl == "engine":
+            trainer = TorchMLPBench(model, B, device)
+        else:
+            trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device, zero_stage=args.zero_stage)
     elif args.impl == "engine":
         trainer = EngineBench(model, x, y, B, device)
     elif args.impl == "dgt-engine":
@@ -336,6 +339,60 @@ class EngineBench:
             self.opt.step()
             self.loss_acc += loss.item()  # the reference's per-step host sync (train.py:115)
         self.params = torch.nn.utils.parameters_to_vector(self.model.parameters()).detach()
+
+    def check(self):
+        pass
+
+    def close(self):
+        pass
+
+
+class TorchMLPBench:
+    """The reference-equivalent stack for the bench-size MLP (BASELINE config #2): nn.Module with
+    fp32 parameters, bf16 autocast (hipBLASLt GEMMs), autograd, bucketed DDP-style all-reduce
+    (torch's own Reducer via DistributedDataParallel when N > 1) and torch's fused Adam."""
+
+    impl = "torch-autocast-bf16"
+
+    def __init__(self, model, B, device, n_batches=8, seed=1234):
+        from distributed_gpu_test_amd.models.synthetic_mlp import synthetic_batch_data
+        from distributed_gpu_test_amd.parallel import comm
+        self.world, self.rank = comm.get_world_size(), comm.get_rank()
+        self.device, self.B, self.n_batches = device, B, n_batches
+        self.model = model.to(device)
+        if self.world > 1:
+            self.model = torch.nn.parallel.DistributedDataParallel(self.model, device_ids=[device.index])
+        self.opt = torch.optim.Adam(self.model.parameters(), lr=1e-4, fused=device.type == "cuda")
+        x, y = synthetic_batch_data(B * n_batches, model.in_features, seed + self.rank)
+        self.X, self.Y = x.to(device), y.to(device)
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=device)
+        self.global_steps = 0
+        self.exchange = f"{comm.backend_name()}-ddp" if self.world > 1 else "none"
+        self._flops = model.flops_per_sample() * B
+
+    def flops_per_step(self):
+        return self._flops
+
+    def epoch_plan(self, epoch):
+        plan = torch.arange(self.n_batches, dtype=torch.int32).view(-1, 1)
+        return plan, torch.ones(self.n_batches, dtype=torch.int32)
+
+    def run_plan(self, plan, counts):
+        crit = torch.nn.BCEWithLogitsLoss()
+        for _ in range(int(plan.shape[0])):
+            j = self.global_steps % self.n_batches
+            x, y = self.X[j * self.B:(j + 1) * self.B], self.Y[j * self.B:(j + 1) * self.B]
+            with torch.autocast(device_type=self.device.type, dtype=torch.bfloat16):
+                loss = crit(self.model(x).view(-1).float(), y)
+            self.opt.zero_grad(set_to_none=True)
+            loss.backward()
+            self.opt.step()
+            self.loss_acc += loss.detach().double()
+            self.global_steps += 1
+
+    @property
+    def params(self):
+        return torch.nn.utils.parameters_to_vector(self.model.parameters()).detach()
 
     def check(self):
         pass
