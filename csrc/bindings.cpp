@@ -248,8 +248,9 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
 void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant) {
-  TORCH_CHECK(variant >= 0 && variant <= 3,
-              "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256) or 3 (128x128, 4 stages)");
+  TORCH_CHECK(variant >= 0 && variant <= 4,
+              "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (128x128, 4 stages) "
+              "or 4 (128x128, 4 stages, 8 waves)");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {  // rows may be strided (column blocks of a wider matrix)

@@ -36,10 +36,12 @@ DGT_DEVICE u16 f2bf(float f) {
 DGT_DEVICE float bf2f(u16 u) { return __uint_as_float(((unsigned)u) << 16); }
 
 // one 128 x 64 bf16 operand tile: 16 LDS-DMA wave-instructions of 1 KiB (8 rows each), 4 per wave
+template <int NWAVE = 4>
 DGT_DEVICE void stage_tile(const u16* __restrict__ src, int ld, int row0, int k0, u16* lds, int w, int l) {
+  constexpr int PER_WAVE = 16 / NWAVE;         // 1 KiB wave-instructions per wave (8 rows each)
 #pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int rblk = (w * 4 + i) * 8;          // first of the 8 rows this wave-instruction writes
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int rblk = (w * PER_WAVE + i) * 8;   // first of the 8 rows this wave-instruction writes
     const int row = rblk + (l >> 3);
     const int p = l & 7;                       // LDS 16-B chunk this lane lands in
     const int c = p ^ (row & 7);               // logical chunk fetched (source-side swizzle)
@@ -182,22 +184,28 @@ DGT_DEVICE void wait_vmcnt() {
   __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
 }
 
-template <int EPI, int S>
-__global__ __launch_bounds__(256, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
+// NW = 4: waves 2 (M) x 2 (N), 64 x 64 each (4 x 4 accumulators).  NW = 8: waves 2 x 4, 64 x 32
+// each: two waves per SIMD, so one wave's LDS fragment reads overlap the other's MFMAs (the
+// 4-wave block leaves the matrix core idle while its only wave waits on LDS).
+template <int EPI, int S, int NW = 4>
+__global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
+  constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
+  constexpr int WCOLS = GBN / WN;                // waves across N
+  constexpr int NJ = WN / 16;                    // accumulator columns per wave
   __shared__ __attribute__((aligned(16))) u16 lds[S][2][GBM * GBK];  // [stage][A|B], 32 KiB per stage
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   int tm, tn;
   tile_of_block(blockIdx.x, g.M / GBM, g.N / GBN, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
-  const int wr = w >> 1, wc = w & 1;
+  const int wr = w / WCOLS, wc = w % WCOLS;
   const u16* A = static_cast<const u16*>(g.A);
   const u16* B = static_cast<const u16*>(g.B);
 
-  f32x4 acc[4][4];
+  f32x4 acc[4][NJ];
 #pragma unroll
   for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   const int nk = g.K / GBK;
   auto compute = [&](int buf) {
@@ -206,40 +214,40 @@ __global__ __launch_bounds__(256, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g
 #pragma unroll
     for (int kk = 0; kk < GBK / 32; ++kk) {
       const int chunk = kk * 4 + (l >> 4);
-      bf16x8 af[4], bfr[4];
+      bf16x8 af[4], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = read_frag(As, wr * 64 + i * 16 + (l & 15), chunk);
 #pragma unroll
-      for (int j = 0; j < 4; ++j) bfr[j] = read_frag(Bs, wc * 64 + j * 16 + (l & 15), chunk);
+      for (int j = 0; j < NJ; ++j) bfr[j] = read_frag(Bs, wc * WN + j * 16 + (l & 15), chunk);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
-        for (int j = 0; j < 4; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
     }
   };
   if constexpr (S == 2) {
-    stage_tile(A, g.lda, m0, 0, lds[0][0], w, l);
-    stage_tile(B, g.ldb, n0, 0, lds[0][1], w, l);
+    stage_tile<NW>(A, g.lda, m0, 0, lds[0][0], w, l);
+    stage_tile<NW>(B, g.ldb, n0, 0, lds[0][1], w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < nk) {
-        stage_tile(A, g.lda, m0, (kt + 1) * GBK, lds[cur ^ 1][0], w, l);
-        stage_tile(B, g.ldb, n0, (kt + 1) * GBK, lds[cur ^ 1][1], w, l);
+        stage_tile<NW>(A, g.lda, m0, (kt + 1) * GBK, lds[cur ^ 1][0], w, l);
+        stage_tile<NW>(B, g.ldb, n0, (kt + 1) * GBK, lds[cur ^ 1][1], w, l);
       }
       compute(cur);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
   } else {
-    constexpr int PER_TILE = 8;  // glds per thread per K-tile (A and B: 4 each)
+    constexpr int PER_TILE = 2 * (16 / NW);  // glds per thread per K-tile (A and B)
 #pragma unroll
     for (int p = 0; p < S - 1; ++p) {
       if (p < nk) {
-        stage_tile(A, g.lda, m0, p * GBK, lds[p][0], w, l);
-        stage_tile(B, g.ldb, n0, p * GBK, lds[p][1], w, l);
+        stage_tile<NW>(A, g.lda, m0, p * GBK, lds[p][0], w, l);
+        stage_tile<NW>(B, g.ldb, n0, p * GBK, lds[p][1], w, l);
       }
     }
     int buf = 0;
@@ -254,8 +262,8 @@ __global__ __launch_bounds__(256, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g
       __builtin_amdgcn_sched_barrier(0);
       if (kt + S - 1 < nk) {
         const int nb = (buf + S - 1) % S;
-        stage_tile(A, g.lda, m0, (kt + S - 1) * GBK, lds[nb][0], w, l);
-        stage_tile(B, g.ldb, n0, (kt + S - 1) * GBK, lds[nb][1], w, l);
+        stage_tile<NW>(A, g.lda, m0, (kt + S - 1) * GBK, lds[nb][0], w, l);
+        stage_tile<NW>(B, g.ldb, n0, (kt + S - 1) * GBK, lds[nb][1], w, l);
       }
       compute(buf);
       buf = (buf + 1 == S) ? 0 : buf + 1;
@@ -265,13 +273,13 @@ __global__ __launch_bounds__(256, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g
 
   // ---- epilogue: D col = l&15 (n), row = 4*(l>>4) + r (m)
   if constexpr (!(EPI & kEpiOutF32)) {
-    epilogue_staged<EPI, GBM, GBN, 64, 64, 256>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
+    epilogue_staged<EPI, GBM, GBN, 64, WN, 64 * NW>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j)
-        epi_store<EPI>(g, acc[i][j], m0 + wr * 64 + i * 16 + 4 * (l >> 4), n0 + wc * 64 + j * 16 + (l & 15));
+      for (int j = 0; j < NJ; ++j)
+        epi_store<EPI>(g, acc[i][j], m0 + wr * 64 + i * 16 + 4 * (l >> 4), n0 + wc * WN + j * 16 + (l & 15));
   }
 }
 
@@ -483,14 +491,15 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   }
 }
 
-// variant: 0 = pick by shape, 1 = 128x128 2-stage, 2 = 256x256 8-phase, 3 = 128x128 4-stage
+// variant: 0 = pick by shape, 1 = 128x128 2-stage, 2 = 256x256 8-phase, 3 = 128x128 4-stage,
+// 4 = 128x128 4-stage with 8 waves
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0;
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks,
   // 2 blocks per CU) wins
   bool big = fits256 && (g.M / 256) * (g.N / 256) >= 200;
-  if (variant == 1 || variant == 3) big = false;
+  if (variant == 1 || variant == 3 || variant == 4) big = false;
   if (variant == 2) {
     if (!fits256) return hipErrorInvalidValue;
     big = true;
@@ -498,10 +507,12 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   const int grid = big ? (g.M / 256) * (g.N / 256) : (g.M / GBM) * (g.N / GBN);
   // a grid that fits the chip at one block per CU gains nothing from 2 blocks/CU: spend the LDS on
   // a deep (4-stage) pipeline instead
-  const bool deep = !big && (variant == 3 || (variant == 0 && grid <= 256));
+  const bool deep = !big && (variant == 3 || variant == 4 || (variant == 0 && grid <= 256));
+  const bool eight = deep && variant != 3;  // measured: 8 waves beat 4 on one-wave grids (817 vs 759 TF)
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
     if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
+    else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else if (deep) hipLaunchKernelGGL((gemm_nt_kernel<E, 4>), dim3(grid), dim3(256), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;

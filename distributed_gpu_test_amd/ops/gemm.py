@@ -41,7 +41,7 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
             bias: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, relu: bool = False,
             out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0) -> None:
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage, 2 = 256x256 8-phase pipeline,
-    3 = 128x128 tiles 4-stage."""
+    3 = 128x128 tiles 4-stage, 4 = 128x128 tiles 4-stage with 8 waves."""
     if not A.is_cuda:
         gemm_nt_reference(A, B, C, CT, bias, mask, relu, out_f32, accumulate, alpha)
         return

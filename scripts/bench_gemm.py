@@ -59,6 +59,7 @@ def main():
         t_ours32 = bench(lambda: gemm_nt(A, B, C=Cf, out_f32=True))
         t_128 = bench(lambda: gemm_nt(A, B, C=C, variant=1))
         t_128d = bench(lambda: gemm_nt(A, B, C=C, variant=3))
+        t_128e = bench(lambda: gemm_nt(A, B, C=C, variant=4))
         fits256 = M % 256 == 0 and N % 256 == 0 and K % 128 == 0
         t_256 = bench(lambda: gemm_nt(A, B, C=C, variant=2)) if fits256 else None
         t_torch = bench(lambda: torch.matmul(A, B.t(), out=C))
@@ -72,12 +73,14 @@ def main():
             extra["T_only_us"] = round(bench(lambda: gemm_nt(A, B, CT=CT, bias=bias, relu=True)) * 1e6, 1)
             extra["dgrad_mask_T_us"] = round(bench(lambda: gemm_nt(A, B, C=C, CT=CT, mask=mask)) * 1e6, 1)
             extra["fwd_bias_relu_T_cold_us"] = round(bench_cold(lambda: gemm_nt(A, B, C=C, CT=CT, bias=bias, relu=True)) * 1e6, 1)
+            extra["fwd_bias_relu_T_cold_8wave_us"] = round(bench_cold(lambda: gemm_nt(A, B, C=C, CT=CT, bias=bias, relu=True, variant=4)) * 1e6, 1)
             extra["fwd_bias_relu_T_cold_2stage_us"] = round(bench_cold(lambda: gemm_nt(A, B, C=C, CT=CT, bias=bias, relu=True, variant=1)) * 1e6, 1)
             extra["torch_cold_us"] = round(bench_cold(lambda: torch.matmul(A, B.t(), out=C)) * 1e6, 1)
         print(json.dumps({"M": M, "N": N, "K": K, "dgt_TFLOPs": round(flops / t_ours / 1e12, 1),
                           "dgt_f32out_TFLOPs": round(flops / t_ours32 / 1e12, 1),
                           "dgt_tile128_TFLOPs": round(flops / t_128 / 1e12, 1),
                           "dgt_tile128_4stage_TFLOPs": round(flops / t_128d / 1e12, 1),
+                          "dgt_tile128_4stage_8wave_TFLOPs": round(flops / t_128e / 1e12, 1),
                           "dgt_tile256_TFLOPs": round(flops / t_256 / 1e12, 1) if t_256 else None,
                           "torch_hipblaslt_TFLOPs": round(flops / t_torch / 1e12, 1),
                           "dgt_us": round(t_ours * 1e6, 1), "torch_us": round(t_torch * 1e6, 1), **extra}), flush=True)

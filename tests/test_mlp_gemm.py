@@ -53,7 +53,8 @@ gpu = pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 1), (512, 256, 1024, 1),
                                            (256, 256, 128, 2), (512, 768, 256, 2), (768, 512, 1152, 2),
                                            (128, 128, 64, 3), (256, 128, 128, 3), (384, 256, 192, 3),
-                                           (512, 256, 1024, 3)])
+                                           (512, 256, 1024, 3), (128, 128, 64, 4), (384, 256, 192, 4),
+                                           (512, 256, 1024, 4)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "mask_T", "f32", "f32_acc"])
 def test_gemm_nt_matches_reference(M, N, K, variant, epi):
     g = torch.Generator().manual_seed(M + N + K)
@@ -82,7 +83,7 @@ def test_gemm_nt_matches_reference(M, N, K, variant, epi):
 
 
 @gpu
-@pytest.mark.parametrize("n,variant", [(128, 1), (256, 2), (128, 3)])
+@pytest.mark.parametrize("n,variant", [(128, 1), (256, 2), (128, 3), (128, 4)])
 def test_gemm_identity_with_asymmetric_operand(n, variant):
     # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
     M = N = K = n
