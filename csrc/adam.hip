@@ -68,8 +68,8 @@ template <bool NT> struct Vec4<__half, NT> {
 };
 
 template <typename GT, typename LT, bool NT>
-DGT_DEVICE void adam_group(const AdamFlatArgs& a, const GT* __restrict__ grad, LT* __restrict__ lp, long long o,
-                           float scale, float step_size_neg, float bc2_sqrt) {
+DGT_DEVICE f32x4 adam_group(const AdamFlatArgs& a, const GT* __restrict__ grad, LT* __restrict__ lp, long long o,
+                            float scale, float step_size_neg, float bc2_sqrt) {
   f32x4 p = Vec4<float, NT>::load(a.master + o), g = Vec4<GT, NT>::load(grad + o);
   f32x4 m = Vec4<float, NT>::load(a.exp_avg + o), v = Vec4<float, NT>::load(a.exp_avg_sq + o);
 #pragma unroll
@@ -83,14 +83,15 @@ DGT_DEVICE void adam_group(const AdamFlatArgs& a, const GT* __restrict__ grad, L
   Vec4<float, NT>::store(a.exp_avg + o, m);
   Vec4<float, NT>::store(a.exp_avg_sq + o, v);
   if (lp) Vec4<LT, NT>::store(lp + o, p);
+  return p;
 }
 
-// GROUPS float4 groups per thread per grid-stride iteration
-template <typename GT, typename LT, bool NT, int GROUPS>
-__global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
-  const long long n4 = a.n >> 2;
-  float step_size_neg = a.step_size_neg, bc2_sqrt = a.bc2_sqrt;
-  if (a.step_dev) {  // graph replay: bias corrections from the device step counter, in double
+// Bias corrections of this update: host scalars, or (graph replay) formed on the device from the
+// step counter in double, exactly as torch's non-capturable Adam does on the host.
+DGT_DEVICE void adam_bias_corrections(const AdamFlatArgs& a, float& step_size_neg, float& bc2_sqrt) {
+  step_size_neg = a.step_size_neg;
+  bc2_sqrt = a.bc2_sqrt;
+  if (a.step_dev) {
     __shared__ float sc[2];
     if (threadIdx.x == 0) {
       const double t = (double)*a.step_dev;
@@ -101,6 +102,14 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
     step_size_neg = sc[0];
     bc2_sqrt = sc[1];
   }
+}
+
+// GROUPS float4 groups per thread per grid-stride iteration
+template <typename GT, typename LT, bool NT, int GROUPS>
+__global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
+  const long long n4 = a.n >> 2;
+  float step_size_neg, bc2_sqrt;
+  adam_bias_corrections(a, step_size_neg, bc2_sqrt);
   float scale = a.grad_scale;
   if (a.grad_scale_dev) scale *= *a.grad_scale_dev;
   const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
@@ -153,6 +162,64 @@ static hipError_t launch_adam_g(const AdamFlatArgs& a, hipStream_t s) {
       b.param_lp = nullptr;  // fp32 params are the master buffer itself
       launch_adam_v<GT, float>(b, s);
     }
+  }
+  return hipGetLastError();
+}
+
+// Adam over one row-major fp32 weight matrix [rows, cols] that writes the bf16 compute copy AND
+// its transpose (the dgrad GEMM's B operand, csrc/gemm.hip) in the same pass, instead of Adam
+// followed by a transpose kernel that re-reads the bf16 copy (the MLP trainer's W^T refresh).
+// Lane (rb, cg) of a wave updates rows 8rb..8rb+7 x cols 4cg..4cg+3 (rb, cg in 0..7): the eight
+// lanes of one rb read a whole 128-byte line of every fp32 stream per row, and the eight lanes of
+// one cg write a whole 128-byte line of W^T (64 rows x bf16) per column with 16-byte stores.
+// No LDS: every transposed value is already in the register that stores it.  A block's four
+// waves sit side by side along the columns: block tile = 64 rows x 128 cols.
+template <typename GT>
+__global__ __launch_bounds__(256) void adam_matrix_t_kernel(AdamFlatArgs a, __hip_bfloat16* __restrict__ lpT,
+                                                            int rows, int cols) {
+  float step_size_neg, bc2_sqrt;
+  adam_bias_corrections(a, step_size_neg, bc2_sqrt);
+  float scale = a.grad_scale;
+  if (a.grad_scale_dev) scale *= *a.grad_scale_dev;
+  const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
+  __hip_bfloat16* __restrict__ lp = static_cast<__hip_bfloat16*>(a.param_lp);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int cg = lane & 7, rb = lane >> 3;
+  const int c = blockIdx.x * 128 + wave * 32 + cg * 4;
+  const int r = blockIdx.y * 64 + rb * 8;
+  unsigned short b[8][4];  // bf16 bits of the updated 8 x 4 block
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const f32x4 p = adam_group<GT, __hip_bfloat16, true>(a, grad, lp, (long long)(r + k) * cols + c, scale,
+                                                         step_size_neg, bc2_sqrt);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) b[k][e] = __bfloat16_as_ushort(__float2bfloat16(p[e]));
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    u32x4 v;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) v[q] = (unsigned)b[2 * q][e] | ((unsigned)b[2 * q + 1][e] << 16);
+    *reinterpret_cast<u32x4*>(lpT + (long long)(c + e) * rows + r) = v;
+  }
+}
+
+hipError_t adam_matrix_t(const AdamFlatArgs& a, void* lpT, int rows, int cols, hipStream_t stream) {
+  if (rows <= 0 || cols <= 0 || rows % 64 || cols % 128 || a.n != (long long)rows * cols || !a.param_lp ||
+      a.lp_dtype != kBF16 || !lpT)
+    return hipErrorInvalidValue;
+  const dim3 grid(cols / 128, rows / 64);
+  switch (a.grad_dtype) {
+    case kBF16:
+      hipLaunchKernelGGL(adam_matrix_t_kernel<__hip_bfloat16>, grid, dim3(256), 0, stream, a,
+                         static_cast<__hip_bfloat16*>(lpT), rows, cols);
+      break;
+    case kF32:
+      hipLaunchKernelGGL(adam_matrix_t_kernel<float>, grid, dim3(256), 0, stream, a,
+                         static_cast<__hip_bfloat16*>(lpT), rows, cols);
+      break;
+    default:
+      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

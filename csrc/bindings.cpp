@@ -165,10 +165,11 @@ void tiny_mlp_grad(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& p
 }
 
 // ------------------------------------------------------------------------------ Adam
-void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_lp, const at::Tensor& grad,
-               const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq, double lr, double beta1, double beta2,
-               double eps, double weight_decay, bool adamw, int64_t step, double grad_scale,
-               const std::optional<at::Tensor>& grad_scale_dev, const std::optional<at::Tensor>& step_dev) {
+dgt::AdamFlatArgs adam_args(const at::Tensor& master, const std::optional<at::Tensor>& param_lp,
+                            const at::Tensor& grad, const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq,
+                            double lr, double beta1, double beta2, double eps, double weight_decay, bool adamw,
+                            int64_t step, double grad_scale, const std::optional<at::Tensor>& grad_scale_dev,
+                            const std::optional<at::Tensor>& step_dev) {
   check_gpu(master, "master", at::kFloat);
   check_gpu(exp_avg, "exp_avg", at::kFloat);
   check_gpu(exp_avg_sq, "exp_avg_sq", at::kFloat);
@@ -178,7 +179,6 @@ void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_
   TORCH_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "dgt: flat size mismatch");
   const bool dev_step = step_dev.has_value() && step_dev->defined();
   TORCH_CHECK(dev_step || step >= 1, "dgt: adam step must be >= 1");
-  c10::DeviceGuard guard(master.device());
   dgt::AdamFlatArgs a;
   a.master = master.data_ptr<float>();
   a.param_lp = nullptr;
@@ -212,7 +212,35 @@ void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_
     check_gpu(*step_dev, "step_dev", at::kLong);
     a.step_dev = reinterpret_cast<const long long*>(step_dev->data_ptr<int64_t>());
   }
+  return a;
+}
+
+void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_lp, const at::Tensor& grad,
+               const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq, double lr, double beta1, double beta2,
+               double eps, double weight_decay, bool adamw, int64_t step, double grad_scale,
+               const std::optional<at::Tensor>& grad_scale_dev, const std::optional<at::Tensor>& step_dev) {
+  const dgt::AdamFlatArgs a = adam_args(master, param_lp, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
+                                        weight_decay, adamw, step, grad_scale, grad_scale_dev, step_dev);
+  c10::DeviceGuard guard(master.device());
   DGT_CHECK_HIP(dgt::adam_flat(a, stream_of(master)));
+}
+
+void adam_matrix_t(const at::Tensor& master, const at::Tensor& param_lp, const at::Tensor& param_lpT,
+                   const at::Tensor& grad, const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq, int64_t rows,
+                   int64_t cols, double lr, double beta1, double beta2, double eps, double weight_decay, bool adamw,
+                   int64_t step, double grad_scale, const std::optional<at::Tensor>& grad_scale_dev,
+                   const std::optional<at::Tensor>& step_dev) {
+  TORCH_CHECK(rows > 0 && cols > 0 && rows % 64 == 0 && cols % 128 == 0 && master.numel() == rows * cols,
+              "dgt: adam_matrix_t needs a [rows, cols] matrix with rows % 64 == 0 and cols % 128 == 0");
+  check_gpu(param_lp, "param_lp", at::kBFloat16);
+  check_gpu(param_lpT, "param_lpT", at::kBFloat16);
+  TORCH_CHECK(param_lpT.numel() == rows * cols, "dgt: param_lpT size mismatch");
+  TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
+              "dgt: adam_matrix_t grad must be fp32 or bf16");
+  const dgt::AdamFlatArgs a = adam_args(master, param_lp, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
+                                        weight_decay, adamw, step, grad_scale, grad_scale_dev, step_dev);
+  c10::DeviceGuard guard(master.device());
+  DGT_CHECK_HIP(dgt::adam_matrix_t(a, param_lpT.data_ptr(), (int)rows, (int)cols, stream_of(master)));
 }
 
 void step_increment(const at::Tensor& counter) {
@@ -421,6 +449,11 @@ TORCH_LIBRARY(dgt, m) {
       "float lr, float beta1, float beta2, float eps, float weight_decay, bool adamw, int step, float grad_scale, "
       "Tensor? grad_scale_dev, Tensor? step_dev=None) -> ()",
       &adam_flat);
+  m.def(
+      "adam_matrix_t(Tensor(a!) master, Tensor(b!) param_lp, Tensor(c!) param_lpT, Tensor grad, Tensor(d!) exp_avg, "
+      "Tensor(e!) exp_avg_sq, int rows, int cols, float lr, float beta1, float beta2, float eps, float weight_decay, "
+      "bool adamw, int step, float grad_scale, Tensor? grad_scale_dev, Tensor? step_dev=None) -> ()",
+      &adam_matrix_t);
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def(
       "oneshot_allreduce(Tensor inp, Tensor(a!) out, float scale, int[] data_ptrs, int rank, "

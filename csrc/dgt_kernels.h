@@ -78,6 +78,10 @@ hipError_t step_increment(long long* counter, hipStream_t stream);
 
 hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream);
 
+// Adam over a row-major [rows, cols] fp32 matrix (a.n = rows * cols, rows a multiple of 64, cols of 128) that also
+// writes the bf16 copy a.param_lp [rows, cols] and its transpose lpT [cols, rows] in the same pass.
+hipError_t adam_matrix_t(const AdamFlatArgs& a, void* lpT, int rows, int cols, hipStream_t stream);
+
 // ---------------------------------------------------------------- IPC one-shot all-reduce
 // in[n] (fp32) from every rank -> out[n] = scale * sum over ranks (rank order, identical bits on
 // every rank).  Uses the Exchange mailboxes; n <= ex.stride.

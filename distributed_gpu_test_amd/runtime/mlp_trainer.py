@@ -12,8 +12,24 @@ One optimizer step, all on the GPU, no host sync:
               each layer's weight gradient leaves for its collective as soon as its wgrad is
               enqueued (RCCL over xGMI on the process group's stream): the collective overlaps
               the remaining backward GEMMs
-    update    fused Adam launches over flat fp32 masters that also write the bf16 compute copy;
-              W_l^T refreshed by a tiled transpose
+    update    fused Adam over the fp32 masters that also writes the bf16 compute copy (ZeRO-1: on
+              the shard, then all-gather); W_l^T refreshed by a tiled transpose
+
+Schedules (``schedule=`` or ``DGT_MLP_SCHEDULE``):
+
+* ``"flat"`` (default for N = 1): after backward, ONE Adam launch over every weight, then the
+  transposes;
+* ``"overlap"`` (default for N > 1): layer l's update runs on a side HIP stream as soon as its
+  collective has landed and backward no longer reads W_l^T, so the Adam of the upper layers
+  overlaps the collectives of the lower ones and only the first layer's update is left after
+  the last collective; the next step's forward GEMM of layer l waits only on layer l's event;
+* ``"serial"``: the same per-layer updates on the main stream after backward.
+
+On one GPU the overlap does not pay: a streaming Adam running beside the backward GEMMs slows
+them by as much as it hides (dgrad 49 -> 70 us, profiles/r1_mlp_schedule_ab.txt) — the GEMMs at
+M = 1024 are bound by the L2/fabric, not by MFMA.  ``DGT_ADAM_MATRIX_T=1`` swaps the per-layer
+Adam + transpose for one kernel that writes W_l and W_l^T in the same pass (adam_matrix_t:
+correct, but its row-piece access pattern measured slower than flat Adam + transpose).
 
 Parameters live in two flat regions:
 
@@ -32,15 +48,19 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import contextlib
+import os
+
 import torch
 import torch.distributed as dist
 
 from ..models.synthetic_mlp import SyntheticMLP, synthetic_batch_data
-from ..ops.adam import adam_flat_
+from ..ops.adam import adam_flat_, adam_matrix_t_
 from ..ops.gemm import gemm_nt, mlp_head, rowsum_bf16, transpose_bf16
 from ..parallel import comm
 
 ALIGN = 64
+SCHEDULES = ("overlap", "serial", "flat")
 
 
 def _round(x: int, m: int = ALIGN) -> int:
@@ -52,9 +72,15 @@ class MLPTrainer:
 
     def __init__(self, model: SyntheticMLP, batch_size: int = 1024, n_batches: int = 8, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 1234,
-                 device: Optional[torch.device] = None, zero_stage: int = 0):
+                 device: Optional[torch.device] = None, zero_stage: int = 0, schedule: Optional[str] = None):
         if zero_stage not in (0, 1):
             raise ValueError("MLPTrainer supports zero_stage 0 or 1")
+        schedule = schedule or os.environ.get("DGT_MLP_SCHEDULE", "auto")
+        if schedule not in SCHEDULES + ("auto",):
+            raise ValueError(f"schedule must be one of {SCHEDULES} or 'auto'")
+        if schedule == "auto":  # measured (profiles/r1_mlp_schedule_ab.txt): see the module docstring
+            schedule = "flat" if comm.get_world_size() == 1 else "overlap"
+        self.matrix_t = os.environ.get("DGT_ADAM_MATRIX_T", "0") == "1"
         self.device = device or torch.device("cuda", torch.cuda.current_device())
         self.model = model
         self.B, self.D, self.L, self.Din = batch_size, model.width, model.depth, model.in_features
@@ -151,6 +177,22 @@ class MLPTrainer:
         kind = "allreduce" if self.zero_stage == 0 else "reducescatter+allgather"
         self.exchange = f"{comm.backend_name()}-{kind}-per-layer" if self.world_size > 1 else "none"
 
+        # ---- schedule: side streams + per-layer events (GPU only; CPU runs everything in order)
+        self.schedule = schedule if dev.type == "cuda" else "serial"
+        self.shapes = [tuple(named[f"layers.{i}.weight"].shape) for i in range(self.L)]
+        self._overlap = self.schedule == "overlap"
+        self._opt_pending = False
+        self.s_main = None
+        if self._overlap:
+            if os.environ.get("DGT_MLP_PRIO", "0") == "1":  # GEMM stream ahead of the optimizer stream
+                self.s_main = torch.cuda.Stream(dev, priority=-1)
+            self.s_opt = torch.cuda.Stream(dev)
+            self.s_comm = torch.cuda.Stream(dev)
+            self.ev_wgrad = [torch.cuda.Event() for _ in range(self.L)]
+            self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
+            self.ev_comm = [torch.cuda.Event() for _ in range(self.L)]
+            self.ev_opt = [torch.cuda.Event() for _ in range(self.L)]
+
     # ------------------------------------------------------------------ helpers
     def _refresh_transposes(self):
         for w, wt in zip(self.W, self.WT):
@@ -161,6 +203,7 @@ class MLPTrainer:
 
     def grad_of(self, name: str) -> torch.Tensor:
         """This rank's local (pre-reduction) gradient of a model parameter, in its shape."""
+        self.join()
         p = dict(self.model.named_parameters())[name]
         if name.startswith("layers.") and name.endswith("weight"):
             return self.gW[int(name.split(".")[1])].reshape(p.shape)
@@ -195,48 +238,115 @@ class MLPTrainer:
         for w in works:
             w.wait()
 
+    # ------------------------------------------------------------------ optimizer pieces
+    def _adam_args(self):
+        return (self.global_steps, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, False)
+
+    def _update_layer(self, i: int) -> None:
+        """Adam on layer i's weights (its shard under ZeRO-1) + refresh of the bf16 W_i and W_i^T."""
+        args, scale = self._adam_args(), 1.0 / self.world_size
+        if self.zero_stage == 0:
+            R, Cc = self.shapes[i]
+            o = self.w_off[i]
+            if self.matrix_t and R % 64 == 0 and Cc % 128 == 0:
+                sl = slice(o, o + R * Cc)
+                adam_matrix_t_(self.master_w[sl], self.params_bf16[sl], self.WT[i], self.grads_w[sl], self.m_w[sl],
+                               self.v_w[sl], R, Cc, *args, grad_scale=scale)
+                return
+            sl = slice(o, o + self.w_len[i])
+            adam_flat_(self.master_w[sl], self.grads_w[sl], self.m_w[sl], self.v_w[sl], *args, grad_scale=scale,
+                       param_lp=self.params_bf16[sl])
+        else:
+            sl = slice(self.shard_off[i], self.shard_off[i] + self.shard_len[i])
+            adam_flat_(self.master_w[sl], self.shard_grad[sl], self.m_w[sl], self.v_w[sl], *args, grad_scale=scale,
+                       param_lp=self.lp_w[sl])
+            works: list = []
+            out = self.params_bf16[self.w_off[i]:self.w_off[i] + self.w_len[i]]
+            self._collective(dist.all_gather_into_tensor, out, self.lp_w[sl], works=works)
+            for w in works:
+                w.wait()
+        transpose_bf16(self.W[i], self.WT[i])
+
+    def join(self) -> None:
+        """Make the caller's stream wait for the side streams (results visible to later work)."""
+        if self._opt_pending:
+            cur = torch.cuda.current_stream(self.device)
+            cur.wait_stream(self.s_opt)
+            cur.wait_stream(self.s_comm)
+            self._opt_pending = False
+
     # ------------------------------------------------------------------ one step
     def step(self, s: int) -> None:
-        B = self.B
+        B, L = self.B, self.L
         j = s % self.n_batches
         x = self.X[j * B:(j + 1) * B]
         xT = self.XT[:, j * B:(j + 1) * B]
         y = self.Y[j * B:(j + 1) * B]
-        # forward
+        ov = self._overlap
+        main = torch.cuda.current_stream(self.device) if ov else None
+        # forward: layer i waits only on its own update of the previous step
         prev = x
-        for i in range(self.L):
+        for i in range(L):
+            if self._opt_pending:
+                main.wait_event(self.ev_opt[i])
             gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True)
             prev = self.a[i + 1]
         # head (+ its gradients); head grads accumulate -> zero them first
         self.ghw.zero_()
         self.ghb.zero_()
         cur = 0
-        mlp_head(self.a[self.L], self.hw, self.hb, y, self.dz, self.ghw, self.ghb, self.loss_acc, self.g[cur],
+        mlp_head(self.a[L], self.hw, self.hb, y, self.dz, self.ghw, self.ghb, self.loss_acc, self.g[cur],
                  self.gT[cur])
+        self.global_steps += 1
         works: list = []
-        # backward, last layer first; each weight bucket leaves as soon as its wgrad is enqueued
-        for i in reversed(range(self.L)):
+        # backward, last layer first; each weight bucket leaves for its collective as soon as its
+        # wgrad is enqueued; with the overlap schedule the layer's optimizer update follows on
+        # s_opt once backward no longer reads W_i^T (after its dgrad) and the collective is done
+        for i in reversed(range(L)):
             a_prevT = xT if i == 0 else self.aT[i]
             gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=True)
             rowsum_bf16(self.gT[cur], self.gb[i])
-            self._reduce_layer(i, works)
+            if self.world_size > 1:
+                if ov:
+                    self.ev_wgrad[i].record(main)
+                    self.s_comm.wait_event(self.ev_wgrad[i])
+                    with torch.cuda.stream(self.s_comm):
+                        lw: list = []
+                        self._reduce_layer(i, lw)
+                        for w in lw:
+                            w.wait()
+                        self.ev_comm[i].record(self.s_comm)
+                else:
+                    self._reduce_layer(i, works)
             if i > 0:
                 gemm_nt(self.g[cur], self.WT[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i])
                 cur ^= 1
+            if ov:
+                self.ev_bwd[i].record(main)
+                self.s_opt.wait_event(self.ev_bwd[i])
+                if self.world_size > 1:
+                    self.s_opt.wait_event(self.ev_comm[i])
+                with torch.cuda.stream(self.s_opt):
+                    self._update_layer(i)
+                    self.ev_opt[i].record(self.s_opt)
         if self.world_size > 1:  # biases + head: one small replicated bucket
             self._collective(dist.all_reduce, self.grads_s, works=works)
         for w in works:
             w.wait()
-        self.global_steps += 1
-        scale = 1.0 / self.world_size
-        grads_w = self.grads_w if self.zero_stage == 0 else self.shard_grad
-        adam_flat_(self.master_w, grads_w, self.m_w, self.v_w, self.global_steps, self.lr, self.betas[0],
-                   self.betas[1], self.eps, self.weight_decay, False, grad_scale=scale, param_lp=self.lp_w)
-        adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, self.global_steps, self.lr, self.betas[0],
-                   self.betas[1], self.eps, self.weight_decay, False, grad_scale=scale)
-        if self.zero_stage == 1:
-            self._allgather_params()
-        self._refresh_transposes()
+        adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *self._adam_args(),
+                   grad_scale=1.0 / self.world_size)
+        if ov:
+            self._opt_pending = True
+        elif self.schedule == "serial":
+            for i in reversed(range(L)):
+                self._update_layer(i)
+        else:  # "flat": one Adam launch over every weight, then the all-gather and the transposes
+            grads_w = self.grads_w if self.zero_stage == 0 else self.shard_grad
+            adam_flat_(self.master_w, grads_w, self.m_w, self.v_w, *self._adam_args(),
+                       grad_scale=1.0 / self.world_size, param_lp=self.lp_w)
+            if self.zero_stage == 1:
+                self._allgather_params()
+            self._refresh_transposes()
 
     # bench.py adapter (same surface as TinyMLPTrainer)
     def epoch_plan(self, epoch: int):
@@ -244,12 +354,21 @@ class MLPTrainer:
         return plan, torch.ones(self.n_batches, dtype=torch.int32)
 
     def run_plan(self, plan, counts) -> None:
-        for _ in range(int(plan.shape[0])):
-            self.step(self.global_steps)
+        if self.s_main is not None:
+            self.s_main.wait_stream(torch.cuda.current_stream(self.device))
+            with torch.cuda.stream(self.s_main):
+                for _ in range(int(plan.shape[0])):
+                    self.step(self.global_steps)
+            torch.cuda.current_stream(self.device).wait_stream(self.s_main)
+        else:
+            for _ in range(int(plan.shape[0])):
+                self.step(self.global_steps)
+        self.join()
 
     @property
     def params(self) -> torch.Tensor:
         """Every parameter as this rank sees it (bf16 matrices + fp32 small params), for checks."""
+        self.join()
         return torch.cat([self.params_bf16.float(), self.master_s])
 
     def check(self) -> None:

@@ -3,6 +3,7 @@
 CPU runs check the trainer's math through the reference ops; GPU runs (marker ``gpu``) check the
 HIP kernels against the same references."""
 import copy
+import os
 
 import pytest
 import torch
@@ -146,3 +147,68 @@ def test_transpose_rowsum_head():
 @gpu
 def test_trainer_gpu_matches_torch():
     _check(torch.device("cuda"))
+
+
+def _run_schedule(device, schedule, steps=3):
+    torch.manual_seed(0)
+    model = SyntheticMLP(width=128, depth=3)
+    tr = MLPTrainer(model, batch_size=128, n_batches=2, lr=1e-3, device=device, schedule=schedule)
+    for s in range(steps):
+        tr.step(s)
+    tr.join()
+    return tr
+
+
+def test_trainer_schedules_agree_cpu():
+    """serial (per-layer Adam + W^T) and flat (one Adam launch + transposes) give the same update."""
+    a, b = _run_schedule(torch.device("cpu"), "serial"), _run_schedule(torch.device("cpu"), "flat")
+    assert torch.equal(a.master_w, b.master_w) and torch.equal(a.m_w, b.m_w) and torch.equal(a.v_w, b.v_w)
+    for wa, wb in zip(a.WT, b.WT):
+        assert torch.equal(wa, wb)
+
+
+@gpu
+@pytest.mark.parametrize("rows,cols,gdt", [(64, 128, torch.float32), (128, 384, torch.float32),
+                                           (192, 256, torch.bfloat16)])
+def test_adam_matrix_t_matches_flat_reference(rows, cols, gdt):
+    from distributed_gpu_test_amd.ops.adam import adam_matrix_t_
+    from distributed_gpu_test_amd.ops.reference import adam_flat_reference_
+    g = torch.Generator().manual_seed(rows * cols)
+    n = rows * cols
+    p, gr = torch.randn(n, generator=g), torch.randn(n, generator=g).to(gdt)
+    m, v = torch.randn(n, generator=g) * 0.1, torch.rand(n, generator=g) * 0.01
+    ref = [p.clone(), gr.float(), m.clone(), v.clone()]
+    lp_ref = torch.empty(n, dtype=torch.bfloat16)
+    adam_flat_reference_(ref[0], ref[1], ref[2], ref[3], 3, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, 0.5, None, lp_ref)
+    d = [t.cuda() for t in (p, gr, m, v)]
+    lp = torch.empty(n, dtype=torch.bfloat16, device="cuda")
+    lpT = torch.empty(cols, rows, dtype=torch.bfloat16, device="cuda")
+    adam_matrix_t_(d[0], lp, lpT, d[1], d[2], d[3], rows, cols, 3, 1e-3, grad_scale=0.5)
+    torch.testing.assert_close(d[0].cpu(), ref[0], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(d[2].cpu(), ref[2], rtol=1e-6, atol=1e-7)
+    torch.testing.assert_close(d[3].cpu(), ref[3], rtol=1e-6, atol=1e-9)
+    assert torch.equal(lp.cpu().view(rows, cols).t(), lpT.cpu()), "W^T must be the transpose of the bf16 copy"
+    torch.testing.assert_close(lp.cpu().float(), lp_ref.float(), rtol=1e-2, atol=1e-6)
+
+
+@gpu
+def test_trainer_overlap_schedule_is_bitwise_serial():
+    """Side-stream per-layer updates are a schedule change only: same weight matrices bit for bit.
+    (The head's gradient accumulates with float atomics, so the small fp32 region and the loss may
+    differ in the last bits between any two runs.)"""
+    dev = torch.device("cuda")
+    runs = {s: _run_schedule(dev, s, steps=4) for s in ("overlap", "serial", "flat")}
+    os.environ["DGT_ADAM_MATRIX_T"] = "1"
+    try:
+        runs["overlap+matrix_t"] = _run_schedule(dev, "overlap", steps=4)
+    finally:
+        del os.environ["DGT_ADAM_MATRIX_T"]
+    base = runs["serial"]
+    for name in ("overlap", "flat", "overlap+matrix_t"):
+        r = runs[name]
+        assert torch.equal(r.master_w, base.master_w), name
+        assert torch.equal(r.params_bf16, base.params_bf16), name
+        for wa, wb in zip(r.WT, base.WT):
+            assert torch.equal(wa, wb), name
+        torch.testing.assert_close(r.master_s, base.master_s, rtol=1e-5, atol=1e-7)
+        torch.testing.assert_close(r.loss_acc, base.loss_acc, rtol=1e-6, atol=0)
