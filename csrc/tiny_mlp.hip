@@ -375,13 +375,16 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
       for (int q = 0; q < C::NQ; ++q) sum[q] = f32x4{0.f, 0.f, 0.f, 0.f};
       const unsigned long long t0 = realtime();
       bool late = false;
-      for (int p0 = 0; p0 < ex.world_size; p0 += 4) {  // 4 peers' lines in flight at a time
-        unsigned long long v[4][4 * C::NQ];
+      // every peer's lines in flight at once: ONE local round trip per poll whatever the world size
+      // (polling in batches of 4 peers cost a second round trip per step at 5-8 ranks)
+      constexpr int PB = kMaxRanks;
+      for (int p0 = 0; p0 < ex.world_size; p0 += PB) {
+        unsigned long long v[PB][4 * C::NQ];
         bool ready;
         do {  // every retry re-reads the whole batch: one round trip per poll, not one per line
           ready = true;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < PB; ++j) {
             const int p = p0 + j;
             if (p < ex.world_size && p != ex.rank) {
               const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, p) + wofs;
@@ -390,7 +393,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
             }
           }
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
+          for (int j = 0; j < PB; ++j) {
             const int p = p0 + j;
             if (p < ex.world_size && p != ex.rank) {
 #pragma unroll
@@ -400,7 +403,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
           if (!ready && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
         } while (!ready && !late);
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
+        for (int j = 0; j < PB; ++j) {
           const int p = p0 + j;
           if (p >= ex.world_size) continue;
           if (p == ex.rank) {

@@ -13,6 +13,7 @@ from distributed_gpu_test_amd.launch import free_port
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 ORACLE2 = [0.5126, 0.2219, 0.1250, 0.0857, 0.0741]
+ORACLE = {4: [0.5857, 0.3375, 0.1943, 0.1321, 0.0969], 8: [0.6378, 0.4770, 0.3251, 0.2162, 0.1515]}
 pytestmark = pytest.mark.gpu
 
 
@@ -91,3 +92,23 @@ def test_bench_mlp_zero1_two_ranks_one_gpu():
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["params_consistent_across_ranks"] is True
     assert "reducescatter+allgather" in out["config"]["exchange"]
+
+
+@pytest.mark.parametrize("ws", [4, 8])
+def test_fused_ipc_exchange_many_ranks_one_gpu(tmp_path, ws):
+    """The 8-rank exchange (two batches of 4 peers in flight, every mailbox slot) on one card:
+    the same code path the 8 x MI355X scaling run takes, checked against the survey's oracle."""
+    r = run(ws, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "exchange=ipc-oneshot-xgmi" in r.stderr, r.stderr[-2000:]
+    assert losses(r.stdout) == ORACLE[ws][:2]
+
+
+def test_bench_eight_ranks_one_gpu():
+    r = run(8, "bench.py", "--gpus", "8", "--steps", "2000", "--warmup", "200", "--no-sweep", timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    import json
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    assert out["n_gpus"] == 8 and out["params_consistent_across_ranks"] is True
+    assert out["config"]["exchange"] == "ipc-oneshot-xgmi"
+    print(json.dumps(out))
