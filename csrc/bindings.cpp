@@ -378,6 +378,9 @@ void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, co
   h.g = g.data_ptr();
   h.gT = gT.data_ptr();
   c10::DeviceGuard guard(a.device());
+  // stream-ordered workspace from the caching allocator (reused in place on later calls)
+  at::Tensor scratch = at::empty({B}, dz.options());
+  h.scratch = scratch.data_ptr<float>();
   DGT_CHECK_HIP(dgt::mlp_head(h, stream_of(a)));
 }
 

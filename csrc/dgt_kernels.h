@@ -121,9 +121,10 @@ struct HeadArgs {      // binary head of the synthetic MLP: Linear(D, 1) + BCE-w
   const float* y;      // fp32 [B]
   int B, D;
   float* dz;           // fp32 [B]
-  float* dw;           // fp32 [D]  (+=)
-  float* db;           // fp32 [1]  (+=)
+  float* dw;           // fp32 [D]  (overwritten)
+  float* db;           // fp32 [1]  (overwritten)
   double* loss_acc;    // += mean loss
+  float* scratch;      // fp32 [B] workspace (per-row loss terms)
   void* g;             // bf16 [B, D] gradient wrt the last pre-activation
   void* gT;            // bf16 [D, B]
 };

@@ -577,7 +577,35 @@ __global__ __launch_bounds__(256) void transpose_bf16_kernel(const u16* __restri
   }
 }
 
+// Full 64 x 64 tiles: one wave per tile, lane (rb, cg) moves the 8 x 8 block rows 8rb.., cols 8cg..
+// entirely in registers: eight 16-byte row loads, eight 16-byte transposed row stores (8 lanes
+// cover one 128-byte line on both sides), no LDS and no barrier.
+__global__ __launch_bounds__(256) void transpose_bf16_tile_kernel(const u16* __restrict__ in, u16* __restrict__ out,
+                                                                  int rows, int cols) {
+  const int l = threadIdx.x & 63, cg = l & 7, rb = l >> 3;
+  const int r = blockIdx.y * 64 + rb * 8, c = (blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6)) * 64 + cg * 8;
+  uint4 v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const uint4*>(in + (long long)(r + k) * cols + c);
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    unsigned o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const unsigned lo = (&v[2 * q].x)[e >> 1], hi = (&v[2 * q + 1].x)[e >> 1];
+      o[q] = (e & 1) ? ((lo >> 16) | (hi & 0xffff0000u)) : ((lo & 0xffffu) | (hi << 16));
+    }
+    *reinterpret_cast<uint4*>(out + (long long)(c + e) * rows + r) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+}
+
 hipError_t transpose_bf16(const void* in, void* out, int rows, int cols, hipStream_t stream) {
+  if (rows % 64 == 0 && cols % 64 == 0) {  // 4 tiles per block side by side when the width allows
+    const int wpb = cols % 256 == 0 ? 4 : 1;
+    hipLaunchKernelGGL(transpose_bf16_tile_kernel, dim3(cols / (64 * wpb), rows / 64), dim3(64 * wpb), 0, stream,
+                       static_cast<const u16*>(in), static_cast<u16*>(out), rows, cols);
+    return hipGetLastError();
+  }
   dim3 grid((cols + 63) / 64, (rows + 63) / 64);
   hipLaunchKernelGGL(transpose_bf16_kernel, grid, dim3(256), 0, stream, static_cast<const u16*>(in),
                      static_cast<u16*>(out), rows, cols);
@@ -610,70 +638,127 @@ hipError_t rowsum_bf16(const void* in, float* out, int rows, int cols, int accum
 
 // ------------------------------------------------------------------ BCE head
 // z[b] = a[b,:] . w + b0; loss += mean BCE; dz = (sigmoid(z) - y) / B;
-// g[b,:] = dz[b] * w * 1[a[b,:] > 0] (bf16, and g^T); dw += sum_b dz[b] a[b,:]; db += sum_b dz[b].
-// Kernel 1: one wave per row computes z, loss, dz.  Kernel 2: per (row-block, col-block) tile
-// writes g / g^T and accumulates dw with one atomic per column per block.
+// g[b,:] = dz[b] * w * 1[a[b,:] > 0] (bf16, and g^T); dw = sum_b dz[b] a[b,:]; db = sum_b dz[b].
+// Kernel 1: one row per wave (every 16-byte load of the row in flight together) computes
+// z, dz and the row's loss term into a scratch vector, and zeroes dw.  No atomics: 1024 float /
+// double atomics on ONE address serialised at the L2 and made this kernel 19 us.
+// Kernel 2: one wave per 64 x 64 tile, 16-byte rows of a in, 16-byte rows of g and g^T out, dw
+// accumulated with one atomic per column per tile; tile (0, 0) also reduces dz -> db and the row
+// losses -> loss_acc in a fixed order (one atomic).
 __global__ __launch_bounds__(256) void head_fwd_kernel(const u16* __restrict__ a, const float* __restrict__ w,
                                                        const float* __restrict__ b0, const float* __restrict__ y,
-                                                       int B, int D, float* __restrict__ dz, float* __restrict__ db,
-                                                       double* __restrict__ loss_acc) {
-  const int row = blockIdx.x * 4 + (threadIdx.x >> 6), l = threadIdx.x & 63;
-  if (row >= B) return;
-  const u16* p = a + (long long)row * D;
-  float s = 0.f;
-  for (int c = l * 8; c < D; c += 64 * 8) {
-    const uint4 v = *reinterpret_cast<const uint4*>(p + c);
-    const unsigned u[4] = {v.x, v.y, v.z, v.w};
+                                                       int B, int D, float* __restrict__ dz,
+                                                       float* __restrict__ lrow, float* __restrict__ dw) {
+  const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (int i = blockIdx.x * 256 + threadIdx.x; i < D; i += gridDim.x * 256) dw[i] = 0.f;
+  constexpr int R = 1;
+  const int row0 = blockIdx.x * 4 + wv * R;
+  float s[R] = {0.f};
+#pragma unroll 8
+  for (int c = l * 8; c < D; c += 64 * 8) {  // unrolled: a row's loads are in flight together
+    const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + c), w1 = *reinterpret_cast<const f32x4*>(w + c + 4);
+    uint4 v[R];
 #pragma unroll
-    for (int e = 0; e < 4; ++e) s += bf2f(u[e] & 0xffff) * w[c + 2 * e] + bf2f(u[e] >> 16) * w[c + 2 * e + 1];
+    for (int r = 0; r < R; ++r) v[r] = *reinterpret_cast<const uint4*>(a + (long long)(row0 + r) * D + c);
+#pragma unroll
+    for (int r = 0; r < R; ++r) {
+      s[r] += bf2f(v[r].x & 0xffff) * w0[0] + bf2f(v[r].x >> 16) * w0[1] + bf2f(v[r].y & 0xffff) * w0[2] +
+              bf2f(v[r].y >> 16) * w0[3] + bf2f(v[r].z & 0xffff) * w1[0] + bf2f(v[r].z >> 16) * w1[1] +
+              bf2f(v[r].w & 0xffff) * w1[2] + bf2f(v[r].w >> 16) * w1[3];
+    }
   }
-  s = wave_sum(s);
-  if (l == 0) {
-    const float z = s + *b0, yy = y[row];
+#pragma unroll
+  for (int r = 0; r < R; ++r) s[r] = wave_sum(s[r]);
+  if (l < R) {
+    float sr = s[0];
+#pragma unroll
+    for (int r = 1; r < R; ++r) sr = l == r ? s[r] : sr;
+    const int row = row0 + l;
+    const float z = sr + *b0, yy = y[row];
     const float e = __expf(-fabsf(z));
     const float sig = z >= 0.f ? 1.f / (1.f + e) : e / (1.f + e);
-    const float d = (sig - yy) / (float)B;
-    dz[row] = d;
-    atomicAdd(db, d);
-    atomicAdd(loss_acc, (double)(((1.f - yy) * z - (fminf(z, 0.f) - log1pf(e))) / (float)B));
+    dz[row] = (sig - yy) / (float)B;
+    lrow[row] = ((1.f - yy) * z - (fminf(z, 0.f) - log1pf(e))) / (float)B;
   }
 }
 
 __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a, const float* __restrict__ w,
-                                                       const float* __restrict__ dz, int B, int D,
-                                                       u16* __restrict__ g, u16* __restrict__ gT,
-                                                       float* __restrict__ dw) {
-  // block: 64 rows x 64 cols; thread t: col c = t & 63, rows (t >> 6) + 4i
-  __shared__ u16 tile[64][65];
-  const int r0 = blockIdx.y * 64, c0 = blockIdx.x * 64, t = threadIdx.x;
-  const int c = c0 + (t & 63);
-  const float wc = w[c];
-  float part = 0.f;
+                                                      const float* __restrict__ dz,
+                                                      const float* __restrict__ lrow, int B, int D,
+                                                      u16* __restrict__ g, u16* __restrict__ gT,
+                                                      float* __restrict__ dw, float* __restrict__ db,
+                                                      double* __restrict__ loss_acc) {
+  // one wave per 64 x 64 tile; lane (rb, cg) owns the 8 x 8 block rows r0 + 8rb.., cols c0 + 8cg..:
+  // eight 16-byte row loads of a, eight 16-byte g row stores (8 lanes = one 128-byte line) and
+  // eight 16-byte g^T row stores (8 consecutive rows of one column): no LDS
+  const int l = threadIdx.x & 63, cg = l & 7, rb = l >> 3, wv = threadIdx.x >> 6;
+  const int r = blockIdx.y * 64 + rb * 8, c = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + cg * 8;
+  const f32x4 w0 = *reinterpret_cast<const f32x4*>(w + c), w1 = *reinterpret_cast<const f32x4*>(w + c + 4);
+  const float wc[8] = {w0[0], w0[1], w0[2], w0[3], w1[0], w1[1], w1[2], w1[3]};
+  uint4 v[8];
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int rr = (t >> 6) + 4 * i, row = r0 + rr;
-    const float av = bf2f(a[(long long)row * D + c]);
-    const float d = dz[row];
-    part += d * av;
-    const u16 gv = f2bf(av > 0.f ? d * wc : 0.f);
-    g[(long long)row * D + c] = gv;
-    tile[rr][t & 63] = gv;
+  for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const uint4*>(a + (long long)(r + k) * D + c);
+  float part[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  u16 gb[8][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    const float d = dz[r + k];
+    const unsigned u[4] = {v[k].x, v[k].y, v[k].z, v[k].w};
+    unsigned o[4];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float av = bf2f((u16)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffff));
+      part[e] += d * av;
+      gb[k][e] = f2bf(av > 0.f ? d * wc[e] : 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (unsigned)gb[k][2 * q] | ((unsigned)gb[k][2 * q + 1] << 16);
+    *reinterpret_cast<uint4*>(g + (long long)(r + k) * D + c) = make_uint4(o[0], o[1], o[2], o[3]);
   }
-  atomicAdd(&dw[c], part);
-  __syncthreads();
 #pragma unroll
-  for (int i = 0; i < 16; ++i) {
-    const int cc = (t >> 6) + 4 * i, rr = t & 63;
-    gT[(long long)(c0 + cc) * B + r0 + rr] = tile[rr][cc];
+  for (int e = 0; e < 8; ++e) {
+    unsigned o[4];
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (unsigned)gb[2 * q][e] | ((unsigned)gb[2 * q + 1][e] << 16);
+    *reinterpret_cast<uint4*>(gT + (long long)(c + e) * B + r) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  // dw: sum the 8 row-blocks (lanes cg, cg + 8, ..., cg + 56), one atomic per column per tile
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float x = part[e];
+    x += __shfl_xor(x, 8);
+    x += __shfl_xor(x, 16);
+    x += __shfl_xor(x, 32);
+    part[e] = x;
+  }
+  if (rb == 0) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) atomicAdd(&dw[c + e], part[e]);
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && wv == 0) {  // db and the step's loss, in a fixed order
+    float sd = 0.f, sl = 0.f;
+    for (int i = l; i < B; i += 64) {
+      sd += dz[i];
+      sl += lrow[i];
+    }
+    sd = wave_sum(sd);
+    sl = wave_sum(sl);
+    if (l == 0) {
+      *db = sd;
+      atomicAdd(loss_acc, (double)sl);
+    }
   }
 }
 
 hipError_t mlp_head(const HeadArgs& h, hipStream_t stream) {
-  if (h.B % 64 || h.D % 64) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(head_fwd_kernel, dim3((h.B + 3) / 4), dim3(256), 0, stream, static_cast<const u16*>(h.a), h.w,
-                     h.b0, h.y, h.B, h.D, h.dz, h.db, h.loss_acc);
-  hipLaunchKernelGGL(head_bwd_kernel, dim3(h.D / 64, h.B / 64), dim3(256), 0, stream, static_cast<const u16*>(h.a),
-                     h.w, h.dz, h.B, h.D, static_cast<u16*>(h.g), static_cast<u16*>(h.gT), h.dw);
+  if (h.B % 64 || h.D % 64 || !h.scratch) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(head_fwd_kernel, dim3(h.B / 4), dim3(256), 0, stream, static_cast<const u16*>(h.a), h.w,
+                     h.b0, h.y, h.B, h.D, h.dz, h.scratch, h.dw);
+  const int wpb = h.D % 256 == 0 ? 4 : 1;  // 4 tiles per block side by side when the width allows
+  hipLaunchKernelGGL(head_bwd_kernel, dim3(h.D / (64 * wpb), h.B / 64), dim3(64 * wpb), 0, stream,
+                     static_cast<const u16*>(h.a),
+                     h.w, h.dz, h.scratch, h.B, h.D, static_cast<u16*>(h.g), static_cast<u16*>(h.gT), h.dw, h.db,
+                     h.loss_acc);
   return hipGetLastError();
 }
 

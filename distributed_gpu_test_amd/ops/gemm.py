@@ -67,7 +67,8 @@ def rowsum_bf16(inp: torch.Tensor, out: torch.Tensor, accumulate: bool = False) 
 
 
 def mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT) -> None:
-    """Linear(D,1) + BCE-with-logits (mean) forward and backward; dw/db/loss_acc accumulate."""
+    """Linear(D,1) + BCE-with-logits (mean) forward and backward; dw, db are overwritten with the
+    head's gradients, loss_acc accumulates the mean loss."""
     if a.is_cuda:
         require().mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT)
         return
@@ -76,8 +77,8 @@ def mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT) -> None:
     loss = torch.nn.functional.binary_cross_entropy_with_logits(z, y)
     d = (torch.sigmoid(z) - y) / a.shape[0]
     dz.copy_(d)
-    dw.add_(d @ af)
-    db.add_(d.sum())
+    dw.copy_(d @ af)
+    db.copy_(d.sum())
     loss_acc.add_(float(loss))
     gg = torch.outer(d, w) * (af > 0)
     g.copy_(gg.to(g.dtype))

@@ -291,9 +291,7 @@ class MLPTrainer:
                 main.wait_event(self.ev_opt[i])
             gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True)
             prev = self.a[i + 1]
-        # head (+ its gradients); head grads accumulate -> zero them first
-        self.ghw.zero_()
-        self.ghb.zero_()
+        # head (+ its gradients, written in place: no zero fills)
         cur = 0
         mlp_head(self.a[L], self.hw, self.hb, y, self.dz, self.ghw, self.ghb, self.loss_acc, self.g[cur],
                  self.gT[cur])

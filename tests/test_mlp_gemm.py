@@ -123,10 +123,12 @@ def test_gemm_strided_operand():
 
 @gpu
 def test_transpose_rowsum_head():
+    for shape in [(192, 320), (100, 72), (64, 4096)]:  # full 64 x 64 tiles (register kernel) and ragged
+        x = torch.randn(*shape).to(torch.bfloat16).cuda()
+        xt = torch.empty(shape[1], shape[0], dtype=torch.bfloat16).cuda()
+        transpose_bf16(x, xt)
+        assert torch.equal(xt, x.t().contiguous()), shape
     x = torch.randn(192, 320).to(torch.bfloat16).cuda()
-    xt = torch.empty(320, 192, dtype=torch.bfloat16).cuda()
-    transpose_bf16(x, xt)
-    assert torch.equal(xt, x.t().contiguous())
     out = torch.empty(192).cuda()
     rowsum_bf16(x, out)
     torch.testing.assert_close(out, x.float().sum(1), rtol=1e-4, atol=1e-3)
