@@ -120,7 +120,8 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   a.beta1 = beta1;
   a.beta2 = beta2;
   a.adam_step0 = adam_step0;
-  at::Tensor bc = at::empty({std::max<int64_t>(plan.size(0), 1) * 2}, X.options());
+  // one spare entry: the kernel prefetches step s+1's corrections while it runs step s
+  at::Tensor bc = at::empty({(std::max<int64_t>(plan.size(0), 1) + 1) * 2}, X.options());
   a.bc = bc.data_ptr<float>();
   a.loss_acc = loss_acc.data_ptr<double>();
   a.status = status.data_ptr<int>();

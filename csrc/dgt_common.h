@@ -163,9 +163,11 @@ typedef float f32x2 __attribute__((ext_vector_type(2)));
 // adam_update_fast on two elements: the non-transcendental math runs as packed fp32
 // (v_pk_fma_f32 / v_pk_mul_f32 / v_pk_add_f32: two lanes' worth per instruction, same IEEE result
 // per element as the scalar form); sqrt and rcp stay per element.
+// WD = false: compiled without the weight-decay branches (the caller checked weight_decay == 0).
+template <bool WD = true>
 DGT_DEVICE f32x2 adam_update_fast2(f32x2 p, f32x2 g, f32x2& m, f32x2& v, const AdamHyper& h, float step_size_neg,
                                    float inv_bc2_sqrt) {
-  if (h.weight_decay != 0.f) {
+  if (WD && h.weight_decay != 0.f) {
     if (h.adamw) p = p * h.decay;
     else g = __builtin_elementwise_fma(f32x2(h.weight_decay), p, g);
   }

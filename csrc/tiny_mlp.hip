@@ -273,7 +273,9 @@ DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row
 // ------------------------------------------------------------------ persistent training kernel
 // XCH: world size > 1 (the exchange is compiled in).  The single-rank kernel has no exchange
 // branch, so backward and Adam form one basic block the scheduler can interleave.
-template <int F, int H, bool SMALLB, bool XCH>
+// WD: weight decay != 0 (Adam's L2 term / AdamW's decay compiled in; the reference's Adam has none,
+// and the per-pair uniform branches cost ~12 scalar branches per step).
+template <int F, int H, bool SMALLB, bool XCH, bool WD>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
   __shared__ TinySmem<F, H> sm;
@@ -303,6 +305,9 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   double loss_total = 0.0;
   float zs = 0.f, ys = 0.f, ibs = 0.f;  // deferred-loss ring (wave 0)
   const float inv_ws = 1.0f / (float)ex.world_size;
+  // Adam bias corrections of the current step, loaded a step ahead: the scalar load of step s+1's
+  // pair is in flight during step s (a K$ miss every 8th step otherwise stalled the Adam section)
+  float bc_ss = load_uniform(a.bc), bc_ib = load_uniform(a.bc + 1);
 #ifdef DGT_TINY_STAMPS
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0;
 #endif
@@ -310,6 +315,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(0);
     const int Bt = load_uniform(a.counts + s);
     const float invB = __builtin_amdgcn_rcpf((float)Bt);
+    const float bc_ss_next = load_uniform(a.bc + 2 * s + 2), bc_ib_next = load_uniform(a.bc + 2 * s + 3);
     // prefetch step s+1 rows into registers; consumed by the next step's forward
     load_rows<F, H>(a.X, a.Y, idx_next, lq, xn, yn);
     // sampler index of step s+3, issued now so the end-of-step rotation never waits on it
@@ -432,13 +438,15 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     }
     DGT_STAMP(4);
 
-    // ---- Adam; bias corrections of this step from the table (wave-uniform scalar loads)
-    const float step_size_neg = load_uniform(a.bc + 2 * s), inv_bc2_sqrt = load_uniform(a.bc + 2 * s + 1);
+    // ---- Adam; bias corrections of this step from the table (wave-uniform, prefetched)
+    const float step_size_neg = bc_ss, inv_bc2_sqrt = bc_ib;
+    bc_ss = bc_ss_next;
+    bc_ib = bc_ib_next;
     // two parameters per packed-fp32 update (W2 and b2 form the last pair)
 #pragma unroll
     for (int i = 0; i < C::NSP; i += 2) {
       f32x2 m = {st.m1[i], st.m1[i + 1]}, v = {st.v1[i], st.v1[i + 1]};
-      const f32x2 pn = adam_update_fast2(f32x2{st.w1[i], st.w1[i + 1]}, f32x2{gw1[i], gw1[i + 1]}, m, v, a.hp,
+      const f32x2 pn = adam_update_fast2<WD>(f32x2{st.w1[i], st.w1[i + 1]}, f32x2{gw1[i], gw1[i + 1]}, m, v, a.hp,
                                          step_size_neg, inv_bc2_sqrt);
       st.w1[i] = pn.x;
       st.w1[i + 1] = pn.y;
@@ -449,7 +457,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     }
     {
       f32x2 m = {st.mbw, st.mb2}, v = {st.vbw, st.vb2};
-      const f32x2 pn = adam_update_fast2(f32x2{st.bw, st.b2}, f32x2{gbw, gb2}, m, v, a.hp, step_size_neg,
+      const f32x2 pn = adam_update_fast2<WD>(f32x2{st.bw, st.b2}, f32x2{gbw, gb2}, m, v, a.hp, step_size_neg,
                                          inv_bc2_sqrt);
       st.bw = pn.x;
       st.b2 = pn.y;
@@ -565,24 +573,29 @@ __global__ void adam_bias_table_kernel(float* bc, int n, long long step0, double
 
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
   if (!a.bc) return hipErrorInvalidValue;
+  const bool wd = a.hp.weight_decay != 0.f;
   hipLaunchKernelGGL(adam_bias_table_kernel, dim3((a.n_steps + 255) / 256), dim3(256), 0, stream, a.bc, a.n_steps,
                      a.adam_step0, a.lr, a.beta1, a.beta2);
+#define DGT_TINY_LAUNCH(F_, H_, SB, XC)                                                          \
+  do {                                                                                      \
+    if (wd)                                                                                 \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, XC, true>), dim3(1), blk, 0, stream, a); \
+    else                                                                                    \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, XC, false>), dim3(1), blk, 0, stream, a); \
+  } while (0)
 #define X_(F_, H_)                                                                            \
   if (f == F_ && h == H_) {                                                                   \
     const dim3 blk(TinyCfg<F_, H_>::T);                                                       \
     const bool xch = a.ex.world_size > 1;                                                     \
-    if (a.bmax <= 4 && !xch)                                                                  \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, true, false>), dim3(1), blk, 0, stream, a); \
-    else if (a.bmax <= 4)                                                                     \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, true, true>), dim3(1), blk, 0, stream, a); \
-    else if (!xch)                                                                            \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, false, false>), dim3(1), blk, 0, stream, a); \
-    else                                                                                      \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, false, true>), dim3(1), blk, 0, stream, a); \
+    if (a.bmax <= 4 && !xch) DGT_TINY_LAUNCH(F_, H_, true, false);                            \
+    else if (a.bmax <= 4) DGT_TINY_LAUNCH(F_, H_, true, true);                                \
+    else if (!xch) DGT_TINY_LAUNCH(F_, H_, false, false);                                     \
+    else DGT_TINY_LAUNCH(F_, H_, false, true);                                                \
     return hipGetLastError();                                                                 \
   }
   DGT_TINY_SHAPES(X_)
 #undef X_
+#undef DGT_TINY_LAUNCH
   return hipErrorInvalidValue;
 }
 
