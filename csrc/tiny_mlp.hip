@@ -72,6 +72,7 @@ struct TinyCfg {
   static constexpr int PP = (P + 3) / 4 * 4;
   static constexpr int G_B1 = H * F, G_W2 = H * F + H, G_B2 = H * F + 2 * H;
   static_assert(H % 16 == 0 && H >= 16 && H <= 256, "hidden must be a multiple of 16 in [16, 256]");
+  static_assert((NW & (NW - 1)) == 0, "the loss ring rotates over a power-of-two number of waves");
   static_assert(F % 4 == 0 && F >= 4 && F <= 64, "n_features must be a multiple of 4 in [4, 64]");
 
   // feature index of W1 slot i (= 4ct + r) in lane-row lq
@@ -100,6 +101,7 @@ template <int F, int H>
 struct __attribute__((aligned(16))) TinySmem {
   using C = TinyCfg<F, H>;
   WaveSmem<F, H> w[C::NW];
+  double loss[C::NW];        // per-wave deferred-loss totals, summed in wave order at the end
   float Z[2][C::NW * 16];    // per-wave partial logits, double-buffered by step parity
   int err;
 };
@@ -327,15 +329,20 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(1);
     __syncthreads();  // the step's only workgroup barrier: all partial logits published
     DGT_STAMP(2);
-    if (sm.err) break;
+    // only the exchange can fail, so the single-rank loop reads no flag after the barrier
+    if constexpr (XCH) {
+      if (sm.err) break;
+    }
     float gw1[C::NSP];
     const StepGrads sg = wave_backward<F, H, false, SMALLB>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
     float gbw = sg.bw, gb2 = sg.b2;
-    // Deferred loss (reporting only, off the per-step critical path): wave 0's lane row lq keeps
-    // step s's logits when s % 4 == lq; every 4th step one wave-wide reduction folds 4 steps in.
-    // (Logging the logits to memory for a follow-up kernel measured slower: the store joins the
-    // in-order vmcnt queue the row prefetch waits on.)
-    if (w == 0) {
+    // Deferred loss (reporting only, off the per-step critical path): steps 4j..4j+3 belong to
+    // wave j % NW, whose lane row lq keeps step s's logits when s % 4 == lq; at the block's last
+    // step one wave-wide reduction folds the 4 steps in.  Rotating the owner spreads the work
+    // evenly, so no wave is the last to reach the barrier every step.  (Logging the logits to
+    // memory for a follow-up kernel measured slower: the store joins the in-order vmcnt queue the
+    // row prefetch waits on.)
+    if (w == ((s >> 2) & (C::NW - 1))) {
       if (lq == (s & 3)) {
         zs = sg.z;
         ys = y;
@@ -474,7 +481,8 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     idx_next2 = idx_next3;
     DGT_STAMP(5);
   }
-  if (w == 0) loss_total += (double)deferred_loss(zs, ys, ibs);  // the partial last ring
+  loss_total += (double)deferred_loss(zs, ys, ibs);  // the partial last ring (empty rings add 0)
+  if (l == 0) sm.loss[w] = loss_total;
 #ifdef DGT_TINY_STAMPS
   if (a.stamps && l == 0 && w < 2)
     for (int i = 0; i < 5; ++i) a.stamps[w * 8 + i] = st_acc[i];
@@ -503,7 +511,10 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   }
   __syncthreads();
   if (t == 0) {
-    *a.loss_acc += loss_total;
+    double total = 0.0;
+#pragma unroll
+    for (int i = 0; i < C::NW; ++i) total += sm.loss[i];
+    *a.loss_acc += total;
     *a.status = sm.err ? kTimeout : kOk;
   }
 }
