@@ -71,7 +71,7 @@ int main(int argc, char** argv) {
   a.ex.rank = 0; a.ex.world_size = 1;
   a.stamps = dStamps;
   float* dBc;
-  CK(hipMalloc(&dBc, (size_t)steps * 2 * sizeof(float)));
+  CK(hipMalloc(&dBc, (size_t)(steps + 1) * 2 * sizeof(float)));  // +1: read-ahead of the kernel
   a.bc = dBc;
   CK(dgt::tiny_mlp_train(F, H, a, 0));
   CK(hipDeviceSynchronize());
