@@ -58,10 +58,12 @@ DGT_DEVICE long long ll_slot(const Exchange& ex, int parity, int src) {
   return (long long)(parity * kMaxRanks + src) * ex.stride * 2;
 }
 
-// push one LL line (two payload floats) into a peer's mailbox: one 16-byte streaming store
+// push one LL line (two payload floats) into a peer's mailbox: one plain 16-byte store (the
+// mailbox is uncached memory, so it goes straight to the peer's HBM; the streaming (nt) hint is
+// left off: on hand-off traffic it measured slower, MI355X_MICROARCH.md "nt-handoff")
 DGT_DEVICE void ll_put(unsigned* dst, float a, float b, unsigned tag) {
   u32x4 v = {__float_as_uint(a), tag, __float_as_uint(b), tag};
-  __builtin_nontemporal_store(v, reinterpret_cast<u32x4*>(dst));
+  *reinterpret_cast<u32x4*>(dst) = v;
 }
 
 // one {payload, tag} pair from the local mailbox: a relaxed system-scope 64-bit load (sc0 sc1,
