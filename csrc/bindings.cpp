@@ -386,12 +386,17 @@ void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, co
 }
 
 // ------------------------------------------------------------------------------ IPC runtime
-int64_t ipc_alloc(int64_t nbytes, bool uncached, int64_t device) {
+// kind: 0 = coarse-grained (hipMalloc), 1 = uncached (no cache holds a line: peers' xGMI writes
+// are seen by the next poll), 2 = fine-grained (cacheable, kept coherent by the fabric)
+int64_t ipc_alloc(int64_t nbytes, int64_t kind, int64_t device) {
   TORCH_CHECK(nbytes > 0, "dgt: ipc_alloc needs a positive size");
+  TORCH_CHECK(kind >= 0 && kind <= 2, "dgt: ipc_alloc kind must be 0 (coarse), 1 (uncached) or 2 (fine-grained)");
   c10::DeviceGuard guard(c10::Device(c10::DeviceType::CUDA, (c10::DeviceIndex)device));
   void* p = nullptr;
-  if (uncached) {
+  if (kind == 1) {
     DGT_CHECK_HIP(hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocUncached));
+  } else if (kind == 2) {
+    DGT_CHECK_HIP(hipExtMallocWithFlags(&p, (size_t)nbytes, hipDeviceMallocFinegrained));
   } else {
     DGT_CHECK_HIP(hipMalloc(&p, (size_t)nbytes));
   }
@@ -473,7 +478,7 @@ TORCH_LIBRARY(dgt, m) {
       "mlp_head(Tensor a, Tensor w, Tensor b0, Tensor y, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!) db, "
       "Tensor(d!) loss_acc, Tensor(e!) g, Tensor(f!) gT) -> ()",
       &mlp_head);
-  m.def("ipc_alloc(int nbytes, bool uncached, int device) -> int", &ipc_alloc);
+  m.def("ipc_alloc(int nbytes, int kind, int device) -> int", &ipc_alloc);
   m.def("ipc_handle(int ptr) -> Tensor", &ipc_handle);
   m.def("ipc_open(Tensor handle, int device) -> int", &ipc_open);
   m.def("ipc_close(int ptr) -> ()", &ipc_close);

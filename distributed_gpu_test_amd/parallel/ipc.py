@@ -21,6 +21,7 @@ rank disables the channel everywhere and callers fall back to RCCL.
 from __future__ import annotations
 
 import os
+import socket
 from typing import List, Optional
 
 import torch
@@ -30,6 +31,16 @@ from . import comm
 
 MAX_RANKS = 8
 TICKS_PER_SECOND = 100_000_000  # s_memrealtime runs at 100 MHz
+MEM_KINDS = {"coarse": 0, "uncached": 1, "fine": 2}
+
+
+def mem_kind() -> str:
+    """Mailbox memory: ``uncached`` (default: correct by construction across GPUs, no cache ever
+    holds a mailbox line) or ``fine`` (``DGT_IPC_MEM=fine``: cacheable fine-grained memory)."""
+    k = os.environ.get("DGT_IPC_MEM", "uncached")
+    if k not in MEM_KINDS:
+        raise ValueError(f"DGT_IPC_MEM must be one of {sorted(MEM_KINDS)}")
+    return k
 
 
 class IpcChannel:
@@ -53,11 +64,17 @@ class IpcChannel:
         self.error: Optional[BaseException] = None
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         handle = b""
-        try:
-            self.local_ptr = self.ops.ipc_alloc(self.nbytes, True, self.device.index)
-            handle = bytes(self.ops.ipc_handle(self.local_ptr).numpy().tobytes())
-        except Exception as e:  # IPC not supported here: every rank must learn it below
-            self.error = e
+        # IPC handles only name memory on THIS node: a job that spans nodes never opens them
+        # (callers fall back to RCCL, which bridges nodes over the network)
+        hosts = comm.all_gather_object(socket.gethostname())
+        if len(set(hosts)) > 1:
+            self.error = RuntimeError(f"ranks span {len(set(hosts))} hosts: no cross-node IPC mailboxes")
+        else:
+            try:
+                self.local_ptr = self.ops.ipc_alloc(self.nbytes, MEM_KINDS[mem_kind()], self.device.index)
+                handle = bytes(self.ops.ipc_handle(self.local_ptr).numpy().tobytes())
+            except Exception as e:  # IPC not supported here: every rank must learn it below
+                self.error = e
         handles = comm.all_gather_object(handle)
         if self.error is None:
             try:
