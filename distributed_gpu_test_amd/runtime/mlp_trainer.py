@@ -6,7 +6,7 @@ One optimizer step, all on the GPU, no host sync:
 
     forward   a_l = relu(a_{l-1} W_l^T + b_l)   gemm_nt epilogue: bias + ReLU + bf16 a_l and a_l^T
     head      z = a_L w + b, BCE, dz, g_L = dz w^T * 1[a_L > 0] (+ g_L^T), dw, db      (mlp_head)
-    backward  dW_l = g_l^T a_{l-1}   -> fp32 gradient buffer                           (gemm_nt)
+    backward  dW_l = g_l^T a_{l-1}   -> bf16 (or fp32) gradient buffer                  (gemm_nt)
               db_l = row sums of g_l^T                                              (rowsum_bf16)
               g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0] (+ g_{l-1}^T)   epilogue: mask      (gemm_nt)
               each layer's weight gradient leaves for its collective as soon as its wgrad is
@@ -33,16 +33,19 @@ correct, but its row-piece access pattern measured slower than flat Adam + trans
 
 Parameters live in two flat regions:
 
-* the big region — the L weight matrices, bf16 for compute + fp32 gradients, each matrix padded to
-  a multiple of 64 * world_size elements (a per-layer communication bucket);
+* the big region — the L weight matrices, bf16 for compute + gradients (bf16 by default, as
+  PyTorch autocast's matmul backward produces them: half the wgrad store, Adam read and
+  collective bytes; ``grad_dtype=torch.float32`` / ``DGT_MLP_GRAD_DTYPE=fp32`` keeps fp32), each
+  matrix padded to a multiple of 64 * world_size elements (a per-layer communication bucket);
 * the small region — biases and the head, fp32 (the GEMM epilogues read fp32 biases), replicated
   on every rank and all-reduced as one bucket.
 
 ``zero_stage=0``: every rank keeps the full fp32 master of the big region; its buckets are
 all-reduced and one Adam launch updates everything.  ``zero_stage=1`` (DeepSpeed ZeRO-1/2 for the
-matrices): each bucket is REDUCE-SCATTERED into this rank's fp32 gradient shard, Adam updates
+matrices): each bucket is REDUCE-SCATTERED into this rank's gradient shard, Adam updates
 only the 1/N master shard (N x less optimizer traffic and memory), and the bf16 parameter shards
-are ALL-GATHERED back: 4 + 2 bytes on the wire per parameter instead of an fp32 all-reduce's 8.
+are ALL-GATHERED back: one reduce-scatter + one all-gather pass on the wire per parameter, the
+same bytes as an all-reduce, with 1/N of the Adam traffic.
 """
 from __future__ import annotations
 
@@ -72,9 +75,15 @@ class MLPTrainer:
 
     def __init__(self, model: SyntheticMLP, batch_size: int = 1024, n_batches: int = 8, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 1234,
-                 device: Optional[torch.device] = None, zero_stage: int = 0, schedule: Optional[str] = None):
+                 device: Optional[torch.device] = None, zero_stage: int = 0, schedule: Optional[str] = None,
+                 grad_dtype: Optional[torch.dtype] = None):
         if zero_stage not in (0, 1):
             raise ValueError("MLPTrainer supports zero_stage 0 or 1")
+        if grad_dtype is None:
+            grad_dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[os.environ.get("DGT_MLP_GRAD_DTYPE", "bf16")]
+        if grad_dtype not in (torch.bfloat16, torch.float32):
+            raise ValueError("grad_dtype must be torch.bfloat16 or torch.float32")
+        self.grad_dtype = grad_dtype
         schedule = schedule or os.environ.get("DGT_MLP_SCHEDULE", "auto")
         if schedule not in SCHEDULES + ("auto",):
             raise ValueError(f"schedule must be one of {SCHEDULES} or 'auto'")
@@ -119,7 +128,7 @@ class MLPTrainer:
         comm.broadcast_(s_full, 0)
 
         self.params_bf16 = w_full.to(torch.bfloat16)  # compute copy of every W_l
-        self.grads_w = torch.zeros(self.total_w, dtype=torch.float32, device=dev)
+        self.grads_w = torch.zeros(self.total_w, dtype=grad_dtype, device=dev)
         self.master_s = s_full
         self.grads_s = torch.zeros_like(self.master_s)
         self.m_s, self.v_s = torch.zeros_like(self.master_s), torch.zeros_like(self.master_s)
@@ -136,7 +145,7 @@ class MLPTrainer:
                       for i, n in enumerate(self.shard_len)]
             self.master_w = torch.cat(pieces).contiguous()
             self.lp_w = torch.empty(self.master_w.numel(), dtype=torch.bfloat16, device=dev)
-            self.shard_grad = torch.zeros_like(self.master_w)
+            self.shard_grad = torch.zeros(self.master_w.numel(), dtype=grad_dtype, device=dev)
             del w_full
         self.m_w, self.v_w = torch.zeros_like(self.master_w), torch.zeros_like(self.master_w)
 
@@ -302,7 +311,7 @@ class MLPTrainer:
         # s_opt once backward no longer reads W_i^T (after its dgrad) and the collective is done
         for i in reversed(range(L)):
             a_prevT = xT if i == 0 else self.aT[i]
-            gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=True)
+            gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=self.grad_dtype == torch.float32)
             rowsum_bf16(self.gT[cur], self.gb[i])
             if self.world_size > 1:
                 if ov:

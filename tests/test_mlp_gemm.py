@@ -13,13 +13,13 @@ from distributed_gpu_test_amd.ops.gemm import gemm_nt, gemm_nt_reference, mlp_he
 from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
 
 
-def _trainer_vs_torch(device):
+def _trainer_vs_torch(device, grad_dtype=torch.bfloat16):
     """One step of the trainer vs torch autograd on the same bf16-rounded weights and inputs:
     returns (trainer gradient, reference gradient, trainer loss, reference loss)."""
     torch.manual_seed(0)
     model = SyntheticMLP(width=128, depth=2)
     ref = copy.deepcopy(model)
-    tr = MLPTrainer(model, batch_size=128, n_batches=2, lr=1e-3, device=device)
+    tr = MLPTrainer(model, batch_size=128, n_batches=2, lr=1e-3, device=device, grad_dtype=grad_dtype)
     x = tr.X[:128].float().cpu()
     y = tr.Y[:128].float().cpu()
     with torch.no_grad():
@@ -29,13 +29,13 @@ def _trainer_vs_torch(device):
     ref_loss = torch.nn.functional.binary_cross_entropy_with_logits(ref(x).view(-1), y)
     ref_loss.backward()
     tr.step(0)
-    got = torch.cat([tr.grad_of(n).reshape(-1).cpu() for n, _ in ref.named_parameters()])
+    got = torch.cat([tr.grad_of(n).reshape(-1).float().cpu() for n, _ in ref.named_parameters()])
     want = torch.cat([p.grad.reshape(-1) for p in ref.parameters()])
     return got, want, float(tr.loss_acc.item()), float(ref_loss)
 
 
-def _check(device):
-    got, want, loss, ref_loss = _trainer_vs_torch(device)
+def _check(device, grad_dtype=torch.bfloat16):
+    got, want, loss, ref_loss = _trainer_vs_torch(device, grad_dtype)
     assert abs(loss - ref_loss) < 1e-2 * max(1.0, abs(ref_loss))
     scale = want.abs().max()
     torch.testing.assert_close(got / scale, want / scale, rtol=0, atol=3e-2)  # bf16 activations
@@ -43,8 +43,9 @@ def _check(device):
     assert cos > 0.999, float(cos)
 
 
-def test_trainer_cpu_reference_path():
-    _check(torch.device("cpu"))
+@pytest.mark.parametrize("grad_dtype", [torch.bfloat16, torch.float32])
+def test_trainer_cpu_reference_path(grad_dtype):
+    _check(torch.device("cpu"), grad_dtype)
 
 
 gpu = pytest.mark.gpu
@@ -147,8 +148,9 @@ def test_transpose_rowsum_head():
 
 
 @gpu
-def test_trainer_gpu_matches_torch():
-    _check(torch.device("cuda"))
+@pytest.mark.parametrize("grad_dtype", [torch.bfloat16, torch.float32])
+def test_trainer_gpu_matches_torch(grad_dtype):
+    _check(torch.device("cuda"), grad_dtype)
 
 
 def _run_schedule(device, schedule, steps=3):
