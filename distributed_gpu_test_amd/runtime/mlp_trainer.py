@@ -163,7 +163,8 @@ class MLPTrainer:
         self.gb = [sview(self.grads_s, f"layers.{i}.bias") for i in range(self.L)]
         self.hw, self.hb = sview(self.master_s, "head.weight"), sview(self.master_s, "head.bias")
         self.ghw, self.ghb = sview(self.grads_s, "head.weight"), sview(self.grads_s, "head.bias")
-        self.WT = [torch.empty(w.shape[1], w.shape[0], dtype=torch.bfloat16, device=dev) for w in self.W]
+        # W_l^T feeds the dgrad of layer l > 0 only (the input needs no gradient): no W_0^T
+        self.WT = [None] + [torch.empty(w.shape[1], w.shape[0], dtype=torch.bfloat16, device=dev) for w in self.W[1:]]
         self._refresh_transposes()
 
         # ---- activations (both layouts) and gradient scratch
@@ -192,6 +193,15 @@ class MLPTrainer:
         self._overlap = self.schedule == "overlap"
         self._opt_pending = False
         self.s_main = None
+        # "flat" on GPU: the W^T refresh runs on a side stream beside the next step's forward GEMMs
+        # (only the dgrads read W^T); DGT_MLP_T_SIDE=0 keeps it on the main stream
+        self._t_side = (self.schedule == "flat" and dev.type == "cuda"
+                        and os.environ.get("DGT_MLP_T_SIDE", "1") == "1" and self.L > 1)
+        self._t_pending = False
+        if self._t_side:
+            self.s_t = torch.cuda.Stream(dev)
+            self.ev_adam = torch.cuda.Event()
+            self.ev_t = [torch.cuda.Event() for _ in range(self.L)]
         if self._overlap:
             if os.environ.get("DGT_MLP_PRIO", "0") == "1":  # GEMM stream ahead of the optimizer stream
                 self.s_main = torch.cuda.Stream(dev, priority=-1)
@@ -204,8 +214,9 @@ class MLPTrainer:
 
     # ------------------------------------------------------------------ helpers
     def _refresh_transposes(self):
-        for w, wt in zip(self.W, self.WT):
-            transpose_bf16(w, wt)
+        # W_0^T is never read (layer 0 has no dgrad: the input needs no gradient)
+        for i in range(1, self.L):
+            transpose_bf16(self.W[i], self.WT[i])
 
     def flops_per_step(self) -> int:
         return self.model.flops_per_sample() * self.B
@@ -257,7 +268,7 @@ class MLPTrainer:
         if self.zero_stage == 0:
             R, Cc = self.shapes[i]
             o = self.w_off[i]
-            if self.matrix_t and R % 64 == 0 and Cc % 128 == 0:
+            if self.matrix_t and i > 0 and R % 64 == 0 and Cc % 128 == 0:
                 sl = slice(o, o + R * Cc)
                 adam_matrix_t_(self.master_w[sl], self.params_bf16[sl], self.WT[i], self.grads_w[sl], self.m_w[sl],
                                self.v_w[sl], R, Cc, *args, grad_scale=scale)
@@ -274,10 +285,14 @@ class MLPTrainer:
             self._collective(dist.all_gather_into_tensor, out, self.lp_w[sl], works=works)
             for w in works:
                 w.wait()
-        transpose_bf16(self.W[i], self.WT[i])
+        if i > 0:  # W_0^T is never read
+            transpose_bf16(self.W[i], self.WT[i])
 
     def join(self) -> None:
         """Make the caller's stream wait for the side streams (results visible to later work)."""
+        if self._t_pending:
+            torch.cuda.current_stream(self.device).wait_stream(self.s_t)
+            self._t_pending = False
         if self._opt_pending:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_stream(self.s_opt)
@@ -326,6 +341,8 @@ class MLPTrainer:
                 else:
                     self._reduce_layer(i, works)
             if i > 0:
+                if self._t_pending:
+                    torch.cuda.current_stream(self.device).wait_event(self.ev_t[i])
                 gemm_nt(self.g[cur], self.WT[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i])
                 cur ^= 1
             if ov:
@@ -353,7 +370,17 @@ class MLPTrainer:
                        grad_scale=1.0 / self.world_size, param_lp=self.lp_w)
             if self.zero_stage == 1:
                 self._allgather_params()
-            self._refresh_transposes()
+            if self._t_side:
+                main_s = torch.cuda.current_stream(self.device)
+                self.ev_adam.record(main_s)
+                self.s_t.wait_event(self.ev_adam)
+                with torch.cuda.stream(self.s_t):
+                    for i in reversed(range(1, L)):  # the order the next backward reads them
+                        transpose_bf16(self.W[i], self.WT[i])
+                        self.ev_t[i].record(self.s_t)
+                self._t_pending = True
+            else:
+                self._refresh_transposes()
 
     # bench.py adapter (same surface as TinyMLPTrainer)
     def epoch_plan(self, epoch: int):

