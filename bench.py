@@ -220,10 +220,11 @@ def main(argv=None):
         # learns about it here and the whole job re-runs on the RCCL path instead of dying
         if getattr(trainer, "impl", "") != "fused":
             raise
-        fallback = "graph" if comm.backend_name() == "nccl" else "stepwise"
-        print(f"[bench] fused path failed ({e}); falling back to {fallback} (RCCL)", file=sys.stderr, flush=True)
+        print(f"[bench] fused path failed ({e}); falling back to the RCCL path", file=sys.stderr, flush=True)
         trainer.close()
-        trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=fallback, device=device)
+        # use_ipc=False: the trainer's own automatic fallback (HIP graph with the native RCCL
+        # communicator, or plain ProcessGroupNCCL if that cannot be set up on every rank)
+        trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl="fused", device=device, use_ipc=False)
         plan, counts = build_plan(trainer, args.warmup + args.steps)
         elapsed_max, mean_loss = timed_run(trainer, plan, counts, args, device, comm)
 

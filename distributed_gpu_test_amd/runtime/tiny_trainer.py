@@ -98,14 +98,29 @@ class TinyMLPTrainer:
                                         else os.environ.get("DGT_EXCHANGE_TIMEOUT_S", 60.0))
         self.faults = FaultInjector.from_env(self.rank)
 
+        self._auto_fallback = False
         if self.impl == "fused" and self.world_size > 1:
             self.channel = self._open_channel() if use_ipc else None
             if self.channel is None:
                 self.impl = "graph" if comm.backend_name() == "nccl" else "stepwise"
+                self._auto_fallback = True
         self._graph = None
         self.rccl = None
         if self.impl == "graph":
-            self._setup_graph()
+            try:
+                self._setup_graph()
+            except Exception as e:
+                # an automatic fallback must not take the job down: every rank agrees on the
+                # plain ProcessGroupNCCL path instead
+                if not self._auto_fallback:
+                    raise
+                print(f"[dgt] graph path unavailable ({e}); using stepwise", flush=True)
+                self.impl = "stepwise"
+        if self._auto_fallback and self.world_size > 1:
+            agreed = comm.all_reduce_max(1.0 if self.impl == "stepwise" else 0.0)
+            if agreed > 0 and self.impl != "stepwise":
+                self.close_graph_resources()
+                self.impl = "stepwise"
 
     # ------------------------------------------------------------------ setup helpers
     def _open_channel(self):
@@ -284,6 +299,12 @@ class TinyMLPTrainer:
             self.global_steps = int(states.get("global_steps", 0))
         self.global_samples = int(states.get("global_samples", 0))
         return path, states.get("client_state", {})
+
+    def close_graph_resources(self) -> None:
+        if self.rccl is not None:
+            self.rccl.close()
+            self.rccl = None
+        self._graph = None
 
     def close(self) -> None:
         if self.channel is not None:
