@@ -277,11 +277,14 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
 void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant) {
+  TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
   TORCH_CHECK(variant >= 0 && variant <= 4,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (128x128, 4 stages) "
               "or 4 (128x128, 4 stages, 8 waves)");
-  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt needs A[M,K], B[N,K]");
-  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+  const bool b_kn = (epi & dgt::kEpiBKN) != 0;
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
+              b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
+  const int64_t M = A.size(0), N = B.size(b_kn ? 1 : 0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {  // rows may be strided (column blocks of a wider matrix)
     TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16, "dgt: gemm_nt operands must be bf16 GPU tensors");
     TORCH_CHECK(t->stride(1) == 1 && t->stride(0) >= t->size(1) && t->stride(0) % 8 == 0,

@@ -96,9 +96,11 @@ enum GemmEpilogue : int {
   kEpiStoreT = 8,      // also write C^T (bf16, row stride ldct)
   kEpiOutF32 = 16,     // C is fp32 (else bf16)
   kEpiAccumulate = 32, // C += result (fp32 only)
+  kEpiBKN = 64,        // B is given as [K, N] (N contiguous): C = A . B, read with transposed LDS reads
 };
 
 struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 A/B, fp32 accumulate
+                       // (kEpiBKN: B is [K,N] and C = alpha * A . B)
   const void* A;
   const void* B;
   void* C;             // bf16 or fp32 [M, ldc]; may be null when only C^T is wanted

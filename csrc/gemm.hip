@@ -56,6 +56,61 @@ DGT_DEVICE bf16x8 read_frag(const u16* lds, int row, int chunk) {
   return *reinterpret_cast<const bf16x8*>(lds + row * GBK + p * 8);
 }
 
+// ---- B given as [K, N] (N contiguous, e.g. the weight W[out, in] as the dgrad's B operand): the
+// K-tile is staged as it lies in memory, [64 k][128 n] with 256-byte rows, and the MFMA B fragment
+// (8 consecutive k of one n per lane) is read with two gfx950 ds_read_b64_tr_b16 transposed reads
+// (cdna_hip_programming.md T10), so no transposed copy of W is ever materialised.  The 16 16-byte
+// chunks of row r are XOR-swizzled by ((r & 3) << 2) | ((r >> 2) & 3) (the guide's 256-byte-row
+// image): conflict-free for the two 4-row blocks 8 rows apart that a 32-lane half reads.
+DGT_DEVICE int kn_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
+
+template <int NWAVE = 4>
+DGT_DEVICE void stage_tile_kn(const u16* __restrict__ src, int ld, int k0, int n0, u16* lds, int w, int l) {
+  constexpr int PER_WAVE = 16 / NWAVE;         // 1 KiB wave-instructions per wave (4 rows each)
+#pragma unroll
+  for (int i = 0; i < PER_WAVE; ++i) {
+    const int rblk = (w * PER_WAVE + i) * 4;   // first of the 4 k-rows this wave-instruction writes
+    const int row = rblk + (l >> 4);
+    const int c = (l & 15) ^ kn_swz(row);      // logical chunk fetched into physical chunk l & 15
+    const u16* g = src + (long long)(k0 + row) * ld + n0 + c * 8;
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(g), reinterpret_cast<int*>(lds + rblk * GBN), 16, 0,
+                                     0);
+  }
+}
+
+// B operand staging of the 128x128 kernel: [N, K] rows (stage_tile) or [K, N] rows (stage_tile_kn)
+template <bool KN, int NWAVE>
+DGT_DEVICE void stage_b(const u16* __restrict__ src, int ld, int n0, int k0, u16* lds, int w, int l) {
+  if constexpr (KN) stage_tile_kn<NWAVE>(src, ld, k0, n0, lds, w, l);
+  else stage_tile<NWAVE>(src, ld, n0, k0, lds, w, l);
+}
+
+typedef short i16x4 __attribute__((ext_vector_type(4)));
+typedef short i16x8 __attribute__((ext_vector_type(8)));
+
+// lane (n = l & 15, kg = l >> 4) receives B[kb + 8kg + e][nb + n], e = 0..7: lane 4q + p of its
+// 16-lane group supplies the address of row kb + 8kg + q (+4), columns nb + 4p .. nb + 4p + 3.
+// Inline asm: the builtin's memory operand makes the compiler drain every in-flight LDS-DMA
+// (vmcnt(0)) before each read, which serialises the staging pipeline; the caller waits lgkmcnt
+// itself (tr_wait) before the fragments are used.
+DGT_DEVICE void read_frag_kn(const u16* lds, int kb, int nb, int l, i16x4& lo, i16x4& hi) {
+  const int q = (l >> 2) & 3, col = nb + 4 * (l & 3);
+  const int r0 = kb + 8 * (l >> 4) + q, r1 = r0 + 4;
+  const u16* a0 = lds + r0 * GBN + (((col >> 3) ^ kn_swz(r0)) << 3) + (col & 4);
+  const u16* a1 = lds + r1 * GBN + (((col >> 3) ^ kn_swz(r1)) << 3) + (col & 4);
+  const unsigned o0 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) const u16*)(a0));
+  const unsigned o1 = (unsigned)(uintptr_t)((__attribute__((address_space(3))) const u16*)(a1));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(o0));
+  asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(o1));
+}
+
+// wait for the asm transposed reads; the operands tie the wait to the registers it guards
+DGT_DEVICE bf16x8 tr_wait(i16x4& lo, i16x4& hi) {
+  asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(lo), "+v"(hi));
+  const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // One MFMA accumulator (rows mb..mb+3 of column n) through the fused epilogue.
 template <int EPI>
 DGT_DEVICE void epi_store(const GemmArgs& g, const f32x4& acc, int mb, int n) {
@@ -189,6 +244,7 @@ DGT_DEVICE void wait_vmcnt() {
 // 4-wave block leaves the matrix core idle while its only wave waits on LDS).
 template <int EPI, int S, int NW = 4>
 __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
+  constexpr bool KN = (EPI & kEpiBKN) != 0;      // B is [K, N]: staged as is, transposed reads
   constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
   constexpr int WCOLS = GBN / WN;                // waves across N
   constexpr int NJ = WN / 16;                    // accumulator columns per wave
@@ -217,8 +273,16 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       bf16x8 af[4], bfr[NJ];
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[i] = read_frag(As, wr * 64 + i * 16 + (l & 15), chunk);
+      if constexpr (KN) {
+        i16x4 blo[NJ], bhi[NJ];
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = read_frag(Bs, wc * WN + j * 16 + (l & 15), chunk);
+        for (int j = 0; j < NJ; ++j) read_frag_kn(Bs, kk * 32, wc * WN + j * 16, l, blo[j], bhi[j]);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[j] = tr_wait(blo[j], bhi[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[j] = read_frag(Bs, wc * WN + j * 16 + (l & 15), chunk);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -228,14 +292,14 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
   };
   if constexpr (S == 2) {
     stage_tile<NW>(A, g.lda, m0, 0, lds[0][0], w, l);
-    stage_tile<NW>(B, g.ldb, n0, 0, lds[0][1], w, l);
+    stage_b<KN, NW>(B, g.ldb, n0, 0, lds[0][1], w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < nk) {
         stage_tile<NW>(A, g.lda, m0, (kt + 1) * GBK, lds[cur ^ 1][0], w, l);
-        stage_tile<NW>(B, g.ldb, n0, (kt + 1) * GBK, lds[cur ^ 1][1], w, l);
+        stage_b<KN, NW>(B, g.ldb, n0, (kt + 1) * GBK, lds[cur ^ 1][1], w, l);
       }
       compute(cur);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -247,7 +311,7 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
     for (int p = 0; p < S - 1; ++p) {
       if (p < nk) {
         stage_tile<NW>(A, g.lda, m0, p * GBK, lds[p][0], w, l);
-        stage_tile<NW>(B, g.ldb, n0, p * GBK, lds[p][1], w, l);
+        stage_b<KN, NW>(B, g.ldb, n0, p * GBK, lds[p][1], w, l);
       }
     }
     int buf = 0;
@@ -263,7 +327,7 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       if (kt + S - 1 < nk) {
         const int nb = (buf + S - 1) % S;
         stage_tile<NW>(A, g.lda, m0, (kt + S - 1) * GBK, lds[nb][0], w, l);
-        stage_tile<NW>(B, g.ldb, n0, (kt + S - 1) * GBK, lds[nb][1], w, l);
+        stage_b<KN, NW>(B, g.ldb, n0, (kt + S - 1) * GBK, lds[nb][1], w, l);
       }
       compute(buf);
       buf = (buf + 1 == S) ? 0 : buf + 1;
@@ -504,11 +568,21 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
     if (!fits256) return hipErrorInvalidValue;
     big = true;
   }
+  if (epi & kEpiBKN) {  // only the 128x128 kernel reads a [K, N] B operand
+    if (variant == 2) return hipErrorInvalidValue;
+    big = false;
+  }
   const int grid = big ? (g.M / 256) * (g.N / 256) : (g.M / GBM) * (g.N / GBN);
   // a grid that fits the chip at one block per CU gains nothing from 2 blocks/CU: spend the LDS on
   // a deep (4-stage) pipeline instead
   const bool deep = !big && (variant == 3 || variant == 4 || (variant == 0 && grid <= 256));
   const bool eight = deep && variant != 3;  // measured: 8 waves beat 4 on one-wave grids (817 vs 759 TF)
+#define DGT_EPI_CASE_KN(E)                                                                        \
+  case E:                                                                                         \
+    if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (deep) hipLaunchKernelGGL((gemm_nt_kernel<E, 4>), dim3(grid), dim3(256), 0, stream, g); \
+    else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
+    break;
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
     if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
@@ -524,10 +598,14 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
     DGT_EPI_CASE(kEpiOutF32)                                       // wgrad into fp32 grads
     DGT_EPI_CASE(kEpiOutF32 | kEpiAccumulate)                      // wgrad, gradient accumulation
     DGT_EPI_CASE(kEpiOutF32 | kEpiBias)                            // generic fp32 out
+    DGT_EPI_CASE_KN(kEpiMask | kEpiStoreT | kEpiBKN)               // dgrad straight from W[out, in]
+    DGT_EPI_CASE_KN(kEpiBKN)                                       // plain A . B
+    DGT_EPI_CASE_KN(kEpiOutF32 | kEpiBKN)
     default:
       return hipErrorInvalidValue;
   }
 #undef DGT_EPI_CASE
+#undef DGT_EPI_CASE_KN
   return hipGetLastError();
 }
 

@@ -15,12 +15,12 @@ import torch
 
 from ._ext import require
 
-EPI_BIAS, EPI_RELU, EPI_MASK, EPI_STORE_T, EPI_OUT_F32, EPI_ACCUMULATE = 1, 2, 4, 8, 16, 32
+EPI_BIAS, EPI_RELU, EPI_MASK, EPI_STORE_T, EPI_OUT_F32, EPI_ACCUMULATE, EPI_B_KN = 1, 2, 4, 8, 16, 32, 64
 
 
 def gemm_nt_reference(A, B, C=None, CT=None, bias=None, mask=None, relu=False, out_f32=False,
-                      accumulate=False, alpha=1.0):
-    r = (A.float() @ B.float().t()) * alpha
+                      accumulate=False, alpha=1.0, b_kn=False):
+    r = (A.float() @ (B.float() if b_kn else B.float().t())) * alpha
     if bias is not None:
         r = r + bias.float()
     if relu:
@@ -39,15 +39,19 @@ def gemm_nt_reference(A, B, C=None, CT=None, bias=None, mask=None, relu=False, o
 
 def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, CT: Optional[torch.Tensor] = None,
             bias: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, relu: bool = False,
-            out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0) -> None:
+            out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0,
+            b_kn: bool = False) -> None:
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage, 2 = 256x256 8-phase pipeline,
-    3 = 128x128 tiles 4-stage, 4 = 128x128 tiles 4-stage with 8 waves."""
+    3 = 128x128 tiles 4-stage, 4 = 128x128 tiles 4-stage with 8 waves.
+
+    ``b_kn=True``: B is given as ``[K, N]`` (N contiguous) and ``C = alpha * A @ B`` — the operand is
+    staged as it lies and read with transposed LDS reads (128x128 kernels only)."""
     if not A.is_cuda:
-        gemm_nt_reference(A, B, C, CT, bias, mask, relu, out_f32, accumulate, alpha)
+        gemm_nt_reference(A, B, C, CT, bias, mask, relu, out_f32, accumulate, alpha, b_kn)
         return
     epi = ((EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | (EPI_MASK if mask is not None else 0)
            | (EPI_STORE_T if CT is not None else 0) | (EPI_OUT_F32 if out_f32 else 0)
-           | (EPI_ACCUMULATE if accumulate else 0))
+           | (EPI_ACCUMULATE if accumulate else 0) | (EPI_B_KN if b_kn else 0))
     require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant))
 
 

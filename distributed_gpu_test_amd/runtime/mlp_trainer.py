@@ -8,12 +8,13 @@ One optimizer step, all on the GPU, no host sync:
     head      z = a_L w + b, BCE, dz, g_L = dz w^T * 1[a_L > 0] (+ g_L^T), dw, db      (mlp_head)
     backward  dW_l = g_l^T a_{l-1}   -> bf16 (or fp32) gradient buffer                  (gemm_nt)
               db_l = row sums of g_l^T                                              (rowsum_bf16)
-              g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0] (+ g_{l-1}^T)   epilogue: mask      (gemm_nt)
+              g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0] (+ g_{l-1}^T)   epilogue: mask  (gemm_nt, b_kn)
               each layer's weight gradient leaves for its collective as soon as its wgrad is
               enqueued (RCCL over xGMI on the process group's stream): the collective overlaps
               the remaining backward GEMMs
     update    fused Adam over the fp32 masters that also writes the bf16 compute copy (ZeRO-1: on
-              the shard, then all-gather); W_l^T refreshed by a tiled transpose
+              the shard, then all-gather); the dgrad GEMM reads W_l[out, in] directly (a [K, N]
+              operand through gfx950 transposed LDS reads), so no transposed weight copy exists
 
 Schedules (``schedule=`` or ``DGT_MLP_SCHEDULE``):
 
@@ -163,8 +164,15 @@ class MLPTrainer:
         self.gb = [sview(self.grads_s, f"layers.{i}.bias") for i in range(self.L)]
         self.hw, self.hb = sview(self.master_s, "head.weight"), sview(self.master_s, "head.bias")
         self.ghw, self.ghb = sview(self.grads_s, "head.weight"), sview(self.grads_s, "head.bias")
-        # W_l^T feeds the dgrad of layer l > 0 only (the input needs no gradient): no W_0^T
-        self.WT = [None] + [torch.empty(w.shape[1], w.shape[0], dtype=torch.bfloat16, device=dev) for w in self.W[1:]]
+        # dgrad g_{l-1} = g_l . W_l: by default the GEMM reads W_l[out, in] as a [K, N] operand
+        # through transposed LDS reads (gemm_nt(..., b_kn=True)), so no W^T exists at all;
+        # DGT_MLP_DGRAD=nt keeps a refreshed bf16 W_l^T and the plain NT kernel (A/B baseline).
+        # W_l^T would feed the dgrad of layer l > 0 only (the input needs no gradient): no W_0^T.
+        self.dgrad_kn = os.environ.get("DGT_MLP_DGRAD", "kn") != "nt"
+        self.WT = [None] * self.L
+        if not self.dgrad_kn:
+            self.WT = [None] + [torch.empty(w.shape[1], w.shape[0], dtype=torch.bfloat16, device=dev)
+                                for w in self.W[1:]]
         self._refresh_transposes()
 
         # ---- activations (both layouts) and gradient scratch
@@ -195,7 +203,7 @@ class MLPTrainer:
         self.s_main = None
         # "flat" on GPU: the W^T refresh runs on a side stream beside the next step's forward GEMMs
         # (only the dgrads read W^T); DGT_MLP_T_SIDE=0 keeps it on the main stream
-        self._t_side = (self.schedule == "flat" and dev.type == "cuda"
+        self._t_side = (self.schedule == "flat" and dev.type == "cuda" and not self.dgrad_kn
                         and os.environ.get("DGT_MLP_T_SIDE", "1") == "1" and self.L > 1)
         self._t_pending = False
         if self._t_side:
@@ -215,6 +223,8 @@ class MLPTrainer:
     # ------------------------------------------------------------------ helpers
     def _refresh_transposes(self):
         # W_0^T is never read (layer 0 has no dgrad: the input needs no gradient)
+        if self.dgrad_kn:
+            return
         for i in range(1, self.L):
             transpose_bf16(self.W[i], self.WT[i])
 
@@ -268,7 +278,7 @@ class MLPTrainer:
         if self.zero_stage == 0:
             R, Cc = self.shapes[i]
             o = self.w_off[i]
-            if self.matrix_t and i > 0 and R % 64 == 0 and Cc % 128 == 0:
+            if self.matrix_t and not self.dgrad_kn and i > 0 and R % 64 == 0 and Cc % 128 == 0:
                 sl = slice(o, o + R * Cc)
                 adam_matrix_t_(self.master_w[sl], self.params_bf16[sl], self.WT[i], self.grads_w[sl], self.m_w[sl],
                                self.v_w[sl], R, Cc, *args, grad_scale=scale)
@@ -285,7 +295,7 @@ class MLPTrainer:
             self._collective(dist.all_gather_into_tensor, out, self.lp_w[sl], works=works)
             for w in works:
                 w.wait()
-        if i > 0:  # W_0^T is never read
+        if i > 0 and not self.dgrad_kn:  # W_0^T is never read
             transpose_bf16(self.W[i], self.WT[i])
 
     def join(self) -> None:
@@ -343,7 +353,10 @@ class MLPTrainer:
             if i > 0:
                 if self._t_pending:
                     torch.cuda.current_stream(self.device).wait_event(self.ev_t[i])
-                gemm_nt(self.g[cur], self.WT[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i])
+                if self.dgrad_kn:
+                    gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True)
+                else:
+                    gemm_nt(self.g[cur], self.WT[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i])
                 cur ^= 1
             if ov:
                 self.ev_bwd[i].record(main)
