@@ -32,9 +32,15 @@ struct TinyTrainArgs {
   int* status;           // Status
   Exchange ex;           // world_size 1 -> no exchange
   unsigned long long* stamps;  // diagnostic builds only (-DDGT_TINY_STAMPS); nullptr otherwise
+  int bc_ready;          // 1: bc already holds this launch's table (tiny_mlp_bias_table); skip filling it
 };
 
 hipError_t tiny_mlp_train(int n_features, int hidden, const TinyTrainArgs& a, hipStream_t stream);
+
+// Fill bc[2 s], bc[2 s + 1] (s < n_steps) with the Adam bias corrections of optimizer step
+// step0 + s + 1, as tiny_mlp_train would before its loop (a precomputed schedule, like an LR table).
+hipError_t tiny_mlp_bias_table(float* bc, int n_steps, long long step0, double lr, double beta1, double beta2,
+                               hipStream_t stream);
 
 struct TinyGradArgs {
   const float* X;

@@ -582,11 +582,20 @@ __global__ void adam_bias_table_kernel(float* bc, int n, long long step0, double
   bc[2 * s + 1] = (float)(1.0 / sqrt(1.0 - pow(beta2, t)));
 }
 
+hipError_t tiny_mlp_bias_table(float* bc, int n_steps, long long step0, double lr, double beta1, double beta2,
+                               hipStream_t stream) {
+  if (!bc || n_steps < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(adam_bias_table_kernel, dim3((n_steps + 255) / 256), dim3(256), 0, stream, bc, n_steps, step0, lr,
+                     beta1, beta2);
+  return hipGetLastError();
+}
+
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
   if (!a.bc) return hipErrorInvalidValue;
   const bool wd = a.hp.weight_decay != 0.f;
-  hipLaunchKernelGGL(adam_bias_table_kernel, dim3((a.n_steps + 255) / 256), dim3(256), 0, stream, a.bc, a.n_steps,
-                     a.adam_step0, a.lr, a.beta1, a.beta2);
+  if (!a.bc_ready)
+    hipLaunchKernelGGL(adam_bias_table_kernel, dim3((a.n_steps + 255) / 256), dim3(256), 0, stream, a.bc, a.n_steps,
+                       a.adam_step0, a.lr, a.beta1, a.beta2);
 #define DGT_TINY_LAUNCH(F_, H_, SB, XC)                                                          \
   do {                                                                                      \
     if (wd)                                                                                 \

@@ -106,6 +106,10 @@ class TinyMLPTrainer:
                 self._auto_fallback = True
         self._graph = None
         self.rccl = None
+        self._ws = None
+        self._ws_key = None
+        if self.impl == "fused":
+            self.reserve(self.steps_per_epoch())
         if self.impl == "graph":
             try:
                 self._setup_graph()
@@ -190,6 +194,25 @@ class TinyMLPTrainer:
         return plan.to(self.device), counts.to(self.device)
 
     # ------------------------------------------------------------------ training
+    def reserve(self, n_steps: int) -> None:
+        """Size the fused kernel's per-launch workspace (Adam bias-correction table) for launches of
+        up to ``n_steps`` steps, so no allocation happens on the launch path."""
+        need = (max(int(n_steps), 1) + 1) * 2
+        if self.impl == "fused" and (self._ws is None or self._ws.numel() < need):
+            self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
+            self._ws_key = None
+
+    def prepare(self, n_steps: int) -> None:
+        """Precompute the Adam bias-correction schedule of the NEXT ``n_steps`` optimizer steps (a
+        pure function of the step numbers and lr / betas, like an LR-schedule table), so the next
+        ``run_plan`` of exactly that many steps launches one kernel instead of two."""
+        if self.impl != "fused" or n_steps < 1:
+            return
+        self.reserve(n_steps)
+        _ext.require().tiny_mlp_bias_table(self._ws, int(n_steps), self.global_steps, self.lr, self.betas[0],
+                                           self.betas[1])
+        self._ws_key = (self.global_steps, int(n_steps))
+
     def run_plan(self, plan: torch.Tensor, counts: torch.Tensor) -> None:
         """Run len(plan) optimizer steps (asynchronously on GPU); loss accumulates into loss_acc."""
         n = int(plan.shape[0])
@@ -199,12 +222,16 @@ class TinyMLPTrainer:
             ops = _ext.require()
             ch = self.channel
             seq = ch.next_seq(n) if ch is not None else 0
+            ready = self._ws_key == (self.global_steps, n)
+            self._ws_key = None
+            if not ready:
+                self.reserve(n)
             ops.tiny_mlp_train(self.x, self.y, plan, counts, self.params, self.exp_avg, self.exp_avg_sq,
                                self.loss_acc, self.status, self.F, self.H, self.lr, self.betas[0], self.betas[1],
                                self.eps, self.weight_decay, self.adamw, self.global_steps,
                                ch.data_ptrs if ch else [], self.rank,
                                self.world_size, ch.stride if ch else 0, seq,
-                               ch.timeout_ticks if ch else 0)
+                               ch.timeout_ticks if ch else 0, self._ws, ready)
             self.global_steps += n
         elif self.impl == "graph":
             self.step_dev.fill_(self.global_steps)

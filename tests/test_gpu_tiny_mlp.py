@@ -127,3 +127,28 @@ def test_native_rccl_comm_single_rank():
     torch.testing.assert_close(out, t)
     assert RcclComm.version() >= 22000
     c.close()
+
+
+def test_prepared_bias_table_matches_inline():
+    """prepare(n) precomputes the bias-correction schedule; the next launch of n steps uses it and
+    must be bit-identical to a launch that fills the table itself."""
+    import torch
+    from distributed_gpu_test_amd.data import make_synthetic_data
+    from distributed_gpu_test_amd.models import SimpleNet
+    from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
+    dev = torch.device("cuda", 0)
+    outs = []
+    for prepared in (False, True):
+        torch.manual_seed(42)
+        x, y = make_synthetic_data(2000, 20, 42)
+        tr = TinyMLPTrainer(SimpleNet(20, 64), x, y, 4, impl="fused", device=dev)
+        plan, counts = tr.epoch_plan(1)
+        tr.run_plan(plan[:37], counts[:37])
+        if prepared:
+            tr.prepare(100)
+        tr.run_plan(plan[37:137], counts[37:137])
+        torch.cuda.synchronize()
+        outs.append((tr.params.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(), float(tr.loss_acc.item())))
+    for a, b in zip(outs[0][:3], outs[1][:3]):
+        assert torch.equal(a, b)
+    assert outs[0][3] == outs[1][3]
