@@ -329,12 +329,14 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(1);
     __syncthreads();  // the step's only workgroup barrier: all partial logits published
     DGT_STAMP(2);
-    // only the exchange can fail, so the single-rank loop reads no flag after the barrier
+    float gw1[C::NSP];
+    const StepGrads sg = wave_backward<F, H, false, SMALLB>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
+    // only the exchange can fail, so the single-rank loop reads no flag; with the exchange the flag
+    // is read AFTER the backward (which changes no state), so its LDS round trip overlaps the
+    // backward's instead of sitting between the barrier and the partial-logit reads
     if constexpr (XCH) {
       if (sm.err) break;
     }
-    float gw1[C::NSP];
-    const StepGrads sg = wave_backward<F, H, false, SMALLB>(st, ws, Zb, lr, lq, h, w2v, y, Bt, invB, gw1);
     float gbw = sg.bw, gb2 = sg.b2;
     // Deferred loss (reporting only, off the per-step critical path): steps 4j..4j+3 belong to
     // wave j % NW, whose lane row lq keeps step s's logits when s % 4 == lq; at the block's last
