@@ -273,20 +273,23 @@ DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row
 }
 
 // ------------------------------------------------------------------ persistent training kernel
-// XCH: world size > 1 (the exchange is compiled in).  The single-rank kernel has no exchange
+// NP > 1: the exchange is compiled in (for up to NP ranks).  The single-rank kernel has no exchange
 // branch, so backward and Adam form one basic block the scheduler can interleave.
 // WD: weight decay != 0 (Adam's L2 term / AdamW's decay compiled in; the reference's Adam has none,
 // and the per-pair uniform branches cost ~12 scalar branches per step).
-template <int F, int H, bool SMALLB, bool XCH, bool WD>
+template <int F, int H, bool SMALLB, int NP, bool WD>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
+  // NP: ranks the exchange is compiled for (1 = none; else the world size rounded up to 2, 4 or 8):
+  // the poll registers scale with it, so 2- and 4-rank jobs do not carry the 8-rank register set
+  constexpr bool XCH = NP > 1;
   __shared__ TinySmem<F, H> sm;
   const int t = threadIdx.x, l = t & 63, lr = l & 15, lq = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar branches on w
   const Exchange& ex = a.ex;
   WaveSmem<F, H>& ws = sm.w[w];
 
-  if (a.bmax > (SMALLB ? 4 : C::BM) || a.bmax < 1 || (ex.world_size > 1) != XCH || ex.world_size > kMaxRanks ||
+  if (a.bmax > (SMALLB ? 4 : C::BM) || a.bmax < 1 || (ex.world_size > 1) != XCH || ex.world_size > NP ||
       (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3)))) {
     if (t == 0) *a.status = kBadShape;
     return;
@@ -392,7 +395,8 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
       bool late = false;
       // every peer's lines in flight at once: ONE local round trip per poll whatever the world size
       // (polling in batches of 4 peers cost a second round trip per step at 5-8 ranks)
-      constexpr int PB = kMaxRanks;
+      constexpr int PB = NP;
+      static_assert(NP <= kMaxRanks, "at most kMaxRanks ranks per exchange");
       for (int p0 = 0; p0 < ex.world_size; p0 += PB) {
         unsigned long long v[PB][4 * C::NQ];
         bool ready;
@@ -598,12 +602,19 @@ hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stre
   if (!a.bc_ready)
     hipLaunchKernelGGL(adam_bias_table_kernel, dim3((a.n_steps + 255) / 256), dim3(256), 0, stream, a.bc, a.n_steps,
                        a.adam_step0, a.lr, a.beta1, a.beta2);
-#define DGT_TINY_LAUNCH(F_, H_, SB, XC)                                                          \
+#define DGT_TINY_LAUNCH_NP(F_, H_, SB, NP_)                                                      \
   do {                                                                                      \
     if (wd)                                                                                 \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, XC, true>), dim3(1), blk, 0, stream, a); \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, true>), dim3(1), blk, 0, stream, a); \
     else                                                                                    \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, XC, false>), dim3(1), blk, 0, stream, a); \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, false>), dim3(1), blk, 0, stream, a); \
+  } while (0)
+#define DGT_TINY_LAUNCH(F_, H_, SB, XC)                                                          \
+  do {                                                                                      \
+    if (!(XC)) DGT_TINY_LAUNCH_NP(F_, H_, SB, 1);                                           \
+    else if (a.ex.world_size <= 2) DGT_TINY_LAUNCH_NP(F_, H_, SB, 2);                       \
+    else if (a.ex.world_size <= 4) DGT_TINY_LAUNCH_NP(F_, H_, SB, 4);                       \
+    else DGT_TINY_LAUNCH_NP(F_, H_, SB, 8);                                                 \
   } while (0)
 #define X_(F_, H_)                                                                            \
   if (f == F_ && h == H_) {                                                                   \
@@ -618,6 +629,7 @@ hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stre
   DGT_TINY_SHAPES(X_)
 #undef X_
 #undef DGT_TINY_LAUNCH
+#undef DGT_TINY_LAUNCH_NP
   return hipErrorInvalidValue;
 }
 
