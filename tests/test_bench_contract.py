@@ -1,0 +1,53 @@
+"""bench.py's driver contract on the CPU (gloo): one JSON line from rank 0 with the required keys,
+exactly K timed steps after W warmup steps, whole-job aggregate value, the BASELINE metric."""
+import json
+import os
+import subprocess
+import sys
+
+from distributed_gpu_test_amd.launch import free_port
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+REQUIRED = {"metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+            "vs_baseline", "dtype", "data", "config"}
+
+
+def _json_lines(out):
+    return [json.loads(line) for line in out.splitlines() if line.startswith("{")]
+
+
+def _check(d, n, steps, warmup):
+    assert REQUIRED <= set(d), REQUIRED - set(d)
+    baseline = json.load(open(os.path.join(ROOT, "BASELINE.json")))
+    assert d["metric"] == baseline["metric"]
+    assert d["n_gpus"] == n and d["steps"] == steps and d["warmup"] == warmup
+    assert d["higher_is_better"] is True and d["scaling"] == "weak"
+    assert d["value"] > 0 and d["ms_per_step"] > 0
+    # whole-job aggregate: iterations summed over ranks
+    assert abs(d["value"] - n * 1e3 / d["ms_per_step"]) / d["value"] < 0.02
+    cfg = d["config"]
+    assert {"model", "global_batch", "seq_len", "parallelism"} <= set(cfg)
+    assert cfg["parallelism"] == f"dp{n}" and cfg["global_batch"] == 4 * n
+    assert d["params_consistent_across_ranks"] is True
+
+
+def test_bench_single_process_cpu():
+    env = dict(os.environ, DGT_QUIET="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "40", "--warmup", "5"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    _check(lines[0], 1, 40, 5)
+
+
+def test_bench_two_ranks_gloo_cpu():
+    env = dict(os.environ, DGT_QUIET="1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           f"--master-port={free_port()}", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "30",
+           "--warmup", "3"]
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout  # rank 0 only
+    _check(lines[0], 2, 30, 3)
