@@ -67,3 +67,17 @@ def test_ci_submit_timeout_cancels(tmp_path):
     r = subprocess.run(["bash", os.path.join(ROOT, "scripts", "slurm_submit_and_wait.sh"), str(tmp_path)],
                        cwd=tmp_path, env=env, capture_output=True, text=True, timeout=200)
     assert r.returncode == 124, r.stdout[-2000:]
+
+
+def test_ci_workflow_structure():
+    """The CI pipeline keeps the reference's shape (build -> SLURM acceptance test -> publish only on
+    success, .github/workflows/distributed-gpu-test-ci.yaml:18-231) plus a CPU unit-test gate."""
+    import yaml
+    wf = yaml.safe_load(open(os.path.join(ROOT, ".github", "workflows", "distributed-gpu-test-ci.yaml")))
+    jobs = wf["jobs"]
+    assert {"unit-tests", "build", "test-on-slurm", "publish"} <= set(jobs)
+    needs = lambda j: set([jobs[j]["needs"]] if isinstance(jobs[j].get("needs"), str) else jobs[j].get("needs", []))
+    assert "build" in needs("test-on-slurm")
+    assert {"build", "test-on-slurm"} <= needs("publish")
+    text = open(os.path.join(ROOT, ".github", "workflows", "distributed-gpu-test-ci.yaml")).read()
+    assert "rocm" in text.lower() and "nvidia" not in text.lower()
