@@ -1,0 +1,52 @@
+// Diagnostic harness (not part of the extension): times the 128x128 4-stage 8-wave GEMM on the
+// MLP's M = 1024 shapes with parts of its main loop removed, to see what bounds it.
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -Icsrc [-DDGT_GEMM_ABLATE=1|2] csrc/diag/gemm_ablate.hip -o build/bin/gemm_ablate_N
+//   DGT_GEMM_ABLATE unset: the shipped loop; 1: no staging inside the loop (operands of the first
+//   S-1 tiles reused); 2: LDS fragment reads without MFMAs.
+#include "../gemm.hip"
+
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+#define CK(x)                                                                        \
+  do {                                                                               \
+    hipError_t e_ = (x);                                                             \
+    if (e_ != hipSuccess) {                                                          \
+      fprintf(stderr, "%s failed: %s\n", #x, hipGetErrorString(e_));                 \
+      exit(1);                                                                       \
+    }                                                                                \
+  } while (0)
+
+int main() {
+  const int M = 1024, N = 4096, K = 4096;
+  std::vector<unsigned short> h((size_t)N * K);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = (unsigned short)(0x3c00 + (i * 2654435761u >> 20) % 512);
+  void *A, *B, *C;
+  CK(hipMalloc(&A, (size_t)M * K * 2));
+  CK(hipMalloc(&B, (size_t)N * K * 2));
+  CK(hipMalloc(&C, (size_t)M * N * 2));
+  CK(hipMemcpy(A, h.data(), (size_t)M * K * 2, hipMemcpyHostToDevice));
+  CK(hipMemcpy(B, h.data(), (size_t)N * K * 2, hipMemcpyHostToDevice));
+  dgt::GemmArgs g{};
+  g.A = A; g.B = B; g.C = C; g.M = M; g.N = N; g.K = K; g.lda = K; g.ldb = K; g.ldc = N; g.alpha = 1.f;
+  hipEvent_t e0, e1;
+  CK(hipEventCreate(&e0));
+  CK(hipEventCreate(&e1));
+  for (int w = 0; w < 5; ++w) CK(dgt::gemm_nt(g, 0, 0, 4));
+  CK(hipDeviceSynchronize());
+  const int iters = 50;
+  CK(hipEventRecord(e0, 0));
+  for (int i = 0; i < iters; ++i) CK(dgt::gemm_nt(g, 0, 0, 4));
+  CK(hipEventRecord(e1, 0));
+  CK(hipEventSynchronize(e1));
+  float ms = 0.f;
+  CK(hipEventElapsedTime(&ms, e0, e1));
+#ifdef DGT_GEMM_ABLATE
+  const int ab = DGT_GEMM_ABLATE;
+#else
+  const int ab = 0;
+#endif
+  printf("ablate=%d  %.1f us/gemm (hot)  %.0f TF\n", ab, ms * 1e3 / iters, 2.0 * M * N * K / (ms * 1e-3 / iters) / 1e12);
+  return 0;
+}

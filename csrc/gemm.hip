@@ -283,11 +283,18 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 #pragma unroll
         for (int j = 0; j < NJ; ++j) bfr[j] = read_frag(Bs, wc * WN + j * 16 + (l & 15), chunk);
       }
+#if defined(DGT_GEMM_ABLATE) && DGT_GEMM_ABLATE == 2  // diag: 2 = LDS reads, no MFMA
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) acc[i][j][0] += (float)af[i][0] + (float)bfr[j][0];
+#else
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+#endif
     }
   };
   if constexpr (S == 2) {
@@ -324,11 +331,13 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();  // tile kt visible to all waves; buffer of kt-1 free for reuse
       __builtin_amdgcn_sched_barrier(0);
+#if !(defined(DGT_GEMM_ABLATE) && DGT_GEMM_ABLATE == 1)  // diag: 1 = no staging inside the loop
       if (kt + S - 1 < nk) {
         const int nb = (buf + S - 1) % S;
         stage_tile<NW>(A, g.lda, m0, (kt + S - 1) * GBK, lds[nb][0], w, l);
         stage_b<KN, NW>(B, g.ldb, n0, (kt + S - 1) * GBK, lds[nb][1], w, l);
       }
+#endif
       compute(buf);
       buf = (buf + 1 == S) ? 0 : buf + 1;
     }
