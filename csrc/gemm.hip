@@ -85,6 +85,44 @@ DGT_DEVICE void stage_b(const u16* __restrict__ src, int ld, int n0, int k0, u16
   else stage_tile<NWAVE>(src, ld, n0, k0, lds, w, l);
 }
 
+// Per-thread staging state of one operand of the 128x128 kernel: the global source of each of the
+// thread's LDS-DMA pieces is computed ONCE and advanced by one K-tile per issue (K-tiles are staged
+// strictly in order), instead of recomputing 64-bit row addresses and swizzles for every piece of
+// every K-tile inside the main loop.
+template <int NWAVE, bool KN>
+struct Stager {
+  static constexpr int PER_WAVE = 16 / NWAVE;
+  const u16* p[PER_WAVE];
+  int lds_off[PER_WAVE];  // element offset of the piece in the LDS operand tile (wave-uniform)
+  long long step;         // elements per K-tile
+  // NT operand [rows, K]: rc0 = first row of the block; KN operand [K, N]: rc0 = first column
+  DGT_DEVICE Stager(const u16* __restrict__ src, int ld, int rc0, int w, int l) {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      if constexpr (KN) {
+        const int rblk = (w * PER_WAVE + i) * 4, row = rblk + (l >> 4);
+        const int c = (l & 15) ^ kn_swz(row);
+        p[i] = src + (long long)row * ld + rc0 + c * 8;
+        lds_off[i] = rblk * GBN;
+      } else {
+        const int rblk = (w * PER_WAVE + i) * 8, row = rblk + (l >> 3);
+        const int c = (l & 7) ^ (row & 7);
+        p[i] = src + (long long)(rc0 + row) * ld + c * 8;
+        lds_off[i] = rblk * GBK;
+      }
+    }
+    step = KN ? (long long)GBK * ld : GBK;
+  }
+  DGT_DEVICE void issue(u16* lds) {
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(p[i]), reinterpret_cast<int*>(lds + lds_off[i]),
+                                       16, 0, 0);
+      p[i] += step;
+    }
+  }
+};
+
 typedef short i16x4 __attribute__((ext_vector_type(4)));
 typedef short i16x8 __attribute__((ext_vector_type(8)));
 
@@ -314,11 +352,13 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
     }
   } else {
     constexpr int PER_TILE = 2 * (16 / NW);  // glds per thread per K-tile (A and B)
+    Stager<NW, false> sa(A, g.lda, m0, w, l);
+    Stager<NW, KN> sb(B, g.ldb, n0, w, l);
 #pragma unroll
     for (int p = 0; p < S - 1; ++p) {
       if (p < nk) {
-        stage_tile<NW>(A, g.lda, m0, p * GBK, lds[p][0], w, l);
-        stage_b<KN, NW>(B, g.ldb, n0, p * GBK, lds[p][1], w, l);
+        sa.issue(lds[p][0]);
+        sb.issue(lds[p][1]);
       }
     }
     int buf = 0;
@@ -334,8 +374,8 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 #if !(defined(DGT_GEMM_ABLATE) && DGT_GEMM_ABLATE == 1)  // diag: 1 = no staging inside the loop
       if (kt + S - 1 < nk) {
         const int nb = (buf + S - 1) % S;
-        stage_tile<NW>(A, g.lda, m0, (kt + S - 1) * GBK, lds[nb][0], w, l);
-        stage_b<KN, NW>(B, g.ldb, n0, (kt + S - 1) * GBK, lds[nb][1], w, l);
+        sa.issue(lds[nb][0]);
+        sb.issue(lds[nb][1]);
       }
 #endif
       compute(buf);
