@@ -432,7 +432,8 @@ class DgtEngineBench(EngineBench):
         self.B = B
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
         self.engine, _, _, _ = initialize(model=model, optimizer=opt, model_parameters=model.parameters(), config=cfg)
-        crit = torch.nn.BCEWithLogitsLoss()
+        from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+        crit = BCEWithLogitsLoss()  # fused HIP loss + gradient kernel
         if self.engine.config.amd.hip_graph:
             self.step = self.engine.graph_step(lambda bx, by: crit(self.engine(bx).float(), by))
         else:

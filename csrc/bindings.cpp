@@ -158,6 +158,20 @@ void tiny_mlp_bias_table(const at::Tensor& workspace, int64_t n_steps, int64_t s
                                          stream_of(workspace)));
 }
 
+// ------------------------------------------------------------------------------ fused BCE loss
+void bce_logits(const at::Tensor& z, const at::Tensor& y, const at::Tensor& loss, const at::Tensor& dz) {
+  TORCH_CHECK(z.is_cuda() && z.is_contiguous() && (z.scalar_type() == at::kFloat || z.scalar_type() == at::kBFloat16),
+              "dgt: bce_logits needs contiguous fp32 / bf16 GPU logits");
+  check_gpu(y, "y", at::kFloat);
+  check_gpu(loss, "loss", at::kFloat);
+  check_gpu(dz, "dz", at::kFloat);
+  TORCH_CHECK(y.numel() == z.numel() && dz.numel() == z.numel() && loss.numel() == 1 && z.numel() > 0,
+              "dgt: bce_logits size mismatch");
+  c10::DeviceGuard guard(z.device());
+  DGT_CHECK_HIP(dgt::bce_logits(z.data_ptr(), dtype_code(z.scalar_type()), y.data_ptr<float>(), z.numel(),
+                                loss.data_ptr<float>(), dz.data_ptr<float>(), stream_of(z)));
+}
+
 void tiny_mlp_grad(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& plan, const at::Tensor& counts,
                    int64_t step, const at::Tensor& params, const at::Tensor& grad, const at::Tensor& loss_acc,
                    int64_t n_features, int64_t hidden) {
@@ -493,6 +507,7 @@ TORCH_LIBRARY(dgt, m) {
       "bool adamw, int step, float grad_scale, Tensor? grad_scale_dev, Tensor? step_dev=None) -> ()",
       &adam_matrix_t);
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
+  m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz) -> ()", &bce_logits);
   m.def(
       "oneshot_allreduce(Tensor inp, Tensor(a!) out, float scale, int[] data_ptrs, int rank, "
       "int world_size, int stride, int seq, int timeout_ticks, Tensor(b!) status, int reps=1) -> ()",

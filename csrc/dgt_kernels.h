@@ -88,6 +88,11 @@ hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream);
 // writes the bf16 copy a.param_lp [rows, cols] and its transpose lpT [cols, rows] in the same pass.
 hipError_t adam_matrix_t(const AdamFlatArgs& a, void* lpT, int rows, int cols, hipStream_t stream);
 
+// ---------------------------------------------------------------- fused BCE-with-logits (loss.hip)
+// loss[0] = mean BCE-with-logits of z[n] (fp32 or bf16) against y[n]; dz[n] = (sigmoid(z) - y) / n.
+hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz,
+                      hipStream_t stream);
+
 // ---------------------------------------------------------------- IPC one-shot all-reduce
 // in[n] (fp32) from every rank -> out[n] = scale * sum over ranks (rank order, identical bits on
 // every rank).  Uses the Exchange mailboxes; n <= ex.stride.

@@ -4,4 +4,6 @@ from .reference import adam_flat_reference_, tiny_mlp_forward_loss, tiny_mlp_ste
 from .adam import adam_flat_
 
 __all__ = ["LIB_PATH", "available", "gpu_available", "load", "require", "adam_flat_",
-           "adam_flat_reference_", "tiny_mlp_forward_loss", "tiny_mlp_step_reference"]
+           "adam_flat_reference_", "tiny_mlp_forward_loss", "tiny_mlp_step_reference", "BCEWithLogitsLoss",
+           "bce_with_logits"]
+from .loss import BCEWithLogitsLoss, bce_with_logits  # noqa: F401

@@ -1,0 +1,49 @@
+"""Fused BCE-with-logits loss (``csrc/loss.hip``) for the engine path.
+
+Reference: ``nn.BCEWithLogitsLoss()`` created at ``train.py:96`` and applied at ``train.py:112``.
+
+One HIP kernel computes the mean loss AND d loss / d logits (saved for backward); backward is one
+multiply by the incoming gradient.  torch's loss runs ~11 small kernels per step, and inside a
+HIP-graph-replayed step every node costs a few microseconds whatever it computes.  On CPU tensors
+(or without the extension) it is ``F.binary_cross_entropy_with_logits`` itself.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn.functional as F
+
+from . import _ext
+
+
+class _FusedBCEWithLogits(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        zc = z.contiguous().reshape(-1)
+        yc = y.reshape(-1).to(torch.float32).contiguous()
+        loss = torch.empty(1, dtype=torch.float32, device=z.device)
+        dz = torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
+        _ext.require().bce_logits(zc, yc, loss, dz)
+        ctx.save_for_backward(dz)
+        ctx.shape, ctx.dtype = z.shape, z.dtype
+        return loss.view(())
+
+    @staticmethod
+    def backward(ctx, g: torch.Tensor):
+        (dz,) = ctx.saved_tensors
+        gz = (dz * g).view(ctx.shape)
+        return (gz if ctx.dtype == torch.float32 else gz.to(ctx.dtype)), None
+
+
+def bce_with_logits(z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """Mean BCE-with-logits; the fused HIP kernel on GPU fp32 / bf16 logits."""
+    if (z.is_cuda and z.dtype in (torch.float32, torch.bfloat16) and z.numel() == y.numel() and z.numel() > 0
+            and _ext.available()):
+        return _FusedBCEWithLogits.apply(z, y)
+    return F.binary_cross_entropy_with_logits(z, y.to(z.dtype))
+
+
+class BCEWithLogitsLoss(torch.nn.Module):
+    """Drop-in for ``nn.BCEWithLogitsLoss()`` (mean reduction, no weights)."""
+
+    def forward(self, z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        return bce_with_logits(z, y)

@@ -187,3 +187,16 @@ def test_hip_graph_config_falls_back_to_eager_on_cpu():
         loss = float(step(x, y))
     assert loss < l0 and engine.global_steps == 21
     engine.close()
+
+
+def test_fused_bce_falls_back_to_torch_on_cpu():
+    import torch
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    z = torch.randn(8, 1, requires_grad=True)
+    y = (torch.rand(8, 1) > 0.5).float()
+    ref_z = z.detach().clone().requires_grad_(True)
+    loss = BCEWithLogitsLoss()(z, y)
+    ref = torch.nn.BCEWithLogitsLoss()(ref_z, y)
+    loss.backward()
+    ref.backward()
+    assert torch.equal(loss, ref) and torch.equal(z.grad, ref_z.grad)

@@ -94,3 +94,21 @@ def test_engine_hip_graph_matches_eager(extra):
     torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
     e1.close()
     e2.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,dtype", [(4, torch.float32), (1000, torch.float32), (5000, torch.bfloat16)])
+def test_fused_bce_matches_torch(n, dtype):
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    g = torch.Generator().manual_seed(n)
+    z0 = (torch.randn(n, 1, generator=g) * 4).to(dtype)
+    y = (torch.rand(n, 1, generator=g) > 0.5).float()
+    z = z0.cuda().requires_grad_(True)
+    loss = BCEWithLogitsLoss()(z, y.cuda())
+    loss.backward()
+    zr = z0.float().requires_grad_(True)
+    ref = torch.nn.BCEWithLogitsLoss()(zr, y)
+    ref.backward()
+    torch.testing.assert_close(loss.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(z.grad.float().cpu(), zr.grad, rtol=1e-2 if dtype == torch.bfloat16 else 1e-5,
+                               atol=1e-7)

@@ -35,6 +35,7 @@ import distributed_gpu_test_amd as dgt  # noqa: E402
 from distributed_gpu_test_amd.config import REFERENCE_DS_CONFIG, parse_config  # noqa: E402
 from distributed_gpu_test_amd.data import SyntheticDataset, make_synthetic_data  # noqa: E402
 from distributed_gpu_test_amd.models import SimpleNet  # noqa: E402
+from distributed_gpu_test_amd.ops import BCEWithLogitsLoss  # noqa: E402
 from distributed_gpu_test_amd.parallel import comm  # noqa: E402
 from distributed_gpu_test_amd.utils.fault import FaultInjector  # noqa: E402
 
@@ -133,7 +134,8 @@ def main(argv=None) -> int:
                   f"oneshot={'yes' if engine.oneshot is not None else 'no'} backend={comm.backend_name()} "
                   f"world_size={world}", file=sys.stderr, flush=True)
         data = SyntheticDataset(x, y, MICRO_BATCH, world, comm.get_rank()).to(device)
-        criterion = torch.nn.BCEWithLogitsLoss()
+        # fused HIP loss + gradient kernel on GPU (torch's own loss on CPU)
+        criterion = BCEWithLogitsLoss()
         if args.resume:
             found = newest_checkpoint(args.save_dir)
             if found:
