@@ -57,7 +57,7 @@ def _run(cmd, verbose):
 
 # the fused tiny kernel reads every MFMA result straight back into VALU math: accumulators in
 # VGPRs save the v_accvgpr_read round trips (the GEMMs keep the compiler's AGPR choice)
-PER_FILE_FLAGS = {"tiny_mlp.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
+PER_FILE_FLAGS = {"tiny_mlp.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
 
 
 def build(verbose: bool = False, force: bool = False, jobs: int = 8) -> str:
