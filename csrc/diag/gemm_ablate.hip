@@ -33,20 +33,28 @@ int main() {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  for (int w = 0; w < 5; ++w) CK(dgt::gemm_nt(g, 0, 0, 4));
-  CK(hipDeviceSynchronize());
-  const int iters = 50;
-  CK(hipEventRecord(e0, 0));
-  for (int i = 0; i < iters; ++i) CK(dgt::gemm_nt(g, 0, 0, 4));
-  CK(hipEventRecord(e1, 0));
-  CK(hipEventSynchronize(e1));
-  float ms = 0.f;
-  CK(hipEventElapsedTime(&ms, e0, e1));
 #ifdef DGT_GEMM_ABLATE
   const int ab = DGT_GEMM_ABLATE;
 #else
   const int ab = 0;
 #endif
-  printf("ablate=%d  %.1f us/gemm (hot)  %.0f TF\n", ab, ms * 1e3 / iters, 2.0 * M * N * K / (ms * 1e-3 / iters) / 1e12);
+  // epi 0: B is [N, K] (forward form); kEpiBKN: B is [K, N] (dgrad straight from W)
+  for (int epi : {0, (int)dgt::kEpiBKN}) {
+    for (int w = 0; w < 5; ++w) CK(dgt::gemm_nt(g, epi, 0, 4));
+    CK(hipDeviceSynchronize());
+    const int iters = 50;
+    CK(hipEventRecord(e0, 0));
+    for (int i = 0; i < iters; ++i) CK(dgt::gemm_nt(g, epi, 0, 4));
+    CK(hipEventRecord(e1, 0));
+    CK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    std::vector<unsigned short> c((size_t)M * N);
+    CK(hipMemcpy(c.data(), C, c.size() * 2, hipMemcpyDeviceToHost));
+    unsigned long long sum = 0;
+    for (size_t i = 0; i < c.size(); ++i) sum = sum * 1000003ull + c[i];
+    printf("ablate=%d B=%s  %.1f us/gemm (hot)  %.0f TF  C hash %016llx\n", ab, epi ? "[K,N]" : "[N,K]",
+           ms * 1e3 / iters, 2.0 * M * N * K / (ms * 1e-3 / iters) / 1e12, sum);
+  }
   return 0;
 }
