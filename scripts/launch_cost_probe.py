@@ -1,0 +1,53 @@
+import time, sys, os
+sys.path.insert(0, "/root/repo")
+os.chdir(os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
+import torch, ctypes
+import bench
+from distributed_gpu_test_amd.data import make_synthetic_data
+from distributed_gpu_test_amd.models import SimpleNet
+from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
+from distributed_gpu_test_amd.ops import _ext
+dev = torch.device("cuda", 0)
+torch.manual_seed(42)
+x, y = make_synthetic_data(2000, 20, 42)
+tr = TinyMLPTrainer(SimpleNet(20, 64), x, y, 4, impl="fused", device=dev)
+plan, counts = bench.build_plan(tr, 100000)
+tr.reserve(1000)
+def t(label, f, n=2000):
+    for _ in range(50): f()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(n): f()
+    dt = (time.perf_counter() - t0) / n * 1e6
+    torch.cuda.synchronize()
+    print(f"{label:40s} {dt:7.2f} us", flush=True)
+p1, c1 = plan[:1].contiguous(), counts[:1].contiguous()
+t("current_stream().cuda_stream", lambda: torch.cuda.current_stream(dev).cuda_stream)
+t("slice plan[1:]", lambda: plan[1:])
+t("_bind()", lambda: tr._bind())
+lib = _ext.fast_lib()
+h = tr._bind()
+s = torch.cuda.current_stream(dev).cuda_stream
+t("dgt_tiny_run raw (K=1)", lambda: lib.dgt_tiny_run(h, p1.data_ptr(), c1.data_ptr(), 1, 4, 0, 0, 0, s), 500)
+t("run_plan K=1", lambda: tr.run_plan(p1, c1), 500)
+ops = _ext.require()
+def old():
+    ops.tiny_mlp_train(tr.x, tr.y, p1, c1, tr.params, tr.exp_avg, tr.exp_avg_sq, tr.loss_acc, tr.status, 20, 64,
+                       1e-3, 0.9, 0.999, 1e-8, 0.0, False, 0, [], 0, 1, 0, 0, 0, tr._ws, False)
+t("torch op tiny_mlp_train K=1", old, 500)
+t("synchronize (idle)", lambda: torch.cuda.synchronize())
+e = torch.cuda.Event(enable_timing=True)
+t("event.record", lambda: e.record())
+def launch_sync():
+    lib.dgt_tiny_run(h, p1.data_ptr(), c1.data_ptr(), 1, 4, 0, 0, 0, s)
+    torch.cuda.synchronize()
+t("raw launch + synchronize K=1", launch_sync, 500)
+def empty_sync():
+    torch.empty(0, device=dev).zero_() if False else None
+    torch.cuda.synchronize()
+t("sync only", empty_sync, 500)
+z = torch.zeros(1, device=dev)
+def tiny_kernel_sync():
+    z.add_(1)
+    torch.cuda.synchronize()
+t("torch add_ + synchronize", tiny_kernel_sync, 500)
