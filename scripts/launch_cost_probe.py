@@ -1,7 +1,10 @@
-import time, sys, os
-sys.path.insert(0, "/root/repo")
-os.chdir(os.environ.get("GRAFT_REPO_ROOT", "/root/repo"))
-import torch, ctypes
+"""Host-side costs of one timed run of the fused kernel (torch op dispatch, stream lookup, synchronize)."""
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch
 import bench
 from distributed_gpu_test_amd.data import make_synthetic_data
 from distributed_gpu_test_amd.models import SimpleNet
@@ -24,11 +27,7 @@ def t(label, f, n=2000):
 p1, c1 = plan[:1].contiguous(), counts[:1].contiguous()
 t("current_stream().cuda_stream", lambda: torch.cuda.current_stream(dev).cuda_stream)
 t("slice plan[1:]", lambda: plan[1:])
-t("_bind()", lambda: tr._bind())
-lib = _ext.fast_lib()
-h = tr._bind()
 s = torch.cuda.current_stream(dev).cuda_stream
-t("dgt_tiny_run raw (K=1)", lambda: lib.dgt_tiny_run(h, p1.data_ptr(), c1.data_ptr(), 1, 4, 0, 0, 0, s), 500)
 t("run_plan K=1", lambda: tr.run_plan(p1, c1), 500)
 ops = _ext.require()
 def old():
@@ -39,13 +38,9 @@ t("synchronize (idle)", lambda: torch.cuda.synchronize())
 e = torch.cuda.Event(enable_timing=True)
 t("event.record", lambda: e.record())
 def launch_sync():
-    lib.dgt_tiny_run(h, p1.data_ptr(), c1.data_ptr(), 1, 4, 0, 0, 0, s)
+    old()
     torch.cuda.synchronize()
-t("raw launch + synchronize K=1", launch_sync, 500)
-def empty_sync():
-    torch.empty(0, device=dev).zero_() if False else None
-    torch.cuda.synchronize()
-t("sync only", empty_sync, 500)
+t("fused launch + synchronize K=1", launch_sync, 500)
 z = torch.zeros(1, device=dev)
 def tiny_kernel_sync():
     z.add_(1)
