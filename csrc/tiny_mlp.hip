@@ -164,14 +164,16 @@ template <int F, int H>
 DGT_DEVICE void wave_forward(const LaneState<F, H>& st, WaveSmem<F, H>& ws, float* Zbuf, int w, int lr, int lq,
                              const float (&x)[TinyCfg<F, H>::NSP], float (&h)[4], float (&w2v)[4]) {
   using C = TinyCfg<F, H>;
-  // two independent accumulation chains halve the dependent-MFMA latency
-  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
+  // three independent accumulation chains: a dependent 16x16x4 f32 MFMA waits ~40 cycles for its
+  // predecessor, so NSL = 6 slots run as 3 chains of 2 instead of 2 chains of 3
+  f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f}, acc2 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-  for (int i = 0; i < C::NSL; i += 2) {
+  for (int i = 0; i < C::NSL; i += 3) {
     acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(st.w1[i], x[i], acc0, 0, 0, 0);
     if (i + 1 < C::NSL) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(st.w1[i + 1], x[i + 1], acc1, 0, 0, 0);
+    if (i + 2 < C::NSL) acc2 = __builtin_amdgcn_mfma_f32_16x16x4f32(st.w1[i + 2], x[i + 2], acc2, 0, 0, 0);
   }
-  const f32x4 acc = acc0 + acc1;
+  const f32x4 acc = (acc0 + acc1) + acc2;
   // stage this step's rows for the weight-gradient MFMA (row-major, conflict-free stride)
 #pragma unroll
   for (int i = 0; i < C::NSL; ++i) ws.X[lr * C::SX + C::slot_k(i, lq)] = x[i];
