@@ -136,7 +136,10 @@ DGT_DEVICE void load_state(LaneState<F, H>& st, const float* __restrict__ p, con
   st.vb2 = v ? v[C::G_B2] : 0.f;
 }
 
-// Minibatch values for the lane's row b = l&15: x[b][slot_k(i, l>>4)] and y[b] (0 when padding).
+// Minibatch values for the lane's row b = l&15: x[b][slot_k(i, l>>4)] and y[b].  A padding row
+// (id < 0) loads row 0 instead of zeros: its dz is masked to 0 (valid = b < Bt), so its dh and
+// its weight-gradient terms are exact zeros for any finite x, and its loss term is weighted 0 —
+// no per-value selects in the step.
 // Slot k's are stride-4 (k = 16ct + lq + 4r): scalar loads, issued a step ahead of their use.
 template <int F, int H>
 DGT_DEVICE void load_rows(const float* __restrict__ X, const float* __restrict__ Y, int id, int lq,
@@ -151,9 +154,9 @@ DGT_DEVICE void load_rows(const float* __restrict__ X, const float* __restrict__
       if (16 * (i >> 2) + 15 < F) v = row[k];  // full tile: every k is a feature
       else v = k < F ? row[k] : (k == F ? 1.f : 0.f);
     }
-    x[i] = id >= 0 ? v : 0.f;
+    x[i] = v;
   }
-  y = id >= 0 ? Y[id] : 0.f;
+  y = Y[id >= 0 ? id : 0];
 }
 
 // Forward (MFMA) + bias + ReLU; publishes the wave's partial logits; stages x for the wgrad.
