@@ -447,7 +447,8 @@ class DgtEngineBench(EngineBench):
         graphed = self.engine.graphed is not None
         self.exchange = ("none" if self.world == 1 else
                          ("rccl-native-in-hipgraph" if graphed else f"{comm.backend_name()}-bucketed"))
-        self.impl = "dgt-engine" + ("+hipgraph" if graphed else "") + f"+zero{self.engine.stage}"
+        self.impl = ("dgt-engine" + ("+hipgraph" if graphed else "") + ("+fusedlinear" if self.engine.fused_linear_layers else "")
+                     + f"+zero{self.engine.stage}")
 
     def run_plan(self, plan, counts):
         plan_d = plan.to(self.device).long()

@@ -159,6 +159,50 @@ void tiny_mlp_bias_table(const at::Tensor& workspace, int64_t n_steps, int64_t s
 }
 
 // ------------------------------------------------------------------------------ fused BCE loss
+void linear_fwd(const at::Tensor& x, const at::Tensor& W, const std::optional<at::Tensor>& b, const at::Tensor& y,
+                bool relu) {
+  check_gpu(x, "x", at::kFloat);
+  check_gpu(W, "W", at::kFloat);
+  check_gpu(y, "y", at::kFloat);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && W.size(1) == x.size(1) && y.dim() == 2 && y.size(0) == x.size(0) &&
+                  y.size(1) == W.size(0),
+              "dgt: linear_fwd shapes: x [M, K], W [N, K], y [M, N]");
+  const float* bp = nullptr;
+  if (b.has_value() && b->defined()) {
+    check_gpu(*b, "b", at::kFloat);
+    TORCH_CHECK(b->numel() == W.size(0), "dgt: linear_fwd bias must have N elements");
+    bp = b->data_ptr<float>();
+  }
+  if (x.size(0) == 0) return;
+  c10::DeviceGuard guard(x.device());
+  DGT_CHECK_HIP(dgt::linear_fwd(x.data_ptr<float>(), W.data_ptr<float>(), bp, y.data_ptr<float>(), (int)x.size(0),
+                                (int)W.size(0), (int)W.size(1), relu, stream_of(x)));
+}
+
+void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, const std::optional<at::Tensor>& y,
+                const std::optional<at::Tensor>& dx, const at::Tensor& dW, const std::optional<at::Tensor>& db) {
+  check_gpu(dy, "dy", at::kFloat);
+  check_gpu(x, "x", at::kFloat);
+  check_gpu(W, "W", at::kFloat);
+  check_gpu(dW, "dW", at::kFloat);
+  const int64_t M = x.size(0), K = x.size(1), N = W.size(0);
+  TORCH_CHECK(x.dim() == 2 && W.dim() == 2 && W.size(1) == K && dy.dim() == 2 && dy.size(0) == M && dy.size(1) == N &&
+                  dW.sizes() == W.sizes(),
+              "dgt: linear_bwd shapes: dy [M, N], x [M, K], W / dW [N, K]");
+  auto opt = [&](const std::optional<at::Tensor>& t, const char* name, int64_t numel) -> float* {
+    if (!t.has_value() || !t->defined()) return nullptr;
+    check_gpu(*t, name, at::kFloat);
+    TORCH_CHECK(t->numel() == numel, "dgt: linear_bwd ", name, " has ", t->numel(), " elements, expected ", numel);
+    return t->data_ptr<float>();
+  };
+  const float* yp = opt(y, "y", M * N);
+  float* dxp = opt(dx, "dx", M * K);
+  float* dbp = opt(db, "db", N);
+  c10::DeviceGuard guard(x.device());
+  DGT_CHECK_HIP(dgt::linear_bwd(dy.data_ptr<float>(), x.data_ptr<float>(), W.data_ptr<float>(), yp, dxp,
+                                dW.data_ptr<float>(), dbp, (int)M, (int)N, (int)K, stream_of(x)));
+}
+
 void bce_logits(const at::Tensor& z, const at::Tensor& y, const at::Tensor& loss, const at::Tensor& dz) {
   TORCH_CHECK(z.is_cuda() && z.is_contiguous() && (z.scalar_type() == at::kFloat || z.scalar_type() == at::kBFloat16),
               "dgt: bce_logits needs contiguous fp32 / bf16 GPU logits");
@@ -508,6 +552,9 @@ TORCH_LIBRARY(dgt, m) {
       &adam_matrix_t);
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz) -> ()", &bce_logits);
+  m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
+  m.def("linear_bwd(Tensor dy, Tensor x, Tensor W, Tensor? y, Tensor(a!)? dx, Tensor(b!) dW, Tensor(c!)? db) -> ()",
+        &linear_bwd);
   m.def(
       "oneshot_allreduce(Tensor inp, Tensor(a!) out, float scale, int[] data_ptrs, int rank, "
       "int world_size, int stride, int seq, int timeout_ticks, Tensor(b!) status, int reps=1) -> ()",

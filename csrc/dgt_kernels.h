@@ -90,6 +90,11 @@ hipError_t adam_matrix_t(const AdamFlatArgs& a, void* lpT, int rows, int cols, h
 
 // ---------------------------------------------------------------- fused BCE-with-logits (loss.hip)
 // loss[0] = mean BCE-with-logits of z[n] (fp32 or bf16) against y[n]; dz[n] = (sigmoid(z) - y) / n.
+// fused small-batch Linear (+ReLU) forward / backward for the engine's kernel injection (fp32)
+hipError_t linear_fwd(const float* x, const float* W, const float* b, float* y, int M, int N, int K, bool relu,
+                      hipStream_t stream);
+hipError_t linear_bwd(const float* dy, const float* x, const float* W, const float* y, float* dx, float* dW,
+                      float* db, int M, int N, int K, hipStream_t stream);
 hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz,
                       hipStream_t stream);
 

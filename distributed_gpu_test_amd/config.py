@@ -82,6 +82,9 @@ class AMDConfig:
     hip_graph: bool = False
     # extra sync between comm and compute streams: validates overlap logic
     debug_sync_streams: bool = False
+    # kernel injection: nn.Linear (+ following nn.ReLU) -> one fused HIP launch forward and one
+    # backward for small fp32 batches (ops/linear.py)
+    fused_linear: bool = False
 
 
 @dataclass
@@ -208,7 +211,8 @@ def parse_config(config: Union[str, os.PathLike, Dict[str, Any], None], world_si
     amd = AMDConfig(allreduce=str(a.get("allreduce", "auto")),
                     oneshot_max_bytes=int(a.get("oneshot_max_bytes", 256 * 1024)),
                     hip_graph=bool(a.get("hip_graph", False)),
-                    debug_sync_streams=bool(a.get("debug_sync_streams", False)))
+                    debug_sync_streams=bool(a.get("debug_sync_streams", False)),
+                    fused_linear=bool(a.get("fused_linear", False)))
     if amd.allreduce not in ("auto", "rccl", "oneshot"):
         raise ConfigError(f"amd.allreduce={amd.allreduce!r}: expected auto|rccl|oneshot")
 

@@ -81,6 +81,10 @@ class Engine:
         self.device = device
         self.dtype = _DTYPES[config.compute_dtype]
         self.module = model.to(device=device, dtype=self.dtype)
+        self.fused_linear_layers = 0
+        if config.amd.fused_linear and device.type == "cuda" and self.dtype == torch.float32:
+            from .ops.linear import inject_fused_linear
+            self.fused_linear_layers = inject_fused_linear(self.module)
         self.stage = config.zero_stage
         self.gas = config.gradient_accumulation_steps
         self.micro_batch = config.train_micro_batch_size_per_gpu

@@ -1,0 +1,112 @@
+"""Fused small-batch Linear (+ReLU) for the engine path (``csrc/linear.hip``): kernel injection.
+
+Reference: the model's ``Linear(20,64) -> ReLU -> Linear(64,1)`` (``train.py:29-33``), forward at
+``train.py:107``, backward at ``train.py:113``.
+
+Autograd runs a Linear + ReLU as addmm + relu forward and mm + mm + sum + threshold_backward
+backward; at the reference's batch of 4 each is a sub-microsecond kernel, and inside a
+HIP-graph-replayed step each costs a graph node of a few microseconds.  ``FusedLinear`` does one
+launch forward (bias and ReLU folded in) and one launch backward (ReLU mask, dx, dW, db).
+``inject_fused_linear(module)`` swaps every ``nn.Linear`` of a module in place — folding an
+``nn.ReLU`` that directly follows it in an ``nn.Sequential`` — keeping the same Parameter objects
+and state_dict keys, so checkpoints, the engine's flat buffers and optimizers are unaffected.
+
+Taken only for fp32 GPU tensors of small shapes (``SMALL``); anything else runs ``F.linear``.
+"""
+from __future__ import annotations
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from . import _ext
+
+SMALL_M = 256            # rows per call (batch)
+SMALL_WORK = 1 << 22     # M * N * K: beyond this a tiled GEMM (hipBLASLt / csrc/gemm.hip) wins
+
+
+class _FusedLinearFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, weight, bias, relu: bool):
+        y = torch.empty(x.shape[0], weight.shape[0], dtype=torch.float32, device=x.device)
+        _ext.require().linear_fwd(x, weight, bias, y, relu)
+        ctx.relu = relu
+        ctx.has_bias = bias is not None
+        ctx.save_for_backward(x, weight, y if relu else None)
+        return y
+
+    @staticmethod
+    def backward(ctx, dy):
+        x, weight, y = ctx.saved_tensors
+        dy = dy.contiguous()
+        dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        dw = torch.empty_like(weight)
+        db = torch.empty(weight.shape[0], dtype=torch.float32, device=x.device) if ctx.has_bias else None
+        _ext.require().linear_bwd(dy, x, weight, y, dx, dw, db)
+        return dx, dw, db, None
+
+
+def _fusable(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    return (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and weight.dtype == torch.float32
+            and x.shape[0] <= SMALL_M and x.shape[0] * weight.shape[0] * weight.shape[1] <= SMALL_WORK
+            and _ext.available())
+
+
+def fused_linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = False) -> torch.Tensor:
+    if _fusable(x, weight):
+        return _FusedLinearFn.apply(x.contiguous(), weight, bias, relu)
+    y = F.linear(x, weight, bias)
+    return F.relu(y) if relu else y
+
+
+class FusedLinear(nn.Linear):
+    """``nn.Linear`` (optionally followed by ReLU) on the fused kernels; same parameters and keys."""
+
+    def __init__(self, in_features: int, out_features: int, bias: bool = True, relu: bool = False,
+                 device=None, dtype=None):
+        super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
+        self.relu = relu
+
+    @classmethod
+    def from_linear(cls, lin: nn.Linear, relu: bool = False) -> "FusedLinear":
+        m = cls.__new__(cls)
+        nn.Module.__init__(m)
+        m.in_features, m.out_features = lin.in_features, lin.out_features
+        m.weight = lin.weight          # the same Parameter objects
+        m.bias = lin.bias
+        m.relu = relu
+        return m
+
+    def forward(self, x: torch.Tensor) -> torch.Tensor:
+        shp = x.shape
+        y = fused_linear(x.reshape(-1, shp[-1]), self.weight, self.bias, self.relu)
+        return y.reshape(*shp[:-1], self.out_features)
+
+    def extra_repr(self) -> str:
+        return super().extra_repr() + (", relu=True" if self.relu else "")
+
+
+def inject_fused_linear(module: nn.Module) -> int:
+    """Replace nn.Linear (+ a directly following nn.ReLU inside an nn.Sequential) in place,
+    recursively; ``module`` itself may be the Sequential.  Returns the number of Linear layers
+    replaced."""
+    n = 0
+    if isinstance(module, nn.Sequential):
+        kids = list(module.children())
+        for i, k in enumerate(kids):
+            if type(k) is nn.Linear:
+                fold = i + 1 < len(kids) and type(kids[i + 1]) is nn.ReLU
+                module[i] = FusedLinear.from_linear(k, relu=fold)
+                if fold:
+                    module[i + 1] = nn.Identity()
+                n += 1
+            elif not isinstance(k, FusedLinear):
+                n += inject_fused_linear(k)
+        return n
+    for name, child in list(module.named_children()):
+        if type(child) is nn.Linear:
+            setattr(module, name, FusedLinear.from_linear(child))
+            n += 1
+        elif not isinstance(child, FusedLinear):
+            n += inject_fused_linear(child)
+    return n

@@ -200,3 +200,21 @@ def test_fused_bce_falls_back_to_torch_on_cpu():
     loss.backward()
     ref.backward()
     assert torch.equal(loss, ref) and torch.equal(z.grad, ref_z.grad)
+
+
+def test_inject_fused_linear_keeps_parameters_and_falls_back_on_cpu():
+    """Kernel injection swaps Linear(+ReLU) in place: same Parameter objects, same state_dict keys,
+    ReLU folded; on CPU the forward falls back to F.linear and matches the original module."""
+    from distributed_gpu_test_amd.ops.linear import FusedLinear, inject_fused_linear
+    m = _mlp(3)
+    ref = copy.deepcopy(m)
+    params = [id(p) for p in m.parameters()]
+    keys = list(m.state_dict().keys())
+    assert inject_fused_linear(m) == 3
+    assert [id(p) for p in m.parameters()] == params and list(m.state_dict().keys()) == keys
+    assert isinstance(m[0], FusedLinear) and m[0].relu and isinstance(m[1], torch.nn.Identity)
+    assert isinstance(m[2], FusedLinear) and not m[2].relu and isinstance(m[3], torch.nn.Tanh)
+    nested = SimpleNet()
+    assert inject_fused_linear(nested) == 2 and nested.net[0].relu
+    x = torch.randn(5, 12)
+    torch.testing.assert_close(m(x), ref(x))

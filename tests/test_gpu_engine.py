@@ -112,3 +112,46 @@ def test_fused_bce_matches_torch(n, dtype):
     torch.testing.assert_close(loss.cpu(), ref.detach(), rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(z.grad.float().cpu(), zr.grad, rtol=1e-2 if dtype == torch.bfloat16 else 1e-5,
                                atol=1e-7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("M,N,K,relu,bias,need_dx", [(4, 64, 20, True, True, False), (4, 1, 64, False, True, True),
+                                                     (7, 33, 19, True, False, True), (256, 128, 96, True, True, True)])
+def test_fused_linear_matches_torch(M, N, K, relu, bias, need_dx):
+    """csrc/linear.hip forward + one-launch backward vs plain PyTorch fp32 (ReLU mask, dx, dW, db)."""
+    from distributed_gpu_test_amd.ops.linear import _FusedLinearFn
+    g = torch.Generator().manual_seed(M * 1000 + N)
+    x0, w0 = torch.randn(M, K, generator=g), torch.randn(N, K, generator=g) * 0.3
+    b0 = torch.randn(N, generator=g) if bias else None
+    dy0 = torch.randn(M, N, generator=g)
+    xs = [x0.clone().requires_grad_(need_dx), x0.cuda().requires_grad_(need_dx)]
+    ws = [w0.clone().requires_grad_(True), w0.cuda().requires_grad_(True)]
+    bs = [None, None] if b0 is None else [b0.clone().requires_grad_(True), b0.cuda().requires_grad_(True)]
+    ref = torch.nn.functional.linear(xs[0], ws[0], bs[0])
+    ref = torch.relu(ref) if relu else ref
+    ref.backward(dy0)
+    got = _FusedLinearFn.apply(xs[1], ws[1], bs[1], relu)
+    got.backward(dy0.cuda())
+    torch.testing.assert_close(got.detach().cpu(), ref.detach(), rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(ws[1].grad.cpu(), ws[0].grad, rtol=1e-5, atol=1e-5)
+    if bias:
+        torch.testing.assert_close(bs[1].grad.cpu(), bs[0].grad, rtol=1e-5, atol=1e-5)
+    if need_dx:
+        torch.testing.assert_close(xs[1].grad.cpu(), xs[0].grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("graph", [False, True])
+def test_engine_fused_linear_matches_plain(graph):
+    """Kernel injection ("amd": {"fused_linear": true}) keeps the eager engine's trajectory, eager
+    and under whole-step HIP-graph replay."""
+    batches = _batches(10, 11) + _batches(2, 12, bs=8)
+    base = {"train_batch_size": 32}
+    e1, l1, p1 = _run_engine(dict(base), batches)
+    amd = {"fused_linear": True, "hip_graph": graph}
+    e2, l2, p2 = _run_engine(dict(base, amd=amd), batches, graph=graph)
+    assert e2.fused_linear_layers == 2
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(p2, p1, rtol=1e-4, atol=1e-5)
+    e1.close()
+    e2.close()
