@@ -434,16 +434,23 @@ class DgtEngineBench(EngineBench):
         self.engine, _, _, _ = initialize(model=model, optimizer=opt, model_parameters=model.parameters(), config=cfg)
         from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
         crit = BCEWithLogitsLoss()  # fused HIP loss + gradient kernel
+        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=device)
+
+        def loss_fn(rows):
+            # the batch gather and the device-side loss log (the reference's loss.item() sum,
+            # train.py:115) are part of the step, so a HIP graph captures them with it
+            loss = crit(self.engine(self.x[rows]).float(), self.y[rows])
+            self.loss_acc.add_(loss.detach())
+            return loss
+
         if self.engine.config.amd.hip_graph:
-            self.step = self.engine.graph_step(lambda bx, by: crit(self.engine(bx).float(), by))
+            self.step = self.engine.graph_step(loss_fn)
         else:
-            def step(bx, by):
-                loss = crit(self.engine(bx).float(), by)
+            def step(rows):
+                loss = loss_fn(rows)
                 self.engine.backward(loss)
                 self.engine.step()
-                return loss.detach()
             self.step = step
-        self.loss_acc = torch.zeros(1, dtype=torch.float64, device=device)
         graphed = self.engine.graphed is not None
         self.exchange = ("none" if self.world == 1 else
                          ("rccl-native-in-hipgraph" if graphed else f"{comm.backend_name()}-bucketed"))
@@ -453,8 +460,7 @@ class DgtEngineBench(EngineBench):
     def run_plan(self, plan, counts):
         plan_d = plan.to(self.device).long()
         for s in range(plan.shape[0]):
-            rows = plan_d[s, : int(counts[s])]
-            self.loss_acc += self.step(self.x[rows], self.y[rows]).double()
+            self.step(plan_d[s, : int(counts[s])])
 
     @property
     def params(self):

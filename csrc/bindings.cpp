@@ -180,7 +180,8 @@ void linear_fwd(const at::Tensor& x, const at::Tensor& W, const std::optional<at
 }
 
 void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, const std::optional<at::Tensor>& y,
-                const std::optional<at::Tensor>& dx, const at::Tensor& dW, const std::optional<at::Tensor>& db) {
+                const std::optional<at::Tensor>& dx, const at::Tensor& dW, const std::optional<at::Tensor>& db,
+                bool accumulate) {
   check_gpu(dy, "dy", at::kFloat);
   check_gpu(x, "x", at::kFloat);
   check_gpu(W, "W", at::kFloat);
@@ -200,7 +201,8 @@ void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, 
   float* dbp = opt(db, "db", N);
   c10::DeviceGuard guard(x.device());
   DGT_CHECK_HIP(dgt::linear_bwd(dy.data_ptr<float>(), x.data_ptr<float>(), W.data_ptr<float>(), yp, dxp,
-                                dW.data_ptr<float>(), dbp, (int)M, (int)N, (int)K, stream_of(x)));
+                                dW.data_ptr<float>(), dbp, (int)M, (int)N, (int)K, accumulate,
+                                stream_of(x)));
 }
 
 void bce_logits(const at::Tensor& z, const at::Tensor& y, const at::Tensor& loss, const at::Tensor& dz) {
@@ -553,7 +555,8 @@ TORCH_LIBRARY(dgt, m) {
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz) -> ()", &bce_logits);
   m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
-  m.def("linear_bwd(Tensor dy, Tensor x, Tensor W, Tensor? y, Tensor(a!)? dx, Tensor(b!) dW, Tensor(c!)? db) -> ()",
+  m.def("linear_bwd(Tensor dy, Tensor x, Tensor W, Tensor? y, Tensor(a!)? dx, Tensor(b!) dW, Tensor(c!)? db, "
+        "bool accumulate=False) -> ()",
         &linear_bwd);
   m.def(
       "oneshot_allreduce(Tensor inp, Tensor(a!) out, float scale, int[] data_ptrs, int rank, "

@@ -94,7 +94,7 @@ hipError_t adam_matrix_t(const AdamFlatArgs& a, void* lpT, int rows, int cols, h
 hipError_t linear_fwd(const float* x, const float* W, const float* b, float* y, int M, int N, int K, bool relu,
                       hipStream_t stream);
 hipError_t linear_bwd(const float* dy, const float* x, const float* W, const float* y, float* dx, float* dW,
-                      float* db, int M, int N, int K, hipStream_t stream);
+                      float* db, int M, int N, int K, bool accumulate, hipStream_t stream);
 hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz,
                       hipStream_t stream);
 

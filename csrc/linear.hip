@@ -39,13 +39,15 @@ __global__ __launch_bounds__(256) void linear_fwd_kernel(const float* __restrict
 }
 
 // g = dy * 1[y > 0] (relu) or dy.  One launch, three thread ranges:
-//   [0, N*K)            dW[n][k] = sum_m g[m][n] x[m][k]
-//   [N*K, N*K+N)        db[n]    = sum_m g[m][n]                 (if db)
+//   [0, N*K)            dW[n][k] (+)= sum_m g[m][n] x[m][k]
+//   [N*K, N*K+N)        db[n]    (+)= sum_m g[m][n]               (if db)
+// accumulate: add into dW / db (they are the parameters' .grad views into the engine's flat bucket)
 //   [.., + M*K)         dx[m][k] = sum_n g[m][n] W[n][k]         (if dx)
 __global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict__ dy, const float* __restrict__ x,
                                                           const float* __restrict__ W, const float* __restrict__ y,
                                                           float* __restrict__ dx, float* __restrict__ dW,
-                                                          float* __restrict__ db, int M, int N, int K) {
+                                                          float* __restrict__ db, int M, int N, int K,
+                                                          int accumulate) {
   int i = blockIdx.x * 256 + threadIdx.x;
   auto g = [&](int m, int n) {
     const float d = dy[(long long)m * N + n];
@@ -55,7 +57,7 @@ __global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict
     const int n = i / K, k = i % K;
     float acc = 0.f;
     for (int m = 0; m < M; ++m) acc = fmaf(g(m, n), x[(long long)m * K + k], acc);
-    dW[i] = acc;
+    dW[i] = accumulate ? dW[i] + acc : acc;
     return;
   }
   i -= N * K;
@@ -63,7 +65,7 @@ __global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict
     if (i < N) {
       float acc = 0.f;
       for (int m = 0; m < M; ++m) acc += g(m, i);
-      db[i] = acc;
+      db[i] = accumulate ? db[i] + acc : acc;
       return;
     }
     i -= N;
@@ -86,11 +88,11 @@ hipError_t linear_fwd(const float* x, const float* W, const float* b, float* y, 
 }
 
 hipError_t linear_bwd(const float* dy, const float* x, const float* W, const float* y, float* dx, float* dW,
-                      float* db, int M, int N, int K, hipStream_t stream) {
+                      float* db, int M, int N, int K, bool accumulate, hipStream_t stream) {
   if (M <= 0 || N <= 0 || K <= 0) return hipErrorInvalidValue;
   const long long total = (long long)N * K + (db ? N : 0) + (dx ? (long long)M * K : 0);
   hipLaunchKernelGGL(linear_bwd_kernel, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, stream, dy, x, W, y,
-                     dx, dW, db, M, N, K);
+                     dx, dW, db, M, N, K, accumulate ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -84,7 +84,7 @@ class Engine:
         self.fused_linear_layers = 0
         if config.amd.fused_linear and device.type == "cuda" and self.dtype == torch.float32:
             from .ops.linear import inject_fused_linear
-            self.fused_linear_layers = inject_fused_linear(self.module)
+            self.fused_linear_layers = inject_fused_linear(self.module, grad_in_place=True)
         self.stage = config.zero_stage
         self.gas = config.gradient_accumulation_steps
         self.micro_batch = config.train_micro_batch_size_per_gpu

@@ -27,11 +27,14 @@ SMALL_WORK = 1 << 22     # M * N * K: beyond this a tiled GEMM (hipBLASLt / csrc
 
 class _FusedLinearFn(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, x, weight, bias, relu: bool):
+    def forward(ctx, x, weight, bias, relu: bool, grad_in_place: bool = False):
         y = torch.empty(x.shape[0], weight.shape[0], dtype=torch.float32, device=x.device)
         _ext.require().linear_fwd(x, weight, bias, y, relu)
         ctx.relu = relu
         ctx.has_bias = bias is not None
+        # leaf parameters only (no reference cycle through ctx)
+        ctx.grad_in_place = grad_in_place and weight.is_leaf and (bias is None or bias.is_leaf)
+        ctx.params = (weight, bias) if ctx.grad_in_place else (None, None)
         ctx.save_for_backward(x, weight, y if relu else None)
         return y
 
@@ -40,10 +43,25 @@ class _FusedLinearFn(torch.autograd.Function):
         x, weight, y = ctx.saved_tensors
         dy = dy.contiguous()
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
+        w_leaf, b_leaf = ctx.params
+        if ctx.grad_in_place and w_leaf.requires_grad and _grad_view_ok(w_leaf) and (b_leaf is None or _grad_view_ok(b_leaf)):
+            # accumulate straight into the existing .grad views (the engine's flat bucket): no
+            # separate AccumulateGrad add kernel per parameter.  Autograd still runs the leaves'
+            # AccumulateGrad nodes with an undefined gradient, which fire the post-accumulate hooks
+            # (the engine's bucket reducer) after this kernel is queued
+            _ext.require().linear_bwd(dy, x, weight, y, dx, w_leaf.grad,
+                                      None if b_leaf is None else b_leaf.grad, True)
+            return dx, None, None, None, None
         dw = torch.empty_like(weight)
         db = torch.empty(weight.shape[0], dtype=torch.float32, device=x.device) if ctx.has_bias else None
         _ext.require().linear_bwd(dy, x, weight, y, dx, dw, db)
-        return dx, dw, db, None
+        return dx, dw, db, None, None
+
+
+def _grad_view_ok(p) -> bool:
+    g = p.grad
+    return (g is not None and g.is_cuda and g.dtype == torch.float32 and g.is_contiguous()
+            and g.shape == p.shape and not torch.is_grad_enabled())
 
 
 def _fusable(x: torch.Tensor, weight: torch.Tensor) -> bool:
@@ -52,9 +70,13 @@ def _fusable(x: torch.Tensor, weight: torch.Tensor) -> bool:
             and _ext.available())
 
 
-def fused_linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = False) -> torch.Tensor:
+def fused_linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = False,
+                 grad_in_place: bool = False) -> torch.Tensor:
+    """``grad_in_place``: backward adds dW / db into existing ``.grad`` tensors of leaf parameters
+    instead of returning them to autograd (their post-accumulate hooks still fire); only for
+    ``loss.backward()``-style use, never ``torch.autograd.grad`` on the parameters."""
     if _fusable(x, weight):
-        return _FusedLinearFn.apply(x.contiguous(), weight, bias, relu)
+        return _FusedLinearFn.apply(x.contiguous(), weight, bias, relu, grad_in_place)
     y = F.linear(x, weight, bias)
     return F.relu(y) if relu else y
 
@@ -66,47 +88,50 @@ class FusedLinear(nn.Linear):
                  device=None, dtype=None):
         super().__init__(in_features, out_features, bias=bias, device=device, dtype=dtype)
         self.relu = relu
+        self.grad_in_place = False
 
     @classmethod
-    def from_linear(cls, lin: nn.Linear, relu: bool = False) -> "FusedLinear":
+    def from_linear(cls, lin: nn.Linear, relu: bool = False, grad_in_place: bool = False) -> "FusedLinear":
         m = cls.__new__(cls)
         nn.Module.__init__(m)
         m.in_features, m.out_features = lin.in_features, lin.out_features
         m.weight = lin.weight          # the same Parameter objects
         m.bias = lin.bias
         m.relu = relu
+        m.grad_in_place = grad_in_place
         return m
 
     def forward(self, x: torch.Tensor) -> torch.Tensor:
         shp = x.shape
-        y = fused_linear(x.reshape(-1, shp[-1]), self.weight, self.bias, self.relu)
+        y = fused_linear(x.reshape(-1, shp[-1]), self.weight, self.bias, self.relu, self.grad_in_place)
         return y.reshape(*shp[:-1], self.out_features)
 
     def extra_repr(self) -> str:
         return super().extra_repr() + (", relu=True" if self.relu else "")
 
 
-def inject_fused_linear(module: nn.Module) -> int:
+def inject_fused_linear(module: nn.Module, grad_in_place: bool = False) -> int:
     """Replace nn.Linear (+ a directly following nn.ReLU inside an nn.Sequential) in place,
     recursively; ``module`` itself may be the Sequential.  Returns the number of Linear layers
-    replaced."""
+    replaced.  ``grad_in_place``: see ``fused_linear`` (the engine sets it: its .grad tensors are
+    persistent views into the flat gradient bucket)."""
     n = 0
     if isinstance(module, nn.Sequential):
         kids = list(module.children())
         for i, k in enumerate(kids):
             if type(k) is nn.Linear:
                 fold = i + 1 < len(kids) and type(kids[i + 1]) is nn.ReLU
-                module[i] = FusedLinear.from_linear(k, relu=fold)
+                module[i] = FusedLinear.from_linear(k, relu=fold, grad_in_place=grad_in_place)
                 if fold:
                     module[i + 1] = nn.Identity()
                 n += 1
             elif not isinstance(k, FusedLinear):
-                n += inject_fused_linear(k)
+                n += inject_fused_linear(k, grad_in_place)
         return n
     for name, child in list(module.named_children()):
         if type(child) is nn.Linear:
-            setattr(module, name, FusedLinear.from_linear(child))
+            setattr(module, name, FusedLinear.from_linear(child, grad_in_place=grad_in_place))
             n += 1
         elif not isinstance(child, FusedLinear):
-            n += inject_fused_linear(child)
+            n += inject_fused_linear(child, grad_in_place)
     return n

@@ -57,6 +57,11 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
             store = dist.PrefixStore(f"/dgt/attempt_{restart}", store)
             dist.init_process_group(backend=backend, store=store, rank=info.rank, world_size=info.world_size,
                                     timeout=timeout)
+        elif info.source == "bare" and info.world_size == 1:
+            # a lone process has nobody to rendezvous with: an in-memory store, no TCP port to race
+            # for (MASTER_ADDR / MASTER_PORT are still exported for tools that read them)
+            dist.init_process_group(backend=backend, store=dist.HashStore(), rank=0, world_size=1,
+                                    timeout=timeout)
         else:
             dist.init_process_group(backend=backend, init_method="env://", rank=info.rank,
                                     world_size=info.world_size, timeout=timeout)

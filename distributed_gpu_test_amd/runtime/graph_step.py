@@ -67,6 +67,7 @@ class GraphedStep:
         self.pool = torch.cuda.graph_pool_handle()
         self.graphs: Dict[tuple, tuple] = {}  # shape key -> (graph, static inputs, static loss)
         self.seen: Dict[tuple, int] = {}
+        self.seeds: Dict[tuple, torch.Tensor] = {}
         self.replays = 0
         self.eager_steps = 0
         self.failed = ""
@@ -122,7 +123,7 @@ class GraphedStep:
         e.store.rebind_grads()  # .grad views into the flat bucket (host-side binding, no kernel)
         e.store.grad_buf.zero_()
         loss = self.loss_fn(*args)
-        loss.float().backward()
+        loss.float().backward(self._seed(loss))
         grads = self._reduce()
         scale = 1.0 / e.world_size
         coef = self._clip(grads, scale)
@@ -134,6 +135,16 @@ class GraphedStep:
         if e.stage >= 1:
             self._allgather()
         return loss.detach()
+
+    def _seed(self, loss: torch.Tensor) -> Optional[torch.Tensor]:
+        """A persistent ones tensor for the backward seed, so a captured step has no fill node
+        for it.  Made only outside capture (a tensor from the graph's private pool must not
+        outlive its graph); a capture that finds none lets autograd fill its own."""
+        key = (tuple(loss.shape), loss.device)
+        seed = self.seeds.get(key)
+        if seed is None and not torch.cuda.is_current_stream_capturing():
+            seed = self.seeds[key] = torch.ones(loss.shape, dtype=torch.float32, device=loss.device)
+        return seed
 
     # ------------------------------------------------------------------ public
     def __call__(self, *args) -> torch.Tensor:

@@ -155,3 +155,25 @@ def test_engine_fused_linear_matches_plain(graph):
     torch.testing.assert_close(p2, p1, rtol=1e-4, atol=1e-5)
     e1.close()
     e2.close()
+
+
+@pytest.mark.gpu
+def test_fused_linear_grad_in_place_accumulates_and_fires_hooks():
+    """grad_in_place backward adds into the existing .grad tensors (two backwards accumulate) and
+    fires each parameter's post-accumulate hook once per backward, as AccumulateGrad does."""
+    from distributed_gpu_test_amd.ops.linear import inject_fused_linear
+    torch.manual_seed(9)
+    ref = torch.nn.Sequential(torch.nn.Linear(20, 64), torch.nn.ReLU(), torch.nn.Linear(64, 1)).cuda()
+    m = copy.deepcopy(ref)
+    assert inject_fused_linear(m, grad_in_place=True) == 2
+    fired = []
+    for i, p in enumerate(m.parameters()):
+        p.grad = torch.zeros_like(p)
+        p.register_post_accumulate_grad_hook(lambda _p, i=i: fired.append(i))
+    x = torch.randn(4, 20, device="cuda")
+    for _ in range(2):
+        m(x).square().sum().backward()
+        ref(x).square().sum().backward()
+    assert sorted(fired) == [0, 0, 1, 1, 2, 2, 3, 3]
+    for p, q in zip(m.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-5)

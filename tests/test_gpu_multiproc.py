@@ -50,6 +50,18 @@ def test_engine_oneshot_two_ranks_one_gpu(tmp_path):
     assert losses(r.stdout) == ORACLE2[:2]
 
 
+def test_engine_fused_linear_two_ranks_one_gpu(tmp_path):
+    """Kernel injection with in-place gradient accumulation: the bucket hooks still fire (one-shot
+    all-reduce per bucket) and the run prints the ws=2 oracle."""
+    import json
+    cfg = tmp_path / "ds.json"
+    cfg.write_text(json.dumps({"train_batch_size": 64, "gradient_accumulation_steps": 1,
+                               "zero_optimization": {"stage": 0}, "amd": {"fused_linear": True}}))
+    r = run(2, "train.py", "--impl", "engine", "--epochs", "2", "--no-save", "--deepspeed_config", str(cfg))
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert losses(r.stdout) == ORACLE2[:2]
+
+
 def test_bench_two_ranks_one_gpu():
     r = run(2, "bench.py", "--gpus", "2", "--steps", "3000", "--warmup", "300", "--no-sweep")
     assert r.returncode == 0, r.stderr[-4000:]
