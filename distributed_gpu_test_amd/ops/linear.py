@@ -67,7 +67,7 @@ def _grad_view_ok(p) -> bool:
 def _fusable(x: torch.Tensor, weight: torch.Tensor) -> bool:
     return (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and weight.dtype == torch.float32
             and x.shape[0] <= SMALL_M and x.shape[0] * weight.shape[0] * weight.shape[1] <= SMALL_WORK
-            and _ext.available())
+            and _ext.require() is not None)  # a GPU shape we own: a missing extension is an error
 
 
 def fused_linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = False,

@@ -37,7 +37,7 @@ class _FusedBCEWithLogits(torch.autograd.Function):
 def bce_with_logits(z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
     """Mean BCE-with-logits; the fused HIP kernel on GPU fp32 / bf16 logits."""
     if (z.is_cuda and z.dtype in (torch.float32, torch.bfloat16) and z.numel() == y.numel() and z.numel() > 0
-            and _ext.available()):
+            and _ext.require() is not None):  # on the GPU a missing extension is an error, not a fallback
         return _FusedBCEWithLogits.apply(z, y)
     return F.binary_cross_entropy_with_logits(z, y.to(z.dtype))
 
