@@ -86,6 +86,66 @@ DGT_DEVICE f32x4 adam_group(const AdamFlatArgs& a, const GT* __restrict__ grad, 
   return p;
 }
 
+// Eight consecutive elements per thread: the 16-bit streams (bf16/fp16 gradients and the compute
+// copy) then move as 16-byte vectors too, instead of the 8-byte accesses of a float4 group.
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+template <typename T> DGT_DEVICE T from_f32(float x);
+template <> DGT_DEVICE __hip_bfloat16 from_f32<__hip_bfloat16>(float x) { return __float2bfloat16(x); }
+template <> DGT_DEVICE __half from_f32<__half>(float x) { return __float2half(x); }
+template <typename T, bool NT> struct Vec8 {  // 16-bit types: one 16-byte access
+  static DGT_DEVICE void load(const T* p, f32x4& lo, f32x4& hi) {
+    const u32x4 raw = vload<NT>(reinterpret_cast<const u32x4*>(p));
+    const T* h = reinterpret_cast<const T*>(&raw);
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      lo[i] = (float)h[i];
+      hi[i] = (float)h[4 + i];
+    }
+  }
+  static DGT_DEVICE void store(T* p, const f32x4& lo, const f32x4& hi) {
+    T b[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      b[i] = from_f32<T>(lo[i]);
+      b[4 + i] = from_f32<T>(hi[i]);
+    }
+    vstore<NT>(reinterpret_cast<u32x4*>(p), *reinterpret_cast<u32x4*>(b));
+  }
+};
+template <bool NT> struct Vec8<float, NT> {
+  static DGT_DEVICE void load(const float* p, f32x4& lo, f32x4& hi) {
+    lo = Vec4<float, NT>::load(p);
+    hi = Vec4<float, NT>::load(p + 4);
+  }
+  static DGT_DEVICE void store(float* p, const f32x4& lo, const f32x4& hi) {
+    Vec4<float, NT>::store(p, lo);
+    Vec4<float, NT>::store(p + 4, hi);
+  }
+};
+
+template <typename GT, typename LT, bool NT>
+DGT_DEVICE void adam_group8(const AdamFlatArgs& a, const GT* __restrict__ grad, LT* __restrict__ lp, long long o,
+                            float scale, float step_size_neg, float bc2_sqrt) {
+  f32x4 p[2], g[2], m[2], v[2];
+  Vec8<float, NT>::load(a.master + o, p[0], p[1]);
+  Vec8<GT, NT>::load(grad + o, g[0], g[1]);
+  Vec8<float, NT>::load(a.exp_avg + o, m[0], m[1]);
+  Vec8<float, NT>::load(a.exp_avg_sq + o, v[0], v[1]);
+#pragma unroll
+  for (int h = 0; h < 2; ++h)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float mm = m[h][e], vv = v[h][e];
+      p[h][e] = adam_update(p[h][e], g[h][e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
+      m[h][e] = mm;
+      v[h][e] = vv;
+    }
+  Vec8<float, NT>::store(a.master + o, p[0], p[1]);
+  Vec8<float, NT>::store(a.exp_avg + o, m[0], m[1]);
+  Vec8<float, NT>::store(a.exp_avg_sq + o, v[0], v[1]);
+  if (lp) Vec8<LT, NT>::store(lp + o, p[0], p[1]);
+}
+
 // Bias corrections of this update: host scalars, or (graph replay) formed on the device from the
 // step counter in double, exactly as torch's non-capturable Adam does on the host.
 DGT_DEVICE void adam_bias_corrections(const AdamFlatArgs& a, float& step_size_neg, float& bc2_sqrt) {
@@ -123,6 +183,20 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   }
 }
 
+// one 8-element group per thread; a trailing float4 group (n % 8 == 4) goes to thread n / 8
+template <typename GT, typename LT, bool NT>
+__global__ __launch_bounds__(256) void adam_flat8_kernel(AdamFlatArgs a) {
+  float step_size_neg, bc2_sqrt;
+  adam_bias_corrections(a, step_size_neg, bc2_sqrt);
+  float scale = a.grad_scale;
+  if (a.grad_scale_dev) scale *= *a.grad_scale_dev;
+  const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
+  LT* __restrict__ lp = static_cast<LT*>(a.param_lp);
+  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x, n8 = a.n >> 3;
+  if (i < n8) adam_group8<GT, LT, NT>(a, grad, lp, 8 * i, scale, step_size_neg, bc2_sqrt);
+  else if (i == n8 && (a.n & 4)) adam_group<GT, LT, NT>(a, grad, lp, 8 * i, scale, step_size_neg, bc2_sqrt);
+}
+
 // loop shape chosen by measurement (scripts/bench_adam.py); DGT_ADAM_VARIANT overrides it for A/B runs
 static int adam_variant() {
   const char* e = getenv("DGT_ADAM_VARIANT");
@@ -145,6 +219,10 @@ static void launch_adam_v(const AdamFlatArgs& a, hipStream_t s) {
     case 3:  // one group per thread, plain, full grid
       grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);
       hipLaunchKernelGGL((adam_flat_kernel<GT, LT, false, 1>), dim3((int)grid), dim3(256), 0, s, a);
+      break;
+    case 4:  // one 8-element group per thread (16-byte 16-bit streams), streaming hints, full grid
+      grid = std::max<long long>((a.n / 8 + 1 + 255) / 256, 1);
+      hipLaunchKernelGGL((adam_flat8_kernel<GT, LT, true>), dim3((int)grid), dim3(256), 0, s, a);
       break;
     default:  // one group per thread, streaming hints, full grid: 6.1 TB/s at 67M params
       grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);

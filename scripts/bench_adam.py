@@ -13,13 +13,16 @@ from distributed_gpu_test_amd.ops.adam import adam_flat_  # noqa: E402
 
 N = 4 * 4096 * 4096 + 4 * 4096 + 4096 + 1 + 3  # bench MLP, padded to a multiple of 4
 VARIANTS = {0: "1 group, nontemporal, full grid (default)", 1: "2 groups, plain, grid<=4096",
-            2: "2 groups, nontemporal, grid<=4096", 3: "1 group, plain, full grid"}
+            2: "2 groups, nontemporal, grid<=4096", 3: "1 group, plain, full grid",
+            4: "8 elements per thread (16-byte 16-bit streams), nontemporal, full grid"}
+GRAD_DTYPE = torch.bfloat16 if "bf16" in sys.argv[1:] else torch.float32  # the MLP trainer's grads are bf16
+BYTES = 28 if GRAD_DTYPE == torch.bfloat16 else 30
 
 
 def main():
     dev = torch.device("cuda")
     master = torch.randn(N, device=dev)
-    grad = torch.randn(N, device=dev)
+    grad = torch.randn(N, device=dev).to(GRAD_DTYPE)
     m = torch.zeros(N, device=dev)
     v = torch.zeros(N, device=dev)
     lp = torch.empty(N, device=dev, dtype=torch.bfloat16)
@@ -43,8 +46,8 @@ def main():
     for k, name in VARIANTS.items():
         t = sorted(times[k])
         us = t[len(t) // 2]
-        print(json.dumps({"variant": k, "desc": name, "n_params": N, "us_median": round(us, 1), "us_min": round(t[0], 1),
-                          "TBps": round(N * 30 / us / 1e6, 2)}), flush=True)
+        print(json.dumps({"variant": k, "desc": name, "grad": str(GRAD_DTYPE), "n_params": N, "us_median": round(us, 1), "us_min": round(t[0], 1),
+                          "TBps": round(N * BYTES / us / 1e6, 2)}), flush=True)
 
 
 if __name__ == "__main__":

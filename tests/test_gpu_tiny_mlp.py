@@ -96,6 +96,25 @@ def test_adam_flat_matches_reference(gdt, lpdt, wd, adamw):
         torch.testing.assert_close(lp, p2.to(lpdt))
 
 
+@pytest.mark.parametrize("n", [4096 * 3 + 4, 4096 * 3 + 8, 4])
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
+def test_adam_flat_loop_variants_bit_identical(monkeypatch, n, variant):
+    """Every loop shape of the flat Adam (csrc/adam.hip launch_adam_v) gives the default's bits,
+    including the 8-element variant's trailing float4 group (n % 8 == 4)."""
+    g = torch.Generator().manual_seed(1)
+    p0 = torch.randn(n, generator=g).cuda()
+    gr = torch.randn(n, generator=g).cuda().bfloat16()
+    outs = []
+    for var in ("0", variant):
+        monkeypatch.setenv("DGT_ADAM_VARIANT", var)
+        p, m, v = p0.clone(), torch.full_like(p0, 0.1), torch.full_like(p0, 0.2)
+        lp = torch.empty(n, device="cuda", dtype=torch.bfloat16)
+        adam_flat_(p, gr, m, v, 3, 1e-3, 0.9, 0.999, 1e-8, 0.01, True, param_lp=lp)
+        outs.append((p, m, v, lp))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
 def test_graph_impl_matches_oracle_and_stepwise():
     x, y, m1 = _setup()
     _, _, m2 = _setup()
