@@ -2,25 +2,37 @@
 # no Triton on the compute path.  The HIP extension and the rccl_perf tool are compiled for gfx950
 # at build time (hipcc cross-compiles; no GPU needed during `docker build`).
 # Reference: Dockerfile:2-16 (nvcr CUDA 12.8 base + pip torch/deepspeed) -> rocm/pytorch + in-tree HIP build.
+#
+# Layout: the framework is installed under DGT_HOME=/opt/dgt, OUTSIDE /workspace.  The SLURM job
+# mounts the CI submit directory over /workspace (the reference's
+# `--container-mounts=$SLURM_SUBMIT_DIR:/workspace`, slurm_train.sbatch:34-35), which hides
+# whatever the image had there; everything the job executes (train.py, the package with its built
+# _C.so, scripts/health.py, build/bin/rccl_perf) therefore lives in /opt/dgt, and /workspace only
+# receives logs, checkpoints and job_status.txt.  tests/test_slurm_fake.py builds a fake image from
+# THIS file's ENV / WORKDIR / COPY lines and runs the sbatch against it with the CI's file set.
 ARG BASE_IMAGE=rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.7.1
 FROM ${BASE_IMAGE}
 
 ENV DEBIAN_FRONTEND=noninteractive \
     PYTORCH_ROCM_ARCH=gfx950 \
     HSA_ENABLE_IPC_MODE_LEGACY=0 \
-    PYTHONUNBUFFERED=1
+    PYTHONUNBUFFERED=1 \
+    DGT_HOME=/opt/dgt \
+    PYTHONPATH=/opt/dgt
 WORKDIR /workspace
 
-COPY distributed_gpu_test_amd/ /workspace/distributed_gpu_test_amd/
-COPY csrc/ /workspace/csrc/
-COPY tools/ /workspace/tools/
-COPY scripts/ /workspace/scripts/
-COPY configs/ /workspace/configs/
-COPY train.py bench.py __graft_entry__.py slurm_train.sbatch /workspace/
+COPY distributed_gpu_test_amd/ /opt/dgt/distributed_gpu_test_amd/
+COPY csrc/ /opt/dgt/csrc/
+COPY tools/ /opt/dgt/tools/
+COPY scripts/ /opt/dgt/scripts/
+COPY configs/ /opt/dgt/configs/
+COPY train.py bench.py __graft_entry__.py slurm_train.sbatch /opt/dgt/
 
-RUN python3 tools/build_ext.py -j 8 && \
-    python3 -c "import distributed_gpu_test_amd, torch; print('dgt ok, torch', torch.__version__)"
+RUN cd /opt/dgt && python3 tools/build_ext.py -j 8 && \
+    test -x /opt/dgt/build/bin/rccl_perf && \
+    cd / && python3 -c "import distributed_gpu_test_amd as d, torch; from distributed_gpu_test_amd.ops import _ext; \
+assert _ext.available(); print('dgt ok from', d.__file__, 'torch', torch.__version__)"
 
 # A bare `docker run` works: a single process, rank 0 of 1 (the reference's bare entrypoint
 # crashed, SURVEY Q1/Q9).
-CMD ["python3", "/workspace/train.py"]
+CMD ["python3", "/opt/dgt/train.py"]

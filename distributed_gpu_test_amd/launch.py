@@ -131,6 +131,12 @@ def slurm_master_port(job_id: Optional[str], base: int = 20000, span: int = 2000
     return base + int(digits) % span
 
 
+def hostname() -> str:
+    """This node's name for same-host decisions (IPC mailboxes only work within one node).
+    ``DGT_HOSTNAME`` overrides it: the fake-SLURM multi-node tests run every "node" on one machine."""
+    return os.environ.get("DGT_HOSTNAME") or socket.gethostname()
+
+
 def free_port(host: str = "127.0.0.1") -> int:
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind((host, 0))

@@ -21,11 +21,11 @@ rank disables the channel everywhere and callers fall back to RCCL.
 from __future__ import annotations
 
 import os
-import socket
 from typing import List, Optional
 
 import torch
 
+from ..launch import hostname
 from ..ops._ext import require
 from . import comm
 
@@ -66,7 +66,7 @@ class IpcChannel:
         handle = b""
         # IPC handles only name memory on THIS node: a job that spans nodes never opens them
         # (callers fall back to RCCL, which bridges nodes over the network)
-        hosts = comm.all_gather_object(socket.gethostname())
+        hosts = comm.all_gather_object(hostname())
         if len(set(hosts)) > 1:
             self.error = RuntimeError(f"ranks span {len(set(hosts))} hosts: no cross-node IPC mailboxes")
         else:

@@ -77,9 +77,31 @@ def smi_reports():
     return out
 
 
-def bandwidth_sweep(ngpus: int):
+def rccl_perf_path():
+    """The rccl-tests equivalent built next to this script (``<DGT_HOME>/build/bin/rccl_perf``)."""
     exe = os.path.join(ROOT, "build", "bin", "rccl_perf")
-    if not os.path.exists(exe) or ngpus < 1:
+    return exe if os.access(exe, os.X_OK) else None
+
+
+def framework_info():
+    """Where the framework and its native pieces were found (catches an image whose install was
+    hidden by a mount: the SLURM job must run the IMAGE's code, slurm_train.sbatch)."""
+    info = {"dgt_home": ROOT, "rccl_perf": rccl_perf_path()}
+    try:
+        sys.path.insert(0, ROOT)
+        import distributed_gpu_test_amd as dgt
+        from distributed_gpu_test_amd.ops import _ext
+        info["package"] = os.path.dirname(dgt.__file__)
+        info["extension"] = _ext.LIB_PATH if _ext.available() else None
+    except Exception as e:
+        info["package"] = None
+        info["error"] = f"{type(e).__name__}: {e}"
+    return info
+
+
+def bandwidth_sweep(ngpus: int):
+    exe = rccl_perf_path()
+    if exe is None or ngpus < 1:
         return {"skipped": "rccl_perf not built or no GPU"}
     res = {}
     for op in ("all_reduce", "reduce_scatter", "all_gather"):
@@ -110,6 +132,7 @@ def main(argv=None):
     rep = {"host": socket.gethostname(), "node": int(node), "time": time.time(), "tag": tag,
            "env": {k: os.environ.get(k) for k in ("SLURM_JOB_ID", "SLURM_JOB_NODELIST", "HIP_VISIBLE_DEVICES",
                                                    "HSA_ENABLE_IPC_MODE_LEGACY", "NCCL_DEBUG")}}
+    rep["framework"] = framework_info()
     rep["gpu"] = gpu_inventory()
     rep["smi"] = smi_reports()
     n = int(rep["gpu"].get("gpu_count") or 0)
@@ -125,7 +148,7 @@ def main(argv=None):
           f"{rep['gpu'].get('devices', [{}])[0].get('name', '') if n else ''} RCCL {rep['gpu'].get('rccl_version')} "
           f"all_reduce peak busbw {peak} GB/s -> {path}", flush=True)
     wrong = sum(v.get("wrong", 0) for v in bw.values() if isinstance(v, dict)) if isinstance(bw, dict) else 0
-    if a.strict and (n == 0 or wrong):
+    if a.strict and (n == 0 or wrong or not rep["framework"].get("extension")):
         return 1
     return 0
 

@@ -1,67 +1,90 @@
 #!/bin/bash
-# Submit slurm_train.sbatch on a SLURM login node and wait for its verdict (the CI's
-# "test-on-slurm" step, reference .github/workflows/distributed-gpu-test-ci.yaml:107-181, moved
-# into a script so it can be tested against fake SLURM commands).
+# CI "test-on-slurm" step as a script (testable against tests/fake_slurm): size the job to the
+# cluster, submit slurm_train.sbatch, wait for it to leave the queue, then turn the job's
+# job_status.txt into this script's exit code.  Same contract as the reference's inline CI step
+# (.github/workflows/distributed-gpu-test-ci.yaml:107-181 there).
 #
-#   scripts/slurm_submit_and_wait.sh [REMOTE_DIR]
+#   scripts/slurm_submit_and_wait.sh [SUBMIT_DIR]
 #
-# Cluster discovery: NODES = number of nodes (DGT_NODES overrides; the reference counts every
-# node of the cluster), GPUS = gres/gpu of the first node's CfgTRES (DGT_GPUS_PER_NODE overrides).
-# Exit codes (same as the reference): 0 success, 1 fail / unknown / missing status,
-# 2 submission failed, 124 job did not leave squeue in time.
+# Sizing: nodes = NodeName lines of `scontrol show nodes` (DGT_NODES overrides), GPUs per node =
+# gres/gpu of the first node's CfgTRES (DGT_GPUS_PER_NODE overrides; 8 if none is reported).
+# Exit codes: 0 success | 1 job failed, or status unknown / missing | 2 sbatch failed |
+# 124 the job was still queued/running at the deadline (it is cancelled).
+# Timing knobs: DGT_POLL_INTERVAL (10 s) x DGT_POLL_MAX (30) for the queue,
+# DGT_STATUS_POLL_INTERVAL (10 s) x DGT_STATUS_POLL_MAX (3) for the status file.
 set -euo pipefail
 
-REMOTE_DIR=${1:-$PWD}
-cd "$REMOTE_DIR"
+SUBMIT_DIR=${1:-$PWD}
+cd "$SUBMIT_DIR"
+STATUS_FILE="$PWD/job_status.txt"
 
-NODES=${DGT_NODES:-$(scontrol show nodes | grep -c '^NodeName')}
-GPUS=${DGT_GPUS_PER_NODE:-$(scontrol show nodes | sed -n 's/.*CfgTRES=.*gres\/gpu=\([0-9][0-9]*\).*/\1/p' | head -n1)}
-GPUS=${GPUS:-8}
-sed -e "s/^#SBATCH --nodes=.*/#SBATCH --nodes=${NODES}/" \
-    -e "s/^#SBATCH --gres=gpu:.*/#SBATCH --gres=gpu:${GPUS}/" \
-    slurm_train.sbatch > slurm_train.submit.sbatch
-rm -f "$PWD/job_status.txt"
-SBATCH_OUT=$(sbatch --export=ALL,GPUS_PER_NODE="$GPUS",NNODES="$NODES" slurm_train.submit.sbatch || true)
-if [ -z "$SBATCH_OUT" ]; then
-  echo "Failed to submit job; sbatch output: $SBATCH_OUT"
-  exit 2
-fi
-JOB_ID=$(echo "$SBATCH_OUT" | awk '{print $NF}')
-echo "Submitted batch job $JOB_ID (nodes=$NODES gpus/node=$GPUS)"
+log() { echo "[submit] $*"; }
 
-JOB_POLL_INTERVAL=${DGT_POLL_INTERVAL:-10}
-JOB_POLL_MAX=${DGT_POLL_MAX:-30}
-STATE=""
-for (( i=0; i<JOB_POLL_MAX; i++ )); do
-  STATE=$(squeue -j "$JOB_ID" -h -o "%T" 2>/dev/null | tr -d '\r' || true)
-  if [ -z "$STATE" ]; then
-    echo "Job $JOB_ID no longer in squeue (checked $((i+1)) times)"
-    break
+cluster_shape() {
+  local nodes_out
+  nodes_out=$(scontrol show nodes)
+  N_NODES=${DGT_NODES:-$(grep -c '^NodeName' <<<"$nodes_out" || true)}
+  N_GPUS=${DGT_GPUS_PER_NODE:-$(grep -o 'gres/gpu=[0-9]*' <<<"$nodes_out" | head -n 1 | cut -d= -f2 || true)}
+  [ "${N_NODES:-0}" -ge 1 ] 2>/dev/null || N_NODES=1
+  [ "${N_GPUS:-0}" -ge 1 ] 2>/dev/null || N_GPUS=8
+}
+
+render_job() {  # the sbatch with its #SBATCH geometry rewritten for this cluster
+  awk -v n="$N_NODES" -v g="$N_GPUS" '
+    /^#SBATCH --nodes=/   { print "#SBATCH --nodes=" n; next }
+    /^#SBATCH --gres=gpu:/ { print "#SBATCH --gres=gpu:" g; next }
+    { print }' slurm_train.sbatch > slurm_train.submit.sbatch
+}
+
+submit() {
+  local out
+  out=$(sbatch --export=ALL,GPUS_PER_NODE="$N_GPUS",NNODES="$N_NODES" slurm_train.submit.sbatch || true)
+  JOB_ID=$(awk '/Submitted batch job/ { print $NF }' <<<"$out")
+  if [ -z "$JOB_ID" ]; then
+    log "sbatch did not return a job id; output: '$out'"
+    exit 2
   fi
-  echo "Job $JOB_ID state: $STATE — sleeping ${JOB_POLL_INTERVAL}s..."
-  sleep "$JOB_POLL_INTERVAL"
-done
-if [ -n "$STATE" ]; then
-  echo "Job $JOB_ID still in squeue after $((JOB_POLL_MAX * JOB_POLL_INTERVAL)) seconds; cancelling."
+  log "Submitted batch job $JOB_ID (nodes=$N_NODES gpus/node=$N_GPUS)"
+}
+
+wait_for_queue_exit() {
+  local every=${DGT_POLL_INTERVAL:-10} max=${DGT_POLL_MAX:-30} n state
+  for (( n = 1; n <= max; n++ )); do
+    state=$(squeue -j "$JOB_ID" -h -o "%T" 2>/dev/null | tr -d '\r' || true)
+    if [ -z "$state" ]; then
+      log "job $JOB_ID left the queue after $n check(s)"
+      return 0
+    fi
+    log "job $JOB_ID is $state; next check in ${every}s"
+    sleep "$every"
+  done
+  log "job $JOB_ID still queued/running after $((every * max))s: cancelling it"
   scancel "$JOB_ID" || true
   exit 124
-fi
+}
 
-STATUS_FILE="$PWD/job_status.txt"
-STATUS_POLL_INTERVAL=${DGT_STATUS_POLL_INTERVAL:-10}
-STATUS_POLL_MAX=${DGT_STATUS_POLL_MAX:-3}
-for (( j=0; j<STATUS_POLL_MAX; j++ )); do
-  if [ -f "$STATUS_FILE" ]; then
-    STATUS=$(tr -d '\r' < "$STATUS_FILE" || true)
-    echo "Found $STATUS_FILE -> '$STATUS'"
-    case "$STATUS" in
-      success|0) exit 0 ;;
-      fail|1) echo "Remote job reported fail"; exit 1 ;;
-      *) echo "Unknown status file content: '$STATUS' — treating as failure"; exit 1 ;;
-    esac
-  fi
-  echo "Status file not present yet — sleeping ${STATUS_POLL_INTERVAL}s..."
-  sleep "$STATUS_POLL_INTERVAL"
-done
-echo "$STATUS_FILE did not appear after $((STATUS_POLL_MAX * STATUS_POLL_INTERVAL)) seconds — treating as failure"
-exit 1
+verdict() {
+  local every=${DGT_STATUS_POLL_INTERVAL:-10} max=${DGT_STATUS_POLL_MAX:-3} n status
+  for (( n = 1; n <= max; n++ )); do
+    if [ -f "$STATUS_FILE" ]; then
+      status=$(tr -d '\r\n' < "$STATUS_FILE" || true)
+      log "$STATUS_FILE says '$status'"
+      case "$status" in
+        success|0) exit 0 ;;
+        fail|1) log "the job reported failure"; exit 1 ;;
+        *) log "unrecognised status '$status': failing"; exit 1 ;;
+      esac
+    fi
+    log "no $STATUS_FILE yet (shared filesystem lag?); next check in ${every}s"
+    sleep "$every"
+  done
+  log "$STATUS_FILE never appeared: failing"
+  exit 1
+}
+
+cluster_shape
+render_job
+rm -f "$STATUS_FILE"
+submit
+wait_for_queue_exit
+verdict
