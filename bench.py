@@ -11,10 +11,14 @@ cross-rank gradient reduction and optimizer update; nothing is cached or skipped
     python bench.py                                  # 1 GPU
     torchrun --nproc-per-node N bench.py --gpus N    # N GPUs, one rank per GPU (RCCL/xGMI)
 
-Before the timed region (untimed): the fused kernel's per-launch workspace is sized and the Adam
-bias-correction schedule of the K timed steps (lr / (1 - beta1^t), 1 / sqrt(1 - beta2^t) for
-t = W+1 .. W+K: a function of the step number only, like an LR table) is precomputed, so the timed
-region holds exactly one kernel launch that runs all K optimizer steps.
+The timed region of the fused path holds exactly one kernel launch that runs all K optimizer
+steps, including every step's Adam bias corrections (formed in double inside the kernel).  Before
+it, untimed: the W warmup steps and the sampler's index plan of the K steps (the DataLoader's work,
+uploaded once, as the trainer does once per epoch).
+
+``n_gpus`` counts distinct physical devices (host + PCI address gathered over ranks); ``ranks`` is
+the process count and ``oversubscribed`` is true when ranks share a device.  A run whose ranks end
+with different parameters exits non-zero and prints no headline line.
 
 ``value`` is the whole-job aggregate: optimizer iterations per second summed over ranks
 (= N x global steps/s).  ``allreduce_busbw_GBps`` is the peak RCCL all-reduce bus bandwidth of a
@@ -149,29 +153,38 @@ def timed_run(trainer, plan, counts, args, device, comm):
     """W untimed warmup steps, then exactly K timed steps between barrier + device syncs.
     Returns (max elapsed over ranks, mean loss over the timed steps).  Raises on every rank if the
     fused kernel failed on any rank."""
-    if hasattr(trainer, "reserve"):  # launch-path workspaces sized before anything is timed
-        trainer.reserve(max(args.warmup, args.steps))
     if args.warmup:
-        trainer.run_plan(plan[: args.warmup], counts[: args.warmup])
+        # the last few warmup steps run as single-step launches: the launch path itself (HIP
+        # runtime, dispatcher, Python) is then as warm for the timed launch as in steady state
+        tail = min(args.warmup, 4)
+        head = args.warmup - tail
+        if head:
+            trainer.run_plan(plan[:head], counts[:head])
+        for s in range(head, args.warmup):
+            trainer.run_plan(plan[s:s + 1], counts[s:s + 1])
+    timed_plan, timed_counts = plan[args.warmup:], counts[args.warmup:]  # views; the upload happened in build_plan
     if device.type == "cuda":
         torch.cuda.synchronize()
     failed = _failed(trainer)
     if comm.all_reduce_max(float(failed)) > 0:
         raise RuntimeError("warmup failed on some rank")
     trainer.loss_acc.zero_()
-    if hasattr(trainer, "prepare"):  # Adam bias-correction schedule of the K timed steps (step-number table)
-        trainer.prepare(args.steps)
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    trainer.run_plan(plan[args.warmup:], counts[args.warmup:])
+    trainer.run_plan(timed_plan, timed_counts)
+    t1 = time.perf_counter()
     if device.type == "cuda":
         torch.cuda.synchronize()
+    t2 = time.perf_counter()
     comm.barrier()
     if device.type == "cuda":
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
+    if os.environ.get("DGT_BENCH_BREAKDOWN"):
+        print(f"[bench] timed region: host launch {1e6 * (t1 - t0):.1f} us, device wait {1e6 * (t2 - t1):.1f} us, "
+              f"closing barrier+sync {1e6 * (elapsed - (t2 - t0)):.1f} us", file=sys.stderr, flush=True)
     if comm.all_reduce_max(float(_failed(trainer))) > 0:
         raise RuntimeError("timed run failed on some rank")
     mean_loss = float(trainer.loss_acc.item()) / max(1, args.steps)
@@ -187,6 +200,28 @@ def _failed(trainer) -> bool:
         return True
 
 
+def device_identity(device) -> str:
+    """Host + PCI address of this rank's device: ranks sharing one card report the same string.
+    (A CPU rank is its own device: there is no card to share.)"""
+    import socket
+    if device.type != "cuda":
+        return f"{socket.gethostname()}/cpu-rank{dist.get_rank() if dist.is_initialized() else 0}"
+    p = torch.cuda.get_device_properties(device)
+    return f"{socket.gethostname()}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+
+
+def params_consistent(params, world: int) -> bool:
+    """Every rank must hold bit-identical parameters after data-parallel training."""
+    if world == 1:
+        return True
+    p = params.detach().clone()
+    ref = p.clone()
+    dist.broadcast(ref, 0)
+    flag = torch.tensor([0.0 if torch.equal(p, ref) else 1.0], device=p.device)
+    dist.all_reduce(flag, op=dist.ReduceOp.MAX)
+    return flag.item() == 0.0
+
+
 def main(argv=None):
     args = parse_args(argv)
     os.environ.setdefault("DGT_QUIET", "1")  # the engine's steps_per_print lines would be timed too
@@ -199,7 +234,8 @@ def main(argv=None):
     world, rank = comm.get_world_size(), comm.get_rank()
     if args.gpus != world:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
-    device = torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available() else torch.device("cpu")
+    from distributed_gpu_test_amd.accelerator import get_accelerator
+    device = get_accelerator().device()
 
     torch.manual_seed(42)
     x, y = make_synthetic_data(2000, 20, 42)
@@ -237,15 +273,17 @@ def main(argv=None):
         plan, counts = build_plan(trainer, args.warmup + args.steps)
         elapsed_max, mean_loss = timed_run(trainer, plan, counts, args, device, comm)
 
-    # every rank must hold identical parameters after DP training
-    consistent = True
-    if world > 1:
-        p = trainer.params.detach().clone()
-        ref = p.clone()
-        dist.broadcast(ref, 0)
-        flag = torch.tensor([0.0 if torch.equal(p, ref) else 1.0], device=p.device)
-        dist.all_reduce(flag, op=dist.ReduceOp.MAX)
-        consistent = flag.item() == 0.0
+    # every rank must hold identical parameters after DP training; a divergent run has no headline
+    consistent = params_consistent(trainer.params, world)
+    if not consistent:
+        if rank == 0:
+            print(json.dumps({"metric": METRIC, "error": "parameters differ across ranks after training",
+                              "impl": trainer.impl, "exchange": trainer.exchange}), file=sys.stderr, flush=True)
+        trainer.close()
+        comm.destroy()
+        return 3
+    devices = comm.all_gather_object(device_identity(device))
+    n_devices = len(set(devices))
 
     gpu_sweeps = not args.no_sweep and device.type == "cuda" and world > 1
     sweep = allreduce_sweep(device, args.sweep_max_mb, world) if gpu_sweeps and comm.backend_name() == "nccl" else []
@@ -274,7 +312,7 @@ def main(argv=None):
         "metric": METRIC,
         "value": round(world * global_steps_per_s, 2),
         "unit": "iters/s (sum over ranks)",
-        "n_gpus": world,
+        "n_gpus": n_devices,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms, 6),
@@ -291,6 +329,8 @@ def main(argv=None):
         "samples_per_sec": round(global_steps_per_s * B * world, 2),
         "mean_loss": round(mean_loss, 6),
         "model_tflops": None if tflops is None else round(tflops, 2),
+        "ranks": world,
+        "oversubscribed": n_devices < world,
         "params_consistent_across_ranks": consistent,
         "allreduce_busbw_GBps": None if peak_busbw is None else round(peak_busbw, 2),
         "allreduce_5KB_us": None if small is None else round(small["us"], 2),
@@ -303,6 +343,7 @@ def main(argv=None):
         print(json.dumps(out), flush=True)
     trainer.close()
     comm.destroy()
+    return 0
 
 
 class EngineBench:
@@ -475,4 +516,4 @@ class DgtEngineBench(EngineBench):
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

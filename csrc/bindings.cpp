@@ -54,6 +54,7 @@ dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank,
   ex.stride = (int)stride;
   ex.seq_base = seq_base;
   ex.timeout_ticks = timeout_ticks;
+  ex.corrupt_step = -1;
   if (world_size > 1) {
     TORCH_CHECK((int64_t)data_ptrs.size() == world_size, "dgt: need one mailbox pointer per rank");
     TORCH_CHECK(stride > 0 && stride % 256 == 0, "dgt: mailbox stride must be a positive multiple of 256 floats");
@@ -85,7 +86,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
                     double lr, double beta1, double beta2, double eps, double weight_decay, bool adamw,
                     int64_t adam_step0, c10::ArrayRef<int64_t> data_ptrs,
                     int64_t rank, int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks,
-                    const std::optional<at::Tensor>& workspace, bool table_ready) {
+                    int64_t corrupt_step) {
   TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
               " H=", hidden);
   TORCH_CHECK(beta1 > 0.5 && beta1 < 1.0 && beta2 > 0.0 && beta2 < 1.0, "dgt: fused kernel needs 0.5 < beta1 < 1");
@@ -121,24 +122,10 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   a.beta1 = beta1;
   a.beta2 = beta2;
   a.adam_step0 = adam_step0;
-  // Adam bias-correction table, one spare row: the kernel prefetches step s+1's pair while it runs
-  // step s.  A caller-owned workspace keeps allocation (a hipMalloc when the caching allocator has
-  // no block of that size) out of the launch path.
-  const int64_t bc_need = (std::max<int64_t>(plan.size(0), 1) + 1) * 2;
-  at::Tensor bc;
-  if (workspace.has_value() && workspace->defined()) {
-    check_gpu(*workspace, "workspace", at::kFloat);
-    TORCH_CHECK(workspace->numel() >= bc_need, "dgt: tiny_mlp_train workspace needs ", bc_need, " floats");
-    bc = *workspace;
-  } else {
-    TORCH_CHECK(!table_ready, "dgt: table_ready needs the workspace that holds the table");
-    bc = at::empty({bc_need}, X.options());
-  }
-  a.bc = bc.data_ptr<float>();
-  a.bc_ready = table_ready ? 1 : 0;
   a.loss_acc = loss_acc.data_ptr<double>();
   a.status = status.data_ptr<int>();
   a.ex = make_exchange(data_ptrs, rank, world_size, stride, seq_base, timeout_ticks);
+  a.ex.corrupt_step = corrupt_step;
   a.stamps = nullptr;
   if (world_size > 1) {
     const int64_t need = dgt::tiny_mlp_exchange_floats((int)n_features, (int)hidden);
@@ -146,16 +133,6 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   }
   if (a.n_steps == 0) return;
   DGT_CHECK_HIP(dgt::tiny_mlp_train((int)n_features, (int)hidden, a, stream_of(X)));
-}
-
-void tiny_mlp_bias_table(const at::Tensor& workspace, int64_t n_steps, int64_t step0, double lr, double beta1,
-                         double beta2) {
-  check_gpu(workspace, "workspace", at::kFloat);
-  TORCH_CHECK(n_steps >= 1 && workspace.numel() >= (n_steps + 1) * 2, "dgt: bias table workspace needs ",
-              (n_steps + 1) * 2, " floats");
-  c10::DeviceGuard guard(workspace.device());
-  DGT_CHECK_HIP(dgt::tiny_mlp_bias_table(workspace.data_ptr<float>(), (int)n_steps, step0, lr, beta1, beta2,
-                                         stream_of(workspace)));
 }
 
 // ------------------------------------------------------------------------------ fused BCE loss
@@ -533,11 +510,8 @@ TORCH_LIBRARY(dgt, m) {
       "tiny_mlp_train(Tensor X, Tensor Y, Tensor plan, Tensor counts, Tensor(a!) params, Tensor(b!) exp_avg, "
       "Tensor(c!) exp_avg_sq, Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, "
       "float beta1, float beta2, float eps, float weight_decay, bool adamw, int adam_step0, int[] data_ptrs, "
-      "int rank, int world_size, int stride, int seq_base, int timeout_ticks, Tensor(f!)? workspace=None, "
-      "bool table_ready=False) -> ()",
+      "int rank, int world_size, int stride, int seq_base, int timeout_ticks, int corrupt_step=-1) -> ()",
       &tiny_mlp_train);
-  m.def("tiny_mlp_bias_table(Tensor(a!) workspace, int n_steps, int step0, float lr, float beta1, float beta2) -> ()",
-        &tiny_mlp_bias_table);
   m.def(
       "tiny_mlp_grad(Tensor X, Tensor Y, Tensor plan, Tensor counts, int step, Tensor params, Tensor(a!) grad, "
       "Tensor(b!) loss_acc, int n_features, int hidden) -> ()",

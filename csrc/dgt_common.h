@@ -49,6 +49,8 @@ struct Exchange {
   long long seq_base;               // sequence number of the first exchange of this launch (0-based)
   long long timeout_ticks;          // bound on every spin, in s_memrealtime ticks (100 MHz)
   unsigned* data[kMaxRanks];        // each rank's mailbox (index rank = local)
+  long long corrupt_step;           // fault injection: at this 1-based optimizer step the fused kernel
+                                    // corrupts one payload it sends to rank + 1 (-1 = never)
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));

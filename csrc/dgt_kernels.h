@@ -26,21 +26,14 @@ struct TinyTrainArgs {
   AdamHyper hp;
   double lr;             // python-double lr (bias-corrected step size is formed in double)
   double beta1, beta2;
-  long long adam_step0;  // optimizer steps already taken before this launch
-  float* bc;             // [n_steps][2] workspace: per-step bias corrections (filled by tiny_mlp_train)
+  long long adam_step0;  // optimizer steps already taken before this launch (bias corrections in-kernel)
   double* loss_acc;      // += sum over steps of the step's mean loss
   int* status;           // Status
   Exchange ex;           // world_size 1 -> no exchange
   unsigned long long* stamps;  // diagnostic builds only (-DDGT_TINY_STAMPS); nullptr otherwise
-  int bc_ready;          // 1: bc already holds this launch's table (tiny_mlp_bias_table); skip filling it
 };
 
 hipError_t tiny_mlp_train(int n_features, int hidden, const TinyTrainArgs& a, hipStream_t stream);
-
-// Fill bc[2 s], bc[2 s + 1] (s < n_steps) with the Adam bias corrections of optimizer step
-// step0 + s + 1, as tiny_mlp_train would before its loop (a precomputed schedule, like an LR table).
-hipError_t tiny_mlp_bias_table(float* bc, int n_steps, long long step0, double lr, double beta1, double beta2,
-                               hipStream_t stream);
 
 struct TinyGradArgs {
   const float* X;

@@ -70,10 +70,6 @@ int main(int argc, char** argv) {
   a.loss_acc = dLoss; a.status = dStatus;
   a.ex.rank = 0; a.ex.world_size = 1;
   a.stamps = dStamps;
-  a.bc_ready = 0;
-  float* dBc;
-  CK(hipMalloc(&dBc, (size_t)(steps + 1) * 2 * sizeof(float)));  // +1: read-ahead of the kernel
-  a.bc = dBc;
   CK(dgt::tiny_mlp_train(F, H, a, 0));
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;

@@ -31,8 +31,11 @@
 //     until every peer's tags match and sums the contributions in rank order, so every rank
 //     applies bit-identical updates.  This replaces DeepSpeed's flatten -> NCCL all_reduce ->
 //     scale -> unflatten.
-//   * Adam's bias corrections come from a per-step table (torch's double-precision formula,
-//     filled by a one-thread-per-step kernel before the launch): no double math in the loop.
+//   * Adam's bias corrections are formed IN the kernel, in double with torch's formula, T steps at
+//     a time (one step per thread) into a double-buffered LDS ring: the prologue fills steps
+//     0..T-1 (binary exponentiation), and the first step of every T-block fills the next block after its barrier
+//     (beta^t advanced by one multiply with beta^T).  The loop reads one wave-uniform float2 per
+//     step; nothing is precomputed before the launch.
 // Reference: train.py:26-36 (model), 96 (loss), 98-117 (loop), 113 (all-reduce), 114 (Adam step).
 #include "dgt_common.h"
 #include "dgt_kernels.h"
@@ -103,6 +106,7 @@ struct __attribute__((aligned(16))) TinySmem {
   WaveSmem<F, H> w[C::NW];
   double loss[C::NW];        // per-wave deferred-loss totals, summed in wave order at the end
   float Z[2][C::NW * 16];    // per-wave partial logits, double-buffered by step parity
+  float2 bc[2][C::T];        // Adam bias corrections {-lr/(1-b1^t), 1/sqrt(1-b2^t)}: ring of 2 T-step blocks
   int err;
 };
 
@@ -277,6 +281,32 @@ DGT_DEVICE int plan_at(const int* plan, int n_steps, int bmax, int step, int row
   return (step < n_steps && row < bmax) ? plan[(long long)step * bmax + row] : -1;
 }
 
+// Adam bias corrections of one optimizer step from beta1^t and beta2^t, in double as torch's
+// non-capturable foreach Adam forms them on the host (adam.py: step_size = lr / (1 - beta1 ** step),
+// bias_correction2_sqrt = sqrt(1 - beta2 ** step)), rounded to fp32 once.
+DGT_DEVICE float2 adam_bias_pair(double b1p, double b2p, double lr) {
+  return float2{(float)(-(lr / (1.0 - b1p))), (float)(1.0 / sqrt(1.0 - b2p))};
+}
+
+// beta^n by binary exponentiation (<= 2 log2(n) double roundings: ~1e-14 relative at n = 1e6, far
+// below the fp32 rounding of the result; far less code and register pressure than ocml's pow).
+DGT_DEVICE double ipow(double b, long long n) {
+  double r = 1.0;
+  while (n > 0) {
+    if (n & 1) r *= b;
+    b *= b;
+    n >>= 1;
+  }
+  return r;
+}
+
+// Bias-correction ring of one thread: it owns launch steps base + t (one per T-step block) and
+// carries beta^(its optimizer step) in double, advanced by beta^T per block (one multiply).
+struct BiasRing {
+  double b1p, b2p;  // beta1^t, beta2^t of this thread's current entry
+  double b1T, b2T;  // beta1^T, beta2^T
+};
+
 // ------------------------------------------------------------------ persistent training kernel
 // NP > 1: the exchange is compiled in (for up to NP ranks).  The single-rank kernel has no exchange
 // branch, so backward and Adam form one basic block the scheduler can interleave.
@@ -306,6 +336,12 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   for (int i = l; i < C::BM * C::SX; i += 64) ws.X[i] = 0.f;
   for (int i = l; i < C::BM * 17; i += 64) ws.DH[i] = 0.f;
   if (t == 0) sm.err = 0;
+  BiasRing ring;  // bias corrections of launch steps 0 .. T-1 (thread t: optimizer step step0 + t + 1)
+  ring.b1p = ipow(a.beta1, a.adam_step0 + t + 1);
+  ring.b2p = ipow(a.beta2, a.adam_step0 + t + 1);
+  ring.b1T = ipow(a.beta1, C::T);
+  ring.b2T = ipow(a.beta2, C::T);
+  if (t < a.n_steps) sm.bc[0][t] = adam_bias_pair(ring.b1p, ring.b2p, a.lr);
   float x[C::NSP], y, xn[C::NSP], yn;
   load_rows<F, H>(a.X, a.Y, plan_at(a.plan, a.n_steps, a.bmax, 0, lr), lq, x, y);
   int idx_next = plan_at(a.plan, a.n_steps, a.bmax, 1, lr);
@@ -315,9 +351,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   double loss_total = 0.0;
   float zs = 0.f, ys = 0.f, ibs = 0.f;  // deferred-loss ring (wave 0)
   const float inv_ws = 1.0f / (float)ex.world_size;
-  // Adam bias corrections of the current step, loaded a step ahead: the scalar load of step s+1's
-  // pair is in flight during step s (a K$ miss every 8th step otherwise stalled the Adam section)
-  float bc_ss = load_uniform(a.bc), bc_ib = load_uniform(a.bc + 1);
+  constexpr int LOG_T = __builtin_ctz(C::T);  // T = 64 * NW is a power of two
 #ifdef DGT_TINY_STAMPS
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0;
 #endif
@@ -325,7 +359,10 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(0);
     const int Bt = load_uniform(a.counts + s);
     const float invB = __builtin_amdgcn_rcpf((float)Bt);
-    const float bc_ss_next = load_uniform(a.bc + 2 * s + 2), bc_ib_next = load_uniform(a.bc + 2 * s + 3);
+    // this step's bias corrections (wave-uniform LDS broadcast, consumed by the Adam section).  The
+    // entry was written at least one barrier ago: in the prologue, or after the barrier of step
+    // s - T (the first step of the previous block)
+    const float2 bcv = sm.bc[(s >> LOG_T) & 1][s & (C::T - 1)];
     // prefetch step s+1 rows into registers; consumed by the next step's forward
     load_rows<F, H>(a.X, a.Y, idx_next, lq, xn, yn);
     // sampler index of step s+3, issued now so the end-of-step rotation never waits on it
@@ -384,12 +421,16 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
       }
       const long long wofs = (long long)w * C::NQ * 512 + l * 4;
       const long long mine = ll_slot(ex, parity, ex.rank) + wofs;
+      // fault injection (--fail-at R:S:corrupt): one payload to rank + 1 is off by 1.0 at step S, so
+      // the replicas diverge and the per-epoch replica check must catch it (scalar test otherwise)
+      const int victim = (ex.corrupt_step == a.adam_step0 + s + 1 && w == 0) ? (ex.rank + 1) % ex.world_size : -1;
       for (int p = 0; p < ex.world_size; ++p) {
         if (p == ex.rank) continue;
         unsigned* dst = ex.data[p] + mine;
+        const float c0 = (p == victim && l == 0) ? pk[0][0] + 1.0f : pk[0][0];
 #pragma unroll
         for (int q = 0; q < C::NQ; ++q) {
-          ll_put(dst + (2 * q) * 256, pk[q][0], pk[q][1], tag);
+          ll_put(dst + (2 * q) * 256, q == 0 ? c0 : pk[q][0], pk[q][1], tag);
           ll_put(dst + (2 * q + 1) * 256, pk[q][2], pk[q][3], tag);
         }
       }
@@ -456,10 +497,8 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     }
     DGT_STAMP(4);
 
-    // ---- Adam; bias corrections of this step from the table (wave-uniform, prefetched)
-    const float step_size_neg = bc_ss, inv_bc2_sqrt = bc_ib;
-    bc_ss = bc_ss_next;
-    bc_ib = bc_ib_next;
+    // ---- Adam with this step's bias corrections
+    const float step_size_neg = bcv.x, inv_bc2_sqrt = bcv.y;
     // two parameters per packed-fp32 update (W2 and b2 form the last pair)
 #pragma unroll
     for (int i = 0; i < C::NSP; i += 2) {
@@ -483,6 +522,14 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
       st.mb2 = m.y;
       st.vbw = v.x;
       st.vb2 = v.y;
+    }
+    // first step of a block: fill the other ring buffer with the next block.  Every wave is past
+    // this step's barrier, so all reads of that buffer (the previous block, last read at step s - 1)
+    // are done; its first reader (step s + T) is at least one barrier away.
+    if ((s & (C::T - 1)) == 0 && s + C::T < a.n_steps) {
+      ring.b1p *= ring.b1T;
+      ring.b2p *= ring.b2T;
+      if (s + C::T + t < a.n_steps) sm.bc[((s >> LOG_T) + 1) & 1][t] = adam_bias_pair(ring.b1p, ring.b2p, a.lr);
     }
     // rotate the prefetch pipeline
 #pragma unroll
@@ -583,30 +630,8 @@ int tiny_mlp_exchange_floats(int f, int h) {
   return 0;
 }
 
-// Per-step Adam bias corrections for a launch, in double exactly as torch's (non-capturable)
-// foreach Adam forms them on the host: step_size = -(lr / (1 - beta1^t)), 1 / sqrt(1 - beta2^t).
-__global__ void adam_bias_table_kernel(float* bc, int n, long long step0, double lr, double beta1, double beta2) {
-  const int s = blockIdx.x * blockDim.x + threadIdx.x;
-  if (s >= n) return;
-  const double t = (double)(step0 + s + 1);
-  bc[2 * s] = (float)(-(lr / (1.0 - pow(beta1, t))));
-  bc[2 * s + 1] = (float)(1.0 / sqrt(1.0 - pow(beta2, t)));
-}
-
-hipError_t tiny_mlp_bias_table(float* bc, int n_steps, long long step0, double lr, double beta1, double beta2,
-                               hipStream_t stream) {
-  if (!bc || n_steps < 1) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(adam_bias_table_kernel, dim3((n_steps + 255) / 256), dim3(256), 0, stream, bc, n_steps, step0, lr,
-                     beta1, beta2);
-  return hipGetLastError();
-}
-
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
-  if (!a.bc) return hipErrorInvalidValue;
   const bool wd = a.hp.weight_decay != 0.f;
-  if (!a.bc_ready)
-    hipLaunchKernelGGL(adam_bias_table_kernel, dim3((a.n_steps + 255) / 256), dim3(256), 0, stream, a.bc, a.n_steps,
-                       a.adam_step0, a.lr, a.beta1, a.beta2);
 #define DGT_TINY_LAUNCH_NP(F_, H_, SB, NP_)                                                      \
   do {                                                                                      \
     if (wd)                                                                                 \

@@ -8,6 +8,7 @@ PyTorch-ROCm + hand-written HIP/CDNA4 kernels + RCCL over xGMI.
 """
 __version__ = "0.1.0"
 
+from .accelerator import get_accelerator  # noqa: F401
 from .launch import RankInfo, resolve_rank_info  # noqa: F401
 from .config import DSConfig, parse_config, REFERENCE_DS_CONFIG  # noqa: F401
 from .parallel.comm import init_distributed, destroy  # noqa: F401

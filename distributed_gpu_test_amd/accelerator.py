@@ -1,9 +1,13 @@
 """Device abstraction: the role of ``deepspeed.accelerator.get_accelerator()``.
 
-The reference calls ``get_accelerator().set_device(local_rank)`` (``train.py:61``).  Two
-implementations: ``hip`` (AMD Instinct via PyTorch-ROCm, whose device namespace is ``torch.cuda``;
-collectives go to RCCL through the ``nccl`` backend name) and ``cpu`` (gloo).  ``DGT_ACCELERATOR``
-forces one.
+The reference calls ``get_accelerator().set_device(local_rank)`` (``train.py:12,61``).  Here the
+accelerator is the ONE place that decides where a run computes and which collective backend it
+uses: ``comm.init_distributed`` binds the rank's device and picks the backend through it, and the
+engine, the trainers, ``train.py`` and ``bench.py`` take their default device from it.
+
+Two implementations: ``hip`` (AMD Instinct through PyTorch-ROCm, whose device namespace is
+``torch.cuda``; collectives go to RCCL through the ``nccl`` backend name) and ``cpu`` (gloo).
+``DGT_ACCELERATOR=cpu|hip`` forces one; by default ``hip`` when a GPU is visible.
 """
 from __future__ import annotations
 
@@ -25,53 +29,18 @@ class HipAccelerator:
     def current_device(self) -> int:
         return torch.cuda.current_device()
 
-    def set_device(self, index: int) -> None:
-        torch.cuda.set_device(index)
+    def set_device(self, local_rank: int) -> None:
+        """Bind ``local_rank``'s GPU (ranks beyond the visible count wrap: oversubscribed runs)."""
+        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
 
     def device(self, index: Optional[int] = None) -> torch.device:
         return torch.device("cuda", self.current_device() if index is None else index)
-
-    def device_name(self, index: Optional[int] = None) -> str:
-        return f"cuda:{self.current_device() if index is None else index}"
-
-    def device_properties(self, index: Optional[int] = None):
-        return torch.cuda.get_device_properties(self.current_device() if index is None else index)
-
-    def arch(self, index: Optional[int] = None) -> str:
-        return getattr(self.device_properties(index), "gcnArchName", "unknown")
 
     def communication_backend_name(self) -> str:
         return "nccl"  # ProcessGroupNCCL is backed by RCCL on ROCm
 
     def synchronize(self) -> None:
         torch.cuda.synchronize()
-
-    def Stream(self, **kw):
-        return torch.cuda.Stream(**kw)
-
-    def Event(self, **kw):
-        return torch.cuda.Event(**kw)
-
-    def stream(self, s):
-        return torch.cuda.stream(s)
-
-    def current_stream(self):
-        return torch.cuda.current_stream()
-
-    def memory_allocated(self) -> int:
-        return torch.cuda.memory_allocated()
-
-    def max_memory_allocated(self) -> int:
-        return torch.cuda.max_memory_allocated()
-
-    def total_memory(self, index: Optional[int] = None) -> int:
-        return self.device_properties(index).total_memory
-
-    def manual_seed(self, seed: int) -> None:
-        torch.cuda.manual_seed(seed)
-
-    def graph(self, g, **kw):
-        return torch.cuda.graph(g, **kw)
 
 
 class CpuAccelerator:
@@ -86,32 +55,17 @@ class CpuAccelerator:
     def current_device(self) -> int:
         return 0
 
-    def set_device(self, index: int) -> None:
+    def set_device(self, local_rank: int) -> None:
         pass
 
     def device(self, index: Optional[int] = None) -> torch.device:
         return torch.device("cpu")
-
-    def device_name(self, index: Optional[int] = None) -> str:
-        return "cpu"
-
-    def arch(self, index: Optional[int] = None) -> str:
-        return "cpu"
 
     def communication_backend_name(self) -> str:
         return "gloo"
 
     def synchronize(self) -> None:
         pass
-
-    def memory_allocated(self) -> int:
-        return 0
-
-    def max_memory_allocated(self) -> int:
-        return 0
-
-    def manual_seed(self, seed: int) -> None:
-        torch.manual_seed(seed)
 
 
 _ACCEL = None
@@ -121,8 +75,18 @@ def get_accelerator():
     global _ACCEL
     if _ACCEL is None:
         forced = os.environ.get("DGT_ACCELERATOR")
-        if forced == "cpu" or (forced is None and not torch.cuda.is_available()):
+        if forced not in (None, "", "cpu", "hip"):
+            raise ValueError(f"DGT_ACCELERATOR must be 'cpu' or 'hip', got {forced!r}")
+        if forced == "hip" and not torch.cuda.is_available():
+            raise RuntimeError("DGT_ACCELERATOR=hip but no GPU is visible")
+        if forced == "cpu" or (not forced and not torch.cuda.is_available()):
             _ACCEL = CpuAccelerator()
         else:
             _ACCEL = HipAccelerator()
     return _ACCEL
+
+
+def reset_accelerator() -> None:
+    """Forget the cached choice (tests that change ``DGT_ACCELERATOR``)."""
+    global _ACCEL
+    _ACCEL = None

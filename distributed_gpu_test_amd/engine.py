@@ -31,6 +31,7 @@ import torch.distributed as dist
 
 from .config import DSConfig, parse_config
 from .ops.adam import adam_flat_
+from .accelerator import get_accelerator
 from .parallel import comm
 from .parallel.reducer import GradReducer
 from .runtime import checkpoint as ckpt
@@ -76,8 +77,7 @@ class Engine:
         self.world_size = comm.get_world_size()
         self.local_rank = comm.rank_info().local_rank
         if device is None:
-            device = (torch.device("cuda", torch.cuda.current_device()) if torch.cuda.is_available()
-                      else torch.device("cpu"))
+            device = get_accelerator().device()
         self.device = device
         self.dtype = _DTYPES[config.compute_dtype]
         self.module = model.to(device=device, dtype=self.dtype)
@@ -114,8 +114,7 @@ class Engine:
         self.layout = FlatLayout([tuple(p.shape) for p in self.params], bucket_elems, self.world_size,
                                  shard=self.stage >= 1)
         self.store = FlatParamStore(self.params, self.layout, device, self.dtype)
-        if self.world_size > 1:
-            comm.broadcast_(self.store.param_buf, 0)  # DeepSpeed _broadcast_model
+        comm.broadcast_(self.store.param_buf, 0)  # DeepSpeed _broadcast_model
 
         # ---- fp32 master + moments (full for stage 0, this rank's shard for stage >= 1)
         if self.stage == 0:
@@ -246,7 +245,7 @@ class Engine:
             self._grad_norm = None
             return None
         sq = grads.float().pow(2).sum() * (scale * scale)
-        if self.stage >= 1 and self.world_size > 1:
+        if self.stage >= 1:
             comm.all_reduce_(sq)
         norm = sq.sqrt()
         self._grad_norm = norm
@@ -263,7 +262,7 @@ class Engine:
         if self.loss_scaler is not None:
             scale /= self.loss_scaler.scale
             overflow = not bool(torch.isfinite(grads).all().item())
-            if self.stage >= 1 and self.world_size > 1:
+            if self.stage >= 1 and comm.collectives_on(self.world_size):
                 overflow = comm.all_reduce_max(float(overflow), self.device) > 0
             self.loss_scaler.update(overflow)
             if overflow:
@@ -290,15 +289,16 @@ class Engine:
         src = self.param_lp if self.param_lp is not None else self.master
         works = []
         off = 0
+        on = comm.collectives_on(self.world_size)
         for b in self.layout.buckets:
             n = b.numel // self.world_size
             out = self.store.param_buf[b.start:b.start + b.numel]
             piece = src[off:off + n]
-            if self.world_size > 1 and comm.needs_host_staging(out):
+            if on and comm.needs_host_staging(out):
                 host = torch.empty(b.numel, dtype=piece.dtype)
                 dist.all_gather_into_tensor(host, piece.detach().cpu())
                 out.copy_(host)
-            elif self.world_size > 1:
+            elif on:
                 works.append(dist.all_gather_into_tensor(out, piece, async_op=True))
             else:
                 out.copy_(piece)

@@ -16,17 +16,18 @@ from typing import Any, List, Optional
 import torch
 import torch.distributed as dist
 
+from ..accelerator import get_accelerator
 from ..launch import RankInfo, free_port, resolve_rank_info
 
 _RANK_INFO: Optional[RankInfo] = None
 
 
 def default_backend() -> str:
-    """``DGT_BACKEND`` overrides; else nccl (= RCCL) with a GPU, gloo without."""
+    """``DGT_BACKEND`` overrides; else the accelerator's: nccl (= RCCL) on HIP, gloo on CPU."""
     env = os.environ.get("DGT_BACKEND")
     if env:
         return env
-    return "nccl" if torch.cuda.is_available() else "gloo"
+    return get_accelerator().communication_backend_name()
 
 
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
@@ -38,11 +39,13 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
         info = replace(info, master_port=free_port(info.master_addr))
     info.export()
     backend = backend or default_backend()
+    accel = get_accelerator()
     if backend == "nccl":
-        if not torch.cuda.is_available():
-            raise RuntimeError("backend 'nccl' (RCCL) requested but no GPU is visible")
-        if set_device:
-            torch.cuda.set_device(info.local_rank % max(torch.cuda.device_count(), 1))
+        if accel.name != "hip":
+            raise RuntimeError("backend 'nccl' (RCCL) requested but the accelerator is "
+                               f"{accel.name!r} (no GPU visible, or DGT_ACCELERATOR=cpu)")
+        if set_device:  # the reference's get_accelerator().set_device(local_rank) (train.py:61)
+            accel.set_device(info.local_rank)
         # hangs become errors instead of silent stalls
         os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
     if not dist.is_initialized():
@@ -91,8 +94,21 @@ def backend_name() -> str:
     return dist.get_backend() if is_initialized() else "none"
 
 
+def force_collectives() -> bool:
+    """``DGT_FORCE_COLLECTIVES=1``: issue every collective of the training paths even at world
+    size 1, so a one-GPU run executes the exact async RCCL code (streams, events, work handles,
+    in-graph communicator) that an N-GPU run takes.  Numerically a no-op (a 1-rank sum)."""
+    return os.environ.get("DGT_FORCE_COLLECTIVES", "0") not in ("", "0", "false", "False")
+
+
+def collectives_on(world_size: Optional[int] = None) -> bool:
+    """Whether the training paths issue their gradient / parameter collectives."""
+    ws = get_world_size() if world_size is None else world_size
+    return is_initialized() and (ws > 1 or force_collectives())
+
+
 def barrier() -> None:
-    if is_initialized() and get_world_size() > 1:
+    if collectives_on():
         if backend_name() == "nccl":
             dist.barrier(device_ids=[torch.cuda.current_device()])
         else:
@@ -113,7 +129,7 @@ def needs_host_staging(t: torch.Tensor) -> bool:
 
 
 def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
-    if is_initialized() and get_world_size() > 1:
+    if collectives_on():
         if needs_host_staging(t):
             c = t.detach().cpu()
             dist.broadcast(c, src)
@@ -124,7 +140,7 @@ def broadcast_(t: torch.Tensor, src: int = 0) -> torch.Tensor:
 
 
 def all_reduce_(t: torch.Tensor, op=dist.ReduceOp.SUM) -> torch.Tensor:
-    if is_initialized() and get_world_size() > 1:
+    if collectives_on():
         if needs_host_staging(t):
             c = t.detach().cpu()
             dist.all_reduce(c, op=op)

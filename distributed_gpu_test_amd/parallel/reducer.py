@@ -95,7 +95,7 @@ class GradReducer:
         else:
             view = src
         self.bytes_reduced += view.numel() * view.element_size()
-        if self.world_size == 1:
+        if not comm.collectives_on(self.world_size):
             if self.stage >= 1:
                 self.shard_grad[self.shard_offsets[bi]:self.shard_offsets[bi] + b.numel].copy_(view)
             return

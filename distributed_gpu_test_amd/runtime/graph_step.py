@@ -43,7 +43,7 @@ def supported(engine) -> Tuple[bool, str]:
         return False, "fp16 dynamic loss scaling decides on the host"
     if engine.ds_scheduler is not None or engine.lr_scheduler is not None:
         return False, "a learning-rate schedule changes the captured lr"
-    if engine.world_size > 1 and comm.backend_name() != "nccl":
+    if comm.collectives_on(engine.world_size) and comm.backend_name() != "nccl":
         return False, f"collectives in a graph need RCCL (backend is {comm.backend_name()})"
     return True, ""
 
@@ -58,7 +58,7 @@ class GraphedStep:
         self.warmup = warmup
         self.max_graphs = max_graphs
         self.rccl = None
-        if engine.world_size > 1:
+        if comm.collectives_on(engine.world_size):
             from ..parallel.rccl import RcclComm
             self.rccl = RcclComm(engine.device)
         # the Adam step counter the captured launch reads (the step number of THIS update, 1-based)
@@ -101,7 +101,7 @@ class GraphedStep:
         if clip <= 0:
             return None
         sq = grads.float().pow(2).sum() * (scale * scale)
-        if self.e.stage >= 1 and self.e.world_size > 1:
+        if self.e.stage >= 1 and self.rccl is not None:
             self.rccl.all_reduce(sq.reshape(1))
         return torch.clamp(clip / (sq.sqrt() + 1e-6), max=1.0).reshape(1).float()
 

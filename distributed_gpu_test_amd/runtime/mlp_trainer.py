@@ -58,6 +58,7 @@ import os
 import torch
 import torch.distributed as dist
 
+from ..accelerator import get_accelerator
 from ..models.synthetic_mlp import SyntheticMLP, synthetic_batch_data
 from ..ops.adam import adam_flat_, adam_matrix_t_
 from ..ops.gemm import gemm_nt, mlp_head, rowsum_bf16, transpose_bf16
@@ -91,11 +92,13 @@ class MLPTrainer:
         if schedule == "auto":  # measured (profiles/r1_mlp_schedule_ab.txt): see the module docstring
             schedule = "flat" if comm.get_world_size() == 1 else "overlap"
         self.matrix_t = os.environ.get("DGT_ADAM_MATRIX_T", "0") == "1"
-        self.device = device or torch.device("cuda", torch.cuda.current_device())
+        self.device = device or get_accelerator().device()
         self.model = model
         self.B, self.D, self.L, self.Din = batch_size, model.width, model.depth, model.in_features
         self.rank, self.world_size = comm.get_rank(), comm.get_world_size()
-        self.zero_stage = zero_stage if self.world_size > 1 else 0
+        # collectives run at N > 1, or at N = 1 under DGT_FORCE_COLLECTIVES (same code, 1-rank RCCL)
+        self.coll = comm.collectives_on(self.world_size)
+        self.zero_stage = zero_stage if self.coll else 0
         self.lr, self.betas, self.eps, self.weight_decay = lr, betas, eps, weight_decay
         self.global_steps = 0
         dev, ws = self.device, self.world_size
@@ -193,7 +196,7 @@ class MLPTrainer:
         self.Y = y.to(dev)
         self.n_batches = n_batches
         kind = "allreduce" if self.zero_stage == 0 else "reducescatter+allgather"
-        self.exchange = f"{comm.backend_name()}-{kind}-per-layer" if self.world_size > 1 else "none"
+        self.exchange = f"{comm.backend_name()}-{kind}-per-layer" if self.coll else "none"
 
         # ---- schedule: side streams + per-layer events (GPU only; CPU runs everything in order)
         self.schedule = schedule if dev.type == "cuda" else "serial"
@@ -250,7 +253,7 @@ class MLPTrainer:
             works.append(fn(out, *inp, async_op=True))
 
     def _reduce_layer(self, i: int, works: list) -> None:
-        if self.world_size == 1:
+        if not self.coll:
             return
         bucket = self.grads_w[self.w_off[i]:self.w_off[i] + self.w_len[i]]
         if self.zero_stage == 0:
@@ -338,7 +341,7 @@ class MLPTrainer:
             a_prevT = xT if i == 0 else self.aT[i]
             gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=self.grad_dtype == torch.float32)
             rowsum_bf16(self.gT[cur], self.gb[i])
-            if self.world_size > 1:
+            if self.coll:
                 if ov:
                     self.ev_wgrad[i].record(main)
                     self.s_comm.wait_event(self.ev_wgrad[i])
@@ -361,12 +364,12 @@ class MLPTrainer:
             if ov:
                 self.ev_bwd[i].record(main)
                 self.s_opt.wait_event(self.ev_bwd[i])
-                if self.world_size > 1:
+                if self.coll:
                     self.s_opt.wait_event(self.ev_comm[i])
                 with torch.cuda.stream(self.s_opt):
                     self._update_layer(i)
                     self.ev_opt[i].record(self.s_opt)
-        if self.world_size > 1:  # biases + head: one small replicated bucket
+        if self.coll:  # biases + head: one small replicated bucket
             self._collective(dist.all_reduce, self.grads_s, works=works)
         for w in works:
             w.wait()

@@ -27,6 +27,7 @@ from typing import Any, Dict, List, Optional
 import torch
 
 from .. import data as dgt_data
+from ..accelerator import get_accelerator
 from ..models.simple_net import SimpleNet, pack_simple_net, simple_net_layout, simple_net_numel
 from ..ops import _ext
 from ..ops.adam import adam_flat_
@@ -39,8 +40,12 @@ from .optim_state import adam_state_to_flat, flat_to_adam_state
 IMPLS = ("auto", "fused", "graph", "stepwise", "torch")
 
 
+class ReplicaDivergence(RuntimeError):
+    """Data-parallel replicas ended an epoch with different parameters (a corrupted exchange)."""
+
+
 def fused_supported(n_features: int, hidden: int, batch_size: int) -> bool:
-    if not (torch.cuda.is_available() and _ext.available()):
+    if not (get_accelerator().name == "hip" and _ext.available()):
         return False
     return bool(_ext.require().tiny_mlp_supported(n_features, hidden)) and batch_size <= 16
 
@@ -56,8 +61,7 @@ class TinyMLPTrainer:
         self.F = model.n_features
         self.H = model.hidden
         self.B = batch_size
-        self.device = device or (torch.device("cuda", torch.cuda.current_device())
-                                 if torch.cuda.is_available() else torch.device("cpu"))
+        self.device = device or get_accelerator().device()
         self.rank = comm.get_rank()
         self.world_size = comm.get_world_size()
         self.lr, self.betas, self.eps = float(lr), (float(betas[0]), float(betas[1])), float(eps)
@@ -84,8 +88,7 @@ class TinyMLPTrainer:
         flat = torch.zeros(self.padded, dtype=torch.float32)
         flat[: self.numel] = pack_simple_net(model)
         self.params = flat.to(self.device)
-        if self.world_size > 1:  # DeepSpeed broadcasts the model from rank 0 at initialize
-            comm.broadcast_(self.params, 0)
+        comm.broadcast_(self.params, 0)  # DeepSpeed broadcasts the model at initialize
         self.exp_avg = torch.zeros_like(self.params)
         self.exp_avg_sq = torch.zeros_like(self.params)
         self.grad = torch.zeros_like(self.params)
@@ -106,10 +109,6 @@ class TinyMLPTrainer:
                 self._auto_fallback = True
         self._graph = None
         self.rccl = None
-        self._ws = None
-        self._ws_key = None
-        if self.impl == "fused":
-            self.reserve(self.steps_per_epoch())
         if self.impl == "graph":
             try:
                 self._setup_graph()
@@ -136,13 +135,53 @@ class TinyMLPTrainer:
             ch = IpcChannel(max(need, self.padded), self.device, timeout_s=self.exchange_timeout_s)
         except Exception:
             return None
-        if not ch.selftest():
+        if not ch.selftest() or not self._exchange_selftest(ch):
             ch.close()
             return None
         return ch
 
+    def _exchange_selftest(self, ch, n_steps: int = 8, timeout_s: float = 10.0) -> bool:
+        """Drive the training kernel's OWN in-kernel exchange (not the stand-alone one-shot
+        all-reduce of ``IpcChannel.selftest``) for ``n_steps`` steps of this rank's first batches on
+        scratch copies of the state, then check (a) the kernel reported no timeout, (b) the result
+        matches the RCCL path (per-step gradient -> process-group all-reduce -> exact flat Adam)
+        within fp32 tolerance, and (c) every rank holds bit-identical parameters.  Every rank
+        issues the same collectives whatever happens, and all ranks agree on the verdict."""
+        ops = _ext.require()
+        plan, counts = self.epoch_plan(1)
+        plan, counts = plan[:n_steps].contiguous(), counts[:n_steps].contiguous()
+        n = int(plan.shape[0])
+        p = self.params.clone()
+        m, v = torch.zeros_like(p), torch.zeros_like(p)
+        loss = torch.zeros(1, dtype=torch.float64, device=self.device)
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        ok = True
+        try:
+            ops.tiny_mlp_train(self.x, self.y, plan, counts, p, m, v, loss, status, self.F, self.H, self.lr,
+                               self.betas[0], self.betas[1], self.eps, self.weight_decay, self.adamw, 0,
+                               ch.data_ptrs, self.rank, self.world_size, ch.stride, ch.next_seq(n),
+                               int(timeout_s * 100_000_000), -1)
+            torch.cuda.synchronize(self.device)
+            ok = int(status.item()) == 0
+        except Exception as e:
+            print(f"[dgt] in-kernel exchange self-test raised: {e}", flush=True)
+            ok = False
+        rp = self.params.clone()
+        rm, rv, g = torch.zeros_like(rp), torch.zeros_like(rp), torch.zeros_like(rp)
+        lacc = torch.zeros(1, dtype=torch.float64, device=self.device)
+        for s in range(n):  # unconditional: every rank issues the same collectives
+            ops.tiny_mlp_grad(self.x, self.y, plan, counts, s, rp, g, lacc, self.F, self.H)
+            comm.all_reduce_(g)
+            adam_flat_(rp, g, rm, rv, s + 1, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay,
+                       self.adamw, grad_scale=1.0 / self.world_size)
+        ok = ok and bool(torch.allclose(p, rp, rtol=1e-4, atol=1e-6))
+        ref = p.clone()
+        comm.broadcast_(ref, 0)
+        ok = ok and bool(torch.equal(p, ref))
+        return comm.all_reduce_max(0.0 if ok else 1.0) == 0.0
+
     def _setup_graph(self) -> None:
-        if self.world_size > 1:
+        if comm.collectives_on(self.world_size):
             if comm.backend_name() != "nccl":
                 raise RuntimeError("impl='graph' needs RCCL (one GPU per rank)")
             from ..parallel.rccl import RcclComm
@@ -194,25 +233,6 @@ class TinyMLPTrainer:
         return plan.to(self.device), counts.to(self.device)
 
     # ------------------------------------------------------------------ training
-    def reserve(self, n_steps: int) -> None:
-        """Size the fused kernel's per-launch workspace (Adam bias-correction table) for launches of
-        up to ``n_steps`` steps, so no allocation happens on the launch path."""
-        need = (max(int(n_steps), 1) + 1) * 2
-        if self.impl == "fused" and (self._ws is None or self._ws.numel() < need):
-            self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
-            self._ws_key = None
-
-    def prepare(self, n_steps: int) -> None:
-        """Precompute the Adam bias-correction schedule of the NEXT ``n_steps`` optimizer steps (a
-        pure function of the step numbers and lr / betas, like an LR-schedule table), so the next
-        ``run_plan`` of exactly that many steps launches one kernel instead of two."""
-        if self.impl != "fused" or n_steps < 1:
-            return
-        self.reserve(n_steps)
-        _ext.require().tiny_mlp_bias_table(self._ws, int(n_steps), self.global_steps, self.lr, self.betas[0],
-                                           self.betas[1])
-        self._ws_key = (self.global_steps, int(n_steps))
-
     def run_plan(self, plan: torch.Tensor, counts: torch.Tensor) -> None:
         """Run len(plan) optimizer steps (asynchronously on GPU); loss accumulates into loss_acc."""
         n = int(plan.shape[0])
@@ -222,16 +242,13 @@ class TinyMLPTrainer:
             ops = _ext.require()
             ch = self.channel
             seq = ch.next_seq(n) if ch is not None else 0
-            ready = self._ws_key == (self.global_steps, n)
-            self._ws_key = None
-            if not ready:
-                self.reserve(n)
+            # Adam's bias corrections of steps global_steps+1 .. +n are formed inside the kernel
             ops.tiny_mlp_train(self.x, self.y, plan, counts, self.params, self.exp_avg, self.exp_avg_sq,
                                self.loss_acc, self.status, self.F, self.H, self.lr, self.betas[0], self.betas[1],
                                self.eps, self.weight_decay, self.adamw, self.global_steps,
                                ch.data_ptrs if ch else [], self.rank,
                                self.world_size, ch.stride if ch else 0, seq,
-                               ch.timeout_ticks if ch else 0, self._ws, ready)
+                               ch.timeout_ticks if ch else 0, self.faults.corrupt_step())
             self.global_steps += n
         elif self.impl == "graph":
             self.step_dev.fill_(self.global_steps)
@@ -251,8 +268,7 @@ class TinyMLPTrainer:
             for s in range(n):
                 ops.tiny_mlp_grad(self.x, self.y, plan, counts, s, self.params, self.grad, self.loss_acc,
                                   self.F, self.H)
-                if self.world_size > 1:
-                    comm.all_reduce_(self.grad)
+                comm.all_reduce_(self.grad)  # no-op at world size 1 unless DGT_FORCE_COLLECTIVES
                 self.global_steps += 1
                 adam_flat_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, self.global_steps, self.lr,
                            self.betas[0], self.betas[1], self.eps, self.weight_decay, self.adamw,
@@ -264,8 +280,7 @@ class TinyMLPTrainer:
                 loss, g = tiny_mlp_step_reference(self.params, self.x[rows], self.y[rows], self.F, self.H,
                                                   grad_out=self.grad)
                 self.loss_acc += loss
-                if self.world_size > 1:
-                    comm.all_reduce_(self.grad)
+                comm.all_reduce_(self.grad)
                 self.global_steps += 1
                 adam_flat_reference_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, self.global_steps,
                                      self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay,
@@ -281,12 +296,25 @@ class TinyMLPTrainer:
                 raise RuntimeError(f"fused training kernel failed with status {st} "
                                    f"({'cross-GPU exchange timeout' if st == 1 else 'bad launch shape'})")
 
+    def verify_replicas(self) -> None:
+        """Raise ReplicaDivergence on EVERY rank unless all ranks hold bit-identical parameters
+        (data-parallel training keeps them identical; only a corrupted exchange breaks that)."""
+        if self.world_size == 1:
+            return
+        ref = self.params.clone()
+        comm.broadcast_(ref, 0)
+        bad = comm.all_reduce_max(0.0 if bool(torch.equal(self.params, ref)) else 1.0)
+        if bad > 0:
+            raise ReplicaDivergence(f"data-parallel replicas diverged by optimizer step {self.global_steps} "
+                                    f"(impl={self.impl}, exchange={self.exchange})")
+
     def run_epoch(self, epoch: int) -> float:
         plan, counts = self.epoch_plan(epoch)
         self.loss_acc.zero_()
         self.run_plan(plan, counts)
         loss_sum = float(self.loss_acc.item())  # the epoch's single host sync
         self.check()
+        self.verify_replicas()  # one 5.6 KB broadcast per epoch: silent corruption fails the job
         return loss_sum / max(1, int(plan.shape[0]))
 
     # ------------------------------------------------------------------ state

@@ -12,7 +12,10 @@ RANK may be ``*`` (every rank).  STEP is the global optimizer step after which t
   ``job_status.txt`` = fail;
 * ``abort`` — ``os.abort()``: a crash (signal), like a segfaulting worker;
 * ``hang``  — sleep forever: exercises the process-group / CI timeouts;
-* ``nan``   — poison the loss with NaN from that step on (the training must notice / skip).
+* ``nan``   — poison the loss with NaN from that step on (the training must notice / skip);
+* ``corrupt`` — the fused kernel's in-kernel xGMI gradient exchange sends rank RANK+1 one wrong
+  payload at step STEP (``csrc/tiny_mlp.hip``): a silent data corruption that only the per-epoch
+  replica check (``TinyMLPTrainer.verify_replicas``) can catch.  No effect on the RCCL paths.
 
 ``DGT_FAIL_ONCE=<path>`` makes the fault fire only while ``<path>`` does not exist (it is created
 just before firing): a restarted job (torchrun ``--max-restarts``) then runs through, which is how
@@ -28,7 +31,8 @@ from typing import Optional
 
 import torch
 
-MODES = ("exit", "abort", "hang", "nan")
+MODES = ("exit", "abort", "hang", "nan", "corrupt")
+PASSIVE = ("nan", "corrupt")  # modes that alter data instead of ending the process
 
 
 @dataclass
@@ -82,14 +86,20 @@ class FaultInjector:
                 time.sleep(3600)
 
     def maybe_fire(self, step: int) -> None:
-        if self._mine() and self.spec.step is not None and self.spec.mode != "nan" and step >= self.spec.step:
+        if self._mine() and self.spec.step is not None and self.spec.mode not in PASSIVE and step >= self.spec.step:
             self.fire()
 
     def maybe_fire_end(self) -> None:
-        if self._mine() and self.spec.step is None and self.spec.mode != "nan":
+        if self._mine() and self.spec.step is None and self.spec.mode not in PASSIVE:
             self.fire()
 
     def maybe_corrupt_loss(self, loss: torch.Tensor, step: int) -> torch.Tensor:
         if (self._mine() and self.spec.mode == "nan" and (self.spec.step is None or step >= self.spec.step)):
             return loss * float("nan")
         return loss
+
+    def corrupt_step(self) -> int:
+        """1-based optimizer step at which this rank corrupts an exchange payload (-1 = never)."""
+        if self._mine() and self.spec.mode == "corrupt" and self.spec.step is not None:
+            return int(self.spec.step)
+        return -1

@@ -15,7 +15,6 @@ torch.manual_seed(42)
 x, y = make_synthetic_data(2000, 20, 42)
 tr = TinyMLPTrainer(SimpleNet(20, 64), x, y, 4, impl="fused", device=dev)
 plan, counts = bench.build_plan(tr, 100000)
-tr.reserve(1000)
 def t(label, f, n=2000):
     for _ in range(50): f()
     torch.cuda.synchronize()
@@ -32,7 +31,7 @@ t("run_plan K=1", lambda: tr.run_plan(p1, c1), 500)
 ops = _ext.require()
 def old():
     ops.tiny_mlp_train(tr.x, tr.y, p1, c1, tr.params, tr.exp_avg, tr.exp_avg_sq, tr.loss_acc, tr.status, 20, 64,
-                       1e-3, 0.9, 0.999, 1e-8, 0.0, False, 0, [], 0, 1, 0, 0, 0, tr._ws, False)
+                       1e-3, 0.9, 0.999, 1e-8, 0.0, False, 0, [], 0, 1, 0, 0, 0)
 t("torch op tiny_mlp_train K=1", old, 500)
 t("synchronize (idle)", lambda: torch.cuda.synchronize())
 e = torch.cuda.Event(enable_timing=True)

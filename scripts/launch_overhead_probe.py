@@ -1,4 +1,4 @@
-"""Fixed cost of one timed fused run (after prepare): host launch, device span, sync wake-up."""
+"""Fixed cost of one timed fused run (bias corrections in-kernel): host launch, device span, sync wake-up."""
 import time, sys, os
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import torch
@@ -11,14 +11,12 @@ torch.manual_seed(42)
 x, y = make_synthetic_data(2000, 20, 42)
 tr = TinyMLPTrainer(SimpleNet(20, 64), x, y, 4, impl="fused", device=dev)
 plan, counts = bench.build_plan(tr, 100000)
-tr.reserve(1000)
 pos = 0
 for K in (1, 10, 100, 1000):
     rows = []
     for rep in range(6):
         p, c = plan[pos:pos + K], counts[pos:pos + K]
         pos += K
-        tr.prepare(K)
         torch.cuda.synchronize()
         s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0 = time.perf_counter()

@@ -31,7 +31,6 @@ torch.manual_seed(42)
 x, y = make_synthetic_data(2000, 20, 42)
 tr = TinyMLPTrainer(SimpleNet(20, 64), x, y, 4, impl="fused", device=dev)
 plan, counts = bench.build_plan(tr, 100000)
-tr.reserve(1000)
 z = torch.zeros(16, device=dev)
 
 
@@ -54,7 +53,6 @@ def trivial():
 t("trivial kernel + sync", trivial)
 for k in (1, 10, 100):
     pk, ck = plan[:k].contiguous(), counts[:k].contiguous()
-    tr.prepare(k)
 
     def fused(pk=pk, ck=ck):
         tr.run_plan(pk, ck)

@@ -1,0 +1,142 @@
+"""One-GPU worker for tests/test_gpu_force_collectives.py (and its rocprofv3 trace).
+
+Every N > 1 code path that talks to RCCL runs here at world size 1 with ``DGT_FORCE_COLLECTIVES=1``
+on the ``nccl`` backend (ProcessGroupNCCL of size 1 plus the native communicator), so the async
+work handles, side streams, events and in-graph collectives execute on real hardware before an
+8-GPU run does.  Each case runs twice — collectives off, then forced on — and must give bit-identical
+parameters (a 1-rank sum is the identity).  The number of collective calls of each forced run is
+counted through wrappers, so a case that silently skipped its collectives fails too.
+
+Prints one ``RESULT {json}`` line: case -> {"equal": bool, "calls": int}.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("DGT_QUIET", "1")
+
+import torch  # noqa: E402
+import torch.distributed as dist  # noqa: E402
+
+from distributed_gpu_test_amd.parallel import comm  # noqa: E402
+from distributed_gpu_test_amd.parallel import rccl as rccl_mod  # noqa: E402
+
+CALLS = {"n": 0}
+
+
+def _count(fn):
+    def wrapped(*a, **k):
+        CALLS["n"] += 1
+        return fn(*a, **k)
+    return wrapped
+
+
+for _name in ("all_reduce", "reduce_scatter_tensor", "all_gather_into_tensor", "broadcast"):
+    setattr(dist, _name, _count(getattr(dist, _name)))
+for _name in ("all_reduce", "reduce_scatter", "all_gather"):
+    setattr(rccl_mod.RcclComm, _name, _count(getattr(rccl_mod.RcclComm, _name)))
+
+
+def forced(flag: bool):
+    os.environ["DGT_FORCE_COLLECTIVES"] = "1" if flag else "0"
+
+
+def run_pair(fn):
+    out = []
+    for flag in (False, True):
+        forced(flag)
+        CALLS["n"] = 0
+        p = fn()
+        torch.cuda.synchronize()
+        out.append((p.detach().clone(), CALLS["n"]))
+    forced(False)
+    return {"equal": bool(torch.equal(out[0][0], out[1][0])), "calls": out[1][1], "calls_off": out[0][1]}
+
+
+def engine_case(stage, graph):
+    import distributed_gpu_test_amd as dgt
+
+    def fn():
+        torch.manual_seed(4)
+        m = torch.nn.Sequential(torch.nn.Linear(64, 256), torch.nn.ReLU(), torch.nn.Linear(256, 1))
+        cfg = {"train_batch_size": 32, "zero_optimization": {"stage": stage, "reduce_bucket_size": 4096},
+               "amd": {"hip_graph": graph}}
+        engine, _, _, _ = dgt.initialize(model=m, optimizer=torch.optim.Adam(m.parameters(), lr=1e-3), config=cfg)
+        crit = torch.nn.BCEWithLogitsLoss()
+        g = torch.Generator().manual_seed(5)
+        batches = [(torch.randn(32, 64, generator=g).cuda(), (torch.rand(32, 1, generator=g) > 0.5).float().cuda())
+                   for _ in range(8)]
+        if graph:
+            step = engine.graph_step(lambda bx, by: crit(engine(bx).float(), by))
+            assert engine.graphed is not None, engine.graph_fallback_reason
+            for x, y in batches:
+                step(x, y)
+        else:
+            for x, y in batches:
+                engine.backward(crit(engine(x).float(), y))
+                engine.step()
+        p = engine.store.param_buf.detach().clone()
+        engine.close()
+        return p
+    return fn
+
+
+def mlp_case(schedule, stage):
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
+
+    def fn():
+        torch.manual_seed(3)
+        tr = MLPTrainer(SyntheticMLP(width=256, depth=3), batch_size=128, n_batches=2, lr=1e-3,
+                        device=torch.device("cuda", 0), zero_stage=stage, schedule=schedule)
+        for s in range(5):
+            tr.step(s)
+        tr.join()
+        return tr.params.clone()
+    return fn
+
+
+def tiny_case(impl):
+    from distributed_gpu_test_amd.data import make_synthetic_data
+    from distributed_gpu_test_amd.models import SimpleNet
+    from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
+
+    def fn():
+        torch.manual_seed(42)
+        x, y = make_synthetic_data(2000, 20, 42)
+        tr = TinyMLPTrainer(SimpleNet(20, 64), x, y, 4, impl=impl, device=torch.device("cuda", 0))
+        plan, counts = tr.epoch_plan(1)
+        tr.run_plan(plan[:120], counts[:120])
+        p = tr.params.clone()
+        tr.close()
+        return p
+    return fn
+
+
+def main():
+    comm.init_distributed(backend="nccl")
+    assert comm.backend_name() == "nccl" and comm.get_world_size() == 1
+    only = set(sys.argv[1:])
+    cases = {}
+    for stage in (0, 1):
+        for graph in (False, True):
+            cases[f"engine_zero{stage}_{'graph' if graph else 'eager'}"] = engine_case(stage, graph)
+    for schedule in ("overlap", "serial", "flat"):
+        for stage in (0, 1):
+            cases[f"mlp_{schedule}_zero{stage}"] = mlp_case(schedule, stage)
+    for impl in ("graph", "stepwise"):
+        cases[f"tiny_{impl}"] = tiny_case(impl)
+    res = {}
+    for name, fn in cases.items():
+        if only and name not in only:
+            continue
+        res[name] = run_pair(fn)
+        print(f"[force] {name}: {res[name]}", file=sys.stderr, flush=True)
+    print("RESULT " + json.dumps(res), flush=True)
+    comm.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -68,9 +68,30 @@ def test_bench_two_ranks_one_gpu():
     import json
     line = [l for l in r.stdout.splitlines() if l.startswith("{")][-1]
     out = json.loads(line)
-    assert out["n_gpus"] == 2 and out["params_consistent_across_ranks"] is True
+    # two processes on one card: n_gpus counts physical devices, ranks counts processes
+    assert out["n_gpus"] == 1 and out["ranks"] == 2 and out["oversubscribed"] is True
+    assert out["params_consistent_across_ranks"] is True
     assert out["config"]["exchange"] == "ipc-oneshot-xgmi"
     print(line)
+
+
+def test_corrupted_exchange_fails_train_py(tmp_path):
+    """--fail-at 0:37:corrupt makes rank 0's fused kernel send rank 1 one wrong gradient payload at
+    step 37: training itself runs through, and the end-of-epoch replica check must fail the job."""
+    r = run(2, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", "--fail-at", "0:37:corrupt")
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert "replicas diverged" in r.stderr, r.stderr[-3000:]
+    assert "exchange=ipc-oneshot-xgmi" in r.stderr
+    assert "Training completed." not in r.stdout
+
+
+def test_corrupted_exchange_fails_bench():
+    """bench.py prints no headline when the ranks end with different parameters."""
+    r = run(2, "bench.py", "--gpus", "2", "--steps", "200", "--warmup", "20", "--no-sweep",
+            env={"DGT_FAIL_AT": "1:100:corrupt"})
+    assert r.returncode != 0, r.stdout[-2000:]  # bench exits 3; torchrun reports a failed worker as 1
+    assert not [l for l in r.stdout.splitlines() if l.startswith("{")]
+    assert "parameters differ across ranks" in r.stderr
 
 
 def test_oneshot_sweep_two_ranks_one_gpu():
@@ -121,6 +142,7 @@ def test_bench_eight_ranks_one_gpu():
     assert r.returncode == 0, r.stderr[-4000:]
     import json
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
-    assert out["n_gpus"] == 8 and out["params_consistent_across_ranks"] is True
+    assert out["n_gpus"] == 1 and out["ranks"] == 8 and out["oversubscribed"] is True
+    assert out["params_consistent_across_ranks"] is True
     assert out["config"]["exchange"] == "ipc-oneshot-xgmi"
     print(json.dumps(out))

@@ -148,26 +148,26 @@ def test_native_rccl_comm_single_rank():
     c.close()
 
 
-def test_prepared_bias_table_matches_inline():
-    """prepare(n) precomputes the bias-correction schedule; the next launch of n steps uses it and
-    must be bit-identical to a launch that fills the table itself."""
-    import torch
-    from distributed_gpu_test_amd.data import make_synthetic_data
-    from distributed_gpu_test_amd.models import SimpleNet
-    from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
+def test_in_kernel_bias_corrections_are_launch_split_invariant():
+    """The fused kernel forms Adam's bias corrections itself (an LDS ring refilled every T = 256
+    steps), so how the steps are split into launches must not change a single bit: one launch of
+    700 steps (crossing two ring refills) against launches of 1, 37, 255, 257 and 150 steps."""
     dev = torch.device("cuda", 0)
     outs = []
-    for prepared in (False, True):
-        torch.manual_seed(42)
-        x, y = make_synthetic_data(2000, 20, 42)
-        tr = TinyMLPTrainer(SimpleNet(20, 64), x, y, 4, impl="fused", device=dev)
-        plan, counts = tr.epoch_plan(1)
-        tr.run_plan(plan[:37], counts[:37])
-        if prepared:
-            tr.prepare(100)
-        tr.run_plan(plan[37:137], counts[37:137])
+    for cuts in ((700,), (1, 37, 255, 257, 150)):
+        x, y, m = _setup()
+        tr = TinyMLPTrainer(m, x, y, 4, impl="fused", device=dev)
+        p1, c1 = tr.epoch_plan(1)
+        p2, c2 = tr.epoch_plan(2)
+        plan, counts = torch.cat([p1, p2]), torch.cat([c1, c2])
+        s = 0
+        for n in cuts:
+            tr.run_plan(plan[s:s + n], counts[s:s + n])
+            s += n
         torch.cuda.synchronize()
+        tr.check()
         outs.append((tr.params.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(), float(tr.loss_acc.item())))
     for a, b in zip(outs[0][:3], outs[1][:3]):
         assert torch.equal(a, b)
-    assert outs[0][3] == outs[1][3]
+    # the loss log is a per-launch double sum: only its summation order depends on the split
+    assert abs(outs[0][3] - outs[1][3]) <= 1e-12 * abs(outs[0][3])

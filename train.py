@@ -32,6 +32,7 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 import distributed_gpu_test_amd as dgt  # noqa: E402
+from distributed_gpu_test_amd.accelerator import get_accelerator  # noqa: E402
 from distributed_gpu_test_amd.config import REFERENCE_DS_CONFIG, parse_config  # noqa: E402
 from distributed_gpu_test_amd.data import SyntheticDataset, make_synthetic_data  # noqa: E402
 from distributed_gpu_test_amd.models import SimpleNet  # noqa: E402
@@ -95,7 +96,7 @@ def main(argv=None) -> int:
     model = SimpleNet(n_features=x.shape[1], hidden=HIDDEN)
     optimizer = torch.optim.Adam(model.parameters(), lr=args.lr)
 
-    gpu = torch.cuda.is_available()
+    gpu = get_accelerator().name == "hip"
     impl = args.impl
     if impl == "auto":
         from distributed_gpu_test_amd.runtime.tiny_trainer import fused_supported
@@ -183,6 +184,11 @@ def main(argv=None) -> int:
 
 
 if __name__ == "__main__":
-    rc = main()
+    from distributed_gpu_test_amd.runtime.tiny_trainer import ReplicaDivergence
+    try:
+        rc = main()
+    except ReplicaDivergence as e:  # every rank raises it: a loud, non-zero job failure
+        print(f"[dgt] FATAL: {e}", file=sys.stderr, flush=True)
+        rc = 2
     comm.destroy()
     sys.exit(rc)
