@@ -12,9 +12,9 @@ cross-rank gradient reduction and optimizer update; nothing is cached or skipped
     torchrun --nproc-per-node N bench.py --gpus N    # N GPUs, one rank per GPU (RCCL/xGMI)
 
 The timed region of the fused path holds exactly one kernel launch that runs all K optimizer
-steps, including every step's Adam bias corrections (formed in double inside the kernel).  Before
-it, untimed: the W warmup steps and the sampler's index plan of the K steps (the DataLoader's work,
-uploaded once, as the trainer does once per epoch).
+steps, including every step's Adam bias corrections (formed in double by the kernel's prologue).
+Before it, untimed: the W warmup steps, the sampler's index plan of the K steps (the DataLoader's
+work, uploaded once, as the trainer does once per epoch) and the sizing of the kernel's workspace.
 
 ``n_gpus`` counts distinct physical devices (host + PCI address gathered over ranks); ``ranks`` is
 the process count and ``oversubscribed`` is true when ranks share a device.  A run whose ranks end
@@ -153,6 +153,8 @@ def timed_run(trainer, plan, counts, args, device, comm):
     """W untimed warmup steps, then exactly K timed steps between barrier + device syncs.
     Returns (max elapsed over ranks, mean loss over the timed steps).  Raises on every rank if the
     fused kernel failed on any rank."""
+    if hasattr(trainer, "reserve"):  # workspace sizing (allocation only) before anything is timed
+        trainer.reserve(max(args.warmup, args.steps))
     if args.warmup:
         # the last few warmup steps run as single-step launches: the launch path itself (HIP
         # runtime, dispatcher, Python) is then as warm for the timed launch as in steady state
@@ -169,17 +171,19 @@ def timed_run(trainer, plan, counts, args, device, comm):
     if comm.all_reduce_max(float(failed)) > 0:
         raise RuntimeError("warmup failed on some rank")
     trainer.loss_acc.zero_()
-    comm.barrier()
-    if device.type == "cuda":
+    barrier = comm.barrier if comm.collectives_on() else (lambda: None)  # a 1-rank barrier is a no-op
+    gpu = device.type == "cuda"
+    barrier()
+    if gpu:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     trainer.run_plan(timed_plan, timed_counts)
     t1 = time.perf_counter()
-    if device.type == "cuda":
+    if gpu:
         torch.cuda.synchronize()
     t2 = time.perf_counter()
-    comm.barrier()
-    if device.type == "cuda":
+    barrier()
+    if gpu:
         torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if os.environ.get("DGT_BENCH_BREAKDOWN"):

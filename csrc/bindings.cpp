@@ -86,7 +86,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
                     double lr, double beta1, double beta2, double eps, double weight_decay, bool adamw,
                     int64_t adam_step0, c10::ArrayRef<int64_t> data_ptrs,
                     int64_t rank, int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks,
-                    int64_t corrupt_step) {
+                    int64_t corrupt_step, const std::optional<at::Tensor>& workspace) {
   TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
               " H=", hidden);
   TORCH_CHECK(beta1 > 0.5 && beta1 < 1.0 && beta2 > 0.0 && beta2 < 1.0, "dgt: fused kernel needs 0.5 < beta1 < 1");
@@ -122,6 +122,18 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   a.beta1 = beta1;
   a.beta2 = beta2;
   a.adam_step0 = adam_step0;
+  // the kernel writes its steps' Adam bias corrections here (+1 row: the loop reads a step ahead);
+  // a caller-owned workspace keeps allocation (a hipMalloc on a cache miss) off the launch path
+  const int64_t bc_need = (plan.size(0) + 1) * 2;
+  at::Tensor bc;
+  if (workspace.has_value() && workspace->defined()) {
+    check_gpu(*workspace, "workspace", at::kFloat);
+    TORCH_CHECK(workspace->numel() >= bc_need, "dgt: tiny_mlp_train workspace needs ", bc_need, " floats");
+    bc = *workspace;
+  } else {
+    bc = at::empty({bc_need}, X.options());
+  }
+  a.bc = bc.data_ptr<float>();
   a.loss_acc = loss_acc.data_ptr<double>();
   a.status = status.data_ptr<int>();
   a.ex = make_exchange(data_ptrs, rank, world_size, stride, seq_base, timeout_ticks);
@@ -134,6 +146,100 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   if (a.n_steps == 0) return;
   DGT_CHECK_HIP(dgt::tiny_mlp_train((int)n_features, (int)hidden, a, stream_of(X)));
 }
+
+// ------------------------------------------------------------------------------ lean fused launcher
+// The per-epoch (and bench) launch of the fused trainer without the dispatcher: everything that is
+// fixed for a trainer (tensors, hyper-parameters, mailboxes, stream) is validated and packed ONCE
+// into a heap TinyTrainArgs; each launch then passes only the plan, the step count and the
+// sequence numbers through a plain C entry point (dgt_tiny_launch, called with ctypes), so the
+// host cost of a launch is hipLaunchKernel itself.
+struct TinyLauncher {
+  dgt::TinyTrainArgs a;
+  int f, h, device;
+  hipStream_t stream;
+};
+
+int64_t tiny_launcher_create(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& params,
+                             const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq, const at::Tensor& loss_acc,
+                             const at::Tensor& status, int64_t n_features, int64_t hidden, double lr, double beta1,
+                             double beta2, double eps, double weight_decay, bool adamw,
+                             c10::ArrayRef<int64_t> data_ptrs, int64_t rank, int64_t world_size, int64_t stride,
+                             int64_t timeout_ticks, int64_t corrupt_step) {
+  TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
+              " H=", hidden);
+  TORCH_CHECK(beta1 > 0.5 && beta1 < 1.0 && beta2 > 0.0 && beta2 < 1.0, "dgt: fused kernel needs 0.5 < beta1 < 1");
+  check_gpu(X, "X", at::kFloat);
+  check_gpu(Y, "Y", at::kFloat);
+  check_gpu(params, "params", at::kFloat);
+  check_gpu(exp_avg, "exp_avg", at::kFloat);
+  check_gpu(exp_avg_sq, "exp_avg_sq", at::kFloat);
+  check_gpu(loss_acc, "loss_acc", at::kDouble);
+  check_gpu(status, "status", at::kInt);
+  const int64_t pp = dgt::tiny_mlp_padded_numel((int)n_features, (int)hidden);
+  TORCH_CHECK(params.numel() >= pp && exp_avg.numel() >= pp && exp_avg_sq.numel() >= pp,
+              "dgt: flat buffers need ", pp, " elements");
+  TORCH_CHECK(X.dim() == 2 && X.size(1) == n_features, "dgt: X must be [N, ", n_features, "]");
+  TORCH_CHECK(Y.numel() == X.size(0), "dgt: Y must have one label per row of X");
+  if (world_size > 1) {
+    const int64_t need = dgt::tiny_mlp_exchange_floats((int)n_features, (int)hidden);
+    TORCH_CHECK(stride >= need && stride % 4 == 0, "dgt: mailbox stride ", stride, " < ", need);
+  }
+  auto* L = new TinyLauncher();
+  std::memset(&L->a, 0, sizeof(L->a));
+  L->a.X = X.data_ptr<float>();
+  L->a.Y = Y.data_ptr<float>();
+  L->a.params = params.data_ptr<float>();
+  L->a.exp_avg = exp_avg.data_ptr<float>();
+  L->a.exp_avg_sq = exp_avg_sq.data_ptr<float>();
+  L->a.hp = make_hyper(lr, beta1, beta2, eps, weight_decay, adamw);
+  L->a.lr = lr;
+  L->a.beta1 = beta1;
+  L->a.beta2 = beta2;
+  L->a.loss_acc = loss_acc.data_ptr<double>();
+  L->a.status = status.data_ptr<int>();
+  L->a.ex = make_exchange(data_ptrs, rank, world_size, stride, 0, timeout_ticks);
+  L->a.ex.corrupt_step = corrupt_step;
+  L->a.stamps = nullptr;
+  L->f = (int)n_features;
+  L->h = (int)hidden;
+  L->device = (int)X.device().index();
+  L->stream = stream_of(X);
+  return reinterpret_cast<int64_t>(L);
+}
+
+void tiny_launcher_destroy(int64_t handle) { delete reinterpret_cast<TinyLauncher*>(handle); }
+
+}  // namespace
+
+// C entry points (ctypes): the per-launch arguments only.  ``workspace`` holds >= 2 (n_steps + 1)
+// floats (the caller sizes it).  Returns a hipError_t (0 = launched).
+extern "C" int dgt_tiny_launch(int64_t handle, int64_t plan, int64_t counts, int n_steps, int bmax,
+                               long long step0, long long seq_base, int64_t workspace) {
+  auto* L = reinterpret_cast<TinyLauncher*>(handle);
+  if (!L || !plan || !counts || !workspace || n_steps < 0 || bmax < 1 || bmax > 16) return (int)hipErrorInvalidValue;
+  if (n_steps == 0) return 0;
+  int cur = -1;
+  if (hipGetDevice(&cur) != hipSuccess) return (int)hipErrorInvalidDevice;
+  if (cur != L->device && hipSetDevice(L->device) != hipSuccess) return (int)hipErrorInvalidDevice;
+  dgt::TinyTrainArgs a = L->a;
+  a.plan = reinterpret_cast<const int*>(plan);
+  a.counts = reinterpret_cast<const int*>(counts);
+  a.n_steps = n_steps;
+  a.bmax = bmax;
+  a.adam_step0 = step0;
+  a.bc = reinterpret_cast<float*>(workspace);
+  a.ex.seq_base = seq_base;
+  const hipError_t e = dgt::tiny_mlp_train(L->f, L->h, a, L->stream);
+  if (cur != L->device) (void)hipSetDevice(cur);
+  return (int)e;
+}
+
+// Re-target a launcher at another HIP stream (the caller's current stream changed).
+extern "C" void dgt_tiny_launcher_set_stream(int64_t handle, int64_t stream) {
+  reinterpret_cast<TinyLauncher*>(handle)->stream = reinterpret_cast<hipStream_t>(stream);
+}
+
+namespace {
 
 // ------------------------------------------------------------------------------ fused BCE loss
 void linear_fwd(const at::Tensor& x, const at::Tensor& W, const std::optional<at::Tensor>& b, const at::Tensor& y,
@@ -510,8 +616,16 @@ TORCH_LIBRARY(dgt, m) {
       "tiny_mlp_train(Tensor X, Tensor Y, Tensor plan, Tensor counts, Tensor(a!) params, Tensor(b!) exp_avg, "
       "Tensor(c!) exp_avg_sq, Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, "
       "float beta1, float beta2, float eps, float weight_decay, bool adamw, int adam_step0, int[] data_ptrs, "
-      "int rank, int world_size, int stride, int seq_base, int timeout_ticks, int corrupt_step=-1) -> ()",
+      "int rank, int world_size, int stride, int seq_base, int timeout_ticks, int corrupt_step=-1, "
+      "Tensor(f!)? workspace=None) -> ()",
       &tiny_mlp_train);
+  m.def(
+      "tiny_launcher_create(Tensor X, Tensor Y, Tensor(a!) params, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, "
+      "Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, float beta1, float beta2, "
+      "float eps, float weight_decay, bool adamw, int[] data_ptrs, int rank, int world_size, int stride, "
+      "int timeout_ticks, int corrupt_step) -> int",
+      &tiny_launcher_create);
+  m.def("tiny_launcher_destroy(int handle) -> ()", &tiny_launcher_destroy);
   m.def(
       "tiny_mlp_grad(Tensor X, Tensor Y, Tensor plan, Tensor counts, int step, Tensor params, Tensor(a!) grad, "
       "Tensor(b!) loss_acc, int n_features, int hidden) -> ()",

@@ -26,7 +26,8 @@ struct TinyTrainArgs {
   AdamHyper hp;
   double lr;             // python-double lr (bias-corrected step size is formed in double)
   double beta1, beta2;
-  long long adam_step0;  // optimizer steps already taken before this launch (bias corrections in-kernel)
+  long long adam_step0;  // optimizer steps already taken before this launch
+  float* bc;             // [n_steps + 1][2] workspace: the kernel fills it with its steps' bias corrections
   double* loss_acc;      // += sum over steps of the step's mean loss
   int* status;           // Status
   Exchange ex;           // world_size 1 -> no exchange

@@ -70,6 +70,9 @@ int main(int argc, char** argv) {
   a.loss_acc = dLoss; a.status = dStatus;
   a.ex.rank = 0; a.ex.world_size = 1;
   a.stamps = dStamps;
+  float* dBc;
+  CK(hipMalloc(&dBc, (size_t)(steps + 1) * 2 * sizeof(float)));  // +1: read-ahead of the kernel
+  a.bc = dBc;
   CK(dgt::tiny_mlp_train(F, H, a, 0));
   CK(hipDeviceSynchronize());
   hipEvent_t e0, e1;

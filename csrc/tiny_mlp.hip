@@ -31,11 +31,11 @@
 //     until every peer's tags match and sums the contributions in rank order, so every rank
 //     applies bit-identical updates.  This replaces DeepSpeed's flatten -> NCCL all_reduce ->
 //     scale -> unflatten.
-//   * Adam's bias corrections are formed IN the kernel, in double with torch's formula, T steps at
-//     a time (one step per thread) into a double-buffered LDS ring: the prologue fills steps
-//     0..T-1 (binary exponentiation), and the first step of every T-block fills the next block after its barrier
-//     (beta^t advanced by one multiply with beta^T).  The loop reads one wave-uniform float2 per
-//     step; nothing is precomputed before the launch.
+//   * Adam's bias corrections of every step of the launch are formed by the kernel itself, in its
+//     prologue (one step per thread, in double with torch's formula, beta^t advanced by one
+//     multiply per T steps), into a caller-owned workspace that the loop then reads one step ahead
+//     through the scalar cache: no double math and no extra basic block in the loop (an LDS ring
+//     refilled inside the loop measured 0.80-0.86 us/step against 0.75, profiles/r2_tiny_bias_ab.txt).
 // Reference: train.py:26-36 (model), 96 (loss), 98-117 (loop), 113 (all-reduce), 114 (Adam step).
 #include "dgt_common.h"
 #include "dgt_kernels.h"
@@ -106,7 +106,6 @@ struct __attribute__((aligned(16))) TinySmem {
   WaveSmem<F, H> w[C::NW];
   double loss[C::NW];        // per-wave deferred-loss totals, summed in wave order at the end
   float Z[2][C::NW * 16];    // per-wave partial logits, double-buffered by step parity
-  float2 bc[2][C::T];        // Adam bias corrections {-lr/(1-b1^t), 1/sqrt(1-b2^t)}: ring of 2 T-step blocks
   int err;
 };
 
@@ -300,12 +299,23 @@ DGT_DEVICE double ipow(double b, long long n) {
   return r;
 }
 
-// Bias-correction ring of one thread: it owns launch steps base + t (one per T-step block) and
-// carries beta^(its optimizer step) in double, advanced by beta^T per block (one multiply).
-struct BiasRing {
-  double b1p, b2p;  // beta1^t, beta2^t of this thread's current entry
-  double b1T, b2T;  // beta1^T, beta2^T
-};
+// Prologue: bc[2s], bc[2s+1] = bias corrections of launch step s (optimizer step step0 + s + 1) for
+// every s < n_steps; thread t fills s = t, t + T, ... carrying beta^(step) in double.  The stores are
+// drained before the prologue barrier, so the loop's scalar loads (K$ misses: the scalar cache
+// holds none of these lines yet in this dispatch) read them from L2.
+template <int T>
+DGT_DEVICE void fill_bias_table(const TinyTrainArgs& a, int t) {
+  if (t >= a.n_steps) return;
+  double b1p = ipow(a.beta1, a.adam_step0 + t + 1), b2p = ipow(a.beta2, a.adam_step0 + t + 1);
+  const double b1T = ipow(a.beta1, T), b2T = ipow(a.beta2, T);
+  for (int s = t; s < a.n_steps; s += T) {
+    const float2 bc = adam_bias_pair(b1p, b2p, a.lr);
+    a.bc[2 * s] = bc.x;
+    a.bc[2 * s + 1] = bc.y;
+    b1p *= b1T;
+    b2p *= b2T;
+  }
+}
 
 // ------------------------------------------------------------------ persistent training kernel
 // NP > 1: the exchange is compiled in (for up to NP ranks).  The single-rank kernel has no exchange
@@ -336,22 +346,20 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   for (int i = l; i < C::BM * C::SX; i += 64) ws.X[i] = 0.f;
   for (int i = l; i < C::BM * 17; i += 64) ws.DH[i] = 0.f;
   if (t == 0) sm.err = 0;
-  BiasRing ring;  // bias corrections of launch steps 0 .. T-1 (thread t: optimizer step step0 + t + 1)
-  ring.b1p = ipow(a.beta1, a.adam_step0 + t + 1);
-  ring.b2p = ipow(a.beta2, a.adam_step0 + t + 1);
-  ring.b1T = ipow(a.beta1, C::T);
-  ring.b2T = ipow(a.beta2, C::T);
-  if (t < a.n_steps) sm.bc[0][t] = adam_bias_pair(ring.b1p, ring.b2p, a.lr);
   float x[C::NSP], y, xn[C::NSP], yn;
   load_rows<F, H>(a.X, a.Y, plan_at(a.plan, a.n_steps, a.bmax, 0, lr), lq, x, y);
   int idx_next = plan_at(a.plan, a.n_steps, a.bmax, 1, lr);
   int idx_next2 = plan_at(a.plan, a.n_steps, a.bmax, 2, lr);
+  fill_bias_table<C::T>(a, t);
+  __builtin_amdgcn_s_waitcnt(0);  // the table's stores have reached L2 before any wave reads it
   __syncthreads();
 
   double loss_total = 0.0;
   float zs = 0.f, ys = 0.f, ibs = 0.f;  // deferred-loss ring (wave 0)
   const float inv_ws = 1.0f / (float)ex.world_size;
-  constexpr int LOG_T = __builtin_ctz(C::T);  // T = 64 * NW is a power of two
+  // Adam bias corrections of the current step, loaded a step ahead: the scalar load of step s+1's
+  // pair is in flight during step s (a K$ miss every 8th step otherwise stalled the Adam section)
+  float bc_ss = load_uniform(a.bc), bc_ib = load_uniform(a.bc + 1);
 #ifdef DGT_TINY_STAMPS
   unsigned long long st_acc[6] = {0, 0, 0, 0, 0, 0}, st_last = 0;
 #endif
@@ -359,10 +367,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(0);
     const int Bt = load_uniform(a.counts + s);
     const float invB = __builtin_amdgcn_rcpf((float)Bt);
-    // this step's bias corrections (wave-uniform LDS broadcast, consumed by the Adam section).  The
-    // entry was written at least one barrier ago: in the prologue, or after the barrier of step
-    // s - T (the first step of the previous block)
-    const float2 bcv = sm.bc[(s >> LOG_T) & 1][s & (C::T - 1)];
+    const float bc_ss_next = load_uniform(a.bc + 2 * s + 2), bc_ib_next = load_uniform(a.bc + 2 * s + 3);
     // prefetch step s+1 rows into registers; consumed by the next step's forward
     load_rows<F, H>(a.X, a.Y, idx_next, lq, xn, yn);
     // sampler index of step s+3, issued now so the end-of-step rotation never waits on it
@@ -497,8 +502,10 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     }
     DGT_STAMP(4);
 
-    // ---- Adam with this step's bias corrections
-    const float step_size_neg = bcv.x, inv_bc2_sqrt = bcv.y;
+    // ---- Adam; bias corrections of this step from the table (wave-uniform, prefetched)
+    const float step_size_neg = bc_ss, inv_bc2_sqrt = bc_ib;
+    bc_ss = bc_ss_next;
+    bc_ib = bc_ib_next;
     // two parameters per packed-fp32 update (W2 and b2 form the last pair)
 #pragma unroll
     for (int i = 0; i < C::NSP; i += 2) {
@@ -522,14 +529,6 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
       st.mb2 = m.y;
       st.vbw = v.x;
       st.vb2 = v.y;
-    }
-    // first step of a block: fill the other ring buffer with the next block.  Every wave is past
-    // this step's barrier, so all reads of that buffer (the previous block, last read at step s - 1)
-    // are done; its first reader (step s + T) is at least one barrier away.
-    if ((s & (C::T - 1)) == 0 && s + C::T < a.n_steps) {
-      ring.b1p *= ring.b1T;
-      ring.b2p *= ring.b2T;
-      if (s + C::T + t < a.n_steps) sm.bc[((s >> LOG_T) + 1) & 1][t] = adam_bias_pair(ring.b1p, ring.b2p, a.lr);
     }
     // rotate the prefetch pipeline
 #pragma unroll
@@ -631,6 +630,7 @@ int tiny_mlp_exchange_floats(int f, int h) {
 }
 
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
+  if (!a.bc) return hipErrorInvalidValue;
   const bool wd = a.hp.weight_decay != 0.f;
 #define DGT_TINY_LAUNCH_NP(F_, H_, SB, NP_)                                                      \
   do {                                                                                      \

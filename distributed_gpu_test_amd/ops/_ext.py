@@ -48,5 +48,25 @@ def require():
     return torch.ops.dgt
 
 
+_clib = None
+
+
+def c_lib():
+    """The same library through ctypes, for the dispatcher-free launch entry points
+    (``dgt_tiny_launch``: a launch costs hipLaunchKernel, not a boxed op call)."""
+    global _clib
+    if _clib is None:
+        require()
+        import ctypes
+        lib = ctypes.CDLL(LIB_PATH)
+        i64, i32 = ctypes.c_int64, ctypes.c_int
+        lib.dgt_tiny_launch.argtypes = [i64, i64, i64, i32, i32, ctypes.c_longlong, ctypes.c_longlong, i64]
+        lib.dgt_tiny_launch.restype = i32
+        lib.dgt_tiny_launcher_set_stream.argtypes = [i64, i64]
+        lib.dgt_tiny_launcher_set_stream.restype = None
+        _clib = lib
+    return _clib
+
+
 def gpu_available() -> bool:
     return torch.cuda.is_available()

@@ -40,6 +40,10 @@ from .optim_state import adam_state_to_flat, flat_to_adam_state
 IMPLS = ("auto", "fused", "graph", "stepwise", "torch")
 
 
+def _raw_stream(index: int) -> int:
+    return torch._C._cuda_getCurrentRawStream(index)
+
+
 class ReplicaDivergence(RuntimeError):
     """Data-parallel replicas ended an epoch with different parameters (a corrupted exchange)."""
 
@@ -109,6 +113,11 @@ class TinyMLPTrainer:
                 self._auto_fallback = True
         self._graph = None
         self.rccl = None
+        self._lh = None  # lean fused launcher (created on the first fused launch)
+        self._lh_stream = None
+        self._ws = None  # the fused kernel's bias-correction workspace (it fills it itself)
+        if self.impl == "fused":
+            self.reserve(self.steps_per_epoch())
         if self.impl == "graph":
             try:
                 self._setup_graph()
@@ -238,17 +247,30 @@ class TinyMLPTrainer:
         n = int(plan.shape[0])
         if n == 0:
             return
-        if self.impl == "fused":
+        if self.impl == "fused" and self._lean_ok(plan, counts, n):
+            # Adam's bias corrections of steps global_steps+1 .. +n are formed inside the kernel
+            ch = self.channel
+            seq = ch.next_seq(n) if ch is not None else 0
+            stream = _raw_stream(self.device.index)
+            if stream != self._lh_stream:
+                self._clib.dgt_tiny_launcher_set_stream(self._lh, stream)
+                self._lh_stream = stream
+            self.reserve(n)
+            rc = self._clib.dgt_tiny_launch(self._lh, plan.data_ptr(), counts.data_ptr(), n, plan.shape[1],
+                                            self.global_steps, seq, self._ws_ptr)
+            if rc != 0:
+                raise RuntimeError(f"dgt: fused training kernel launch failed (hipError {rc})")
+            self.global_steps += n
+        elif self.impl == "fused":  # the validating op path (it raises on a malformed plan)
             ops = _ext.require()
             ch = self.channel
             seq = ch.next_seq(n) if ch is not None else 0
-            # Adam's bias corrections of steps global_steps+1 .. +n are formed inside the kernel
             ops.tiny_mlp_train(self.x, self.y, plan, counts, self.params, self.exp_avg, self.exp_avg_sq,
                                self.loss_acc, self.status, self.F, self.H, self.lr, self.betas[0], self.betas[1],
                                self.eps, self.weight_decay, self.adamw, self.global_steps,
                                ch.data_ptrs if ch else [], self.rank,
                                self.world_size, ch.stride if ch else 0, seq,
-                               ch.timeout_ticks if ch else 0, self.faults.corrupt_step())
+                               ch.timeout_ticks if ch else 0, self.faults.corrupt_step(), self._ws)
             self.global_steps += n
         elif self.impl == "graph":
             self.step_dev.fill_(self.global_steps)
@@ -287,6 +309,40 @@ class TinyMLPTrainer:
                                      self.adamw, grad_scale=1.0 / self.world_size)
         self.global_samples += n * self.B * self.world_size
         self.faults.maybe_fire(self.global_steps)
+
+    def reserve(self, n_steps: int) -> None:
+        """Size the fused kernel's workspace for launches of up to ``n_steps`` steps (the kernel fills
+        it with its own steps' Adam bias corrections; this is allocation only, no per-step work)."""
+        need = (max(int(n_steps), 1) + 1) * 2
+        if self.impl == "fused" and (self._ws is None or self._ws.numel() < need):
+            self._ws = torch.empty(need, dtype=torch.float32, device=self.device)
+            self._ws_ptr = self._ws.data_ptr()
+
+    def _lean_ok(self, plan: torch.Tensor, counts: torch.Tensor, n: int) -> bool:
+        """Whether this launch can take the dispatcher-free path: a well-formed device plan (the
+        launcher itself was validated once, at creation)."""
+        if not (plan.is_cuda and plan.dtype == torch.int32 and plan.dim() == 2 and plan.is_contiguous()
+                and counts.is_cuda and counts.dtype == torch.int32 and counts.is_contiguous()
+                and counts.numel() == n and 1 <= plan.shape[1] <= 16):
+            return False
+        if self._lh is None:
+            ch = self.channel
+            self._lh = int(_ext.require().tiny_launcher_create(
+                self.x, self.y, self.params, self.exp_avg, self.exp_avg_sq, self.loss_acc, self.status, self.F,
+                self.H, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.adamw,
+                ch.data_ptrs if ch else [], self.rank, self.world_size, ch.stride if ch else 0,
+                ch.timeout_ticks if ch else 0, self.faults.corrupt_step()))
+            self._lh_stream = _raw_stream(self.device.index)  # the launcher was bound to it
+            self._clib = _ext.c_lib()
+        return True
+
+    def _drop_launcher(self) -> None:
+        if getattr(self, "_lh", None):
+            try:
+                _ext.require().tiny_launcher_destroy(self._lh)
+            except Exception:
+                pass
+        self._lh = None
 
     def check(self) -> None:
         """Raise if a kernel reported a failure (cross-GPU timeout, bad shape)."""
@@ -362,6 +418,7 @@ class TinyMLPTrainer:
         self._graph = None
 
     def close(self) -> None:
+        self._drop_launcher()  # holds the mailbox pointers: before the channel goes
         if self.channel is not None:
             self.channel.close()
             self.channel = None

@@ -1,4 +1,5 @@
-"""Host-side costs of one timed run of the fused kernel (torch op dispatch, stream lookup, synchronize)."""
+"""Host-side costs of one timed run of the fused kernel (lean launcher vs torch op dispatch, stream lookup,
+synchronize).  NOTE: the raw launches below keep re-running step 0 on the trainer's state."""
 import os
 import sys
 import time
@@ -27,7 +28,13 @@ p1, c1 = plan[:1].contiguous(), counts[:1].contiguous()
 t("current_stream().cuda_stream", lambda: torch.cuda.current_stream(dev).cuda_stream)
 t("slice plan[1:]", lambda: plan[1:])
 s = torch.cuda.current_stream(dev).cuda_stream
-t("run_plan K=1", lambda: tr.run_plan(p1, c1), 500)
+t("run_plan K=1 (lean ctypes launcher)", lambda: tr.run_plan(p1, c1), 500)
+from distributed_gpu_test_amd.runtime.tiny_trainer import _raw_stream
+t("_raw_stream", lambda: _raw_stream(0))
+t("_lean_ok checks", lambda: tr._lean_ok(p1, c1, 1))
+lib, lh = _ext.c_lib(), tr._lh
+pp, cp = p1.data_ptr(), c1.data_ptr()
+t("dgt_tiny_launch (raw ctypes call)", lambda: lib.dgt_tiny_launch(lh, pp, cp, 1, 4, 0, 0), 500)
 ops = _ext.require()
 def old():
     ops.tiny_mlp_train(tr.x, tr.y, p1, c1, tr.params, tr.exp_avg, tr.exp_avg_sq, tr.loss_acc, tr.status, 20, 64,

@@ -169,5 +169,6 @@ def test_in_kernel_bias_corrections_are_launch_split_invariant():
         outs.append((tr.params.clone(), tr.exp_avg.clone(), tr.exp_avg_sq.clone(), float(tr.loss_acc.item())))
     for a, b in zip(outs[0][:3], outs[1][:3]):
         assert torch.equal(a, b)
-    # the loss log is a per-launch double sum: only its summation order depends on the split
-    assert abs(outs[0][3] - outs[1][3]) <= 1e-12 * abs(outs[0][3])
+    # the loss log folds 4-step groups in fp32 (deferred ring, aligned to the launch start) into a
+    # double: only the grouping depends on the split
+    assert abs(outs[0][3] - outs[1][3]) <= 1e-6 * abs(outs[0][3])
