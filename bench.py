@@ -64,6 +64,8 @@ def parse_args(argv=None):
     ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
                     help="mlp: 0 = all-reduce the weight gradients; 1 = reduce-scatter them, shard Adam, "
                          "all-gather bf16 weights (ZeRO-1/2)")
+    ap.add_argument("--comm-dtype", default=None, choices=["bf16", "fp32"],
+                    help="mlp: gradient wire dtype (DeepSpeed communication_data_type; default bf16)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce bus bandwidth sweep")
     ap.add_argument("--sweep-max-mb", type=int, default=256)
     return ap.parse_known_args(argv)[0]
@@ -253,7 +255,9 @@ def main(argv=None):
         if args.impl == "engine":
             trainer = TorchMLPBench(model, B, device)
         else:
-            trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device, zero_stage=args.zero_stage)
+            cdt = {None: None, "bf16": torch.bfloat16, "fp32": torch.float32}[args.comm_dtype]
+            trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device, zero_stage=args.zero_stage,
+                                 comm_dtype=cdt)
     elif args.impl == "engine":
         trainer = EngineBench(model, x, y, B, device)
     elif args.impl == "dgt-engine":

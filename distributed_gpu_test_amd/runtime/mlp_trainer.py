@@ -37,7 +37,12 @@ Parameters live in two flat regions:
 * the big region — the L weight matrices, bf16 for compute + gradients (bf16 by default, as
   PyTorch autocast's matmul backward produces them: half the wgrad store, Adam read and
   collective bytes; ``grad_dtype=torch.float32`` / ``DGT_MLP_GRAD_DTYPE=fp32`` keeps fp32), each
-  matrix padded to a multiple of 64 * world_size elements (a per-layer communication bucket);
+  matrix padded to a multiple of 64 * world_size elements (a per-layer communication bucket).
+  The collectives carry the gradient buffer itself, so the wire dtype IS the gradient dtype:
+  ``comm_dtype=torch.float32`` (DeepSpeed's ``communication_data_type``) selects fp32 gradients.
+  An 8-rank bf16 sum adds 3.7e-3 relative RMS error against 1.7e-3 for the bf16 rounding of
+  the gradient itself (tests/test_multiproc_cpu.py::test_bf16_gradient_wire_error_eight_ranks),
+  so bf16 stays the default wire;
 * the small region — biases and the head, fp32 (the GEMM epilogues read fp32 biases), replicated
   on every rank and all-reduced as one bucket.
 
@@ -78,11 +83,18 @@ class MLPTrainer:
     def __init__(self, model: SyntheticMLP, batch_size: int = 1024, n_batches: int = 8, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 1234,
                  device: Optional[torch.device] = None, zero_stage: int = 0, schedule: Optional[str] = None,
-                 grad_dtype: Optional[torch.dtype] = None):
+                 grad_dtype: Optional[torch.dtype] = None, comm_dtype: Optional[torch.dtype] = None):
         if zero_stage not in (0, 1):
             raise ValueError("MLPTrainer supports zero_stage 0 or 1")
+        if comm_dtype not in (None, torch.bfloat16, torch.float32):
+            raise ValueError("comm_dtype must be torch.bfloat16 or torch.float32")
         if grad_dtype is None:
             grad_dtype = {"bf16": torch.bfloat16, "fp32": torch.float32}[os.environ.get("DGT_MLP_GRAD_DTYPE", "bf16")]
+        if comm_dtype is not None and comm_dtype != grad_dtype:
+            # DeepSpeed's communication_data_type: the collectives carry the gradient buffer itself,
+            # so an fp32 wire means fp32 gradients straight out of the wgrad epilogue (no cast pass);
+            # a bf16 wire with fp32 gradients would only add rounding
+            grad_dtype = comm_dtype
         if grad_dtype not in (torch.bfloat16, torch.float32):
             raise ValueError("grad_dtype must be torch.bfloat16 or torch.float32")
         self.grad_dtype = grad_dtype

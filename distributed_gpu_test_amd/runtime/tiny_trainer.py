@@ -34,6 +34,7 @@ from ..ops.adam import adam_flat_
 from ..ops.reference import adam_flat_reference_, tiny_mlp_step_reference
 from ..parallel import comm
 from . import checkpoint as ckpt
+from ..utils import tracing
 from ..utils.fault import FaultInjector
 from .optim_state import adam_state_to_flat, flat_to_adam_state
 
@@ -367,10 +368,13 @@ class TinyMLPTrainer:
     def run_epoch(self, epoch: int) -> float:
         plan, counts = self.epoch_plan(epoch)
         self.loss_acc.zero_()
-        self.run_plan(plan, counts)
-        loss_sum = float(self.loss_acc.item())  # the epoch's single host sync
-        self.check()
-        self.verify_replicas()  # one 5.6 KB broadcast per epoch: silent corruption fails the job
+        with tracing.range(f"dgt.{self.impl}.epoch{epoch}"):  # the fused path: ONE kernel launch
+            self.run_plan(plan, counts)
+        with tracing.range("dgt.epoch_sync"):
+            loss_sum = float(self.loss_acc.item())  # the epoch's single host sync
+            self.check()
+        with tracing.range("dgt.replica_check"):
+            self.verify_replicas()  # one 5.6 KB broadcast per epoch: silent corruption fails the job
         return loss_sum / max(1, int(plan.shape[0]))
 
     # ------------------------------------------------------------------ state

@@ -35,9 +35,10 @@ def enable(flag: bool = True) -> None:
 
 
 class Profiler:
-    """``with Profiler(dir, rank, steps):`` ... ``prof.step()`` per training step."""
+    """``with Profiler(dir, rank, steps):`` ... ``prof.step()`` per training step.  The fused path
+    calls ``step()`` once per epoch (one kernel launch runs the epoch) with ``wait=warmup=0``."""
 
-    def __init__(self, out_dir: str | None, rank: int = 0, active_steps: int = 20):
+    def __init__(self, out_dir: str | None, rank: int = 0, active_steps: int = 20, wait: int = 1, warmup: int = 2):
         self.out_dir = out_dir
         self.rank = rank
         self.prof = None
@@ -47,7 +48,7 @@ class Profiler:
             if torch.cuda.is_available():
                 acts.append(torch.profiler.ProfilerActivity.CUDA)
             self.prof = torch.profiler.profile(
-                activities=acts, schedule=torch.profiler.schedule(wait=1, warmup=2, active=active_steps, repeat=1),
+                activities=acts, schedule=torch.profiler.schedule(wait=wait, warmup=warmup, active=active_steps, repeat=1),
                 on_trace_ready=self._save, record_shapes=False)
 
     def _save(self, p):

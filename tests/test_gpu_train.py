@@ -126,3 +126,17 @@ def test_health_report_on_gpu(tmp_path):
     assert files, r.stdout[-2000:]
     rep = json.loads(files[0].read_text())
     assert int(rep["gpu"]["gpu_count"]) >= 1
+
+
+def test_train_py_fused_profile_trace(tmp_path):
+    """--profile on the default (fused) path: one profiler step per epoch launch; the kineto trace
+    holds the fused kernel and, with DGT_ROCTX=1, the per-epoch roctx ranges."""
+    os.environ["DGT_ROCTX"] = "1"
+    try:
+        r = _train("--epochs", "2", "--no-save", "--profile", str(tmp_path / "prof"))
+    finally:
+        os.environ.pop("DGT_ROCTX", None)
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert "impl=fused" in r.stderr
+    text = (tmp_path / "prof" / "trace_rank0.json").read_text()
+    assert "tiny_mlp_train_kernel" in text

@@ -254,3 +254,17 @@ def test_gemm_b_kn_identity_asymmetric(variant):
     C = torch.empty(n, n, dtype=torch.float32).cuda()
     gemm_nt(A, B, C=C, out_f32=True, variant=variant, b_kn=True)
     torch.testing.assert_close(C, B.float())
+
+
+@pytest.mark.parametrize("comm,want", [(None, torch.bfloat16), (torch.bfloat16, torch.bfloat16),
+                                       (torch.float32, torch.float32)])
+def test_trainer_comm_dtype_selects_gradient_wire(comm, want):
+    """communication_data_type for the MLP trainer: the collectives carry the gradient buffer, so
+    an fp32 wire means fp32 gradients from the wgrad epilogue (and the step still trains)."""
+    torch.manual_seed(0)
+    tr = MLPTrainer(SyntheticMLP(width=64, depth=2), batch_size=32, n_batches=2, lr=1e-3,
+                    device=torch.device("cpu"), comm_dtype=comm)
+    assert tr.grads_w.dtype == want
+    before = tr.params.clone()
+    tr.step(0)
+    assert not torch.equal(before, tr.params)

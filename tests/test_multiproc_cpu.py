@@ -139,3 +139,30 @@ def test_mpirun_style_launch_matches_oracle(tmp_path):
     outs = [p.communicate(timeout=300) for p in procs]
     assert all(p.returncode == 0 for p in procs), outs[0][1][-2000:] + outs[1][1][-2000:]
     assert epoch_losses(outs[0][0]) == ORACLE[2][:2]
+
+
+def test_bf16_gradient_wire_error_eight_ranks():
+    """bound the error an 8-rank bf16 gradient sum adds over an fp32 wire.
+    Measured (gloo, CPU; RCCL's ring order emulated): fp32 wire 6e-10, bf16 wire 3.7e-3 relative
+    RMS, against 1.7e-3 for rounding one fp32 gradient to bf16 at all: the bf16 wire roughly
+    doubles the gradient's own bf16 error.  MLPTrainer keeps bf16 as the default wire (half the
+    collective and Adam bytes, as DeepSpeed's bf16 mode does) and communication_data_type=fp32
+    (fp32 gradients straight out of the wgrad epilogue) removes the accumulation error."""
+    r = run(8, script="tests/bf16_wire_worker.py", timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][len("RESULT "):])
+    print(res)
+    assert res["fp32_wire_rel_rms"] < 1e-6
+    # bf16 unit roundoff is 2^-9 = 1.95e-3; 7 rounded additions stay within a few of it
+    assert res["bf16_wire_rel_rms"] < 8e-3 and res["bf16_ring_rel_rms"] < 8e-3
+    assert res["bf16_ring_max_over_l1"] < 7 * 2.0 ** -8  # <= (ws - 1) unit roundoffs of the magnitudes
+    assert 5e-4 < res["bf16_input_quant_rel_rms"] < 2e-3
+
+
+def test_profile_trace_on_default_trainer_path(tmp_path):
+    """--profile wraps the TinyMLPTrainer path too (the default on a GPU: one profiler step per
+    fused epoch launch), not only the engine loop."""
+    r = run(1, "--impl", "torch", "--epochs", "2", "--no-save", "--profile", str(tmp_path / "prof"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    trace = tmp_path / "prof" / "trace_rank0.json"
+    assert trace.exists() and trace.stat().st_size > 1000

@@ -58,7 +58,8 @@ def parse_args(argv=None):
     p.add_argument("--resume", action="store_true", help="continue from the newest checkpoint in --save-dir")
     p.add_argument("--no-save", action="store_true")
     p.add_argument("--dist-timeout", type=float, default=1800.0)
-    p.add_argument("--profile", default=None, help="write a torch.profiler (kineto) trace per rank to this dir")
+    p.add_argument("--profile", default=None, help="write a torch.profiler (kineto) trace per rank to this dir "
+                   "(every path; roctx ranges with DGT_ROCTX=1 name the phases / fused epoch launches)")
     p.add_argument("--debug-sync", action="store_true",
                    help="serialize kernels (AMD_SERIALIZE_KERNEL=3) and sync comm/compute streams: race hunting")
     return p.parse_known_args(argv)[0]
@@ -117,14 +118,20 @@ def main(argv=None) -> int:
             if found:
                 trainer.load_checkpoint(found[1])
                 start_epoch = found[0] + 1
-        for epoch in range(start_epoch, args.epochs + 1):
-            avg_loss = trainer.run_epoch(epoch)
-            if local_rank == 0:
-                print(f"Epoch {epoch:2d} finished. Avg loss: {avg_loss:.4f}", flush=True)
-            if not args.no_save:
-                save_dir = os.path.join(args.save_dir, f"epoch{epoch}")
-                os.makedirs(save_dir, exist_ok=True)
-                trainer.save_checkpoint(save_dir)
+        from distributed_gpu_test_amd.utils.tracing import Profiler
+        # one profiler step per epoch: the fused path runs a whole epoch in one kernel launch
+        prof = Profiler(args.profile, comm.get_rank(), active_steps=max(1, args.epochs - start_epoch + 1), wait=0,
+                        warmup=0)
+        with prof:
+            for epoch in range(start_epoch, args.epochs + 1):
+                avg_loss = trainer.run_epoch(epoch)
+                prof.step()
+                if local_rank == 0:
+                    print(f"Epoch {epoch:2d} finished. Avg loss: {avg_loss:.4f}", flush=True)
+                if not args.no_save:
+                    save_dir = os.path.join(args.save_dir, f"epoch{epoch}")
+                    os.makedirs(save_dir, exist_ok=True)
+                    trainer.save_checkpoint(save_dir)
         trainer.close()
     else:
         engine, optimizer, _, _ = dgt.initialize(args=ds_config, model=model, optimizer=optimizer,
