@@ -2,7 +2,9 @@
 // seven _foreach_* multi-tensor launches plus the DeepSpeed 1/world_size scale and the host-side
 // bias-correction .item() syncs.  Memory-bound: 16-byte vector accesses on
 // every stream (Guideline 13), nontemporal hints (each byte is touched once), one float4 group per
-// thread over a full grid: 6.1 TB/s on the bench MLP's 67M parameters (scripts/bench_adam.py).
+// thread over a full grid.  On the bench MLP's 67M parameters (profiles/r1_adam_v8_ab.txt): 5.41 TB/s
+// with fp32 gradients (the plain variant 3 ties it), 6.43 TB/s with bf16 gradients where the
+// streaming hints pay (6.12 without) - the bf16 MLP step is the case the default is tuned for.
 // Reference: torch.optim.Adam created at train.py:85, stepped by model_engine.step() at train.py:114.
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
@@ -197,11 +199,26 @@ __global__ __launch_bounds__(256) void adam_flat8_kernel(AdamFlatArgs a) {
   else if (i == n8 && (a.n & 4)) adam_group<GT, LT, NT>(a, grad, lp, 8 * i, scale, step_size_neg, bc2_sqrt);
 }
 
-// loop shape chosen by measurement (scripts/bench_adam.py); DGT_ADAM_VARIANT overrides it for A/B runs
+// Loop shape chosen by measurement (scripts/bench_adam.py).  DGT_ADAM_VARIANT (read ONCE, at the
+// first launch: no getenv on the launch path) or adam_set_variant() selects another for A/B runs.
+static int g_adam_variant = -1;
+
 static int adam_variant() {
-  const char* e = getenv("DGT_ADAM_VARIANT");
-  return e ? atoi(e) : 0;
+  if (g_adam_variant < 0) {
+    const char* e = getenv("DGT_ADAM_VARIANT");
+    const int v = e ? atoi(e) : 0;
+    g_adam_variant = (v >= 0 && v <= 4) ? v : 0;
+  }
+  return g_adam_variant;
 }
+
+bool adam_set_variant(int v) {
+  if (v < 0 || v > 4) return false;
+  g_adam_variant = v;
+  return true;
+}
+
+static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 template <typename GT, typename LT>
 static void launch_adam_v(const AdamFlatArgs& a, hipStream_t s) {
@@ -221,10 +238,16 @@ static void launch_adam_v(const AdamFlatArgs& a, hipStream_t s) {
       hipLaunchKernelGGL((adam_flat_kernel<GT, LT, false, 1>), dim3((int)grid), dim3(256), 0, s, a);
       break;
     case 4:  // one 8-element group per thread (16-byte 16-bit streams), streaming hints, full grid
+      // 16-byte loads/stores of the 16-bit streams: a slice at a 4-element offset takes the default
+      if ((sizeof(GT) == 2 && !aligned16(a.grad)) || (a.param_lp && sizeof(LT) == 2 && !aligned16(a.param_lp))) {
+        grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);
+        hipLaunchKernelGGL((adam_flat_kernel<GT, LT, true, 1>), dim3((int)grid), dim3(256), 0, s, a);
+        break;
+      }
       grid = std::max<long long>((a.n / 8 + 1 + 255) / 256, 1);
       hipLaunchKernelGGL((adam_flat8_kernel<GT, LT, true>), dim3((int)grid), dim3(256), 0, s, a);
       break;
-    default:  // one group per thread, streaming hints, full grid: 6.1 TB/s at 67M params
+    default:  // one group per thread, streaming hints, full grid
       grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);
       hipLaunchKernelGGL((adam_flat_kernel<GT, LT, true, 1>), dim3((int)grid), dim3(256), 0, s, a);
   }

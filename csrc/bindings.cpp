@@ -343,6 +343,12 @@ dgt::AdamFlatArgs adam_args(const at::Tensor& master, const std::optional<at::Te
   TORCH_CHECK(grad.is_cuda() && grad.is_contiguous(), "dgt: grad must be a contiguous GPU tensor");
   const int64_t n = master.numel();
   TORCH_CHECK(n % 4 == 0, "dgt: flat buffers must be padded to a multiple of 4 elements");
+  // the kernels move float4 (fp32) and 4 x 16-bit groups: slices must start on such a group
+  auto al = [](const void* p, int b) { return (reinterpret_cast<uintptr_t>(p) % b) == 0; };
+  TORCH_CHECK(al(master.data_ptr(), 16) && al(exp_avg.data_ptr(), 16) && al(exp_avg_sq.data_ptr(), 16),
+              "dgt: adam_flat fp32 buffers must be 16-byte aligned (slice offsets a multiple of 4)");
+  TORCH_CHECK(al(grad.data_ptr(), 4 * (int)grad.element_size()),
+              "dgt: adam_flat grad must be aligned to a 4-element group");
   TORCH_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "dgt: flat size mismatch");
   const bool dev_step = step_dev.has_value() && step_dev->defined();
   TORCH_CHECK(dev_step || step >= 1, "dgt: adam step must be >= 1");
@@ -352,6 +358,8 @@ dgt::AdamFlatArgs adam_args(const at::Tensor& master, const std::optional<at::Te
   a.lp_dtype = dgt::kF32;
   if (param_lp.has_value() && param_lp->defined()) {
     TORCH_CHECK(param_lp->is_cuda() && param_lp->is_contiguous() && param_lp->numel() == n, "dgt: bad param_lp");
+    TORCH_CHECK(al(param_lp->data_ptr(), 4 * (int)param_lp->element_size()),
+                "dgt: adam_flat param_lp must be aligned to a 4-element group");
     a.param_lp = param_lp->data_ptr();
     a.lp_dtype = dtype_code(param_lp->scalar_type());
   }
@@ -409,6 +417,8 @@ void adam_matrix_t(const at::Tensor& master, const at::Tensor& param_lp, const a
   c10::DeviceGuard guard(master.device());
   DGT_CHECK_HIP(dgt::adam_matrix_t(a, param_lpT.data_ptr(), (int)rows, (int)cols, stream_of(master)));
 }
+
+void adam_set_variant(int64_t v) { TORCH_CHECK(dgt::adam_set_variant((int)v), "dgt: unknown adam variant ", v); }
 
 void step_increment(const at::Tensor& counter) {
   check_gpu(counter, "counter", at::kLong);
@@ -497,6 +507,52 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
   if (variant == 2)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
   DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A), (int)variant));
+}
+
+// wgrad + Adam in one launch: the weight gradient alpha * A . B^T ([M, N], never stored) updates the
+// fp32 master / exp_avg / exp_avg_sq [M, N] and the bf16 compute copy param_lp [M, N] in place.
+void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& master, const at::Tensor& exp_avg,
+                  const at::Tensor& exp_avg_sq, const at::Tensor& param_lp, int64_t step, double lr, double beta1,
+                  double beta2, double eps, double weight_decay, bool adamw, double grad_scale, int64_t variant) {
+  TORCH_CHECK(variant >= 0 && variant <= 4 && step >= 1, "dgt: gemm_nt_adam needs variant 0-4 and step >= 1");
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt_adam needs A[M,K], B[N,K]");
+  const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
+  for (const at::Tensor* t : {&A, &B}) {
+    TORCH_CHECK(t->is_cuda() && t->scalar_type() == at::kBFloat16, "dgt: gemm_nt_adam operands must be bf16 GPU tensors");
+    TORCH_CHECK(t->stride(1) == 1 && t->stride(0) >= t->size(1) && t->stride(0) % 8 == 0,
+                "dgt: gemm_nt_adam operand rows must be unit-stride with a 16-byte aligned row stride");
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "dgt: gemm_nt_adam operand must be 16-byte aligned");
+  }
+  TORCH_CHECK(M % 128 == 0 && N % 128 == 0 && K % 64 == 0, "dgt: gemm_nt_adam needs M, N % 128 == 0 and K % 64 == 0");
+  check_2d(master, "master", at::kFloat, M, N);
+  check_2d(exp_avg, "exp_avg", at::kFloat, M, N);
+  check_2d(exp_avg_sq, "exp_avg_sq", at::kFloat, M, N);
+  check_2d(param_lp, "param_lp", at::kBFloat16, M, N);
+  for (const at::Tensor* t : {&master, &exp_avg, &exp_avg_sq, &param_lp})
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "dgt: gemm_nt_adam state must be 16-byte aligned");
+  if (variant == 2)
+    TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
+  dgt::GemmArgs g;
+  std::memset(&g, 0, sizeof(g));
+  g.A = A.data_ptr();
+  g.B = B.data_ptr();
+  g.M = (int)M;
+  g.N = (int)N;
+  g.K = (int)K;
+  g.lda = (int)A.stride(0);
+  g.ldb = (int)B.stride(0);
+  g.ldc = (int)N;
+  g.alpha = (float)grad_scale;
+  g.adam.master = master.data_ptr<float>();
+  g.adam.m = exp_avg.data_ptr<float>();
+  g.adam.v = exp_avg_sq.data_ptr<float>();
+  g.adam.lp = param_lp.data_ptr();
+  g.adam.hp = make_hyper(lr, beta1, beta2, eps, weight_decay, adamw);
+  const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
+  g.adam.step_size_neg = (float)(-(lr / bc1));
+  g.adam.bc2_sqrt = (float)std::sqrt(bc2);
+  c10::DeviceGuard guard(A.device());
+  DGT_CHECK_HIP(dgt::gemm_nt(g, dgt::kEpiAdam, stream_of(A), (int)variant));
 }
 
 void transpose_bf16(const at::Tensor& in, const at::Tensor& out) {
@@ -609,6 +665,12 @@ bool can_access_peer(int64_t dev, int64_t peer) {
 }  // namespace
 
 TORCH_LIBRARY(dgt, m) {
+  m.def(
+      "gemm_nt_adam(Tensor A, Tensor B, Tensor(a!) master, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, "
+      "Tensor(d!) param_lp, int step, float lr, float beta1, float beta2, float eps, float weight_decay, bool adamw, "
+      "float grad_scale, int variant=0) -> ()",
+      &gemm_nt_adam);
+  m.def("adam_set_variant(int variant) -> ()", &adam_set_variant);
   m.def("tiny_mlp_supported(int f, int h) -> bool", &tiny_mlp_supported);
   m.def("tiny_mlp_padded_numel(int f, int h) -> int", &tiny_mlp_padded_numel);
   m.def("tiny_mlp_exchange_floats(int f, int h) -> int", &tiny_mlp_exchange_floats);

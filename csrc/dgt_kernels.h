@@ -77,6 +77,8 @@ struct AdamFlatArgs {
 hipError_t step_increment(long long* counter, hipStream_t stream);
 
 hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream);
+// Select the flat Adam loop shape (0 = default; 1-4 = A/B variants of csrc/adam.hip); false if unknown.
+bool adam_set_variant(int variant);
 
 // Adam over a row-major [rows, cols] fp32 matrix (a.n = rows * cols, rows a multiple of 64, cols of 128) that also
 // writes the bf16 copy a.param_lp [rows, cols] and its transpose lpT [cols, rows] in the same pass.
@@ -107,6 +109,18 @@ enum GemmEpilogue : int {
   kEpiOutF32 = 16,     // C is fp32 (else bf16)
   kEpiAccumulate = 32, // C += result (fp32 only)
   kEpiBKN = 64,        // B is given as [K, N] (N contiguous): C = A . B, read with transposed LDS reads
+  kEpiAdam = 128,      // C is a weight GRADIENT consumed in place: Adam updates adam.master / m / v [M, ldc]
+                       // and writes the bf16 copy adam.lp; no gradient is stored (single-rank ZeRO-0)
+};
+
+struct GemmAdam {      // kEpiAdam: fp32 master, moments and the bf16 compute copy of the [M, N] weight
+  float* master;
+  float* m;
+  float* v;
+  void* lp;            // bf16
+  AdamHyper hp;
+  float step_size_neg; // -lr / (1 - beta1^t)
+  float bc2_sqrt;      // sqrt(1 - beta2^t)
 };
 
 struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 A/B, fp32 accumulate
@@ -120,6 +134,7 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   int M, N, K;
   int lda, ldb, ldc, ldct, ldmask;
   float alpha;
+  GemmAdam adam;       // kEpiAdam only (the gradient is alpha * A . B^T; ldc = row stride of the weight)
 };
 
 hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream, int variant = 0);

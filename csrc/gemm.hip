@@ -208,6 +208,64 @@ DGT_DEVICE int etile(int r, int n) {
   return r * TN + ((((c ^ (r >> 3)) & 15) | (c & ~15)) << 3) + (n & 7);
 }
 
+// kEpiAdam epilogue: the block's fp32 gradient tile goes through LDS (the operand stages are idle)
+// so that every global access of the optimizer update is a 16-byte vector: per float4 of the weight,
+// 16-B loads of master / exp_avg / exp_avg_sq, torch's Adam in fp32 (the same per-element op order
+// as adam_flat), 16-B stores of the three and an 8-B store of the bf16 compute copy.  The gradient
+// never reaches memory: this replaces the wgrad's gradient store (2-4 B/param), the optimizer's
+// gradient read (2-4 B/param) and the separate Adam launch, and overlaps the update's HBM traffic
+// with the MFMA work of the blocks still in their K loop.
+// LDS image: [RP rows][TN] fp32 per pass, the 16-float column group XOR-swizzled by (row >> 2) & 3:
+// the MFMA layout writes 4 rows 4 apart x 16 consecutive columns per instruction (conflict-free),
+// the update reads 16-B row pieces.  Waves whose WM-row band lies in pass h write in that pass.
+template <int TN>
+DGT_DEVICE int adam_slot(int r, int c) { return r * TN + (c ^ (((r >> 2) & 3) << 4)); }
+
+template <int TM, int TN, int WM, int WN, int NT, int RP>
+DGT_DEVICE void epilogue_adam(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN / 16], float* tile, int m0, int n0,
+                              int wr, int wc, int l, int tid) {
+  static_assert(TM % RP == 0 && RP % WM == 0 && TN >= 64 && (RP * TN / 4) % NT == 0, "adam epilogue geometry");
+  const GemmAdam& a = g.adam;
+  __hip_bfloat16* lp = static_cast<__hip_bfloat16*>(a.lp);
+#pragma unroll 1
+  for (int h = 0; h < TM / RP; ++h) {
+    __syncthreads();  // operand stages (h = 0) or the previous pass's tile (h = 1) fully read
+    if (wr * WM / RP == h) {
+#pragma unroll
+      for (int i = 0; i < WM / 16; ++i)
+#pragma unroll
+        for (int j = 0; j < WN / 16; ++j)
+#pragma unroll
+          for (int rr = 0; rr < 4; ++rr)
+            tile[adam_slot<TN>(wr * WM - h * RP + i * 16 + 4 * (l >> 4) + rr, wc * WN + j * 16 + (l & 15))] =
+                acc[i][j][rr] * g.alpha;
+    }
+    __syncthreads();
+#pragma unroll 4
+    for (int it = 0; it < RP * TN / 4 / NT; ++it) {
+      const int idx = tid + NT * it, r = idx / (TN / 4), c = (idx % (TN / 4)) * 4;
+      const f32x4 gr = *reinterpret_cast<const f32x4*>(tile + adam_slot<TN>(r, c));
+      const long long o = (long long)(m0 + h * RP + r) * g.ldc + n0 + c;
+      f32x4 p = *reinterpret_cast<const f32x4*>(a.master + o);
+      f32x4 m = *reinterpret_cast<const f32x4*>(a.m + o);
+      f32x4 v = *reinterpret_cast<const f32x4*>(a.v + o);
+      __hip_bfloat16 b[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float mm = m[e], vv = v[e];
+        p[e] = adam_update(p[e], gr[e], mm, vv, a.hp, a.step_size_neg, a.bc2_sqrt);
+        m[e] = mm;
+        v[e] = vv;
+        b[e] = __float2bfloat16(p[e]);
+      }
+      *reinterpret_cast<f32x4*>(a.master + o) = p;
+      *reinterpret_cast<f32x4*>(a.m + o) = m;
+      *reinterpret_cast<f32x4*>(a.v + o) = v;
+      *reinterpret_cast<uint2*>(lp + o) = *reinterpret_cast<const uint2*>(b);
+    }
+  }
+}
+
 template <int EPI, int TM, int TN, int WM, int WN, int NT>
 DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN / 16], u16* tile, int m0, int n0,
                                 int wr, int wc, int l, int tid) {
@@ -385,7 +443,11 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
   }
 
   // ---- epilogue: D col = l&15 (n), row = 4*(l>>4) + r (m)
-  if constexpr (!(EPI & kEpiOutF32)) {
+  if constexpr ((EPI & kEpiAdam) != 0) {
+    // fp32 128 x 128 tile = 64 KiB: one pass fits the 2-stage (64 KiB) and 4-stage LDS
+    epilogue_adam<GBM, GBN, 64, WN, 64 * NW, GBM>(g, acc, reinterpret_cast<float*>(&lds[0][0][0]), m0, n0, wr, wc, l,
+                                                  tid);
+  } else if constexpr (!(EPI & kEpiOutF32)) {
     epilogue_staged<EPI, GBM, GBN, 64, WN, 64 * NW>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
   } else {
 #pragma unroll
@@ -593,7 +655,10 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   for (int it = 0; it + 1 < nit; ++it) iteration<false>(c, it, f, acc);
   iteration<true>(c, nit - 1, f, acc);
 
-  if constexpr (!(EPI & kEpiOutF32)) {
+  if constexpr ((EPI & kEpiAdam) != 0) {
+    // fp32 256 x 256 tile = 256 KiB: two passes of 128 rows through the 128 KiB of operand LDS
+    epilogue_adam<BM, BN, 128, 64, 512, 128>(g, acc, reinterpret_cast<float*>(lds), m0, n0, c.wr, c.wc, c.l, tid);
+  } else if constexpr (!(EPI & kEpiOutF32)) {
     epilogue_staged<EPI, BM, BN, 128, 64, 512>(g, acc, lds, m0, n0, c.wr, c.wc, c.l, tid);
   } else {
 #pragma unroll
@@ -647,6 +712,7 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
     DGT_EPI_CASE(kEpiOutF32)                                       // wgrad into fp32 grads
     DGT_EPI_CASE(kEpiOutF32 | kEpiAccumulate)                      // wgrad, gradient accumulation
     DGT_EPI_CASE(kEpiOutF32 | kEpiBias)                            // generic fp32 out
+    DGT_EPI_CASE(kEpiAdam)                                         // wgrad consumed by Adam in place
     DGT_EPI_CASE_KN(kEpiMask | kEpiStoreT | kEpiBKN)               // dgrad straight from W[out, in]
     DGT_EPI_CASE_KN(kEpiBKN)                                       // plain A . B
     DGT_EPI_CASE_KN(kEpiOutF32 | kEpiBKN)

@@ -55,6 +55,24 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant))
 
 
+def gemm_nt_adam_(A: torch.Tensor, B: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor,
+                  exp_avg_sq: torch.Tensor, param_lp: torch.Tensor, step: int, lr: float, beta1: float, beta2: float,
+                  eps: float, weight_decay: float = 0.0, adamw: bool = False, grad_scale: float = 1.0,
+                  variant: int = 0) -> None:
+    """Weight gradient ``grad_scale * A @ B.T`` ([M, N], never materialised) consumed in place by
+    Adam: updates the fp32 ``master`` / ``exp_avg`` / ``exp_avg_sq`` ([M, N]) and writes the bf16
+    compute copy ``param_lp``.  One launch instead of wgrad GEMM + gradient store + flat Adam."""
+    if not A.is_cuda:
+        from .reference import adam_flat_reference_
+        g = (A.float() @ B.float().t()).reshape(-1)
+        p, m, v = master.view(-1), exp_avg.view(-1), exp_avg_sq.view(-1)
+        adam_flat_reference_(p, g, m, v, step, lr, beta1, beta2, eps, weight_decay, adamw, grad_scale=grad_scale)
+        param_lp.copy_(master.to(param_lp.dtype))
+        return
+    require().gemm_nt_adam(A, B, master, exp_avg, exp_avg_sq, param_lp, int(step), float(lr), float(beta1),
+                           float(beta2), float(eps), float(weight_decay), bool(adamw), float(grad_scale), int(variant))
+
+
 def transpose_bf16(inp: torch.Tensor, out: torch.Tensor) -> None:
     if inp.is_cuda:
         require().transpose_bf16(inp, out)

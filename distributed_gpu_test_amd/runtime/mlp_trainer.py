@@ -66,7 +66,7 @@ import torch.distributed as dist
 from ..accelerator import get_accelerator
 from ..models.synthetic_mlp import SyntheticMLP, synthetic_batch_data
 from ..ops.adam import adam_flat_, adam_matrix_t_
-from ..ops.gemm import gemm_nt, mlp_head, rowsum_bf16, transpose_bf16
+from ..ops.gemm import gemm_nt, gemm_nt_adam_, mlp_head, rowsum_bf16, transpose_bf16
 from ..parallel import comm
 
 ALIGN = 64
@@ -83,7 +83,8 @@ class MLPTrainer:
     def __init__(self, model: SyntheticMLP, batch_size: int = 1024, n_batches: int = 8, lr: float = 1e-4,
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 1234,
                  device: Optional[torch.device] = None, zero_stage: int = 0, schedule: Optional[str] = None,
-                 grad_dtype: Optional[torch.dtype] = None, comm_dtype: Optional[torch.dtype] = None):
+                 grad_dtype: Optional[torch.dtype] = None, comm_dtype: Optional[torch.dtype] = None,
+                 fuse_adam: Optional[bool] = None):
         if zero_stage not in (0, 1):
             raise ValueError("MLPTrainer supports zero_stage 0 or 1")
         if comm_dtype not in (None, torch.bfloat16, torch.float32):
@@ -189,6 +190,12 @@ class MLPTrainer:
             self.WT = [None] + [torch.empty(w.shape[1], w.shape[0], dtype=torch.bfloat16, device=dev)
                                 for w in self.W[1:]]
         self._refresh_transposes()
+        # single rank, ZeRO-0: nothing reduces the weight gradients, so each wgrad GEMM applies Adam
+        # to its tile in its epilogue (gemm_nt_adam_) and no gradient ever reaches memory
+        if fuse_adam is None:
+            fuse_adam = os.environ.get("DGT_MLP_FUSED_ADAM", "1") != "0"
+        self.fused_adam = bool(fuse_adam and dev.type == "cuda" and not self.coll and self.zero_stage == 0
+                               and self.dgrad_kn and not self.matrix_t)
 
         # ---- activations (both layouts) and gradient scratch
         B, D = self.B, self.D
@@ -248,6 +255,9 @@ class MLPTrainer:
 
     def grad_of(self, name: str) -> torch.Tensor:
         """This rank's local (pre-reduction) gradient of a model parameter, in its shape."""
+        if self.fused_adam and name.startswith("layers.") and name.endswith("weight"):
+            raise RuntimeError("weight gradients are consumed in place by the fused wgrad+Adam; "
+                               "construct MLPTrainer(fuse_adam=False) to inspect them")
         self.join()
         p = dict(self.model.named_parameters())[name]
         if name.startswith("layers.") and name.endswith("weight"):
@@ -345,6 +355,9 @@ class MLPTrainer:
         mlp_head(self.a[L], self.hw, self.hb, y, self.dz, self.ghw, self.ghb, self.loss_acc, self.g[cur],
                  self.gT[cur])
         self.global_steps += 1
+        if self.fused_adam:
+            self._backward_fused_adam(xT, cur)
+            return
         works: list = []
         # backward, last layer first; each weight bucket leaves for its collective as soon as its
         # wgrad is enqueued; with the overlap schedule the layer's optimizer update follows on
@@ -409,6 +422,28 @@ class MLPTrainer:
                 self._t_pending = True
             else:
                 self._refresh_transposes()
+
+    def _backward_fused_adam(self, xT: torch.Tensor, cur: int) -> None:
+        """Single-rank backward + update: per layer, the bias-gradient row sums, the dgrad (it
+        reads W_l, so it runs BEFORE W_l changes), then ONE launch that computes dW_l and applies
+        Adam to W_l in its epilogue (fp32 master / moments + the bf16 compute copy).  The weight
+        region moves 26 B/param (12 read + 14 written) instead of the wgrad store + flat Adam's
+        2 + 28 B/param, and the update overlaps the other blocks' MFMA work."""
+        args = self._adam_args()
+        for i in reversed(range(self.L)):
+            a_prevT = xT if i == 0 else self.aT[i]
+            rowsum_bf16(self.gT[cur], self.gb[i])
+            if i > 0:
+                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True)
+            R, Cc = self.shapes[i]
+            o = self.w_off[i]
+            sl = slice(o, o + R * Cc)
+            gemm_nt_adam_(self.gT[cur], a_prevT, self.master_w[sl].view(R, Cc), self.m_w[sl].view(R, Cc),
+                          self.v_w[sl].view(R, Cc), self.params_bf16[sl].view(R, Cc), *args,
+                          grad_scale=1.0 / self.world_size)
+            if i > 0:
+                cur ^= 1
+        adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *args, grad_scale=1.0 / self.world_size)
 
     # bench.py adapter (same surface as TinyMLPTrainer)
     def epoch_plan(self, epoch: int):

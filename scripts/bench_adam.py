@@ -31,7 +31,7 @@ def main():
     step = 0
     for rnd in range(5):
         for k in VARIANTS:
-            os.environ["DGT_ADAM_VARIANT"] = str(k)
+            torch.ops.dgt.adam_set_variant(k)
             for _ in range(3):
                 step += 1
                 adam_flat_(master, grad, m, v, step, 1e-4, param_lp=lp)

@@ -19,7 +19,8 @@ def _trainer_vs_torch(device, grad_dtype=torch.bfloat16):
     torch.manual_seed(0)
     model = SyntheticMLP(width=128, depth=2)
     ref = copy.deepcopy(model)
-    tr = MLPTrainer(model, batch_size=128, n_batches=2, lr=1e-3, device=device, grad_dtype=grad_dtype)
+    tr = MLPTrainer(model, batch_size=128, n_batches=2, lr=1e-3, device=device, grad_dtype=grad_dtype,
+                    fuse_adam=False)  # the gradients are inspected
     x = tr.X[:128].float().cpu()
     y = tr.Y[:128].float().cpu()
     with torch.no_grad():
@@ -268,3 +269,49 @@ def test_trainer_comm_dtype_selects_gradient_wire(comm, want):
     before = tr.params.clone()
     tr.step(0)
     assert not torch.equal(before, tr.params)
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 3), (512, 256, 1024, 4),
+                                           (256, 256, 128, 2), (512, 768, 256, 2)])
+@pytest.mark.parametrize("wd,adamw", [(0.0, False), (0.01, True)])
+def test_gemm_nt_adam_matches_reference(M, N, K, variant, wd, adamw):
+    """wgrad + Adam in one launch (kEpiAdam epilogue through LDS, both kernels) against an fp32
+    gradient GEMM followed by the reference Adam."""
+    from distributed_gpu_test_amd.ops.gemm import gemm_nt_adam_
+    from distributed_gpu_test_amd.ops.reference import adam_flat_reference_
+    g = torch.Generator().manual_seed(M * 7 + N + K)
+    A = (torch.randn(M, K, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    B = (torch.randn(N, K, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    p = torch.randn(M, N, generator=g).cuda()
+    m = (torch.randn(M, N, generator=g) * 1e-2).cuda()
+    v = (torch.rand(M, N, generator=g) * 1e-3).cuda()
+    lp = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+    grad = (A.float() @ B.float().t()) * 0.5
+    p2, m2, v2 = p.clone().view(-1), m.clone().view(-1), v.clone().view(-1)
+    adam_flat_reference_(p2, grad.reshape(-1), m2, v2, 7, 1e-3, 0.9, 0.999, 1e-8, wd, adamw)
+    gemm_nt_adam_(A, B, p, m, v, lp, 7, 1e-3, 0.9, 0.999, 1e-8, wd, adamw, grad_scale=0.5, variant=variant)
+    torch.testing.assert_close(p.view(-1), p2, rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(m.view(-1), m2, rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(v.view(-1), v2, rtol=1e-4, atol=1e-9)
+    assert torch.equal(lp, p.to(torch.bfloat16))
+
+
+@gpu
+def test_mlp_fused_adam_matches_unfused_fp32_grads():
+    """The fused single-rank step (dgrad first, then wgrad + Adam in one launch per layer) moves the
+    parameters exactly like the unfused step with fp32 gradients: same fp32 gradient values, same
+    per-element Adam."""
+    outs = []
+    for fused in (False, True):
+        torch.manual_seed(0)
+        tr = MLPTrainer(SyntheticMLP(width=256, depth=3), batch_size=128, n_batches=2, lr=1e-3,
+                        device=torch.device("cuda"), grad_dtype=torch.float32, fuse_adam=fused)
+        assert tr.fused_adam == fused
+        for s in range(4):
+            tr.step(s)
+        torch.cuda.synchronize()
+        outs.append((tr.params.clone(), tr.master_w.clone(), tr.m_w.clone(), tr.v_w.clone(), float(tr.loss_acc.item())))
+    for a, b in zip(outs[0][:4], outs[1][:4]):
+        assert torch.equal(a, b)
+    assert outs[0][4] == outs[1][4]
