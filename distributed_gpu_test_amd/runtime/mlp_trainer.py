@@ -196,6 +196,11 @@ class MLPTrainer:
             fuse_adam = os.environ.get("DGT_MLP_FUSED_ADAM", "1") != "0"
         self.fused_adam = bool(fuse_adam and dev.type == "cuda" and not self.coll and self.zero_stage == 0
                                and self.dgrad_kn and not self.matrix_t)
+        # kernel for the fused wgrad+Adam (0 = by shape: 256^2 tiles at 4096^2).  Alone, 128^2 tiles
+        # at 2 blocks per CU overlap one block's Adam epilogue with the other's K loop best (94.7 us
+        # vs 100.2 vs 118.6 unfused, profiles/r2_wgrad_adam.jsonl); inside the step they lose
+        # (1178 vs 1283 it/s, profiles/r2_mlp_fused_adam_ab.txt), so the default stays shape-picked
+        self.fused_variant = int(os.environ.get("DGT_MLP_FUSED_VARIANT", "0"))
 
         # ---- activations (both layouts) and gradient scratch
         B, D = self.B, self.D
@@ -440,7 +445,7 @@ class MLPTrainer:
             sl = slice(o, o + R * Cc)
             gemm_nt_adam_(self.gT[cur], a_prevT, self.master_w[sl].view(R, Cc), self.m_w[sl].view(R, Cc),
                           self.v_w[sl].view(R, Cc), self.params_bf16[sl].view(R, Cc), *args,
-                          grad_scale=1.0 / self.world_size)
+                          grad_scale=1.0 / self.world_size, variant=self.fused_variant)
             if i > 0:
                 cur ^= 1
         adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *args, grad_scale=1.0 / self.world_size)
