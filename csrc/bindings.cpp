@@ -452,11 +452,12 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
 
 void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
-             const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant) {
+             const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
+             const std::optional<at::Tensor>& sk_slab, const std::optional<at::Tensor>& sk_flags) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK(variant >= 0 && variant <= 4,
-              "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (128x128, 4 stages) "
-              "or 4 (128x128, 4 stages, 8 waves)");
+  TORCH_CHECK(variant >= 0 && variant <= 5,
+              "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (128x128, 4 stages), "
+              "4 (128x128, 4 stages, 8 waves) or 5 (256x128, split-K 2)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
@@ -503,9 +504,24 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
     g.mask = mask->data_ptr();
     g.ldmask = (int)N;
   }
+  if (sk_slab.has_value() && sk_slab->defined() && sk_flags.has_value() && sk_flags->defined()) {
+    // split-K workspace: one fp32 256 x 128 partial per tile, two zeroed ints per tile (the kernel
+    // re-arms them); launches that share it must be stream-ordered (the caller keys it per stream)
+    const int64_t tiles = (M % 256 == 0 && N % 128 == 0) ? (M / 256) * (N / 128) : 0;
+    check_gpu(*sk_slab, "sk_slab", at::kFloat);
+    check_gpu(*sk_flags, "sk_flags", at::kInt);
+    if (tiles > 0 && sk_slab->numel() >= tiles * 256 * 128 && sk_flags->numel() >= 2 * tiles) {
+      g.sk_slab = sk_slab->data_ptr<float>();
+      g.sk_flags = sk_flags->data_ptr<int>();
+    }
+  }
   c10::DeviceGuard guard(A.device());
   if (variant == 2)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
+  if (variant == 5)
+    TORCH_CHECK(g.sk_slab && M % 256 == 0 && N % 128 == 0 && K % 128 == 0 && ((M / 256) * (N / 128)) % 8 == 0,
+                "dgt: the split-K gemm needs its workspace, M % 256 == 0, N % 128 == 0, K % 128 == 0 and a tile "
+                "count divisible by 8");
   DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A), (int)variant));
 }
 
@@ -714,7 +730,7 @@ TORCH_LIBRARY(dgt, m) {
       &oneshot_allreduce);
   m.def(
       "gemm_nt(Tensor A, Tensor B, Tensor(a!)? C, Tensor(b!)? CT, Tensor? bias, Tensor? mask, int epi, "
-      "float alpha, int variant=0) -> ()",
+      "float alpha, int variant=0, Tensor(c!)? sk_slab=None, Tensor(d!)? sk_flags=None) -> ()",
       &gemm_nt);
   m.def("transpose_bf16(Tensor inp, Tensor(a!) out) -> ()", &transpose_bf16);
   m.def("rowsum_bf16(Tensor inp, Tensor(a!) out, bool accumulate) -> ()", &rowsum_bf16);

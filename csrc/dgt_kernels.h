@@ -135,6 +135,8 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   int lda, ldb, ldc, ldct, ldmask;
   float alpha;
   GemmAdam adam;       // kEpiAdam only (the gradient is alpha * A . B^T; ldc = row stride of the weight)
+  float* sk_slab;      // split-K kernel (variant 5): fp32 partial tiles, (M/256)(N/128) x 256 x 128
+  int* sk_flags;       // split-K kernel: 2 ints per tile (arrivals, slab ready), zero between launches
 };
 
 hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream, int variant = 0);

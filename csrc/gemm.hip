@@ -458,6 +458,185 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
   }
 }
 
+// ------------------------------------------------------------------ 256 x 128 tile, split-K 2
+// For the MLP's M = 1024 products (forward a . W^T and dgrad g . W at N = K = 4096): a 128 x 128
+// tile per CU (the only way 256 tiles fill 256 CUs without splitting K) re-reads 64 B of operand per
+// 2 x 64 x 64 x 2 FLOP, and those reads - global -> LDS staging and LDS fragment reads - bound the
+// loop (profiles/r1_gemm128_ablation.txt).  Here a block owns a 256 x 128 tile over HALF of K:
+// 25 % fewer staged bytes per FLOP and 64 x 64 wave tiles (4 (M) x 2 (N) waves of 4 x 4
+// accumulators: 33 % fewer LDS fragment bytes per FLOP than the 64 x 32 wave tiles of the 8-wave
+// 128 kernel), and M = 1024 still gives 4 x 32 tiles x 2 halves = 256 blocks.
+// The halves meet through a per-tile arrival counter: the first to finish writes its fp32 partial
+// tile (128 KiB) to the slab and publishes it (agent-scope release, flag); the second waits for
+// the flag (acquire), adds the slab to its accumulators (fp32 a + b == b + a: the result does not
+// depend on which half came first) and runs the fused epilogue.  Only the FIRST block ever waits
+// on nothing and the waiting block's partner has already arrived, so no co-residency is assumed.
+// Blocks 8 apart share an XCD: both halves of a tile get ids 8 apart (same XCD, slab in that
+// XCD's L2), and each XCD takes a contiguous range of tiles, M-tiles fastest (T1).
+namespace sk {
+constexpr int BM = 256, BN = 128, BK = 64, S = 3, NW = 8;
+constexpr int A_ELEMS = BM * BK, B_ELEMS = BN * BK, STAGE = A_ELEMS + B_ELEMS;  // u16 per stage (48 KiB)
+constexpr int PW_A = (BM / 8) / NW;  // A: 1 KiB wave-instructions (8 rows x 128 B) per wave = 4
+constexpr int PW_B = 16 / NW;        // B: [N,K] 8 rows x 128 B, or [K,N] 4 k-rows x 256 B = 2
+constexpr int PER_TILE = PW_A + PW_B;
+
+template <bool KN>
+struct Stage {
+  const u16* pa[PW_A];
+  const u16* pb[PW_B];
+  int la[PW_A], lb[PW_B];
+  long long stepb;
+  DGT_DEVICE Stage(const u16* A, int lda, int m0, const u16* B, int ldb, int n0, int k0, int w, int l) {
+#pragma unroll
+    for (int i = 0; i < PW_A; ++i) {
+      const int rblk = (w * PW_A + i) * 8, row = rblk + (l >> 3);
+      const int c = (l & 7) ^ (row & 7);
+      pa[i] = A + (long long)(m0 + row) * lda + k0 + c * 8;
+      la[i] = rblk * BK;
+    }
+#pragma unroll
+    for (int i = 0; i < PW_B; ++i) {
+      if constexpr (KN) {
+        const int rblk = (w * PW_B + i) * 4, row = rblk + (l >> 4);
+        const int c = (l & 15) ^ kn_swz(row);
+        pb[i] = B + (long long)(k0 + row) * ldb + n0 + c * 8;
+        lb[i] = rblk * BN;
+      } else {
+        const int rblk = (w * PW_B + i) * 8, row = rblk + (l >> 3);
+        const int c = (l & 7) ^ (row & 7);
+        pb[i] = B + (long long)(n0 + row) * ldb + k0 + c * 8;
+        lb[i] = rblk * BK;
+      }
+    }
+    stepb = KN ? (long long)BK * ldb : BK;
+  }
+  DGT_DEVICE void issue(u16* st) {
+#pragma unroll
+    for (int i = 0; i < PW_A; ++i) {
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(pa[i]), reinterpret_cast<int*>(st + la[i]), 16, 0,
+                                       0);
+      pa[i] += BK;
+    }
+#pragma unroll
+    for (int i = 0; i < PW_B; ++i) {
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(pb[i]),
+                                       reinterpret_cast<int*>(st + A_ELEMS + lb[i]), 16, 0, 0);
+      pb[i] += stepb;
+    }
+  }
+};
+}  // namespace sk
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_nt_sk_kernel(GemmArgs g) {
+  using namespace sk;
+  constexpr bool KN = (EPI & kEpiBKN) != 0;
+  __shared__ __attribute__((aligned(16))) u16 lds[S * STAGE];  // ONE array: 144 KiB
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int wr = w >> 1, wc = w & 1;  // 4 (M) x 2 (N) waves of 64 x 64
+  const int MT = g.M / BM, T = MT * (g.N / BN);
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3, half = slot & 1;
+  const int t = xcd * (T / 8) + (slot >> 1);
+  const int m0 = (t % MT) * BM, n0 = (t / MT) * BN;
+  const int kh = g.K / 2, nk = kh / BK;
+  const u16* A = static_cast<const u16*>(g.A);
+  const u16* B = static_cast<const u16*>(g.B);
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  Stage<KN> st(A, g.lda, m0, B, g.ldb, n0, half * kh, w, l);
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p)
+    if (p < nk) st.issue(lds + p * STAGE);
+  int buf = 0;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tiles kt .. min(kt + S - 2, nk - 1) are in flight; retire tile kt
+    if (kt + S - 2 < nk) wait_vmcnt<(S - 2) * PER_TILE>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // tile kt visible to every wave; the buffer of kt - 1 is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + S - 1 < nk) st.issue(lds + ((buf + S - 1) % S) * STAGE);
+    const u16* As = lds + buf * STAGE;
+    const u16* Bs = As + A_ELEMS;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int chunk = kk * 4 + (l >> 4);
+      bf16x8 af[4], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[i] = read_frag(As, wr * 64 + i * 16 + (l & 15), chunk);
+      if constexpr (KN) {
+        i16x4 blo[4], bhi[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) read_frag_kn(Bs, kk * 32, wc * 64 + j * 16, l, blo[j], bhi[j]);
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = tr_wait(blo[j], bhi[j]);
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j) bfr[j] = read_frag(Bs, wc * 64 + j * 16 + (l & 15), chunk);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    buf = (buf + 1 == S) ? 0 : buf + 1;
+  }
+  __builtin_amdgcn_s_barrier();  // every wave is done with the operand stages
+
+  // ---- split-K meeting point (cdna_hip_programming.md, projection GEMM item 2 / Guideline 16)
+  int* arrive = g.sk_flags + 2 * t;
+  int* ready = arrive + 1;
+  float* slab = g.sk_slab + (long long)t * BM * BN;
+  int* order = reinterpret_cast<int*>(lds);  // in the one LDS array (operands are dead)
+  if (tid == 0) *order = __hip_atomic_fetch_add(arrive, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  __syncthreads();
+  const bool first = *order == 0;
+  if (first) {
+    // publish (Guideline 16 R1): write-through (sc1) stores of the partial tile, drained by EVERY
+    // storing wave, barrier, ONE relaxed agent-scope flag store: no release fence (no L2 writeback)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int rr = 0; rr < 4; ++rr)
+          __hip_atomic_store(slab + (wr * 64 + i * 16 + 4 * (l >> 4) + rr) * BN + wc * 64 + j * 16 + (l & 15),
+                             acc[i][j][rr], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_store(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return;
+  }
+  if (tid == 0) {
+    // the partner has arrived (the counter said so): it is writing the slab.  Bounded all the same
+    // (~0.5 s), so a corrupted flag can only produce a wrong tile, never a hung GPU
+    for (int spin = 0; spin < (1 << 24) && __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+         ++spin)
+      __builtin_amdgcn_s_sleep(1);
+    // both halves are past their last use of the flags: re-arm them for the next launch
+    __hip_atomic_store(arrive, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(ready, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  __syncthreads();
+  // every load of the slab is an sc1 (agent-scope) load: it bypasses this CU's L1, so no acquire
+  // fence is needed (Guideline 16: all payload stores sc1 + drained, flag atomic, all loads sc1)
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+#pragma unroll
+      for (int rr = 0; rr < 4; ++rr)
+        acc[i][j][rr] += __hip_atomic_load(slab + (wr * 64 + i * 16 + 4 * (l >> 4) + rr) * BN + wc * 64 + j * 16 + (l & 15),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  epilogue_staged<EPI, BM, BN, 64, 64, 512>(g, acc, lds, m0, n0, wr, wc, l, tid);
+}
+
 // ------------------------------------------------------------------ 256 x 256 tile, 8-phase pipeline
 // For large M x N (>= ~200 tiles): 512 threads = 8 waves in 2 (M) x 4 (N), each wave 128 x 64 =
 // 8 x 4 accumulators of 16x16 (128 VGPRs).  A K-tile (BK = 64) of A and of B is staged as four
@@ -670,9 +849,36 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 }
 
 // variant: 0 = pick by shape, 1 = 128x128 2-stage, 2 = 256x256 8-phase, 3 = 128x128 4-stage,
-// 4 = 128x128 4-stage with 8 waves
+// 4 = 128x128 4-stage with 8 waves, 5 = 256x128 split-K 2 (needs the sk workspace)
+static bool sk_fits(const GemmArgs& g) {
+  const int T = (g.M % 256 == 0 && g.N % 128 == 0) ? (g.M / 256) * (g.N / 128) : 0;
+  return T > 0 && T % 8 == 0 && g.K % 128 == 0 && g.sk_slab && g.sk_flags;
+}
+
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
+  // split-K 256 x 128 (variant 5) on request only: on the M = 1024 MLP products it ties the 8-wave
+  // 128 x 128 kernel (fwd 46.2 vs 48.1 us hot, 53.9 vs 53.4 cold; dgrad 50.7 vs 49.5 hot,
+  // profiles/r2_gemm_m1024.jsonl), so the shape-picked default stays the 128 x 128 kernel
+  const bool sk_epi = !(epi & (kEpiOutF32 | kEpiAccumulate | kEpiAdam));
+  if (variant == 5 && (!sk_fits(g) || !sk_epi)) return hipErrorInvalidValue;
+  const bool use_sk = variant == 5;
+  if (use_sk) {
+    const int grid = (g.M / 256) * (g.N / 128) * 2;
+    switch (epi) {
+#define DGT_SK_CASE(E) \
+  case E: hipLaunchKernelGGL((gemm_nt_sk_kernel<E>), dim3(grid), dim3(512), 0, stream, g); return hipGetLastError();
+      DGT_SK_CASE(0)
+      DGT_SK_CASE(kEpiBias | kEpiRelu | kEpiStoreT)
+      DGT_SK_CASE(kEpiBias | kEpiRelu)
+      DGT_SK_CASE(kEpiMask | kEpiStoreT)
+      DGT_SK_CASE(kEpiMask | kEpiStoreT | kEpiBKN)
+      DGT_SK_CASE(kEpiBKN)
+#undef DGT_SK_CASE
+      default:
+        if (variant == 5) return hipErrorInvalidValue;  // no split-K instance: fall through to the others
+    }
+  }
   const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0;
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks,
   // 2 blocks per CU) wins

@@ -42,7 +42,8 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
             out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0,
             b_kn: bool = False) -> None:
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage, 2 = 256x256 8-phase pipeline,
-    3 = 128x128 tiles 4-stage, 4 = 128x128 tiles 4-stage with 8 waves.
+    3 = 128x128 tiles 4-stage, 4 = 128x128 tiles 4-stage with 8 waves, 5 = 256x128 tiles with K
+    split over two blocks that meet through a per-tile counter (the M = 1024 MLP products).
 
     ``b_kn=True``: B is given as ``[K, N]`` (N contiguous) and ``C = alpha * A @ B`` — the operand is
     staged as it lies and read with transposed LDS reads (128x128 kernels only)."""
@@ -52,7 +53,27 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     epi = ((EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | (EPI_MASK if mask is not None else 0)
            | (EPI_STORE_T if CT is not None else 0) | (EPI_OUT_F32 if out_f32 else 0)
            | (EPI_ACCUMULATE if accumulate else 0) | (EPI_B_KN if b_kn else 0))
-    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant))
+    M, N = A.shape[0], B.shape[1] if b_kn else B.shape[0]
+    slab, flags = _sk_workspace(A.device, M, N) if variant == 5 and not out_f32 else (None, None)
+    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant), slab, flags)
+
+
+_SK: dict = {}
+
+
+def _sk_workspace(device: torch.device, M: int, N: int):
+    """Workspace of the split-K kernel (variant 5): fp32 partial tiles + zeroed per-tile flags that
+    the kernel re-arms.  One per (device, stream): launches sharing it are stream-ordered."""
+    if M % 256 or N % 128 or ((M // 256) * (N // 128)) % 8:
+        return None, None
+    tiles = (M // 256) * (N // 128)
+    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
+    ws = _SK.get(key)
+    if ws is None or ws[1].numel() < 2 * tiles:
+        ws = (torch.empty(tiles * 256 * 128, dtype=torch.float32, device=device),
+              torch.zeros(2 * tiles, dtype=torch.int32, device=device))
+        _SK[key] = ws
+    return ws
 
 
 def gemm_nt_adam_(A: torch.Tensor, B: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor,

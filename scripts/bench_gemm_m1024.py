@@ -1,0 +1,36 @@
+#!/usr/bin/env python3
+"""The bf16 MLP's M = 1024 products (forward a . W^T with bias + ReLU + C^T, dgrad g . W with the
+ReLU mask + C^T, W given as [K, N]) on every kernel that can run them, hot and with caches flushed,
+against torch.matmul (hipBLASLt, no epilogue).  Random N(0,1) data.  One JSON line per arm."""
+import json
+import os
+import sys
+
+import torch
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from distributed_gpu_test_amd.ops.gemm import gemm_nt  # noqa: E402
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+from bench_gemm import bench, bench_cold  # noqa: E402
+
+M, N, K = 1024, 4096, 4096
+a = torch.randn(M, K, device="cuda").bfloat16()
+w = torch.randn(N, K, device="cuda").bfloat16()
+g = torch.randn(M, N, device="cuda").bfloat16()
+C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+CT = torch.empty(N, M, device="cuda", dtype=torch.bfloat16)
+bias = torch.randn(N, device="cuda")
+mask = (torch.randn(M, N, device="cuda") > 0).bfloat16()
+arms = {}
+for v in (4, 5):
+    arms[f"fwd plain v{v}"] = lambda v=v: gemm_nt(a, w, C=C, variant=v)
+    arms[f"fwd bias+relu+T v{v}"] = lambda v=v: gemm_nt(a, w, C=C, CT=CT, bias=bias, relu=True, variant=v)
+    arms[f"dgrad [K,N] mask+T v{v}"] = lambda v=v: gemm_nt(g, w, C=C, CT=CT, mask=mask, b_kn=True, variant=v)
+arms["hipBLASLt a @ W^T"] = lambda: torch.matmul(a, w.t(), out=C)
+arms["hipBLASLt g @ W"] = lambda: torch.matmul(g, w, out=C)
+for name, fn in arms.items():
+    hot = bench(fn, iters=40, warmup=10)
+    cold = bench_cold(fn, iters=10)
+    print(json.dumps({"arm": name, "hot_us": round(hot * 1e6, 1), "cold_us": round(cold * 1e6, 1),
+                      "hot_TFLOPs": round(2 * M * N * K / hot / 1e12, 1)}), flush=True)

@@ -315,3 +315,44 @@ def test_mlp_fused_adam_matches_unfused_fp32_grads():
     for a, b in zip(outs[0][:4], outs[1][:4]):
         assert torch.equal(a, b)
     assert outs[0][4] == outs[1][4]
+
+
+@gpu
+@pytest.mark.parametrize("M,N,K", [(512, 512, 128), (1024, 1024, 256), (1024, 4096, 512)])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "mask_T", "kn_plain", "kn_mask_T"])
+def test_gemm_splitk_matches_reference(M, N, K, epi):
+    """The 256x128 split-K kernel (variant 5: two blocks per tile meet through a counter and an fp32
+    slab): three launches in a row (the kernel re-arms its per-tile flags), each against fp32."""
+    g = torch.Generator().manual_seed(M + 3 * N + K)
+    kn = epi.startswith("kn")
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    B = torch.randn(*((K, N) if kn else (N, K)), generator=g).to(torch.bfloat16).cuda()
+    bias = torch.randn(N, generator=g).cuda()
+    mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).cuda()
+    kw = {}
+    if epi == "bias_relu_T":
+        kw = dict(bias=bias, relu=True)
+    elif epi.endswith("mask_T"):
+        kw = dict(mask=mask)
+    ref = gemm_nt_reference(A.cpu(), B.cpu(), b_kn=kn, **{k: (v.cpu() if torch.is_tensor(v) else v)
+                                                          for k, v in kw.items()}).cuda()
+    for _ in range(3):
+        C = torch.full((M, N), float("nan"), dtype=torch.bfloat16).cuda()
+        CT = torch.full((N, M), float("nan"), dtype=torch.bfloat16).cuda() if epi.endswith("_T") else None
+        gemm_nt(A, B, C=C, CT=CT, variant=5, b_kn=kn, **kw)
+        torch.testing.assert_close(C.float(), ref.to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2 * K ** 0.5)
+        if CT is not None:
+            torch.testing.assert_close(CT.float(), ref.t().to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2 * K ** 0.5)
+
+
+@gpu
+@pytest.mark.parametrize("kn", [False, True])
+def test_gemm_splitk_identity_asymmetric(kn):
+    """A = I with an asymmetric integer B: exact in bf16, so any transposed fragment, wrong half of
+    K or wrong slab tile shows up as a mismatch."""
+    n = 512
+    A = torch.eye(n, dtype=torch.bfloat16).cuda()
+    B = torch.arange(n * n, dtype=torch.float32).remainder(251).reshape(n, n).to(torch.bfloat16).cuda()
+    C = torch.empty(n, n, dtype=torch.bfloat16).cuda()
+    gemm_nt(A, B, C=C, variant=5, b_kn=kn)
+    assert torch.equal(C, B if kn else B.t().contiguous())
