@@ -571,7 +571,9 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     double total = 0.0;
 #pragma unroll
     for (int i = 0; i < C::NW; ++i) total += sm.loss[i];
-    *a.loss_acc += total;
+    // no-return atomic add: the epilogue does not wait a load round trip for the old value (one
+    // writer per launch, so the sum is the same as a read-modify-write)
+    __hip_atomic_fetch_add(a.loss_acc, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *a.status = sm.err ? kTimeout : kOk;
   }
 }
