@@ -167,12 +167,12 @@ def timed_run(trainer, plan, counts, args, device, comm):
         for s in range(head, args.warmup):
             trainer.run_plan(plan[s:s + 1], counts[s:s + 1])
     timed_plan, timed_counts = plan[args.warmup:], counts[args.warmup:]  # views; the upload happened in build_plan
+    trainer.loss_acc.zero_()  # queued behind the warmup: the bracket's opening sync has nothing left to wait on
     if device.type == "cuda":
         torch.cuda.synchronize()
     failed = _failed(trainer)
     if comm.all_reduce_max(float(failed)) > 0:
         raise RuntimeError("warmup failed on some rank")
-    trainer.loss_acc.zero_()
     barrier = comm.barrier if comm.collectives_on() else (lambda: None)  # a 1-rank barrier is a no-op
     gpu = device.type == "cuda"
     barrier()

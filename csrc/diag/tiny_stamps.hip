@@ -89,7 +89,11 @@ int main(int argc, char** argv) {
   CK(hipMemcpy(st, dStamps, sizeof(st), hipMemcpyDeviceToHost));
   const char* names[5] = {"prefetch+fwd GEMM+partial z", "barrier wait", "loss+bwd+wgrad MFMA",
                           "stage next batch+grad regs", "Adam (packed fp32)"};
-  printf("stamped build: %.3f us/step (%d steps)\n", ms * 1e3 / steps, steps);
+  printf("stamped build: %.3f us/step (%d steps), launch event-to-event %.2f us\n", ms * 1e3 / steps, steps,
+         ms * 1e3);
+  printf("phases of wave 0 (s_memrealtime, 10 ns ticks): operands landed %.2f us, prologue barrier %.2f us, "
+         "loop %.2f us, epilogue + store completion %.2f us\n",
+         st[5] * 0.01, st[6] * 0.01, st[7] * 0.01, st[13] * 0.01);
   for (int w = 0; w < 2; ++w) {
     unsigned long long tot = 0;
     for (int i = 0; i < 5; ++i) tot += st[w * 8 + i];

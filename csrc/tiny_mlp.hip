@@ -333,6 +333,9 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar branches on w
   const Exchange& ex = a.ex;
   WaveSmem<F, H>& ws = sm.w[w];
+#ifdef DGT_TINY_STAMPS
+  const unsigned long long rt_entry = realtime();
+#endif
 
   if (a.bmax > (SMALLB ? 4 : C::BM) || a.bmax < 1 || (ex.world_size > 1) != XCH || ex.world_size > NP ||
       (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3)))) {
@@ -352,7 +355,13 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   int idx_next2 = plan_at(a.plan, a.n_steps, a.bmax, 2, lr);
   fill_bias_table<C::T>(a, t);
   __builtin_amdgcn_s_waitcnt(0);  // the table's stores have reached L2 before any wave reads it
+#ifdef DGT_TINY_STAMPS
+  const unsigned long long rt_loaded = realtime();
+#endif
   __syncthreads();
+#ifdef DGT_TINY_STAMPS
+  const unsigned long long rt_loop = realtime();
+#endif
 
   double loss_total = 0.0;
   float zs = 0.f, ys = 0.f, ibs = 0.f;  // deferred-loss ring (wave 0)
@@ -543,6 +552,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
 #ifdef DGT_TINY_STAMPS
   if (a.stamps && l == 0 && w < 2)
     for (int i = 0; i < 5; ++i) a.stamps[w * 8 + i] = st_acc[i];
+  const unsigned long long rt_loop_end = realtime();
 #endif
 
   // ---- epilogue: state back to HBM (b2 belongs to wave 0, lane 0)
@@ -576,6 +586,17 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     __hip_atomic_fetch_add(a.loss_acc, total, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     *a.status = sm.err ? kTimeout : kOk;
   }
+#ifdef DGT_TINY_STAMPS
+  // phase split in s_memrealtime ticks (10 ns) of wave 0: [5] entry -> operands landed,
+  // [6] -> past the prologue barrier, [7] loop, [13] epilogue incl. its stores' completion
+  __builtin_amdgcn_s_waitcnt(0);
+  if (a.stamps && t == 0) {
+    a.stamps[5] = rt_loaded - rt_entry;
+    a.stamps[6] = rt_loop - rt_loaded;
+    a.stamps[7] = rt_loop_end - rt_loop;
+    a.stamps[13] = realtime() - rt_loop_end;
+  }
+#endif
 }
 
 // One step's gradient only (the RCCL path: grad -> all_reduce -> adam_flat).
