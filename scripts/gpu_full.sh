@@ -12,6 +12,11 @@ tail -1 gpurun_out/smoke.log
 echo "== bench default"
 timeout -k 10 300 python bench.py > gpurun_out/bench_default.json 2> gpurun_out/bench_default.err || { tail -20 gpurun_out/bench_default.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/bench_default.json')); print(d['value'], d['ms_per_step'])"
+echo "== bench, the driver's shape"
+for i in 1 2 3; do
+  DGT_BENCH_BREAKDOWN=1 timeout -k 10 120 python bench.py --steps 20 --warmup 5 > gpurun_out/bench_driver_$i.json 2> gpurun_out/bench_driver_$i.err || { tail -20 gpurun_out/bench_driver_$i.err; exit 1; }
+  python -c "import json; d=json.load(open('gpurun_out/bench_driver_$i.json')); print(d['value'], d['ms_per_step'])"
+done
 echo "== bench mlp"
 timeout -k 10 300 python bench.py --model mlp --steps 100 --warmup 10 > gpurun_out/bench_mlp.json 2> gpurun_out/bench_mlp.err || { tail -20 gpurun_out/bench_mlp.err; exit 1; }
 python -c "import json; d=json.load(open('gpurun_out/bench_mlp.json')); print(d['value'], d['ms_per_step'], d['model_tflops'])"

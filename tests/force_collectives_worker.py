@@ -88,8 +88,10 @@ def mlp_case(schedule, stage):
 
     def fn():
         torch.manual_seed(3)
+        # fuse_adam=False: the single-rank fused wgrad+Adam exists only WITHOUT collectives, so both
+        # runs of the pair must take the gradient-buffer path the N > 1 schedules use
         tr = MLPTrainer(SyntheticMLP(width=256, depth=3), batch_size=128, n_batches=2, lr=1e-3,
-                        device=torch.device("cuda", 0), zero_stage=stage, schedule=schedule)
+                        device=torch.device("cuda", 0), zero_stage=stage, schedule=schedule, fuse_adam=False)
         for s in range(5):
             tr.step(s)
         tr.join()
