@@ -7,7 +7,9 @@
 #include <c10/core/DeviceGuard.h>
 #include <torch/library.h>
 
+#include <cstdlib>
 #include <cstring>
+#include <string>
 #include <vector>
 
 #include "dgt_kernels.h"
@@ -43,6 +45,19 @@ dgt::AdamHyper make_hyper(double lr, double beta1, double beta2, double eps, dou
   return h;
 }
 
+// Exchange shape of the fused kernel at this world size: DGT_XCH=oneshot|twoshot|auto.  auto is the
+// one-shot at every size: rehearsed with 4 and 8 ranks on one card the two-shot's second hop costs
+// more than its ~4x smaller polls save (6.5 vs 3.6 us/step at 4 ranks, 12.8 vs 6.9 at 8;
+// profiles/r2_xch_exchange_ab.txt).  Every rank of a job inherits the same environment, so every
+// rank picks the same protocol (the kernel rejects a mismatch with its template as a bad shape).
+int exchange_two_shot(int64_t world_size) {
+  const char* e = std::getenv("DGT_XCH");
+  const std::string m = e ? e : "auto";
+  TORCH_CHECK(m == "auto" || m == "oneshot" || m == "twoshot", "dgt: DGT_XCH must be auto, oneshot or twoshot, got ", m);
+  if (world_size < 4) return 0;  // the two-shot kernels exist for 4+ ranks only
+  return m == "twoshot";
+}
+
 dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank,
                             int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks) {
   dgt::Exchange ex;
@@ -55,6 +70,7 @@ dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank,
   ex.seq_base = seq_base;
   ex.timeout_ticks = timeout_ticks;
   ex.corrupt_step = -1;
+  ex.two_shot = exchange_two_shot(world_size);
   if (world_size > 1) {
     TORCH_CHECK((int64_t)data_ptrs.size() == world_size, "dgt: need one mailbox pointer per rank");
     TORCH_CHECK(stride > 0 && stride % 256 == 0, "dgt: mailbox stride must be a positive multiple of 256 floats");

@@ -51,6 +51,8 @@ struct Exchange {
   unsigned* data[kMaxRanks];        // each rank's mailbox (index rank = local)
   long long corrupt_step;           // fault injection: at this 1-based optimizer step the fused kernel
                                     // corrupts one payload it sends to rank + 1 (-1 = never)
+  int two_shot;                     // fused kernel: reduce-scatter + all-gather instead of one-shot
+                                    // (4+ ranks only; see exchange_two_shot() in bindings.cpp)
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -75,6 +77,19 @@ DGT_DEVICE unsigned long long ll_get(const unsigned* src) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 DGT_DEVICE bool ll_ok(unsigned long long pair, unsigned tag) { return (unsigned)(pair >> 32) == tag; }
+// LL3 line: three payload floats and the tag in ONE 16-byte store / load, relying on an aligned
+// 16-byte access being single-copy atomic (one request to one 64-byte line on both ends, as
+// RCCL's LL128 relies on for whole 128-byte lines).  Were a line ever observed torn, the ranks'
+// parameters would diverge and the per-epoch replica check fails the job.  The poll loop must
+// re-issue the load every round (ll_fence_compiler() at the top of the loop).
+DGT_DEVICE void ll3_put(unsigned* dst, float a, float b, float c, unsigned tag) {
+  u32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), tag};
+  *reinterpret_cast<u32x4*>(dst) = v;
+}
+DGT_DEVICE u32x4 ll3_get(const unsigned* src) {
+  return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
+}
+DGT_DEVICE void ll_fence_compiler() { asm volatile("" ::: "memory"); }
 DGT_DEVICE float ll_val(unsigned long long pair) { return __uint_as_float((unsigned)pair); }
 
 // Full-row DPP permutations (quad_perm, row mirrors, row_newbcast) have a source lane for every

@@ -67,8 +67,14 @@ struct TinyCfg {
   static constexpr int REM = F + 1 - 16 * (NKT - 1);      // live k in the last tile (1..16)
   static constexpr int NSL = 4 * (NKT - 1) + (REM + 3) / 4;  // slots holding any live k
   static constexpr int NSP = NSL + (NSL & 1);    // rounded up to packed-fp32 pairs (extra slot stays 0)
-  static constexpr int NQ = (NSL + 2 + 3) / 4;   // float4s per lane in the exchange (W1 slots, W2, b2)
-  static constexpr int XCH = NW * NQ * 256;      // exchange floats per (parity, rank) mailbox slot
+  // Exchange payload per lane.  DENSE: the last W1 slot is live only in lane row lq == 0 (REM % 4
+  // == 1, e.g. F = 20), so its 48 dead lanes carry the W2 gradients (12 in place, 4 moved from
+  // lanes 0-3 to 20-23) and b2 (lane 24): NSL floats per lane.  Otherwise the W1 slots, W2 and b2
+  // padded to float4s.  Each LL3 line carries three payload floats and the tag.
+  static constexpr bool DENSE = (REM & 3) == 1 && NSL >= 2;
+  static constexpr int NPAY = DENSE ? NSL : NSL + 2;
+  static constexpr int NLINE = (NPAY + 2) / 3;   // LL3 lines per lane and peer
+  static constexpr int XCH = NW * NLINE * 128;   // mailbox slot = 2*XCH words = NW*NLINE lines of 1 KiB
   static constexpr int SX = NKT * 16 + 1;        // LDS row stride of the staged batch (+1: conflict-free)
   static constexpr int BM = 16;                  // max micro-batch (MFMA N of the forward)
   static constexpr int P = H * F + 2 * H + 1;    // global flat parameter count
@@ -322,12 +328,111 @@ DGT_DEVICE void fill_bias_table(const TinyTrainArgs& a, int t) {
 // branch, so backward and Adam form one basic block the scheduler can interleave.
 // WD: weight decay != 0 (Adam's L2 term / AdamW's decay compiled in; the reference's Adam has none,
 // and the per-pair uniform branches cost ~12 scalar branches per step).
-template <int F, int H, bool SMALLB, int NP, bool WD>
+// Poll every peer's NPAY/2 LL lines of this lane in the local mailbox until all carry `tag` (or
+// the timeout passes: late), then sum them with the lane's own payload in rank order.  Every retry
+// re-reads all peers: one local round trip per poll, not one per line or per peer.  (Spinning on
+// one line per peer first and reading the rest after measured slower: the extra round trip costs
+// more than the smaller polls save, profiles/r2_xch_exchange_ab.txt.)
+template <int NPAY, int NP>
+DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, unsigned tag,
+                               const float (&pay)[NPAY], float (&sum)[NPAY], unsigned long long t0, bool& late) {
+  constexpr int NL = (NPAY + 2) / 3;
+  u32x4 v[NP][NL];
+  bool ready;
+  do {
+    ll_fence_compiler();
+    ready = true;
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      if (p < ex.world_size && p != ex.rank) {
+        const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, p) + wofs;
+#pragma unroll
+        for (int j = 0; j < NL; ++j) v[p][j] = ll3_get(src + j * 256);
+      }
+    }
+#pragma unroll
+    for (int p = 0; p < NP; ++p) {
+      if (p < ex.world_size && p != ex.rank) {
+#pragma unroll
+        for (int j = 0; j < NL; ++j) ready = ready && v[p][j][3] == tag;
+      }
+    }
+    if (!ready && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
+  } while (!ready && !late);
+#pragma unroll
+  for (int p = 0; p < NP; ++p) {
+    if (p >= ex.world_size) continue;
+#pragma unroll
+    for (int k = 0; k < NPAY; ++k) sum[k] += p == ex.rank ? pay[k] : __uint_as_float(v[p][k / 3][k % 3]);
+  }
+}
+
+// push this lane's payload into one peer's mailbox as LL3 lines (c0 replaces pay[0]: fault injection)
+template <int NPAY>
+DGT_DEVICE void push_payload(unsigned* dst, const float (&pay)[NPAY], float c0, unsigned tag) {
+#pragma unroll
+  for (int j = 0; j < (NPAY + 2) / 3; ++j) {
+    const int k = 3 * j;
+    ll3_put(dst + j * 256, j == 0 ? c0 : pay[k], k + 1 < NPAY ? pay[k + 1] : 0.f, k + 2 < NPAY ? pay[k + 2] : 0.f, tag);
+  }
+}
+
+// gradients of one lane -> exchange payload (see TinyCfg::DENSE for the dense layout)
+template <int F, int H>
+DGT_DEVICE void pack_payload(const float (&gw1)[TinyCfg<F, H>::NSP], float gbw, float gb2, int l,
+                             float (&pay)[TinyCfg<F, H>::NPAY]) {
+  using C = TinyCfg<F, H>;
+  const int lr = l & 15, lq = l >> 4;
+  if constexpr (C::DENSE) {
+    const float moved = __shfl(gbw, (l + 44) & 63);  // lanes 20-23 take the W2 gradients of lanes 0-3
+#pragma unroll
+    for (int i = 0; i < C::NSL - 1; ++i) pay[i] = gw1[i];
+    pay[C::NSL - 1] = lq == 0 ? gw1[C::NSL - 1]
+                    : lr < 4  ? gbw
+                    : (lq == 1 && lr < 8) ? moved
+                    : l == 24 ? gb2
+                              : 0.f;
+  } else {
+#pragma unroll
+    for (int i = 0; i < C::NPAY; ++i) pay[i] = i < C::NSL ? gw1[i] : (i == C::NSL ? gbw : (i == C::NSL + 1 ? gb2 : 0.f));
+  }
+}
+
+// summed payload -> mean gradients of the lane (sum first, then the 1/world scale, as before the
+// dense layout: the same bits)
+template <int F, int H>
+DGT_DEVICE void unpack_payload(const float (&sum)[TinyCfg<F, H>::NPAY], float inv_ws, int l,
+                               float (&gw1)[TinyCfg<F, H>::NSP], float& gbw, float& gb2) {
+  using C = TinyCfg<F, H>;
+  const int lr = l & 15, lq = l >> 4;
+  if constexpr (C::DENSE) {
+    const float last = sum[C::NSL - 1];
+    const float back = __shfl(last, (l + 20) & 63);  // lanes 0-3 take their W2 sums back from 20-23
+#pragma unroll
+    for (int i = 0; i < C::NSL - 1; ++i) gw1[i] = sum[i] * inv_ws;
+    gw1[C::NSL - 1] = lq == 0 ? last * inv_ws : 0.f;
+    gbw = lr < 4 ? (lq == 0 ? back : last) * inv_ws : 0.f;
+    gb2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(last), 24)) * inv_ws;
+  } else {
+#pragma unroll
+    for (int i = 0; i < C::NPAY; ++i) {
+      const float v = sum[i] * inv_ws;
+      if (i < C::NSL) gw1[i] = v;
+      else if (i == C::NSL) gbw = v;
+      else if (i == C::NSL + 1) gb2 = v;
+    }
+  }
+}
+
+template <int F, int H, bool SMALLB, int NP, bool WD, bool TS>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
   // NP: ranks the exchange is compiled for (1 = none; else the world size rounded up to 2, 4 or 8):
-  // the poll registers scale with it, so 2- and 4-rank jobs do not carry the 8-rank register set
+  // the poll registers scale with it, so 2- and 4-rank jobs do not carry the 8-rank register set.
+  // TS: two-shot exchange (reduce-scatter to lane owners, then all-gather of the sums) instead of
+  // the one-shot all-to-all
   constexpr bool XCH = NP > 1;
+  static_assert(!TS || XCH, "the two-shot exchange needs an exchange");
   __shared__ TinySmem<F, H> sm;
   const int t = threadIdx.x, l = t & 63, lr = l & 15, lq = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar branches on w
@@ -338,7 +443,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
 #endif
 
   if (a.bmax > (SMALLB ? 4 : C::BM) || a.bmax < 1 || (ex.world_size > 1) != XCH || ex.world_size > NP ||
-      (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3)))) {
+      (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3))) || (ex.two_shot != 0) != TS) {
     if (t == 0) *a.status = kBadShape;
     return;
   }
@@ -417,97 +522,81 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     DGT_STAMP(3);
 
     if constexpr (XCH) {
-      // ---- one-shot LL exchange of this wave's gradients over xGMI: push, poll, sum in rank order.
+      // ---- LL exchange of this wave's gradients over xGMI: push, poll, sum in rank order.
       // Every rank maps lanes to parameters identically, so the mailbox is lane-linear: lane l of
-      // wave w packs its slots into NQ float4s = 2*NQ LL lines at [w][line][l]; every store
-      // instruction writes 1 KiB contiguous into a peer, every poll reads the local mailbox.
+      // wave w packs its gradients into NPAY floats = NLINE LL lines at [w][line][l]; every store
+      // instruction writes 1 KiB contiguous into a peer, every poll reads the local mailbox.  The
+      // wave's memory-instruction throughput on uncached memory (~11 ns per 1 KiB instruction and
+      // CU, csrc/diag/store_lat.hip), not the round trip, bounds the exchange at 4-8 ranks: hence
+      // the dense payload (3 lines per peer instead of 4 for F = 20).
       const long long seq = ex.seq_base + s;
       const int parity = (int)(seq & 1);
       const unsigned tag = (unsigned)(seq + 1);
-      f32x4 pk[C::NQ];
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * q + e;
-          pk[q][e] = i < C::NSL ? gw1[i] : (i == C::NSL ? gbw : (i == C::NSL + 1 ? gb2 : 0.f));
-        }
-      }
-      const long long wofs = (long long)w * C::NQ * 512 + l * 4;
+      float pay[C::NPAY];
+      pack_payload<F, H>(gw1, gbw, gb2, l, pay);
+      const long long wofs = (long long)w * C::NLINE * 256 + l * 4;
       const long long mine = ll_slot(ex, parity, ex.rank) + wofs;
+      float sum[C::NPAY];
+#pragma unroll
+      for (int k = 0; k < C::NPAY; ++k) sum[k] = 0.f;
+      const unsigned long long t0 = realtime();
+      bool late = false;
+      static_assert(NP <= kMaxRanks, "at most kMaxRanks ranks per exchange");
       // fault injection (--fail-at R:S:corrupt): one payload to rank + 1 is off by 1.0 at step S, so
       // the replicas diverge and the per-epoch replica check must catch it (scalar test otherwise)
       const int victim = (ex.corrupt_step == a.adam_step0 + s + 1 && w == 0) ? (ex.rank + 1) % ex.world_size : -1;
-      for (int p = 0; p < ex.world_size; ++p) {
-        if (p == ex.rank) continue;
-        unsigned* dst = ex.data[p] + mine;
-        const float c0 = (p == victim && l == 0) ? pk[0][0] + 1.0f : pk[0][0];
-#pragma unroll
-        for (int q = 0; q < C::NQ; ++q) {
-          ll_put(dst + (2 * q) * 256, q == 0 ? c0 : pk[q][0], pk[q][1], tag);
-          ll_put(dst + (2 * q + 1) * 256, pk[q][2], pk[q][3], tag);
+      if constexpr (!TS) {
+        for (int p = 0; p < ex.world_size; ++p) {
+          if (p == ex.rank) continue;
+          push_payload<C::NPAY>(ex.data[p] + mine, pay, (p == victim && l == 0) ? pay[0] + 1.0f : pay[0], tag);
         }
-      }
-      f32x4 sum[C::NQ];
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) sum[q] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const unsigned long long t0 = realtime();
-      bool late = false;
-      // every peer's lines in flight at once: ONE local round trip per poll whatever the world size
-      // (polling in batches of 4 peers cost a second round trip per step at 5-8 ranks)
-      constexpr int PB = NP;
-      static_assert(NP <= kMaxRanks, "at most kMaxRanks ranks per exchange");
-      for (int p0 = 0; p0 < ex.world_size; p0 += PB) {
-        unsigned long long v[PB][4 * C::NQ];
-        bool ready;
-        do {  // every retry re-reads the whole batch: one round trip per poll, not one per line
-          ready = true;
-#pragma unroll
-          for (int j = 0; j < PB; ++j) {
-            const int p = p0 + j;
-            if (p < ex.world_size && p != ex.rank) {
-              const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, p) + wofs;
-#pragma unroll
-              for (int k = 0; k < 4 * C::NQ; ++k) v[j][k] = ll_get(src + (k >> 1) * 256 + (k & 1) * 2);
+        // every peer's lines in flight at once: ONE local round trip per poll whatever the world
+        // size (polling in batches of 4 peers cost a second round trip per step at 5-8 ranks)
+        poll_sum_peers<C::NPAY, NP>(ex, parity, wofs, tag, pay, sum, t0, late);
+      } else {
+        // ---- two-shot: lane l's lines are owned by rank l % P.  Reduce-scatter: every lane sends
+        // its payload to its owner only; the owner sums all ranks in rank order (the same order,
+        // so the same bits, as the one-shot) and all-gathers the sum to every peer.  Both phases
+        // land in the receiver's [parity][sender] slot at lane l: reduce-scatter traffic on the
+        // lanes the receiver owns, all-gather traffic on the lanes the sender owns, so one mailbox
+        // holds both.  A rank reads (P-1)/P of ONE payload per phase instead of P-1 payloads, at
+        // the price of a second hop -- which costs more than the bytes save (opt-in,
+        // DGT_XCH=twoshot; profiles/r2_xch_exchange_ab.txt).
+        const int own = l % ex.world_size;
+        for (int p = 0; p < ex.world_size; ++p) {
+          if (p == ex.rank || p != own) continue;
+          push_payload<C::NPAY>(ex.data[p] + mine, pay, pay[0], tag);
+        }
+        // owner lanes FIRST, in program order: a lane waiting for an all-gather must never run
+        // ahead of its own wave's owner lanes, which other ranks wait on
+        if (own == ex.rank) {
+          poll_sum_peers<C::NPAY, NP>(ex, parity, wofs, tag, pay, sum, t0, late);
+          if (!late) {
+            for (int p = 0; p < ex.world_size; ++p) {
+              if (p == ex.rank) continue;
+              push_payload<C::NPAY>(ex.data[p] + mine, sum, (p == victim && l == ex.rank) ? sum[0] + 1.0f : sum[0], tag);
             }
           }
+        }
+        if (own != ex.rank) {
+          const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, own) + wofs;
+          u32x4 v[C::NLINE];
+          bool ready;
+          do {
+            ll_fence_compiler();
+            ready = true;
 #pragma unroll
-          for (int j = 0; j < PB; ++j) {
-            const int p = p0 + j;
-            if (p < ex.world_size && p != ex.rank) {
+            for (int j = 0; j < C::NLINE; ++j) v[j] = ll3_get(src + j * 256);
 #pragma unroll
-              for (int k = 0; k < 4 * C::NQ; ++k) ready = ready && ll_ok(v[j][k], tag);
-            }
-          }
-          if (!ready && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
-        } while (!ready && !late);
+            for (int j = 0; j < C::NLINE; ++j) ready = ready && v[j][3] == tag;
+            if (!ready && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
+          } while (!ready && !late);
 #pragma unroll
-        for (int j = 0; j < PB; ++j) {
-          const int p = p0 + j;
-          if (p >= ex.world_size) continue;
-          if (p == ex.rank) {
-#pragma unroll
-            for (int q = 0; q < C::NQ; ++q) sum[q] += pk[q];
-          } else {
-#pragma unroll
-            for (int q = 0; q < C::NQ; ++q)
-              sum[q] += f32x4{ll_val(v[j][4 * q]), ll_val(v[j][4 * q + 1]), ll_val(v[j][4 * q + 2]),
-                              ll_val(v[j][4 * q + 3])};
-          }
+          for (int k = 0; k < C::NPAY; ++k) sum[k] = __uint_as_float(v[k / 3][k % 3]);
         }
       }
       if (late) sm.err = 1;
-#pragma unroll
-      for (int q = 0; q < C::NQ; ++q) {
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int i = 4 * q + e;
-          const float v = sum[q][e] * inv_ws;
-          if (i < C::NSL) gw1[i] = v;
-          else if (i == C::NSL) gbw = v;
-          else if (i == C::NSL + 1) gb2 = v;
-        }
-      }
+      unpack_payload<F, H>(sum, inv_ws, l, gw1, gbw, gb2);
     }
     DGT_STAMP(4);
 
@@ -655,12 +744,19 @@ int tiny_mlp_exchange_floats(int f, int h) {
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
   if (!a.bc) return hipErrorInvalidValue;
   const bool wd = a.hp.weight_decay != 0.f;
-#define DGT_TINY_LAUNCH_NP(F_, H_, SB, NP_)                                                      \
+#define DGT_TINY_LAUNCH_TS(F_, H_, SB, NP_, TS_)                                                \
   do {                                                                                      \
     if (wd)                                                                                 \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, true>), dim3(1), blk, 0, stream, a); \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, true, TS_>), dim3(1), blk, 0, stream, a); \
     else                                                                                    \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, false>), dim3(1), blk, 0, stream, a); \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, false, TS_>), dim3(1), blk, 0, stream, a); \
+  } while (0)
+// the two-shot exchange is compiled for 4- and 8-rank jobs only (at 2 ranks it moves the same bytes
+// as the one-shot in two hops)
+#define DGT_TINY_LAUNCH_NP(F_, H_, SB, NP_)                                                      \
+  do {                                                                                      \
+    if (NP_ >= 4 && a.ex.two_shot) DGT_TINY_LAUNCH_TS(F_, H_, SB, NP_, (NP_ >= 4));         \
+    else DGT_TINY_LAUNCH_TS(F_, H_, SB, NP_, false);                                        \
   } while (0)
 #define DGT_TINY_LAUNCH(F_, H_, SB, XC)                                                          \
   do {                                                                                      \
@@ -683,6 +779,7 @@ hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stre
 #undef X_
 #undef DGT_TINY_LAUNCH
 #undef DGT_TINY_LAUNCH_NP
+#undef DGT_TINY_LAUNCH_TS
   return hipErrorInvalidValue;
 }
 

@@ -10,7 +10,8 @@ rendezvous is needed.
 
 Buffer layout: LL lines ``[2 parity][8 src ranks][stride / 2]`` of 16 bytes; a line carries two
 ``{payload float, tag}`` pairs (``csrc/dgt_common.h``), so ``stride`` payload floats take
-``8 * stride`` bytes per slot.  A channel carries a monotonically increasing sequence number per
+``8 * stride`` bytes per slot.  (The fused trainer's kernel fills the same slots with LL3 lines,
+three payload floats and one tag per 16 bytes, ``csrc/dgt_common.h`` ``ll3_put``.)  A channel carries a monotonically increasing sequence number per
 exchange and the tag of exchange ``seq`` is ``seq + 1``; a reader polls its own mailbox until
 every line carries the expected tag.  No flags and no fences: the tag travels with the data.
 

@@ -45,6 +45,17 @@ def _raw_stream(index: int) -> int:
     return torch._C._cuda_getCurrentRawStream(index)
 
 
+def xch_mode(world_size: int) -> str:
+    """Protocol of the fused kernel's gradient exchange, as csrc/bindings.cpp exchange_two_shot()
+    picks it: DGT_XCH=oneshot|twoshot|auto.  auto = one-shot: the two-shot (reduce-scatter to lane
+    owners + all-gather, 4+ ranks) reads ~4x fewer bytes per poll but pays a second hop, and
+    measured ~2x slower per step in the 4/8-rank rehearsals (profiles/r2_xch_exchange_ab.txt)."""
+    mode = os.environ.get("DGT_XCH", "auto")
+    if mode not in ("auto", "oneshot", "twoshot"):
+        raise ValueError(f"DGT_XCH must be auto, oneshot or twoshot, got {mode!r}")
+    return "twoshot" if world_size >= 4 and mode == "twoshot" else "oneshot"
+
+
 class ReplicaDivergence(RuntimeError):
     """Data-parallel replicas ended an epoch with different parameters (a corrupted exchange)."""
 
@@ -228,7 +239,7 @@ class TinyMLPTrainer:
         if self.world_size == 1:
             return "none"
         if self.impl == "fused":
-            return "ipc-oneshot-xgmi"
+            return f"ipc-{xch_mode(self.world_size)}-xgmi"
         if self.impl == "graph":
             return "rccl-native-in-hipgraph"
         return f"{comm.backend_name()}-allreduce"

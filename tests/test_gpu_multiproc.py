@@ -1,6 +1,6 @@
 """GPU multi-rank rehearsal on ONE MI355X: 2 ranks share the card over gloo, exercising the IPC
-mailboxes (hipIpcGetMemHandle / hipIpcOpenMemHandle across processes) and the in-kernel one-shot
-gradient exchange of the fused trainer.  The 8-GPU xGMI run happens only in the driver's scaling
+mailboxes (hipIpcGetMemHandle / hipIpcOpenMemHandle across processes) and the in-kernel one- and
+two-shot gradient exchanges of the fused trainer.  The 8-GPU xGMI run happens only in the driver's scaling
 bench; these tests pin the protocol (LL tags, parities, rank-order sums) on real hardware."""
 import os
 import re
@@ -127,14 +127,57 @@ def test_bench_mlp_zero1_two_ranks_one_gpu():
     assert "reducescatter+allgather" in out["config"]["exchange"]
 
 
+@pytest.mark.parametrize("mode", ["twoshot", "oneshot"])
 @pytest.mark.parametrize("ws", [4, 8])
-def test_fused_ipc_exchange_many_ranks_one_gpu(tmp_path, ws):
-    """The 8-rank exchange (two batches of 4 peers in flight, every mailbox slot) on one card:
-    the same code path the 8 x MI355X scaling run takes, checked against the survey's oracle."""
-    r = run(ws, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", timeout=600)
+def test_fused_ipc_exchange_many_ranks_one_gpu(tmp_path, ws, mode):
+    """The 4- and 8-rank exchanges (every mailbox slot) on one card, both protocols: the code path
+    the 8 x MI355X scaling run takes (one-shot by default), checked against the survey's oracle.
+    Both sum in rank order, so both print the same oracle digits."""
+    r = run(ws, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", timeout=600, env={"DGT_XCH": mode})
     assert r.returncode == 0, r.stderr[-4000:]
-    assert "exchange=ipc-oneshot-xgmi" in r.stderr, r.stderr[-2000:]
+    assert f"exchange=ipc-{mode}-xgmi" in r.stderr, r.stderr[-2000:]
     assert losses(r.stdout) == ORACLE[ws][:2]
+
+
+def test_twoshot_matches_oneshot_bitwise_four_ranks(tmp_path):
+    """The two-shot's owners sum every rank in rank order, as the one-shot does: parameters after
+    an epoch are bit-identical between the protocols."""
+    import torch
+    out = {}
+    for mode in ("oneshot", "twoshot"):
+        d = tmp_path / mode
+        r = run(4, "train.py", "--impl", "fused", "--epochs", "1", "--save-dir", str(d), env={"DGT_XCH": mode})
+        assert r.returncode == 0, r.stderr[-4000:]
+        ck = [p for p in d.rglob("*.pt")]
+        assert ck, list(d.rglob("*"))
+        out[mode] = {p.relative_to(d).as_posix(): torch.load(p, map_location="cpu", weights_only=True) for p in ck}
+    assert out["oneshot"].keys() == out["twoshot"].keys()
+    a, b = _flat_tensors(out["oneshot"]), _flat_tensors(out["twoshot"])
+    assert a.keys() == b.keys() and any("module" in k for k in a), sorted(a)[:8]
+    for k in a:
+        assert torch.equal(a[k], b[k]), k
+
+
+def _flat_tensors(obj, prefix=""):
+    """Every tensor inside nested dicts / lists, keyed by its path."""
+    import torch
+    if torch.is_tensor(obj):
+        return {prefix: obj}
+    out = {}
+    items = obj.items() if isinstance(obj, dict) else enumerate(obj) if isinstance(obj, (list, tuple)) else ()
+    for k, v in items:
+        out.update(_flat_tensors(v, f"{prefix}/{k}"))
+    return out
+
+
+def test_corrupted_twoshot_exchange_fails_train_py():
+    """Two-shot at 4 ranks: rank 0 all-gathers one wrong sum to rank 1 only; the replica check
+    must fail the job."""
+    r = run(4, "train.py", "--impl", "fused", "--epochs", "1", "--no-save", "--fail-at", "0:37:corrupt",
+            env={"DGT_XCH": "twoshot"})
+    assert r.returncode != 0, r.stdout[-2000:]
+    assert "exchange=ipc-twoshot-xgmi" in r.stderr
+    assert "replicas diverged" in r.stderr, r.stderr[-3000:]
 
 
 def test_bench_eight_ranks_one_gpu():
@@ -146,3 +189,20 @@ def test_bench_eight_ranks_one_gpu():
     assert out["params_consistent_across_ranks"] is True
     assert out["config"]["exchange"] == "ipc-oneshot-xgmi"
     print(json.dumps(out))
+
+
+@pytest.mark.parametrize("ws", [2, 4])
+def test_fused_exchange_every_shape(ws):
+    """Every compiled (features, hidden) shape, dense (F = 20, 32, 8) and wide (H = 128) payload
+    layouts, through the in-kernel exchange: matches the stepwise trainer to fp32 rounding and the
+    ranks stay bit-identical."""
+    import json
+    r = run(ws, "tests/xch_shapes_worker.py", timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][7:])
+    assert len(res) == 4, res
+    for shape, row in res.items():
+        assert row["exchange"] == "ipc-oneshot-xgmi", (shape, row)
+        assert row["consistent"], (shape, row)
+        assert row["max_abs_diff"] < 1e-5, (shape, row)
+    print(json.dumps(res))

@@ -1,0 +1,58 @@
+"""Multi-rank worker for tests/test_gpu_multiproc.py::test_fused_exchange_every_shape: every
+compiled (features, hidden) shape of the fused kernel trains through the in-kernel IPC exchange
+(dense and padded LL3 payload layouts alike) and must match the stepwise trainer (per-step
+kernels + a host all-reduce over the control-plane backend) and keep the ranks bit-identical.
+
+Prints one ``RESULT {json}`` line on rank 0: "F,H" -> {"exchange", "max_abs_diff", "consistent"}.
+"""
+import json
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+os.environ.setdefault("DGT_QUIET", "1")
+
+import torch  # noqa: E402
+
+from distributed_gpu_test_amd.data import make_synthetic_data  # noqa: E402
+from distributed_gpu_test_amd.models import SimpleNet  # noqa: E402
+from distributed_gpu_test_amd.parallel import comm  # noqa: E402
+from distributed_gpu_test_amd.runtime.tiny_trainer import ReplicaDivergence, TinyMLPTrainer  # noqa: E402
+
+SHAPES = [(20, 64), (32, 64), (20, 128), (8, 16)]
+
+
+def train(f, h, impl, dev, steps=60):
+    x, y = make_synthetic_data(512, f, 7)
+    torch.manual_seed(11)
+    tr = TinyMLPTrainer(SimpleNet(f, h), x, y, 4, impl=impl, device=dev)
+    plan, counts = tr.epoch_plan(1)
+    tr.run_plan(plan[:steps], counts[:steps])
+    torch.cuda.synchronize(dev)
+    try:
+        tr.verify_replicas()
+        consistent = True
+    except ReplicaDivergence:
+        consistent = False
+    out = tr.params[: tr.numel].detach().clone(), tr.exchange, consistent
+    tr.close()
+    return out
+
+
+def main():
+    comm.init_distributed(backend="gloo")
+    dev = torch.device("cuda", 0)
+    res = {}
+    for f, h in SHAPES:
+        pf, xch, ok = train(f, h, "fused", dev)
+        ps, _, ok_s = train(f, h, "stepwise", dev)
+        res[f"{f},{h}"] = {"exchange": xch, "max_abs_diff": float((pf - ps).abs().max()),
+                           "consistent": bool(ok and ok_s)}
+    if comm.get_rank() == 0:
+        print("RESULT " + json.dumps(res), flush=True)
+    comm.destroy()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())
