@@ -175,26 +175,49 @@ def timed_run(trainer, plan, counts, args, device, comm):
         raise RuntimeError("warmup failed on some rank")
     barrier = comm.barrier if comm.collectives_on() else (lambda: None)  # a 1-rank barrier is a no-op
     gpu = device.type == "cuda"
+    # The ranks' kernels wait for each other from their first exchange, so start skew between the
+    # ranks lands inside the slowest rank's timed region.  Opening barrier: the process-group
+    # barrier, then (with IPC mailboxes) a device-side barrier whose kernels end within a
+    # microsecond of each other on every rank, so the hosts leave their syncs nearly together.
+    use_dev = comm.collectives_on() and not os.environ.get("DGT_BENCH_PG_BARRIER")
     barrier()
+    if use_dev:
+        getattr(trainer, "device_barrier", lambda: False)()
     if gpu:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     trainer.run_plan(timed_plan, timed_counts)
     t1 = time.perf_counter()
+    # closing barrier: with IPC mailboxes a device-side barrier queued behind the last step (one
+    # tiny one-shot all-reduce, done when every rank's steps are), then ONE sync; otherwise sync +
+    # the process group's barrier + sync
+    device_barrier = use_dev and getattr(trainer, "device_barrier", lambda: False)()
     if gpu:
         torch.cuda.synchronize()
     t2 = time.perf_counter()
-    barrier()
-    if gpu:
-        torch.cuda.synchronize()
+    if not device_barrier:
+        barrier()
+        if gpu:
+            torch.cuda.synchronize()
     elapsed = time.perf_counter() - t0
     if os.environ.get("DGT_BENCH_BREAKDOWN"):
         print(f"[bench] timed region: host launch {1e6 * (t1 - t0):.1f} us, device wait {1e6 * (t2 - t1):.1f} us, "
-              f"closing barrier+sync {1e6 * (elapsed - (t2 - t0)):.1f} us", file=sys.stderr, flush=True)
+              f"closing barrier+sync {1e6 * (elapsed - (t2 - t0)):.1f} us "
+              f"({'device barrier inside the wait' if device_barrier else 'process-group barrier'})",
+              file=sys.stderr, flush=True)
     if comm.all_reduce_max(float(_failed(trainer))) > 0:
         raise RuntimeError("timed run failed on some rank")
     mean_loss = float(trainer.loss_acc.item()) / max(1, args.steps)
     return comm.all_reduce_max(elapsed), mean_loss
+
+
+def closing_barrier_kind(trainer, world: int) -> str:
+    """Which barrier closed the timed region (see timed_run)."""
+    if world == 1:
+        return "none (1 rank)"
+    ch = getattr(trainer, "channel", None)
+    ipc = ch is not None and ch.healthy and not os.environ.get("DGT_BENCH_PG_BARRIER")
+    return "ipc-device" if ipc else "process-group"
 
 
 def _failed(trainer) -> bool:
@@ -332,7 +355,8 @@ def main(argv=None):
                  "synthetic N(0,1) batches, random-init weights"),
         "config": {"model": model_desc,
                    "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
-                   "micro_batch_per_gpu": B, "impl": trainer.impl, "exchange": trainer.exchange},
+                   "micro_batch_per_gpu": B, "impl": trainer.impl, "exchange": trainer.exchange,
+                   "closing_barrier": closing_barrier_kind(trainer, world)},
         "global_steps_per_sec": round(global_steps_per_s, 2),
         "samples_per_sec": round(global_steps_per_s * B * world, 2),
         "mean_loss": round(mean_loss, 6),

@@ -63,6 +63,8 @@ class IpcChannel:
         self.base_ptrs: List[int] = []
         self._opened: List[int] = []
         self.error: Optional[BaseException] = None
+        self._bar: Optional[torch.Tensor] = None
+        self._bar_out: Optional[torch.Tensor] = None
         self.status = torch.zeros(1, dtype=torch.int32, device=self.device)
         handle = b""
         # IPC handles only name memory on THIS node: a job that spans nodes never opens them
@@ -111,6 +113,17 @@ class IpcChannel:
         self.ops.oneshot_allreduce(inp, out, float(scale), self.data_ptrs, self.rank, self.world_size,
                                    self.stride, self.next_seq(reps), self.timeout_ticks, self.status, int(reps))
         return out
+
+    def barrier(self) -> None:
+        """Device-side barrier through the mailboxes: a one-shot all-reduce of one 16-byte line,
+        queued on the current stream.  A rank's kernel ends only after every peer's kernel has
+        written to it, and a peer launches its kernel only once its host reached the barrier, so
+        after the caller's stream sync every rank has arrived.  A few microseconds on xGMI against
+        tens for a process-group barrier; a timeout sets ``status`` (see ``check_status``)."""
+        if self._bar is None:
+            self._bar = torch.zeros(4, device=self.device)
+            self._bar_out = torch.empty_like(self._bar)
+        self.allreduce(self._bar, self._bar_out)
 
     def check_status(self) -> int:
         return int(self.status.item())

@@ -360,9 +360,21 @@ class TinyMLPTrainer:
         """Raise if a kernel reported a failure (cross-GPU timeout, bad shape)."""
         if self.device.type == "cuda":
             st = int(self.status.item())
+            if st == 0 and self.channel is not None:
+                st = self.channel.check_status()
             if st != 0:
                 raise RuntimeError(f"fused training kernel failed with status {st} "
                                    f"({'cross-GPU exchange timeout' if st == 1 else 'bad launch shape'})")
+
+    def device_barrier(self) -> bool:
+        """Queue a device-side barrier over this trainer's IPC mailboxes on the current stream
+        (``IpcChannel.barrier``); False when there is none (1 rank, or the exchange fell back to
+        RCCL), so the caller uses the process group's barrier.  Failures surface in ``check()``."""
+        ch = self.channel
+        if ch is None or not ch.healthy or self.world_size == 1:
+            return False
+        ch.barrier()
+        return True
 
     def verify_replicas(self) -> None:
         """Raise ReplicaDivergence on EVERY rank unless all ranks hold bit-identical parameters

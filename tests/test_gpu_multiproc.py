@@ -72,7 +72,20 @@ def test_bench_two_ranks_one_gpu():
     assert out["n_gpus"] == 1 and out["ranks"] == 2 and out["oversubscribed"] is True
     assert out["params_consistent_across_ranks"] is True
     assert out["config"]["exchange"] == "ipc-oneshot-xgmi"
+    assert out["config"]["closing_barrier"] == "ipc-device"
     print(line)
+
+
+def test_bench_driver_shape_two_ranks_device_barrier():
+    """The driver's --steps 20 --warmup 5 shape at 2 ranks: the device barrier brackets the timed
+    region, and a process-group-barrier run agrees on the trained parameters' consistency."""
+    import json
+    for env, kind in (({}, "ipc-device"), ({"DGT_BENCH_PG_BARRIER": "1"}, "process-group")):
+        r = run(2, "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-sweep", env=env)
+        assert r.returncode == 0, r.stderr[-4000:]
+        out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+        assert out["config"]["closing_barrier"] == kind and out["params_consistent_across_ranks"] is True
+        assert out["steps"] == 20 and out["warmup"] == 5
 
 
 def test_corrupted_exchange_fails_train_py(tmp_path):
