@@ -528,7 +528,7 @@ class DgtEngineBench(EngineBench):
         self.exchange = ("none" if self.world == 1 else
                          ("rccl-native-in-hipgraph" if graphed else f"{comm.backend_name()}-bucketed"))
         self.impl = ("dgt-engine" + ("+hipgraph" if graphed else "") + ("+fusedlinear" if self.engine.fused_linear_layers else "")
-                     + f"+zero{self.engine.stage}")
+                     + ("+graphmodule" if self.engine.graph_module else "") + f"+zero{self.engine.stage}")
 
     def run_plan(self, plan, counts):
         plan_d = plan.to(self.device).long()

@@ -85,6 +85,9 @@ class AMDConfig:
     # kernel injection: nn.Linear (+ following nn.ReLU) -> one fused HIP launch forward and one
     # backward for small fp32 batches (ops/linear.py)
     fused_linear: bool = False
+    # the module's forward and backward replayed from HIP graphs (one pair per input shape) under
+    # the ordinary engine(x) / engine.backward(loss) / engine.step() calls (engine.py)
+    graph_module: bool = False
 
 
 @dataclass
@@ -212,7 +215,8 @@ def parse_config(config: Union[str, os.PathLike, Dict[str, Any], None], world_si
                     oneshot_max_bytes=int(a.get("oneshot_max_bytes", 256 * 1024)),
                     hip_graph=bool(a.get("hip_graph", False)),
                     debug_sync_streams=bool(a.get("debug_sync_streams", False)),
-                    fused_linear=bool(a.get("fused_linear", False)))
+                    fused_linear=bool(a.get("fused_linear", False)),
+                    graph_module=bool(a.get("graph_module", False)))
     if amd.allreduce not in ("auto", "rccl", "oneshot"):
         raise ConfigError(f"amd.allreduce={amd.allreduce!r}: expected auto|rccl|oneshot")
 

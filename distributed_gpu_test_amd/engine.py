@@ -161,6 +161,13 @@ class Engine:
         self.training = True
         self.graphed = None
         self.graph_fallback_reason = ""
+        # ---- module forward/backward from HIP graphs under the eager API (amd.graph_module)
+        self.graph_module = bool(config.amd.graph_module and device.type == "cuda")
+        self.graph_module_reason = ""
+        self._graphed_fwd: Dict[tuple, Any] = {}
+        if self.graph_module and self.fused_linear_layers:
+            self.graph_module = False
+            self.graph_module_reason = "fused_linear kernels accumulate gradients outside autograd"
 
     # ------------------------------------------------------------------ helpers
     def _names(self, params):
@@ -212,7 +219,34 @@ class Engine:
             args = tuple(a.to(self.dtype) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)
         self.tput.start()
         with tracing.range("dgt.forward"):
+            if self.graph_module and self.training and not kwargs and args and all(torch.is_tensor(a) for a in args):
+                fn = self._graphed_forward(args)
+                if fn is not None:
+                    return fn(*args)
             return self.module(*args, **kwargs)
+
+    MAX_GRAPHED_SHAPES = 4
+
+    def _graphed_forward(self, args):
+        """The module as a graphed callable for this input signature (``runtime/graph_module.py``):
+        forward and backward each replay one HIP graph and the backward graph accumulates straight
+        into the flat gradient buckets, so a step costs two graph launches instead of one launch
+        per op, autograd node and parameter; the bucket hooks still fire.  Up to
+        MAX_GRAPHED_SHAPES signatures are captured; others, and any capture failure, run eagerly."""
+        from .runtime.graph_module import GraphedModule
+        key = tuple((tuple(a.shape), a.dtype, a.requires_grad) for a in args)
+        fn = self._graphed_fwd.get(key)
+        if fn is not None or len(self._graphed_fwd) >= self.MAX_GRAPHED_SHAPES:
+            return fn
+        self.store.rebind_grads()
+        try:
+            fn = GraphedModule(self.module, self.params, args)
+        except Exception as e:  # data-dependent control flow, host syncs, ...: stay eager
+            self.graph_module = False
+            self.graph_module_reason = f"capture failed: {type(e).__name__}: {e}"
+            return None
+        self._graphed_fwd[key] = fn
+        return fn
 
     __call__ = forward
 

@@ -1,0 +1,124 @@
+"""The engine's module forward and backward replayed from HIP graphs under the eager API.
+
+DeepSpeed users drive a step as ``loss = crit(engine(x), y); engine.backward(loss); engine.step()``
+(reference ``train.py:110-114``).  Eagerly, every op of the module is one host launch and one
+autograd node, so a small model is host-bound (~300-400 us per step for the reference MLP).  With
+``"amd": {"graph_module": true}`` the engine captures, per input signature:
+
+* a forward graph: ``static_out = module(*static_in)``;
+* a backward graph: ``autograd.grad(static_out, params, static_gout)`` followed by an in-graph
+  ``grad_view.add_(g)`` into the engine's flat gradient buckets — the accumulation autograd's
+  ``AccumulateGrad`` would otherwise launch once per parameter.
+
+``engine(x)`` then copies ``x`` into the static input and replays the forward graph; the user's
+loss runs eagerly; ``engine.backward`` reaches ``_Replay.backward``, which copies the incoming
+gradient and replays the backward graph.  ``_Replay`` returns no gradient for the parameters, so
+autograd runs their ``AccumulateGrad`` nodes with an undefined gradient: nothing is added twice and
+the post-accumulate hooks (the bucket reducer: all-reduce / reduce-scatter overlapped with the rest
+of backward) still fire, as for the fused Linear kernels (``ops/linear.py``).
+
+Same kernels, same accumulation order: the trajectory matches the eager engine.  The returned
+outputs alias the static output buffers (overwritten by the next replay of that signature), as with
+``torch.cuda.make_graphed_callables``.
+"""
+from __future__ import annotations
+
+from typing import List, Sequence, Tuple
+
+import torch
+
+
+def _as_tuple(out) -> Tuple[torch.Tensor, ...]:
+    if torch.is_tensor(out):
+        return (out,)
+    if isinstance(out, (tuple, list)) and all(torch.is_tensor(o) for o in out):
+        return tuple(out)
+    raise TypeError(f"graph_module needs a module returning a tensor or a tuple of tensors, got {type(out).__name__}")
+
+
+class GraphedModule:
+    def __init__(self, module: torch.nn.Module, params: Sequence[torch.nn.Parameter], args: Sequence[torch.Tensor],
+                 warmup: int = 2):
+        self.params: List[torch.nn.Parameter] = list(params)
+        self.grad_views = [p.grad for p in self.params]
+        if any(g is None or g.shape != p.shape for g, p in zip(self.grad_views, self.params)):
+            raise RuntimeError("graph_module needs the engine's gradient views bound (.grad) before capture")
+        self.static_in = tuple(a.detach().clone().requires_grad_(a.requires_grad) for a in args)
+        self.in_rg = [i for i, a in enumerate(self.static_in) if a.requires_grad]
+        # The graphs run the module on ALIASES of its parameters (same storage, so optimizer updates
+        # are seen, but separate autograd leaves): capture never touches the real parameters'
+        # AccumulateGrad nodes.  Those are created by the eager _Replay on the caller's stream;
+        # created on a capture stream they would put a cross-stream wait into every later backward
+        # (and, during capture, an event wait on a non-capturing stream).
+        by_id = {id(p): n for n, p in module.named_parameters()}
+        if any(id(p) not in by_id for p in self.params):
+            raise RuntimeError("graph_module: every trained tensor must be a parameter of the module")
+        self.aliases = {n: p.detach().requires_grad_(p.requires_grad) for n, p in module.named_parameters()}
+        targets = [self.aliases[by_id[id(p)]] for p in self.params] + [self.static_in[i] for i in self.in_rg]
+
+        def run():
+            return _as_tuple(torch.func.functional_call(module, self.aliases, self.static_in))
+
+        cur = torch.cuda.current_stream()
+        side = torch.cuda.Stream()
+        side.wait_stream(cur)
+        with torch.cuda.stream(side):  # library handles / workspaces before capture
+            for _ in range(warmup):
+                outs = [o for o in run() if o.requires_grad]
+                torch.autograd.grad(outs, targets, grad_outputs=[torch.ones_like(o) for o in outs],
+                                    allow_unused=True)
+                del outs
+        cur.wait_stream(side)
+        self.pool = torch.cuda.graph_pool_handle()
+        self.fwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.fwd, pool=self.pool):
+            out = run()
+        self.static_out = out
+        self.grad_out_idx = [i for i, o in enumerate(out) if o.requires_grad]
+        self.static_gout = [torch.empty_like(out[i]) for i in self.grad_out_idx]
+        self.bwd = torch.cuda.CUDAGraph()
+        with torch.cuda.graph(self.bwd, pool=self.pool):
+            gs = torch.autograd.grad([out[i] for i in self.grad_out_idx], targets, grad_outputs=self.static_gout,
+                                     allow_unused=True)
+            with torch.no_grad():
+                for gv, g in zip(self.grad_views, gs[:len(self.params)]):
+                    if g is not None:
+                        gv.add_(g)
+        self.static_gin = gs[len(self.params):]
+        self.single = torch.is_tensor(out) or len(out) == 1
+        self.replays = 0
+
+    def __call__(self, *args):
+        outs = _Replay.apply(self, *args, *self.params)
+        return outs[0] if self.single else outs
+
+
+class _Replay(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, runner: GraphedModule, *tensors):
+        for dst, src in zip(runner.static_in, tensors[:len(runner.static_in)]):
+            if dst.data_ptr() != src.data_ptr():
+                dst.copy_(src)
+        runner.fwd.replay()
+        runner.replays += 1
+        ctx.runner = runner
+        outs = tuple(o.detach() for o in runner.static_out)
+        for i, o in enumerate(outs):
+            if i not in runner.grad_out_idx:
+                ctx.mark_non_differentiable(o)
+        return outs
+
+    @staticmethod
+    def backward(ctx, *gouts):
+        r: GraphedModule = ctx.runner
+        for dst, i in zip(r.static_gout, r.grad_out_idx):
+            g = gouts[i]
+            if g is None:
+                dst.zero_()
+            else:
+                dst.copy_(g)
+        r.bwd.replay()
+        grads_in: List = [None] * len(r.static_in)
+        for i, g in zip(r.in_rg, r.static_gin):
+            grads_in[i] = None if g is None else g.detach().clone()
+        return (None, *grads_in, *([None] * len(r.params)))

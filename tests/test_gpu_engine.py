@@ -96,6 +96,42 @@ def test_engine_hip_graph_matches_eager(extra):
     e2.close()
 
 
+@pytest.mark.parametrize("extra", [{}, {"gradient_clipping": 0.5}, {"zero_optimization": {"stage": 1}},
+                                   {"gradient_accumulation_steps": 2, "train_batch_size": 64},
+                                   {"bf16": {"enabled": True}}])
+def test_engine_graph_module_matches_eager(extra):
+    """amd.graph_module: the module's forward and backward replay HIP graphs under the ordinary
+    engine(x) / backward / step calls.  Same kernels, same accumulation order: the trajectory
+    matches the eager engine, across a second input shape (a short batch)."""
+    batches = _batches(10, 5) + _batches(1, 6, bs=8) + _batches(10, 7) + _batches(3, 8, bs=8)
+    cfg = {"train_batch_size": 32, **extra}
+    e1, l1, p1 = _run_engine(dict(cfg), batches)
+    e2, l2, p2 = _run_engine(dict(cfg, amd={"graph_module": True}), batches)
+    assert e2.graph_module, e2.graph_module_reason
+    assert len(e2._graphed_fwd) == 2  # one graph pair per input shape
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
+    e1.close()
+    e2.close()
+
+
+def test_engine_graph_module_shape_cap_and_eval():
+    """Beyond MAX_GRAPHED_SHAPES input shapes, and in eval mode, the module runs eagerly."""
+    m = _mlp(9)
+    engine, _, _, _ = dgt.initialize(model=m, config={"train_batch_size": 32, "amd": {"graph_module": True}})
+    crit = torch.nn.BCEWithLogitsLoss()
+    for bs in (4, 8, 12, 16, 20, 24):
+        x, y = _batches(1, bs, bs=bs)[0]
+        engine.backward(crit(engine(x), y))
+        engine.step()
+    assert len(engine._graphed_fwd) == engine.MAX_GRAPHED_SHAPES and engine.graph_module
+    engine.eval()
+    with torch.no_grad():
+        out = engine(_batches(1, 3, bs=5)[0][0])
+    assert out.shape == (5, 1)
+    engine.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,dtype", [(4, torch.float32), (1000, torch.float32), (5000, torch.bfloat16)])
 def test_fused_bce_matches_torch(n, dtype):
