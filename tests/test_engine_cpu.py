@@ -189,6 +189,21 @@ def test_hip_graph_config_falls_back_to_eager_on_cpu():
     engine.close()
 
 
+def test_graph_module_config_parses_and_stays_eager_on_cpu():
+    from distributed_gpu_test_amd.config import parse_config
+    assert parse_config({"train_batch_size": 4, "amd": {"graph_module": True}}).amd.graph_module
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 1))
+    engine, _, _, _ = dgt.initialize(model=m, config={"train_batch_size": 4, "amd": {"graph_module": True}})
+    assert engine.graph_module is False  # HIP graphs only: the CPU engine runs the module eagerly
+    crit = torch.nn.BCEWithLogitsLoss()
+    x, y = torch.randn(4, 8), (torch.rand(4, 1) > 0.5).float()
+    engine.backward(crit(engine(x), y))
+    engine.step()
+    assert engine.global_steps == 1 and not engine._graphed_fwd
+    engine.close()
+
+
 def test_fused_bce_falls_back_to_torch_on_cpu():
     import torch
     from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
