@@ -67,7 +67,7 @@ def parse_args(argv=None):
     ap.add_argument("--comm-dtype", default=None, choices=["bf16", "fp32"],
                     help="mlp: gradient wire dtype (DeepSpeed communication_data_type; default bf16)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce bus bandwidth sweep")
-    ap.add_argument("--sweep-max-mb", type=int, default=256)
+    ap.add_argument("--sweep-max-mb", type=int, default=1024)  # rccl-tests range: 8 B .. 1 GiB
     return ap.parse_known_args(argv)[0]
 
 
