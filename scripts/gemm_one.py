@@ -2,6 +2,8 @@
 """Run one gemm_nt shape a few times (a compact target for rocprofv3 counter collection).
 
     python scripts/gemm_one.py M N K [variant] [iters]
+
+variant -1 runs torch.matmul(A, B^T) (hipBLASLt) on the same operands, for side-by-side counters.
 """
 import os
 import sys
@@ -18,6 +20,9 @@ A = torch.randn(M, K, device="cuda").to(torch.bfloat16)
 B = torch.randn(N, K, device="cuda").to(torch.bfloat16)
 C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 for _ in range(iters):
-    gemm_nt(A, B, C=C, variant=variant)
+    if variant < 0:
+        torch.matmul(A, B.t(), out=C)
+    else:
+        gemm_nt(A, B, C=C, variant=variant)
 torch.cuda.synchronize()
 print("ok", M, N, K, variant)
