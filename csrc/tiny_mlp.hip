@@ -330,7 +330,7 @@ DGT_DEVICE void fill_bias_table(const TinyTrainArgs& a, int t) {
 // and the per-pair uniform branches cost ~12 scalar branches per step).
 // Poll every peer's NPAY/2 LL lines of this lane in the local mailbox until all carry `tag` (or
 // the timeout passes: late), then sum them with the lane's own payload in rank order.  Every retry
-// re-reads all peers: one local round trip per poll, not one per line or per peer.  (Spinning on
+// re-reads the peers still pending: one local round trip per poll, not one per line or per peer.  (Spinning on
 // one line per peer first and reading the rest after measured slower: the extra round trip costs
 // more than the smaller polls save, profiles/r2_xch_exchange_ab.txt.)
 template <int NPAY, int NP>
@@ -338,13 +338,16 @@ DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, u
                                const float (&pay)[NPAY], float (&sum)[NPAY], unsigned long long t0, bool& late) {
   constexpr int NL = (NPAY + 2) / 3;
   u32x4 v[NP][NL];
-  bool ready;
+  // wave-uniform set of peers with a line still lacking the tag: a retry round re-reads only those
+  unsigned pend = 0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+    if (p < ex.world_size && p != ex.rank) pend |= 1u << p;
   do {
     ll_fence_compiler();
-    ready = true;
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-      if (p < ex.world_size && p != ex.rank) {
+      if ((pend >> p) & 1u) {
         const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, p) + wofs;
 #pragma unroll
         for (int j = 0; j < NL; ++j) v[p][j] = ll3_get(src + j * 256);
@@ -352,13 +355,15 @@ DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, u
     }
 #pragma unroll
     for (int p = 0; p < NP; ++p) {
-      if (p < ex.world_size && p != ex.rank) {
+      if ((pend >> p) & 1u) {
+        bool ok = true;
 #pragma unroll
-        for (int j = 0; j < NL; ++j) ready = ready && v[p][j][3] == tag;
+        for (int j = 0; j < NL; ++j) ok = ok && v[p][j][3] == tag;
+        if (__all(ok)) pend &= ~(1u << p);
       }
     }
-    if (!ready && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
-  } while (!ready && !late);
+    if (pend && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
+  } while (pend && !late);
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     if (p >= ex.world_size) continue;
