@@ -546,7 +546,8 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
 void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& master, const at::Tensor& exp_avg,
                   const at::Tensor& exp_avg_sq, const at::Tensor& param_lp, int64_t step, double lr, double beta1,
                   double beta2, double eps, double weight_decay, bool adamw, double grad_scale, int64_t variant) {
-  TORCH_CHECK(variant >= 0 && variant <= 4 && step >= 1, "dgt: gemm_nt_adam needs variant 0-4 and step >= 1");
+  TORCH_CHECK(((variant >= 0 && variant <= 4) || variant == 6) && step >= 1,
+              "dgt: gemm_nt_adam needs variant 0-4 or 6 and step >= 1");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt_adam needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {

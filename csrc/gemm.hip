@@ -19,6 +19,8 @@
 // Block ids are remapped so blocks sharing an XCD (id % 8) get neighbouring tiles (T1).
 // Reference: Linear(20,64) / Linear(64,1) of train.py:29-33, forward train.py:107, backward train.py:113.
 #include <hip/hip_bf16.h>
+
+#include <algorithm>
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 
@@ -848,8 +850,199 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ wgrad + Adam, wave-specialised
+// The MLP's weight-gradient GEMM dW = g^T . a (M = N = 4096, K = batch = 1024) with Adam applied to
+// each 128 x 128 gradient tile in place (kEpiAdam).  In the one-tile-per-block kernels every CU runs
+// its K loop (MFMA-bound) and THEN its tile's update (HBM-bound: 26 B/param), so the chip alternates
+// between the two limits (profiles/r2_mlp_fused_adam_ab.txt).  Here a persistent block walks
+// T / gridDim tiles with two wave groups sharing one LDS:
+//   * 8 MFMA waves (2 x 4 of 64 x 32) stream the operands through a 3-slot LDS-DMA ring across tile
+//     boundaries and, at the end of each tile, hand the fp32 tile to a 64 KiB LDS buffer;
+//   * 4 Adam waves update the PREVIOUS tile from that buffer, one 1/16 chunk (one float4 per lane)
+//     per K step, with master / m / v loads R-1 chunks ahead in registers,
+// so the update of tile i streams from HBM while the matrix cores compute tile i+1.  All 12 waves
+// meet at every K step's ring barrier (raw s_barrier: the wave groups run different code, one
+// barrier sequence); at a tile boundary two more barriers fence the hand-off buffer.  The last
+// tile's update runs after the loop.  Per element the update is epilogue_adam's: the same fp32
+// gradient (alpha * acc) and the same adam_update, so results are bit-identical to variant 0.
+// Measured (csrc/diag/wsa_ablate.hip, profiles/r2_wgrad_adam_ws_ab.txt): the GEMM alone runs 33 us
+// in this structure and the update alone 72 us, but together 103-110 us -- the sum, no overlap: the
+// 128 x 128 tiles re-read ~0.5 GB of operands through L2 per layer, and that traffic and the
+// update's HBM stream contend in the memory system rather than in the CU.  Opt-in only (variant 6).
+namespace wsa {
+constexpr int BM = 128, BN = 128, BK = 64, S = 3, NMW = 8, NAW = 4, NT = 64 * (NMW + NAW);
+constexpr int NK = 16;         // K steps per tile: K = 1024 (one float4 per Adam lane per step)
+constexpr int R = 8;           // Adam register ring: chunks R-1 ahead
+constexpr int WN = 32, NJ = WN / 16, WCOLS = BN / WN;
+constexpr int PER_TILE = 2 * (16 / NMW);  // LDS-DMA instructions per MFMA thread per K step
+static_assert(NK % R == 0 && BM * BN / 4 == NK * 64 * NAW, "one float4 per Adam lane per K step");
+
+struct AdamIn {
+  f32x4 p, m, v;
+};
+
+DGT_DEVICE void tile_origin(int vid, int tiles_m, int tiles_n, int& m0, int& n0) {
+  int tm, tn;
+  tile_of_block(vid, tiles_m, tiles_n, tm, tn);
+  m0 = tm * BM;
+  n0 = tn * BN;
+}
+}  // namespace wsa
+
+__global__ __launch_bounds__(wsa::NT, 1) void gemm_wgrad_adam_ws_kernel(GemmArgs g) {
+  using namespace wsa;
+  __shared__ __attribute__((aligned(16))) u16 ring[S][2][BM * BK];  // 96 KiB operand ring
+  __shared__ __attribute__((aligned(16))) float hand[BM * BN];      // 64 KiB gradient hand-off
+  const int tid = threadIdx.x, l = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int tiles_m = g.M / BM, tiles_n = g.N / BN, T = tiles_m * tiles_n, G = gridDim.x;
+  const int ntb = (T - (int)blockIdx.x + G - 1) / G;  // this block's tiles: blockIdx.x + i * G
+  const int Q = ntb * NK;                             // K steps of this block
+  if (w < NMW) {
+    // ---------------- MFMA waves
+    const int wr = w / WCOLS, wc = w % WCOLS;
+    const u16* A = static_cast<const u16*>(g.A);
+    const u16* B = static_cast<const u16*>(g.B);
+    auto issue = [&](int q) {
+      const int i = q / NK, kt = q - i * NK;
+      int m0, n0;
+      tile_origin((int)blockIdx.x + i * G, tiles_m, tiles_n, m0, n0);
+      stage_tile<NMW>(A, g.lda, m0, kt * BK, ring[q % S][0], w, l);
+      stage_tile<NMW>(B, g.ldb, n0, kt * BK, ring[q % S][1], w, l);
+    };
+    f32x4 acc[4][NJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int p = 0; p < S - 1; ++p)
+      if (p < Q) issue(p);
+    for (int q = 0; q < Q; ++q) {
+      if (q + 1 < Q) wait_vmcnt<(S - 2) * PER_TILE>();
+      else wait_vmcnt<0>();
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();  // B1: step q's operands visible; slot of step q-1 free
+      __builtin_amdgcn_sched_barrier(0);
+#if !(defined(DGT_WSA_ABLATE) && DGT_WSA_ABLATE == 2)  // diag: 2 = MFMA waves idle (barriers only)
+      if (q + S - 1 < Q) issue(q + S - 1);
+      const u16* As = ring[q % S][0];
+      const u16* Bs = ring[q % S][1];
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int chunk = kk * 4 + (l >> 4);
+        bf16x8 af[4], bfr[NJ];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[i] = read_frag(As, wr * 64 + i * 16 + (l & 15), chunk);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[j] = read_frag(Bs, wc * WN + j * 16 + (l & 15), chunk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+      }
+#endif
+      if (q % NK == NK - 1) {
+        __builtin_amdgcn_s_barrier();  // B2: the Adam waves are done with the previous tile's hand-off
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) {
+#pragma unroll
+            for (int rr = 0; rr < 4; ++rr)
+              hand[adam_slot<BN>(wr * 64 + i * 16 + 4 * (l >> 4) + rr, wc * WN + j * 16 + (l & 15))] =
+                  acc[i][j][rr] * g.alpha;
+            acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+          }
+        __builtin_amdgcn_s_waitcnt(0xc07f);  // lgkmcnt(0): the hand-off stores are in LDS
+        __builtin_amdgcn_s_barrier();        // B3: hand-off complete
+      }
+    }
+    return;
+  }
+  // ---------------- Adam waves.  Chunk c of tile ti is the float4 at row 8c + at / 32, column
+  // 4 (at % 32) of the tile, updated during K step (ti + 1) * NK + c (the MFMA waves' next tile);
+  // the last tile's chunks after the loop.  Straight-line per tile (16 chunks unrolled, loads R-1
+  // chunks ahead in a register ring, no per-lane branches) so the compiler's vmcnt waits are counted,
+  // not drains.
+  const GemmAdam& ad = g.adam;
+  __hip_bfloat16* lp = static_cast<__hip_bfloat16*>(ad.lp);
+  const int at = (w - NMW) * 64 + l;
+  const int r0 = at / (BN / 4), c0 = (at % (BN / 4)) * 4;
+  const long long lane_off = (long long)r0 * g.ldc + c0, step_off = 8LL * g.ldc;
+  auto tile_base = [&](int ti) -> long long {
+    int m0, n0;
+    tile_origin((int)blockIdx.x + min(ti, ntb - 1) * G, tiles_m, tiles_n, m0, n0);
+    return (long long)m0 * g.ldc + n0;
+  };
+  auto load = [&](long long o, AdamIn& in) {
+#if defined(DGT_WSA_ABLATE) && DGT_WSA_ABLATE == 1  // diag: 1 = Adam waves idle (barriers only)
+    return;
+#endif
+    in.p = *reinterpret_cast<const f32x4*>(ad.master + o);
+    in.m = *reinterpret_cast<const f32x4*>(ad.m + o);
+    in.v = *reinterpret_cast<const f32x4*>(ad.v + o);
+  };
+  auto update = [&](long long o, int c, AdamIn& in) {
+#if defined(DGT_WSA_ABLATE) && DGT_WSA_ABLATE == 1
+    return;
+#endif
+    const f32x4 gr = *reinterpret_cast<const f32x4*>(hand + adam_slot<BN>(r0 + 8 * c, c0));
+    __hip_bfloat16 b[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float mm = in.m[e], vv = in.v[e];
+      in.p[e] = adam_update(in.p[e], gr[e], mm, vv, ad.hp, ad.step_size_neg, ad.bc2_sqrt);
+      in.m[e] = mm;
+      in.v[e] = vv;
+      b[e] = __float2bfloat16(in.p[e]);
+    }
+    *reinterpret_cast<f32x4*>(ad.master + o) = in.p;
+    *reinterpret_cast<f32x4*>(ad.m + o) = in.m;
+    *reinterpret_cast<f32x4*>(ad.v + o) = in.v;
+    *reinterpret_cast<uint2*>(lp + o) = *reinterpret_cast<const uint2*>(b);
+  };
+  AdamIn buf[R];
+  {
+    const long long b0 = tile_base(0) + lane_off;
+#pragma unroll
+    for (int u = 0; u < R - 1; ++u) load(b0 + u * step_off, buf[u]);
+  }
+  // the MFMA waves' first tile: barriers only
+  for (int q = 0; q < NK; ++q) __builtin_amdgcn_s_barrier();  // B1
+  __builtin_amdgcn_s_barrier();                                // B2
+  __builtin_amdgcn_s_barrier();                                // B3
+  for (int ti = 0; ti < ntb; ++ti) {
+    const bool overlapped = ti < ntb - 1;  // the MFMA waves are computing tile ti + 1
+    const long long cur = tile_base(ti) + lane_off, nxt = tile_base(ti + 1) + lane_off;
+#pragma unroll
+    for (int c = 0; c < NK; ++c) {
+      if (overlapped) __builtin_amdgcn_s_barrier();  // B1 of K step (ti + 1) * NK + c
+      const int cp = c + R - 1;                      // chunk prefetched now (this tile or the next)
+      load(cp < NK ? cur + cp * step_off : nxt + (cp - NK) * step_off, buf[cp % R]);
+      update(cur + c * step_off, c, buf[c % R]);
+      if (overlapped && c == NK - 1) {
+        __builtin_amdgcn_s_barrier();  // B2: done with this tile's hand-off
+        __builtin_amdgcn_s_barrier();  // B3: the next tile's gradient is in the hand-off buffer
+      }
+    }
+  }
+}
+
 // variant: 0 = pick by shape, 1 = 128x128 2-stage, 2 = 256x256 8-phase, 3 = 128x128 4-stage,
-// 4 = 128x128 4-stage with 8 waves, 5 = 256x128 split-K 2 (needs the sk workspace)
+// 4 = 128x128 4-stage with 8 waves, 5 = 256x128 split-K 2 (needs the sk workspace),
+// 6 = wgrad + Adam with wave-specialised update overlap (kEpiAdam, K = 1024 only)
+static int cu_count() {
+  static int n = 0;
+  if (n == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        n <= 0)
+      n = 256;
+  }
+  return n;
+}
 static bool sk_fits(const GemmArgs& g) {
   const int T = (g.M % 256 == 0 && g.N % 128 == 0) ? (g.M / 256) * (g.N / 128) : 0;
   return T > 0 && T % 8 == 0 && g.K % 128 == 0 && g.sk_slab && g.sk_flags;
@@ -860,6 +1053,12 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // split-K 256 x 128 (variant 5) on request only: on the M = 1024 MLP products it ties the 8-wave
   // 128 x 128 kernel (fwd 46.2 vs 48.1 us hot, 53.9 vs 53.4 cold; dgrad 50.7 vs 49.5 hot,
   // profiles/r2_gemm_m1024.jsonl), so the shape-picked default stays the 128 x 128 kernel
+  if (variant == 6) {
+    if (epi != kEpiAdam || g.K != wsa::NK * wsa::BK || g.M % wsa::BM || g.N % wsa::BN) return hipErrorInvalidValue;
+    const int T = (g.M / wsa::BM) * (g.N / wsa::BN);
+    hipLaunchKernelGGL(gemm_wgrad_adam_ws_kernel, dim3(std::min(T, cu_count())), dim3(wsa::NT), 0, stream, g);
+    return hipGetLastError();
+  }
   const bool sk_epi = !(epi & (kEpiOutF32 | kEpiAccumulate | kEpiAdam));
   if (variant == 5 && (!sk_fits(g) || !sk_epi)) return hipErrorInvalidValue;
   const bool use_sk = variant == 5;

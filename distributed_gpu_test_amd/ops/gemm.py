@@ -82,7 +82,9 @@ def gemm_nt_adam_(A: torch.Tensor, B: torch.Tensor, master: torch.Tensor, exp_av
                   variant: int = 0) -> None:
     """Weight gradient ``grad_scale * A @ B.T`` ([M, N], never materialised) consumed in place by
     Adam: updates the fp32 ``master`` / ``exp_avg`` / ``exp_avg_sq`` ([M, N]) and writes the bf16
-    compute copy ``param_lp``.  One launch instead of wgrad GEMM + gradient store + flat Adam."""
+    compute copy ``param_lp``.  One launch instead of wgrad GEMM + gradient store + flat Adam.
+    variant as ``gemm_nt`` (0-4), or 6: persistent blocks whose MFMA waves hand each finished tile
+    to Adam waves that update it while the next tile computes (K = 1024 only)."""
     if not A.is_cuda:
         from .reference import adam_flat_reference_
         g = (A.float() @ B.float().t()).reshape(-1)

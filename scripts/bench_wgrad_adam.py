@@ -35,7 +35,7 @@ def unfused():
 arms = {"unfused (wgrad bf16 + flat Adam)": unfused, "wgrad GEMM alone": lambda: gemm_nt(gT, aT, C=grad),
         "flat Adam alone": lambda: adam_flat_(master.view(-1), grad.view(-1), m.view(-1), v.view(-1), *args,
                                                param_lp=lp.view(-1))}
-for var in (0, 1, 2, 3, 4):
+for var in (0, 1, 2, 3, 4, 6):
     arms[f"fused variant {var}"] = (lambda var=var: gemm_nt_adam_(gT, aT, master, m, v, lp, *args, variant=var))
 for name, fn in arms.items():
     t = bench(fn, iters=30, warmup=5)

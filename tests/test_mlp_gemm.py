@@ -275,7 +275,7 @@ def test_trainer_comm_dtype_selects_gradient_wire(comm, want):
 
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 3), (512, 256, 1024, 4),
-                                           (256, 256, 128, 2), (512, 768, 256, 2)])
+                                           (256, 256, 128, 2), (512, 768, 256, 2), (512, 256, 1024, 6)])
 @pytest.mark.parametrize("wd,adamw", [(0.0, False), (0.01, True)])
 def test_gemm_nt_adam_matches_reference(M, N, K, variant, wd, adamw):
     """wgrad + Adam in one launch (kEpiAdam epilogue through LDS, both kernels) against an fp32
@@ -297,6 +297,33 @@ def test_gemm_nt_adam_matches_reference(M, N, K, variant, wd, adamw):
     torch.testing.assert_close(m.view(-1), m2, rtol=1e-4, atol=1e-7)
     torch.testing.assert_close(v.view(-1), v2, rtol=1e-4, atol=1e-9)
     assert torch.equal(lp, p.to(torch.bfloat16))
+
+
+@gpu
+@pytest.mark.parametrize("M,N", [(4096, 2048), (4096, 2560), (1024, 1024)])
+def test_gemm_wgrad_adam_ws_bit_identical(M, N):
+    """Variant 6 (persistent blocks, MFMA waves hand each tile to Adam waves that update it while the
+    next tile computes; 2, 2-3 and 1 tiles per block here) gives exactly the one-tile-per-block
+    kernel's results: same fp32 gradient, same per-element Adam."""
+    from distributed_gpu_test_amd.ops.gemm import gemm_nt_adam_
+    K = 1024
+    g = torch.Generator().manual_seed(M + N)
+    A = (torch.randn(M, K, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    B = (torch.randn(N, K, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    p0 = torch.randn(M, N, generator=g).cuda()
+    m0 = (torch.randn(M, N, generator=g) * 1e-2).cuda()
+    v0 = (torch.rand(M, N, generator=g) * 1e-3).cuda()
+    out = []
+    for variant in (4, 6):
+        p, m, v = p0.clone(), m0.clone(), v0.clone()
+        lp = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+        for step in (3, 4):  # two updates: the second reads the first's state
+            gemm_nt_adam_(A, B, p, m, v, lp, step, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, grad_scale=0.25,
+                          variant=variant)
+        torch.cuda.synchronize()
+        out.append((p, m, v, lp))
+    for a, b in zip(*out):
+        assert torch.equal(a, b)
 
 
 @gpu
