@@ -476,6 +476,7 @@ class Engine:
         if self.graphed is not None:
             self.graphed.close()
             self.graphed = None
+        self._graphed_fwd.clear()  # graph_module: the captured graphs and their memory pools
         for h in self._hooks:
             h.remove()
         self._hooks = []
