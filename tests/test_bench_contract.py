@@ -39,6 +39,7 @@ def test_bench_single_process_cpu():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout
     _check(lines[0], 1, 40, 5)
+    assert lines[0]["config"]["closing_barrier"] == "none (1 rank)"
 
 
 def test_bench_two_ranks_gloo_cpu():
@@ -51,3 +52,17 @@ def test_bench_two_ranks_gloo_cpu():
     lines = _json_lines(r.stdout)
     assert len(lines) == 1, r.stdout  # rank 0 only
     _check(lines[0], 2, 30, 3)
+    # no IPC mailboxes on the CPU: the process group's barrier brackets the timed region
+    assert lines[0]["config"]["closing_barrier"] == "process-group"
+
+
+def test_exchange_mode_selection(monkeypatch):
+    from distributed_gpu_test_amd.runtime.tiny_trainer import xch_mode
+    monkeypatch.delenv("DGT_XCH", raising=False)
+    assert [xch_mode(n) for n in (2, 4, 8)] == ["oneshot"] * 3  # auto: one-shot at every size
+    monkeypatch.setenv("DGT_XCH", "twoshot")
+    assert [xch_mode(n) for n in (2, 4, 8)] == ["oneshot", "twoshot", "twoshot"]  # two-shot: 4+ ranks
+    monkeypatch.setenv("DGT_XCH", "threeshot")
+    import pytest
+    with pytest.raises(ValueError):
+        xch_mode(8)
