@@ -88,6 +88,10 @@ class GradReducer:
             return
         self._launched[bi] = True
         b = self.layout.buckets[bi]
+        if self.comm_buf is None and self.stage == 0 and not comm.collectives_on(self.world_size):
+            # one rank, nothing to send (the optimizer reads grad_buf directly): account only
+            self.bytes_reduced += b.numel * self.grad_buf.element_size()
+            return
         src = self.grad_buf[b.start:b.start + b.numel]
         if self.comm_buf is not None:
             view = self.comm_buf[b.start:b.start + b.numel]

@@ -100,21 +100,28 @@ class FlatParamStore:
         self.dtype = dtype
         self.param_buf = torch.zeros(layout.total, dtype=dtype, device=device)
         self.grad_buf = torch.zeros(layout.total, dtype=dtype, device=device)
+        self.grad_views: List[torch.Tensor] = []
         with torch.no_grad():
             for p, off, n, shape in zip(params, layout.offsets, layout.numels, layout.shapes):
                 view = self.param_buf[off:off + n].view(shape)
                 view.copy_(p.data.to(device=device, dtype=dtype))
                 p.data = view
-                p.grad = self.grad_buf[off:off + n].view(shape)
+                self.grad_views.append(self.grad_buf[off:off + n].view(shape))
+                p.grad = self.grad_views[-1]
 
     def rebind_grads(self) -> None:
-        """Re-attach gradient views (after user code set ``.grad = None``)."""
-        for p, off, n, shape in zip(self.params, self.layout.offsets, self.layout.numels, self.layout.shapes):
+        """Re-attach gradient views (after user code set ``.grad = None``).  Called every backward:
+        the common case (every .grad still IS its cached view) costs one identity test per
+        parameter, not a slice per parameter."""
+        for p, view in zip(self.params, self.grad_views):
             g = p.grad
-            if g is None or g.data_ptr() != self.grad_buf[off:off + n].data_ptr():
-                if g is not None:  # user replaced the grad tensor: fold it back in
-                    self.grad_buf[off:off + n].view(shape).copy_(g)
-                p.grad = self.grad_buf[off:off + n].view(shape)
+            if g is view:
+                continue
+            if g is not None and g.data_ptr() == view.data_ptr() and g.shape == view.shape:
+                continue  # an equivalent view of the same storage
+            if g is not None:  # user replaced the grad tensor: fold it back in
+                view.copy_(g)
+            p.grad = view
 
     def zero_grad(self) -> None:
         self.grad_buf.zero_()
