@@ -62,6 +62,15 @@ def test_engine_fused_linear_two_ranks_one_gpu(tmp_path):
     assert losses(r.stdout) == ORACLE2[:2]
 
 
+def test_engine_graph_module_two_ranks_one_gpu(tmp_path):
+    """amd.graph_module under two ranks: the graphed backward still fires the bucket hooks, the
+    gradients are averaged across ranks and the run prints the ws=2 oracle."""
+    r = run(2, "train.py", "--impl", "engine", "--epochs", "2", "--no-save",
+            "--deepspeed_config", os.path.join(ROOT, "configs", "ds_graph_module.json"))
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert losses(r.stdout) == ORACLE2[:2]
+
+
 def test_bench_two_ranks_one_gpu():
     r = run(2, "bench.py", "--gpus", "2", "--steps", "3000", "--warmup", "300", "--no-sweep")
     assert r.returncode == 0, r.stderr[-4000:]
