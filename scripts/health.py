@@ -55,6 +55,12 @@ def gpu_inventory():
                 info["devices"].append({"index": i, "name": p.name, "arch": getattr(p, "gcnArchName", None),
                                         "total_memory_GB": round(p.total_memory / 2**30, 1),
                                         "multi_processor_count": p.multi_processor_count})
+            # GPU-to-GPU access (the fused trainer's IPC mailboxes need it between every pair of
+            # a node's GPUs; without it the exchange falls back to RCCL)
+            n = torch.cuda.device_count()
+            info["peer_access"] = [[i == j or bool(torch.cuda.can_device_access_peer(i, j)) for j in range(n)]
+                                   for i in range(n)]
+            info["peer_access_all"] = all(all(r) for r in info["peer_access"])
             try:
                 info["rccl_version"] = ".".join(str(v) for v in torch.cuda.nccl.version())
             except Exception as e:  # pragma: no cover
@@ -105,7 +111,7 @@ def bandwidth_sweep(ngpus: int):
         return {"skipped": "rccl_perf not built or no GPU"}
     res = {}
     for op in ("all_reduce", "reduce_scatter", "all_gather"):
-        r = _run([exe, "-o", op, "-b", "8", "-e", str(256 << 20), "-f", "4", "-g", str(ngpus), "-n", "10",
+        r = _run([exe, "-o", op, "-b", "8", "-e", str(1 << 30), "-f", "4", "-g", str(ngpus), "-n", "10",
                   "-w", "3", "-j"], timeout=300)
         rows = []
         for line in (r.get("stdout") or "").splitlines():
@@ -146,7 +152,7 @@ def main(argv=None):
     peak = bw.get("all_reduce", {}).get("peak_busbw_GBps") if isinstance(bw, dict) else None
     print(f"[health] node{node} {rep['host']}: {n} GPU(s) "
           f"{rep['gpu'].get('devices', [{}])[0].get('name', '') if n else ''} RCCL {rep['gpu'].get('rccl_version')} "
-          f"all_reduce peak busbw {peak} GB/s -> {path}", flush=True)
+          f"all_reduce peak busbw {peak} GB/s, peer access {rep['gpu'].get('peer_access_all')} -> {path}", flush=True)
     wrong = sum(v.get("wrong", 0) for v in bw.values() if isinstance(v, dict)) if isinstance(bw, dict) else 0
     if a.strict and (n == 0 or wrong or not rep["framework"].get("extension")):
         return 1
