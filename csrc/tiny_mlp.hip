@@ -323,15 +323,11 @@ DGT_DEVICE void fill_bias_table(const TinyTrainArgs& a, int t) {
   }
 }
 
-// ------------------------------------------------------------------ persistent training kernel
-// NP > 1: the exchange is compiled in (for up to NP ranks).  The single-rank kernel has no exchange
-// branch, so backward and Adam form one basic block the scheduler can interleave.
-// WD: weight decay != 0 (Adam's L2 term / AdamW's decay compiled in; the reference's Adam has none,
-// and the per-pair uniform branches cost ~12 scalar branches per step).
-// Poll every peer's NPAY/2 LL lines of this lane in the local mailbox until all carry `tag` (or
+// ------------------------------------------------------------------ gradient exchange (NP > 1)
+// Poll every peer's (NPAY+2)/3 LL3 lines of this lane in the local mailbox until all carry `tag` (or
 // the timeout passes: late), then sum them with the lane's own payload in rank order.  Every retry
-// re-reads the peers still pending: one local round trip per poll, not one per line or per peer.  (Spinning on
-// one line per peer first and reading the rest after measured slower: the extra round trip costs
+// re-reads the peers still pending: one local round trip per poll, not one per line or per
+// peer.  (Spinning on one line per peer first and reading the rest after measured slower: the extra round trip costs
 // more than the smaller polls save, profiles/r2_xch_exchange_ab.txt.)
 template <int NPAY, int NP>
 DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, unsigned tag,
@@ -429,6 +425,11 @@ DGT_DEVICE void unpack_payload(const float (&sum)[TinyCfg<F, H>::NPAY], float in
   }
 }
 
+// ------------------------------------------------------------------ persistent training kernel
+// NP > 1: the exchange is compiled in (for up to NP ranks).  The single-rank kernel has no exchange
+// branch, so backward and Adam form one basic block the scheduler can interleave.
+// WD: weight decay != 0 (Adam's L2 term / AdamW's decay compiled in; the reference's Adam has none,
+// and the per-pair uniform branches cost ~12 scalar branches per step).
 template <int F, int H, bool SMALLB, int NP, bool WD, bool TS>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
