@@ -16,13 +16,18 @@ steps, including every step's Adam bias corrections (formed in double by the ker
 Before it, untimed: the W warmup steps, the sampler's index plan of the K steps (the DataLoader's
 work, uploaded once, as the trainer does once per epoch) and the sizing of the kernel's workspace.
 
+The timed region is bracketed on both sides by a barrier and a device synchronisation, and the
+time is the maximum over ranks.  With N > 1 and IPC mailboxes the barrier is device-side: a 16-byte
+one-shot all-reduce over the same mailboxes (opening: after the process group's barrier; closing:
+queued behind the last step, then one sync), ``config.closing_barrier`` says which was used.
+
 ``n_gpus`` counts distinct physical devices (host + PCI address gathered over ranks); ``ranks`` is
 the process count and ``oversubscribed`` is true when ranks share a device.  A run whose ranks end
 with different parameters exits non-zero and prints no headline line.
 
 ``value`` is the whole-job aggregate: optimizer iterations per second summed over ranks
 (= N x global steps/s).  ``allreduce_busbw_GBps`` is the peak RCCL all-reduce bus bandwidth of a
-short size sweep run after the timed region (rccl-tests convention, busbw = algbw x 2(n-1)/n).
+size sweep (8 B - 1 GiB) run after the timed region (rccl-tests convention, busbw = algbw x 2(n-1)/n).
 """
 from __future__ import annotations
 
