@@ -34,11 +34,13 @@ t("_raw_stream", lambda: _raw_stream(0))
 t("_lean_ok checks", lambda: tr._lean_ok(p1, c1, 1))
 lib, lh = _ext.c_lib(), tr._lh
 pp, cp = p1.data_ptr(), c1.data_ptr()
-t("dgt_tiny_launch (raw ctypes call)", lambda: lib.dgt_tiny_launch(lh, pp, cp, 1, 4, 0, 0), 500)
+tr.reserve(1)
+wp = tr._ws_ptr
+t("dgt_tiny_launch (raw ctypes call)", lambda: lib.dgt_tiny_launch(lh, pp, cp, 1, 4, 0, 0, wp), 500)
 ops = _ext.require()
 def old():
     ops.tiny_mlp_train(tr.x, tr.y, p1, c1, tr.params, tr.exp_avg, tr.exp_avg_sq, tr.loss_acc, tr.status, 20, 64,
-                       1e-3, 0.9, 0.999, 1e-8, 0.0, False, 0, [], 0, 1, 0, 0, 0)
+                       1e-3, 0.9, 0.999, 1e-8, 0.0, False, 0, [], 0, 1, 0, 0, 0, -1, tr._ws)
 t("torch op tiny_mlp_train K=1", old, 500)
 t("synchronize (idle)", lambda: torch.cuda.synchronize())
 e = torch.cuda.Event(enable_timing=True)
