@@ -213,7 +213,7 @@ def test_bench_eight_ranks_one_gpu():
     print(json.dumps(out))
 
 
-@pytest.mark.parametrize("ws", [2, 4])
+@pytest.mark.parametrize("ws", [2, 3, 4])
 def test_fused_exchange_every_shape(ws):
     """Every compiled (features, hidden) shape, dense (F = 20, 32, 8) and wide (H = 128) payload
     layouts, through the in-kernel exchange: matches the stepwise trainer to fp32 rounding and the
