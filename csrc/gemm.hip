@@ -37,25 +37,30 @@ DGT_DEVICE u16 f2bf(float f) {
 }
 DGT_DEVICE float bf2f(u16 u) { return __uint_as_float(((unsigned)u) << 16); }
 
-// one 128 x 64 bf16 operand tile: 16 LDS-DMA wave-instructions of 1 KiB (8 rows each), 4 per wave
-template <int NWAVE = 4>
+// one 128 x BK bf16 operand tile: rows of BK/8 16-byte chunks, the chunk XOR-swizzled by the low
+// bits of the row (BK = 64: 128-B rows, row & 7; BK = 128: 256-B rows, row & 15), so the 16 lanes
+// of a ds_read_b128 group reading one chunk index of 16 consecutive rows hit distinct bank groups.
+// 128 * BK * 2 / 1 KiB LDS-DMA wave-instructions per tile, 64 / (BK/8) rows each.
+template <int NWAVE = 4, int BK = GBK>
 DGT_DEVICE void stage_tile(const u16* __restrict__ src, int ld, int row0, int k0, u16* lds, int w, int l) {
-  constexpr int PER_WAVE = 16 / NWAVE;         // 1 KiB wave-instructions per wave (8 rows each)
+  constexpr int CH = BK / 8, RPI = 64 / CH;    // chunks per row, rows per wave-instruction
+  constexpr int PER_WAVE = GBM / RPI / NWAVE;  // 1 KiB wave-instructions per wave
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
-    const int rblk = (w * PER_WAVE + i) * 8;   // first of the 8 rows this wave-instruction writes
-    const int row = rblk + (l >> 3);
-    const int p = l & 7;                       // LDS 16-B chunk this lane lands in
-    const int c = p ^ (row & 7);               // logical chunk fetched (source-side swizzle)
+    const int rblk = (w * PER_WAVE + i) * RPI; // first of the rows this wave-instruction writes
+    const int row = rblk + l / CH;
+    const int p = l % CH;                      // LDS 16-B chunk this lane lands in
+    const int c = p ^ (row & (CH - 1));        // logical chunk fetched (source-side swizzle)
     const u16* g = src + (long long)(row0 + row) * ld + k0 + c * 8;
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(g), reinterpret_cast<int*>(lds + rblk * GBK), 16, 0,
+    __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(g), reinterpret_cast<int*>(lds + rblk * BK), 16, 0,
                                      0);
   }
 }
 
+template <int BK = GBK>
 DGT_DEVICE bf16x8 read_frag(const u16* lds, int row, int chunk) {
-  const int p = chunk ^ (row & 7);
-  return *reinterpret_cast<const bf16x8*>(lds + row * GBK + p * 8);
+  const int p = chunk ^ (row & (BK / 8 - 1));
+  return *reinterpret_cast<const bf16x8*>(lds + row * BK + p * 8);
 }
 
 // ---- B given as [K, N] (N contiguous, e.g. the weight W[out, in] as the dgrad's B operand): the
@@ -66,9 +71,9 @@ DGT_DEVICE bf16x8 read_frag(const u16* lds, int row, int chunk) {
 // image): conflict-free for the two 4-row blocks 8 rows apart that a 32-lane half reads.
 DGT_DEVICE int kn_swz(int row) { return ((row & 3) << 2) | ((row >> 2) & 3); }
 
-template <int NWAVE = 4>
+template <int NWAVE = 4, int BK = GBK>
 DGT_DEVICE void stage_tile_kn(const u16* __restrict__ src, int ld, int k0, int n0, u16* lds, int w, int l) {
-  constexpr int PER_WAVE = 16 / NWAVE;         // 1 KiB wave-instructions per wave (4 rows each)
+  constexpr int PER_WAVE = BK / 4 / NWAVE;     // 1 KiB wave-instructions per wave (4 k-rows each)
 #pragma unroll
   for (int i = 0; i < PER_WAVE; ++i) {
     const int rblk = (w * PER_WAVE + i) * 4;   // first of the 4 k-rows this wave-instruction writes
@@ -81,10 +86,10 @@ DGT_DEVICE void stage_tile_kn(const u16* __restrict__ src, int ld, int k0, int n
 }
 
 // B operand staging of the 128x128 kernel: [N, K] rows (stage_tile) or [K, N] rows (stage_tile_kn)
-template <bool KN, int NWAVE>
+template <bool KN, int NWAVE, int BK = GBK>
 DGT_DEVICE void stage_b(const u16* __restrict__ src, int ld, int n0, int k0, u16* lds, int w, int l) {
-  if constexpr (KN) stage_tile_kn<NWAVE>(src, ld, k0, n0, lds, w, l);
-  else stage_tile<NWAVE>(src, ld, n0, k0, lds, w, l);
+  if constexpr (KN) stage_tile_kn<NWAVE, BK>(src, ld, k0, n0, lds, w, l);
+  else stage_tile<NWAVE, BK>(src, ld, n0, k0, lds, w, l);
 }
 
 // Per-thread staging state of one operand of the 128x128 kernel: the global source of each of the
@@ -340,13 +345,16 @@ DGT_DEVICE void wait_vmcnt() {
 // NW = 4: waves 2 (M) x 2 (N), 64 x 64 each (4 x 4 accumulators).  NW = 8: waves 2 x 4, 64 x 32
 // each: two waves per SIMD, so one wave's LDS fragment reads overlap the other's MFMAs (the
 // 4-wave block leaves the matrix core idle while its only wave waits on LDS).
-template <int EPI, int S, int NW = 4>
-__global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
+// BK = 128 (S = 2 only, 128 KiB of LDS, one block per CU): hipBLASLt's macro-tile depth -- half the
+// barriers and vmcnt drains per FLOP of BK = 64, and 4 MFMA k-steps between them instead of 2.
+template <int EPI, int S, int NW = 4, int BK = GBK>
+__global__ __launch_bounds__(64 * NW, (S == 2 && BK == GBK) ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
+  static_assert(BK == GBK || (BK == 2 * GBK && S == 2), "BK = 128 only with the 2-stage loop");
   constexpr bool KN = (EPI & kEpiBKN) != 0;      // B is [K, N]: staged as is, transposed reads
   constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
   constexpr int WCOLS = GBN / WN;                // waves across N
   constexpr int NJ = WN / 16;                    // accumulator columns per wave
-  __shared__ __attribute__((aligned(16))) u16 lds[S][2][GBM * GBK];  // [stage][A|B], 32 KiB per stage
+  __shared__ __attribute__((aligned(16))) u16 lds[S][2][GBM * BK];  // [stage][A|B], 32 KiB per stage at BK 64
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   int tm, tn;
   tile_of_block(blockIdx.x, g.M / GBM, g.N / GBN, tm, tn);
@@ -361,16 +369,16 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = g.K / GBK;
+  const int nk = g.K / BK;
   auto compute = [&](int buf) {
     const u16* As = lds[buf][0];
     const u16* Bs = lds[buf][1];
 #pragma unroll
-    for (int kk = 0; kk < GBK / 32; ++kk) {
+    for (int kk = 0; kk < BK / 32; ++kk) {
       const int chunk = kk * 4 + (l >> 4);
       bf16x8 af[4], bfr[NJ];
 #pragma unroll
-      for (int i = 0; i < 4; ++i) af[i] = read_frag(As, wr * 64 + i * 16 + (l & 15), chunk);
+      for (int i = 0; i < 4; ++i) af[i] = read_frag<BK>(As, wr * 64 + i * 16 + (l & 15), chunk);
       if constexpr (KN) {
         i16x4 blo[NJ], bhi[NJ];
 #pragma unroll
@@ -379,7 +387,7 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
         for (int j = 0; j < NJ; ++j) bfr[j] = tr_wait(blo[j], bhi[j]);
       } else {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) bfr[j] = read_frag(Bs, wc * WN + j * 16 + (l & 15), chunk);
+        for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<BK>(Bs, wc * WN + j * 16 + (l & 15), chunk);
       }
 #if defined(DGT_GEMM_ABLATE) && DGT_GEMM_ABLATE == 2  // diag: 2 = LDS reads, no MFMA
 #pragma unroll
@@ -396,15 +404,15 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
     }
   };
   if constexpr (S == 2) {
-    stage_tile<NW>(A, g.lda, m0, 0, lds[0][0], w, l);
-    stage_b<KN, NW>(B, g.ldb, n0, 0, lds[0][1], w, l);
+    stage_tile<NW, BK>(A, g.lda, m0, 0, lds[0][0], w, l);
+    stage_b<KN, NW, BK>(B, g.ldb, n0, 0, lds[0][1], w, l);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int kt = 0; kt < nk; ++kt) {
       const int cur = kt & 1;
       if (kt + 1 < nk) {
-        stage_tile<NW>(A, g.lda, m0, (kt + 1) * GBK, lds[cur ^ 1][0], w, l);
-        stage_b<KN, NW>(B, g.ldb, n0, (kt + 1) * GBK, lds[cur ^ 1][1], w, l);
+        stage_tile<NW, BK>(A, g.lda, m0, (kt + 1) * BK, lds[cur ^ 1][0], w, l);
+        stage_b<KN, NW, BK>(B, g.ldb, n0, (kt + 1) * BK, lds[cur ^ 1][1], w, l);
       }
       compute(cur);
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -1032,7 +1040,8 @@ __global__ __launch_bounds__(wsa::NT, 1) void gemm_wgrad_adam_ws_kernel(GemmArgs
 
 // variant: 0 = pick by shape, 1 = 128x128 2-stage, 2 = 256x256 8-phase, 3 = 128x128 4-stage,
 // 4 = 128x128 4-stage with 8 waves, 5 = 256x128 split-K 2 (needs the sk workspace),
-// 6 = wgrad + Adam with wave-specialised update overlap (kEpiAdam, K = 1024 only)
+// 6 = wgrad + Adam with wave-specialised update overlap (kEpiAdam, K = 1024 only),
+// 7 = 128x128 2-stage with 8 waves at BK = 128 (K % 128 == 0)
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -1082,7 +1091,9 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks,
   // 2 blocks per CU) wins
   bool big = fits256 && (g.M / 256) * (g.N / 256) >= 200;
-  if (variant == 1 || variant == 3 || variant == 4) big = false;
+  if (variant == 1 || variant == 3 || variant == 4 || variant == 7) big = false;
+  if (variant == 7 && g.K % (2 * GBK)) return hipErrorInvalidValue;
+  const bool bk128 = variant == 7;
   if (variant == 2) {
     if (!fits256) return hipErrorInvalidValue;
     big = true;
@@ -1098,13 +1109,15 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   const bool eight = deep && variant != 3;  // measured: 8 waves beat 4 on one-wave grids (817 vs 759 TF)
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
-    if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
+    if (bk128) hipLaunchKernelGGL((gemm_nt_kernel<E, 2, 8, 2 * GBK>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else if (deep) hipLaunchKernelGGL((gemm_nt_kernel<E, 4>), dim3(grid), dim3(256), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
     if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
+    else if (bk128) hipLaunchKernelGGL((gemm_nt_kernel<E, 2, 8, 2 * GBK>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else if (deep) hipLaunchKernelGGL((gemm_nt_kernel<E, 4>), dim3(grid), dim3(256), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \

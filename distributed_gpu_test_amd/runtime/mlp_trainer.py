@@ -201,6 +201,8 @@ class MLPTrainer:
         # vs 100.2 vs 118.6 unfused, profiles/r2_wgrad_adam.jsonl); inside the step they lose
         # (1178 vs 1283 it/s, profiles/r2_mlp_fused_adam_ab.txt), so the default stays shape-picked
         self.fused_variant = int(os.environ.get("DGT_MLP_FUSED_VARIANT", "0"))
+        # kernel for the forward and dgrad products (0 = by shape; 7 = BK 128 per barrier)
+        self.gemm_variant = int(os.environ.get("DGT_MLP_GEMM_VARIANT", "0"))
 
         # ---- activations (both layouts) and gradient scratch
         B, D = self.B, self.D
@@ -353,7 +355,8 @@ class MLPTrainer:
         for i in range(L):
             if self._opt_pending:
                 main.wait_event(self.ev_opt[i])
-            gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True)
+            gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True,
+                    variant=self.gemm_variant)
             prev = self.a[i + 1]
         # head (+ its gradients, written in place: no zero fills)
         cur = 0
@@ -387,7 +390,8 @@ class MLPTrainer:
                 if self._t_pending:
                     torch.cuda.current_stream(self.device).wait_event(self.ev_t[i])
                 if self.dgrad_kn:
-                    gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True)
+                    gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True,
+                            variant=self.gemm_variant)
                 else:
                     gemm_nt(self.g[cur], self.WT[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i])
                 cur ^= 1
@@ -439,7 +443,8 @@ class MLPTrainer:
             a_prevT = xT if i == 0 else self.aT[i]
             rowsum_bf16(self.gT[cur], self.gb[i])
             if i > 0:
-                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True)
+                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True,
+                        variant=self.gemm_variant)
             R, Cc = self.shapes[i]
             o = self.w_off[i]
             sl = slice(o, o + R * Cc)
