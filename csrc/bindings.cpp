@@ -471,9 +471,10 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
              const std::optional<at::Tensor>& sk_slab, const std::optional<at::Tensor>& sk_flags) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK((variant >= 0 && variant <= 5) || variant == 7,
+  TORCH_CHECK((variant >= 0 && variant <= 5) || variant == 7 || variant == 8,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (128x128, 4 stages), "
-              "4 (128x128, 4 stages, 8 waves), 5 (256x128, split-K 2) or 7 (128x128, BK 128, 8 waves)");
+              "4 (128x128, 4 stages, 8 waves), 5 (256x128, split-K 2), 7 (128x128, BK 128, 8 waves) or 8 (128x128, "
+              "5 stages, 8 waves, 2 K-tiles per barrier)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
@@ -538,7 +539,7 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
     TORCH_CHECK(g.sk_slab && M % 256 == 0 && N % 128 == 0 && K % 128 == 0 && ((M / 256) * (N / 128)) % 8 == 0,
                 "dgt: the split-K gemm needs its workspace, M % 256 == 0, N % 128 == 0, K % 128 == 0 and a tile "
                 "count divisible by 8");
-  if (variant == 7) TORCH_CHECK(K % 128 == 0, "dgt: the BK = 128 gemm needs K % 128 == 0");
+  if (variant == 7 || variant == 8) TORCH_CHECK(K % 128 == 0, "dgt: gemm variants 7 and 8 need K % 128 == 0");
   DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A), (int)variant));
 }
 
@@ -547,8 +548,8 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
 void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& master, const at::Tensor& exp_avg,
                   const at::Tensor& exp_avg_sq, const at::Tensor& param_lp, int64_t step, double lr, double beta1,
                   double beta2, double eps, double weight_decay, bool adamw, double grad_scale, int64_t variant) {
-  TORCH_CHECK(((variant >= 0 && variant <= 4) || variant == 6 || variant == 7) && step >= 1,
-              "dgt: gemm_nt_adam needs variant 0-4, 6 or 7 and step >= 1");
+  TORCH_CHECK(((variant >= 0 && variant <= 4) || variant == 6 || variant == 7 || variant == 8) && step >= 1,
+              "dgt: gemm_nt_adam needs variant 0-4 or 6-8 and step >= 1");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt_adam needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {
@@ -566,7 +567,7 @@ void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& ma
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "dgt: gemm_nt_adam state must be 16-byte aligned");
   if (variant == 2)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
-  if (variant == 7) TORCH_CHECK(K % 128 == 0, "dgt: the BK = 128 gemm needs K % 128 == 0");
+  if (variant == 7 || variant == 8) TORCH_CHECK(K % 128 == 0, "dgt: gemm variants 7 and 8 need K % 128 == 0");
   dgt::GemmArgs g;
   std::memset(&g, 0, sizeof(g));
   g.A = A.data_ptr();

@@ -347,9 +347,13 @@ DGT_DEVICE void wait_vmcnt() {
 // 4-wave block leaves the matrix core idle while its only wave waits on LDS).
 // BK = 128 (S = 2 only, 128 KiB of LDS, one block per CU): hipBLASLt's macro-tile depth -- half the
 // barriers and vmcnt drains per FLOP of BK = 64, and 4 MFMA k-steps between them instead of 2.
-template <int EPI, int S, int NW = 4, int BK = GBK>
+// G = 2 (S = 5, 160 KiB): the same halved barrier count at BK = 64 granularity -- one barrier per
+// two K-tiles, three K-tiles (96 KiB) in flight behind the pair being computed, as deep as the
+// 4-stage loop, where BK = 128 x 2 stages keeps only one 64 KiB tile ahead (cold operands stall it).
+template <int EPI, int S, int NW = 4, int BK = GBK, int G = 1>
 __global__ __launch_bounds__(64 * NW, (S == 2 && BK == GBK) ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(BK == GBK || (BK == 2 * GBK && S == 2), "BK = 128 only with the 2-stage loop");
+  static_assert(G == 1 || (S > 2 && S >= 2 * G + 1 && BK == GBK), "G tiles per barrier need S >= 2G + 1 stages");
   constexpr bool KN = (EPI & kEpiBKN) != 0;      // B is [K, N]: staged as is, transposed reads
   constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
   constexpr int WCOLS = GBN / WN;                // waves across N
@@ -420,34 +424,41 @@ __global__ __launch_bounds__(64 * NW, (S == 2 && BK == GBK) ? 2 : 1) void gemm_n
     }
   } else {
     constexpr int PER_TILE = 2 * (16 / NW);  // glds per thread per K-tile (A and B)
+    constexpr int AHEAD = S - 2 * G;         // K-tiles left in flight past the G being retired
     Stager<NW, false> sa(A, g.lda, m0, w, l);
     Stager<NW, KN> sb(B, g.ldb, n0, w, l);
 #pragma unroll
-    for (int p = 0; p < S - 1; ++p) {
+    for (int p = 0; p < S - G; ++p) {
       if (p < nk) {
         sa.issue(lds[p][0]);
         sb.issue(lds[p][1]);
       }
     }
-    int buf = 0;
-    for (int kt = 0; kt < nk; ++kt) {
-      // tiles kt .. min(kt + S - 2, nk - 1) are in flight; retire tile kt
-      const int ahead = min(S - 2, nk - 1 - kt);
-      if (ahead >= S - 2) wait_vmcnt<(S - 2) * PER_TILE>();
-      else if (S > 3 && ahead == 1) wait_vmcnt<PER_TILE>();
+    int buf = 0, nb = S - G;  // buffer of tile kt, buffer the next staged tile lands in (tile % S)
+    for (int kt = 0; kt < nk; kt += G) {
+      // tiles kt .. min(kt + S - G - 1, nk - 1) are in flight; retire tiles kt .. kt + G - 1
+      const int ahead = min(AHEAD, nk - kt - G);
+      if (ahead >= AHEAD) wait_vmcnt<AHEAD * PER_TILE>();
+      else if (AHEAD > 1 && ahead == 1) wait_vmcnt<PER_TILE>();
       else wait_vmcnt<0>();
       __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();  // tile kt visible to all waves; buffer of kt-1 free for reuse
+      __builtin_amdgcn_s_barrier();  // tiles kt.. visible to all waves; buffers of kt-G .. kt-1 free for reuse
       __builtin_amdgcn_sched_barrier(0);
 #if !(defined(DGT_GEMM_ABLATE) && DGT_GEMM_ABLATE == 1)  // diag: 1 = no staging inside the loop
-      if (kt + S - 1 < nk) {
-        const int nb = (buf + S - 1) % S;
-        sa.issue(lds[nb][0]);
-        sb.issue(lds[nb][1]);
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        if (kt + S - G + i < nk) {
+          sa.issue(lds[nb][0]);
+          sb.issue(lds[nb][1]);
+        }
+        nb = (nb + 1 == S) ? 0 : nb + 1;
       }
 #endif
-      compute(buf);
-      buf = (buf + 1 == S) ? 0 : buf + 1;
+#pragma unroll
+      for (int i = 0; i < G; ++i) {
+        compute(buf);
+        buf = (buf + 1 == S) ? 0 : buf + 1;
+      }
     }
     __builtin_amdgcn_s_barrier();
   }
@@ -1041,7 +1052,8 @@ __global__ __launch_bounds__(wsa::NT, 1) void gemm_wgrad_adam_ws_kernel(GemmArgs
 // variant: 0 = pick by shape, 1 = 128x128 2-stage, 2 = 256x256 8-phase, 3 = 128x128 4-stage,
 // 4 = 128x128 4-stage with 8 waves, 5 = 256x128 split-K 2 (needs the sk workspace),
 // 6 = wgrad + Adam with wave-specialised update overlap (kEpiAdam, K = 1024 only),
-// 7 = 128x128 2-stage with 8 waves at BK = 128 (K % 128 == 0)
+// 7 = 128x128 2-stage with 8 waves at BK = 128 (K % 128 == 0),
+// 8 = 128x128 5-stage with 8 waves, one barrier per two K-tiles (K % 128 == 0)
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -1091,9 +1103,9 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks,
   // 2 blocks per CU) wins
   bool big = fits256 && (g.M / 256) * (g.N / 256) >= 200;
-  if (variant == 1 || variant == 3 || variant == 4 || variant == 7) big = false;
-  if (variant == 7 && g.K % (2 * GBK)) return hipErrorInvalidValue;
-  const bool bk128 = variant == 7;
+  if (variant == 1 || variant == 3 || variant == 4 || variant == 7 || variant == 8) big = false;
+  if ((variant == 7 || variant == 8) && g.K % (2 * GBK)) return hipErrorInvalidValue;
+  const bool bk128 = variant == 7, pair = variant == 8;
   if (variant == 2) {
     if (!fits256) return hipErrorInvalidValue;
     big = true;
@@ -1110,6 +1122,7 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
     if (bk128) hipLaunchKernelGGL((gemm_nt_kernel<E, 2, 8, 2 * GBK>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (pair) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, GBK, 2>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else if (deep) hipLaunchKernelGGL((gemm_nt_kernel<E, 4>), dim3(grid), dim3(256), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
@@ -1118,6 +1131,7 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   case E:                                                                                         \
     if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
     else if (bk128) hipLaunchKernelGGL((gemm_nt_kernel<E, 2, 8, 2 * GBK>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (pair) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, GBK, 2>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else if (deep) hipLaunchKernelGGL((gemm_nt_kernel<E, 4>), dim3(grid), dim3(256), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \

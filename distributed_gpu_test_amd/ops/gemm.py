@@ -44,7 +44,8 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage, 2 = 256x256 8-phase pipeline,
     3 = 128x128 tiles 4-stage, 4 = 128x128 tiles 4-stage with 8 waves, 5 = 256x128 tiles with K
     split over two blocks that meet through a per-tile counter (the M = 1024 MLP products),
-    7 = 128x128 tiles, 8 waves, 2 stages of BK = 128 (K % 128 == 0; one block per CU).
+    7 = 128x128 tiles, 8 waves, 2 stages of BK = 128 (K % 128 == 0; one block per CU),
+    8 = 128x128 tiles, 8 waves, 5 stages of BK = 64 with one barrier per two K-tiles (K % 128 == 0).
 
     ``b_kn=True``: B is given as ``[K, N]`` (N contiguous) and ``C = alpha * A @ B`` — the operand is
     staged as it lies and read with transposed LDS reads (128x128 kernels only)."""
@@ -84,7 +85,7 @@ def gemm_nt_adam_(A: torch.Tensor, B: torch.Tensor, master: torch.Tensor, exp_av
     """Weight gradient ``grad_scale * A @ B.T`` ([M, N], never materialised) consumed in place by
     Adam: updates the fp32 ``master`` / ``exp_avg`` / ``exp_avg_sq`` ([M, N]) and writes the bf16
     compute copy ``param_lp``.  One launch instead of wgrad GEMM + gradient store + flat Adam.
-    variant as ``gemm_nt`` (0-4, 7), or 6: persistent blocks whose MFMA waves hand each finished tile
+    variant as ``gemm_nt`` (0-4, 7, 8), or 6: persistent blocks whose MFMA waves hand each finished tile
     to Adam waves that update it while the next tile computes (K = 1024 only)."""
     if not A.is_cuda:
         from .reference import adam_flat_reference_

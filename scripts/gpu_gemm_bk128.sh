@@ -8,7 +8,7 @@ timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method threa
 timeout -k 10 300 python scripts/bench_gemm_m1024.py > gpurun_out/bk_m1024.jsonl 2>&1 || exit 1
 cat gpurun_out/bk_m1024.jsonl
 for r in $(seq ${REPS:-3}); do
-  for v in 0 7; do
+  for v in 0 7 8; do
     DGT_MLP_GEMM_VARIANT=$v timeout -k 10 200 python bench.py --model mlp --steps 100 --warmup 10 > gpurun_out/bk.json 2>/dev/null || exit 1
     python -c "import json; d=json.loads(open('gpurun_out/bk.json').read().splitlines()[-1]); print('gemm_variant=$v', d['value'], round(d['ms_per_step'], 4))"
   done

@@ -58,7 +58,8 @@ gpu = pytest.mark.gpu
                                            (128, 128, 64, 3), (256, 128, 128, 3), (384, 256, 192, 3),
                                            (512, 256, 1024, 3), (128, 128, 64, 4), (384, 256, 192, 4),
                                            (512, 256, 1024, 4), (128, 128, 128, 7), (384, 256, 384, 7),
-                                           (512, 256, 1024, 7)])
+                                           (512, 256, 1024, 7), (128, 128, 128, 8), (384, 256, 384, 8),
+                                           (512, 256, 1024, 8), (256, 128, 256, 8)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "mask_T", "f32", "f32_acc"])
 def test_gemm_nt_matches_reference(M, N, K, variant, epi):
     g = torch.Generator().manual_seed(M + N + K)
@@ -87,7 +88,7 @@ def test_gemm_nt_matches_reference(M, N, K, variant, epi):
 
 
 @gpu
-@pytest.mark.parametrize("n,variant", [(128, 1), (256, 2), (128, 3), (128, 4), (256, 7)])
+@pytest.mark.parametrize("n,variant", [(128, 1), (256, 2), (128, 3), (128, 4), (256, 7), (256, 8)])
 def test_gemm_identity_with_asymmetric_operand(n, variant):
     # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
     M = N = K = n
@@ -229,7 +230,8 @@ def test_trainer_overlap_schedule_is_bitwise_serial():
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 1), (128, 128, 64, 3),
                                            (384, 256, 192, 3), (128, 128, 64, 4), (384, 256, 192, 4),
                                            (512, 256, 1024, 4), (256, 512, 512, 0), (128, 128, 128, 7),
-                                           (384, 256, 384, 7), (512, 256, 1024, 7)])
+                                           (384, 256, 384, 7), (512, 256, 1024, 7), (128, 128, 128, 8),
+                                           (384, 256, 384, 8), (512, 256, 1024, 8)])
 @pytest.mark.parametrize("epi", ["plain", "mask_T", "f32"])
 def test_gemm_b_kn_matches_reference(M, N, K, variant, epi):
     """B given as [K, N] (the dgrad reading W[out, in] directly through transposed LDS reads)."""
@@ -250,7 +252,7 @@ def test_gemm_b_kn_matches_reference(M, N, K, variant, epi):
 
 
 @gpu
-@pytest.mark.parametrize("variant", [1, 3, 4, 7])
+@pytest.mark.parametrize("variant", [1, 3, 4, 7, 8])
 def test_gemm_b_kn_identity_asymmetric(variant):
     # A = I: C must equal B exactly, catching any transposed / swizzled fragment read
     n = 256
@@ -278,7 +280,7 @@ def test_trainer_comm_dtype_selects_gradient_wire(comm, want):
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 3), (512, 256, 1024, 4),
                                            (256, 256, 128, 2), (512, 768, 256, 2), (512, 256, 1024, 6),
-                                           (384, 256, 256, 7)])
+                                           (384, 256, 256, 7), (384, 256, 256, 8)])
 @pytest.mark.parametrize("wd,adamw", [(0.0, False), (0.01, True)])
 def test_gemm_nt_adam_matches_reference(M, N, K, variant, wd, adamw):
     """wgrad + Adam in one launch (kEpiAdam epilogue through LDS, both kernels) against an fp32
@@ -393,17 +395,19 @@ def test_gemm_splitk_identity_asymmetric(kn):
 @gpu
 @pytest.mark.parametrize("kn", [False, True])
 def test_gemm_bk128_bit_identical_to_bk64(kn):
-    """Variant 7 (BK = 128 per barrier) runs the same MFMAs in the same k order as the BK = 64
-    kernels: bit-identical outputs on the M = 1024 MLP shape with a fused mask + C^T epilogue."""
+    """Variants 7 (BK = 128 per barrier) and 8 (5 stages, a barrier per two K-tiles) run the same
+    MFMAs in the same k order as the BK = 64 kernels: bit-identical outputs on the M = 1024 MLP
+    shape with a fused mask + C^T epilogue."""
     M, N, K = 1024, 1024, 2048
     g = torch.Generator().manual_seed(11)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
     B = torch.randn(*((K, N) if kn else (N, K)), generator=g).to(torch.bfloat16).cuda()
     mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).cuda()
     out = []
-    for variant in (4, 7):
+    for variant in (4, 7, 8):
         C = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
         CT = torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
         gemm_nt(A, B, C=C, CT=CT, mask=mask, variant=variant, b_kn=kn)
         out.append((C, CT))
-    assert torch.equal(out[0][0], out[1][0]) and torch.equal(out[0][1], out[1][1])
+    for C, CT in out[1:]:
+        assert torch.equal(out[0][0], C) and torch.equal(out[0][1], CT)
