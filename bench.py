@@ -185,6 +185,7 @@ def timed_run(trainer, plan, counts, args, device, comm):
     # barrier, then (with IPC mailboxes) a device-side barrier whose kernels end within a
     # microsecond of each other on every rank, so the hosts leave their syncs nearly together.
     use_dev = comm.collectives_on() and not os.environ.get("DGT_BENCH_PG_BARRIER")
+    multi = comm.collectives_on()  # decided outside the timed region: the lookup costs microseconds
     barrier()
     if use_dev:
         getattr(trainer, "device_barrier", lambda: False)()
@@ -195,12 +196,13 @@ def timed_run(trainer, plan, counts, args, device, comm):
     t1 = time.perf_counter()
     # closing barrier: with IPC mailboxes a device-side barrier queued behind the last step (one
     # tiny one-shot all-reduce, done when every rank's steps are), then ONE sync; otherwise sync +
-    # the process group's barrier + sync
+    # the process group's barrier + sync.  One rank: the sync alone (its barrier is a no-op, so a
+    # second sync would only time an idle round trip)
     device_barrier = use_dev and getattr(trainer, "device_barrier", lambda: False)()
     if gpu:
         torch.cuda.synchronize()
     t2 = time.perf_counter()
-    if not device_barrier:
+    if not device_barrier and multi:
         barrier()
         if gpu:
             torch.cuda.synchronize()
@@ -218,7 +220,8 @@ def timed_run(trainer, plan, counts, args, device, comm):
 
 def closing_barrier_kind(trainer, world: int) -> str:
     """Which barrier closed the timed region (see timed_run)."""
-    if world == 1:
+    from distributed_gpu_test_amd.parallel import comm
+    if not comm.collectives_on():
         return "none (1 rank)"
     ch = getattr(trainer, "channel", None)
     ipc = ch is not None and ch.healthy and not os.environ.get("DGT_BENCH_PG_BARRIER")

@@ -32,6 +32,7 @@ class HipAccelerator:
     def set_device(self, local_rank: int) -> None:
         """Bind ``local_rank``'s GPU (ranks beyond the visible count wrap: oversubscribed runs)."""
         torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+        set_wait_mode(os.environ.get("DGT_HIP_WAIT", ""))
 
     def device(self, index: Optional[int] = None) -> torch.device:
         return torch.device("cuda", self.current_device() if index is None else index)
@@ -66,6 +67,26 @@ class CpuAccelerator:
 
     def synchronize(self) -> None:
         pass
+
+
+# hipSetDeviceFlags schedule bits: how a host thread waits for the device (synchronize, events)
+_WAIT_FLAGS = {"auto": 0, "spin": 1, "yield": 2, "blocking": 4}
+
+
+def set_wait_mode(mode: str) -> bool:
+    """``DGT_HIP_WAIT=spin|yield|blocking|auto``: the current device's host wait mode.  ``spin`` keeps
+    the waiting thread polling the completion signal instead of sleeping on an interrupt once the
+    runtime's short active-wait window has passed, which shortens the launch -> completion -> wake-up
+    round trip of a short kernel.  Empty: leave the runtime default.  Returns True if applied."""
+    if not mode:
+        return False
+    if mode not in _WAIT_FLAGS:
+        raise ValueError(f"DGT_HIP_WAIT must be one of {sorted(_WAIT_FLAGS)}, got {mode!r}")
+    import ctypes
+    rc = ctypes.CDLL("libamdhip64.so").hipSetDeviceFlags(ctypes.c_uint(_WAIT_FLAGS[mode]))
+    if rc != 0:
+        raise RuntimeError(f"hipSetDeviceFlags({mode}) failed with HIP error {rc}")
+    return True
 
 
 _ACCEL = None

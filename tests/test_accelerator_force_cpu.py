@@ -5,6 +5,7 @@ import os
 import subprocess
 import sys
 
+import pytest
 import torch
 
 from distributed_gpu_test_amd import accelerator
@@ -87,3 +88,11 @@ comm.destroy()
     env = dict(os.environ, DGT_QUIET="1", DGT_ACCELERATOR="cpu")
     r = subprocess.run([sys.executable, "-c", code], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "FORCED_OK" in r.stdout, r.stderr[-3000:]
+
+
+def test_wait_mode_validation():
+    """DGT_HIP_WAIT: empty leaves the runtime default; unknown modes are rejected before any HIP call."""
+    from distributed_gpu_test_amd.accelerator import set_wait_mode
+    assert set_wait_mode("") is False
+    with pytest.raises(ValueError):
+        set_wait_mode("busy")
