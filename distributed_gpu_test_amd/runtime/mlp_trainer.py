@@ -203,13 +203,18 @@ class MLPTrainer:
         self.fused_variant = int(os.environ.get("DGT_MLP_FUSED_VARIANT", "0"))
         # kernel for the forward and dgrad products (0 = by shape; 7 = BK 128 per barrier)
         self.gemm_variant = int(os.environ.get("DGT_MLP_GEMM_VARIANT", "0"))
+        # DGT_MLP_FUSED_SIDE=1: each layer's wgrad + Adam launch runs on a side stream beside the
+        # next layer's dgrad (a third gradient buffer keeps the dgrad from overwriting the g^T the
+        # side launch still reads); the next step's forward GEMM of layer l waits on layer l's update
+        self.fused_side = self.fused_adam and os.environ.get("DGT_MLP_FUSED_SIDE", "0") == "1" and self.L > 1
 
         # ---- activations (both layouts) and gradient scratch
         B, D = self.B, self.D
         self.a = [None] + [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(self.L)]
         self.aT = [None] + [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(self.L)]
-        self.g = [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(2)]
-        self.gT = [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        nbuf = 3 if self.fused_side else 2
+        self.g = [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(nbuf)]
+        self.gT = [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(nbuf)]
         self.dz = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
 
@@ -239,6 +244,10 @@ class MLPTrainer:
             self.s_t = torch.cuda.Stream(dev)
             self.ev_adam = torch.cuda.Event()
             self.ev_t = [torch.cuda.Event() for _ in range(self.L)]
+        if self.fused_side:
+            self.s_opt = torch.cuda.Stream(dev)
+            self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
+            self.ev_opt = [torch.cuda.Event() for _ in range(self.L)]
         if self._overlap:
             if os.environ.get("DGT_MLP_PRIO", "0") == "1":  # GEMM stream ahead of the optimizer stream
                 self.s_main = torch.cuda.Stream(dev, priority=-1)
@@ -338,7 +347,8 @@ class MLPTrainer:
         if self._opt_pending:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_stream(self.s_opt)
-            cur.wait_stream(self.s_comm)
+            if self._overlap:
+                cur.wait_stream(self.s_comm)
             self._opt_pending = False
 
     # ------------------------------------------------------------------ one step
@@ -349,7 +359,7 @@ class MLPTrainer:
         xT = self.XT[:, j * B:(j + 1) * B]
         y = self.Y[j * B:(j + 1) * B]
         ov = self._overlap
-        main = torch.cuda.current_stream(self.device) if ov else None
+        main = torch.cuda.current_stream(self.device) if (ov or self.fused_side) else None
         # forward: layer i waits only on its own update of the previous step
         prev = x
         for i in range(L):
@@ -439,21 +449,35 @@ class MLPTrainer:
         region moves 26 B/param (12 read + 14 written) instead of the wgrad store + flat Adam's
         2 + 28 B/param, and the update overlaps the other blocks' MFMA work."""
         args = self._adam_args()
+        side = self.fused_side
+        main = torch.cuda.current_stream(self.device) if side else None
+        nbuf = len(self.g)
         for i in reversed(range(self.L)):
             a_prevT = xT if i == 0 else self.aT[i]
+            nxt = (cur + 1) % nbuf
             rowsum_bf16(self.gT[cur], self.gb[i])
             if i > 0:
-                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True,
+                if side and i + 2 < self.L:  # the buffer written now was read by layer i + 2's update
+                    main.wait_event(self.ev_opt[i + 2])
+                gemm_nt(self.g[cur], self.W[i], C=self.g[nxt], CT=self.gT[nxt], mask=self.a[i], b_kn=True,
                         variant=self.gemm_variant)
             R, Cc = self.shapes[i]
             o = self.w_off[i]
             sl = slice(o, o + R * Cc)
-            gemm_nt_adam_(self.gT[cur], a_prevT, self.master_w[sl].view(R, Cc), self.m_w[sl].view(R, Cc),
-                          self.v_w[sl].view(R, Cc), self.params_bf16[sl].view(R, Cc), *args,
-                          grad_scale=1.0 / self.world_size, variant=self.fused_variant)
+            with (torch.cuda.stream(self.s_opt) if side else contextlib.nullcontext()):
+                if side:  # W_i is rewritten below: after its dgrad (and the rows it reads) on main
+                    self.ev_bwd[i].record(main)
+                    self.s_opt.wait_event(self.ev_bwd[i])
+                gemm_nt_adam_(self.gT[cur], a_prevT, self.master_w[sl].view(R, Cc), self.m_w[sl].view(R, Cc),
+                              self.v_w[sl].view(R, Cc), self.params_bf16[sl].view(R, Cc), *args,
+                              grad_scale=1.0 / self.world_size, variant=self.fused_variant)
+                if side:
+                    self.ev_opt[i].record(self.s_opt)
             if i > 0:
-                cur ^= 1
+                cur = nxt
         adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *args, grad_scale=1.0 / self.world_size)
+        if side:
+            self._opt_pending = True
 
     # bench.py adapter (same surface as TinyMLPTrainer)
     def epoch_plan(self, epoch: int):

@@ -1,0 +1,12 @@
+#!/bin/bash
+# bf16 MLP step at N = 1: fused wgrad + Adam in line (default) vs on a side stream beside the next
+# layer's dgrad (DGT_MLP_FUSED_SIDE=1); the schedule test, then interleaved fresh-process runs.
+set -o pipefail
+mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_mlp_gemm.py -k "fused" > gpurun_out/side_tests.log 2>&1; rc=$?; tail -1 gpurun_out/side_tests.log; [ $rc -eq 0 ] || exit $rc
+for r in $(seq ${REPS:-3}); do
+  for v in 0 1; do
+    DGT_MLP_FUSED_SIDE=$v timeout -k 10 200 python bench.py --model mlp --steps 100 --warmup 10 > gpurun_out/side.json 2>/dev/null || exit 1
+    python -c "import json; d=json.loads(open('gpurun_out/side.json').read().splitlines()[-1]); print('fused_side=$v', d['value'], round(d['ms_per_step'], 4))"
+  done
+done

@@ -411,3 +411,23 @@ def test_gemm_bk128_bit_identical_to_bk64(kn):
         out.append((C, CT))
     for C, CT in out[1:]:
         assert torch.equal(out[0][0], C) and torch.equal(out[0][1], CT)
+
+
+@gpu
+def test_mlp_fused_side_stream_is_bitwise_in_order(monkeypatch):
+    """DGT_MLP_FUSED_SIDE=1 (each layer's wgrad + Adam on a side stream beside the next dgrad, three
+    rotating gradient buffers, the next forward waiting per layer) is a schedule change only."""
+    outs = []
+    for side in ("0", "1"):
+        monkeypatch.setenv("DGT_MLP_FUSED_SIDE", side)
+        torch.manual_seed(0)
+        tr = MLPTrainer(SyntheticMLP(width=256, depth=4), batch_size=128, n_batches=2, lr=1e-3,
+                        device=torch.device("cuda"), fuse_adam=True)
+        assert tr.fused_side == (side == "1")
+        plan, counts = tr.epoch_plan(0)
+        for _ in range(3):
+            tr.run_plan(plan, counts)
+        torch.cuda.synchronize()
+        outs.append((tr.params.clone(), tr.master_w.clone(), tr.m_w.clone(), tr.v_w.clone()))
+    for a, b in zip(*outs):
+        assert torch.equal(a, b)
