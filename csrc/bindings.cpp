@@ -470,11 +470,12 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
              const std::optional<at::Tensor>& sk_slab, const std::optional<at::Tensor>& sk_flags) {
-  TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK((variant >= 0 && variant <= 5) || variant == 7 || variant == 8,
+  TORCH_CHECK(!(epi & dgt::kEpiBKN) || (variant != 2 && variant != 9),
+              "dgt: a [K, N] B operand runs on the 128x128 kernels only");
+  TORCH_CHECK((variant >= 0 && variant <= 5) || (variant >= 7 && variant <= 9),
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (128x128, 4 stages), "
               "4 (128x128, 4 stages, 8 waves), 5 (256x128, split-K 2), 7 (128x128, BK 128, 8 waves) or 8 (128x128, "
-              "5 stages, 8 waves, 2 K-tiles per barrier)");
+              "5 stages, 8 waves, 2 K-tiles per barrier) or 9 (256x256, 2 stages, one barrier per K-tile)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
@@ -533,7 +534,7 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
     }
   }
   c10::DeviceGuard guard(A.device());
-  if (variant == 2)
+  if (variant == 2 || variant == 9)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
   if (variant == 5)
     TORCH_CHECK(g.sk_slab && M % 256 == 0 && N % 128 == 0 && K % 128 == 0 && ((M / 256) * (N / 128)) % 8 == 0,
@@ -548,8 +549,8 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
 void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& master, const at::Tensor& exp_avg,
                   const at::Tensor& exp_avg_sq, const at::Tensor& param_lp, int64_t step, double lr, double beta1,
                   double beta2, double eps, double weight_decay, bool adamw, double grad_scale, int64_t variant) {
-  TORCH_CHECK(((variant >= 0 && variant <= 4) || variant == 6 || variant == 7 || variant == 8) && step >= 1,
-              "dgt: gemm_nt_adam needs variant 0-4 or 6-8 and step >= 1");
+  TORCH_CHECK(((variant >= 0 && variant <= 4) || (variant >= 6 && variant <= 9)) && step >= 1,
+              "dgt: gemm_nt_adam needs variant 0-4 or 6-9 and step >= 1");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt_adam needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {
@@ -565,7 +566,7 @@ void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& ma
   check_2d(param_lp, "param_lp", at::kBFloat16, M, N);
   for (const at::Tensor* t : {&master, &exp_avg, &exp_avg_sq, &param_lp})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "dgt: gemm_nt_adam state must be 16-byte aligned");
-  if (variant == 2)
+  if (variant == 2 || variant == 9)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
   if (variant == 7 || variant == 8) TORCH_CHECK(K % 128 == 0, "dgt: gemm variants 7 and 8 need K % 128 == 0");
   dgt::GemmArgs g;

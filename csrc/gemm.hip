@@ -869,6 +869,75 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   }
 }
 
+// ------------------------------------------------------------------ 256 x 256 tile, one barrier per K-tile
+// The 8-phase kernel above meets at two barriers per 16 MFMAs per wave (16 per BK = 64 K-tile); at
+// K = 1024 (the MLP's weight gradient) those meetings, not the matrix cores, set the pace.  Here the
+// same 8 waves (2 (M) x 4 (N), 128 x 64 each, 8 x 4 accumulators) run the plain two-stage loop of the
+// 128 x 128 kernel: the whole next K-tile (256 + 256 rows x 64, 64 KiB) is staged by LDS-DMA while
+// the current one is consumed by 64 MFMAs per wave, then ONE vmcnt(0) + barrier.  The two waves on a
+// SIMD overlap each other's fragment reads with MFMAs.  Same MFMAs in the same k order as the other
+// kernels (bit-identical results).  B as [N, K] only.
+template <int EPI>
+__global__ __launch_bounds__(512) void gemm_nt_256s_kernel(GemmArgs g) {
+  static_assert(!(EPI & kEpiBKN), "the 256 x 256 single-barrier kernel reads B as [N, K]");
+  constexpr int BM = 256, BN = 256, BK = GBK, NW = 8;
+  __shared__ __attribute__((aligned(16))) u16 lds[2][2][BM * BK];  // [stage][A|B], 64 KiB per stage
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  int tm, tn;
+  tile_of_block(blockIdx.x, g.M / BM, g.N / BN, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN, wr = w >> 2, wc = w & 3;
+  const u16* A = static_cast<const u16*>(g.A);
+  const u16* B = static_cast<const u16*>(g.B);
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto stage = [&](int kt, int buf) {  // 128-row halves: stage_tile's swizzle depends on row & 7 only
+    stage_tile<NW>(A, g.lda, m0, kt * BK, lds[buf][0], w, l);
+    stage_tile<NW>(A, g.lda, m0 + 128, kt * BK, lds[buf][0] + 128 * BK, w, l);
+    stage_tile<NW>(B, g.ldb, n0, kt * BK, lds[buf][1], w, l);
+    stage_tile<NW>(B, g.ldb, n0 + 128, kt * BK, lds[buf][1] + 128 * BK, w, l);
+  };
+  const int nk = g.K / BK;
+  stage(0, 0);
+  wait_vmcnt<0>();
+  __syncthreads();
+  for (int kt = 0; kt < nk; ++kt) {
+    const int cur = kt & 1;
+    if (kt + 1 < nk) stage(kt + 1, cur ^ 1);
+    const u16* As = lds[cur][0];
+    const u16* Bs = lds[cur][1];
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int chunk = kk * 4 + (l >> 4);
+      bf16x8 af[8], bfr[4];
+#pragma unroll
+      for (int i = 0; i < 8; ++i) af[i] = read_frag(As, wr * 128 + i * 16 + (l & 15), chunk);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bfr[j] = read_frag(Bs, wc * 64 + j * 16 + (l & 15), chunk);
+#pragma unroll
+      for (int i = 0; i < 8; ++i)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[i], bfr[j], acc[i][j], 0, 0, 0);
+    }
+    wait_vmcnt<0>();
+    __syncthreads();
+  }
+  if constexpr ((EPI & kEpiAdam) != 0) {
+    // fp32 256 x 256 tile = 256 KiB: two passes of 128 rows through the 128 KiB of operand LDS
+    epilogue_adam<BM, BN, 128, 64, 512, 128>(g, acc, reinterpret_cast<float*>(&lds[0][0][0]), m0, n0, wr, wc, l, tid);
+  } else if constexpr (!(EPI & kEpiOutF32)) {
+    epilogue_staged<EPI, BM, BN, 128, 64, 512>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        epi_store<EPI>(g, acc[i][j], m0 + wr * 128 + i * 16 + 4 * (l >> 4), n0 + wc * 64 + j * 16 + (l & 15));
+  }
+}
+
 // ------------------------------------------------------------------ wgrad + Adam, wave-specialised
 // The MLP's weight-gradient GEMM dW = g^T . a (M = N = 4096, K = batch = 1024) with Adam applied to
 // each 128 x 128 gradient tile in place (kEpiAdam).  In the one-tile-per-block kernels every CU runs
@@ -1053,7 +1122,8 @@ __global__ __launch_bounds__(wsa::NT, 1) void gemm_wgrad_adam_ws_kernel(GemmArgs
 // 4 = 128x128 4-stage with 8 waves, 5 = 256x128 split-K 2 (needs the sk workspace),
 // 6 = wgrad + Adam with wave-specialised update overlap (kEpiAdam, K = 1024 only),
 // 7 = 128x128 2-stage with 8 waves at BK = 128 (K % 128 == 0),
-// 8 = 128x128 5-stage with 8 waves, one barrier per two K-tiles (K % 128 == 0)
+// 8 = 128x128 5-stage with 8 waves, one barrier per two K-tiles (K % 128 == 0),
+// 9 = 256x256 2-stage with 8 waves of 128x64, one barrier per K-tile (B as [N, K])
 static int cu_count() {
   static int n = 0;
   if (n == 0) {
@@ -1106,14 +1176,15 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   if (variant == 1 || variant == 3 || variant == 4 || variant == 7 || variant == 8) big = false;
   if ((variant == 7 || variant == 8) && g.K % (2 * GBK)) return hipErrorInvalidValue;
   const bool bk128 = variant == 7, pair = variant == 8;
-  if (variant == 2) {
+  if (variant == 2 || variant == 9) {
     if (!fits256) return hipErrorInvalidValue;
     big = true;
   }
   if (epi & kEpiBKN) {  // only the 128x128 kernel reads a [K, N] B operand
-    if (variant == 2) return hipErrorInvalidValue;
+    if (variant == 2 || variant == 9) return hipErrorInvalidValue;
     big = false;
   }
+  const bool single = big && variant == 9;
   const int grid = big ? (g.M / 256) * (g.N / 256) : (g.M / GBM) * (g.N / GBN);
   // a grid that fits the chip at one block per CU gains nothing from 2 blocks/CU: spend the LDS on
   // a deep (4-stage) pipeline instead
@@ -1129,7 +1200,8 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
     break;
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
-    if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
+    if (single) hipLaunchKernelGGL((gemm_nt_256s_kernel<E>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g); \
     else if (bk128) hipLaunchKernelGGL((gemm_nt_kernel<E, 2, 8, 2 * GBK>), dim3(grid), dim3(512), 0, stream, g); \
     else if (pair) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, GBK, 2>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
@@ -1245,6 +1317,7 @@ __global__ __launch_bounds__(256) void rowsum_bf16_kernel(const u16* __restrict_
   if (row >= rows) return;
   const u16* p = in + (long long)row * cols;
   float s = 0.f;
+#pragma unroll 4  // the row's 16-byte loads in flight together (same summation order)
   for (int c = l * 8; c < cols; c += 64 * 8) {
     const uint4 v = *reinterpret_cast<const uint4*>(p + c);
     s += bf2f(v.x & 0xffff) + bf2f(v.x >> 16) + bf2f(v.y & 0xffff) + bf2f(v.y >> 16) + bf2f(v.z & 0xffff) +

@@ -22,9 +22,9 @@ p = torch.randn(D, D, device="cuda")
 m, v = torch.zeros_like(p), torch.zeros_like(p)
 lp = torch.empty(D, D, device="cuda", dtype=torch.bfloat16)
 arms = {}
-for var in [int(x) for x in os.environ.get("VARIANTS", "0,2,4,7,8").split(",")]:
+for var in [int(x) for x in os.environ.get("VARIANTS", "0,2,9").split(",")]:
     arms[f"wgrad bf16 v{var}"] = lambda var=var: gemm_nt(gT, aT, C=C, variant=var)
-    if var in (0, 2, 4, 7, 8):
+    if var in (0, 2, 4, 7, 8, 9):
         arms[f"wgrad+Adam v{var}"] = lambda var=var: gemm_nt_adam_(gT, aT, p, m, v, lp, 5, 1e-4, 0.9, 0.999, 1e-8,
                                                                     variant=var)
 arms["hipBLASLt gT @ aT^T"] = lambda: torch.matmul(gT, aT.t(), out=C)

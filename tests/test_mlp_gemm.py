@@ -59,7 +59,8 @@ gpu = pytest.mark.gpu
                                            (512, 256, 1024, 3), (128, 128, 64, 4), (384, 256, 192, 4),
                                            (512, 256, 1024, 4), (128, 128, 128, 7), (384, 256, 384, 7),
                                            (512, 256, 1024, 7), (128, 128, 128, 8), (384, 256, 384, 8),
-                                           (512, 256, 1024, 8), (256, 128, 256, 8)])
+                                           (512, 256, 1024, 8), (256, 128, 256, 8), (256, 256, 128, 9),
+                                           (512, 768, 256, 9), (768, 512, 1152, 9)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "mask_T", "f32", "f32_acc"])
 def test_gemm_nt_matches_reference(M, N, K, variant, epi):
     g = torch.Generator().manual_seed(M + N + K)
@@ -88,7 +89,7 @@ def test_gemm_nt_matches_reference(M, N, K, variant, epi):
 
 
 @gpu
-@pytest.mark.parametrize("n,variant", [(128, 1), (256, 2), (128, 3), (128, 4), (256, 7), (256, 8)])
+@pytest.mark.parametrize("n,variant", [(128, 1), (256, 2), (128, 3), (128, 4), (256, 7), (256, 8), (256, 9)])
 def test_gemm_identity_with_asymmetric_operand(n, variant):
     # A = I with an asymmetric B catches a transposed C write (cdna_hip_programming.md §3)
     M = N = K = n
@@ -280,7 +281,7 @@ def test_trainer_comm_dtype_selects_gradient_wire(comm, want):
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 3), (512, 256, 1024, 4),
                                            (256, 256, 128, 2), (512, 768, 256, 2), (512, 256, 1024, 6),
-                                           (384, 256, 256, 7), (384, 256, 256, 8)])
+                                           (384, 256, 256, 7), (384, 256, 256, 8), (512, 768, 256, 9)])
 @pytest.mark.parametrize("wd,adamw", [(0.0, False), (0.01, True)])
 def test_gemm_nt_adam_matches_reference(M, N, K, variant, wd, adamw):
     """wgrad + Adam in one launch (kEpiAdam epilogue through LDS, both kernels) against an fp32
@@ -430,4 +431,30 @@ def test_mlp_fused_side_stream_is_bitwise_in_order(monkeypatch):
         torch.cuda.synchronize()
         outs.append((tr.params.clone(), tr.master_w.clone(), tr.m_w.clone(), tr.v_w.clone()))
     for a, b in zip(*outs):
+        assert torch.equal(a, b)
+
+
+@gpu
+@pytest.mark.parametrize("epi", ["bf16", "adam"])
+def test_gemm_256_single_barrier_bit_identical(epi):
+    """Variant 9 (256 x 256, two stages, one barrier per K-tile) runs the 8-phase kernel's MFMAs in
+    the same k order: bit-identical on the MLP's weight-gradient shape, bf16 out and fused Adam."""
+    from distributed_gpu_test_amd.ops.gemm import gemm_nt_adam_
+    D, B = 1024, 1024
+    g = torch.Generator().manual_seed(5)
+    gT = (torch.randn(D, B, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    aT = (torch.randn(D, B, generator=g) * 0.1).to(torch.bfloat16).cuda()
+    p0 = torch.randn(D, D, generator=g).cuda()
+    out = []
+    for variant in (2, 9):
+        if epi == "bf16":
+            C = torch.empty(D, D, dtype=torch.bfloat16, device="cuda")
+            gemm_nt(gT, aT, C=C, variant=variant)
+            out.append((C,))
+        else:
+            p, m, v = p0.clone(), torch.zeros_like(p0), torch.zeros_like(p0)
+            lp = torch.empty(D, D, dtype=torch.bfloat16, device="cuda")
+            gemm_nt_adam_(gT, aT, p, m, v, lp, 3, 1e-3, 0.9, 0.999, 1e-8, grad_scale=0.5, variant=variant)
+            out.append((p, m, v, lp))
+    for a, b in zip(*out):
         assert torch.equal(a, b)
