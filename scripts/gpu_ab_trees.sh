@@ -10,7 +10,7 @@ trees=("$@")
 : > $out
 for rep in $(seq ${REPS:-3}); do
   for t in "${trees[@]}"; do
-    for k in ${KS:-"200000,5000 20,5"}; do
+    for k in ${KS:-200000,5000 20,5}; do
       k=${k/,/ }
       set -- $k
       (cd $t && DGT_BENCH_BREAKDOWN=1 timeout -k 10 120 python bench.py --steps $1 --warmup $2 > /tmp/ab.json 2> /tmp/ab.err) || { tail -5 /tmp/ab.err; exit 1; }
