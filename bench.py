@@ -306,23 +306,31 @@ def main(argv=None):
         trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=args.impl if device.type == "cuda" else "torch",
                                  device=device)
     plan, counts = build_plan(trainer, args.warmup + args.steps)
+    fallback_reason = None
     try:
         elapsed_max, mean_loss = timed_run(trainer, plan, counts, args, device, comm)
+        # every rank must hold identical parameters after DP training
+        consistent = params_consistent(trainer.params, world)
+        if not consistent and getattr(trainer, "channel", None) is not None:
+            raise RuntimeError("parameters differ across ranks after the IPC-exchange run")
     except RuntimeError as e:
-        # the fused kernel reports a cross-GPU exchange timeout through its status word; every rank
-        # learns about it here and the whole job re-runs on the RCCL path instead of dying
+        # the fused kernel reports a cross-GPU exchange timeout through its status word, and a
+        # replica divergence is seen by every rank through the check above; either way the whole
+        # job re-runs on the RCCL path (loudly, and recorded in the JSON) instead of dying
         if getattr(trainer, "impl", "") != "fused":
             raise
-        print(f"[bench] fused path failed ({e}); falling back to the RCCL path", file=sys.stderr, flush=True)
+        fallback_reason = str(e)
+        print(f"[bench] WARNING: fused IPC path failed ({e}); re-running on the RCCL path",
+              file=sys.stderr, flush=True)
         trainer.close()
         # use_ipc=False: the trainer's own automatic fallback (HIP graph with the native RCCL
         # communicator, or plain ProcessGroupNCCL if that cannot be set up on every rank)
         trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl="fused", device=device, use_ipc=False)
         plan, counts = build_plan(trainer, args.warmup + args.steps)
         elapsed_max, mean_loss = timed_run(trainer, plan, counts, args, device, comm)
+        consistent = params_consistent(trainer.params, world)
 
-    # every rank must hold identical parameters after DP training; a divergent run has no headline
-    consistent = params_consistent(trainer.params, world)
+    # a divergent run (after any fallback) has no headline
     if not consistent:
         if rank == 0:
             print(json.dumps({"metric": METRIC, "error": "parameters differ across ranks after training",
@@ -381,6 +389,7 @@ def main(argv=None):
         "ranks": world,
         "oversubscribed": n_devices < world,
         "params_consistent_across_ranks": consistent,
+        "ipc_fallback_reason": fallback_reason,
         "allreduce_busbw_GBps": None if peak_busbw is None else round(peak_busbw, 2),
         "allreduce_5KB_us": None if small is None else round(small["us"], 2),
         "oneshot_xgmi_5KB_us": None if small_os is None else round(small_os["us"], 2),
