@@ -83,8 +83,10 @@ class AMDConfig:
     # extra sync between comm and compute streams: validates overlap logic
     debug_sync_streams: bool = False
     # kernel injection: nn.Linear (+ following nn.ReLU) -> one fused HIP launch forward and one
-    # backward for small fp32 batches (ops/linear.py)
-    fused_linear: bool = False
+    # backward for small fp32 batches (ops/linear.py).  None = auto: on for an fp32 GPU engine
+    # unless graph_module is asked for (torch's F.linear costs ~37 us of host dispatch per call on
+    # ROCm at these shapes: eager engine 2,450 -> 4,300 it/s, profiles/r2_engine_host_profile.txt)
+    fused_linear: Optional[bool] = None
     # the module's forward and backward replayed from HIP graphs (one pair per input shape) under
     # the ordinary engine(x) / engine.backward(loss) / engine.step() calls (engine.py)
     graph_module: bool = False
@@ -215,7 +217,7 @@ def parse_config(config: Union[str, os.PathLike, Dict[str, Any], None], world_si
                     oneshot_max_bytes=int(a.get("oneshot_max_bytes", 256 * 1024)),
                     hip_graph=bool(a.get("hip_graph", False)),
                     debug_sync_streams=bool(a.get("debug_sync_streams", False)),
-                    fused_linear=bool(a.get("fused_linear", False)),
+                    fused_linear=None if a.get("fused_linear") is None else bool(a["fused_linear"]),
                     graph_module=bool(a.get("graph_module", False)))
     if amd.allreduce not in ("auto", "rccl", "oneshot"):
         raise ConfigError(f"amd.allreduce={amd.allreduce!r}: expected auto|rccl|oneshot")

@@ -82,7 +82,10 @@ class Engine:
         self.dtype = _DTYPES[config.compute_dtype]
         self.module = model.to(device=device, dtype=self.dtype)
         self.fused_linear_layers = 0
-        if config.amd.fused_linear and device.type == "cuda" and self.dtype == torch.float32:
+        fused_linear = config.amd.fused_linear
+        if fused_linear is None:  # auto: kernel injection unless the graphed module is asked for
+            fused_linear = not config.amd.graph_module
+        if fused_linear and device.type == "cuda" and self.dtype == torch.float32:
             from .ops.linear import inject_fused_linear
             self.fused_linear_layers = inject_fused_linear(self.module, grad_in_place=True)
         self.stage = config.zero_stage

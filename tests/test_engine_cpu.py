@@ -192,6 +192,8 @@ def test_hip_graph_config_falls_back_to_eager_on_cpu():
 def test_graph_module_config_parses_and_stays_eager_on_cpu():
     from distributed_gpu_test_amd.config import parse_config
     assert parse_config({"train_batch_size": 4, "amd": {"graph_module": True}}).amd.graph_module
+    assert parse_config({"train_batch_size": 4}).amd.fused_linear is None  # auto
+    assert parse_config({"train_batch_size": 4, "amd": {"fused_linear": False}}).amd.fused_linear is False
     torch.manual_seed(0)
     m = torch.nn.Sequential(torch.nn.Linear(8, 16), torch.nn.ReLU(), torch.nn.Linear(16, 1))
     engine, _, _, _ = dgt.initialize(model=m, config={"train_batch_size": 4, "amd": {"graph_module": True}})

@@ -183,7 +183,8 @@ def test_engine_fused_linear_matches_plain(graph):
     and under whole-step HIP-graph replay."""
     batches = _batches(10, 11) + _batches(2, 12, bs=8)
     base = {"train_batch_size": 32}
-    e1, l1, p1 = _run_engine(dict(base), batches)
+    e1, l1, p1 = _run_engine(dict(base, amd={"fused_linear": False}), batches)
+    assert e1.fused_linear_layers == 0
     amd = {"fused_linear": True, "hip_graph": graph}
     e2, l2, p2 = _run_engine(dict(base, amd=amd), batches, graph=graph)
     assert e2.fused_linear_layers == 2
@@ -213,3 +214,16 @@ def test_fused_linear_grad_in_place_accumulates_and_fires_hooks():
     assert sorted(fired) == [0, 0, 1, 1, 2, 2, 3, 3]
     for p, q in zip(m.parameters(), ref.parameters()):
         torch.testing.assert_close(p.grad, q.grad, rtol=1e-5, atol=1e-5)
+
+
+@pytest.mark.gpu
+def test_engine_fused_linear_auto_default():
+    """fused_linear unset = auto: an fp32 GPU engine injects the fused Linear kernels, a bf16 one
+    and a graph_module one do not."""
+    cases = [({}, 2), ({"amd": {"graph_module": True}}, 0), ({"bf16": {"enabled": True}}, 0),
+             ({"amd": {"fused_linear": False}}, 0)]
+    for extra, want in cases:
+        m = _mlp(4)
+        e, _, _, _ = dgt.initialize(model=m, config=dict({"train_batch_size": 32}, **extra))
+        assert e.fused_linear_layers == want, extra
+        e.close()
