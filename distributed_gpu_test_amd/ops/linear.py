@@ -110,11 +110,85 @@ class FusedLinear(nn.Linear):
         return super().extra_repr() + (", relu=True" if self.relu else "")
 
 
+class _FusedChainFn(torch.autograd.Function):
+    """A chain of fused Linear(+ReLU) layers as ONE autograd node: the forward queues one
+    ``linear_fwd`` per layer and the backward one ``linear_bwd`` per layer in reverse, the same
+    kernels in the same order as the per-layer path (bit-identical results), but one Function
+    apply and one backward node for the whole chain instead of one per layer (the eager engine's
+    step is host-bound: profiles/r2_engine_host_profile.txt)."""
+
+    @staticmethod
+    def forward(ctx, x, relus, grad_in_place, *wb):
+        ops = _ext.require()
+        acts = [x]
+        h = x
+        for i, relu in enumerate(relus):
+            w = wb[2 * i]
+            y = torch.empty(h.shape[0], w.shape[0], dtype=torch.float32, device=h.device)
+            ops.linear_fwd(h, w, wb[2 * i + 1], y, relu)
+            acts.append(y)
+            h = y
+        ctx.relus = relus
+        ctx.has_bias = tuple(b is not None for b in wb[1::2])
+        ctx.grad_in_place = grad_in_place and all(p is None or p.is_leaf for p in wb)
+        ctx.params = wb if ctx.grad_in_place else ()
+        ctx.save_for_backward(*acts, *wb[0::2])
+        return h
+
+    @staticmethod
+    def backward(ctx, dy):
+        ops = _ext.require()
+        L = len(ctx.relus)
+        saved = ctx.saved_tensors
+        acts, ws = saved[:L + 1], saved[L + 1:]
+        in_place = ctx.grad_in_place and all(p is None or _grad_view_ok(p) for p in ctx.params)
+        grads = [None] * (2 * L)
+        dy = dy.contiguous()
+        for i in reversed(range(L)):
+            dx = torch.empty_like(acts[i]) if (i > 0 or ctx.needs_input_grad[0]) else None
+            y = acts[i + 1] if ctx.relus[i] else None
+            if in_place:
+                w_leaf, b_leaf = ctx.params[2 * i], ctx.params[2 * i + 1]
+                ops.linear_bwd(dy, acts[i], ws[i], y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad, True)
+            else:
+                dw = torch.empty_like(ws[i])
+                db = torch.empty(ws[i].shape[0], dtype=torch.float32, device=dy.device) if ctx.has_bias[i] else None
+                ops.linear_bwd(dy, acts[i], ws[i], y, dx, dw, db)
+                grads[2 * i], grads[2 * i + 1] = dw, db
+            dy = dx
+        return (dy, None, None, *grads)
+
+
+class FusedChain(nn.Sequential):
+    """An ``nn.Sequential`` whose children are all ``FusedLinear`` (folded ReLUs left as
+    ``nn.Identity``): a 2-D fp32 GPU input every layer can take runs as one ``_FusedChainFn``;
+    anything else runs layer by layer.  Same children, keys and parameters as the Sequential."""
+
+    def _chain(self):
+        layers = [m for m in self if not isinstance(m, nn.Identity)]
+        return layers if layers and all(isinstance(m, FusedLinear) for m in layers) else None
+
+    def forward(self, x):
+        layers = self.__dict__.get("_dgt_layers")
+        if layers is None:
+            layers = self._chain() or []
+            self.__dict__["_dgt_layers"] = layers
+        if len(layers) > 1 and x.dim() == 2 and all(_fusable(x, m.weight) for m in layers):
+            wb = []
+            for m in layers:
+                wb.append(m.weight)
+                wb.append(m.bias)
+            return _FusedChainFn.apply(x.contiguous(), tuple(m.relu for m in layers), layers[0].grad_in_place, *wb)
+        return super().forward(x)
+
+
 def inject_fused_linear(module: nn.Module, grad_in_place: bool = False) -> int:
     """Replace nn.Linear (+ a directly following nn.ReLU inside an nn.Sequential) in place,
-    recursively; ``module`` itself may be the Sequential.  Returns the number of Linear layers
-    replaced.  ``grad_in_place``: see ``fused_linear`` (the engine sets it: its .grad tensors are
-    persistent views into the flat gradient bucket)."""
+    recursively; ``module`` itself may be the Sequential.  A plain ``nn.Sequential`` left holding
+    only fused layers becomes a ``FusedChain`` (its class is swapped in place, so the object, its
+    children and keys stay the same).  Returns the number of Linear layers replaced.
+    ``grad_in_place``: see ``fused_linear`` (the engine sets it: its .grad tensors are persistent
+    views into the flat gradient bucket)."""
     n = 0
     if isinstance(module, nn.Sequential):
         kids = list(module.children())
@@ -127,6 +201,8 @@ def inject_fused_linear(module: nn.Module, grad_in_place: bool = False) -> int:
                 n += 1
             elif not isinstance(k, FusedLinear):
                 n += inject_fused_linear(k, grad_in_place)
+        if type(module) is nn.Sequential and FusedChain._chain(module):
+            module.__class__ = FusedChain
         return n
     for name, child in list(module.named_children()):
         if type(child) is nn.Linear:

@@ -227,3 +227,44 @@ def test_engine_fused_linear_auto_default():
         e, _, _, _ = dgt.initialize(model=m, config=dict({"train_batch_size": 32}, **extra))
         assert e.fused_linear_layers == want, extra
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("in_place", [False, True])
+def test_fused_chain_is_bitwise_per_layer(in_place):
+    """A Sequential of fused layers runs as one autograd node (FusedChain): same kernels in the same
+    order as layer by layer, so outputs, input gradients and parameter gradients are bit-identical,
+    and with grad_in_place every parameter's post-accumulate hook fires once per backward."""
+    from distributed_gpu_test_amd.ops.linear import FusedChain, inject_fused_linear
+    torch.manual_seed(21)
+    base = torch.nn.Sequential(torch.nn.Linear(20, 64), torch.nn.ReLU(), torch.nn.Linear(64, 32),
+                               torch.nn.ReLU(), torch.nn.Linear(32, 1)).cuda()
+    chain, layered = copy.deepcopy(base), copy.deepcopy(base)
+    assert inject_fused_linear(chain, grad_in_place=in_place) == 3 and type(chain) is FusedChain
+    inject_fused_linear(layered, grad_in_place=in_place)
+    fired = []
+    for net in (chain, layered):
+        for i, p in enumerate(net.parameters()):
+            if in_place:
+                p.grad = torch.zeros_like(p)
+                p.register_post_accumulate_grad_hook(lambda _p, i=i, net=net: fired.append((id(net), i)))
+    x0 = torch.randn(4, 20, device="cuda")
+    outs, dxs = [], []
+    for net in (chain, layered):
+        x = x0.clone().requires_grad_(True)
+        for _ in range(2):
+            y = net(x) if net is chain else _layer_by_layer(net, x)
+            y.square().sum().backward()
+        outs.append(y.detach())
+        dxs.append(x.grad)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(dxs[0], dxs[1])
+    for p, q in zip(chain.parameters(), layered.parameters()):
+        assert torch.equal(p.grad, q.grad)
+    if in_place:
+        assert sorted(i for n, i in fired if n == id(chain)) == sorted(list(range(6)) * 2)
+
+
+def _layer_by_layer(net, x):
+    for m in net:
+        x = m(x)
+    return x
