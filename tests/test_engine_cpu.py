@@ -222,7 +222,7 @@ def test_fused_bce_falls_back_to_torch_on_cpu():
 def test_inject_fused_linear_keeps_parameters_and_falls_back_on_cpu():
     """Kernel injection swaps Linear(+ReLU) in place: same Parameter objects, same state_dict keys,
     ReLU folded; on CPU the forward falls back to F.linear and matches the original module."""
-    from distributed_gpu_test_amd.ops.linear import FusedLinear, inject_fused_linear
+    from distributed_gpu_test_amd.ops.linear import FusedChain, FusedLinear, inject_fused_linear
     m = _mlp(3)
     ref = copy.deepcopy(m)
     params = [id(p) for p in m.parameters()]
@@ -232,6 +232,14 @@ def test_inject_fused_linear_keeps_parameters_and_falls_back_on_cpu():
     assert isinstance(m[0], FusedLinear) and m[0].relu and isinstance(m[1], torch.nn.Identity)
     assert isinstance(m[2], FusedLinear) and not m[2].relu and isinstance(m[3], torch.nn.Tanh)
     nested = SimpleNet()
+    nested_ref = copy.deepcopy(nested)
+    nested_keys = list(nested.state_dict().keys())
     assert inject_fused_linear(nested) == 2 and nested.net[0].relu
+    # a Sequential left holding only fused layers becomes one FusedChain (same object and keys);
+    # one with another layer type (the Tanh above) stays a plain Sequential
+    assert type(nested.net) is FusedChain and list(nested.state_dict().keys()) == nested_keys
+    assert type(m) is torch.nn.Sequential
     x = torch.randn(5, 12)
     torch.testing.assert_close(m(x), ref(x))
+    x20 = torch.randn(4, 20)
+    torch.testing.assert_close(nested(x20), nested_ref(x20))
