@@ -90,6 +90,7 @@ def build_plan(trainer, n_steps: int):
 
 def oneshot_sweep(device, world: int, max_bytes: int = 1024 * 1024):
     """The IPC one-shot all-reduce over xGMI (csrc/comm.hip) on the small sizes where latency rules."""
+    from distributed_gpu_test_amd.parallel.comm import all_reduce_max as comm_max
     from distributed_gpu_test_amd.parallel.ipc import IpcChannel
     if world < 2:
         return []
@@ -108,6 +109,11 @@ def oneshot_sweep(device, world: int, max_bytes: int = 1024 * 1024):
             for _ in range(3):
                 ch.allreduce(t, o)
             torch.cuda.synchronize()
+            # a timed-out exchange (status word) ends the sweep on every rank: each further launch
+            # would spin until its own timeout
+            if comm_max(float(ch.check_status() != 0)) > 0:
+                print(f"[bench] one-shot sweep stopped at {size} B: exchange timeout", file=sys.stderr)
+                break
             dist.barrier()
             t0 = time.perf_counter()
             for _ in range(iters):
@@ -124,6 +130,8 @@ def oneshot_sweep(device, world: int, max_bytes: int = 1024 * 1024):
             algbw = n * 4 / dt_dev / 1e9
             out.append({"bytes": n * 4, "us": dt_dev * 1e6, "us_per_launch": dt * 1e6, "algbw_GBps": algbw,
                         "busbw_GBps": algbw * 2 * (world - 1) / world, "correct": ok})
+            if comm_max(0.0 if ok else 1.0) > 0:
+                break
             size *= 4
         return out
     finally:
@@ -344,7 +352,7 @@ def main(argv=None):
     gpu_sweeps = not args.no_sweep and device.type == "cuda" and world > 1
     sweep = allreduce_sweep(device, args.sweep_max_mb, world) if gpu_sweeps and comm.backend_name() == "nccl" else []
     oneshot = []
-    if gpu_sweeps:
+    if gpu_sweeps and fallback_reason is None:  # after an IPC failure the mailboxes are not retried
         try:
             oneshot = oneshot_sweep(device, world)
         except Exception as e:  # the sweep is informational; never lose the headline number to it
