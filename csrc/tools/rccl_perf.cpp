@@ -195,10 +195,10 @@ int main(int argc, char** argv) {
   }
   for (int i = 0; i < n; ++i) {
     HIPCHECK(hipSetDevice(devs[i]));
-    hipFree(sendb[i]);
-    hipFree(recvb[i]);
-    hipFree(wrong[i]);
-    ncclCommDestroy(comms[i]);
+    HIPCHECK(hipFree(sendb[i]));
+    HIPCHECK(hipFree(recvb[i]));
+    HIPCHECK(hipFree(wrong[i]));
+    NCCLCHECK(ncclCommDestroy(comms[i]));
   }
   (void)max_elems;
   return 0;

@@ -99,14 +99,40 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 8) -> str:
     return OUT
 
 
+# host-side AddressSanitizer + UBSan builds of the standalone tools.  Only the host
+# compile is instrumented: each -fsanitize= directly follows -Xarch_host (GPU ASan needs xnack+
+# code objects, which this pool does not run).  Run them with
+# ASAN_OPTIONS=detect_leaks=0:verify_asan_link_order=0 (the HIP runtime keeps its allocations to exit).
+SANITIZE = ["-Xarch_host", "-fsanitize=address", "-Xarch_host", "-fsanitize=undefined",
+            "-Xarch_host", "-fno-omit-frame-pointer", "-Xarch_host", "-fno-sanitize-recover=undefined"]
+
+
+def build_sanitized(verbose: bool = False, force: bool = False) -> list:
+    os.makedirs(BIN, exist_ok=True)
+    headers = glob.glob(os.path.join(CSRC, "*.h"))
+    out = []
+    for src in sorted(glob.glob(os.path.join(CSRC, "tools", "*.cpp"))):
+        exe = os.path.join(BIN, os.path.splitext(os.path.basename(src))[0] + "_asan")
+        if force or _newer(exe, [src] + headers):
+            _run([HIPCC, f"--offload-arch={ARCH}", "-O1", "-g", "-std=c++17", f"-I{CSRC}", *SANITIZE, src,
+                  "-o", exe, f"-L{ROCM}/lib", "-lrccl", f"-Wl,-rpath,{ROCM}/lib"], verbose)
+        out.append(exe)
+    return out
+
+
 def main(argv=None):
     ap = argparse.ArgumentParser()
     ap.add_argument("-v", "--verbose", action="store_true")
     ap.add_argument("-f", "--force", action="store_true")
     ap.add_argument("-j", "--jobs", type=int, default=8)
+    ap.add_argument("--sanitize", action="store_true",
+                    help="also build host-ASan/UBSan copies of the standalone tools (build/bin/*_asan)")
     a = ap.parse_args(argv)
     out = build(verbose=a.verbose, force=a.force, jobs=a.jobs)
     print(f"built {out}")
+    if a.sanitize:
+        for exe in build_sanitized(verbose=a.verbose, force=a.force):
+            print(f"built {exe}")
 
 
 if __name__ == "__main__":
