@@ -159,6 +159,7 @@ class Engine:
         self.metrics = MetricsSink.from_env(self.rank)
         self.faults = FaultInjector.from_env(self.rank)
         self._timers: Dict[str, float] = {}
+        self._seed_one: Optional[torch.Tensor] = None
         self._grad_norm: Optional[torch.Tensor] = None
         self._boundary_pending = False
         self.training = True
@@ -265,7 +266,7 @@ class Engine:
             scaled = scaled * self.loss_scaler.scale
         t0 = time.perf_counter() if self.config.wall_clock_breakdown else 0.0
         with tracing.range("dgt.backward"):
-            scaled.backward(retain_graph=retain_graph)
+            scaled.backward(self._backward_seed(scaled), retain_graph=retain_graph)
         if boundary:
             with tracing.range("dgt.allreduce_wait"):
                 self.reducer.finish()
@@ -275,6 +276,20 @@ class Engine:
                 torch.cuda.synchronize()
             self._timers["backward_ms"] = (time.perf_counter() - t0) * 1e3
         return loss
+
+    def _backward_seed(self, loss: torch.Tensor) -> Optional[torch.Tensor]:
+        """A persistent fp32 scalar 1 as the backward seed of a scalar loss: autograd would otherwise
+        launch a fill kernel (``ones_like``) every step, on a host-bound eager step.  Autograd never
+        writes its seed, and the parameters' .grad are the flat bucket's views (rebound before every
+        backward), so no AccumulateGrad can take the seed over as a .grad."""
+        if loss.dim() != 0 or loss.dtype != torch.float32 or loss.grad_fn is None:
+            return None
+        if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
+            return None
+        seed = self._seed_one
+        if seed is None or seed.device != loss.device:
+            seed = self._seed_one = torch.ones((), dtype=torch.float32, device=loss.device)
+        return seed
 
     def _clip_coef(self, grads: torch.Tensor, scale: float) -> Optional[torch.Tensor]:
         clip = self.config.gradient_clipping
