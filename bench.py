@@ -67,8 +67,8 @@ def parse_args(argv=None):
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--batch", type=int, default=1024, help="mlp: per-GPU micro-batch")
     ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
-                    help="mlp: 0 = all-reduce the weight gradients; 1 = reduce-scatter them, shard Adam, "
-                         "all-gather bf16 weights (ZeRO-1/2)")
+                    help="0 = all-reduce the gradients; 1 = ZeRO-1: reduce-scatter them, shard Adam, all-gather "
+                         "the parameters (simple: inside the fused kernel's exchange; mlp: per-layer RCCL)")
     ap.add_argument("--comm-dtype", default=None, choices=["bf16", "fp32"],
                     help="mlp: gradient wire dtype (DeepSpeed communication_data_type; default bf16)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce bus bandwidth sweep")
@@ -255,13 +255,8 @@ def _failed(trainer) -> bool:
 
 
 def device_identity(device) -> str:
-    """Host + PCI address of this rank's device: ranks sharing one card report the same string.
-    (A CPU rank is its own device: there is no card to share.)"""
-    import socket
-    if device.type != "cuda":
-        return f"{socket.gethostname()}/cpu-rank{dist.get_rank() if dist.is_initialized() else 0}"
-    p = torch.cuda.get_device_properties(device)
-    return f"{socket.gethostname()}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
+    from distributed_gpu_test_amd.accelerator import device_identity as ident
+    return ident(device)
 
 
 def params_consistent(params, world: int) -> bool:
@@ -312,8 +307,9 @@ def main(argv=None):
         trainer = DgtEngineBench(model, x, y, B, device, args.ds_config)
     else:
         trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=args.impl if device.type == "cuda" else "torch",
-                                 device=device)
+                                 device=device, zero_stage=args.zero_stage)
     plan, counts = build_plan(trainer, args.warmup + args.steps)
+    selftest = list(getattr(trainer, "xch_report", []))  # the IPC trainer's, kept across a fallback
     fallback_reason = None
     try:
         elapsed_max, mean_loss = timed_run(trainer, plan, counts, args, device, comm)
@@ -333,7 +329,8 @@ def main(argv=None):
         trainer.close()
         # use_ipc=False: the trainer's own automatic fallback (HIP graph with the native RCCL
         # communicator, or plain ProcessGroupNCCL if that cannot be set up on every rank)
-        trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl="fused", device=device, use_ipc=False)
+        trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl="fused", device=device, use_ipc=False,
+                                 zero_stage=args.zero_stage)
         plan, counts = build_plan(trainer, args.warmup + args.steps)
         elapsed_max, mean_loss = timed_run(trainer, plan, counts, args, device, comm)
         consistent = params_consistent(trainer.params, world)
@@ -389,7 +386,7 @@ def main(argv=None):
         "config": {"model": model_desc,
                    "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
                    "micro_batch_per_gpu": B, "impl": trainer.impl, "exchange": trainer.exchange,
-                   "closing_barrier": closing_barrier_kind(trainer, world)},
+                   "zero_stage": args.zero_stage, "closing_barrier": closing_barrier_kind(trainer, world)},
         "global_steps_per_sec": round(global_steps_per_s, 2),
         "samples_per_sec": round(global_steps_per_s * B * world, 2),
         "mean_loss": round(mean_loss, 6),
@@ -398,6 +395,7 @@ def main(argv=None):
         "oversubscribed": n_devices < world,
         "params_consistent_across_ranks": consistent,
         "ipc_fallback_reason": fallback_reason,
+        "exchange_selftest": selftest,
         "allreduce_busbw_GBps": None if peak_busbw is None else round(peak_busbw, 2),
         "allreduce_5KB_us": None if small is None else round(small["us"], 2),
         "oneshot_xgmi_5KB_us": None if small_os is None else round(small_os["us"], 2),

@@ -45,21 +45,10 @@ dgt::AdamHyper make_hyper(double lr, double beta1, double beta2, double eps, dou
   return h;
 }
 
-// Exchange shape of the fused kernel at this world size: DGT_XCH=oneshot|twoshot|auto.  auto is the
-// one-shot at every size: rehearsed with 4 and 8 ranks on one card the two-shot's second hop costs
-// more than its ~4x smaller polls save (6.5 vs 3.6 us/step at 4 ranks, 12.8 vs 6.9 at 8;
-// profiles/r2_xch_exchange_ab.txt).  Every rank of a job inherits the same environment, so every
-// rank picks the same protocol (the kernel rejects a mismatch with its template as a bad shape).
-int exchange_two_shot(int64_t world_size) {
-  const char* e = std::getenv("DGT_XCH");
-  const std::string m = e ? e : "auto";
-  TORCH_CHECK(m == "auto" || m == "oneshot" || m == "twoshot", "dgt: DGT_XCH must be auto, oneshot or twoshot, got ", m);
-  if (world_size < 4) return 0;  // the two-shot kernels exist for 4+ ranks only
-  return m == "twoshot";
-}
-
-dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank,
-                            int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks) {
+// zero1 / line: the fused kernel's exchange shape (ZeRO-1 or one-shot) and line format (3 = LL3,
+// 2 = LL2), chosen by the trainer (runtime/tiny_trainer.py) and the same on every rank
+dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank, int64_t world_size, int64_t stride,
+                            int64_t seq_base, int64_t timeout_ticks, int64_t zero1 = 0, int64_t line = 3) {
   dgt::Exchange ex;
   std::memset(&ex, 0, sizeof(ex));
   TORCH_CHECK(world_size >= 1 && world_size <= dgt::kMaxRanks, "dgt: world_size must be in [1, 8], got ", world_size);
@@ -70,7 +59,9 @@ dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank,
   ex.seq_base = seq_base;
   ex.timeout_ticks = timeout_ticks;
   ex.corrupt_step = -1;
-  ex.two_shot = exchange_two_shot(world_size);
+  TORCH_CHECK(line == 2 || line == 3, "dgt: exchange line format must be 2 (LL2) or 3 (LL3), got ", line);
+  ex.zero1 = zero1 ? 1 : 0;
+  ex.line = (int)line;
   if (world_size > 1) {
     TORCH_CHECK((int64_t)data_ptrs.size() == world_size, "dgt: need one mailbox pointer per rank");
     TORCH_CHECK(stride > 0 && stride % 256 == 0, "dgt: mailbox stride must be a positive multiple of 256 floats");
@@ -102,7 +93,8 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
                     double lr, double beta1, double beta2, double eps, double weight_decay, bool adamw,
                     int64_t adam_step0, c10::ArrayRef<int64_t> data_ptrs,
                     int64_t rank, int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks,
-                    int64_t corrupt_step, const std::optional<at::Tensor>& workspace) {
+                    int64_t corrupt_step, const std::optional<at::Tensor>& workspace, int64_t zero1,
+                    int64_t line) {
   TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
               " H=", hidden);
   TORCH_CHECK(beta1 > 0.5 && beta1 < 1.0 && beta2 > 0.0 && beta2 < 1.0, "dgt: fused kernel needs 0.5 < beta1 < 1");
@@ -152,7 +144,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   a.bc = bc.data_ptr<float>();
   a.loss_acc = loss_acc.data_ptr<double>();
   a.status = status.data_ptr<int>();
-  a.ex = make_exchange(data_ptrs, rank, world_size, stride, seq_base, timeout_ticks);
+  a.ex = make_exchange(data_ptrs, rank, world_size, stride, seq_base, timeout_ticks, zero1, line);
   a.ex.corrupt_step = corrupt_step;
   a.stamps = nullptr;
   if (world_size > 1) {
@@ -180,7 +172,7 @@ int64_t tiny_launcher_create(const at::Tensor& X, const at::Tensor& Y, const at:
                              const at::Tensor& status, int64_t n_features, int64_t hidden, double lr, double beta1,
                              double beta2, double eps, double weight_decay, bool adamw,
                              c10::ArrayRef<int64_t> data_ptrs, int64_t rank, int64_t world_size, int64_t stride,
-                             int64_t timeout_ticks, int64_t corrupt_step) {
+                             int64_t timeout_ticks, int64_t corrupt_step, int64_t zero1, int64_t line) {
   TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
               " H=", hidden);
   TORCH_CHECK(beta1 > 0.5 && beta1 < 1.0 && beta2 > 0.0 && beta2 < 1.0, "dgt: fused kernel needs 0.5 < beta1 < 1");
@@ -213,7 +205,7 @@ int64_t tiny_launcher_create(const at::Tensor& X, const at::Tensor& Y, const at:
   L->a.beta2 = beta2;
   L->a.loss_acc = loss_acc.data_ptr<double>();
   L->a.status = status.data_ptr<int>();
-  L->a.ex = make_exchange(data_ptrs, rank, world_size, stride, 0, timeout_ticks);
+  L->a.ex = make_exchange(data_ptrs, rank, world_size, stride, 0, timeout_ticks, zero1, line);
   L->a.ex.corrupt_step = corrupt_step;
   L->a.stamps = nullptr;
   L->f = (int)n_features;
@@ -224,6 +216,23 @@ int64_t tiny_launcher_create(const at::Tensor& X, const at::Tensor& Y, const at:
 }
 
 void tiny_launcher_destroy(int64_t handle) { delete reinterpret_cast<TinyLauncher*>(handle); }
+
+// the fused kernel's exchange alone, n_steps times, with torn-line-revealing payloads (tiny_mlp.hip)
+void tiny_xch_stress(int64_t n_features, int64_t hidden, c10::ArrayRef<int64_t> data_ptrs, int64_t rank,
+                     int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks, int64_t line,
+                     int64_t n_steps, const at::Tensor& status, const at::Tensor& errors) {
+  TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
+              " H=", hidden);
+  TORCH_CHECK(world_size >= 2 && n_steps >= 1, "dgt: the exchange stress test needs 2+ ranks and 1+ steps");
+  check_gpu(status, "status", at::kInt);
+  check_gpu(errors, "errors", at::kInt);
+  const int64_t need = dgt::tiny_mlp_exchange_floats((int)n_features, (int)hidden);
+  TORCH_CHECK(stride >= need && stride % 4 == 0, "dgt: mailbox stride ", stride, " < ", need);
+  c10::DeviceGuard guard(status.device());
+  const dgt::Exchange ex = make_exchange(data_ptrs, rank, world_size, stride, seq_base, timeout_ticks, 0, line);
+  DGT_CHECK_HIP(dgt::tiny_xch_stress((int)n_features, (int)hidden, ex, (int)n_steps, status.data_ptr<int>(),
+                                     errors.data_ptr<int>(), stream_of(status)));
+}
 
 }  // namespace
 
@@ -716,15 +725,19 @@ TORCH_LIBRARY(dgt, m) {
       "Tensor(c!) exp_avg_sq, Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, "
       "float beta1, float beta2, float eps, float weight_decay, bool adamw, int adam_step0, int[] data_ptrs, "
       "int rank, int world_size, int stride, int seq_base, int timeout_ticks, int corrupt_step=-1, "
-      "Tensor(f!)? workspace=None) -> ()",
+      "Tensor(f!)? workspace=None, int zero1=0, int line=3) -> ()",
       &tiny_mlp_train);
   m.def(
       "tiny_launcher_create(Tensor X, Tensor Y, Tensor(a!) params, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, "
       "Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, float beta1, float beta2, "
       "float eps, float weight_decay, bool adamw, int[] data_ptrs, int rank, int world_size, int stride, "
-      "int timeout_ticks, int corrupt_step) -> int",
+      "int timeout_ticks, int corrupt_step, int zero1=0, int line=3) -> int",
       &tiny_launcher_create);
   m.def("tiny_launcher_destroy(int handle) -> ()", &tiny_launcher_destroy);
+  m.def(
+      "tiny_xch_stress(int n_features, int hidden, int[] data_ptrs, int rank, int world_size, int stride, "
+      "int seq_base, int timeout_ticks, int line, int n_steps, Tensor(a!) status, Tensor(b!) errors) -> ()",
+      &tiny_xch_stress);
   m.def(
       "tiny_mlp_grad(Tensor X, Tensor Y, Tensor plan, Tensor counts, int step, Tensor params, Tensor(a!) grad, "
       "Tensor(b!) loss_acc, int n_features, int hidden) -> ()",

@@ -38,10 +38,10 @@ struct AdamHyper {
 // "mailbox" allocation (uncached device memory, IPC-exported); peers write into it over xGMI.
 //   data : LL lines [2 parity][kMaxRanks src][stride / 2]     (stride = payload floats per slot)
 // A low-latency (LL) line is 16 bytes = two {payload float, tag} pairs; the tag is the exchange's
-// sequence number + 1.  Each aligned 8-byte pair lands atomically, so a reader that sees both
-// tags of a line has both payloads: no release fence, no separate flag, no acquire fence, and
-// the reader's polls return the data itself (one xGMI latency per exchange).  Tags increase
-// monotonically per channel, so mailboxes are zeroed once, at creation.
+// sequence number + 1.  Each aligned 8-byte pair is written and read with ONE 64-bit atomic access,
+// so a reader that sees both tags of a line has both payloads: no release fence, no separate flag,
+// no acquire fence, and the reader's polls return the data itself (one xGMI latency per exchange).
+// Tags increase monotonically per channel, so mailboxes are zeroed once, at creation.
 struct Exchange {
   int rank;
   int world_size;
@@ -51,8 +51,10 @@ struct Exchange {
   unsigned* data[kMaxRanks];        // each rank's mailbox (index rank = local)
   long long corrupt_step;           // fault injection: at this 1-based optimizer step the fused kernel
                                     // corrupts one payload it sends to rank + 1 (-1 = never)
-  int two_shot;                     // fused kernel: reduce-scatter + all-gather instead of one-shot
-                                    // (4+ ranks only; see exchange_two_shot() in bindings.cpp)
+  int zero1;                        // fused kernel: ZeRO-1 exchange (gradients reduce-scattered to lane
+                                    // owners, owners update, parameters all-gathered) instead of the
+                                    // one-shot all-to-all of gradients
+  int line;                         // fused kernel line format: 3 = LL3 (16-byte lines), 2 = LL2 (8-byte pairs)
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
@@ -62,12 +64,18 @@ DGT_DEVICE long long ll_slot(const Exchange& ex, int parity, int src) {
   return (long long)(parity * kMaxRanks + src) * ex.stride * 2;
 }
 
-// push one LL line (two payload floats) into a peer's mailbox: one plain 16-byte store (the
-// mailbox is uncached memory, so it goes straight to the peer's HBM; the streaming (nt) hint is
-// left off: on hand-off traffic it measured slower, MI355X_MICROARCH.md "nt-handoff")
+// one {payload, tag} pair as ONE relaxed system-scope 64-bit store (global_store_dwordx2 sc0 sc1: the
+// mailbox is uncached memory, so it goes straight to the peer's HBM).  A naturally aligned 64-bit
+// atomic access is single-copy atomic, so the pair can never be seen half-written.
+DGT_DEVICE void ll_put_pair(unsigned* dst, float a, unsigned tag) {
+  const unsigned long long v = (unsigned long long)__float_as_uint(a) | ((unsigned long long)tag << 32);
+  __hip_atomic_store(reinterpret_cast<unsigned long long*>(dst), v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// push one LL line (two payload floats) into a peer's mailbox: two 64-bit atomic pair stores
 DGT_DEVICE void ll_put(unsigned* dst, float a, float b, unsigned tag) {
-  u32x4 v = {__float_as_uint(a), tag, __float_as_uint(b), tag};
-  *reinterpret_cast<u32x4*>(dst) = v;
+  ll_put_pair(dst, a, tag);
+  ll_put_pair(dst + 2, b, tag);
 }
 
 // one {payload, tag} pair from the local mailbox: a relaxed system-scope 64-bit load (sc0 sc1,
@@ -77,10 +85,14 @@ DGT_DEVICE unsigned long long ll_get(const unsigned* src) {
                            __HIP_MEMORY_SCOPE_SYSTEM);
 }
 DGT_DEVICE bool ll_ok(unsigned long long pair, unsigned tag) { return (unsigned)(pair >> 32) == tag; }
-// LL3 line: three payload floats and the tag in ONE 16-byte store / load, relying on an aligned
-// 16-byte access being single-copy atomic (one request to one 64-byte line on both ends, as
-// RCCL's LL128 relies on for whole 128-byte lines).  Were a line ever observed torn, the ranks'
-// parameters would diverge and the per-epoch replica check fails the job.  The poll loop must
+// LL3 line: three payload floats and the tag in ONE 16-byte store / load (global_store_dwordx4 /
+// global_load_dwordx4).  Correctness needs an aligned 16-byte access to be single-copy atomic end
+// to end over xGMI (one request to one 64-byte line on both ends, as RCCL's LL128 assumes for whole
+// 128-byte lines).  No document available to this build guarantees that width: the guaranteed
+// width is the 64-bit atomic that the LL2 format (ll_put_pair / ll_get) is built on.  So LL3 is
+// used only after an in-kernel stress test of >= 1000 exchanges with payloads that expose any torn
+// line (tiny_xch_stress, runtime/tiny_trainer.py) passed on this node; otherwise the trainer falls
+// back to LL2, and a replica divergence at run time re-runs the epoch on RCCL.  The poll loop must
 // re-issue the load every round (ll_fence_compiler() at the top of the loop).
 DGT_DEVICE void ll3_put(unsigned* dst, float a, float b, float c, unsigned tag) {
   u32x4 v = {__float_as_uint(a), __float_as_uint(b), __float_as_uint(c), tag};
@@ -89,6 +101,30 @@ DGT_DEVICE void ll3_put(unsigned* dst, float a, float b, float c, unsigned tag) 
 DGT_DEVICE u32x4 ll3_get(const unsigned* src) {
   return __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(src));
 }
+
+// Line formats of the fused kernel's exchange, as one interface: LN payload floats per 16-byte line.
+//   LL3: {p0, p1, p2, tag}, one 16-byte store / load;  LL2: {p0, tag, p1, tag}, two 64-bit atomics each way.
+template <int LN>
+struct LLine;
+
+template <>
+struct LLine<3> {
+  DGT_DEVICE static void put(unsigned* dst, float a, float b, float c, unsigned tag) { ll3_put(dst, a, b, c, tag); }
+  DGT_DEVICE static u32x4 get(const unsigned* src) { return ll3_get(src); }
+  DGT_DEVICE static bool ok(const u32x4& v, unsigned tag) { return v[3] == tag; }
+  DGT_DEVICE static unsigned word(const u32x4& v, int i) { return v[i]; }
+};
+
+template <>
+struct LLine<2> {
+  DGT_DEVICE static void put(unsigned* dst, float a, float b, float, unsigned tag) { ll_put(dst, a, b, tag); }
+  DGT_DEVICE static u32x4 get(const unsigned* src) {
+    const unsigned long long lo = ll_get(src), hi = ll_get(src + 2);
+    return u32x4{(unsigned)lo, (unsigned)(lo >> 32), (unsigned)hi, (unsigned)(hi >> 32)};
+  }
+  DGT_DEVICE static bool ok(const u32x4& v, unsigned tag) { return v[1] == tag && v[3] == tag; }
+  DGT_DEVICE static unsigned word(const u32x4& v, int i) { return v[2 * i]; }
+};
 DGT_DEVICE void ll_fence_compiler() { asm volatile("" ::: "memory"); }
 DGT_DEVICE float ll_val(unsigned long long pair) { return __uint_as_float((unsigned)pair); }
 

@@ -36,6 +36,11 @@ struct TinyTrainArgs {
 
 hipError_t tiny_mlp_train(int n_features, int hidden, const TinyTrainArgs& a, hipStream_t stream);
 
+// n_steps exchanges of the fused kernel's mailbox layout and line format (ex.line) with payloads that
+// expose any torn or lost line: bad words are added to *errors, a timeout sets *status.
+hipError_t tiny_xch_stress(int n_features, int hidden, const Exchange& ex, int n_steps, int* status, int* errors,
+                           hipStream_t stream);
+
 struct TinyGradArgs {
   const float* X;
   const float* Y;

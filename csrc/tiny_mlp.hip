@@ -70,11 +70,14 @@ struct TinyCfg {
   // Exchange payload per lane.  DENSE: the last W1 slot is live only in lane row lq == 0 (REM % 4
   // == 1, e.g. F = 20), so its 48 dead lanes carry the W2 gradients (12 in place, 4 moved from
   // lanes 0-3 to 20-23) and b2 (lane 24): NSL floats per lane.  Otherwise the W1 slots, W2 and b2
-  // padded to float4s.  Each LL3 line carries three payload floats and the tag.
+  // padded to float4s.  ZeRO-1 (NPAYZ) always uses the plain layout: a lane's payload then holds
+  // only the parameters whose Adam state lives in that lane (plus the replicated b2), so the rank
+  // that owns the lane can update them.  A line carries LN = 3 (LL3) or 2 (LL2) payload floats.
   static constexpr bool DENSE = (REM & 3) == 1 && NSL >= 2;
   static constexpr int NPAY = DENSE ? NSL : NSL + 2;
-  static constexpr int NLINE = (NPAY + 2) / 3;   // LL3 lines per lane and peer
-  static constexpr int XCH = NW * NLINE * 128;   // mailbox slot = 2*XCH words = NW*NLINE lines of 1 KiB
+  static constexpr int NPAYZ = NSL + 2;
+  static constexpr int NLMAX = (NPAYZ + 1) / 2;  // the most lines per lane and peer (ZeRO-1, LL2)
+  static constexpr int XCH = NW * NLMAX * 128;   // mailbox slot = 2*XCH words = NW*NLMAX lines of 1 KiB
   static constexpr int SX = NKT * 16 + 1;        // LDS row stride of the staged batch (+1: conflict-free)
   static constexpr int BM = 16;                  // max micro-batch (MFMA N of the forward)
   static constexpr int P = H * F + 2 * H + 1;    // global flat parameter count
@@ -324,21 +327,23 @@ DGT_DEVICE void fill_bias_table(const TinyTrainArgs& a, int t) {
 }
 
 // ------------------------------------------------------------------ gradient exchange (NP > 1)
-// Poll every peer's (NPAY+2)/3 LL3 lines of this lane in the local mailbox until all carry `tag` (or
-// the timeout passes: late), then sum them with the lane's own payload in rank order.  Every retry
-// re-reads the peers still pending: one local round trip per poll, not one per line or per
-// peer.  (Spinning on one line per peer first and reading the rest after measured slower: the extra round trip costs
-// more than the smaller polls save, profiles/r2_xch_exchange_ab.txt.)
-template <int NPAY, int NP>
-DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, unsigned tag,
-                               const float (&pay)[NPAY], float (&sum)[NPAY], unsigned long long t0, bool& late) {
-  constexpr int NL = (NPAY + 2) / 3;
-  u32x4 v[NP][NL];
-  // wave-uniform set of peers with a line still lacking the tag: a retry round re-reads only those
-  unsigned pend = 0;
-#pragma unroll
-  for (int p = 0; p < NP; ++p)
-    if (p < ex.world_size && p != ex.rank) pend |= 1u << p;
+// Lines of one lane's payload for one peer: line j of wave w, lane l sits at word
+// (w * NL + j) * 256 + 4 l of the (parity, sender) slot, so every store or poll instruction of a
+// wave moves 1 KiB contiguous.
+template <int NPAY, int LN>
+struct LinesOf {
+  static constexpr int NL = (NPAY + LN - 1) / LN;
+};
+
+// Poll the given peers' lines of this lane in the local mailbox until all carry `tag` (or the
+// timeout passes: late).  Every retry re-reads the peers still pending: one local round trip per
+// poll, not one per line or per peer.  (Spinning on one line per peer first and reading the rest
+// after measured slower: the extra round trip costs more than the smaller polls save,
+// profiles/r2_xch_exchange_ab.txt.)  `pend` is a wave-uniform mask of the peers to wait for.
+template <int NPAY, int NP, int LN>
+DGT_DEVICE void poll_peers(const Exchange& ex, int parity, long long wofs, unsigned tag, unsigned pend,
+                           u32x4 (&v)[NP][LinesOf<NPAY, LN>::NL], unsigned long long t0, bool& late) {
+  constexpr int NL = LinesOf<NPAY, LN>::NL;
   do {
     ll_fence_compiler();
 #pragma unroll
@@ -346,7 +351,7 @@ DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, u
       if ((pend >> p) & 1u) {
         const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, p) + wofs;
 #pragma unroll
-        for (int j = 0; j < NL; ++j) v[p][j] = ll3_get(src + j * 256);
+        for (int j = 0; j < NL; ++j) v[p][j] = LLine<LN>::get(src + j * 256);
       }
     }
 #pragma unroll
@@ -354,28 +359,68 @@ DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, u
       if ((pend >> p) & 1u) {
         bool ok = true;
 #pragma unroll
-        for (int j = 0; j < NL; ++j) ok = ok && v[p][j][3] == tag;
+        for (int j = 0; j < NL; ++j) ok = ok && LLine<LN>::ok(v[p][j], tag);
         if (__all(ok)) pend &= ~(1u << p);
       }
     }
     if (pend && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
   } while (pend && !late);
+}
+
+template <int NPAY, int LN>
+DGT_DEVICE float line_payload(const u32x4 (&v)[LinesOf<NPAY, LN>::NL], int k) {
+  return __uint_as_float(LLine<LN>::word(v[k / LN], k % LN));
+}
+
+// every peer's payload of this lane, summed with the lane's own in rank order (the same order, so
+// the same bits, on every rank)
+template <int NPAY, int NP, int LN>
+DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, unsigned tag,
+                               const float (&pay)[NPAY], float (&sum)[NPAY], unsigned long long t0, bool& late) {
+  u32x4 v[NP][LinesOf<NPAY, LN>::NL];
+  unsigned pend = 0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+    if (p < ex.world_size && p != ex.rank) pend |= 1u << p;
+  poll_peers<NPAY, NP, LN>(ex, parity, wofs, tag, pend, v, t0, late);
 #pragma unroll
   for (int p = 0; p < NP; ++p) {
     if (p >= ex.world_size) continue;
 #pragma unroll
-    for (int k = 0; k < NPAY; ++k) sum[k] += p == ex.rank ? pay[k] : __uint_as_float(v[p][k / 3][k % 3]);
+    for (int k = 0; k < NPAY; ++k) sum[k] += p == ex.rank ? pay[k] : line_payload<NPAY, LN>(v[p], k);
   }
 }
 
-// push this lane's payload into one peer's mailbox as LL3 lines (c0 replaces pay[0]: fault injection)
-template <int NPAY>
+// push this lane's payload into one peer's mailbox as LN-payload lines (c0 replaces pay[0]: fault
+// injection)
+template <int NPAY, int LN>
 DGT_DEVICE void push_payload(unsigned* dst, const float (&pay)[NPAY], float c0, unsigned tag) {
 #pragma unroll
-  for (int j = 0; j < (NPAY + 2) / 3; ++j) {
-    const int k = 3 * j;
-    ll3_put(dst + j * 256, j == 0 ? c0 : pay[k], k + 1 < NPAY ? pay[k + 1] : 0.f, k + 2 < NPAY ? pay[k + 2] : 0.f, tag);
+  for (int j = 0; j < LinesOf<NPAY, LN>::NL; ++j) {
+    const int k = LN * j;
+    LLine<LN>::put(dst + j * 256, j == 0 ? c0 : pay[k], k + 1 < NPAY ? pay[k + 1] : 0.f,
+                   k + 2 < NPAY ? pay[k + 2] : 0.f, tag);
   }
+}
+
+// ZeRO-1 payload (plain layout, either direction): the lane's W1 slots, its W2 element and b2
+template <int F, int H>
+DGT_DEVICE void pack_plain(const float (&w1)[TinyCfg<F, H>::NSP], float bw, float b2,
+                           float (&pay)[TinyCfg<F, H>::NPAYZ]) {
+  using C = TinyCfg<F, H>;
+#pragma unroll
+  for (int i = 0; i < C::NSL; ++i) pay[i] = w1[i];
+  pay[C::NSL] = bw;
+  pay[C::NSL + 1] = b2;
+}
+template <int F, int H>
+DGT_DEVICE void unpack_plain(const float (&pay)[TinyCfg<F, H>::NPAYZ], float scale,
+                             float (&w1)[TinyCfg<F, H>::NSP], float& bw, float& b2) {
+  using C = TinyCfg<F, H>;
+#pragma unroll
+  for (int i = 0; i < C::NSP; ++i) w1[i] = i < C::NSL ? pay[i] * scale : 0.f;
+  bw = pay[C::NSL] * scale;
+  b2 = pay[C::NSL + 1] * scale;
 }
 
 // gradients of one lane -> exchange payload (see TinyCfg::DENSE for the dense layout)
@@ -430,15 +475,44 @@ DGT_DEVICE void unpack_payload(const float (&sum)[TinyCfg<F, H>::NPAY], float in
 // branch, so backward and Adam form one basic block the scheduler can interleave.
 // WD: weight decay != 0 (Adam's L2 term / AdamW's decay compiled in; the reference's Adam has none,
 // and the per-pair uniform branches cost ~12 scalar branches per step).
-template <int F, int H, bool SMALLB, int NP, bool WD, bool TS>
+// One Adam step of the lane's register-resident parameters: two per packed-fp32 update (W2 and b2
+// form the last pair).
+template <int F, int H, bool WD>
+DGT_DEVICE void adam_lane(LaneState<F, H>& st, const float (&gw1)[TinyCfg<F, H>::NSP], float gbw, float gb2,
+                          const AdamHyper& hp, float step_size_neg, float inv_bc2_sqrt) {
+  using C = TinyCfg<F, H>;
+#pragma unroll
+  for (int i = 0; i < C::NSP; i += 2) {
+    f32x2 m = {st.m1[i], st.m1[i + 1]}, v = {st.v1[i], st.v1[i + 1]};
+    const f32x2 pn = adam_update_fast2<WD>(f32x2{st.w1[i], st.w1[i + 1]}, f32x2{gw1[i], gw1[i + 1]}, m, v, hp,
+                                           step_size_neg, inv_bc2_sqrt);
+    st.w1[i] = pn.x;
+    st.w1[i + 1] = pn.y;
+    st.m1[i] = m.x;
+    st.m1[i + 1] = m.y;
+    st.v1[i] = v.x;
+    st.v1[i + 1] = v.y;
+  }
+  f32x2 m = {st.mbw, st.mb2}, v = {st.vbw, st.vb2};
+  const f32x2 pn = adam_update_fast2<WD>(f32x2{st.bw, st.b2}, f32x2{gbw, gb2}, m, v, hp, step_size_neg, inv_bc2_sqrt);
+  st.bw = pn.x;
+  st.b2 = pn.y;
+  st.mbw = m.x;
+  st.mb2 = m.y;
+  st.vbw = v.x;
+  st.vb2 = v.y;
+}
+
+template <int F, int H, bool SMALLB, int NP, bool WD, int LN, bool Z>
 __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(TinyTrainArgs a) {
   using C = TinyCfg<F, H>;
   // NP: ranks the exchange is compiled for (1 = none; else the world size rounded up to 2, 4 or 8):
   // the poll registers scale with it, so 2- and 4-rank jobs do not carry the 8-rank register set.
-  // TS: two-shot exchange (reduce-scatter to lane owners, then all-gather of the sums) instead of
-  // the one-shot all-to-all
+  // LN: exchange line format (3 = LL3, 2 = LL2; dgt_common.h).  Z: ZeRO-1 exchange (gradients
+  // reduce-scattered to lane owners, the owner's Adam, parameters all-gathered) instead of the
+  // one-shot all-to-all of gradients.
   constexpr bool XCH = NP > 1;
-  static_assert(!TS || XCH, "the two-shot exchange needs an exchange");
+  static_assert(!Z || XCH, "the ZeRO-1 exchange needs ranks to exchange with");
   __shared__ TinySmem<F, H> sm;
   const int t = threadIdx.x, l = t & 63, lr = l & 15, lq = l >> 4;
   const int w = __builtin_amdgcn_readfirstlane(t >> 6);  // wave-uniform: scalar branches on w
@@ -449,7 +523,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
 #endif
 
   if (a.bmax > (SMALLB ? 4 : C::BM) || a.bmax < 1 || (ex.world_size > 1) != XCH || ex.world_size > NP ||
-      (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3))) || (ex.two_shot != 0) != TS) {
+      (ex.world_size > 1 && (ex.stride < C::XCH || (ex.stride & 3) || ex.line != LN)) || (ex.zero1 != 0) != Z) {
     if (t == 0) *a.status = kBadShape;
     return;
   }
@@ -527,113 +601,97 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     }
     DGT_STAMP(3);
 
+    // Adam bias corrections of this step from the table (wave-uniform, prefetched)
+    const float step_size_neg = bc_ss, inv_bc2_sqrt = bc_ib;
+    bc_ss = bc_ss_next;
+    bc_ib = bc_ib_next;
     if constexpr (XCH) {
-      // ---- LL exchange of this wave's gradients over xGMI: push, poll, sum in rank order.
+      // ---- LL exchange of this wave's gradients over xGMI.
       // Every rank maps lanes to parameters identically, so the mailbox is lane-linear: lane l of
-      // wave w packs its gradients into NPAY floats = NLINE LL lines at [w][line][l]; every store
-      // instruction writes 1 KiB contiguous into a peer, every poll reads the local mailbox.  The
-      // wave's memory-instruction throughput on uncached memory (~11 ns per 1 KiB instruction and
-      // CU, csrc/diag/store_lat.hip), not the round trip, bounds the exchange at 4-8 ranks: hence
-      // the dense payload (3 lines per peer instead of 4 for F = 20).
+      // wave w packs its payload into NL lines at [w][line][l]; every store instruction writes
+      // 1 KiB contiguous into a peer, every poll reads the local mailbox.  The wave's
+      // memory-instruction throughput on uncached memory (~11 ns per 1 KiB instruction and CU,
+      // csrc/diag/store_lat.hip), not the round trip, bounds the exchange at 4-8 ranks: hence the
+      // dense one-shot payload (2 LL3 lines per peer for F = 20).
       const long long seq = ex.seq_base + s;
       const int parity = (int)(seq & 1);
       const unsigned tag = (unsigned)(seq + 1);
-      float pay[C::NPAY];
-      pack_payload<F, H>(gw1, gbw, gb2, l, pay);
-      const long long wofs = (long long)w * C::NLINE * 256 + l * 4;
+      constexpr int NPX = Z ? C::NPAYZ : C::NPAY;
+      constexpr int NL = LinesOf<NPX, LN>::NL;
+      const long long wofs = (long long)w * NL * 256 + l * 4;
       const long long mine = ll_slot(ex, parity, ex.rank) + wofs;
-      float sum[C::NPAY];
+      float pay[NPX], sum[NPX];
 #pragma unroll
-      for (int k = 0; k < C::NPAY; ++k) sum[k] = 0.f;
+      for (int k = 0; k < NPX; ++k) sum[k] = 0.f;
       const unsigned long long t0 = realtime();
       bool late = false;
       static_assert(NP <= kMaxRanks, "at most kMaxRanks ranks per exchange");
       // fault injection (--fail-at R:S:corrupt): one payload to rank + 1 is off by 1.0 at step S, so
       // the replicas diverge and the per-epoch replica check must catch it (scalar test otherwise)
       const int victim = (ex.corrupt_step == a.adam_step0 + s + 1 && w == 0) ? (ex.rank + 1) % ex.world_size : -1;
-      if constexpr (!TS) {
+      if constexpr (!Z) {
+        // ---- one-shot: push to every peer, poll every peer, sum in rank order, everybody updates
+        pack_payload<F, H>(gw1, gbw, gb2, l, pay);
         for (int p = 0; p < ex.world_size; ++p) {
           if (p == ex.rank) continue;
-          push_payload<C::NPAY>(ex.data[p] + mine, pay, (p == victim && l == 0) ? pay[0] + 1.0f : pay[0], tag);
+          push_payload<NPX, LN>(ex.data[p] + mine, pay, (p == victim && l == 0) ? pay[0] + 1.0f : pay[0], tag);
         }
         // every peer's lines in flight at once: ONE local round trip per poll whatever the world
         // size (polling in batches of 4 peers cost a second round trip per step at 5-8 ranks)
-        poll_sum_peers<C::NPAY, NP>(ex, parity, wofs, tag, pay, sum, t0, late);
+        poll_sum_peers<NPX, NP, LN>(ex, parity, wofs, tag, pay, sum, t0, late);
+        if (late) sm.err = 1;
+        unpack_payload<F, H>(sum, inv_ws, l, gw1, gbw, gb2);
+        adam_lane<F, H, WD>(st, gw1, gbw, gb2, a.hp, step_size_neg, inv_bc2_sqrt);
       } else {
-        // ---- two-shot: lane l's lines are owned by rank l % P.  Reduce-scatter: every lane sends
-        // its payload to its owner only; the owner sums all ranks in rank order (the same order,
-        // so the same bits, as the one-shot) and all-gathers the sum to every peer.  Both phases
-        // land in the receiver's [parity][sender] slot at lane l: reduce-scatter traffic on the
-        // lanes the receiver owns, all-gather traffic on the lanes the sender owns, so one mailbox
-        // holds both.  A rank reads (P-1)/P of ONE payload per phase instead of P-1 payloads, at
-        // the price of a second hop -- which costs more than the bytes save (opt-in,
-        // DGT_XCH=twoshot; profiles/r2_xch_exchange_ab.txt).
+        // ---- ZeRO-1: lane l (its W1 slots, W2 element, Adam moments) is owned by rank l % P.
+        // Reduce-scatter: every lane sends its gradient payload to its owner only; the owner sums
+        // all ranks in rank order (the same order, so the same bits, as the one-shot), applies Adam
+        // to the state only it keeps current, and all-gathers the updated PARAMETERS to every
+        // peer.  Both phases land in the receiver's [parity][sender] slot at lane l: reduce-scatter
+        // traffic on the lanes the receiver owns, all-gather traffic on the lanes the sender owns,
+        // so one mailbox holds both.  Non-owner lanes never touch their moments: each rank's
+        // optimizer state is current only for its 1/P of the lanes (its checkpoint shard).
+        pack_plain<F, H>(gw1, gbw, gb2, pay);
         const int own = l % ex.world_size;
-        for (int p = 0; p < ex.world_size; ++p) {
-          if (p == ex.rank || p != own) continue;
-          push_payload<C::NPAY>(ex.data[p] + mine, pay, pay[0], tag);
-        }
+        if (own != ex.rank) push_payload<NPX, LN>(ex.data[own] + mine, pay, pay[0], tag);
         // owner lanes FIRST, in program order: a lane waiting for an all-gather must never run
         // ahead of its own wave's owner lanes, which other ranks wait on
         if (own == ex.rank) {
-          poll_sum_peers<C::NPAY, NP>(ex, parity, wofs, tag, pay, sum, t0, late);
+          poll_sum_peers<NPX, NP, LN>(ex, parity, wofs, tag, pay, sum, t0, late);
           if (!late) {
+            unpack_plain<F, H>(sum, inv_ws, gw1, gbw, gb2);
+            adam_lane<F, H, WD>(st, gw1, gbw, gb2, a.hp, step_size_neg, inv_bc2_sqrt);
+            pack_plain<F, H>(st.w1, st.bw, st.b2, pay);
             for (int p = 0; p < ex.world_size; ++p) {
               if (p == ex.rank) continue;
-              push_payload<C::NPAY>(ex.data[p] + mine, sum, (p == victim && l == ex.rank) ? sum[0] + 1.0f : sum[0], tag);
+              push_payload<NPX, LN>(ex.data[p] + mine, pay, (p == victim && l == ex.rank) ? pay[0] + 1.0f : pay[0],
+                                    tag);
             }
           }
         }
         if (own != ex.rank) {
           const unsigned* src = ex.data[ex.rank] + ll_slot(ex, parity, own) + wofs;
-          u32x4 v[C::NLINE];
+          u32x4 v[NL];
           bool ready;
           do {
             ll_fence_compiler();
             ready = true;
 #pragma unroll
-            for (int j = 0; j < C::NLINE; ++j) v[j] = ll3_get(src + j * 256);
+            for (int j = 0; j < NL; ++j) v[j] = LLine<LN>::get(src + j * 256);
 #pragma unroll
-            for (int j = 0; j < C::NLINE; ++j) ready = ready && v[j][3] == tag;
+            for (int j = 0; j < NL; ++j) ready = ready && LLine<LN>::ok(v[j], tag);
             if (!ready && (long long)(realtime() - t0) > ex.timeout_ticks) late = true;
           } while (!ready && !late);
 #pragma unroll
-          for (int k = 0; k < C::NPAY; ++k) sum[k] = __uint_as_float(v[k / 3][k % 3]);
+          for (int k = 0; k < NPX; ++k) sum[k] = line_payload<NPX, LN>(v, k);
+          unpack_plain<F, H>(sum, 1.0f, st.w1, st.bw, st.b2);
         }
+        if (late) sm.err = 1;
       }
-      if (late) sm.err = 1;
-      unpack_payload<F, H>(sum, inv_ws, l, gw1, gbw, gb2);
+    } else {
+      adam_lane<F, H, WD>(st, gw1, gbw, gb2, a.hp, step_size_neg, inv_bc2_sqrt);
     }
     DGT_STAMP(4);
-
-    // ---- Adam; bias corrections of this step from the table (wave-uniform, prefetched)
-    const float step_size_neg = bc_ss, inv_bc2_sqrt = bc_ib;
-    bc_ss = bc_ss_next;
-    bc_ib = bc_ib_next;
-    // two parameters per packed-fp32 update (W2 and b2 form the last pair)
-#pragma unroll
-    for (int i = 0; i < C::NSP; i += 2) {
-      f32x2 m = {st.m1[i], st.m1[i + 1]}, v = {st.v1[i], st.v1[i + 1]};
-      const f32x2 pn = adam_update_fast2<WD>(f32x2{st.w1[i], st.w1[i + 1]}, f32x2{gw1[i], gw1[i + 1]}, m, v, a.hp,
-                                         step_size_neg, inv_bc2_sqrt);
-      st.w1[i] = pn.x;
-      st.w1[i + 1] = pn.y;
-      st.m1[i] = m.x;
-      st.m1[i + 1] = m.y;
-      st.v1[i] = v.x;
-      st.v1[i + 1] = v.y;
-    }
-    {
-      f32x2 m = {st.mbw, st.mb2}, v = {st.vbw, st.vb2};
-      const f32x2 pn = adam_update_fast2<WD>(f32x2{st.bw, st.b2}, f32x2{gbw, gb2}, m, v, a.hp, step_size_neg,
-                                         inv_bc2_sqrt);
-      st.bw = pn.x;
-      st.b2 = pn.y;
-      st.mbw = m.x;
-      st.mb2 = m.y;
-      st.vbw = v.x;
-      st.vb2 = v.y;
-    }
     // rotate the prefetch pipeline
 #pragma unroll
     for (int i = 0; i < C::NSP; ++i) x[i] = xn[i];
@@ -728,8 +786,92 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_grad_kernel(TinyG
   }
 }
 
+// ------------------------------------------------------------------ exchange stress test
+// n_steps exchanges through the training kernel's own mailbox layout, line format and push / poll
+// code, every lane of every wave to every peer, with payloads that name (sequence, sender, wave,
+// lane, slot).  A line observed with the current tag but any word from an earlier exchange -- a
+// torn line -- fails the word comparison, as does a lost or misplaced write.  Bad words are counted
+// into *errors (one vector atomic per lane at the end); a spin past the timeout sets *status.
+// Payload words are normal floats in +-[1, 2) carrying 24 hashed bits.
+DGT_DEVICE unsigned stress_word(long long seq, int src, int w, int l, int k) {
+  unsigned x = (unsigned)seq * 0x9E3779B1u ^ (unsigned)(seq >> 32) * 0x85EBCA77u;
+  x ^= (unsigned)src * 0x27D4EB2Fu + (unsigned)w * 0x165667B1u + (unsigned)l * 0xC2B2AE3Du + (unsigned)k * 0x61C88647u;
+  x ^= x >> 15;
+  x *= 0x2C1B3C6Du;
+  x ^= x >> 12;
+  return (x & 0x807FFFFFu) | 0x3F800000u;
+}
+
+template <int F, int H, int NP, int LN>
+__global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_xch_stress_kernel(Exchange ex, int n_steps, int* status,
+                                                                            int* errors) {
+  using C = TinyCfg<F, H>;
+  constexpr int NPX = C::NPAYZ, NL = LinesOf<NPX, LN>::NL;  // the longest payload of the training kernel
+  const int t = threadIdx.x, l = t & 63;
+  const int w = __builtin_amdgcn_readfirstlane(t >> 6);
+  if (ex.world_size < 2 || ex.world_size > NP || ex.stride < C::XCH || (ex.stride & 3) || ex.line != LN) {
+    if (t == 0) *status = kBadShape;
+    return;
+  }
+  int bad = 0;
+  bool late = false;
+  unsigned all = 0;
+#pragma unroll
+  for (int p = 0; p < NP; ++p)
+    if (p < ex.world_size && p != ex.rank) all |= 1u << p;
+  for (int s = 0; s < n_steps && !late; ++s) {
+    const long long seq = ex.seq_base + s;
+    const int parity = (int)(seq & 1);
+    const unsigned tag = (unsigned)(seq + 1);
+    const long long wofs = (long long)w * NL * 256 + l * 4;
+    const long long mine = ll_slot(ex, parity, ex.rank) + wofs;
+    float pay[NPX];
+#pragma unroll
+    for (int k = 0; k < NPX; ++k) pay[k] = __uint_as_float(stress_word(seq, ex.rank, w, l, k));
+    for (int p = 0; p < ex.world_size; ++p)
+      if (p != ex.rank) push_payload<NPX, LN>(ex.data[p] + mine, pay, pay[0], tag);
+    u32x4 v[NP][NL];
+    poll_peers<NPX, NP, LN>(ex, parity, wofs, tag, all, v, realtime(), late);
+    if (!late) {
+#pragma unroll
+      for (int p = 0; p < NP; ++p) {
+        if (!((all >> p) & 1u)) continue;
+#pragma unroll
+        for (int k = 0; k < NPX; ++k) bad += LLine<LN>::word(v[p][k / LN], k % LN) != stress_word(seq, p, w, l, k);
+      }
+    }
+  }
+  if (bad) atomicAdd(errors, bad);
+  if (late) atomicExch(status, (int)kTimeout);
+}
+
 // ------------------------------------------------------------------ dispatch
 #define DGT_TINY_SHAPES(X) X(20, 64) X(32, 64) X(20, 128) X(8, 16)
+
+hipError_t tiny_xch_stress(int f, int h, const Exchange& ex, int n_steps, int* status, int* errors,
+                           hipStream_t stream) {
+  if (n_steps < 1 || ex.world_size < 2 || ex.world_size > kMaxRanks || (ex.line != 2 && ex.line != 3))
+    return hipErrorInvalidValue;
+#define DGT_XS_NP(F_, H_, NP_)                                                                           \
+  do {                                                                                                   \
+    if (ex.line == 2)                                                                                    \
+      hipLaunchKernelGGL((tiny_xch_stress_kernel<F_, H_, NP_, 2>), dim3(1), blk, 0, stream, ex, n_steps, status, errors); \
+    else                                                                                                 \
+      hipLaunchKernelGGL((tiny_xch_stress_kernel<F_, H_, NP_, 3>), dim3(1), blk, 0, stream, ex, n_steps, status, errors); \
+  } while (0)
+#define X_(F_, H_)                                                  \
+  if (f == F_ && h == H_) {                                         \
+    const dim3 blk(TinyCfg<F_, H_>::T);                             \
+    if (ex.world_size <= 2) DGT_XS_NP(F_, H_, 2);                   \
+    else if (ex.world_size <= 4) DGT_XS_NP(F_, H_, 4);              \
+    else DGT_XS_NP(F_, H_, 8);                                      \
+    return hipGetLastError();                                       \
+  }
+  DGT_TINY_SHAPES(X_)
+#undef X_
+#undef DGT_XS_NP
+  return hipErrorInvalidValue;
+}
 
 bool tiny_mlp_supported(int f, int h) {
 #define X_(F_, H_) if (f == F_ && h == H_) return true;
@@ -750,26 +892,29 @@ int tiny_mlp_exchange_floats(int f, int h) {
 hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
   if (!a.bc) return hipErrorInvalidValue;
   const bool wd = a.hp.weight_decay != 0.f;
-#define DGT_TINY_LAUNCH_TS(F_, H_, SB, NP_, TS_)                                                \
-  do {                                                                                      \
-    if (wd)                                                                                 \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, true, TS_>), dim3(1), blk, 0, stream, a); \
-    else                                                                                    \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, false, TS_>), dim3(1), blk, 0, stream, a); \
+  const bool ll2 = a.ex.line == 2, z = a.ex.zero1 != 0;
+  if (a.ex.world_size > 1 && a.ex.line != 2 && a.ex.line != 3) return hipErrorInvalidValue;
+#define DGT_TINY_LAUNCH_K(F_, H_, SB, NP_, LN_, Z_)                                                   \
+  do {                                                                                             \
+    if (wd)                                                                                        \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, true, LN_, Z_>), dim3(1), blk, 0, stream, a); \
+    else                                                                                           \
+      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, false, LN_, Z_>), dim3(1), blk, 0, stream, a); \
   } while (0)
-// the two-shot exchange is compiled for 4- and 8-rank jobs only (at 2 ranks it moves the same bytes
-// as the one-shot in two hops)
-#define DGT_TINY_LAUNCH_NP(F_, H_, SB, NP_)                                                      \
-  do {                                                                                      \
-    if (NP_ >= 4 && a.ex.two_shot) DGT_TINY_LAUNCH_TS(F_, H_, SB, NP_, (NP_ >= 4));         \
-    else DGT_TINY_LAUNCH_TS(F_, H_, SB, NP_, false);                                        \
+// exchange kernels: line format x ZeRO-1, for 2, 4 or 8 compiled ranks
+#define DGT_TINY_LAUNCH_NP(F_, H_, SB, NP_)                                                        \
+  do {                                                                                             \
+    if (ll2 && z) DGT_TINY_LAUNCH_K(F_, H_, SB, NP_, 2, true);                                     \
+    else if (ll2) DGT_TINY_LAUNCH_K(F_, H_, SB, NP_, 2, false);                                    \
+    else if (z) DGT_TINY_LAUNCH_K(F_, H_, SB, NP_, 3, true);                                       \
+    else DGT_TINY_LAUNCH_K(F_, H_, SB, NP_, 3, false);                                             \
   } while (0)
-#define DGT_TINY_LAUNCH(F_, H_, SB, XC)                                                          \
-  do {                                                                                      \
-    if (!(XC)) DGT_TINY_LAUNCH_NP(F_, H_, SB, 1);                                           \
-    else if (a.ex.world_size <= 2) DGT_TINY_LAUNCH_NP(F_, H_, SB, 2);                       \
-    else if (a.ex.world_size <= 4) DGT_TINY_LAUNCH_NP(F_, H_, SB, 4);                       \
-    else DGT_TINY_LAUNCH_NP(F_, H_, SB, 8);                                                 \
+#define DGT_TINY_LAUNCH(F_, H_, SB, XC)                                                            \
+  do {                                                                                             \
+    if (!(XC)) DGT_TINY_LAUNCH_K(F_, H_, SB, 1, 3, false);                                         \
+    else if (a.ex.world_size <= 2) DGT_TINY_LAUNCH_NP(F_, H_, SB, 2);                              \
+    else if (a.ex.world_size <= 4) DGT_TINY_LAUNCH_NP(F_, H_, SB, 4);                              \
+    else DGT_TINY_LAUNCH_NP(F_, H_, SB, 8);                                                        \
   } while (0)
 #define X_(F_, H_)                                                                            \
   if (f == F_ && h == H_) {                                                                   \
@@ -785,7 +930,7 @@ hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stre
 #undef X_
 #undef DGT_TINY_LAUNCH
 #undef DGT_TINY_LAUNCH_NP
-#undef DGT_TINY_LAUNCH_TS
+#undef DGT_TINY_LAUNCH_K
   return hipErrorInvalidValue;
 }
 

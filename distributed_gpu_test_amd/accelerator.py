@@ -30,8 +30,17 @@ class HipAccelerator:
         return torch.cuda.current_device()
 
     def set_device(self, local_rank: int) -> None:
-        """Bind ``local_rank``'s GPU (ranks beyond the visible count wrap: oversubscribed runs)."""
-        torch.cuda.set_device(local_rank % max(torch.cuda.device_count(), 1))
+        """Bind ``local_rank``'s GPU.  A local rank beyond the visible devices (a wrong
+        ``HIP_VISIBLE_DEVICES`` or ``GPUS_PER_NODE``) is an error: silently wrapping it onto a card
+        another rank uses would oversubscribe the node.  ``DGT_ALLOW_OVERSUBSCRIBE=1`` wraps on
+        purpose (the one-card multi-rank rehearsals); train.py and bench.py report it as
+        ``oversubscribed``."""
+        n = max(torch.cuda.device_count(), 1)
+        if local_rank >= n and not allow_oversubscribe():
+            raise RuntimeError(f"local rank {local_rank} has no GPU of its own: {n} visible device(s) "
+                               f"(HIP_VISIBLE_DEVICES={os.environ.get('HIP_VISIBLE_DEVICES', '<unset>')}); "
+                               "fix --nproc-per-node / GPUS_PER_NODE, or set DGT_ALLOW_OVERSUBSCRIBE=1 to share cards")
+        torch.cuda.set_device(local_rank % n)
         set_wait_mode(os.environ.get("DGT_HIP_WAIT", ""))
 
     def device(self, index: Optional[int] = None) -> torch.device:
@@ -67,6 +76,21 @@ class CpuAccelerator:
 
     def synchronize(self) -> None:
         pass
+
+
+def allow_oversubscribe() -> bool:
+    return os.environ.get("DGT_ALLOW_OVERSUBSCRIBE", "0") not in ("", "0", "false", "False")
+
+
+def device_identity(device) -> str:
+    """Host + PCI address of ``device``: ranks sharing one card report the same string (a CPU rank
+    is its own device: there is no card to share)."""
+    import socket
+    if device.type != "cuda":
+        import torch.distributed as dist
+        return f"{socket.gethostname()}/cpu-rank{dist.get_rank() if dist.is_initialized() else 0}"
+    p = torch.cuda.get_device_properties(device)
+    return f"{socket.gethostname()}/{p.pci_domain_id:04x}:{p.pci_bus_id:02x}:{p.pci_device_id:02x}"
 
 
 # hipSetDeviceFlags schedule bits: how a host thread waits for the device (synchronize, events)

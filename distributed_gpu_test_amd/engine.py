@@ -131,6 +131,7 @@ class Engine:
                              else torch.empty(self.master.numel(), dtype=self.dtype, device=device))
         self.exp_avg = torch.zeros_like(self.master)
         self.exp_avg_sq = torch.zeros_like(self.master)
+        self._ag_groups = None  # ZeRO: all-gather groups (allgather_bucket_size), built on first use
 
         # ---- communication
         comm_dtype = None
@@ -225,7 +226,9 @@ class Engine:
         with tracing.range("dgt.forward"):
             if self.graph_module and self.training and not kwargs and args and all(torch.is_tensor(a) for a in args):
                 fn = self._graphed_forward(args)
-                if fn is not None:
+                # a second forward of this signature before the first one's backward runs eagerly:
+                # replaying would overwrite the activations the pending backward still needs
+                if fn is not None and not fn.pending:
                     return fn(*args)
             return self.module(*args, **kwargs)
 
@@ -265,8 +268,9 @@ class Engine:
         if self.loss_scaler is not None:
             scaled = scaled * self.loss_scaler.scale
         t0 = time.perf_counter() if self.config.wall_clock_breakdown else 0.0
-        with tracing.range("dgt.backward"):
-            scaled.backward(self._backward_seed(scaled), retain_graph=retain_graph)
+        from .ops.linear import engine_backward
+        with tracing.range("dgt.backward"), engine_backward():
+            scaled.backward(self._backward_seed(scaled, loss), retain_graph=retain_graph)
         if boundary:
             with tracing.range("dgt.allreduce_wait"):
                 self.reducer.finish()
@@ -277,18 +281,22 @@ class Engine:
             self._timers["backward_ms"] = (time.perf_counter() - t0) * 1e3
         return loss
 
-    def _backward_seed(self, loss: torch.Tensor) -> Optional[torch.Tensor]:
-        """A persistent fp32 scalar 1 as the backward seed of a scalar loss: autograd would otherwise
-        launch a fill kernel (``ones_like``) every step, on a host-bound eager step.  Autograd never
-        writes its seed, and the parameters' .grad are the flat bucket's views (rebound before every
-        backward), so no AccumulateGrad can take the seed over as a .grad."""
-        if loss.dim() != 0 or loss.dtype != torch.float32 or loss.grad_fn is None:
+    def _backward_seed(self, scaled: torch.Tensor, loss: torch.Tensor) -> Optional[torch.Tensor]:
+        """A persistent fp32 scalar 1 as the backward seed, saving autograd's per-step ``ones_like``
+        fill kernel on a host-bound eager step -- but only when the seed goes into a node the
+        engine itself created (the 1/gas division or the loss-scale multiply), whose backward
+        reads its incoming gradient without writing it.  A loss the user's code produced directly
+        gets autograd's own fresh seed: a custom Function may edit grad_output in place, which
+        would corrupt a shared seed for every later step."""
+        if scaled is loss or scaled.grad_fn is None or scaled.grad_fn is loss.grad_fn:
+            return None
+        if scaled.dim() != 0 or scaled.dtype != torch.float32:
             return None
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             return None
         seed = self._seed_one
-        if seed is None or seed.device != loss.device:
-            seed = self._seed_one = torch.ones((), dtype=torch.float32, device=loss.device)
+        if seed is None or seed.device != scaled.device:
+            seed = self._seed_one = torch.ones((), dtype=torch.float32, device=scaled.device)
         return seed
 
     def _clip_coef(self, grads: torch.Tensor, scale: float) -> Optional[torch.Tensor]:
@@ -337,24 +345,53 @@ class Engine:
                 torch.cuda.synchronize()
             self._timers["step_ms"] = (time.perf_counter() - t0) * 1e3
 
+    def _allgather_group_plan(self):
+        """Reduce buckets grouped into all-gather groups of at most ``allgather_bucket_size``
+        elements (DeepSpeed's knob; default 8M elements = 32 MiB of fp32).  Each group goes out as ONE
+        coalesced RCCL launch (a group call: every rank's shards of every bucket of the group in
+        flight together), so on an 8 x MI355X node a group keeps the 7 xGMI links of every GPU busy
+        for tens of microseconds instead of paying one collective's latency per small bucket."""
+        cap = max(int(self.config.zero.allgather_bucket_size), 1)
+        groups, cur, n = [], [], 0
+        for i, b in enumerate(self.layout.buckets):
+            if cur and n + b.numel > cap:
+                groups.append(cur)
+                cur, n = [], 0
+            cur.append(i)
+            n += b.numel
+        if cur:
+            groups.append(cur)
+        return groups
+
     def _allgather_params(self) -> None:
         src = self.param_lp if self.param_lp is not None else self.master
-        works = []
-        off = 0
         on = comm.collectives_on(self.world_size)
+        if self._ag_groups is None:
+            self._ag_groups = self._allgather_group_plan()
+        pieces, off = [], 0
         for b in self.layout.buckets:
             n = b.numel // self.world_size
-            out = self.store.param_buf[b.start:b.start + b.numel]
-            piece = src[off:off + n]
-            if on and comm.needs_host_staging(out):
-                host = torch.empty(b.numel, dtype=piece.dtype)
-                dist.all_gather_into_tensor(host, piece.detach().cpu())
-                out.copy_(host)
-            elif on:
-                works.append(dist.all_gather_into_tensor(out, piece, async_op=True))
-            else:
-                out.copy_(piece)
+            pieces.append((self.store.param_buf[b.start:b.start + b.numel], src[off:off + n]))
             off += n
+        works = []
+        coalesce = on and comm.backend_name() == "nccl" and hasattr(dist, "_coalescing_manager")
+        for group in self._ag_groups:
+            if not on:
+                for i in group:
+                    pieces[i][0].copy_(pieces[i][1])
+            elif comm.needs_host_staging(pieces[group[0]][0]):
+                for i in group:
+                    out, piece = pieces[i]
+                    host = torch.empty(out.numel(), dtype=piece.dtype)
+                    dist.all_gather_into_tensor(host, piece.detach().cpu())
+                    out.copy_(host)
+            elif coalesce:
+                with dist._coalescing_manager(device=self.device, async_ops=True) as cm:
+                    for i in group:
+                        dist.all_gather_into_tensor(pieces[i][0], pieces[i][1])
+                works.append(cm)
+            else:
+                works.extend(dist.all_gather_into_tensor(pieces[i][0], pieces[i][1], async_op=True) for i in group)
         for w in works:
             w.wait()
 

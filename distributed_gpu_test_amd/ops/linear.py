@@ -15,11 +15,34 @@ Taken only for fp32 GPU tensors of small shapes (``SMALL``); anything else runs 
 """
 from __future__ import annotations
 
+import contextlib
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
 from . import _ext
+
+# > 0 while the engine runs a backward (Engine.backward / the graphed step): only then do the
+# in-place kernels add dW / db straight into the parameters' .grad views (the engine's flat
+# gradient buckets).  Autograd runs a HIP Function's backward on its device thread, so this is a
+# process-wide counter, not a thread-local.  Any other backward -- torch.autograd.grad on the
+# parameters, a user's own loss.backward() -- gets dW / db returned to autograd as usual.
+_ENGINE_BACKWARD = 0
+
+
+@contextlib.contextmanager
+def engine_backward():
+    global _ENGINE_BACKWARD
+    _ENGINE_BACKWARD += 1
+    try:
+        yield
+    finally:
+        _ENGINE_BACKWARD -= 1
+
+
+def _in_place_active() -> bool:
+    return _ENGINE_BACKWARD > 0
 
 SMALL_M = 256            # rows per call (batch)
 SMALL_WORK = 1 << 22     # M * N * K: beyond this a tiled GEMM (hipBLASLt / csrc/gemm.hip) wins
@@ -44,7 +67,8 @@ class _FusedLinearFn(torch.autograd.Function):
         dy = dy.contiguous()
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         w_leaf, b_leaf = ctx.params
-        if ctx.grad_in_place and w_leaf.requires_grad and _grad_view_ok(w_leaf) and (b_leaf is None or _grad_view_ok(b_leaf)):
+        if (ctx.grad_in_place and _in_place_active() and ctx.needs_input_grad[1] and w_leaf.requires_grad
+                and _grad_view_ok(w_leaf) and (b_leaf is None or (b_leaf.requires_grad and _grad_view_ok(b_leaf)))):
             # accumulate straight into the existing .grad views (the engine's flat bucket): no
             # separate AccumulateGrad add kernel per parameter.  Autograd still runs the leaves'
             # AccumulateGrad nodes with an undefined gradient, which fire the post-accumulate hooks
@@ -72,9 +96,9 @@ def _fusable(x: torch.Tensor, weight: torch.Tensor) -> bool:
 
 def fused_linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = False,
                  grad_in_place: bool = False) -> torch.Tensor:
-    """``grad_in_place``: backward adds dW / db into existing ``.grad`` tensors of leaf parameters
-    instead of returning them to autograd (their post-accumulate hooks still fire); only for
-    ``loss.backward()``-style use, never ``torch.autograd.grad`` on the parameters."""
+    """``grad_in_place``: inside the engine's backward (``engine_backward``), backward adds dW / db
+    into the existing ``.grad`` tensors of leaf parameters instead of returning them to autograd
+    (their post-accumulate hooks still fire); any other backward gets them returned as usual."""
     if _fusable(x, weight):
         return _FusedLinearFn.apply(x.contiguous(), weight, bias, relu, grad_in_place)
     y = F.linear(x, weight, bias)
@@ -141,20 +165,27 @@ class _FusedChainFn(torch.autograd.Function):
         L = len(ctx.relus)
         saved = ctx.saved_tensors
         acts, ws = saved[:L + 1], saved[L + 1:]
-        in_place = ctx.grad_in_place and all(p is None or _grad_view_ok(p) for p in ctx.params)
+        active = ctx.grad_in_place and _in_place_active()
         grads = [None] * (2 * L)
         dy = dy.contiguous()
         for i in reversed(range(L)):
             dx = torch.empty_like(acts[i]) if (i > 0 or ctx.needs_input_grad[0]) else None
             y = acts[i + 1] if ctx.relus[i] else None
+            # per layer: a parameter frozen after injection (requires_grad False) gets nothing, and
+            # only a layer whose trained tensors all have live .grad views accumulates in place
+            w_need, b_need = ctx.needs_input_grad[3 + 2 * i], ctx.has_bias[i] and ctx.needs_input_grad[4 + 2 * i]
+            w_leaf = ctx.params[2 * i] if active else None
+            b_leaf = ctx.params[2 * i + 1] if active else None
+            in_place = (active and w_need and _grad_view_ok(w_leaf)
+                        and (not ctx.has_bias[i] or (b_need and _grad_view_ok(b_leaf))))
             if in_place:
-                w_leaf, b_leaf = ctx.params[2 * i], ctx.params[2 * i + 1]
                 ops.linear_bwd(dy, acts[i], ws[i], y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad, True)
             else:
                 dw = torch.empty_like(ws[i])
                 db = torch.empty(ws[i].shape[0], dtype=torch.float32, device=dy.device) if ctx.has_bias[i] else None
                 ops.linear_bwd(dy, acts[i], ws[i], y, dx, dw, db)
-                grads[2 * i], grads[2 * i + 1] = dw, db
+                grads[2 * i] = dw if w_need else None
+                grads[2 * i + 1] = db if b_need else None
             dy = dx
         return (dy, None, None, *grads)
 

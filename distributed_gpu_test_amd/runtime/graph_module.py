@@ -17,9 +17,13 @@ autograd runs their ``AccumulateGrad`` nodes with an undefined gradient: nothing
 the post-accumulate hooks (the bucket reducer: all-reduce / reduce-scatter overlapped with the rest
 of backward) still fire, as for the fused Linear kernels (``ops/linear.py``).
 
-Same kernels, same accumulation order: the trajectory matches the eager engine.  The returned
-outputs alias the static output buffers (overwritten by the next replay of that signature), as with
-``torch.cuda.make_graphed_callables``.
+Same kernels, same accumulation order: the trajectory matches the eager engine.  The warmup runs
+before capture execute the module for real, so the module's buffers (BatchNorm running stats,
+``num_batches_tracked``) and the CPU / GPU RNG states are saved before them and restored after.
+The returned outputs alias the static output buffers (overwritten by the next replay of that
+signature), as with ``torch.cuda.make_graphed_callables``; so a signature's graph is only
+replayed once its previous forward's backward has run (``pending``): a second forward of the same
+signature before that runs eagerly instead of overwriting the first one's activations.
 """
 from __future__ import annotations
 
@@ -62,6 +66,9 @@ class GraphedModule:
         cur = torch.cuda.current_stream()
         side = torch.cuda.Stream()
         side.wait_stream(cur)
+        # the warmup executes the module: keep its buffers and the RNG streams as they were
+        bufs = [(b, b.detach().clone()) for b in module.buffers()]
+        cpu_rng, gpu_rng = torch.get_rng_state(), torch.cuda.get_rng_state()
         with torch.cuda.stream(side):  # library handles / workspaces before capture
             for _ in range(warmup):
                 outs = [o for o in run() if o.requires_grad]
@@ -69,6 +76,11 @@ class GraphedModule:
                                     allow_unused=True)
                 del outs
         cur.wait_stream(side)
+        with torch.no_grad():
+            for b, saved in bufs:
+                b.copy_(saved)
+        torch.set_rng_state(cpu_rng)
+        torch.cuda.set_rng_state(gpu_rng)
         self.pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
         with torch.cuda.graph(self.fwd, pool=self.pool):
@@ -87,6 +99,7 @@ class GraphedModule:
         self.static_gin = gs[len(self.params):]
         self.single = torch.is_tensor(out) or len(out) == 1
         self.replays = 0
+        self.pending = False  # a replayed forward whose backward has not run yet
 
     def __call__(self, *args):
         outs = _Replay.apply(self, *args, *self.params)
@@ -101,6 +114,7 @@ class _Replay(torch.autograd.Function):
                 dst.copy_(src)
         runner.fwd.replay()
         runner.replays += 1
+        runner.pending = torch.is_grad_enabled()  # under no_grad no backward will come
         ctx.runner = runner
         outs = tuple(o.detach() for o in runner.static_out)
         for i, o in enumerate(outs):
@@ -111,6 +125,7 @@ class _Replay(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *gouts):
         r: GraphedModule = ctx.runner
+        r.pending = False
         for dst, i in zip(r.static_gout, r.grad_out_idx):
             g = gouts[i]
             if g is None:

@@ -123,7 +123,9 @@ class GraphedStep:
         e.store.rebind_grads()  # .grad views into the flat bucket (host-side binding, no kernel)
         e.store.grad_buf.zero_()
         loss = self.loss_fn(*args)
-        loss.float().backward(self._seed(loss))
+        from ..ops.linear import engine_backward
+        with engine_backward():
+            loss.float().backward(self._seed(loss))
         grads = self._reduce()
         scale = 1.0 / e.world_size
         coef = self._clip(grads, scale)
@@ -137,13 +139,16 @@ class GraphedStep:
         return loss.detach()
 
     def _seed(self, loss: torch.Tensor) -> Optional[torch.Tensor]:
-        """A persistent ones tensor for the backward seed, so a captured step has no fill node
-        for it.  Made only outside capture (a tensor from the graph's private pool must not
-        outlive its graph); a capture that finds none lets autograd fill its own."""
+        """A persistent tensor for the backward seed.  Made only outside capture (a tensor from the
+        graph's private pool must not outlive its graph); a capture that finds none lets autograd
+        fill its own.  It is re-filled with 1 before every use (one fill node in the captured step):
+        the loss comes from user code, and a custom Function may edit its grad_output in place."""
         key = (tuple(loss.shape), loss.device)
         seed = self.seeds.get(key)
         if seed is None and not torch.cuda.is_current_stream_capturing():
             seed = self.seeds[key] = torch.ones(loss.shape, dtype=torch.float32, device=loss.device)
+        elif seed is not None:
+            seed.fill_(1.0)
         return seed
 
     # ------------------------------------------------------------------ public

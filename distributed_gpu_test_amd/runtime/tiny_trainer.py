@@ -18,10 +18,25 @@ GPU instead:
 
 The epoch's mean loss is accumulated on the device and read once per epoch, giving the same
 printed value as the reference's per-step ``loss.item()`` sum.
+
+Exchange robustness (the fused path at world size > 1): before training, the mailboxes pass the
+one-shot all-reduce self-test, then the in-kernel exchange's line format is chosen by a stress
+test of >= 1000 exchanges whose payloads expose any torn or lost line (``DGT_XCH_LINE``: LL3,
+16-byte lines, if it passes, else LL2, 8-byte atomic pairs, else RCCL), then 8 training steps are
+checked against the RCCL path.  At run time every epoch starts from a snapshot (params, moments,
+step counters); a kernel-reported exchange timeout or a replica divergence at the epoch's end
+makes every rank restore it and re-run the epoch on the RCCL path (``exchange_fallback``, logged
+to stderr, ``DGT_METRICS_JSONL`` and ``DGT_HEALTH_LOG``), unless ``strict_exchange`` keeps it
+fatal.
+
+``zero_stage=1`` (DeepSpeed ZeRO-1): the fused kernel's exchange becomes reduce-scatter
+of the gradients to lane owners, the owner's Adam on the moments only it keeps, and all-gather of
+the updated parameters; checkpoints hold one ``zero_pp_rank_{r}`` shard of owned elements per rank.
 """
 from __future__ import annotations
 
 import os
+import sys
 from typing import Any, Dict, List, Optional
 
 import torch
@@ -36,28 +51,66 @@ from ..parallel import comm
 from . import checkpoint as ckpt
 from ..utils import tracing
 from ..utils.fault import FaultInjector
+from ..utils.metrics import MetricsSink, health_event
 from .optim_state import adam_state_to_flat, flat_to_adam_state
 
 IMPLS = ("auto", "fused", "graph", "stepwise", "torch")
+LINES = {"ll3": 3, "ll2": 2}
 
 
 def _raw_stream(index: int) -> int:
     return torch._C._cuda_getCurrentRawStream(index)
 
 
-def xch_mode(world_size: int) -> str:
-    """Protocol of the fused kernel's gradient exchange, as csrc/bindings.cpp exchange_two_shot()
-    picks it: DGT_XCH=oneshot|twoshot|auto.  auto = one-shot: the two-shot (reduce-scatter to lane
-    owners + all-gather, 4+ ranks) reads ~4x fewer bytes per poll but pays a second hop, and
-    measured ~2x slower per step in the 4/8-rank rehearsals (profiles/r2_xch_exchange_ab.txt)."""
-    mode = os.environ.get("DGT_XCH", "auto")
-    if mode not in ("auto", "oneshot", "twoshot"):
-        raise ValueError(f"DGT_XCH must be auto, oneshot or twoshot, got {mode!r}")
-    return "twoshot" if world_size >= 4 and mode == "twoshot" else "oneshot"
+def line_candidates() -> List[int]:
+    """Exchange line formats to try, in order (``DGT_XCH_LINE=auto|ll3|ll2``): auto = LL3 (three
+    payload floats per 16-byte line, fewest instructions) if its stress test passes, else LL2
+    (two 8-byte {payload, tag} pairs per line: needs only 64-bit single-copy atomicity)."""
+    mode = os.environ.get("DGT_XCH_LINE", "auto")
+    if mode == "auto":
+        return [3, 2]
+    if mode not in LINES:
+        raise ValueError(f"DGT_XCH_LINE must be auto, ll3 or ll2, got {mode!r}")
+    return [LINES[mode]]
+
+
+def stress_steps() -> int:
+    return max(1, int(os.environ.get("DGT_XCH_STRESS_STEPS", "2000")))
+
+
+def zero1_owner_map(n_features: int, hidden: int, world_size: int) -> torch.Tensor:
+    """Owning rank of every flat parameter under the fused kernel's ZeRO-1 exchange: the kernel
+    keeps W1[j][k] / b1[j] in lane (j % 16, slot) of wave j // 16 and W2 in lanes 0-3 of each DPP
+    row (``csrc/tiny_mlp.hip`` TinyCfg::slot_index / bw_index); lane l is owned by rank l % world;
+    b2 is replicated and written back by lane 0 (rank 0)."""
+    F, H = n_features, hidden
+    nkt = (F + 1 + 15) // 16
+    rem = F + 1 - 16 * (nkt - 1)
+    nsl = 4 * (nkt - 1) + (rem + 3) // 4
+    g_b1, g_w2, g_b2 = H * F, H * F + H, H * F + 2 * H
+    owner = torch.full((simple_net_numel(F, H),), -1, dtype=torch.int64)
+    for w in range(H // 16):
+        for l in range(64):
+            lr, lq, own = l & 15, l >> 4, l % world_size
+            for i in range(nsl):
+                k = 16 * (i >> 2) + lq + 4 * (i & 3)
+                if k < F:
+                    owner[(16 * w + lr) * F + k] = own
+                elif k == F:
+                    owner[g_b1 + 16 * w + lr] = own
+            if lr < 4:
+                owner[g_w2 + 16 * w + 4 * lq + lr] = own
+    owner[g_b2] = 0
+    assert bool((owner >= 0).all()), "every parameter has an owner lane"
+    return owner
 
 
 class ReplicaDivergence(RuntimeError):
     """Data-parallel replicas ended an epoch with different parameters (a corrupted exchange)."""
+
+
+class ExchangeFailure(RuntimeError):
+    """The fused kernel's in-kernel exchange failed on some rank (timeout or replica divergence)."""
 
 
 def fused_supported(n_features: int, hidden: int, batch_size: int) -> bool:
@@ -71,9 +124,12 @@ class TinyMLPTrainer:
                  lr: float = 1e-3, betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0,
                  adamw: bool = False, device: Optional[torch.device] = None, impl: str = "auto",
                  sampler_seed: int = 0, ds_config: Optional[Dict[str, Any]] = None, use_ipc: bool = True,
-                 exchange_timeout_s: Optional[float] = None):
+                 exchange_timeout_s: Optional[float] = None, zero_stage: int = 0,
+                 strict_exchange: Optional[bool] = None):
         if impl not in IMPLS:
             raise ValueError(f"impl must be one of {IMPLS}")
+        if zero_stage not in (0, 1):
+            raise ValueError("TinyMLPTrainer supports zero_stage 0 or 1")
         self.F = model.n_features
         self.H = model.hidden
         self.B = batch_size
@@ -87,6 +143,13 @@ class TinyMLPTrainer:
         self.global_steps = 0
         self.global_samples = 0
         self.channel = None
+        self.zero_stage = zero_stage
+        self.line = 3            # exchange line format of the fused kernel (set by the stress test)
+        self.xch_report: List[Dict[str, Any]] = []  # start-up self-tests of the exchange
+        self.fallbacks: List[Dict[str, Any]] = []   # run-time exchange fallbacks
+        self.strict_exchange = (os.environ.get("DGT_STRICT_EXCHANGE", "0") not in ("", "0")
+                                if strict_exchange is None else bool(strict_exchange))
+        self._corrupt_off = False  # the torch path's corrupt fault is one-shot (a re-run is clean)
 
         if impl == "auto":
             impl = "fused" if (self.device.type == "cuda" and fused_supported(self.F, self.H, self.B)) else (
@@ -116,7 +179,10 @@ class TinyMLPTrainer:
         self.exchange_timeout_s = float(exchange_timeout_s if exchange_timeout_s is not None
                                         else os.environ.get("DGT_EXCHANGE_TIMEOUT_S", 60.0))
         self.faults = FaultInjector.from_env(self.rank)
+        self.metrics = MetricsSink.from_env(self.rank)
 
+        # ZeRO-1 exchange inside the fused kernel (one rank: nothing to shard, the plain kernel)
+        self.zero1 = self.zero_stage == 1 and self.world_size > 1
         self._auto_fallback = False
         if self.impl == "fused" and self.world_size > 1:
             self.channel = self._open_channel() if use_ipc else None
@@ -145,6 +211,10 @@ class TinyMLPTrainer:
             if agreed > 0 and self.impl != "stepwise":
                 self.close_graph_resources()
                 self.impl = "stepwise"
+        if self.impl != "fused":
+            # the RCCL / PyTorch paths run ZeRO-1 with ZeRO-0 math (replicated moments: 1409 params
+            # make the shard's memory saving moot); checkpoints are still written as ZeRO-1 shards
+            self.zero1 = False
 
     # ------------------------------------------------------------------ setup helpers
     def _open_channel(self):
@@ -156,10 +226,48 @@ class TinyMLPTrainer:
             ch = IpcChannel(max(need, self.padded), self.device, timeout_s=self.exchange_timeout_s)
         except Exception:
             return None
-        if not ch.selftest() or not self._exchange_selftest(ch):
+        if not ch.selftest():
+            ch.close()
+            return None
+        line = self._pick_line(ch)
+        if line is None or not self._exchange_selftest(ch):
             ch.close()
             return None
         return ch
+
+    def _pick_line(self, ch) -> Optional[int]:
+        """The first line format (``line_candidates``) whose stress test passes on every rank."""
+        for line in line_candidates():
+            ok, detail = self._stress(ch, line, stress_steps())
+            self.xch_report.append({"test": "stress", "line": f"ll{line}", "ok": ok, **detail})
+            if ok:
+                self.line = line
+                return line
+            if self.rank == 0:
+                print(f"[dgt] exchange stress test failed for LL{line} ({detail}); "
+                      f"{'trying the next line format' if line != line_candidates()[-1] else 'using RCCL'}",
+                      file=sys.stderr, flush=True)
+        return None
+
+    def _stress(self, ch, line: int, n_steps: int, timeout_s: float = 10.0):
+        """``n_steps`` exchanges of the fused kernel's own mailbox layout and line format with
+        payloads that expose any torn line (``tiny_xch_stress``); every rank agrees on the verdict."""
+        ops = _ext.require()
+        status = torch.zeros(1, dtype=torch.int32, device=self.device)
+        errors = torch.zeros(1, dtype=torch.int32, device=self.device)
+        err, st = 0, 0
+        try:
+            ops.tiny_xch_stress(self.F, self.H, ch.data_ptrs, self.rank, self.world_size, ch.stride,
+                                ch.next_seq(n_steps), int(timeout_s * 100_000_000), line, n_steps, status, errors)
+            torch.cuda.synchronize(self.device)
+            err, st = int(errors.item()), int(status.item())
+        except Exception as e:
+            print(f"[dgt] exchange stress test raised: {e}", file=sys.stderr, flush=True)
+            st = -1
+        bad_words = comm.all_reduce_max(float(err))
+        worst = comm.all_reduce_max(float(st != 0))
+        ok = bad_words == 0 and worst == 0
+        return ok, {"steps": n_steps, "max_bad_words": int(bad_words), "timeout_or_error": bool(worst)}
 
     def _exchange_selftest(self, ch, n_steps: int = 8, timeout_s: float = 10.0) -> bool:
         """Drive the training kernel's OWN in-kernel exchange (not the stand-alone one-shot
@@ -181,7 +289,7 @@ class TinyMLPTrainer:
             ops.tiny_mlp_train(self.x, self.y, plan, counts, p, m, v, loss, status, self.F, self.H, self.lr,
                                self.betas[0], self.betas[1], self.eps, self.weight_decay, self.adamw, 0,
                                ch.data_ptrs, self.rank, self.world_size, ch.stride, ch.next_seq(n),
-                               int(timeout_s * 100_000_000), -1)
+                               int(timeout_s * 100_000_000), -1, None, int(self.zero1), self.line)
             torch.cuda.synchronize(self.device)
             ok = int(status.item()) == 0
         except Exception as e:
@@ -199,7 +307,9 @@ class TinyMLPTrainer:
         ref = p.clone()
         comm.broadcast_(ref, 0)
         ok = ok and bool(torch.equal(p, ref))
-        return comm.all_reduce_max(0.0 if ok else 1.0) == 0.0
+        agreed = comm.all_reduce_max(0.0 if ok else 1.0) == 0.0
+        self.xch_report.append({"test": "train_steps", "line": f"ll{self.line}", "ok": agreed, "steps": n})
+        return agreed
 
     def _setup_graph(self) -> None:
         if comm.collectives_on(self.world_size):
@@ -239,7 +349,7 @@ class TinyMLPTrainer:
         if self.world_size == 1:
             return "none"
         if self.impl == "fused":
-            return f"ipc-{xch_mode(self.world_size)}-xgmi"
+            return f"ipc-{'zero1' if self.zero1 else 'oneshot'}-xgmi/ll{self.line}"
         if self.impl == "graph":
             return "rccl-native-in-hipgraph"
         return f"{comm.backend_name()}-allreduce"
@@ -282,7 +392,8 @@ class TinyMLPTrainer:
                                self.eps, self.weight_decay, self.adamw, self.global_steps,
                                ch.data_ptrs if ch else [], self.rank,
                                self.world_size, ch.stride if ch else 0, seq,
-                               ch.timeout_ticks if ch else 0, self.faults.corrupt_step(), self._ws)
+                               ch.timeout_ticks if ch else 0, self.faults.corrupt_step(), self._ws,
+                               int(self.zero1), self.line)
             self.global_steps += n
         elif self.impl == "graph":
             self.step_dev.fill_(self.global_steps)
@@ -316,6 +427,7 @@ class TinyMLPTrainer:
                 self.loss_acc += loss
                 comm.all_reduce_(self.grad)
                 self.global_steps += 1
+                self._maybe_corrupt_torch()
                 adam_flat_reference_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, self.global_steps,
                                      self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay,
                                      self.adamw, grad_scale=1.0 / self.world_size)
@@ -343,7 +455,7 @@ class TinyMLPTrainer:
                 self.x, self.y, self.params, self.exp_avg, self.exp_avg_sq, self.loss_acc, self.status, self.F,
                 self.H, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.adamw,
                 ch.data_ptrs if ch else [], self.rank, self.world_size, ch.stride if ch else 0,
-                ch.timeout_ticks if ch else 0, self.faults.corrupt_step()))
+                ch.timeout_ticks if ch else 0, self.faults.corrupt_step(), int(self.zero1), self.line))
             self._lh_stream = _raw_stream(self.device.index)  # the launcher was bound to it
             self._clib = _ext.c_lib()
         return True
@@ -388,17 +500,108 @@ class TinyMLPTrainer:
             raise ReplicaDivergence(f"data-parallel replicas diverged by optimizer step {self.global_steps} "
                                     f"(impl={self.impl}, exchange={self.exchange})")
 
+    def _torch_corrupt_spec(self):
+        spec = self.faults.spec
+        ok = (spec is not None and spec.mode == "corrupt" and spec.step is not None and spec.rank is not None
+              and not self._corrupt_off)
+        return spec if ok else None
+
+    def _maybe_corrupt_torch(self) -> None:
+        """The ``corrupt`` fault on the plain-PyTorch path (CPU rehearsal of the fused kernel's):
+        rank RANK + 1 receives a gradient sum off by 1.0 in one element at step STEP, once."""
+        spec = self._torch_corrupt_spec()
+        if (spec is not None and self.world_size > 1 and self.global_steps == spec.step
+                and self.rank == (spec.rank + 1) % self.world_size):
+            self.grad[0] += 1.0
+
+    def _snapshot(self):
+        return ([t.clone() for t in (self.params, self.exp_avg, self.exp_avg_sq)],
+                (self.global_steps, self.global_samples))
+
+    def _restore(self, snap) -> None:
+        (p, m, v), (steps, samples) = snap
+        for dst, src in zip((self.params, self.exp_avg, self.exp_avg_sq), (p, m, v)):
+            dst.copy_(src)
+        self.global_steps, self.global_samples = steps, samples
+        self.status.zero_()
+
+    def _can_fall_back(self) -> bool:
+        # the same answer on every rank (it decides whether the ranks re-run an epoch together)
+        return self.world_size > 1 and not self.strict_exchange and (
+            self.impl == "fused" or (self.impl == "torch" and self._torch_corrupt_spec() is not None))
+
+    def _epoch_failure(self) -> Optional[str]:
+        """Why this epoch's result cannot be trusted on SOME rank (agreed by every rank), or None."""
+        local = None
+        try:
+            self.check()
+        except RuntimeError as e:
+            local = str(e)
+        if self.world_size > 1 and comm.all_reduce_max(1.0 if local else 0.0) > 0:
+            return local or "a peer's fused kernel reported an exchange failure"
+        if local:
+            return local
+        try:
+            self.verify_replicas()
+        except ReplicaDivergence as e:
+            return str(e)
+        return None
+
     def run_epoch(self, epoch: int) -> float:
         plan, counts = self.epoch_plan(epoch)
+        snap = self._snapshot() if self._can_fall_back() else None
         self.loss_acc.zero_()
         with tracing.range(f"dgt.{self.impl}.epoch{epoch}"):  # the fused path: ONE kernel launch
             self.run_plan(plan, counts)
         with tracing.range("dgt.epoch_sync"):
             loss_sum = float(self.loss_acc.item())  # the epoch's single host sync
-            self.check()
         with tracing.range("dgt.replica_check"):
-            self.verify_replicas()  # one 5.6 KB broadcast per epoch: silent corruption fails the job
+            # one 5.6 KB broadcast per epoch: silent corruption is caught here
+            why = self._epoch_failure() if self.world_size > 1 else None
+            if why is None and self.world_size == 1:
+                self.check()
+        if why is not None:
+            if snap is None:  # strict (or nothing to fall back to): the job fails loudly
+                if "diverged" in why:
+                    raise ReplicaDivergence(why)
+                raise ExchangeFailure(why)
+            return self._fall_back_and_rerun(epoch, snap, why)
         return loss_sum / max(1, int(plan.shape[0]))
+
+    def _fall_back_and_rerun(self, epoch: int, snap, why: str) -> float:
+        """Every rank restores the epoch-start snapshot, leaves the in-kernel exchange for the RCCL
+        path (HIP-graph-captured native RCCL if every rank can set it up, else ProcessGroupNCCL /
+        gloo step by step) and re-runs the epoch there; the job then continues on that path."""
+        was = f"{self.impl}/{self.exchange}"
+        self._restore(snap)
+        if self.zero1:  # leaving the sharded kernel: every rank needs every element's moments
+            self._gather_zero1_moments()
+            self.zero1 = False
+        if self.impl == "fused":
+            self._drop_launcher()
+            if self.channel is not None:
+                self.channel.close()
+                self.channel = None
+            self.impl = "graph" if comm.backend_name() == "nccl" else "stepwise"
+            if self.impl == "graph":
+                try:
+                    self._setup_graph()
+                    ok = 0.0
+                except Exception as e:
+                    print(f"[dgt] graph path unavailable ({e})", file=sys.stderr, flush=True)
+                    ok = 1.0
+                if comm.all_reduce_max(ok) > 0:  # every rank takes the same path
+                    self.close_graph_resources()
+                    self.impl = "stepwise"
+        self._corrupt_off = True
+        rec = {"event": "exchange_fallback", "epoch": epoch, "from": was, "to": f"{self.impl}/{self.exchange}",
+               "reason": why, "rank": self.rank, "world_size": self.world_size, "global_steps": self.global_steps}
+        self.fallbacks.append(rec)
+        print(f"[dgt] WARNING: exchange_fallback at epoch {epoch}: {why}; restored the epoch-start state and "
+              f"re-running the epoch on {rec['to']}", file=sys.stderr, flush=True)
+        self.metrics.log(rec)
+        health_event(rec)
+        return self.run_epoch(epoch)
 
     # ------------------------------------------------------------------ state
     def sync_model(self) -> SimpleNet:
@@ -415,26 +618,79 @@ class TinyMLPTrainer:
         return flat_to_adam_state(self.exp_avg, self.exp_avg_sq, self.segments, self.global_steps, self.lr,
                                   self.betas, self.eps, self.weight_decay, self.adamw)
 
+    # ---- ZeRO-1: each rank's optimizer state is current only on the elements it owns
+    @property
+    def _sharded_ckpt(self) -> bool:
+        return self.zero_stage == 1  # DeepSpeed writes zero_pp_rank shards at any world size
+
+    def _owned_index(self) -> torch.Tensor:
+        own = zero1_owner_map(self.F, self.H, self.world_size)
+        return torch.nonzero(own == self.rank).reshape(-1)
+
+    def _gather_zero1_moments(self) -> None:
+        """Replicate the moments from their owners (each rank contributes its owned elements): the
+        state a replicated (ZeRO-0-math) path needs after the sharded fused kernel."""
+        own = zero1_owner_map(self.F, self.H, self.world_size)
+        mask = torch.zeros(self.padded, dtype=torch.float32)
+        mask[: self.numel] = (own == self.rank).float()
+        mask = mask.to(self.device)
+        for t in (self.exp_avg, self.exp_avg_sq):
+            t.mul_(mask)
+            comm.all_reduce_(t)
+
+    def _zero_shard(self) -> Dict[str, Any]:
+        idx = self._owned_index()
+        idx_d = idx.to(self.device)
+        return {
+            "zero_stage": 1,
+            "partition_rank": self.rank,
+            "partition_world_size": self.world_size,
+            "index": idx,  # owned flat elements (the fused kernel's lane ownership, zero1_owner_map)
+            "total": self.numel,
+            "names": [n for n, _, _ in simple_net_layout(self.F, self.H)],
+            "offsets": [o for _, _, o in simple_net_layout(self.F, self.H)],
+            "shapes": [list(shp) for _, shp, _ in simple_net_layout(self.F, self.H)],
+            "fp32_flat": self.params[idx_d].detach().cpu().clone(),
+            "exp_avg": self.exp_avg[idx_d].detach().cpu().clone(),
+            "exp_avg_sq": self.exp_avg_sq[idx_d].detach().cpu().clone(),
+            "step": self.global_steps,
+            "param_groups": [{"lr": self.lr, "betas": list(self.betas), "eps": self.eps,
+                              "weight_decay": self.weight_decay, "adamw": self.adamw}],
+        }
+
     def save_checkpoint(self, save_dir: str, tag: Optional[str] = None, client_state: Optional[dict] = None) -> str:
         self.sync_model()
+        shard = self._zero_shard() if self._sharded_ckpt else None
         return ckpt.save(save_dir, tag, self.global_steps,
                          {k: v.detach().cpu().clone() for k, v in self.model.state_dict().items()},
-                         self.optimizer_state_dict(),
+                         None if shard is not None else self.optimizer_state_dict(),
                          {"global_samples": self.global_samples, "dp_world_size": self.world_size,
                           "client_state": client_state or {}},
-                         self.ds_config)
+                         self.ds_config, zero_shard=shard)
 
     def load_checkpoint(self, load_dir: str, tag: Optional[str] = None, load_optimizer_states: bool = True):
-        path, states, _ = ckpt.load(load_dir, tag)
+        path, states, shard = ckpt.load(load_dir, tag)
         if states is None:
             return None, None
         self.model.load_state_dict(states["module"])
         self.params[: self.numel].copy_(pack_simple_net(self.model).to(self.device))
-        if load_optimizer_states and states.get("optimizer"):
+        self.global_steps = int(states.get("global_steps", 0))
+        if load_optimizer_states and self._sharded_ckpt:
+            if shard is None or "index" not in shard:
+                raise FileNotFoundError(f"missing fused-kernel ZeRO-1 shard for rank {self.rank} under {path}")
+            if int(shard["partition_world_size"]) != self.world_size or int(shard["total"]) != self.numel:
+                raise RuntimeError("ZeRO-1 checkpoint was written with a different world size / model; "
+                                   "consolidate it with zero_to_fp32.py and load the fp32 weights instead")
+            idx = shard["index"].to(self.device)
+            self.exp_avg.zero_()
+            self.exp_avg_sq.zero_()
+            self.exp_avg[idx] = shard["exp_avg"].to(self.device)
+            self.exp_avg_sq[idx] = shard["exp_avg_sq"].to(self.device)
+            if not (self.zero1 and self.impl == "fused"):
+                self._gather_zero1_moments()  # a replicated path needs every element's moments
+        elif load_optimizer_states and states.get("optimizer"):
             step = adam_state_to_flat(states["optimizer"], self.exp_avg, self.exp_avg_sq, self.segments)
             self.global_steps = int(states.get("global_steps", step))
-        else:
-            self.global_steps = int(states.get("global_steps", 0))
         self.global_samples = int(states.get("global_samples", 0))
         return path, states.get("client_state", {})
 

@@ -6,6 +6,8 @@ DeepSpeed's ``ThroughputTimer`` derives samples/sec from ``train_batch_size`` (w
 hard-codes to 64 while the real global batch is 4 x world_size), so it over-reports.
 ``ThroughputTimer`` here counts the samples actually processed.  ``MetricsSink`` writes one JSON
 object per optimizer step when ``DGT_METRICS_JSONL`` names a file (``{rank}`` is substituted).
+``health_event`` appends run-time health events (e.g. an exchange fallback) to ``DGT_HEALTH_LOG``,
+the job's health log next to the pre-flight report (``slurm_train.sbatch``).
 """
 from __future__ import annotations
 
@@ -76,3 +78,18 @@ class MetricsSink:
         if self._fh is not None:
             self._fh.close()
             self._fh = None
+
+
+def health_event(record: Dict[str, Any]) -> None:
+    """Append one JSON line to ``DGT_HEALTH_LOG`` (``{rank}`` substituted; a shared file is
+    appended to by every rank: one short line per event, written with a single write call)."""
+    p = os.environ.get("DGT_HEALTH_LOG")
+    if not p:
+        return
+    p = p.replace("{rank}", str(record.get("rank", 0)))
+    d = os.path.dirname(p)
+    if d:
+        os.makedirs(d, exist_ok=True)
+    line = json.dumps({"ts": time.time(), **{k: v for k, v in record.items() if v is not None}}) + "\n"
+    with open(p, "a") as fh:
+        fh.write(line)

@@ -6,8 +6,10 @@ Reference: the script DeepSpeed copies next to checkpoints written at ``train.py
     python zero_to_fp32.py <checkpoint_dir> <output.pt> [--tag global_stepN]
 
 <checkpoint_dir> is the directory holding ``latest`` (e.g. ds_checkpoints/epoch5).  Each rank's
-``zero_pp_rank_{r}_mp_rank_00_optim_states.pt`` holds its contiguous fp32 master shard: for every
-gradient bucket (start, numel) rank r owns elements [start + r*numel/W, start + (r+1)*numel/W).
+``zero_pp_rank_{r}_mp_rank_00_optim_states.pt`` holds its fp32 master shard, either contiguous per
+gradient bucket (the engine: for every bucket (start, numel) rank r owns elements
+[start + r*numel/W, start + (r+1)*numel/W)) or as an explicit ``index`` of owned flat elements (the
+fused kernel's lane ownership, ``runtime/tiny_trainer.py`` ``zero1_owner_map``).
 Stage-0 checkpoints (no shards) are converted from the module weights.  Loads use
 ``torch.load(weights_only=True)`` only.
 """
@@ -37,12 +39,20 @@ def consolidate(ckpt_dir, tag=None):
         raise RuntimeError(f"expected {ws} shards, found ranks {sorted(shards)}")
     meta = shards[0]
     full = torch.zeros(meta["total"], dtype=torch.float32)
-    cursor = [0] * ws
-    for start, numel in meta["buckets"]:
-        n = numel // ws
+    if "index" in meta:  # element-wise ownership: every element exactly once over the ranks
+        seen = torch.zeros(meta["total"], dtype=torch.int64)
         for r in range(ws):
-            full[start + r * n:start + (r + 1) * n] = shards[r]["fp32_flat"][cursor[r]:cursor[r] + n]
-            cursor[r] += n
+            full[shards[r]["index"]] = shards[r]["fp32_flat"].float()
+            seen[shards[r]["index"]] += 1
+        if not bool((seen == 1).all()):
+            raise RuntimeError("index shards do not cover every element exactly once")
+    else:
+        cursor = [0] * ws
+        for start, numel in meta["buckets"]:
+            n = numel // ws
+            for r in range(ws):
+                full[start + r * n:start + (r + 1) * n] = shards[r]["fp32_flat"][cursor[r]:cursor[r] + n]
+                cursor[r] += n
     out = {}
     for name, off, shape in zip(meta["names"], meta["offsets"], meta["shapes"]):
         numel = 1

@@ -1,4 +1,5 @@
 #!/bin/bash
+export DGT_ALLOW_OVERSUBSCRIBE=1  # ranks share the one card of the rehearsal box
 # A/B of the 2- and 8-rank exchange rehearsal between this tree and _ab/ (interleaved).
 set -o pipefail
 export TMPDIR=/tmp DGT_BACKEND=gloo OMP_NUM_THREADS=1 DGT_EXCHANGE_TIMEOUT_S=20

@@ -1,4 +1,5 @@
 #!/bin/bash
+export DGT_ALLOW_OVERSUBSCRIBE=1  # ranks share the one card of the rehearsal box
 # The driver's bench shape (--steps 20 --warmup 5) with 2 and 8 ranks sharing one GPU, closing the
 # timed region with the IPC device barrier (default) vs the process-group barrier
 # (DGT_BENCH_PG_BARRIER=1), REPS interleaved fresh-process runs each.

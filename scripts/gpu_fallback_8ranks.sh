@@ -1,4 +1,5 @@
 #!/bin/bash
+export DGT_ALLOW_OVERSUBSCRIBE=1  # ranks share the one card of the rehearsal box
 # bench.py at 8 ranks on one GPU (gloo) with a corrupted exchange at step 100 on rank 1: every rank
 # sees the replica divergence, the timed region re-runs on the RCCL path, one JSON line with
 # ipc_fallback_reason set.

@@ -1,4 +1,5 @@
 #!/bin/bash
+export DGT_ALLOW_OVERSUBSCRIBE=1  # ranks share the one card of the rehearsal box
 # DGT_BENCH_WARM_LAST=0/1 at the driver's shape with RANKS ranks sharing one GPU (gloo control plane,
 # IPC device barriers), interleaved fresh launches, REPS each.
 set -o pipefail

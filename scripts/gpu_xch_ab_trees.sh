@@ -1,4 +1,5 @@
 #!/bin/bash
+export DGT_ALLOW_OVERSUBSCRIBE=1  # ranks share the one card of the rehearsal box
 # Interleaved A/B of the multi-rank exchange rehearsal (ranks sharing one GPU, gloo control plane)
 # over tree copies given as arguments (e.g. _v1 .): RANKS (2 4 8), REPS (2), STEPS (30000).
 set -o pipefail

@@ -1,4 +1,5 @@
 #!/bin/bash
+export DGT_ALLOW_OVERSUBSCRIBE=1  # ranks share the one card of the rehearsal box
 # Exchange rehearsal benches on one GPU (gloo control plane): 2, 4 and 8 ranks through the fused
 # kernel; at 4 and 8 ranks both protocols (DGT_XCH=oneshot / twoshot), REPS times interleaved.
 set -o pipefail

@@ -96,3 +96,23 @@ def test_wait_mode_validation():
     assert set_wait_mode("") is False
     with pytest.raises(ValueError):
         set_wait_mode("busy")
+
+
+def test_hip_set_device_refuses_silent_oversubscription(monkeypatch):
+    """a local rank beyond the visible GPUs is an error (a wrong HIP_VISIBLE_DEVICES or
+    GPUS_PER_NODE), unless DGT_ALLOW_OVERSUBSCRIBE=1 asks for the one-card rehearsal's wrap."""
+    import pytest
+    import torch
+    from distributed_gpu_test_amd.accelerator import HipAccelerator
+    bound = []
+    monkeypatch.setattr(torch.cuda, "device_count", lambda: 2)
+    monkeypatch.setattr(torch.cuda, "set_device", lambda i: bound.append(i))
+    monkeypatch.delenv("DGT_HIP_WAIT", raising=False)
+    monkeypatch.delenv("DGT_ALLOW_OVERSUBSCRIBE", raising=False)
+    acc = HipAccelerator()
+    acc.set_device(1)
+    with pytest.raises(RuntimeError, match="no GPU of its own"):
+        acc.set_device(3)
+    monkeypatch.setenv("DGT_ALLOW_OVERSUBSCRIBE", "1")
+    acc.set_device(3)
+    assert bound == [1, 1]

@@ -56,13 +56,28 @@ def test_bench_two_ranks_gloo_cpu():
     assert lines[0]["config"]["closing_barrier"] == "process-group"
 
 
-def test_exchange_mode_selection(monkeypatch):
-    from distributed_gpu_test_amd.runtime.tiny_trainer import xch_mode
-    monkeypatch.delenv("DGT_XCH", raising=False)
-    assert [xch_mode(n) for n in (2, 4, 8)] == ["oneshot"] * 3  # auto: one-shot at every size
-    monkeypatch.setenv("DGT_XCH", "twoshot")
-    assert [xch_mode(n) for n in (2, 4, 8)] == ["oneshot", "twoshot", "twoshot"]  # two-shot: 4+ ranks
-    monkeypatch.setenv("DGT_XCH", "threeshot")
+def test_exchange_line_selection(monkeypatch):
     import pytest
+    from distributed_gpu_test_amd.runtime.tiny_trainer import line_candidates
+    monkeypatch.delenv("DGT_XCH_LINE", raising=False)
+    assert line_candidates() == [3, 2]  # auto: LL3 if its stress test passes, else LL2
+    monkeypatch.setenv("DGT_XCH_LINE", "ll2")
+    assert line_candidates() == [2]
+    monkeypatch.setenv("DGT_XCH_LINE", "ll4")
     with pytest.raises(ValueError):
-        xch_mode(8)
+        line_candidates()
+
+
+def test_zero1_owner_map_partitions_every_element():
+    """The fused kernel's ZeRO-1 lane ownership covers every parameter exactly once, spreads the
+    elements evenly over the ranks and puts b2 on rank 0 (lane 0 writes it back)."""
+    import torch
+    from distributed_gpu_test_amd.models.simple_net import simple_net_numel
+    from distributed_gpu_test_amd.runtime.tiny_trainer import zero1_owner_map
+    for f, h in ((20, 64), (32, 64), (20, 128), (8, 16)):
+        for ws in (1, 2, 3, 4, 8):
+            own = zero1_owner_map(f, h, ws)
+            assert own.numel() == simple_net_numel(f, h) and int(own.min()) == 0 and int(own.max()) == ws - 1
+            counts = torch.bincount(own, minlength=ws)
+            assert int(counts.max() - counts.min()) <= (simple_net_numel(f, h) // ws) // 2 + 16, counts
+            assert int(own[-1]) == 0

@@ -243,3 +243,66 @@ def test_inject_fused_linear_keeps_parameters_and_falls_back_on_cpu():
     torch.testing.assert_close(m(x), ref(x))
     x20 = torch.randn(4, 20)
     torch.testing.assert_close(nested(x20), nested_ref(x20))
+
+
+class _ScaleGradInPlace(torch.autograd.Function):
+    """A user Function whose backward edits grad_output IN PLACE (legal autograd code)."""
+
+    @staticmethod
+    def forward(ctx, x):
+        return x.clone()
+
+    @staticmethod
+    def backward(ctx, g):
+        return g.mul_(3.0)
+
+
+@pytest.mark.parametrize("gas", [1, 2])
+def test_backward_seed_survives_in_place_grad_output(gas):
+    """a loss whose grad_fn edits its incoming gradient in place must not corrupt later
+    steps through a shared backward seed: the engine's trajectory equals plain torch's."""
+    m = _mlp(21)
+    ref = copy.deepcopy(m)
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    crit = torch.nn.BCEWithLogitsLoss()
+    batches = _batches(6, 22)
+    for i, (x, y) in enumerate(batches):
+        (_ScaleGradInPlace.apply(crit(ref(x), y)) / gas).backward()
+        if (i + 1) % gas == 0:
+            opt.step()
+            opt.zero_grad()
+    engine, _, _, _ = dgt.initialize(model=m, optimizer=torch.optim.Adam(m.parameters(), lr=1e-3),
+                                     config={"train_micro_batch_size_per_gpu": 8, "gradient_accumulation_steps": gas})
+    for x, y in batches:
+        engine.backward(_ScaleGradInPlace.apply(crit(engine(x), y)))
+        engine.step()
+    got = torch.nn.utils.parameters_to_vector(engine.module.parameters()).detach()
+    want = torch.nn.utils.parameters_to_vector(ref.parameters()).detach()
+    torch.testing.assert_close(got, want, rtol=1e-5, atol=1e-6)
+    engine.close()
+
+
+def test_allgather_bucket_size_groups_buckets():
+    """ZeRO's all-gather is grouped by allgather_bucket_size (one coalesced RCCL
+    launch per group on GPUs): a small size splits the reduce buckets into several groups, the
+    default (8M elements = 32 MiB fp32) keeps them in one; numerics are unchanged."""
+    torch.manual_seed(23)
+    m = torch.nn.Sequential(torch.nn.Linear(12, 256), torch.nn.ReLU(), torch.nn.Linear(256, 64), torch.nn.Tanh(),
+                            torch.nn.Linear(64, 1))
+    base = {"train_batch_size": 8}
+    cap = 5000
+    e_small, p_small = _engine_run(copy.deepcopy(m), _batches(4, 24), dict(base, zero_optimization={
+        "stage": 1, "reduce_bucket_size": 1024, "allgather_bucket_size": cap}))
+    e_def, p_def = _engine_run(copy.deepcopy(m), _batches(4, 24), dict(base, zero_optimization={
+        "stage": 1, "reduce_bucket_size": 1024}))
+    assert e_small.config.zero.allgather_bucket_size == cap
+    assert e_def.config.zero.allgather_bucket_size == 8 * 1024 * 1024
+    g_small, g_def = e_small._allgather_group_plan(), e_def._allgather_group_plan()
+    nb = len(e_small.layout.buckets)
+    assert nb > 2 and len(g_def) == 1 and 1 < len(g_small) <= nb
+    assert sorted(i for g in g_small for i in g) == list(range(nb))
+    for g in g_small:  # every group fits the cap unless it is a single oversized bucket
+        assert len(g) == 1 or sum(e_small.layout.buckets[i].numel for i in g) <= cap
+    torch.testing.assert_close(p_small, p_def, rtol=0, atol=0)
+    e_small.close()
+    e_def.close()

@@ -207,9 +207,11 @@ def test_fused_linear_grad_in_place_accumulates_and_fires_hooks():
     for i, p in enumerate(m.parameters()):
         p.grad = torch.zeros_like(p)
         p.register_post_accumulate_grad_hook(lambda _p, i=i: fired.append(i))
+    from distributed_gpu_test_amd.ops.linear import engine_backward
     x = torch.randn(4, 20, device="cuda")
     for _ in range(2):
-        m(x).square().sum().backward()
+        with engine_backward():  # in place only inside the engine's backward
+            m(x).square().sum().backward()
         ref(x).square().sum().backward()
     assert sorted(fired) == [0, 0, 1, 1, 2, 2, 3, 3]
     for p, q in zip(m.parameters(), ref.parameters()):
@@ -248,13 +250,15 @@ def test_fused_chain_is_bitwise_per_layer(in_place):
             if in_place:
                 p.grad = torch.zeros_like(p)
                 p.register_post_accumulate_grad_hook(lambda _p, i=i, net=net: fired.append((id(net), i)))
+    from distributed_gpu_test_amd.ops.linear import engine_backward
     x0 = torch.randn(4, 20, device="cuda")
     outs, dxs = [], []
     for net in (chain, layered):
         x = x0.clone().requires_grad_(True)
         for _ in range(2):
             y = net(x) if net is chain else _layer_by_layer(net, x)
-            y.square().sum().backward()
+            with engine_backward():
+                y.square().sum().backward()
         outs.append(y.detach())
         dxs.append(x.grad)
     assert torch.equal(outs[0], outs[1]) and torch.equal(dxs[0], dxs[1])
@@ -268,3 +272,77 @@ def _layer_by_layer(net, x):
     for m in net:
         x = m(x)
     return x
+
+
+@pytest.mark.gpu
+def test_autograd_grad_on_injected_engine_returns_grads():
+    """with the default fused-Linear injection (in-place gradients), a plain
+    torch.autograd.grad on the engine's parameters returns the right tensors and leaves the flat
+    gradient buckets untouched: the kernels accumulate in place only inside engine.backward."""
+    m = _mlp(13)
+    ref = copy.deepcopy(m).cuda()
+    e, _, _, _ = dgt.initialize(model=m, config={"train_batch_size": 32})
+    assert e.fused_linear_layers == 2
+    x, y = _batches(1, 14)[0]
+    crit = torch.nn.BCEWithLogitsLoss()
+    gs = torch.autograd.grad(crit(e(x), y), list(e.module.parameters()))
+    want = torch.autograd.grad(crit(ref(x), y), list(ref.parameters()))
+    assert all(g is not None for g in gs)
+    for g, w in zip(gs, want):
+        torch.testing.assert_close(g, w, rtol=1e-5, atol=1e-6)
+    assert float(e.store.grad_buf.abs().max()) == 0.0
+    e.backward(crit(e(x), y))  # the engine's own backward still accumulates in place
+    assert float(e.store.grad_buf.abs().max()) > 0.0
+    e.close()
+
+
+@pytest.mark.gpu
+def test_fused_chain_frozen_layer_stays_frozen():
+    """a layer frozen after injection gets no gradient from the chain's backward, so the
+    flat Adam leaves it unchanged; the trainable layers still learn."""
+    torch.manual_seed(31)
+    m = torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.ReLU(), torch.nn.Linear(128, 64), torch.nn.ReLU(),
+                            torch.nn.Linear(64, 1))
+    e, _, _, _ = dgt.initialize(model=m, config={"train_batch_size": 32})
+    assert e.fused_linear_layers == 3
+    frozen = e.module[2].weight
+    frozen.requires_grad_(False)
+    before = frozen.detach().clone()
+    head = e.module[4].weight.detach().clone()
+    crit = torch.nn.BCEWithLogitsLoss()
+    for x, y in _batches(3, 15):
+        e.backward(crit(e(x), y))
+        e.step()
+    assert torch.equal(frozen.detach(), before)
+    assert not torch.equal(e.module[4].weight.detach(), head)
+    e.close()
+
+
+@pytest.mark.gpu
+def test_graph_module_keeps_buffers_and_rng_and_guards_double_forward():
+    """graph_module's capture warmup leaves BatchNorm running stats as they were, and a second forward of one signature before the first one's backward runs eagerly
+    (the pending backward keeps its activations): the trajectory equals the eager engine's."""
+    def net(seed):
+        torch.manual_seed(seed)
+        return torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.BatchNorm1d(128), torch.nn.ReLU(),
+                                   torch.nn.Linear(128, 1))
+    crit = torch.nn.BCEWithLogitsLoss()
+    res = []
+    for amd in ({"graph_module": False}, {"graph_module": True}):
+        e, _, _, _ = dgt.initialize(model=net(17), config={"train_batch_size": 32, "amd": amd})
+        torch.manual_seed(5)
+        losses = []
+        for x, y in _batches(6, 18):
+            out1 = e(x)
+            out2 = e(x * 0.5)  # same signature, before out1's backward
+            loss = crit(out1, y) + crit(out2, y)
+            e.backward(loss)
+            e.step()
+            losses.append(float(loss))
+        res.append((losses, e.store.param_buf.detach().clone(), [b.detach().clone() for b in e.module.buffers()]))
+        e.close()
+    (l1, p1, b1), (l2, p2, b2) = res
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
+    for u, v in zip(b1, b2):
+        torch.testing.assert_close(u.float(), v.float(), rtol=1e-5, atol=1e-6)

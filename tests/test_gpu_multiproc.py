@@ -1,6 +1,7 @@
-"""GPU multi-rank rehearsal on ONE MI355X: 2 ranks share the card over gloo, exercising the IPC
-mailboxes (hipIpcGetMemHandle / hipIpcOpenMemHandle across processes) and the in-kernel one- and
-two-shot gradient exchanges of the fused trainer.  The 8-GPU xGMI run happens only in the driver's scaling
+"""GPU multi-rank rehearsal on ONE MI355X: 2-8 ranks share the card over gloo, exercising the IPC
+mailboxes (hipIpcGetMemHandle / hipIpcOpenMemHandle across processes), the in-kernel one-shot and
+ZeRO-1 exchanges of the fused trainer in both line formats (LL3 / LL2), the start-up stress test
+and the run-time fallback to the RCCL path.  The 8-GPU xGMI run happens only in the driver's scaling
 bench; these tests pin the protocol (LL tags, parities, rank-order sums) on real hardware."""
 import os
 import re
@@ -19,7 +20,8 @@ pytestmark = pytest.mark.gpu
 
 def run(nproc, script, *args, env=None, timeout=300):
     e = dict(os.environ)
-    e.update({"DGT_QUIET": "1", "DGT_BACKEND": "gloo", "OMP_NUM_THREADS": "1", "DGT_EXCHANGE_TIMEOUT_S": "20"})
+    e.update({"DGT_QUIET": "1", "DGT_BACKEND": "gloo", "OMP_NUM_THREADS": "1", "DGT_EXCHANGE_TIMEOUT_S": "20",
+              "DGT_ALLOW_OVERSUBSCRIBE": "1"})
     e.update(env or {})
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={nproc}",
            "--master-addr=127.0.0.1", f"--master-port={free_port()}", os.path.join(ROOT, script), *args]
@@ -80,7 +82,7 @@ def test_bench_two_ranks_one_gpu():
     # two processes on one card: n_gpus counts physical devices, ranks counts processes
     assert out["n_gpus"] == 1 and out["ranks"] == 2 and out["oversubscribed"] is True
     assert out["params_consistent_across_ranks"] is True
-    assert out["config"]["exchange"] == "ipc-oneshot-xgmi"
+    assert out["config"]["exchange"].startswith("ipc-oneshot-xgmi")
     assert out["config"]["closing_barrier"] == "ipc-device"
     print(line)
 
@@ -97,14 +99,51 @@ def test_bench_driver_shape_two_ranks_device_barrier():
         assert out["steps"] == 20 and out["warmup"] == 5
 
 
-def test_corrupted_exchange_fails_train_py(tmp_path):
+@pytest.mark.parametrize("ws", [2, 8])
+def test_corrupted_exchange_falls_back_train_py(tmp_path, ws):
     """--fail-at 0:37:corrupt makes rank 0's fused kernel send rank 1 one wrong gradient payload at
-    step 37: training itself runs through, and the end-of-epoch replica check must fail the job."""
-    r = run(2, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", "--fail-at", "0:37:corrupt")
+    step 37.  The end-of-epoch replica check sees the divergence on every rank; the job restores
+    the epoch-start snapshot, re-runs the epoch on the RCCL path, prints the oracle to 4 dp, exits
+    0 and logs exchange_fallback to stderr, the metrics JSONL and the health log."""
+    import json
+    metrics, health = tmp_path / "m_{rank}.jsonl", tmp_path / "health.jsonl"
+    r = run(ws, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", "--fail-at", "0:37:corrupt",
+            env={"DGT_METRICS_JSONL": str(metrics), "DGT_HEALTH_LOG": str(health)}, timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "exchange=ipc-oneshot-xgmi" in r.stderr
+    assert "exchange_fallback at epoch 1" in r.stderr and "replicas diverged" in r.stderr, r.stderr[-3000:]
+    want = ORACLE2 if ws == 2 else ORACLE[ws]
+    assert losses(r.stdout) == want[:2]
+    assert "Training completed." in r.stdout
+    events = [json.loads(l) for l in health.read_text().splitlines()]
+    assert len(events) == ws and all(e["event"] == "exchange_fallback" and e["epoch"] == 1 for e in events)
+    assert all(e["to"].startswith(("graph", "stepwise")) for e in events), events
+    m0 = [json.loads(l) for l in (tmp_path / "m_0.jsonl").read_text().splitlines()]
+    assert any(e.get("event") == "exchange_fallback" for e in m0)
+
+
+def test_corrupted_exchange_strict_fails_train_py():
+    """--strict-exchange keeps the old contract: the divergence fails the job (rc 2) on every rank."""
+    r = run(2, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", "--fail-at", "0:37:corrupt",
+            "--strict-exchange")
     assert r.returncode != 0, r.stdout[-2000:]
     assert "replicas diverged" in r.stderr, r.stderr[-3000:]
-    assert "exchange=ipc-oneshot-xgmi" in r.stderr
+    assert "exchange_fallback" not in r.stderr
     assert "Training completed." not in r.stdout
+
+
+def test_stress_selftest_reported_and_ll2_selectable(tmp_path):
+    """Start-up: the exchange stress test (>= 1000 exchanges, torn-line-revealing payloads) runs
+    and passes; DGT_XCH_LINE=ll2 selects the 8-byte-pair line format, which trains to the same
+    oracle."""
+    for line in ("auto", "ll2"):
+        r = run(2, "train.py", "--impl", "fused", "--epochs", "1", "--no-save",
+                env={"DGT_XCH_LINE": line, "DGT_XCH_STRESS_STEPS": "5000"})
+        assert r.returncode == 0, r.stderr[-4000:]
+        want = "ll2" if line == "ll2" else "ll3"
+        assert f"exchange=ipc-oneshot-xgmi/{want}" in r.stderr, r.stderr[-2000:]
+        assert '"test": "stress"' in r.stderr and '"steps": 5000' in r.stderr and '"max_bad_words": 0' in r.stderr
+        assert losses(r.stdout) == ORACLE2[:1]
 
 
 def test_corrupted_exchange_falls_back_in_bench():
@@ -155,35 +194,48 @@ def test_bench_mlp_zero1_two_ranks_one_gpu():
     assert "reducescatter+allgather" in out["config"]["exchange"]
 
 
-@pytest.mark.parametrize("mode", ["twoshot", "oneshot"])
+@pytest.mark.parametrize("zero", [0, 1])
 @pytest.mark.parametrize("ws", [4, 8])
-def test_fused_ipc_exchange_many_ranks_one_gpu(tmp_path, ws, mode):
-    """The 4- and 8-rank exchanges (every mailbox slot) on one card, both protocols: the code path
-    the 8 x MI355X scaling run takes (one-shot by default), checked against the survey's oracle.
-    Both sum in rank order, so both print the same oracle digits."""
-    r = run(ws, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", timeout=600, env={"DGT_XCH": mode})
+def test_fused_ipc_exchange_many_ranks_one_gpu(tmp_path, ws, zero):
+    """The 4- and 8-rank exchanges (every mailbox slot) on one card, ZeRO-0 (one-shot) and ZeRO-1
+    (reduce-scatter to owners, owner Adam, parameter all-gather): the code paths the 8 x MI355X
+    scaling run takes, checked against the survey's oracle.  Both sum in rank order, so both print
+    the same oracle digits."""
+    cfg = os.path.join(ROOT, "configs", "ds_zero1.json" if zero else "ds_zero0.json")
+    r = run(ws, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", "--deepspeed_config", cfg, timeout=600)
     assert r.returncode == 0, r.stderr[-4000:]
-    assert f"exchange=ipc-{mode}-xgmi" in r.stderr, r.stderr[-2000:]
+    assert f"exchange=ipc-{'zero1' if zero else 'oneshot'}-xgmi" in r.stderr, r.stderr[-2000:]
     assert losses(r.stdout) == ORACLE[ws][:2]
 
 
-def test_twoshot_matches_oneshot_bitwise_four_ranks(tmp_path):
-    """The two-shot's owners sum every rank in rank order, as the one-shot does: parameters after
-    an epoch are bit-identical between the protocols."""
+def test_zero1_matches_zero0_bitwise_and_consolidates(tmp_path):
+    """Fused ZeRO-1 at 4 ranks: parameters after an epoch are bit-identical to the one-shot
+    ZeRO-0 run (owners sum every rank in rank order and apply the same Adam); each rank writes a
+    zero_pp_rank shard of the elements it owns, zero_to_fp32 consolidates them to the module's
+    weights, and the run resumes from the shards (epoch 2 prints the uninterrupted oracle)."""
     import torch
+    from distributed_gpu_test_amd.utils.zero_to_fp32 import consolidate
     out = {}
-    for mode in ("oneshot", "twoshot"):
-        d = tmp_path / mode
-        r = run(4, "train.py", "--impl", "fused", "--epochs", "1", "--save-dir", str(d), env={"DGT_XCH": mode})
+    for zero in (0, 1):
+        d = tmp_path / f"z{zero}"
+        cfg = os.path.join(ROOT, "configs", "ds_zero1.json" if zero else "ds_zero0.json")
+        r = run(4, "train.py", "--impl", "fused", "--epochs", "1", "--save-dir", str(d), "--deepspeed_config", cfg)
         assert r.returncode == 0, r.stderr[-4000:]
-        ck = [p for p in d.rglob("*.pt")]
-        assert ck, list(d.rglob("*"))
-        out[mode] = {p.relative_to(d).as_posix(): torch.load(p, map_location="cpu", weights_only=True) for p in ck}
-    assert out["oneshot"].keys() == out["twoshot"].keys()
-    a, b = _flat_tensors(out["oneshot"]), _flat_tensors(out["twoshot"])
-    assert a.keys() == b.keys() and any("module" in k for k in a), sorted(a)[:8]
-    for k in a:
-        assert torch.equal(a[k], b[k]), k
+        ck = d / "epoch1"
+        out[zero] = torch.load(ck / "global_step125" / "mp_rank_00_model_states.pt", map_location="cpu",
+                               weights_only=True)["module"]
+    for k in out[0]:
+        assert torch.equal(out[0][k], out[1][k]), k
+    ck = tmp_path / "z1" / "epoch1"
+    for rr in range(4):
+        assert (ck / "global_step125" / f"zero_pp_rank_{rr}_mp_rank_00_optim_states.pt").exists()
+    full = consolidate(str(ck))
+    for k, v in out[1].items():
+        assert torch.equal(full[k], v.float()), k
+    r = run(4, "train.py", "--impl", "fused", "--epochs", "2", "--resume", "--save-dir", str(tmp_path / "z1"),
+            "--deepspeed_config", os.path.join(ROOT, "configs", "ds_zero1.json"))
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert losses(r.stdout) == ORACLE[4][1:2]
 
 
 def _flat_tensors(obj, prefix=""):
@@ -198,14 +250,15 @@ def _flat_tensors(obj, prefix=""):
     return out
 
 
-def test_corrupted_twoshot_exchange_fails_train_py():
-    """Two-shot at 4 ranks: rank 0 all-gathers one wrong sum to rank 1 only; the replica check
-    must fail the job."""
-    r = run(4, "train.py", "--impl", "fused", "--epochs", "1", "--no-save", "--fail-at", "0:37:corrupt",
-            env={"DGT_XCH": "twoshot"})
-    assert r.returncode != 0, r.stdout[-2000:]
-    assert "exchange=ipc-twoshot-xgmi" in r.stderr
-    assert "replicas diverged" in r.stderr, r.stderr[-3000:]
+def test_corrupted_zero1_exchange_falls_back():
+    """ZeRO-1 at 4 ranks: rank 0 all-gathers one wrong parameter to rank 1 only; the replica check
+    catches it, the moments are gathered from their owners and the epoch re-runs on RCCL."""
+    r = run(4, "train.py", "--impl", "fused", "--epochs", "2", "--no-save", "--fail-at", "0:37:corrupt",
+            "--deepspeed_config", os.path.join(ROOT, "configs", "ds_zero1.json"))
+    assert r.returncode == 0, r.stderr[-4000:]
+    assert "exchange=ipc-zero1-xgmi" in r.stderr
+    assert "exchange_fallback at epoch 1" in r.stderr, r.stderr[-3000:]
+    assert losses(r.stdout) == ORACLE[4][:2]
 
 
 def test_bench_eight_ranks_one_gpu():
@@ -215,7 +268,7 @@ def test_bench_eight_ranks_one_gpu():
     out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
     assert out["n_gpus"] == 1 and out["ranks"] == 8 and out["oversubscribed"] is True
     assert out["params_consistent_across_ranks"] is True
-    assert out["config"]["exchange"] == "ipc-oneshot-xgmi"
+    assert out["config"]["exchange"].startswith("ipc-oneshot-xgmi")
     print(json.dumps(out))
 
 
@@ -230,7 +283,9 @@ def test_fused_exchange_every_shape(ws):
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][7:])
     assert len(res) == 4, res
     for shape, row in res.items():
-        assert row["exchange"] == "ipc-oneshot-xgmi", (shape, row)
+        assert row["exchange"] == "ipc-oneshot-xgmi/ll3", (shape, row)
         assert row["consistent"], (shape, row)
         assert row["max_abs_diff"] < 1e-5, (shape, row)
+        # LL2 and ZeRO-1 move the same gradients: bit-identical parameters
+        assert row["ll2_equal"] and row["zero1_equal"] and row["zero1_ll2_equal"], (shape, row)
     print(json.dumps(res))

@@ -166,3 +166,28 @@ def test_profile_trace_on_default_trainer_path(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     trace = tmp_path / "prof" / "trace_rank0.json"
     assert trace.exists() and trace.stat().st_size > 1000
+
+
+def test_exchange_fallback_reruns_epoch_cpu(tmp_path):
+    """The run-time fallback's mechanics on the CPU (the torch path emulates the fused kernel's
+    ``corrupt`` fault: rank 1 receives a gradient sum off by 1.0 at step 37).  The epoch-end replica
+    check sees the divergence on both ranks; both restore the epoch-start snapshot, re-run the epoch
+    and the job prints the uninterrupted oracle, exits 0, and logs exchange_fallback to stderr, the
+    metrics JSONL and the health log."""
+    health = tmp_path / "health.jsonl"
+    r = run(2, "--impl", "torch", "--epochs", "2", "--no-save", "--fail-at", "0:37:corrupt",
+            env={"DGT_HEALTH_LOG": str(health), "DGT_METRICS_JSONL": str(tmp_path / "m.jsonl")})
+    assert r.returncode == 0, r.stderr[-3000:]
+    assert epoch_losses(r.stdout) == ORACLE[2][:2]
+    assert "oversubscribed=False" in r.stderr  # CPU ranks are their own devices
+    assert "exchange_fallback at epoch 1" in r.stderr and "replicas diverged" in r.stderr, r.stderr[-2000:]
+    ev = [json.loads(l) for l in health.read_text().splitlines()]
+    assert sorted(e["rank"] for e in ev) == [0, 1] and all(e["event"] == "exchange_fallback" for e in ev)
+    assert any(json.loads(l).get("event") == "exchange_fallback" for l in (tmp_path / "m.jsonl").read_text().splitlines())
+
+
+def test_exchange_fallback_strict_fails_cpu():
+    r = run(2, "--impl", "torch", "--epochs", "1", "--no-save", "--fail-at", "0:37:corrupt", "--strict-exchange")
+    assert r.returncode != 0, r.stderr[-2000:]  # the workers exit 2; torchrun reports the failure
+    assert "[dgt] FATAL" in r.stderr and "replicas diverged" in r.stderr and "exitcode  : 2" in r.stderr
+    assert "Training completed." not in r.stdout

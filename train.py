@@ -14,7 +14,12 @@ Differences by design:
   gradient exchange over xGMI inside the kernel); ``--impl engine`` runs the generic
   DeepSpeed-style engine (PyTorch modules + bucketed RCCL all-reduce + fused Adam);
 * extra flags: ``--deepspeed_config``, ``--impl``, ``--backend``, ``--fail-at``, ``--resume``,
-  ``--no-save``, ``--dist-timeout``.
+  ``--no-save``, ``--dist-timeout``, ``--strict-exchange``;
+* the fused path survives a failing in-kernel exchange: a timeout or replica divergence at an
+  epoch's end restores the epoch-start state on every rank and re-runs the epoch on the RCCL path
+  (``exchange_fallback`` on stderr, in ``DGT_METRICS_JSONL`` and ``DGT_HEALTH_LOG``; rc stays 0),
+  unless ``--strict-exchange`` keeps it fatal (rc 2), as the reference's job succeeds whenever
+  NCCL works (``slurm_train.sbatch:34-44``).
 """
 from __future__ import annotations
 
@@ -60,9 +65,21 @@ def parse_args(argv=None):
     p.add_argument("--dist-timeout", type=float, default=1800.0)
     p.add_argument("--profile", default=None, help="write a torch.profiler (kineto) trace per rank to this dir "
                    "(every path; roctx ranges with DGT_ROCTX=1 name the phases / fused epoch launches)")
+    p.add_argument("--strict-exchange", action="store_true",
+                   help="fail the job (rc 2) on an in-kernel exchange timeout / replica divergence instead of "
+                        "re-running the epoch on the RCCL path")
     p.add_argument("--debug-sync", action="store_true",
                    help="serialize kernels (AMD_SERIALIZE_KERNEL=3) and sync comm/compute streams: race hunting")
     return p.parse_known_args(argv)[0]
+
+
+def oversubscribed(device) -> bool:
+    """True when ranks share a physical device (host + PCI address gathered over ranks), as
+    bench.py reports it; a job that wraps ranks onto fewer cards says so instead of silently
+    oversubscribing them (accelerator.set_device refuses unless DGT_ALLOW_OVERSUBSCRIBE=1)."""
+    from distributed_gpu_test_amd.accelerator import device_identity
+    ids = comm.all_gather_object(device_identity(device))
+    return len(set(ids)) < len(ids)
 
 
 def newest_checkpoint(save_dir: str):
@@ -101,7 +118,8 @@ def main(argv=None) -> int:
     impl = args.impl
     if impl == "auto":
         from distributed_gpu_test_amd.runtime.tiny_trainer import fused_supported
-        fused_ok = gpu and cfg.zero_stage == 0 and cfg.gradient_accumulation_steps == 1 and \
+        # ZeRO-0 and ZeRO-1 (sharded in-kernel exchange) both run on the fused kernel
+        fused_ok = gpu and cfg.zero_stage in (0, 1) and cfg.gradient_accumulation_steps == 1 and \
             cfg.compute_dtype == "fp32" and fused_supported(N_FEATURES, HIDDEN, MICRO_BATCH)
         impl = "fused" if fused_ok else "engine"
 
@@ -109,10 +127,15 @@ def main(argv=None) -> int:
     if impl in ("fused", "graph", "stepwise", "torch"):
         from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
         trainer = TinyMLPTrainer(model, x, y, MICRO_BATCH, lr=args.lr, impl=impl, ds_config=cfg.to_dict(),
-                                 device=None if impl != "torch" else torch.device("cpu"))
+                                 device=None if impl != "torch" else torch.device("cpu"),
+                                 zero_stage=cfg.zero_stage if cfg.zero_stage in (0, 1) else 0,
+                                 strict_exchange=args.strict_exchange or None)
+        over = oversubscribed(trainer.device)
         if comm.get_rank() == 0:
-            print(f"[dgt] impl={trainer.impl} exchange={trainer.exchange} world_size={world}", file=sys.stderr,
-                  flush=True)
+            print(f"[dgt] impl={trainer.impl} exchange={trainer.exchange} zero_stage={trainer.zero_stage} "
+                  f"world_size={world} oversubscribed={over}", file=sys.stderr, flush=True)
+            for rep in trainer.xch_report:
+                print(f"[dgt] exchange self-test: {json.dumps(rep)}", file=sys.stderr, flush=True)
         if args.resume:
             found = newest_checkpoint(args.save_dir)
             if found:
@@ -132,15 +155,19 @@ def main(argv=None) -> int:
                     save_dir = os.path.join(args.save_dir, f"epoch{epoch}")
                     os.makedirs(save_dir, exist_ok=True)
                     trainer.save_checkpoint(save_dir)
+        if trainer.fallbacks and comm.get_rank() == 0:
+            print(f"[dgt] finished on {trainer.impl}/{trainer.exchange} after {len(trainer.fallbacks)} "
+                  f"exchange_fallback(s)", file=sys.stderr, flush=True)
         trainer.close()
     else:
         engine, optimizer, _, _ = dgt.initialize(args=ds_config, model=model, optimizer=optimizer,
                                                  model_parameters=model.parameters(), config=ds_config)
         device = engine.device
+        over = oversubscribed(device)
         if comm.get_rank() == 0:
             print(f"[dgt] impl=engine zero_stage={cfg.zero_stage} dtype={cfg.compute_dtype} "
                   f"oneshot={'yes' if engine.oneshot is not None else 'no'} backend={comm.backend_name()} "
-                  f"world_size={world}", file=sys.stderr, flush=True)
+                  f"world_size={world} oversubscribed={over}", file=sys.stderr, flush=True)
         data = SyntheticDataset(x, y, MICRO_BATCH, world, comm.get_rank()).to(device)
         # fused HIP loss + gradient kernel on GPU (torch's own loss on CPU)
         criterion = BCEWithLogitsLoss()
@@ -191,10 +218,10 @@ def main(argv=None) -> int:
 
 
 if __name__ == "__main__":
-    from distributed_gpu_test_amd.runtime.tiny_trainer import ReplicaDivergence
+    from distributed_gpu_test_amd.runtime.tiny_trainer import ExchangeFailure, ReplicaDivergence
     try:
         rc = main()
-    except ReplicaDivergence as e:  # every rank raises it: a loud, non-zero job failure
+    except (ReplicaDivergence, ExchangeFailure) as e:  # --strict-exchange: every rank raises it, rc 2
         print(f"[dgt] FATAL: {e}", file=sys.stderr, flush=True)
         rc = 2
     comm.destroy()
