@@ -297,6 +297,13 @@ def main(argv=None):
         B = args.batch
         if args.impl == "engine":
             trainer = TorchMLPBench(model, B, device)
+        elif args.impl == "dgt-engine":
+            import json as _json
+            from distributed_gpu_test_amd.runtime.engine_mlp import EngineMLPTrainer
+            cfg = _json.load(open(args.ds_config or os.path.join(ROOT, "configs", "ds_bench_mlp_bf16.json")))
+            cfg = dict(cfg, train_micro_batch_size_per_gpu=B)
+            cfg.pop("train_batch_size", None)
+            trainer = EngineMLPTrainer(model, B, 8, cfg)
         else:
             cdt = {None: None, "bf16": torch.bfloat16, "fp32": torch.float32}[args.comm_dtype]
             trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device, zero_stage=args.zero_stage,

@@ -3,15 +3,15 @@
 // bias-correction .item() syncs.  Memory-bound: 16-byte vector accesses on
 // every stream (Guideline 13), nontemporal hints (each byte is touched once), one float4 group per
 // thread over a full grid.  On the bench MLP's 67M parameters (profiles/r1_adam_v8_ab.txt): 5.41 TB/s
-// with fp32 gradients (the plain variant 3 ties it), 6.43 TB/s with bf16 gradients where the
-// streaming hints pay (6.12 without) - the bf16 MLP step is the case the default is tuned for.
+// with fp32 gradients, 6.43 TB/s with bf16 gradients where the streaming hints pay (6.12 without).
+// The round-1/2 loop-shape variants (two groups per thread, 8-element groups, the Adam + W^T matrix
+// kernel) measured no better and were removed; their A/B records stay in profiles/.
 // Reference: torch.optim.Adam created at train.py:85, stepped by model_engine.step() at train.py:114.
 #include <hip/hip_bf16.h>
 #include <hip/hip_fp16.h>
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 #include <algorithm>
-#include <cstdlib>
 
 namespace dgt {
 
@@ -88,66 +88,6 @@ DGT_DEVICE f32x4 adam_group(const AdamFlatArgs& a, const GT* __restrict__ grad, 
   return p;
 }
 
-// Eight consecutive elements per thread: the 16-bit streams (bf16/fp16 gradients and the compute
-// copy) then move as 16-byte vectors too, instead of the 8-byte accesses of a float4 group.
-typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
-template <typename T> DGT_DEVICE T from_f32(float x);
-template <> DGT_DEVICE __hip_bfloat16 from_f32<__hip_bfloat16>(float x) { return __float2bfloat16(x); }
-template <> DGT_DEVICE __half from_f32<__half>(float x) { return __float2half(x); }
-template <typename T, bool NT> struct Vec8 {  // 16-bit types: one 16-byte access
-  static DGT_DEVICE void load(const T* p, f32x4& lo, f32x4& hi) {
-    const u32x4 raw = vload<NT>(reinterpret_cast<const u32x4*>(p));
-    const T* h = reinterpret_cast<const T*>(&raw);
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      lo[i] = (float)h[i];
-      hi[i] = (float)h[4 + i];
-    }
-  }
-  static DGT_DEVICE void store(T* p, const f32x4& lo, const f32x4& hi) {
-    T b[8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      b[i] = from_f32<T>(lo[i]);
-      b[4 + i] = from_f32<T>(hi[i]);
-    }
-    vstore<NT>(reinterpret_cast<u32x4*>(p), *reinterpret_cast<u32x4*>(b));
-  }
-};
-template <bool NT> struct Vec8<float, NT> {
-  static DGT_DEVICE void load(const float* p, f32x4& lo, f32x4& hi) {
-    lo = Vec4<float, NT>::load(p);
-    hi = Vec4<float, NT>::load(p + 4);
-  }
-  static DGT_DEVICE void store(float* p, const f32x4& lo, const f32x4& hi) {
-    Vec4<float, NT>::store(p, lo);
-    Vec4<float, NT>::store(p + 4, hi);
-  }
-};
-
-template <typename GT, typename LT, bool NT>
-DGT_DEVICE void adam_group8(const AdamFlatArgs& a, const GT* __restrict__ grad, LT* __restrict__ lp, long long o,
-                            float scale, float step_size_neg, float bc2_sqrt) {
-  f32x4 p[2], g[2], m[2], v[2];
-  Vec8<float, NT>::load(a.master + o, p[0], p[1]);
-  Vec8<GT, NT>::load(grad + o, g[0], g[1]);
-  Vec8<float, NT>::load(a.exp_avg + o, m[0], m[1]);
-  Vec8<float, NT>::load(a.exp_avg_sq + o, v[0], v[1]);
-#pragma unroll
-  for (int h = 0; h < 2; ++h)
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-      float mm = m[h][e], vv = v[h][e];
-      p[h][e] = adam_update(p[h][e], g[h][e] * scale, mm, vv, a.hp, step_size_neg, bc2_sqrt);
-      m[h][e] = mm;
-      v[h][e] = vv;
-    }
-  Vec8<float, NT>::store(a.master + o, p[0], p[1]);
-  Vec8<float, NT>::store(a.exp_avg + o, m[0], m[1]);
-  Vec8<float, NT>::store(a.exp_avg_sq + o, v[0], v[1]);
-  if (lp) Vec8<LT, NT>::store(lp + o, p[0], p[1]);
-}
-
 // Bias corrections of this update: host scalars, or (graph replay) formed on the device from the
 // step counter in double, exactly as torch's non-capturable Adam does on the host.
 DGT_DEVICE void adam_bias_corrections(const AdamFlatArgs& a, float& step_size_neg, float& bc2_sqrt) {
@@ -166,8 +106,8 @@ DGT_DEVICE void adam_bias_corrections(const AdamFlatArgs& a, float& step_size_ne
   }
 }
 
-// GROUPS float4 groups per thread per grid-stride iteration
-template <typename GT, typename LT, bool NT, int GROUPS>
+// one float4 group per thread over a full grid (grid-stride past 2^20 blocks)
+template <typename GT, typename LT>
 __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   const long long n4 = a.n >> 2;
   float step_size_neg, bc2_sqrt;
@@ -177,80 +117,14 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
   LT* __restrict__ lp = static_cast<LT*>(a.param_lp);
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += GROUPS * stride) {
-#pragma unroll
-    for (int gi = 0; gi < GROUPS; ++gi)
-      if (gi == 0 || i + gi * stride < n4)
-        adam_group<GT, LT, NT>(a, grad, lp, 4 * (i + gi * stride), scale, step_size_neg, bc2_sqrt);
-  }
+  for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride)
+    adam_group<GT, LT, true>(a, grad, lp, 4 * i, scale, step_size_neg, bc2_sqrt);
 }
-
-// one 8-element group per thread; a trailing float4 group (n % 8 == 4) goes to thread n / 8
-template <typename GT, typename LT, bool NT>
-__global__ __launch_bounds__(256) void adam_flat8_kernel(AdamFlatArgs a) {
-  float step_size_neg, bc2_sqrt;
-  adam_bias_corrections(a, step_size_neg, bc2_sqrt);
-  float scale = a.grad_scale;
-  if (a.grad_scale_dev) scale *= *a.grad_scale_dev;
-  const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
-  LT* __restrict__ lp = static_cast<LT*>(a.param_lp);
-  const long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x, n8 = a.n >> 3;
-  if (i < n8) adam_group8<GT, LT, NT>(a, grad, lp, 8 * i, scale, step_size_neg, bc2_sqrt);
-  else if (i == n8 && (a.n & 4)) adam_group<GT, LT, NT>(a, grad, lp, 8 * i, scale, step_size_neg, bc2_sqrt);
-}
-
-// Loop shape chosen by measurement (scripts/bench_adam.py).  DGT_ADAM_VARIANT (read ONCE, at the
-// first launch: no getenv on the launch path) or adam_set_variant() selects another for A/B runs.
-static int g_adam_variant = -1;
-
-static int adam_variant() {
-  if (g_adam_variant < 0) {
-    const char* e = getenv("DGT_ADAM_VARIANT");
-    const int v = e ? atoi(e) : 0;
-    g_adam_variant = (v >= 0 && v <= 4) ? v : 0;
-  }
-  return g_adam_variant;
-}
-
-bool adam_set_variant(int v) {
-  if (v < 0 || v > 4) return false;
-  g_adam_variant = v;
-  return true;
-}
-
-static bool aligned16(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 template <typename GT, typename LT>
 static void launch_adam_v(const AdamFlatArgs& a, hipStream_t s) {
-  const long long n4 = a.n / 4;
-  long long grid;
-  switch (adam_variant()) {
-    case 1:  // two groups per thread, plain, capped grid
-      grid = std::min<long long>(std::max<long long>((n4 + 511) / 512, 1), 4096);
-      hipLaunchKernelGGL((adam_flat_kernel<GT, LT, false, 2>), dim3((int)grid), dim3(256), 0, s, a);
-      break;
-    case 2:  // two groups, streaming hints, capped grid
-      grid = std::min<long long>(std::max<long long>((n4 + 511) / 512, 1), 4096);
-      hipLaunchKernelGGL((adam_flat_kernel<GT, LT, true, 2>), dim3((int)grid), dim3(256), 0, s, a);
-      break;
-    case 3:  // one group per thread, plain, full grid
-      grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);
-      hipLaunchKernelGGL((adam_flat_kernel<GT, LT, false, 1>), dim3((int)grid), dim3(256), 0, s, a);
-      break;
-    case 4:  // one 8-element group per thread (16-byte 16-bit streams), streaming hints, full grid
-      // 16-byte loads/stores of the 16-bit streams: a slice at a 4-element offset takes the default
-      if ((sizeof(GT) == 2 && !aligned16(a.grad)) || (a.param_lp && sizeof(LT) == 2 && !aligned16(a.param_lp))) {
-        grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);
-        hipLaunchKernelGGL((adam_flat_kernel<GT, LT, true, 1>), dim3((int)grid), dim3(256), 0, s, a);
-        break;
-      }
-      grid = std::max<long long>((a.n / 8 + 1 + 255) / 256, 1);
-      hipLaunchKernelGGL((adam_flat8_kernel<GT, LT, true>), dim3((int)grid), dim3(256), 0, s, a);
-      break;
-    default:  // one group per thread, streaming hints, full grid
-      grid = std::min<long long>(std::max<long long>((n4 + 255) / 256, 1), 1 << 20);
-      hipLaunchKernelGGL((adam_flat_kernel<GT, LT, true, 1>), dim3((int)grid), dim3(256), 0, s, a);
-  }
+  const long long grid = std::min<long long>(std::max<long long>((a.n / 4 + 255) / 256, 1), 1 << 20);
+  hipLaunchKernelGGL((adam_flat_kernel<GT, LT>), dim3((int)grid), dim3(256), 0, s, a);
 }
 
 template <typename GT>
@@ -263,64 +137,6 @@ static hipError_t launch_adam_g(const AdamFlatArgs& a, hipStream_t s) {
       b.param_lp = nullptr;  // fp32 params are the master buffer itself
       launch_adam_v<GT, float>(b, s);
     }
-  }
-  return hipGetLastError();
-}
-
-// Adam over one row-major fp32 weight matrix [rows, cols] that writes the bf16 compute copy AND
-// its transpose (the dgrad GEMM's B operand, csrc/gemm.hip) in the same pass, instead of Adam
-// followed by a transpose kernel that re-reads the bf16 copy (the MLP trainer's W^T refresh).
-// Lane (rb, cg) of a wave updates rows 8rb..8rb+7 x cols 4cg..4cg+3 (rb, cg in 0..7): the eight
-// lanes of one rb read a whole 128-byte line of every fp32 stream per row, and the eight lanes of
-// one cg write a whole 128-byte line of W^T (64 rows x bf16) per column with 16-byte stores.
-// No LDS: every transposed value is already in the register that stores it.  A block's four
-// waves sit side by side along the columns: block tile = 64 rows x 128 cols.
-template <typename GT>
-__global__ __launch_bounds__(256) void adam_matrix_t_kernel(AdamFlatArgs a, __hip_bfloat16* __restrict__ lpT,
-                                                            int rows, int cols) {
-  float step_size_neg, bc2_sqrt;
-  adam_bias_corrections(a, step_size_neg, bc2_sqrt);
-  float scale = a.grad_scale;
-  if (a.grad_scale_dev) scale *= *a.grad_scale_dev;
-  const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
-  __hip_bfloat16* __restrict__ lp = static_cast<__hip_bfloat16*>(a.param_lp);
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int cg = lane & 7, rb = lane >> 3;
-  const int c = blockIdx.x * 128 + wave * 32 + cg * 4;
-  const int r = blockIdx.y * 64 + rb * 8;
-  unsigned short b[8][4];  // bf16 bits of the updated 8 x 4 block
-#pragma unroll
-  for (int k = 0; k < 8; ++k) {
-    const f32x4 p = adam_group<GT, __hip_bfloat16, true>(a, grad, lp, (long long)(r + k) * cols + c, scale,
-                                                         step_size_neg, bc2_sqrt);
-#pragma unroll
-    for (int e = 0; e < 4; ++e) b[k][e] = __bfloat16_as_ushort(__float2bfloat16(p[e]));
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    u32x4 v;
-#pragma unroll
-    for (int q = 0; q < 4; ++q) v[q] = (unsigned)b[2 * q][e] | ((unsigned)b[2 * q + 1][e] << 16);
-    *reinterpret_cast<u32x4*>(lpT + (long long)(c + e) * rows + r) = v;
-  }
-}
-
-hipError_t adam_matrix_t(const AdamFlatArgs& a, void* lpT, int rows, int cols, hipStream_t stream) {
-  if (rows <= 0 || cols <= 0 || rows % 64 || cols % 128 || a.n != (long long)rows * cols || !a.param_lp ||
-      a.lp_dtype != kBF16 || !lpT)
-    return hipErrorInvalidValue;
-  const dim3 grid(cols / 128, rows / 64);
-  switch (a.grad_dtype) {
-    case kBF16:
-      hipLaunchKernelGGL(adam_matrix_t_kernel<__hip_bfloat16>, grid, dim3(256), 0, stream, a,
-                         static_cast<__hip_bfloat16*>(lpT), rows, cols);
-      break;
-    case kF32:
-      hipLaunchKernelGGL(adam_matrix_t_kernel<float>, grid, dim3(256), 0, stream, a,
-                         static_cast<__hip_bfloat16*>(lpT), rows, cols);
-      break;
-    default:
-      return hipErrorInvalidValue;
   }
   return hipGetLastError();
 }

@@ -425,26 +425,6 @@ void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_
   DGT_CHECK_HIP(dgt::adam_flat(a, stream_of(master)));
 }
 
-void adam_matrix_t(const at::Tensor& master, const at::Tensor& param_lp, const at::Tensor& param_lpT,
-                   const at::Tensor& grad, const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq, int64_t rows,
-                   int64_t cols, double lr, double beta1, double beta2, double eps, double weight_decay, bool adamw,
-                   int64_t step, double grad_scale, const std::optional<at::Tensor>& grad_scale_dev,
-                   const std::optional<at::Tensor>& step_dev) {
-  TORCH_CHECK(rows > 0 && cols > 0 && rows % 64 == 0 && cols % 128 == 0 && master.numel() == rows * cols,
-              "dgt: adam_matrix_t needs a [rows, cols] matrix with rows % 64 == 0 and cols % 128 == 0");
-  check_gpu(param_lp, "param_lp", at::kBFloat16);
-  check_gpu(param_lpT, "param_lpT", at::kBFloat16);
-  TORCH_CHECK(param_lpT.numel() == rows * cols, "dgt: param_lpT size mismatch");
-  TORCH_CHECK(grad.scalar_type() == at::kFloat || grad.scalar_type() == at::kBFloat16,
-              "dgt: adam_matrix_t grad must be fp32 or bf16");
-  const dgt::AdamFlatArgs a = adam_args(master, param_lp, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
-                                        weight_decay, adamw, step, grad_scale, grad_scale_dev, step_dev);
-  c10::DeviceGuard guard(master.device());
-  DGT_CHECK_HIP(dgt::adam_matrix_t(a, param_lpT.data_ptr(), (int)rows, (int)cols, stream_of(master)));
-}
-
-void adam_set_variant(int64_t v) { TORCH_CHECK(dgt::adam_set_variant((int)v), "dgt: unknown adam variant ", v); }
-
 void step_increment(const at::Tensor& counter) {
   check_gpu(counter, "counter", at::kLong);
   c10::DeviceGuard guard(counter.device());
@@ -477,14 +457,11 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
 
 void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
-             const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
-             const std::optional<at::Tensor>& sk_slab, const std::optional<at::Tensor>& sk_flags) {
-  TORCH_CHECK(!(epi & dgt::kEpiBKN) || (variant != 2 && variant != 9),
-              "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK((variant >= 0 && variant <= 5) || (variant >= 7 && variant <= 9),
-              "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (128x128, 4 stages), "
-              "4 (128x128, 4 stages, 8 waves), 5 (256x128, split-K 2), 7 (128x128, BK 128, 8 waves) or 8 (128x128, "
-              "5 stages, 8 waves, 2 K-tiles per barrier) or 9 (256x256, 2 stages, one barrier per K-tile)");
+             const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant) {
+  TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
+  TORCH_CHECK(variant == 0 || variant == 1 || variant == 2 || variant == 4,
+              "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256) or 4 (128x128, 4 stages, "
+              "8 waves); the round-2 variants live in csrc/diag/gemm_variants_r2.h");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
@@ -512,7 +489,8 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
     g.C = C->data_ptr();
     g.ldc = (int)N;
   } else {
-    TORCH_CHECK(!(epi & dgt::kEpiOutF32) && (epi & dgt::kEpiStoreT), "dgt: gemm_nt without C must store C^T");
+    TORCH_CHECK(!(epi & dgt::kEpiOutF32) && !(epi & dgt::kEpiAccumulate) && (epi & dgt::kEpiStoreT),
+                "dgt: gemm_nt without C must store C^T");
   }
   if (epi & dgt::kEpiStoreT) {
     TORCH_CHECK(CT.has_value() && CT->defined(), "dgt: kEpiStoreT needs CT");
@@ -531,25 +509,9 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
     g.mask = mask->data_ptr();
     g.ldmask = (int)N;
   }
-  if (sk_slab.has_value() && sk_slab->defined() && sk_flags.has_value() && sk_flags->defined()) {
-    // split-K workspace: one fp32 256 x 128 partial per tile, two zeroed ints per tile (the kernel
-    // re-arms them); launches that share it must be stream-ordered (the caller keys it per stream)
-    const int64_t tiles = (M % 256 == 0 && N % 128 == 0) ? (M / 256) * (N / 128) : 0;
-    check_gpu(*sk_slab, "sk_slab", at::kFloat);
-    check_gpu(*sk_flags, "sk_flags", at::kInt);
-    if (tiles > 0 && sk_slab->numel() >= tiles * 256 * 128 && sk_flags->numel() >= 2 * tiles) {
-      g.sk_slab = sk_slab->data_ptr<float>();
-      g.sk_flags = sk_flags->data_ptr<int>();
-    }
-  }
   c10::DeviceGuard guard(A.device());
-  if (variant == 2 || variant == 9)
+  if (variant == 2)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
-  if (variant == 5)
-    TORCH_CHECK(g.sk_slab && M % 256 == 0 && N % 128 == 0 && K % 128 == 0 && ((M / 256) * (N / 128)) % 8 == 0,
-                "dgt: the split-K gemm needs its workspace, M % 256 == 0, N % 128 == 0, K % 128 == 0 and a tile "
-                "count divisible by 8");
-  if (variant == 7 || variant == 8) TORCH_CHECK(K % 128 == 0, "dgt: gemm variants 7 and 8 need K % 128 == 0");
   DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A), (int)variant));
 }
 
@@ -558,8 +520,8 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
 void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& master, const at::Tensor& exp_avg,
                   const at::Tensor& exp_avg_sq, const at::Tensor& param_lp, int64_t step, double lr, double beta1,
                   double beta2, double eps, double weight_decay, bool adamw, double grad_scale, int64_t variant) {
-  TORCH_CHECK(((variant >= 0 && variant <= 4) || (variant >= 6 && variant <= 9)) && step >= 1,
-              "dgt: gemm_nt_adam needs variant 0-4 or 6-9 and step >= 1");
+  TORCH_CHECK((variant == 0 || variant == 1 || variant == 2 || variant == 4) && step >= 1,
+              "dgt: gemm_nt_adam needs variant 0, 1, 2 or 4 and step >= 1");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt_adam needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {
@@ -575,9 +537,8 @@ void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& ma
   check_2d(param_lp, "param_lp", at::kBFloat16, M, N);
   for (const at::Tensor* t : {&master, &exp_avg, &exp_avg_sq, &param_lp})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "dgt: gemm_nt_adam state must be 16-byte aligned");
-  if (variant == 2 || variant == 9)
+  if (variant == 2)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
-  if (variant == 7 || variant == 8) TORCH_CHECK(K % 128 == 0, "dgt: gemm variants 7 and 8 need K % 128 == 0");
   dgt::GemmArgs g;
   std::memset(&g, 0, sizeof(g));
   g.A = A.data_ptr();
@@ -612,11 +573,58 @@ void transpose_bf16(const at::Tensor& in, const at::Tensor& out) {
 void rowsum_bf16(const at::Tensor& in, const at::Tensor& out, bool accumulate) {
   TORCH_CHECK(in.dim() == 2 && in.size(1) % 8 == 0, "dgt: rowsum needs [rows, cols % 8 == 0]");
   check_2d(in, "in", at::kBFloat16, in.size(0), in.size(1));
-  check_gpu(out, "out", at::kFloat);
+  TORCH_CHECK(out.scalar_type() == at::kFloat || out.scalar_type() == at::kBFloat16, "dgt: rowsum out must be fp32 or bf16");
+  check_gpu(out, "out", out.scalar_type());
   TORCH_CHECK(out.numel() == in.size(0), "dgt: rowsum out must have one entry per row");
   c10::DeviceGuard guard(in.device());
-  DGT_CHECK_HIP(dgt::rowsum_bf16(in.data_ptr(), out.data_ptr<float>(), (int)in.size(0), (int)in.size(1),
-                                 accumulate ? 1 : 0, stream_of(in)));
+  DGT_CHECK_HIP(dgt::rowsum_bf16(in.data_ptr(), out.data_ptr(), out.scalar_type() == at::kBFloat16 ? 1 : 0,
+                                 (int)in.size(0), (int)in.size(1), accumulate ? 1 : 0, stream_of(in)));
+}
+
+// skinny bf16 head Linear(K, N <= 4): z = a . W^T + b
+void skinny_fwd_bf16(const at::Tensor& a, const at::Tensor& W, const std::optional<at::Tensor>& b,
+                     const at::Tensor& z) {
+  TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && W.size(1) == a.size(1), "dgt: skinny_fwd needs a [M, K], W [N, K]");
+  const int64_t M = a.size(0), K = a.size(1), N = W.size(0);
+  TORCH_CHECK(N >= 1 && N <= 4 && K % 8 == 0, "dgt: skinny_fwd needs N <= 4, K % 8 == 0");
+  check_2d(a, "a", at::kBFloat16, M, K);
+  check_2d(W, "W", at::kBFloat16, N, K);
+  check_gpu(z, "z", at::kBFloat16);
+  TORCH_CHECK(z.numel() == M * N, "dgt: skinny_fwd z must be [M, N]");
+  const void* bp = nullptr;
+  if (b.has_value() && b->defined()) {
+    check_gpu(*b, "b", at::kBFloat16);
+    TORCH_CHECK(b->numel() == N, "dgt: skinny_fwd bias must have N elements");
+    bp = b->data_ptr();
+  }
+  c10::DeviceGuard guard(a.device());
+  DGT_CHECK_HIP(dgt::skinny_fwd_bf16(a.data_ptr(), W.data_ptr(), bp, z.data_ptr(), (int)M, (int)N, (int)K,
+                                     stream_of(a)));
+}
+
+// its backward: g = (dz . W) * 1[a > 0] (mask) and g^T; dW / db accumulate in fp32
+void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor& W, bool mask, const at::Tensor& g,
+                     const std::optional<at::Tensor>& gT, const at::Tensor& dW, const at::Tensor& db) {
+  const int64_t M = a.size(0), K = a.size(1), N = W.size(0);
+  TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && W.size(1) == K && N >= 1 && N <= 4 && M % 64 == 0 && K % 64 == 0,
+              "dgt: skinny_bwd needs a [M, K], W [N <= 4, K], M, K % 64 == 0");
+  check_gpu(dz, "dz", at::kBFloat16);
+  TORCH_CHECK(dz.numel() == M * N, "dgt: skinny_bwd dz must be [M, N]");
+  check_2d(a, "a", at::kBFloat16, M, K);
+  check_2d(W, "W", at::kBFloat16, N, K);
+  check_2d(g, "g", at::kBFloat16, M, K);
+  void* gTp = nullptr;
+  if (gT.has_value() && gT->defined()) {
+    check_2d(*gT, "gT", at::kBFloat16, K, M);
+    gTp = gT->data_ptr();
+  }
+  check_gpu(dW, "dW", at::kFloat);
+  check_gpu(db, "db", at::kFloat);
+  TORCH_CHECK(dW.numel() == N * K && db.numel() == N, "dgt: skinny_bwd dW [N, K] and db [N] (fp32)");
+  c10::DeviceGuard guard(a.device());
+  DGT_CHECK_HIP(dgt::skinny_bwd_bf16(dz.data_ptr(), a.data_ptr(), W.data_ptr(), mask ? 1 : 0, g.data_ptr(), gTp,
+                                     dW.data_ptr<float>(), db.data_ptr<float>(), (int)M, (int)N, (int)K,
+                                     stream_of(a)));
 }
 
 void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& y,
@@ -716,7 +724,6 @@ TORCH_LIBRARY(dgt, m) {
       "Tensor(d!) param_lp, int step, float lr, float beta1, float beta2, float eps, float weight_decay, bool adamw, "
       "float grad_scale, int variant=0) -> ()",
       &gemm_nt_adam);
-  m.def("adam_set_variant(int variant) -> ()", &adam_set_variant);
   m.def("tiny_mlp_supported(int f, int h) -> bool", &tiny_mlp_supported);
   m.def("tiny_mlp_padded_numel(int f, int h) -> int", &tiny_mlp_padded_numel);
   m.def("tiny_mlp_exchange_floats(int f, int h) -> int", &tiny_mlp_exchange_floats);
@@ -747,11 +754,6 @@ TORCH_LIBRARY(dgt, m) {
       "float lr, float beta1, float beta2, float eps, float weight_decay, bool adamw, int step, float grad_scale, "
       "Tensor? grad_scale_dev, Tensor? step_dev=None) -> ()",
       &adam_flat);
-  m.def(
-      "adam_matrix_t(Tensor(a!) master, Tensor(b!) param_lp, Tensor(c!) param_lpT, Tensor grad, Tensor(d!) exp_avg, "
-      "Tensor(e!) exp_avg_sq, int rows, int cols, float lr, float beta1, float beta2, float eps, float weight_decay, "
-      "bool adamw, int step, float grad_scale, Tensor? grad_scale_dev, Tensor? step_dev=None) -> ()",
-      &adam_matrix_t);
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz) -> ()", &bce_logits);
   m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
@@ -764,10 +766,15 @@ TORCH_LIBRARY(dgt, m) {
       &oneshot_allreduce);
   m.def(
       "gemm_nt(Tensor A, Tensor B, Tensor(a!)? C, Tensor(b!)? CT, Tensor? bias, Tensor? mask, int epi, "
-      "float alpha, int variant=0, Tensor(c!)? sk_slab=None, Tensor(d!)? sk_flags=None) -> ()",
+      "float alpha, int variant=0) -> ()",
       &gemm_nt);
   m.def("transpose_bf16(Tensor inp, Tensor(a!) out) -> ()", &transpose_bf16);
   m.def("rowsum_bf16(Tensor inp, Tensor(a!) out, bool accumulate) -> ()", &rowsum_bf16);
+  m.def("skinny_fwd_bf16(Tensor a, Tensor W, Tensor? b, Tensor(a!) z) -> ()", &skinny_fwd_bf16);
+  m.def(
+      "skinny_bwd_bf16(Tensor dz, Tensor a, Tensor W, bool mask, Tensor(a!) g, Tensor(b!)? gT, Tensor(c!) dW, "
+      "Tensor(d!) db) -> ()",
+      &skinny_bwd_bf16);
   m.def(
       "mlp_head(Tensor a, Tensor w, Tensor b0, Tensor y, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!) db, "
       "Tensor(d!) loss_acc, Tensor(e!) g, Tensor(f!) gT) -> ()",

@@ -82,12 +82,6 @@ struct AdamFlatArgs {
 hipError_t step_increment(long long* counter, hipStream_t stream);
 
 hipError_t adam_flat(const AdamFlatArgs& a, hipStream_t stream);
-// Select the flat Adam loop shape (0 = default; 1-4 = A/B variants of csrc/adam.hip); false if unknown.
-bool adam_set_variant(int variant);
-
-// Adam over a row-major [rows, cols] fp32 matrix (a.n = rows * cols, rows a multiple of 64, cols of 128) that also
-// writes the bf16 copy a.param_lp [rows, cols] and its transpose lpT [cols, rows] in the same pass.
-hipError_t adam_matrix_t(const AdamFlatArgs& a, void* lpT, int rows, int cols, hipStream_t stream);
 
 // ---------------------------------------------------------------- fused BCE-with-logits (loss.hip)
 // loss[0] = mean BCE-with-logits of z[n] (fp32 or bf16) against y[n]; dz[n] = (sigmoid(z) - y) / n.
@@ -112,7 +106,7 @@ enum GemmEpilogue : int {
   kEpiMask = 4,        // * 1[mask[m][n] > 0]   (mask: bf16 [M, N], row stride ldmask)
   kEpiStoreT = 8,      // also write C^T (bf16, row stride ldct)
   kEpiOutF32 = 16,     // C is fp32 (else bf16)
-  kEpiAccumulate = 32, // C += result (fp32 only)
+  kEpiAccumulate = 32, // C += result (fp32, or bf16 summed in fp32 and rounded once)
   kEpiBKN = 64,        // B is given as [K, N] (N contiguous): C = A . B, read with transposed LDS reads
   kEpiAdam = 128,      // C is a weight GRADIENT consumed in place: Adam updates adam.master / m / v [M, ldc]
                        // and writes the bf16 copy adam.lp; no gradient is stored (single-rank ZeRO-0)
@@ -140,13 +134,25 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   int lda, ldb, ldc, ldct, ldmask;
   float alpha;
   GemmAdam adam;       // kEpiAdam only (the gradient is alpha * A . B^T; ldc = row stride of the weight)
-  float* sk_slab;      // split-K kernel (variant 5): fp32 partial tiles, (M/256)(N/128) x 256 x 128
-  int* sk_flags;       // split-K kernel: 2 ints per tile (arrivals, slab ready), zero between launches
+  float* sk_slab;      // diag split-K kernel only (csrc/diag/gemm_variants_r2.h): fp32 partial tiles
+  int* sk_flags;       // diag split-K kernel only: 2 ints per tile (arrivals, slab ready)
 };
 
 hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream, int variant = 0);
 hipError_t transpose_bf16(const void* in, void* out, int rows, int cols, hipStream_t stream);
-hipError_t rowsum_bf16(const void* in, float* out, int rows, int cols, int accumulate, hipStream_t stream);
+// out (fp32, or bf16 when out_bf16) [rows] (+)= row sums of a bf16 [rows, cols] matrix
+hipError_t rowsum_bf16(const void* in, void* out, int out_bf16, int rows, int cols, int accumulate,
+                       hipStream_t stream);
+
+// ---------------------------------------------------------------- skinny bf16 Linear (head.hip)
+// The binary head of an MLP (Linear(K, N), N <= 4) in bf16 for the engine's MFMA chain:
+//   forward   z[M, N] = a[M, K] . W[N, K]^T + b           (bf16 in / out, fp32 accumulation)
+//   backward  g[M, K] = (dz . W) * 1[a > 0] (mask optional), g^T[K, M] (optional),
+//             dW[N, K] += dz^T . a (fp32), db[N] += sum_m dz (fp32)
+hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z, int M, int N, int K,
+                           hipStream_t stream);
+hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, float* dW,
+                           float* db, int M, int N, int K, hipStream_t stream);
 
 struct HeadArgs {      // binary head of the synthetic MLP: Linear(D, 1) + BCE-with-logits (mean)
   const void* a;       // bf16 [B, D] last hidden activation

@@ -1,0 +1,177 @@
+// Skinny bf16 Linear (N <= 4 outputs) for the engine's MFMA Linear chain (ops/linear.py): the
+// binary head of an MLP, Linear(K, 1) on the last hidden activation, which no 128x128 MFMA tile
+// fits.  Left to F.linear it runs a vendor GEMV / GEMM (hipBLASLt); here it is two bandwidth-bound
+// passes over the activation with 16-byte accesses.
+//   forward   z[M, N] = a[M, K] . W[N, K]^T + b     one wave per row, fp32 accumulation, bf16 out
+//   backward  g = (dz . W) * 1[a > 0] (+ g^T)       one wave per 64 x 64 tile of a, 8 x 8 per lane:
+//             dW += dz^T . a, db += sum dz          eight 16-B row loads of a, eight 16-B row stores
+//                                                   of g and eight of g^T per lane, no LDS; dW with
+//                                                   one fp32 atomic per column per tile
+// g (masked by the ReLU that produced a) and g^T are exactly the top hidden layer's pre-activation
+// gradient in both layouts, which its wgrad and dgrad GEMMs read next (csrc/gemm.hip).
+// Reference: the Linear(64, 1) output layer of train.py:32, widened (SyntheticMLP's head).
+#include <hip/hip_bf16.h>
+
+#include "dgt_common.h"
+#include "dgt_kernels.h"
+
+namespace dgt {
+
+namespace {
+typedef unsigned short u16;
+DGT_DEVICE float b2f(u16 u) { return __uint_as_float(((unsigned)u) << 16); }
+DGT_DEVICE u16 f2b(float f) {
+  __hip_bfloat16 b = __float2bfloat16(f);
+  return *reinterpret_cast<u16*>(&b);
+}
+DGT_DEVICE void unpack8(const uint4& v, float (&o)[8]) {
+  const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    o[2 * q] = b2f((u16)(w[q] & 0xffff));
+    o[2 * q + 1] = __uint_as_float(w[q] & 0xffff0000u);
+  }
+}
+}  // namespace
+
+template <int N>
+__global__ __launch_bounds__(256) void skinny_fwd_kernel(const u16* __restrict__ a, const u16* __restrict__ W,
+                                                         const u16* __restrict__ b, u16* __restrict__ z, int M, int K) {
+  const int l = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const u16* ar = a + (long long)row * K;
+  float acc[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) acc[n] = 0.f;
+#pragma unroll 4  // the row's 16-byte loads in flight together
+  for (int c = l * 8; c < K; c += 64 * 8) {
+    float av[8];
+    unpack8(*reinterpret_cast<const uint4*>(ar + c), av);
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      float wv[8];
+      unpack8(*reinterpret_cast<const uint4*>(W + (long long)n * K + c), wv);
+#pragma unroll
+      for (int e = 0; e < 8; ++e) acc[n] = fmaf(av[e], wv[e], acc[n]);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) acc[n] = wave_sum(acc[n]);
+  if (l < N) {
+    float v = acc[0];
+#pragma unroll
+    for (int n = 1; n < N; ++n) v = l == n ? acc[n] : v;
+    z[(long long)row * N + l] = f2b(v + (b ? b2f(b[l]) : 0.f));
+  }
+}
+
+template <int N>
+__global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__ dz, const u16* __restrict__ a,
+                                                         const u16* __restrict__ W, int mask, u16* __restrict__ g,
+                                                         u16* __restrict__ gT, float* __restrict__ dW,
+                                                         float* __restrict__ db, int M, int K) {
+  const int l = threadIdx.x & 63, cg = l & 7, rb = l >> 3, wv = threadIdx.x >> 6;
+  const int r = blockIdx.y * 64 + rb * 8, c = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + cg * 8;
+  float w[N][8];
+#pragma unroll
+  for (int n = 0; n < N; ++n) unpack8(*reinterpret_cast<const uint4*>(W + (long long)n * K + c), w[n]);
+  uint4 av[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) av[k] = *reinterpret_cast<const uint4*>(a + (long long)(r + k) * K + c);
+  float part[N][8];
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) part[n][e] = 0.f;
+  u16 gb[8][8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float d[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) d[n] = b2f(dz[(long long)(r + k) * N + n]);
+    float x[8];
+    unpack8(av[k], x);
+    unsigned o[4];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float s = 0.f;
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        s = fmaf(d[n], w[n][e], s);
+        part[n][e] = fmaf(d[n], x[e], part[n][e]);
+      }
+      gb[k][e] = f2b((!mask || x[e] > 0.f) ? s : 0.f);
+    }
+#pragma unroll
+    for (int q = 0; q < 4; ++q) o[q] = (unsigned)gb[k][2 * q] | ((unsigned)gb[k][2 * q + 1] << 16);
+    *reinterpret_cast<uint4*>(g + (long long)(r + k) * K + c) = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  if (gT) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      unsigned o[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) o[q] = (unsigned)gb[2 * q][e] | ((unsigned)gb[2 * q + 1][e] << 16);
+      *reinterpret_cast<uint4*>(gT + (long long)(c + e) * M + r) = make_uint4(o[0], o[1], o[2], o[3]);
+    }
+  }
+  // dW: sum the 8 row-blocks of the tile (lanes cg, cg + 8, ..., cg + 56), one atomic per column
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = part[n][e];
+      x += __shfl_xor(x, 8);
+      x += __shfl_xor(x, 16);
+      x += __shfl_xor(x, 32);
+      part[n][e] = x;
+    }
+  if (rb == 0) {
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) atomicAdd(&dW[(long long)n * K + c + e], part[n][e]);
+  }
+  if (blockIdx.x == 0 && blockIdx.y == 0 && wv == 0) {  // db, in a fixed order
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      float s = 0.f;
+      for (int i = l; i < M; i += 64) s += b2f(dz[(long long)i * N + n]);
+      s = wave_sum(s);
+      if (l == 0) atomicAdd(&db[n], s);
+    }
+  }
+}
+
+hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z, int M, int N, int K,
+                           hipStream_t stream) {
+  if (N < 1 || N > 4 || K % 8 || M <= 0) return hipErrorInvalidValue;
+  const dim3 grid((M + 3) / 4), blk(256);
+  const u16 *ap = static_cast<const u16*>(a), *wp = static_cast<const u16*>(W), *bp = static_cast<const u16*>(b);
+  u16* zp = static_cast<u16*>(z);
+  switch (N) {
+    case 1: hipLaunchKernelGGL(skinny_fwd_kernel<1>, grid, blk, 0, stream, ap, wp, bp, zp, M, K); break;
+    case 2: hipLaunchKernelGGL(skinny_fwd_kernel<2>, grid, blk, 0, stream, ap, wp, bp, zp, M, K); break;
+    case 3: hipLaunchKernelGGL(skinny_fwd_kernel<3>, grid, blk, 0, stream, ap, wp, bp, zp, M, K); break;
+    default: hipLaunchKernelGGL(skinny_fwd_kernel<4>, grid, blk, 0, stream, ap, wp, bp, zp, M, K);
+  }
+  return hipGetLastError();
+}
+
+hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, float* dW,
+                           float* db, int M, int N, int K, hipStream_t stream) {
+  if (N < 1 || N > 4 || M % 64 || K % 64 || M <= 0 || K <= 0) return hipErrorInvalidValue;
+  const int wpb = K % 256 == 0 ? 4 : 1;  // 4 tiles per block side by side when the width allows
+  const dim3 grid(K / (64 * wpb), M / 64), blk(64 * wpb);
+  const u16 *dp = static_cast<const u16*>(dz), *ap = static_cast<const u16*>(a), *wp = static_cast<const u16*>(W);
+  u16 *gp = static_cast<u16*>(g), *gtp = static_cast<u16*>(gT);
+  switch (N) {
+    case 1: hipLaunchKernelGGL(skinny_bwd_kernel<1>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, dW, db, M, K); break;
+    case 2: hipLaunchKernelGGL(skinny_bwd_kernel<2>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, dW, db, M, K); break;
+    case 3: hipLaunchKernelGGL(skinny_bwd_kernel<3>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, dW, db, M, K); break;
+    default: hipLaunchKernelGGL(skinny_bwd_kernel<4>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, dW, db, M, K);
+  }
+  return hipGetLastError();
+}
+
+}  // namespace dgt

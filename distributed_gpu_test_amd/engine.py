@@ -85,7 +85,9 @@ class Engine:
         fused_linear = config.amd.fused_linear
         if fused_linear is None:  # auto: kernel injection unless the graphed module is asked for
             fused_linear = not config.amd.graph_module
-        if fused_linear and device.type == "cuda" and self.dtype == torch.float32:
+        if fused_linear and device.type == "cuda" and self.dtype in (torch.float32, torch.bfloat16):
+            # fp32: the small-batch fused Linear kernels (csrc/linear.hip); bf16: the MFMA GEMM chain
+            # (ops/mfma_linear.py: gemm.hip + head.hip, no vendor BLAS)
             from .ops.linear import inject_fused_linear
             self.fused_linear_layers = inject_fused_linear(self.module, grad_in_place=True)
         self.stage = config.zero_stage
@@ -161,6 +163,7 @@ class Engine:
         self.faults = FaultInjector.from_env(self.rank)
         self._timers: Dict[str, float] = {}
         self._seed_one: Optional[torch.Tensor] = None
+        self._grads_dirty = False  # the flat gradient buffer holds something since the last zero_grad
         self._grad_norm: Optional[torch.Tensor] = None
         self._boundary_pending = False
         self.training = True
@@ -214,6 +217,13 @@ class Engine:
 
     def zero_grad(self) -> None:
         self.store.zero_grad()
+        self._grads_dirty = False
+
+    @property
+    def linear_fallbacks(self) -> Dict[str, int]:
+        """Calls that left the hand-written Linear kernels for F.linear (vendor BLAS), by reason."""
+        from .ops.linear import FALLBACKS
+        return dict(FALLBACKS)
 
     # ------------------------------------------------------------------ forward / backward / step
     def forward(self, *args, **kwargs):
@@ -260,7 +270,8 @@ class Engine:
     def backward(self, loss: torch.Tensor, retain_graph: bool = False) -> torch.Tensor:
         loss = self.faults.maybe_corrupt_loss(loss, self.global_steps)
         boundary = self.is_gradient_accumulation_boundary()
-        self.store.rebind_grads()
+        if self.store.rebind_grads():
+            self._grads_dirty = True
         self.reducer.arm(boundary and self.training)
         scaled = loss.float()
         if self.gas > 1:
@@ -269,8 +280,9 @@ class Engine:
             scaled = scaled * self.loss_scaler.scale
         t0 = time.perf_counter() if self.config.wall_clock_breakdown else 0.0
         from .ops.linear import engine_backward
-        with tracing.range("dgt.backward"), engine_backward():
+        with tracing.range("dgt.backward"), engine_backward(grads_zero=not self._grads_dirty):
             scaled.backward(self._backward_seed(scaled, loss), retain_graph=retain_graph)
+        self._grads_dirty = True
         if boundary:
             with tracing.range("dgt.allreduce_wait"):
                 self.reducer.finish()
@@ -421,7 +433,7 @@ class Engine:
 
     def _finish_step(self, skipped: bool, zero: bool = True) -> None:
         if zero:
-            self.store.zero_grad()
+            self.zero_grad()
         self.global_steps += 1
         self.global_samples += self.config.train_batch_size
         if self.lr_scheduler is not None and not skipped:

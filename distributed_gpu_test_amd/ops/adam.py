@@ -33,21 +33,3 @@ def adam_flat_(master: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, 
             step = int(step_dev.item())
         adam_flat_reference_(master, grad, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, weight_decay,
                              adamw, grad_scale, grad_scale_dev, param_lp)
-
-
-def adam_matrix_t_(master: torch.Tensor, param_lp: torch.Tensor, param_lpT: torch.Tensor, grad: torch.Tensor,
-                   exp_avg: torch.Tensor, exp_avg_sq: torch.Tensor, rows: int, cols: int, step: int, lr: float,
-                   beta1: float = 0.9, beta2: float = 0.999, eps: float = 1e-8, weight_decay: float = 0.0,
-                   adamw: bool = False, grad_scale: float = 1.0,
-                   grad_scale_dev: Optional[torch.Tensor] = None, step_dev: Optional[torch.Tensor] = None) -> None:
-    """Adam over a flat row-major ``[rows, cols]`` fp32 matrix that also writes the bf16 copy
-    ``param_lp`` ([rows, cols]) and its transpose ``param_lpT`` ([cols, rows]) in the same pass
-    (the MLP trainer's weight + W^T refresh).  Same numerics as ``adam_flat_``."""
-    if master.is_cuda:
-        require().adam_matrix_t(master, param_lp, param_lpT, grad, exp_avg, exp_avg_sq, int(rows), int(cols),
-                                float(lr), float(beta1), float(beta2), float(eps), float(weight_decay), bool(adamw),
-                                int(step), float(grad_scale), grad_scale_dev, step_dev)
-    else:
-        adam_flat_(master, grad, exp_avg, exp_avg_sq, step, lr, beta1, beta2, eps, weight_decay, adamw, grad_scale,
-                   grad_scale_dev, param_lp, step_dev)
-        param_lpT.copy_(param_lp.view(rows, cols).t().reshape(param_lpT.shape))

@@ -28,8 +28,8 @@ def gemm_nt_reference(A, B, C=None, CT=None, bias=None, mask=None, relu=False, o
     if mask is not None:
         r = torch.where(mask.float() > 0, r, torch.zeros_like(r))
     if C is not None:
-        if out_f32 and accumulate:
-            C.add_(r)
+        if accumulate:
+            C.copy_((C.float() + r).to(C.dtype))
         else:
             C.copy_(r.to(C.dtype))
     if CT is not None:
@@ -41,41 +41,19 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
             bias: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, relu: bool = False,
             out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0,
             b_kn: bool = False) -> None:
-    """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage, 2 = 256x256 8-phase pipeline,
-    3 = 128x128 tiles 4-stage, 4 = 128x128 tiles 4-stage with 8 waves, 5 = 256x128 tiles with K
-    split over two blocks that meet through a per-tile counter (the M = 1024 MLP products),
-    7 = 128x128 tiles, 8 waves, 2 stages of BK = 128 (K % 128 == 0; one block per CU),
-    8 = 128x128 tiles, 8 waves, 5 stages of BK = 64 with one barrier per two K-tiles (K % 128 == 0).
+    """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage (2 blocks per CU),
+    2 = 256x256 8-phase pipeline, 4 = 128x128 tiles 4-stage with 8 waves (1 block per CU).
 
     ``b_kn=True``: B is given as ``[K, N]`` (N contiguous) and ``C = alpha * A @ B`` — the operand is
-    staged as it lies and read with transposed LDS reads (128x128 kernels only)."""
+    staged as it lies and read with transposed LDS reads (128x128 kernels only).  ``accumulate``
+    adds into C (fp32, or bf16 summed in fp32 and rounded once)."""
     if not A.is_cuda:
         gemm_nt_reference(A, B, C, CT, bias, mask, relu, out_f32, accumulate, alpha, b_kn)
         return
     epi = ((EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | (EPI_MASK if mask is not None else 0)
            | (EPI_STORE_T if CT is not None else 0) | (EPI_OUT_F32 if out_f32 else 0)
            | (EPI_ACCUMULATE if accumulate else 0) | (EPI_B_KN if b_kn else 0))
-    M, N = A.shape[0], B.shape[1] if b_kn else B.shape[0]
-    slab, flags = _sk_workspace(A.device, M, N) if variant == 5 and not out_f32 else (None, None)
-    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant), slab, flags)
-
-
-_SK: dict = {}
-
-
-def _sk_workspace(device: torch.device, M: int, N: int):
-    """Workspace of the split-K kernel (variant 5): fp32 partial tiles + zeroed per-tile flags that
-    the kernel re-arms.  One per (device, stream): launches sharing it are stream-ordered."""
-    if M % 256 or N % 128 or ((M // 256) * (N // 128)) % 8:
-        return None, None
-    tiles = (M // 256) * (N // 128)
-    key = (device.index, torch.cuda.current_stream(device).cuda_stream)
-    ws = _SK.get(key)
-    if ws is None or ws[1].numel() < 2 * tiles:
-        ws = (torch.empty(tiles * 256 * 128, dtype=torch.float32, device=device),
-              torch.zeros(2 * tiles, dtype=torch.int32, device=device))
-        _SK[key] = ws
-    return ws
+    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant))
 
 
 def gemm_nt_adam_(A: torch.Tensor, B: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor,
@@ -85,8 +63,7 @@ def gemm_nt_adam_(A: torch.Tensor, B: torch.Tensor, master: torch.Tensor, exp_av
     """Weight gradient ``grad_scale * A @ B.T`` ([M, N], never materialised) consumed in place by
     Adam: updates the fp32 ``master`` / ``exp_avg`` / ``exp_avg_sq`` ([M, N]) and writes the bf16
     compute copy ``param_lp``.  One launch instead of wgrad GEMM + gradient store + flat Adam.
-    variant as ``gemm_nt`` (0-4, 7, 8), or 6: persistent blocks whose MFMA waves hand each finished tile
-    to Adam waves that update it while the next tile computes (K = 1024 only)."""
+    variant as ``gemm_nt``."""
     if not A.is_cuda:
         from .reference import adam_flat_reference_
         g = (A.float() @ B.float().t()).reshape(-1)
@@ -106,11 +83,41 @@ def transpose_bf16(inp: torch.Tensor, out: torch.Tensor) -> None:
 
 
 def rowsum_bf16(inp: torch.Tensor, out: torch.Tensor, accumulate: bool = False) -> None:
+    """out (fp32 or bf16) [rows] (+)= row sums of a bf16 [rows, cols] matrix (summed in fp32)."""
     if inp.is_cuda:
         require().rowsum_bf16(inp, out, accumulate)
     else:
         s = inp.float().sum(1)
-        out.add_(s) if accumulate else out.copy_(s)
+        out.copy_((out.float() + s).to(out.dtype) if accumulate else s.to(out.dtype))
+
+
+def skinny_fwd_bf16(a: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor], z: torch.Tensor) -> None:
+    """Head Linear(K, N <= 4) in bf16: z[M, N] = a . w^T + b (fp32 accumulation, csrc/head.hip)."""
+    if a.is_cuda:
+        require().skinny_fwd_bf16(a, w, b, z)
+        return
+    r = a.float() @ w.float().t()
+    if b is not None:
+        r = r + b.float()
+    z.copy_(r.reshape(z.shape).to(z.dtype))
+
+
+def skinny_bwd_bf16(dz: torch.Tensor, a: torch.Tensor, w: torch.Tensor, mask: bool, g: torch.Tensor,
+                    gT: Optional[torch.Tensor], dw: torch.Tensor, db: torch.Tensor) -> None:
+    """Its backward: g = (dz . w) * 1[a > 0] (if mask) and g^T (bf16); dw [N, K] and db [N] (fp32)
+    accumulate dz^T . a and the column sums of dz."""
+    if a.is_cuda:
+        require().skinny_bwd_bf16(dz, a, w, mask, g, gT, dw, db)
+        return
+    d = dz.float().reshape(a.shape[0], w.shape[0])
+    gg = d @ w.float()
+    if mask:
+        gg = gg * (a.float() > 0)
+    g.copy_(gg.to(g.dtype))
+    if gT is not None:
+        gT.copy_(gg.t().to(gT.dtype))
+    dw.add_(d.t() @ a.float())
+    db.add_(d.sum(0))
 
 
 def mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT) -> None:

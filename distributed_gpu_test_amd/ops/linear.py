@@ -11,11 +11,16 @@ launch forward (bias and ReLU folded in) and one launch backward (ReLU mask, dx,
 ``nn.ReLU`` that directly follows it in an ``nn.Sequential`` — keeping the same Parameter objects
 and state_dict keys, so checkpoints, the engine's flat buffers and optimizers are unaffected.
 
-Taken only for fp32 GPU tensors of small shapes (``SMALL``); anything else runs ``F.linear``.
+Taken only for fp32 GPU tensors of small shapes (``SMALL``); anything else runs ``F.linear`` and is
+counted (``FALLBACKS``).  bf16 models get the MFMA GEMM chain of ``ops/mfma_linear.py`` instead:
+``inject_fused_linear`` dispatches on the parameters' dtype.
 """
 from __future__ import annotations
 
+import collections
 import contextlib
+import os
+import sys
 
 import torch
 import torch.nn as nn
@@ -29,20 +34,42 @@ from . import _ext
 # process-wide counter, not a thread-local.  Any other backward -- torch.autograd.grad on the
 # parameters, a user's own loss.backward() -- gets dW / db returned to autograd as usual.
 _ENGINE_BACKWARD = 0
+# the engine's flat gradient buffer is all zeros at the start of this backward (the first micro-step
+# after zero_grad): the bf16 MFMA chain then STORES its weight gradients instead of accumulating
+_GRADS_ZERO = False
 
 
 @contextlib.contextmanager
-def engine_backward():
-    global _ENGINE_BACKWARD
+def engine_backward(grads_zero: bool = False):
+    global _ENGINE_BACKWARD, _GRADS_ZERO
     _ENGINE_BACKWARD += 1
+    prev, _GRADS_ZERO = _GRADS_ZERO, bool(grads_zero)
     try:
         yield
     finally:
         _ENGINE_BACKWARD -= 1
+        _GRADS_ZERO = prev
 
 
 def _in_place_active() -> bool:
     return _ENGINE_BACKWARD > 0
+
+
+def _grads_zero() -> bool:
+    return _GRADS_ZERO
+
+
+# Every call that leaves the hand-written kernels for F.linear (hipBLASLt / rocBLAS), by reason:
+# the engine reports them (Engine.linear_fallbacks, one stderr warning per reason on rank 0).
+FALLBACKS: "collections.Counter[str]" = collections.Counter()
+_WARNED: set = set()
+
+
+def count_fallback(reason: str) -> None:
+    FALLBACKS[reason] += 1
+    if reason not in _WARNED and os.environ.get("RANK", "0") == "0":
+        _WARNED.add(reason)
+        print(f"[dgt] WARNING: Linear falls back to F.linear (vendor BLAS): {reason}", file=sys.stderr, flush=True)
 
 SMALL_M = 256            # rows per call (batch)
 SMALL_WORK = 1 << 22     # M * N * K: beyond this a tiled GEMM (hipBLASLt / csrc/gemm.hip) wins
@@ -82,9 +109,9 @@ class _FusedLinearFn(torch.autograd.Function):
         return dx, dw, db, None, None
 
 
-def _grad_view_ok(p) -> bool:
+def _grad_view_ok(p, dtype=torch.float32) -> bool:
     g = p.grad
-    return (g is not None and g.is_cuda and g.dtype == torch.float32 and g.is_contiguous()
+    return (g is not None and g.is_cuda and g.dtype == dtype and g.is_contiguous()
             and g.shape == p.shape and not torch.is_grad_enabled())
 
 
@@ -101,6 +128,9 @@ def fused_linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = 
     (their post-accumulate hooks still fire); any other backward gets them returned as usual."""
     if _fusable(x, weight):
         return _FusedLinearFn.apply(x.contiguous(), weight, bias, relu, grad_in_place)
+    if x.is_cuda:
+        count_fallback(f"fp32 Linear({weight.shape[1]}, {weight.shape[0]}) on {tuple(x.shape)} {x.dtype} input is "
+                       "beyond the small-batch kernels")
     y = F.linear(x, weight, bias)
     return F.relu(y) if relu else y
 
@@ -219,7 +249,12 @@ def inject_fused_linear(module: nn.Module, grad_in_place: bool = False) -> int:
     only fused layers becomes a ``FusedChain`` (its class is swapped in place, so the object, its
     children and keys stay the same).  Returns the number of Linear layers replaced.
     ``grad_in_place``: see ``fused_linear`` (the engine sets it: its .grad tensors are persistent
-    views into the flat gradient bucket)."""
+    views into the flat gradient bucket).  A bf16 module goes to the MFMA chain injection
+    (``ops/mfma_linear.py``)."""
+    p = next(module.parameters(), None)
+    if p is not None and p.dtype == torch.bfloat16:
+        from .mfma_linear import inject_mfma_linear
+        return inject_mfma_linear(module, grad_in_place)
     n = 0
     if isinstance(module, nn.Sequential):
         kids = list(module.children())

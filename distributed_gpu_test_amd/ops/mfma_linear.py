@@ -1,0 +1,267 @@
+"""bf16 Linear(+ReLU) chains on the hand-written MFMA GEMMs, for the engine's bf16 path.
+
+Reference: the model's ``Linear -> ReLU -> Linear`` (``train.py:29-33``), forward at
+``train.py:107`` and backward at ``train.py:113``, scaled to the bench MLP (BASELINE config #2).
+
+Left to autograd, a bf16 ``nn.Linear`` runs ``F.linear`` = hipBLASLt (``Cijk_*`` kernels) plus
+separate bias, ReLU and ReLU-backward elementwise passes.  A chain of layers here is ONE autograd
+node whose kernels are this framework's (``csrc/gemm.hip``, ``csrc/head.hip``):
+
+    forward   y_i = relu(x_i W_i^T + b_i)          gemm_nt, bias + ReLU epilogue, plus y_i^T (the next
+                                                   layer's wgrad operand) from the same epilogue
+    head      z = y_L w^T + b  (N <= 4 outputs)    skinny_fwd_bf16
+    backward  g_L = (dz w) * 1[y_L > 0], g_L^T     skinny_bwd_bf16 (+ the head's dw, db)
+              dW_i = g_i^T x_i  -> the .grad view   gemm_nt (stores into the engine's flat bf16
+                                                   gradient bucket; accumulates after the first
+                                                   micro-step of an accumulation window)
+              db_i = row sums of g_i^T              rowsum_bf16 (bf16 out)
+              g_{i-1} = (g_i W_i) * 1[x_i > 0], g^T  gemm_nt reading W_i[out, in] as a [K, N] operand
+                                                   (transposed LDS reads), mask + C^T epilogue
+
+Inside the engine's backward (``ops.linear.engine_backward``) the gradients land straight in the
+parameters' ``.grad`` views; any other backward gets them returned to autograd.  Structures
+recognised: an ``nn.Sequential`` of ``Linear[, ReLU]`` ... ending in a ``Linear`` (MFMA-sized or a
+skinny head), and ``SyntheticMLP`` (``layers`` + ReLU + ``head``).  MFMA-sized means in and out
+features multiples of 128; at run time the batch must be a multiple of 128 too.  Anything else
+runs the module's own forward (``F.linear``) and is counted in ``ops.linear.FALLBACKS``.
+"""
+from __future__ import annotations
+
+from typing import List, Optional, Sequence, Tuple
+
+import torch
+import torch.nn as nn
+
+from ..models.synthetic_mlp import SyntheticMLP
+from .gemm import gemm_nt, rowsum_bf16, skinny_bwd_bf16, skinny_fwd_bf16, transpose_bf16
+from .linear import _grad_view_ok, _grads_zero, _in_place_active, count_fallback
+
+MAX_HEAD = 4
+BF16 = torch.bfloat16
+
+
+def _mfma_sized(lin: nn.Linear) -> bool:
+    return lin.in_features % 128 == 0 and lin.out_features % 128 == 0
+
+
+def _head_sized(lin: nn.Linear) -> bool:
+    return lin.out_features <= MAX_HEAD and lin.in_features % 128 == 0
+
+
+def chain_layout(linears: Sequence[nn.Linear], relus: Sequence[bool]) -> Optional[bool]:
+    """None if the chain cannot run on the kernels, else whether its last Linear is a skinny head."""
+    if not linears or len(linears) != len(relus):
+        return None
+    head = not _mfma_sized(linears[-1])
+    body = linears[:-1] if head else linears
+    if not body or not all(_mfma_sized(l) for l in body):
+        return None
+    if head and (relus[-1] or not _head_sized(linears[-1])):
+        return None
+    for a, b in zip(linears, linears[1:]):
+        if a.out_features != b.in_features:
+            return None
+    return head
+
+
+def _runtime_reason(x: torch.Tensor, params: Sequence[Optional[torch.Tensor]]) -> Optional[str]:
+    if not x.is_cuda or x.dtype != BF16 or x.dim() != 2:
+        return f"input {tuple(x.shape)} {x.dtype} on {x.device.type} is not a 2-D bf16 GPU tensor"
+    if x.shape[0] % 128:
+        return f"batch {x.shape[0]} is not a multiple of 128 (the MFMA GEMM's tile)"
+    for p in params:
+        if p is not None and (p.dtype != BF16 or not p.is_contiguous() or p.data_ptr() % 16):
+            return "a parameter is not a contiguous, 16-byte aligned bf16 tensor"
+    return None
+
+
+class _MfmaChainFn(torch.autograd.Function):
+    @staticmethod
+    def forward(ctx, x, relus, head, grad_in_place, *wb):
+        L = len(relus) - (1 if head else 0)  # MFMA layers; the head (if any) is the last pair of wb
+        need = ctx.needs_input_grad
+        M, dev = x.shape[0], x.device
+        xs: List[torch.Tensor] = [x]
+        xTs: List[Optional[torch.Tensor]] = [None] * L
+        if need[4]:  # layer 0's wgrad reads x^T
+            xTs[0] = torch.empty(x.shape[1], M, dtype=BF16, device=dev)
+            transpose_bf16(x, xTs[0])
+        h = x
+        for i in range(L):
+            w, b = wb[2 * i], wb[2 * i + 1]
+            y = torch.empty(M, w.shape[0], dtype=BF16, device=dev)
+            yT = None
+            if i + 1 < L and need[4 + 2 * (i + 1)]:
+                yT = xTs[i + 1] = torch.empty(w.shape[0], M, dtype=BF16, device=dev)
+            gemm_nt(h, w, C=y, CT=yT, bias=None if b is None else b.float(), relu=relus[i])
+            xs.append(y)
+            h = y
+        out = h
+        if head:
+            wh, bh = wb[2 * L], wb[2 * L + 1]
+            out = torch.empty(M, wh.shape[0], dtype=BF16, device=dev)
+            skinny_fwd_bf16(h, wh, bh, out)
+        ctx.relus, ctx.head, ctx.L = tuple(relus), bool(head), L
+        ctx.has_bias = tuple(b is not None for b in wb[1::2])
+        ctx.grad_in_place = grad_in_place and all(p is None or p.is_leaf for p in wb)
+        ctx.params = wb if ctx.grad_in_place else ()
+        ctx.save_for_backward(*xs, *xTs, *wb[0::2])
+        return out
+
+    @staticmethod
+    def backward(ctx, dout):
+        L, head, relus = ctx.L, ctx.head, ctx.relus
+        saved = ctx.saved_tensors
+        xs, xTs, ws = saved[:L + 1], saved[L + 1:2 * L + 1], saved[2 * L + 1:]
+        need = ctx.needs_input_grad
+        active = ctx.grad_in_place and _in_place_active()
+        zero = _grads_zero()
+        M, dev = xs[0].shape[0], xs[0].device
+        n_pairs = L + (1 if head else 0)
+        grads: List[Optional[torch.Tensor]] = [None] * (2 * n_pairs)
+        dout = dout.to(BF16).contiguous()
+
+        def leaf(j):
+            return ctx.params[j] if active else None
+
+        if head:
+            wh = ws[L]
+            kh = wh.shape[1]
+            g = torch.empty(M, kh, dtype=BF16, device=dev)
+            gT = torch.empty(kh, M, dtype=BF16, device=dev)
+            dw = torch.zeros(wh.shape, dtype=torch.float32, device=dev)
+            db = torch.zeros(wh.shape[0], dtype=torch.float32, device=dev)
+            skinny_bwd_bf16(dout, xs[L], wh, relus[L - 1] if L > 0 else False, g, gT, dw, db)
+            jw, jb = 2 * L, 2 * L + 1
+            for j, val in ((jw, dw), (jb, db)):
+                if j == jb and not ctx.has_bias[L]:
+                    continue
+                if not need[4 + j]:
+                    continue
+                p = leaf(j)
+                if p is not None and _grad_view_ok(p, BF16):
+                    p.grad.add_(val)  # tiny: [N <= 4, K] and [N]
+                else:
+                    grads[j] = val.to(BF16)
+        else:
+            y = xs[L]
+            g = (dout * (y > 0)).contiguous() if relus[L - 1] else dout
+            gT = torch.empty(g.shape[1], M, dtype=BF16, device=dev)
+            transpose_bf16(g, gT)
+        dx = None
+        for i in reversed(range(L)):
+            w = ws[i]
+            jw, jb = 2 * i, 2 * i + 1
+            if need[4 + jw]:
+                p = leaf(jw)
+                if p is not None and _grad_view_ok(p, BF16):
+                    gemm_nt(gT, xTs[i], C=p.grad, accumulate=not zero)
+                else:
+                    grads[jw] = torch.empty_like(w)
+                    gemm_nt(gT, xTs[i], C=grads[jw])
+            if ctx.has_bias[i] and need[4 + jb]:
+                p = leaf(jb)
+                if p is not None and _grad_view_ok(p, BF16):
+                    rowsum_bf16(gT, p.grad, accumulate=not zero)
+                else:
+                    grads[jb] = torch.empty(w.shape[0], dtype=BF16, device=dev)
+                    rowsum_bf16(gT, grads[jb])
+            if i > 0:
+                k = w.shape[1]
+                g_prev = torch.empty(M, k, dtype=BF16, device=dev)
+                gT_prev = torch.empty(k, M, dtype=BF16, device=dev)
+                gemm_nt(g, w, C=g_prev, CT=gT_prev, mask=xs[i] if relus[i - 1] else None, b_kn=True)
+                g, gT = g_prev, gT_prev
+            elif need[0]:
+                dx = torch.empty_like(xs[0])
+                gemm_nt(g, w, C=dx, b_kn=True)
+        return (dx, None, None, None, *grads)
+
+
+def run_chain(x: torch.Tensor, linears: Sequence[nn.Linear], relus: Sequence[bool], head: bool,
+              grad_in_place: bool) -> Optional[torch.Tensor]:
+    """The chain on the kernels, or None (after counting the reason) if this call cannot run there."""
+    wb = []
+    for l in linears:
+        wb.append(l.weight)
+        wb.append(l.bias)
+    why = _runtime_reason(x, wb)
+    if why is None and x.requires_grad and linears[0].in_features % 128:
+        why = "the input needs a gradient and its features are not a multiple of 128"
+    if why is not None:
+        count_fallback(f"bf16 MFMA chain: {why}")
+        return None
+    return _MfmaChainFn.apply(x.contiguous(), tuple(relus), head, grad_in_place, *wb)
+
+
+class MfmaSequential(nn.Sequential):
+    """An ``nn.Sequential`` of ``Linear[, ReLU]`` ... ``Linear`` run as one MFMA chain (same children,
+    keys and parameters; the class is swapped in place by ``inject_mfma_linear``)."""
+
+    def _spec(self):
+        spec = self.__dict__.get("_dgt_spec")
+        if spec is None:
+            kids = list(self.children())
+            linears, relus, ok = [], [], True
+            for k in kids:
+                if type(k) is nn.Linear:
+                    linears.append(k)
+                    relus.append(False)
+                elif type(k) is nn.ReLU and linears and not relus[-1]:
+                    relus[-1] = True
+                else:
+                    ok = False
+            head = chain_layout(linears, relus) if ok else None
+            spec = (linears, relus, head)
+            self.__dict__["_dgt_spec"] = spec
+        return spec
+
+    def forward(self, x):
+        linears, relus, head = self._spec()
+        if head is not None and x.dim() == 2:
+            out = run_chain(x, linears, relus, head, self.__dict__.get("_dgt_in_place", False))
+            if out is not None:
+                return out
+        return super().forward(x)
+
+
+class MfmaSyntheticMLP(SyntheticMLP):
+    """``SyntheticMLP`` (``layers`` each followed by ReLU, then ``head``) as one MFMA chain."""
+
+    def forward(self, x):
+        linears = list(self.layers) + [self.head]
+        relus = [True] * len(self.layers) + [False]
+        head = chain_layout(linears, relus)
+        if head is not None and x.dim() == 2:
+            out = run_chain(x, linears, relus, head, self.__dict__.get("_dgt_in_place", False))
+            if out is not None:
+                return out
+        return super().forward(x)
+
+
+def inject_mfma_linear(module: nn.Module, grad_in_place: bool = False) -> int:
+    """Swap every recognised bf16 chain inside ``module`` (or ``module`` itself) for its MFMA form,
+    in place: same objects, children, parameters and state_dict keys.  Returns the number of Linear
+    layers that run on the kernels; a chain that does not fit is left alone and counted."""
+    if type(module) is SyntheticMLP:
+        linears = list(module.layers) + [module.head]
+        if chain_layout(linears, [True] * len(module.layers) + [False]) is None:
+            count_fallback(f"bf16 SyntheticMLP(width={module.width}) is not MFMA-sized (multiples of 128)")
+            return 0
+        module.__class__ = MfmaSyntheticMLP
+        module.__dict__["_dgt_in_place"] = grad_in_place
+        return len(linears)
+    if type(module) is nn.Sequential:
+        module.__class__ = MfmaSequential
+        linears, relus, head = module._spec()
+        if head is not None:
+            module.__dict__["_dgt_in_place"] = grad_in_place
+            return len(linears)
+        module.__class__ = nn.Sequential  # not a chain: look inside instead
+        module.__dict__.pop("_dgt_spec", None)
+    n = 0
+    for child in module.children():
+        n += inject_mfma_linear(child, grad_in_place)
+    if n == 0 and type(module) is nn.Linear:
+        count_fallback(f"bf16 Linear({module.in_features}, {module.out_features}) outside a recognised chain")
+    return n

@@ -109,10 +109,11 @@ class FlatParamStore:
                 self.grad_views.append(self.grad_buf[off:off + n].view(shape))
                 p.grad = self.grad_views[-1]
 
-    def rebind_grads(self) -> None:
+    def rebind_grads(self) -> bool:
         """Re-attach gradient views (after user code set ``.grad = None``).  Called every backward:
         the common case (every .grad still IS its cached view) costs one identity test per
-        parameter, not a slice per parameter."""
+        parameter, not a slice per parameter.  Returns True if a user-set gradient was folded in."""
+        folded = False
         for p, view in zip(self.params, self.grad_views):
             g = p.grad
             if g is view:
@@ -121,7 +122,9 @@ class FlatParamStore:
                 continue  # an equivalent view of the same storage
             if g is not None:  # user replaced the grad tensor: fold it back in
                 view.copy_(g)
+                folded = True
             p.grad = view
+        return folded
 
     def zero_grad(self) -> None:
         self.grad_buf.zero_()

@@ -124,7 +124,7 @@ class GraphedStep:
         e.store.grad_buf.zero_()
         loss = self.loss_fn(*args)
         from ..ops.linear import engine_backward
-        with engine_backward():
+        with engine_backward(grads_zero=True):  # zeroed just above
             loss.float().backward(self._seed(loss))
         grads = self._reduce()
         scale = 1.0 / e.world_size

@@ -18,19 +18,19 @@ One optimizer step, all on the GPU, no host sync:
 
 Schedules (``schedule=`` or ``DGT_MLP_SCHEDULE``):
 
-* ``"flat"`` (default for N = 1): after backward, ONE Adam launch over every weight, then the
-  transposes;
+* ``"flat"``: after backward, ONE Adam launch over every weight (one rank: each layer's wgrad GEMM
+  applies Adam in its epilogue instead, ``gemm_nt_adam_``, so no gradient reaches memory);
 * ``"overlap"`` (default for N > 1): layer l's update runs on a side HIP stream as soon as its
-  collective has landed and backward no longer reads W_l^T, so the Adam of the upper layers
+  collective has landed and backward no longer reads W_l, so the Adam of the upper layers
   overlaps the collectives of the lower ones and only the first layer's update is left after
   the last collective; the next step's forward GEMM of layer l waits only on layer l's event;
 * ``"serial"``: the same per-layer updates on the main stream after backward.
 
 On one GPU the overlap does not pay: a streaming Adam running beside the backward GEMMs slows
 them by as much as it hides (dgrad 49 -> 70 us, profiles/r1_mlp_schedule_ab.txt) — the GEMMs at
-M = 1024 are bound by the L2/fabric, not by MFMA.  ``DGT_ADAM_MATRIX_T=1`` swaps the per-layer
-Adam + transpose for one kernel that writes W_l and W_l^T in the same pass (adam_matrix_t:
-correct, but its row-piece access pattern measured slower than flat Adam + transpose).
+M = 1024 are bound by the L2/fabric, not by MFMA.  (The round-1/2 A/B switches -- a refreshed W^T
+for the dgrad, an Adam kernel writing W and W^T, a side-stream wgrad + Adam, GEMM variants -- were
+measured slower or no better and removed; their records stay in profiles/.)
 
 Parameters live in two flat regions:
 
@@ -46,6 +46,12 @@ Parameters live in two flat regions:
 * the small region — biases and the head, fp32 (the GEMM epilogues read fp32 biases), replicated
   on every rank and all-reduced as one bucket.
 
+Checkpoints (``save_checkpoint`` / ``load_checkpoint``) use the DeepSpeed layout of
+``runtime/checkpoint.py``: the module's fp32 weights and, for ZeRO-0, the Adam state in torch's
+per-parameter format in ``mp_rank_00_model_states.pt``; for ZeRO-1 each rank's fp32 master and
+moment shards of the weight buckets in ``zero_pp_rank_{r}_mp_rank_00_optim_states.pt`` (bucket
+format, so ``zero_to_fp32.py`` consolidates them), with the replicated small region alongside.
+
 ``zero_stage=0``: every rank keeps the full fp32 master of the big region; its buckets are
 all-reduced and one Adam launch updates everything.  ``zero_stage=1`` (DeepSpeed ZeRO-1/2 for the
 matrices): each bucket is REDUCE-SCATTERED into this rank's gradient shard, Adam updates
@@ -57,7 +63,6 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
-import contextlib
 import os
 
 import torch
@@ -65,9 +70,10 @@ import torch.distributed as dist
 
 from ..accelerator import get_accelerator
 from ..models.synthetic_mlp import SyntheticMLP, synthetic_batch_data
-from ..ops.adam import adam_flat_, adam_matrix_t_
+from ..ops.adam import adam_flat_
 from ..ops.gemm import gemm_nt, gemm_nt_adam_, mlp_head, rowsum_bf16, transpose_bf16
 from ..parallel import comm
+from . import checkpoint as ckpt
 
 ALIGN = 64
 SCHEDULES = ("overlap", "serial", "flat")
@@ -104,7 +110,6 @@ class MLPTrainer:
             raise ValueError(f"schedule must be one of {SCHEDULES} or 'auto'")
         if schedule == "auto":  # measured (profiles/r1_mlp_schedule_ab.txt): see the module docstring
             schedule = "flat" if comm.get_world_size() == 1 else "overlap"
-        self.matrix_t = os.environ.get("DGT_ADAM_MATRIX_T", "0") == "1"
         self.device = device or get_accelerator().device()
         self.model = model
         self.B, self.D, self.L, self.Din = batch_size, model.width, model.depth, model.in_features
@@ -180,41 +185,20 @@ class MLPTrainer:
         self.gb = [sview(self.grads_s, f"layers.{i}.bias") for i in range(self.L)]
         self.hw, self.hb = sview(self.master_s, "head.weight"), sview(self.master_s, "head.bias")
         self.ghw, self.ghb = sview(self.grads_s, "head.weight"), sview(self.grads_s, "head.bias")
-        # dgrad g_{l-1} = g_l . W_l: by default the GEMM reads W_l[out, in] as a [K, N] operand
-        # through transposed LDS reads (gemm_nt(..., b_kn=True)), so no W^T exists at all;
-        # DGT_MLP_DGRAD=nt keeps a refreshed bf16 W_l^T and the plain NT kernel (A/B baseline).
-        # W_l^T would feed the dgrad of layer l > 0 only (the input needs no gradient): no W_0^T.
-        self.dgrad_kn = os.environ.get("DGT_MLP_DGRAD", "kn") != "nt"
-        self.WT = [None] * self.L
-        if not self.dgrad_kn:
-            self.WT = [None] + [torch.empty(w.shape[1], w.shape[0], dtype=torch.bfloat16, device=dev)
-                                for w in self.W[1:]]
-        self._refresh_transposes()
+        # dgrad g_{l-1} = g_l . W_l: the GEMM reads W_l[out, in] as a [K, N] operand through
+        # transposed LDS reads (gemm_nt(..., b_kn=True)), so no W^T exists at all
         # single rank, ZeRO-0: nothing reduces the weight gradients, so each wgrad GEMM applies Adam
         # to its tile in its epilogue (gemm_nt_adam_) and no gradient ever reaches memory
         if fuse_adam is None:
             fuse_adam = os.environ.get("DGT_MLP_FUSED_ADAM", "1") != "0"
-        self.fused_adam = bool(fuse_adam and dev.type == "cuda" and not self.coll and self.zero_stage == 0
-                               and self.dgrad_kn and not self.matrix_t)
-        # kernel for the fused wgrad+Adam (0 = by shape: 256^2 tiles at 4096^2).  Alone, 128^2 tiles
-        # at 2 blocks per CU overlap one block's Adam epilogue with the other's K loop best (94.7 us
-        # vs 100.2 vs 118.6 unfused, profiles/r2_wgrad_adam.jsonl); inside the step they lose
-        # (1178 vs 1283 it/s, profiles/r2_mlp_fused_adam_ab.txt), so the default stays shape-picked
-        self.fused_variant = int(os.environ.get("DGT_MLP_FUSED_VARIANT", "0"))
-        # kernel for the forward and dgrad products (0 = by shape; 7 = BK 128 per barrier)
-        self.gemm_variant = int(os.environ.get("DGT_MLP_GEMM_VARIANT", "0"))
-        # DGT_MLP_FUSED_SIDE=1: each layer's wgrad + Adam launch runs on a side stream beside the
-        # next layer's dgrad (a third gradient buffer keeps the dgrad from overwriting the g^T the
-        # side launch still reads); the next step's forward GEMM of layer l waits on layer l's update
-        self.fused_side = self.fused_adam and os.environ.get("DGT_MLP_FUSED_SIDE", "0") == "1" and self.L > 1
+        self.fused_adam = bool(fuse_adam and dev.type == "cuda" and not self.coll and self.zero_stage == 0)
 
         # ---- activations (both layouts) and gradient scratch
         B, D = self.B, self.D
         self.a = [None] + [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(self.L)]
         self.aT = [None] + [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(self.L)]
-        nbuf = 3 if self.fused_side else 2
-        self.g = [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(nbuf)]
-        self.gT = [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(nbuf)]
+        self.g = [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        self.gT = [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(2)]
         self.dz = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
 
@@ -235,22 +219,7 @@ class MLPTrainer:
         self._overlap = self.schedule == "overlap"
         self._opt_pending = False
         self.s_main = None
-        # "flat" on GPU: the W^T refresh runs on a side stream beside the next step's forward GEMMs
-        # (only the dgrads read W^T); DGT_MLP_T_SIDE=0 keeps it on the main stream
-        self._t_side = (self.schedule == "flat" and dev.type == "cuda" and not self.dgrad_kn
-                        and os.environ.get("DGT_MLP_T_SIDE", "1") == "1" and self.L > 1)
-        self._t_pending = False
-        if self._t_side:
-            self.s_t = torch.cuda.Stream(dev)
-            self.ev_adam = torch.cuda.Event()
-            self.ev_t = [torch.cuda.Event() for _ in range(self.L)]
-        if self.fused_side:
-            self.s_opt = torch.cuda.Stream(dev)
-            self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
-            self.ev_opt = [torch.cuda.Event() for _ in range(self.L)]
         if self._overlap:
-            if os.environ.get("DGT_MLP_PRIO", "0") == "1":  # GEMM stream ahead of the optimizer stream
-                self.s_main = torch.cuda.Stream(dev, priority=-1)
             self.s_opt = torch.cuda.Stream(dev)
             self.s_comm = torch.cuda.Stream(dev)
             self.ev_wgrad = [torch.cuda.Event() for _ in range(self.L)]
@@ -259,13 +228,6 @@ class MLPTrainer:
             self.ev_opt = [torch.cuda.Event() for _ in range(self.L)]
 
     # ------------------------------------------------------------------ helpers
-    def _refresh_transposes(self):
-        # W_0^T is never read (layer 0 has no dgrad: the input needs no gradient)
-        if self.dgrad_kn:
-            return
-        for i in range(1, self.L):
-            transpose_bf16(self.W[i], self.WT[i])
-
     def flops_per_step(self) -> int:
         return self.model.flops_per_sample() * self.B
 
@@ -314,16 +276,10 @@ class MLPTrainer:
         return (self.global_steps, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, False)
 
     def _update_layer(self, i: int) -> None:
-        """Adam on layer i's weights (its shard under ZeRO-1) + refresh of the bf16 W_i and W_i^T."""
+        """Adam on layer i's weights (its shard under ZeRO-1) + refresh of the bf16 W_i."""
         args, scale = self._adam_args(), 1.0 / self.world_size
         if self.zero_stage == 0:
-            R, Cc = self.shapes[i]
             o = self.w_off[i]
-            if self.matrix_t and not self.dgrad_kn and i > 0 and R % 64 == 0 and Cc % 128 == 0:
-                sl = slice(o, o + R * Cc)
-                adam_matrix_t_(self.master_w[sl], self.params_bf16[sl], self.WT[i], self.grads_w[sl], self.m_w[sl],
-                               self.v_w[sl], R, Cc, *args, grad_scale=scale)
-                return
             sl = slice(o, o + self.w_len[i])
             adam_flat_(self.master_w[sl], self.grads_w[sl], self.m_w[sl], self.v_w[sl], *args, grad_scale=scale,
                        param_lp=self.params_bf16[sl])
@@ -336,14 +292,9 @@ class MLPTrainer:
             self._collective(dist.all_gather_into_tensor, out, self.lp_w[sl], works=works)
             for w in works:
                 w.wait()
-        if i > 0 and not self.dgrad_kn:  # W_0^T is never read
-            transpose_bf16(self.W[i], self.WT[i])
 
     def join(self) -> None:
         """Make the caller's stream wait for the side streams (results visible to later work)."""
-        if self._t_pending:
-            torch.cuda.current_stream(self.device).wait_stream(self.s_t)
-            self._t_pending = False
         if self._opt_pending:
             cur = torch.cuda.current_stream(self.device)
             cur.wait_stream(self.s_opt)
@@ -359,14 +310,13 @@ class MLPTrainer:
         xT = self.XT[:, j * B:(j + 1) * B]
         y = self.Y[j * B:(j + 1) * B]
         ov = self._overlap
-        main = torch.cuda.current_stream(self.device) if (ov or self.fused_side) else None
+        main = torch.cuda.current_stream(self.device) if ov else None
         # forward: layer i waits only on its own update of the previous step
         prev = x
         for i in range(L):
             if self._opt_pending:
                 main.wait_event(self.ev_opt[i])
-            gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True,
-                    variant=self.gemm_variant)
+            gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True)
             prev = self.a[i + 1]
         # head (+ its gradients, written in place: no zero fills)
         cur = 0
@@ -397,13 +347,7 @@ class MLPTrainer:
                 else:
                     self._reduce_layer(i, works)
             if i > 0:
-                if self._t_pending:
-                    torch.cuda.current_stream(self.device).wait_event(self.ev_t[i])
-                if self.dgrad_kn:
-                    gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True,
-                            variant=self.gemm_variant)
-                else:
-                    gemm_nt(self.g[cur], self.WT[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i])
+                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True)
                 cur ^= 1
             if ov:
                 self.ev_bwd[i].record(main)
@@ -424,23 +368,12 @@ class MLPTrainer:
         elif self.schedule == "serial":
             for i in reversed(range(L)):
                 self._update_layer(i)
-        else:  # "flat": one Adam launch over every weight, then the all-gather and the transposes
+        else:  # "flat": one Adam launch over every weight, then the all-gather
             grads_w = self.grads_w if self.zero_stage == 0 else self.shard_grad
             adam_flat_(self.master_w, grads_w, self.m_w, self.v_w, *self._adam_args(),
                        grad_scale=1.0 / self.world_size, param_lp=self.lp_w)
             if self.zero_stage == 1:
                 self._allgather_params()
-            if self._t_side:
-                main_s = torch.cuda.current_stream(self.device)
-                self.ev_adam.record(main_s)
-                self.s_t.wait_event(self.ev_adam)
-                with torch.cuda.stream(self.s_t):
-                    for i in reversed(range(1, L)):  # the order the next backward reads them
-                        transpose_bf16(self.W[i], self.WT[i])
-                        self.ev_t[i].record(self.s_t)
-                self._t_pending = True
-            else:
-                self._refresh_transposes()
 
     def _backward_fused_adam(self, xT: torch.Tensor, cur: int) -> None:
         """Single-rank backward + update: per layer, the bias-gradient row sums, the dgrad (it
@@ -449,35 +382,133 @@ class MLPTrainer:
         region moves 26 B/param (12 read + 14 written) instead of the wgrad store + flat Adam's
         2 + 28 B/param, and the update overlaps the other blocks' MFMA work."""
         args = self._adam_args()
-        side = self.fused_side
-        main = torch.cuda.current_stream(self.device) if side else None
-        nbuf = len(self.g)
         for i in reversed(range(self.L)):
             a_prevT = xT if i == 0 else self.aT[i]
-            nxt = (cur + 1) % nbuf
             rowsum_bf16(self.gT[cur], self.gb[i])
             if i > 0:
-                if side and i + 2 < self.L:  # the buffer written now was read by layer i + 2's update
-                    main.wait_event(self.ev_opt[i + 2])
-                gemm_nt(self.g[cur], self.W[i], C=self.g[nxt], CT=self.gT[nxt], mask=self.a[i], b_kn=True,
-                        variant=self.gemm_variant)
+                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True)
             R, Cc = self.shapes[i]
-            o = self.w_off[i]
-            sl = slice(o, o + R * Cc)
-            with (torch.cuda.stream(self.s_opt) if side else contextlib.nullcontext()):
-                if side:  # W_i is rewritten below: after its dgrad (and the rows it reads) on main
-                    self.ev_bwd[i].record(main)
-                    self.s_opt.wait_event(self.ev_bwd[i])
-                gemm_nt_adam_(self.gT[cur], a_prevT, self.master_w[sl].view(R, Cc), self.m_w[sl].view(R, Cc),
-                              self.v_w[sl].view(R, Cc), self.params_bf16[sl].view(R, Cc), *args,
-                              grad_scale=1.0 / self.world_size, variant=self.fused_variant)
-                if side:
-                    self.ev_opt[i].record(self.s_opt)
+            sl = slice(self.w_off[i], self.w_off[i] + R * Cc)
+            gemm_nt_adam_(self.gT[cur], a_prevT, self.master_w[sl].view(R, Cc), self.m_w[sl].view(R, Cc),
+                          self.v_w[sl].view(R, Cc), self.params_bf16[sl].view(R, Cc), *args,
+                          grad_scale=1.0 / self.world_size)
             if i > 0:
-                cur = nxt
+                cur ^= 1
         adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *args, grad_scale=1.0 / self.world_size)
-        if side:
-            self._opt_pending = True
+
+    # ------------------------------------------------------------------ checkpoints
+    def _param_names(self) -> List[str]:
+        return [n for n, _ in self.model.named_parameters()]
+
+    def _full_fp32(self, name: str) -> torch.Tensor:
+        """A parameter's current fp32 value (the master where this rank holds it whole)."""
+        p = dict(self.model.named_parameters())[name]
+        if name.startswith("layers.") and name.endswith("weight"):
+            i = int(name.split(".")[1])
+            src = self.master_w if self.zero_stage == 0 else self.params_bf16
+            return src[self.w_off[i]:self.w_off[i] + p.numel()].float().view(p.shape)
+        o = self.s_off[name]
+        return self.master_s[o:o + p.numel()].view(p.shape)
+
+    def _moments(self, name: str):
+        p = dict(self.model.named_parameters())[name]
+        if name.startswith("layers.") and name.endswith("weight"):
+            i = int(name.split(".")[1])
+            o = self.w_off[i]
+            return self.m_w[o:o + p.numel()].view(p.shape), self.v_w[o:o + p.numel()].view(p.shape)
+        o = self.s_off[name]
+        return self.m_s[o:o + p.numel()].view(p.shape), self.v_s[o:o + p.numel()].view(p.shape)
+
+    def _zero_shard(self) -> Dict:
+        names = [f"layers.{i}.weight" for i in range(self.L)]
+        return {
+            "zero_stage": 1,
+            "partition_rank": self.rank,
+            "partition_world_size": self.world_size,
+            "buckets": [[self.w_off[i], self.w_len[i]] for i in range(self.L)],
+            "offsets": list(self.w_off),
+            "shapes": [list(self.shapes[i]) for i in range(self.L)],
+            "names": names,
+            "total": self.total_w,
+            "fp32_flat": self.master_w.detach().cpu().clone(),
+            "exp_avg": self.m_w.detach().cpu().clone(),
+            "exp_avg_sq": self.v_w.detach().cpu().clone(),
+            "small": {"master": self.master_s.detach().cpu().clone(), "exp_avg": self.m_s.detach().cpu().clone(),
+                      "exp_avg_sq": self.v_s.detach().cpu().clone(), "offsets": dict(self.s_off)},
+            "step": self.global_steps,
+            "param_groups": [{"lr": self.lr, "betas": list(self.betas), "eps": self.eps,
+                              "weight_decay": self.weight_decay, "adamw": False}],
+        }
+
+    def save_checkpoint(self, save_dir: str, tag: Optional[str] = None, client_state: Optional[dict] = None,
+                        ds_config: Optional[dict] = None) -> str:
+        """DeepSpeed-layout checkpoint of the current step (see the module docstring)."""
+        self.join()
+        names = self._param_names()
+        module = {n: self._full_fp32(n).detach().cpu().clone() for n in names}
+        optimizer = None
+        if self.zero_stage == 0:
+            state = {}
+            if self.global_steps > 0:
+                for i, n in enumerate(names):
+                    m, v = self._moments(n)
+                    state[i] = {"step": torch.tensor(float(self.global_steps)), "exp_avg": m.detach().cpu().clone(),
+                                "exp_avg_sq": v.detach().cpu().clone()}
+            optimizer = {"state": state, "param_groups": [{
+                "lr": self.lr, "betas": tuple(self.betas), "eps": self.eps, "weight_decay": self.weight_decay,
+                "amsgrad": False, "maximize": False, "foreach": None, "capturable": False, "differentiable": False,
+                "fused": None, "params": list(range(len(names)))}]}
+        return ckpt.save(save_dir, tag, self.global_steps, module, optimizer,
+                         {"global_samples": self.global_steps * self.B * self.world_size,
+                          "dp_world_size": self.world_size, "client_state": client_state or {}},
+                         ds_config or {}, zero_shard=self._zero_shard() if self.zero_stage == 1 else None)
+
+    def load_checkpoint(self, load_dir: str, tag: Optional[str] = None, load_optimizer_states: bool = True):
+        """Restore masters, bf16 compute copies, moments and the step from ``save_checkpoint``'s layout."""
+        path, states, shard = ckpt.load(load_dir, tag)
+        if states is None:
+            return None, None
+        self.join()
+        names = self._param_names()
+        sd = states["module"]
+        dev = self.device
+        with torch.no_grad():
+            for i in range(self.L):
+                w = sd[f"layers.{i}.weight"].reshape(-1).float().to(dev)
+                n = w.numel()
+                self.params_bf16[self.w_off[i]:self.w_off[i] + n].copy_(w.to(torch.bfloat16))
+                if self.zero_stage == 0:
+                    self.master_w[self.w_off[i]:self.w_off[i] + n].copy_(w)
+            for n in names:
+                if n in self.s_off:
+                    o = self.s_off[n]
+                    v = sd[n].reshape(-1).float().to(dev)
+                    self.master_s[o:o + v.numel()].copy_(v)
+            self.m_w.zero_(), self.v_w.zero_(), self.m_s.zero_(), self.v_s.zero_()
+            if self.zero_stage == 1:
+                if shard is None:
+                    raise FileNotFoundError(f"missing ZeRO-1 shard for rank {self.rank} under {path}")
+                if int(shard["partition_world_size"]) != self.world_size or int(shard["total"]) != self.total_w:
+                    raise RuntimeError("ZeRO-1 checkpoint was written with a different world size / model; "
+                                       "consolidate it with zero_to_fp32.py and load the fp32 weights instead")
+                self.master_w.copy_(shard["fp32_flat"].to(dev))
+                self.lp_w.copy_(self.master_w.to(torch.bfloat16))
+                if load_optimizer_states:
+                    self.m_w.copy_(shard["exp_avg"].to(dev))
+                    self.v_w.copy_(shard["exp_avg_sq"].to(dev))
+                    self.m_s.copy_(shard["small"]["exp_avg"].to(dev))
+                    self.v_s.copy_(shard["small"]["exp_avg_sq"].to(dev))
+                self._allgather_params()  # the bf16 compute copy from the exact fp32 shards
+            elif load_optimizer_states and states.get("optimizer"):
+                st = states["optimizer"]["state"]
+                for i, n in enumerate(names):
+                    e = st.get(i, st.get(str(i)))
+                    if e:
+                        m, v = self._moments(n)
+                        m.copy_(e["exp_avg"].reshape(m.shape).to(dev))
+                        v.copy_(e["exp_avg_sq"].reshape(v.shape).to(dev))
+        self.global_steps = int(states.get("global_steps", 0))
+        return path, states.get("client_state", {})
 
     # bench.py adapter (same surface as TinyMLPTrainer)
     def epoch_plan(self, epoch: int):

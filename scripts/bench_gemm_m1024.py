@@ -23,7 +23,7 @@ CT = torch.empty(N, M, device="cuda", dtype=torch.bfloat16)
 bias = torch.randn(N, device="cuda")
 mask = (torch.randn(M, N, device="cuda") > 0).bfloat16()
 arms = {}
-for v in [int(x) for x in os.environ.get("VARIANTS", "4,5,7,8").split(",")]:
+for v in [int(x) for x in os.environ.get("VARIANTS", "1,4").split(",")]:
     arms[f"fwd plain v{v}"] = lambda v=v: gemm_nt(a, w, C=C, variant=v)
     arms[f"fwd bias+relu+T v{v}"] = lambda v=v: gemm_nt(a, w, C=C, CT=CT, bias=bias, relu=True, variant=v)
     arms[f"dgrad [K,N] mask+T v{v}"] = lambda v=v: gemm_nt(g, w, C=C, CT=CT, mask=mask, b_kn=True, variant=v)

@@ -346,3 +346,85 @@ def test_graph_module_keeps_buffers_and_rng_and_guards_double_forward():
     torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
     for u, v in zip(b1, b2):
         torch.testing.assert_close(u.float(), v.float(), rtol=1e-5, atol=1e-6)
+
+
+def _bf16_mlp_engine(fused, seed=41, width=512, depth=3, B=256, steps=4, extra=None):
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.runtime.engine_mlp import EngineMLPTrainer
+    torch.manual_seed(seed)
+    cfg = {"train_micro_batch_size_per_gpu": B, "bf16": {"enabled": True},
+           "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "amd": {"fused_linear": fused}, **(extra or {})}
+    tr = EngineMLPTrainer(SyntheticMLP(width, depth), B, 4, cfg)
+    losses = []
+    for _ in range(steps):
+        tr.loss_acc.zero_()
+        tr.run_plan(*[t[:1] for t in tr.epoch_plan(1)])
+        losses.append(float(tr.loss_acc.item()))
+    return tr, losses
+
+
+@pytest.mark.gpu
+def test_engine_bf16_mfma_chain_matches_autograd_engine():
+    """a bf16 engine injects the MFMA Linear chain (every Linear incl. the head) and
+    follows the trajectory of the same engine on autograd + F.linear within bf16 tolerance."""
+    a, la = _bf16_mlp_engine(True)
+    b, lb = _bf16_mlp_engine(False)
+    assert a.engine.fused_linear_layers == 4 and b.engine.fused_linear_layers == 0
+    torch.testing.assert_close(torch.tensor(la), torch.tensor(lb), rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(a.engine.master, b.engine.master, rtol=0, atol=2e-3)
+    assert not a.engine.linear_fallbacks or all("MFMA" not in k for k in a.engine.linear_fallbacks)
+    a.close()
+    b.close()
+
+
+@pytest.mark.gpu
+def test_engine_bf16_gradient_accumulation_uses_accumulating_epilogue():
+    """gas = 2: the second micro-step's wgrad / bias row sums accumulate into the bf16 bucket; the
+    trajectory still follows the autograd engine."""
+    extra = {"gradient_accumulation_steps": 2}
+    a, la = _bf16_mlp_engine(True, steps=4, extra=extra)
+    b, lb = _bf16_mlp_engine(False, steps=4, extra=extra)
+    assert a.engine.global_steps == 2
+    torch.testing.assert_close(torch.tensor(la), torch.tensor(lb), rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(a.engine.master, b.engine.master, rtol=0, atol=2e-3)
+    a.close()
+    b.close()
+
+
+@pytest.mark.gpu
+def test_engine_bf16_step_runs_no_vendor_gemm():
+    """The bf16 engine step launches this framework's GEMM / head / Adam kernels and no hipBLASLt
+    (Cijk_*) or rocBLAS kernel (torch profiler kernel names of two steps)."""
+    from torch.profiler import ProfilerActivity, profile
+    tr, _ = _bf16_mlp_engine(True, steps=1)
+    with profile(activities=[ProfilerActivity.CUDA]) as prof:
+        tr.run_plan(*tr.epoch_plan(1))
+        torch.cuda.synchronize()
+    names = [e.key for e in prof.key_averages()]
+    assert any("gemm_nt_kernel" in n for n in names), names
+    assert any("skinny" in n for n in names) and any("adam_flat" in n for n in names), names
+    vendor = [n for n in names if n.startswith("Cijk") or "rocblas" in n.lower() or "gemv" in n.lower()]
+    assert not vendor, vendor
+    tr.close()
+
+
+@pytest.mark.gpu
+def test_engine_bf16_matches_mlp_trainer():
+    """The DeepSpeed-API path and the bench trainer (MLPTrainer) on the same model, data and Adam:
+    same trajectory within bf16 tolerance (the engine keeps bf16 biases, MLPTrainer fp32 ones)."""
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
+    eng, le = _bf16_mlp_engine(True, seed=43, steps=3)
+    torch.manual_seed(43)
+    mt = MLPTrainer(SyntheticMLP(512, 3), batch_size=256, n_batches=4, lr=1e-3, device=torch.device("cuda"))
+    lm = []
+    for _ in range(3):
+        mt.loss_acc.zero_()
+        mt.run_plan(*[t[:1] for t in mt.epoch_plan(1)])
+        lm.append(float(mt.loss_acc.item()))
+    torch.testing.assert_close(torch.tensor(le), torch.tensor(lm), rtol=2e-2, atol=2e-3)
+    for i in range(3):
+        w_eng = eng.engine.module.layers[i].weight.detach().float()
+        w_mt = mt.W[i].float()
+        torch.testing.assert_close(w_eng, w_mt, rtol=0, atol=4e-3)
+    eng.close()

@@ -173,3 +173,25 @@ def test_train_py_fused_profile_trace(tmp_path):
     assert "impl=fused" in r.stderr
     text = (tmp_path / "prof" / "trace_rank0.json").read_text()
     assert "tiny_mlp_train_kernel" in text
+
+
+@pytest.mark.parametrize("impl", ["auto", "engine"])
+def test_train_py_model_mlp_saves_and_resumes_on_gpu(tmp_path, impl):
+    """BASELINE config #2 as a train.py job on the GPU: MLPTrainer (auto) or the
+    engine's MFMA chain saves DeepSpeed-layout checkpoints every epoch and --resume continues to the
+    uninterrupted run's epoch loss."""
+    common = ["--model", "mlp", "--width", "512", "--depth", "2", "--mlp-batches", "4", "--impl", impl]
+    cfg = tmp_path / "mlp.json"
+    cfg.write_text(json.dumps({"train_micro_batch_size_per_gpu": 256, "bf16": {"enabled": True},
+                               "communication_data_type": "fp32", "zero_optimization": {"stage": 0},
+                               "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}}))
+    full = _train(*common, "--epochs", "3", "--deepspeed_config", str(cfg), "--save-dir", str(tmp_path / "a"))
+    assert full.returncode == 0, full.stderr[-3000:]
+    lf = _losses(full.stdout)
+    assert len(lf) == 3 and lf[2] < lf[0]
+    part = _train(*common, "--epochs", "2", "--deepspeed_config", str(cfg), "--save-dir", str(tmp_path / "b"))
+    assert part.returncode == 0, part.stderr[-3000:]
+    res = _train(*common, "--epochs", "3", "--resume", "--deepspeed_config", str(cfg), "--save-dir",
+                 str(tmp_path / "b"))
+    assert res.returncode == 0, res.stderr[-3000:]
+    assert _losses(res.stdout) == lf[2:], (res.stdout, lf)

@@ -191,3 +191,54 @@ def test_exchange_fallback_strict_fails_cpu():
     assert r.returncode != 0, r.stderr[-2000:]  # the workers exit 2; torchrun reports the failure
     assert "[dgt] FATAL" in r.stderr and "replicas diverged" in r.stderr and "exitcode  : 2" in r.stderr
     assert "Training completed." not in r.stdout
+
+
+def _mlp_cfg(tmp_path, stage):
+    p = tmp_path / f"mlp_z{stage}.json"
+    p.write_text(json.dumps({"train_micro_batch_size_per_gpu": 64, "gradient_accumulation_steps": 1,
+                             "bf16": {"enabled": True}, "communication_data_type": "fp32",
+                             "zero_optimization": {"stage": stage},
+                             "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}}))
+    return str(p)
+
+
+def test_train_py_model_mlp_zero1_checkpoint_resume_consolidate(tmp_path):
+    """BASELINE config #2 as a train.py job: --model mlp runs MLPTrainer with the
+    DeepSpeed JSON's micro-batch / ZeRO stage, saves DeepSpeed-layout checkpoints every epoch and
+    resumes from them bit-exactly; the ZeRO-1 shards consolidate (zero_to_fp32) to exactly the
+    ZeRO-0 run's fp32 masters."""
+    import torch
+    from distributed_gpu_test_amd.utils.zero_to_fp32 import consolidate
+    common = ["--model", "mlp", "--width", "128", "--depth", "2", "--mlp-batches", "4"]
+    full = {}
+    for stage in (0, 1):
+        r = run(2, *common, "--epochs", "3", "--deepspeed_config", _mlp_cfg(tmp_path, stage),
+                "--save-dir", str(tmp_path / f"full{stage}"))
+        assert r.returncode == 0, r.stderr[-3000:]
+        full[stage] = epoch_losses(r.stdout)
+        assert len(full[stage]) == 3 and full[stage][2] < full[stage][0]
+    assert full[0] == full[1]
+    z0 = torch.load(tmp_path / "full0" / "epoch3" / "global_step12" / "mp_rank_00_model_states.pt",
+                    weights_only=True)["module"]
+    tag1 = tmp_path / "full1" / "epoch3" / "global_step12"
+    assert (tag1 / "zero_pp_rank_1_mp_rank_00_optim_states.pt").exists()
+    cons = consolidate(str(tmp_path / "full1" / "epoch3"))
+    for k, v in z0.items():
+        assert torch.equal(cons[k], v), k
+    part = run(2, *common, "--epochs", "2", "--deepspeed_config", _mlp_cfg(tmp_path, 1),
+               "--save-dir", str(tmp_path / "part"))
+    assert part.returncode == 0, part.stderr[-3000:]
+    res = run(2, *common, "--epochs", "3", "--resume", "--deepspeed_config", _mlp_cfg(tmp_path, 1),
+              "--save-dir", str(tmp_path / "part"))
+    assert res.returncode == 0, res.stderr[-3000:]
+    assert epoch_losses(res.stdout) == full[1][2:]
+
+
+def test_train_py_model_mlp_engine_path(tmp_path):
+    """--model mlp --impl engine: the same model through initialize / backward / step."""
+    r = run(1, "--model", "mlp", "--width", "128", "--depth", "2", "--mlp-batches", "4", "--epochs", "2",
+            "--impl", "engine", "--deepspeed_config", _mlp_cfg(tmp_path, 0), "--save-dir", str(tmp_path / "e"))
+    assert r.returncode == 0, r.stderr[-3000:]
+    l = epoch_losses(r.stdout)
+    assert len(l) == 2 and l[1] < l[0]
+    assert (tmp_path / "e" / "epoch2" / "global_step8" / "mp_rank_00_model_states.pt").exists()

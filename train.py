@@ -65,12 +65,68 @@ def parse_args(argv=None):
     p.add_argument("--dist-timeout", type=float, default=1800.0)
     p.add_argument("--profile", default=None, help="write a torch.profiler (kineto) trace per rank to this dir "
                    "(every path; roctx ranges with DGT_ROCTX=1 name the phases / fused epoch launches)")
+    p.add_argument("--model", default="simple", choices=["simple", "mlp"],
+                   help="simple: the reference SimpleNet (default); mlp: the bench-size bf16 SyntheticMLP on the "
+                        "hand-written MFMA GEMMs (BASELINE config #2; default config configs/ds_bench_mlp_bf16.json)")
+    p.add_argument("--width", type=int, default=4096, help="mlp: hidden width")
+    p.add_argument("--depth", type=int, default=4, help="mlp: hidden layers")
+    p.add_argument("--mlp-batches", type=int, default=8, help="mlp: optimizer steps per epoch (per-rank batches)")
     p.add_argument("--strict-exchange", action="store_true",
                    help="fail the job (rc 2) on an in-kernel exchange timeout / replica divergence instead of "
                         "re-running the epoch on the RCCL path")
     p.add_argument("--debug-sync", action="store_true",
                    help="serialize kernels (AMD_SERIALIZE_KERNEL=3) and sync comm/compute streams: race hunting")
     return p.parse_known_args(argv)[0]
+
+
+def run_mlp(args, cfg, ds_config, world: int, local_rank: int) -> None:
+    """BASELINE config #2 as a train.py / SLURM job: the bench-size bf16 SyntheticMLP, per-rank
+    synthetic batches (weak scaling, as bench.py --model mlp), the DeepSpeed JSON's micro-batch,
+    Adam hyper-parameters, ZeRO stage and communication dtype, epoch loss lines and per-epoch
+    checkpoints in the reference's layout.  ``--impl auto`` runs MLPTrainer (hand-written MFMA
+    GEMMs, fused wgrad+Adam, per-layer RCCL buckets); ``--impl engine`` runs the same model through
+    ``initialize`` (the engine's bf16 MFMA Linear chain)."""
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
+    from distributed_gpu_test_amd.utils.tracing import Profiler
+    model = SyntheticMLP(args.width, args.depth)
+    B = cfg.train_micro_batch_size_per_gpu
+    o = cfg.optimizer
+    lr, betas, eps = (o.lr, tuple(o.betas), o.eps) if o is not None else (args.lr, (0.9, 0.999), 1e-8)
+    cdt = {"fp32": torch.float32, "float32": torch.float32, "bf16": torch.bfloat16, "bfloat16": torch.bfloat16,
+           None: None}[cfg.communication_data_type]
+    if args.impl == "engine":
+        from distributed_gpu_test_amd.runtime.engine_mlp import EngineMLPTrainer
+        trainer = EngineMLPTrainer(model, B, args.mlp_batches, ds_config)
+    else:
+        trainer = MLPTrainer(model, batch_size=B, n_batches=args.mlp_batches, lr=lr, betas=betas, eps=eps,
+                             zero_stage=cfg.zero_stage if cfg.zero_stage in (0, 1) else 0, comm_dtype=cdt)
+    over = oversubscribed(trainer.device)
+    if comm.get_rank() == 0:
+        print(f"[dgt] model=mlp impl={trainer.impl} width={args.width} depth={args.depth} micro_batch={B} "
+              f"zero_stage={getattr(trainer, 'zero_stage', cfg.zero_stage)} exchange={trainer.exchange} "
+              f"world_size={world} oversubscribed={over}", file=sys.stderr, flush=True)
+    start_epoch = 1
+    if args.resume:
+        found = newest_checkpoint(args.save_dir)
+        if found:
+            trainer.load_checkpoint(found[1])
+            start_epoch = found[0] + 1
+    plan, counts = trainer.epoch_plan(1)
+    prof = Profiler(args.profile, comm.get_rank())
+    with prof:
+        for epoch in range(start_epoch, args.epochs + 1):
+            trainer.loss_acc.zero_()
+            trainer.run_plan(plan, counts)
+            prof.step()
+            avg_loss = float(trainer.loss_acc.item()) / max(1, int(plan.shape[0]))
+            if local_rank == 0:
+                print(f"Epoch {epoch:2d} finished. Avg loss: {avg_loss:.4f}", flush=True)
+            if not args.no_save:
+                save_dir = os.path.join(args.save_dir, f"epoch{epoch}")
+                os.makedirs(save_dir, exist_ok=True)
+                trainer.save_checkpoint(save_dir, ds_config=cfg.to_dict())
+    trainer.close()
 
 
 def oversubscribed(device) -> bool:
@@ -105,10 +161,19 @@ def main(argv=None) -> int:
     if args.fail_at:
         os.environ["DGT_FAIL_AT"] = args.fail_at
 
+    if args.model == "mlp" and args.deepspeed_config is None:
+        args.deepspeed_config = os.path.join(ROOT, "configs", "ds_bench_mlp_bf16.json")
     ds_config = REFERENCE_DS_CONFIG if args.deepspeed_config is None else json.load(open(args.deepspeed_config))
     if args.debug_sync:
         ds_config = dict(ds_config, amd=dict(ds_config.get("amd", {}), debug_sync_streams=True))
     cfg = parse_config(ds_config, world)  # DeepSpeed's batch assertion on every path
+
+    if args.model == "mlp":
+        run_mlp(args, cfg, ds_config, world, local_rank)
+        if local_rank == 0:
+            print("Training completed.", flush=True)
+        faults.maybe_fire_end()
+        return 0
 
     x, y = make_synthetic_data(n_samples=N_SAMPLES, n_features=N_FEATURES, seed=args.seed)
     model = SimpleNet(n_features=x.shape[1], hidden=HIDDEN)
