@@ -621,10 +621,12 @@ void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor
   check_gpu(dW, "dW", at::kFloat);
   check_gpu(db, "db", at::kFloat);
   TORCH_CHECK(dW.numel() == N * K && db.numel() == N, "dgt: skinny_bwd dW [N, K] and db [N] (fp32)");
+  TORCH_CHECK(dW.is_contiguous(), "dgt: skinny_bwd dW must be contiguous");
   c10::DeviceGuard guard(a.device());
+  at::Tensor ws = at::empty({M / 64, N, K}, a.options().dtype(at::kFloat));  // per-row-tile dW partials
   DGT_CHECK_HIP(dgt::skinny_bwd_bf16(dz.data_ptr(), a.data_ptr(), W.data_ptr(), mask ? 1 : 0, g.data_ptr(), gTp,
-                                     dW.data_ptr<float>(), db.data_ptr<float>(), (int)M, (int)N, (int)K,
-                                     stream_of(a)));
+                                     dW.data_ptr<float>(), db.data_ptr<float>(), ws.data_ptr<float>(), (int)M,
+                                     (int)N, (int)K, stream_of(a)));
 }
 
 void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& y,
@@ -659,7 +661,7 @@ void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, co
   h.gT = gT.data_ptr();
   c10::DeviceGuard guard(a.device());
   // stream-ordered workspace from the caching allocator (reused in place on later calls)
-  at::Tensor scratch = at::empty({B}, dz.options());
+  at::Tensor scratch = at::empty({B + (B / 64) * D}, dz.options());
   h.scratch = scratch.data_ptr<float>();
   DGT_CHECK_HIP(dgt::mlp_head(h, stream_of(a)));
 }

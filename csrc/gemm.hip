@@ -206,13 +206,15 @@ DGT_DEVICE void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
 // threads whose waves own WM x WN sub-tiles: the MFMA layout gives each lane 4 rows of ONE column,
 // so direct stores are 2-byte scatters; staged, every global access (C rows, C^T rows, mask rows)
 // is a 16-byte vector and 16 lanes cover one 256-byte row piece.  The low 4 bits of a row's
-// 16-byte chunk index are XOR-swizzled by row / 8, so both the row reads (C) and the column reads
-// (C^T: 16 lanes at rows 8k + e of one column) hit 16 distinct bank groups.  Values are rounded to
+// 16-byte chunk index are XOR-swizzled by (row / 8) ^ bit 2 of the row, so the row reads (C: 16
+// lanes per row, row pairs never straddling a 4-row group), the column reads (C^T: 16 lanes at
+// rows 8k + e of one column) and the MFMA-layout writes (rows 4 apart in one 32-lane half, which
+// the row / 8 term alone put on one bank) all hit distinct bank groups.  Values are rounded to
 // bf16 once (after bias / ReLU) and masked after rounding (identical results: the mask only zeroes).
 template <int TN>
 DGT_DEVICE int etile(int r, int n) {
   const int c = n >> 3;
-  return r * TN + ((((c ^ (r >> 3)) & 15) | (c & ~15)) << 3) + (n & 7);
+  return r * TN + ((((c ^ (r >> 3) ^ ((r >> 2) & 1)) & 15) | (c & ~15)) << 3) + (n & 7);
 }
 
 // kEpiAdam epilogue: the block's fp32 gradient tile goes through LDS (the operand stages are idle)
@@ -873,17 +875,17 @@ hipError_t rowsum_bf16(const void* in, void* out, int out_bf16, int rows, int co
 // z[b] = a[b,:] . w + b0; loss += mean BCE; dz = (sigmoid(z) - y) / B;
 // g[b,:] = dz[b] * w * 1[a[b,:] > 0] (bf16, and g^T); dw = sum_b dz[b] a[b,:]; db = sum_b dz[b].
 // Kernel 1: one row per wave (every 16-byte load of the row in flight together) computes
-// z, dz and the row's loss term into a scratch vector, and zeroes dw.  No atomics: 1024 float /
-// double atomics on ONE address serialised at the L2 and made this kernel 19 us.
-// Kernel 2: one wave per 64 x 64 tile, 16-byte rows of a in, 16-byte rows of g and g^T out, dw
-// accumulated with one atomic per column per tile; tile (0, 0) also reduces dz -> db and the row
-// losses -> loss_acc in a fixed order (one atomic).
+// z, dz and the row's loss term into a scratch vector.  No atomics: 1024 float / double atomics
+// on ONE address serialised at the L2 and made this kernel 19 us.
+// Kernel 2: one wave per 64 x 64 tile, 16-byte rows of a in, 16-byte rows of g and g^T out, the
+// tile's dw partial stored to the workspace; tile (0, 0) also reduces dz -> db and the row losses
+// -> loss_acc in a fixed order (one atomic, one address, one launch: deterministic).
+// Kernel 3 (partials_reduce): dw = the tiles' partials summed in row-tile order.
 __global__ __launch_bounds__(256) void head_fwd_kernel(const u16* __restrict__ a, const float* __restrict__ w,
                                                        const float* __restrict__ b0, const float* __restrict__ y,
                                                        int B, int D, float* __restrict__ dz,
                                                        float* __restrict__ lrow, float* __restrict__ dw) {
   const int l = threadIdx.x & 63, wv = threadIdx.x >> 6;
-  for (int i = blockIdx.x * 256 + threadIdx.x; i < D; i += gridDim.x * 256) dw[i] = 0.f;
   constexpr int R = 1;
   const int row0 = blockIdx.x * 4 + wv * R;
   float s[R] = {0.f};
@@ -919,7 +921,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
                                                       const float* __restrict__ dz,
                                                       const float* __restrict__ lrow, int B, int D,
                                                       u16* __restrict__ g, u16* __restrict__ gT,
-                                                      float* __restrict__ dw, float* __restrict__ db,
+                                                      float* __restrict__ dw_part, float* __restrict__ db,
                                                       double* __restrict__ loss_acc) {
   // one wave per 64 x 64 tile; lane (rb, cg) owns the 8 x 8 block rows r0 + 8rb.., cols c0 + 8cg..:
   // eight 16-byte row loads of a, eight 16-byte g row stores (8 lanes = one 128-byte line) and
@@ -955,7 +957,8 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
     for (int q = 0; q < 4; ++q) o[q] = (unsigned)gb[2 * q][e] | ((unsigned)gb[2 * q + 1][e] << 16);
     *reinterpret_cast<uint4*>(gT + (long long)(c + e) * B + r) = make_uint4(o[0], o[1], o[2], o[3]);
   }
-  // dw: sum the 8 row-blocks (lanes cg, cg + 8, ..., cg + 56), one atomic per column per tile
+  // dw partial of the tile: sum the 8 row-blocks (lanes cg, cg + 8, ..., cg + 56) and store it at
+  // dw_part[row tile][column]; partials_reduce sums the tiles in order (no atomics: reproducible)
 #pragma unroll
   for (int e = 0; e < 8; ++e) {
     float x = part[e];
@@ -965,8 +968,9 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
     part[e] = x;
   }
   if (rb == 0) {
-#pragma unroll
-    for (int e = 0; e < 8; ++e) atomicAdd(&dw[c + e], part[e]);
+    float4* o = reinterpret_cast<float4*>(dw_part + (long long)blockIdx.y * D + c);
+    o[0] = make_float4(part[0], part[1], part[2], part[3]);
+    o[1] = make_float4(part[4], part[5], part[6], part[7]);
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && wv == 0) {  // db and the step's loss, in a fixed order
     float sd = 0.f, sl = 0.f;
@@ -990,9 +994,11 @@ hipError_t mlp_head(const HeadArgs& h, hipStream_t stream) {
   const int wpb = h.D % 256 == 0 ? 4 : 1;  // 4 tiles per block side by side when the width allows
   hipLaunchKernelGGL(head_bwd_kernel, dim3(h.D / (64 * wpb), h.B / 64), dim3(64 * wpb), 0, stream,
                      static_cast<const u16*>(h.a),
-                     h.w, h.dz, h.scratch, h.B, h.D, static_cast<u16*>(h.g), static_cast<u16*>(h.gT), h.dw, h.db,
-                     h.loss_acc);
-  return hipGetLastError();
+                     h.w, h.dz, h.scratch, h.B, h.D, static_cast<u16*>(h.g), static_cast<u16*>(h.gT),
+                     h.scratch + h.B, h.db, h.loss_acc);
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return partials_reduce(h.scratch + h.B, h.dw, h.B / 64, h.D, 0, stream);
 }
 
 }  // namespace dgt

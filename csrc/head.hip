@@ -5,8 +5,10 @@
 //   forward   z[M, N] = a[M, K] . W[N, K]^T + b     one wave per row, fp32 accumulation, bf16 out
 //   backward  g = (dz . W) * 1[a > 0] (+ g^T)       one wave per 64 x 64 tile of a, 8 x 8 per lane:
 //             dW += dz^T . a, db += sum dz          eight 16-B row loads of a, eight 16-B row stores
-//                                                   of g and eight of g^T per lane, no LDS; dW with
-//                                                   one fp32 atomic per column per tile
+//                                                   of g and eight of g^T per lane, no LDS; each tile
+//                                                   stores its dW partial, a second pass sums them in
+//                                                   row-tile order (no atomics: bit-reproducible, so a
+//                                                   resumed run replays the uninterrupted one exactly)
 // g (masked by the ReLU that produced a) and g^T are exactly the top hidden layer's pre-activation
 // gradient in both layouts, which its wgrad and dgrad GEMMs read next (csrc/gemm.hip).
 // Reference: the Linear(64, 1) output layer of train.py:32, widened (SyntheticMLP's head).
@@ -68,7 +70,7 @@ __global__ __launch_bounds__(256) void skinny_fwd_kernel(const u16* __restrict__
 template <int N>
 __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__ dz, const u16* __restrict__ a,
                                                          const u16* __restrict__ W, int mask, u16* __restrict__ g,
-                                                         u16* __restrict__ gT, float* __restrict__ dW,
+                                                         u16* __restrict__ gT, float* __restrict__ part_ws,
                                                          float* __restrict__ db, int M, int K) {
   const int l = threadIdx.x & 63, cg = l & 7, rb = l >> 3, wv = threadIdx.x >> 6;
   const int r = blockIdx.y * 64 + rb * 8, c = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + cg * 8;
@@ -115,7 +117,8 @@ __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__
       *reinterpret_cast<uint4*>(gT + (long long)(c + e) * M + r) = make_uint4(o[0], o[1], o[2], o[3]);
     }
   }
-  // dW: sum the 8 row-blocks of the tile (lanes cg, cg + 8, ..., cg + 56), one atomic per column
+  // dW partial of the tile: sum its 8 row-blocks (lanes cg, cg + 8, ..., cg + 56), stored at
+  // part_ws[row tile][n][column]
 #pragma unroll
   for (int n = 0; n < N; ++n)
 #pragma unroll
@@ -128,9 +131,11 @@ __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__
     }
   if (rb == 0) {
 #pragma unroll
-    for (int n = 0; n < N; ++n)
-#pragma unroll
-      for (int e = 0; e < 8; ++e) atomicAdd(&dW[(long long)n * K + c + e], part[n][e]);
+    for (int n = 0; n < N; ++n) {
+      float4* o = reinterpret_cast<float4*>(part_ws + ((long long)blockIdx.y * N + n) * K + c);
+      o[0] = make_float4(part[n][0], part[n][1], part[n][2], part[n][3]);
+      o[1] = make_float4(part[n][4], part[n][5], part[n][6], part[n][7]);
+    }
   }
   if (blockIdx.x == 0 && blockIdx.y == 0 && wv == 0) {  // db, in a fixed order
 #pragma unroll
@@ -138,9 +143,35 @@ __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__
       float s = 0.f;
       for (int i = l; i < M; i += 64) s += b2f(dz[(long long)i * N + n]);
       s = wave_sum(s);
-      if (l == 0) atomicAdd(&db[n], s);
+      if (l == 0) db[n] += s;
     }
   }
+}
+
+// out[i] (+)= sum over row tiles t (in order) of part[t][i], i < n
+__global__ __launch_bounds__(256) void partials_reduce_kernel(const float* __restrict__ part_ws,
+                                                              float* __restrict__ dW, int tiles, int nk, int acc) {
+  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i >= nk) return;
+  float4 s = *reinterpret_cast<const float4*>(part_ws + i);
+  for (int t = 1; t < tiles; ++t) {
+    const float4 p = *reinterpret_cast<const float4*>(part_ws + (long long)t * nk + i);
+    s.x += p.x, s.y += p.y, s.z += p.z, s.w += p.w;
+  }
+  float4* d = reinterpret_cast<float4*>(dW + i);
+  if (acc) {
+    const float4 o = *d;
+    s = make_float4(o.x + s.x, o.y + s.y, o.z + s.z, o.w + s.w);
+  }
+  *d = s;
+}
+
+hipError_t partials_reduce(const float* part, float* out, int tiles, int n, int accumulate, hipStream_t stream) {
+  if (n % 4 || tiles < 1 || ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out)) & 15))
+    return hipErrorInvalidValue;
+  hipLaunchKernelGGL(partials_reduce_kernel, dim3((n / 4 + 255) / 256), dim3(256), 0, stream, part, out, tiles, n,
+                     accumulate);
+  return hipGetLastError();
 }
 
 hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z, int M, int N, int K,
@@ -159,19 +190,21 @@ hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z,
 }
 
 hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, float* dW,
-                           float* db, int M, int N, int K, hipStream_t stream) {
+                           float* db, float* part_ws, int M, int N, int K, hipStream_t stream) {
   if (N < 1 || N > 4 || M % 64 || K % 64 || M <= 0 || K <= 0) return hipErrorInvalidValue;
   const int wpb = K % 256 == 0 ? 4 : 1;  // 4 tiles per block side by side when the width allows
   const dim3 grid(K / (64 * wpb), M / 64), blk(64 * wpb);
   const u16 *dp = static_cast<const u16*>(dz), *ap = static_cast<const u16*>(a), *wp = static_cast<const u16*>(W);
   u16 *gp = static_cast<u16*>(g), *gtp = static_cast<u16*>(gT);
   switch (N) {
-    case 1: hipLaunchKernelGGL(skinny_bwd_kernel<1>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, dW, db, M, K); break;
-    case 2: hipLaunchKernelGGL(skinny_bwd_kernel<2>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, dW, db, M, K); break;
-    case 3: hipLaunchKernelGGL(skinny_bwd_kernel<3>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, dW, db, M, K); break;
-    default: hipLaunchKernelGGL(skinny_bwd_kernel<4>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, dW, db, M, K);
+    case 1: hipLaunchKernelGGL(skinny_bwd_kernel<1>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, M, K); break;
+    case 2: hipLaunchKernelGGL(skinny_bwd_kernel<2>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, M, K); break;
+    case 3: hipLaunchKernelGGL(skinny_bwd_kernel<3>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, M, K); break;
+    default: hipLaunchKernelGGL(skinny_bwd_kernel<4>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, M, K);
   }
-  return hipGetLastError();
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return partials_reduce(part_ws, dW, M / 64, N * K, 1, stream);  // K % 64 == 0: whole float4 groups
 }
 
 }  // namespace dgt

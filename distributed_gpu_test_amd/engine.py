@@ -465,8 +465,14 @@ class Engine:
         g = self.optimizer.param_groups[0]
         if self.stage >= 1:
             raise RuntimeError("ZeRO optimizer state is sharded; see the zero_pp_rank_* checkpoint files")
-        return flat_to_adam_state(self.exp_avg, self.exp_avg_sq, self.layout.segments(), self.global_steps
-                                  - self.skipped_steps, g["lr"], g["betas"], g["eps"], g["weight_decay"], g["adamw"])
+        st = flat_to_adam_state(self.exp_avg, self.exp_avg_sq, self.layout.segments(), self.global_steps
+                                - self.skipped_steps, g["lr"], g["betas"], g["eps"], g["weight_decay"], g["adamw"])
+        if self.master.data_ptr() != self.store.param_buf.data_ptr():
+            # bf16 / fp16 run: the module holds the low-precision copy, so the fp32 masters travel with
+            # the optimizer state (DeepSpeed's bf16 optimizer keeps its fp32 groups there too) --
+            # without them a resumed run restarts from rounded weights and drifts off the original
+            st["single_partition_of_fp32_groups"] = [self.master.detach().cpu().clone()]
+        return st
 
     def _zero_shard_state(self) -> Dict[str, Any]:
         g = self.optimizer.param_groups[0]
@@ -512,7 +518,11 @@ class Engine:
         self.skipped_steps = int(states.get("skipped_steps", 0))
         if self.stage == 0:
             if self.master.data_ptr() != self.store.param_buf.data_ptr():
-                self.master.copy_(self.store.param_buf.float())
+                fp32 = (states.get("optimizer") or {}).get("single_partition_of_fp32_groups")
+                if fp32 and fp32[0].numel() == self.master.numel():
+                    self.master.copy_(fp32[0].to(self.master))
+                else:  # a checkpoint without masters (fp32 run, or another writer): start from the module
+                    self.master.copy_(self.store.param_buf.float())
             if load_optimizer_states and states.get("optimizer"):
                 adam_state_to_flat(states["optimizer"], self.exp_avg, self.exp_avg_sq, self.layout.segments())
         else:

@@ -125,6 +125,31 @@ def test_checkpoint_round_trip(tmp_path):
     e2.close()
 
 
+def test_bf16_stage0_checkpoint_keeps_fp32_masters(tmp_path):
+    """bf16 run: the module holds bf16 weights, so the fp32 masters ride in the optimizer state and a
+    resumed run continues bit for bit (the GPU twin: test_train_py_model_mlp_saves_and_resumes_on_gpu)."""
+    cfg = {"train_batch_size": 8, "bf16": {"enabled": True}, "zero_optimization": {"stage": 0}}
+    crit = torch.nn.BCEWithLogitsLoss()
+    engine, _ = _engine_run(_mlp(6), _batches(4), cfg)
+    engine.save_checkpoint(str(tmp_path))
+    for x, y in _batches(3, 9):
+        engine.backward(crit(engine(x).float(), y))
+        engine.step()
+    a, ma = engine.master.clone(), torch.nn.utils.parameters_to_vector(engine.module.parameters()).detach()
+    engine.close()
+    e2, _, _, _ = dgt.initialize(model=_mlp(99), config=cfg)
+    e2.load_checkpoint(str(tmp_path))
+    for x, y in _batches(3, 9):
+        e2.backward(crit(e2(x).float(), y))
+        e2.step()
+    assert torch.equal(e2.master, a)
+    assert torch.equal(torch.nn.utils.parameters_to_vector(e2.module.parameters()).detach(), ma)
+    sd = torch.load(os.path.join(tmp_path, "global_step4", "mp_rank_00_model_states.pt"), weights_only=True)
+    assert sd["optimizer"]["single_partition_of_fp32_groups"][0].dtype == torch.float32
+    torch.optim.Adam(_mlp().parameters()).load_state_dict(sd["optimizer"])  # still torch Adam's format
+    e2.close()
+
+
 def test_flat_layout_buckets_and_shards():
     shapes = [(64, 20), (64,), (1, 64), (1,)]
     lay = FlatLayout(shapes, bucket_elems=100, world_size=4, shard=True)
