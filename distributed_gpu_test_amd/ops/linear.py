@@ -35,20 +35,25 @@ from . import _ext
 # parameters, a user's own loss.backward() -- gets dW / db returned to autograd as usual.
 _ENGINE_BACKWARD = 0
 # the engine's flat gradient buffer is all zeros at the start of this backward (the first micro-step
-# after zero_grad): the bf16 MFMA chain then STORES its weight gradients instead of accumulating
+# after zero_grad): the bf16 MFMA chain then STORES a weight gradient instead of accumulating it --
+# the FIRST time that gradient is written in this backward only (a module called twice before one
+# backward writes each of its gradients twice: the second write must add)
 _GRADS_ZERO = False
+_WRITTEN: set = set()
 
 
 @contextlib.contextmanager
 def engine_backward(grads_zero: bool = False):
-    global _ENGINE_BACKWARD, _GRADS_ZERO
+    global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN
     _ENGINE_BACKWARD += 1
     prev, _GRADS_ZERO = _GRADS_ZERO, bool(grads_zero)
+    prev_written, _WRITTEN = _WRITTEN, set()
     try:
         yield
     finally:
         _ENGINE_BACKWARD -= 1
         _GRADS_ZERO = prev
+        _WRITTEN = prev_written
 
 
 def _in_place_active() -> bool:
@@ -57,6 +62,18 @@ def _in_place_active() -> bool:
 
 def _grads_zero() -> bool:
     return _GRADS_ZERO
+
+
+def _first_write(grad: torch.Tensor) -> bool:
+    """True if ``grad`` (a view of the zeroed flat buffer) may be STORED rather than accumulated:
+    the buffer was zero when this backward began and nothing has written this view since."""
+    if not _GRADS_ZERO:
+        return False
+    key = (grad.data_ptr(), grad.numel())
+    if key in _WRITTEN:
+        return False
+    _WRITTEN.add(key)
+    return True
 
 
 # Every call that leaves the hand-written kernels for F.linear (hipBLASLt / rocBLAS), by reason:

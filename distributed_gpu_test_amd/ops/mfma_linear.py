@@ -34,7 +34,7 @@ import torch.nn as nn
 
 from ..models.synthetic_mlp import SyntheticMLP
 from .gemm import gemm_nt, rowsum_bf16, skinny_bwd_bf16, skinny_fwd_bf16, transpose_bf16
-from .linear import _grad_view_ok, _grads_zero, _in_place_active, count_fallback
+from .linear import _first_write, _grad_view_ok, _in_place_active, count_fallback
 
 MAX_HEAD = 4
 BF16 = torch.bfloat16
@@ -115,7 +115,6 @@ class _MfmaChainFn(torch.autograd.Function):
         xs, xTs, ws = saved[:L + 1], saved[L + 1:2 * L + 1], saved[2 * L + 1:]
         need = ctx.needs_input_grad
         active = ctx.grad_in_place and _in_place_active()
-        zero = _grads_zero()
         M, dev = xs[0].shape[0], xs[0].device
         n_pairs = L + (1 if head else 0)
         grads: List[Optional[torch.Tensor]] = [None] * (2 * n_pairs)
@@ -155,14 +154,14 @@ class _MfmaChainFn(torch.autograd.Function):
             if need[4 + jw]:
                 p = leaf(jw)
                 if p is not None and _grad_view_ok(p, BF16):
-                    gemm_nt(gT, xTs[i], C=p.grad, accumulate=not zero)
+                    gemm_nt(gT, xTs[i], C=p.grad, accumulate=not _first_write(p.grad))
                 else:
                     grads[jw] = torch.empty_like(w)
                     gemm_nt(gT, xTs[i], C=grads[jw])
             if ctx.has_bias[i] and need[4 + jb]:
                 p = leaf(jb)
                 if p is not None and _grad_view_ok(p, BF16):
-                    rowsum_bf16(gT, p.grad, accumulate=not zero)
+                    rowsum_bf16(gT, p.grad, accumulate=not _first_write(p.grad))
                 else:
                     grads[jb] = torch.empty(w.shape[0], dtype=BF16, device=dev)
                     rowsum_bf16(gT, grads[jb])

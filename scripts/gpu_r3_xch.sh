@@ -5,8 +5,8 @@
 set -o pipefail
 mkdir -p gpurun_out/r3a
 export TMPDIR=/tmp DGT_QUIET=1
-P="python -u -m pytest -x -v --timeout 600 --timeout-method thread"
-timeout -k 10 600 $P tests/test_gpu_tiny_mlp.py tests/test_gpu_train.py tests/test_gpu_engine.py tests/test_mlp_gemm.py > gpurun_out/r3a/pytest_single.log 2>&1 || { tail -40 gpurun_out/r3a/pytest_single.log; exit 1; }
+P="python -u -m pytest -v --timeout 600 --timeout-method thread"
+timeout -k 10 600 $P tests/test_gpu_tiny_mlp.py tests/test_gpu_train.py tests/test_gpu_engine.py tests/test_mlp_gemm.py > gpurun_out/r3a/pytest_single.log 2>&1 || { grep -E "^(FAILED|ERROR)|passed|failed" gpurun_out/r3a/pytest_single.log | tail -30; exit 1; }
 tail -2 gpurun_out/r3a/pytest_single.log
 timeout -k 10 900 $P tests/test_gpu_multiproc.py -k "${MP_K:-fallback or strict or stress or zero1 or every_shape or many_ranks}" > gpurun_out/r3a/pytest_multi.log 2>&1 || { tail -60 gpurun_out/r3a/pytest_multi.log; exit 1; }
 tail -2 gpurun_out/r3a/pytest_multi.log

@@ -321,14 +321,16 @@ def test_fused_chain_frozen_layer_stays_frozen():
 @pytest.mark.gpu
 def test_graph_module_keeps_buffers_and_rng_and_guards_double_forward():
     """graph_module's capture warmup leaves BatchNorm running stats as they were, and a second forward of one signature before the first one's backward runs eagerly
-    (the pending backward keeps its activations): the trajectory equals the eager engine's."""
+    (the pending backward keeps its activations): the trajectory equals the eager engine's.  Both
+    runs use F.linear (fused_linear off): the graphs must change the schedule, not the kernels --
+    under Adam two GEMM implementations' last-bit differences grow past any tight tolerance."""
     def net(seed):
         torch.manual_seed(seed)
         return torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.BatchNorm1d(128), torch.nn.ReLU(),
                                    torch.nn.Linear(128, 1))
     crit = torch.nn.BCEWithLogitsLoss()
     res = []
-    for amd in ({"graph_module": False}, {"graph_module": True}):
+    for amd in ({"graph_module": False, "fused_linear": False}, {"graph_module": True, "fused_linear": False}):
         e, _, _, _ = dgt.initialize(model=net(17), config={"train_batch_size": 32, "amd": amd})
         torch.manual_seed(5)
         losses = []
@@ -389,6 +391,29 @@ def test_engine_bf16_gradient_accumulation_uses_accumulating_epilogue():
     torch.testing.assert_close(a.engine.master, b.engine.master, rtol=0, atol=2e-3)
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+def test_engine_bf16_chain_called_twice_before_backward():
+    """Two forwards of the MFMA chain before one backward, right after zero_grad: each weight
+    gradient is written twice in that backward -- stored the first time (the bucket was zero), added
+    the second -- and matches the autograd engine's gradient of the same two-call loss."""
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    grads = []
+    for fused in (True, False):
+        torch.manual_seed(7)
+        cfg = {"train_micro_batch_size_per_gpu": 256, "bf16": {"enabled": True},
+               "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "amd": {"fused_linear": fused}}
+        e, _, _, _ = dgt.initialize(model=SyntheticMLP(256, 2), config=cfg)
+        g = torch.Generator().manual_seed(3)
+        x = torch.randn(256, 256, generator=g).to(torch.bfloat16).cuda()
+        y = (torch.rand(256, generator=g) > 0.5).float().cuda()
+        crit = torch.nn.BCEWithLogitsLoss()
+        loss = crit(e(x).view(-1).float(), y) + crit(e(x * 0.5).view(-1).float(), y)
+        e.backward(loss)
+        grads.append(torch.cat([p.grad.float().reshape(-1) for p in e.module.parameters()]))
+        e.close()
+    torch.testing.assert_close(grads[0], grads[1], rtol=3e-2, atol=2e-4)
 
 
 @pytest.mark.gpu
