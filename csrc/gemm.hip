@@ -96,7 +96,26 @@ DGT_DEVICE void stage_b(const u16* __restrict__ src, int ld, int n0, int k0, u16
 // thread's LDS-DMA pieces is computed ONCE and advanced by one K-tile per issue (K-tiles are staged
 // strictly in order), instead of recomputing 64-bit row addresses and swizzles for every piece of
 // every K-tile inside the main loop.
-template <int NWAVE, bool KN>
+// LDS-DMA issued from inline asm (FR kernel): the compiler's waitcnt insertion treats a
+// global_load_lds it can see as an LDS event and then drains every ds_read with lgkmcnt(0) before
+// the first MFMA that uses one; hidden in asm it counts the reads (lgkmcnt(N)).  The caller owns
+// the DMA's vmcnt accounting (wait_vmcnt) and its ordering against LDS reads (s_barrier).  M0 is
+// saved and restored around the DMA's use of it.
+DGT_DEVICE void glds_asm(const u16* gptr, const u16* lds) {
+  const unsigned la =
+      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((__attribute__((address_space(3))) const u16*)(lds)));
+  unsigned saved;
+  asm volatile(
+      "s_mov_b32 %0, m0\n\t"
+      "s_mov_b32 m0, %2\n\t"
+      "global_load_lds_dwordx4 %1, off\n\t"
+      "s_mov_b32 m0, %0"
+      : "=&s"(saved)
+      : "v"(gptr), "s"(la)
+      : "memory");
+}
+
+template <int NWAVE, bool KN, bool ASM = false>
 struct Stager {
   static constexpr int PER_WAVE = 16 / NWAVE;
   const u16* p[PER_WAVE];
@@ -123,8 +142,10 @@ struct Stager {
   DGT_DEVICE void issue(u16* lds) {
 #pragma unroll
     for (int i = 0; i < PER_WAVE; ++i) {
-      __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(p[i]), reinterpret_cast<int*>(lds + lds_off[i]),
-                                       16, 0, 0);
+      if constexpr (ASM) glds_asm(p[i], lds + lds_off[i]);
+      else
+        __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(p[i]), reinterpret_cast<int*>(lds + lds_off[i]),
+                                         16, 0, 0);
       p[i] += step;
     }
   }
@@ -362,9 +383,15 @@ DGT_DEVICE void wait_vmcnt() {
 // each: two waves per SIMD, so one wave's LDS fragment reads overlap the other's MFMAs (the
 // 4-wave block leaves the matrix core idle while its only wave waits on LDS).
 // (Round-2 BK = 128 / two-K-tiles-per-barrier forms of this loop: csrc/diag/gemm_variants_r2.h.)
-template <int EPI, int S, int NW = 4>
+// FR (front-loaded fragment reads, NT operands only): each wave issues ALL its ds_reads of a K-tile
+// (both 32-deep halves) before its first MFMA and lets counted lgkmcnt waits release the MFMAs as
+// fragments land.  After the per-K-tile barrier all waves otherwise move in lockstep through
+// read -> lgkmcnt(0) -> 4 MFMAs phases, so the LDS and the matrix cores take turns instead of
+// overlapping.
+template <int EPI, int S, int NW = 4, bool FR = false>
 __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(S == 2 || S == 4, "two stages (2 blocks / CU) or four (1 block / CU)");
+  static_assert(!FR || (EPI & kEpiBKN) == 0, "front-loaded reads: NT operands only");
   constexpr int BK = GBK;
   constexpr bool KN = (EPI & kEpiBKN) != 0;      // B is [K, N]: staged as is, transposed reads
   constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
@@ -389,6 +416,29 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
   auto compute = [&](int buf) {
     const u16* As = lds[buf][0];
     const u16* Bs = lds[buf][1];
+    if constexpr (FR) {
+      // all 12 reads of the K-tile (per 32-deep half: A0..A3, B0, B1) ahead of the 16 MFMAs; the
+      // compiler's counted lgkmcnt waits release each MFMA as its two fragments land
+      bf16x8 af[BK / 32][4], bfr[BK / 32][NJ];
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int chunk = kk * 4 + (l >> 4);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[kk][j] = read_frag<BK>(Bs, wc * WN + j * 16 + (l & 15), chunk);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) af[kk][i] = read_frag<BK>(As, wr * 64 + i * 16 + (l & 15), chunk);
+      }
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, (BK / 32) * (4 + NJ), 0);  // every DS read first
+      __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ, 0);    // then the MFMAs
+      return;
+    }
 #pragma unroll
     for (int kk = 0; kk < BK / 32; ++kk) {
       const int chunk = kk * 4 + (l >> 4);
@@ -437,8 +487,8 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
   } else {
     constexpr int PER_TILE = 2 * (16 / NW);  // glds per thread per K-tile (A and B)
     constexpr int AHEAD = S - 2;             // K-tiles left in flight past the one being retired
-    Stager<NW, false> sa(A, g.lda, m0, w, l);
-    Stager<NW, KN> sb(B, g.ldb, n0, w, l);
+    Stager<NW, false, FR> sa(A, g.lda, m0, w, l);
+    Stager<NW, KN, FR> sb(B, g.ldb, n0, w, l);
 #pragma unroll
     for (int p = 0; p < S - 1; ++p) {
       if (p < nk) {
@@ -697,17 +747,18 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 }
 
 // variant: 0 = pick by shape, 1 = 128x128 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase,
+// 3 = variant 4 with front-loaded fragment reads (FR; NT operands, else as 4),
 // 4 = 128x128 4-stage with 8 waves (1 block / CU).  The round-2 variants measured slower or no
 // better inside the MLP step (3, 5-9) live in csrc/diag/gemm_variants_r2.h.
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant != 0 && variant != 1 && variant != 2 && variant != 4) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 4) return hipErrorInvalidValue;
   const bool kn = (epi & kEpiBKN) != 0;  // only the 128x128 kernels read a [K, N] B operand
   const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0;
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks)
   // wins
   bool big = fits256 && !kn && (g.M / 256) * (g.N / 256) >= 200;
-  if (variant == 1 || variant == 4) big = false;
+  if (variant == 1 || variant == 3 || variant == 4) big = false;
   if (variant == 2) {
     if (!fits256 || kn) return hipErrorInvalidValue;
     big = true;
@@ -715,7 +766,8 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   const int grid = big ? (g.M / 256) * (g.N / 256) : (g.M / GBM) * (g.N / GBN);
   // a grid that fits the chip at one block per CU gains nothing from 2 blocks / CU: spend the LDS on
   // a deep (4-stage) pipeline and 8 waves instead (measured: 8 waves beat 4 on one-wave grids)
-  const bool eight = !big && (variant == 4 || (variant == 0 && grid <= 256));
+  const bool eight = !big && (variant == 3 || variant == 4 || (variant == 0 && grid <= 256));
+  const bool fr = eight && !kn && variant == 3;
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
     if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
@@ -724,6 +776,7 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
     if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
+    else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, true>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;

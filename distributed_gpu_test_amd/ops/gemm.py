@@ -11,6 +11,8 @@ from __future__ import annotations
 
 from typing import Optional
 
+import os
+
 import torch
 
 from ._ext import require
@@ -37,12 +39,18 @@ def gemm_nt_reference(A, B, C=None, CT=None, bias=None, mask=None, relu=False, o
     return r
 
 
+_ENV_VARIANT = int(os.environ.get("DGT_GEMM_VARIANT", "0") or 0)
+
+
 def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, CT: Optional[torch.Tensor] = None,
             bias: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, relu: bool = False,
             out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0,
             b_kn: bool = False) -> None:
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage (2 blocks per CU),
-    2 = 256x256 8-phase pipeline, 4 = 128x128 tiles 4-stage with 8 waves (1 block per CU).
+    2 = 256x256 8-phase pipeline, 3 = variant 4 with front-loaded LDS fragment reads (NT operands;
+    a [K, N] B runs as 4), 4 = 128x128 tiles 4-stage with 8 waves (1 block per CU).
+    ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
+    the shape rule gives to the 128x128 kernels).
 
     ``b_kn=True``: B is given as ``[K, N]`` (N contiguous) and ``C = alpha * A @ B`` — the operand is
     staged as it lies and read with transposed LDS reads (128x128 kernels only).  ``accumulate``
@@ -53,6 +61,8 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     epi = ((EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | (EPI_MASK if mask is not None else 0)
            | (EPI_STORE_T if CT is not None else 0) | (EPI_OUT_F32 if out_f32 else 0)
            | (EPI_ACCUMULATE if accumulate else 0) | (EPI_B_KN if b_kn else 0))
+    if variant == 0 and _ENV_VARIANT and (A.shape[0] // 128) * ((B.shape[1] if b_kn else B.shape[0]) // 128) <= 256:
+        variant = _ENV_VARIANT
     require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant))
 
 

@@ -22,11 +22,26 @@ C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
 CT = torch.empty(N, M, device="cuda", dtype=torch.bfloat16)
 bias = torch.randn(N, device="cuda")
 mask = (torch.randn(M, N, device="cuda") > 0).bfloat16()
+# the MLP's weight gradient: dW[4096, 4096] = g^T . a over the batch (K = 1024), both operands K-major
+gT = torch.randn(N, M, device="cuda").bfloat16()
+aT = torch.randn(K, M, device="cuda").bfloat16()
+dW = torch.empty(N, K, device="cuda", dtype=torch.bfloat16)
+# variant 3 (front-loaded fragment reads) must give variant 4's bits: same MFMAs in the same order
+ref, got = torch.empty_like(C), torch.empty_like(C)
+gemm_nt(a, w, C=ref, CT=CT, bias=bias, relu=True, variant=4)
+gemm_nt(a, w, C=got, CT=CT, bias=bias, relu=True, variant=3)
+print(json.dumps({"check": "v3 == v4 (fwd bias+relu+T)", "bitwise_equal": bool(torch.equal(ref, got)),
+                  "max_abs_vs_fp32": float((got.float() - torch.relu(a.float() @ w.float().t() + bias)).abs().max())}),
+      flush=True)
 arms = {}
 for v in [int(x) for x in os.environ.get("VARIANTS", "1,4").split(",")]:
     arms[f"fwd plain v{v}"] = lambda v=v: gemm_nt(a, w, C=C, variant=v)
     arms[f"fwd bias+relu+T v{v}"] = lambda v=v: gemm_nt(a, w, C=C, CT=CT, bias=bias, relu=True, variant=v)
     arms[f"dgrad [K,N] mask+T v{v}"] = lambda v=v: gemm_nt(g, w, C=C, CT=CT, mask=mask, b_kn=True, variant=v)
+for v in [int(x) for x in os.environ.get("WGRAD_VARIANTS", "").split(",") if x]:
+    arms[f"wgrad 4096x4096x1024 v{v}"] = lambda v=v: gemm_nt(gT, aT, C=dW, variant=v)
+if os.environ.get("WGRAD_VARIANTS"):
+    arms["hipBLASLt g^T @ a (wgrad)"] = lambda: torch.matmul(gT, aT.t(), out=dW)
 arms["hipBLASLt a @ W^T"] = lambda: torch.matmul(a, w.t(), out=C)
 arms["hipBLASLt g @ W"] = lambda: torch.matmul(g, w, out=C)
 for name, fn in arms.items():
