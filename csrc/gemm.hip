@@ -177,6 +177,20 @@ DGT_DEVICE bf16x8 tr_wait(i16x4& lo, i16x4& hi) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+// read_frag_kn through the compiler builtin (FR kernel: with the LDS-DMA hidden in asm the compiler
+// counts these reads like any ds_read instead of draining the staging pipeline before each one)
+DGT_DEVICE bf16x8 read_frag_kn_fr(const u16* lds, int kb, int nb, int l) {
+  const int q = (l >> 2) & 3, col = nb + 4 * (l & 3);
+  const int r0 = kb + 8 * (l >> 4) + q, r1 = r0 + 4;
+  const u16* a0 = lds + r0 * GBN + (((col >> 3) ^ kn_swz(r0)) << 3) + (col & 4);
+  const u16* a1 = lds + r1 * GBN + (((col >> 3) ^ kn_swz(r1)) << 3) + (col & 4);
+  typedef short __attribute__((ext_vector_type(4))) __attribute__((address_space(3))) * p4;
+  const i16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((p4)((__attribute__((address_space(3))) const u16*)(a0)));
+  const i16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((p4)((__attribute__((address_space(3))) const u16*)(a1)));
+  const i16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
+
 // One MFMA accumulator (rows mb..mb+3 of column n) through the fused epilogue.
 template <int EPI>
 DGT_DEVICE void epi_store(const GemmArgs& g, const f32x4& acc, int mb, int n) {
@@ -383,7 +397,7 @@ DGT_DEVICE void wait_vmcnt() {
 // each: two waves per SIMD, so one wave's LDS fragment reads overlap the other's MFMAs (the
 // 4-wave block leaves the matrix core idle while its only wave waits on LDS).
 // (Round-2 BK = 128 / two-K-tiles-per-barrier forms of this loop: csrc/diag/gemm_variants_r2.h.)
-// FR (front-loaded fragment reads, NT operands only): each wave issues ALL its ds_reads of a K-tile
+// FR (front-loaded fragment reads): each wave issues ALL its ds_reads of a K-tile
 // (both 32-deep halves) before its first MFMA and lets counted lgkmcnt waits release the MFMAs as
 // fragments land.  After the per-K-tile barrier all waves otherwise move in lockstep through
 // read -> lgkmcnt(0) -> 4 MFMAs phases, so the LDS and the matrix cores take turns instead of
@@ -391,7 +405,6 @@ DGT_DEVICE void wait_vmcnt() {
 template <int EPI, int S, int NW = 4, bool FR = false>
 __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(S == 2 || S == 4, "two stages (2 blocks / CU) or four (1 block / CU)");
-  static_assert(!FR || (EPI & kEpiBKN) == 0, "front-loaded reads: NT operands only");
   constexpr int BK = GBK;
   constexpr bool KN = (EPI & kEpiBKN) != 0;      // B is [K, N]: staged as is, transposed reads
   constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
@@ -424,7 +437,10 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       for (int kk = 0; kk < BK / 32; ++kk) {
         const int chunk = kk * 4 + (l >> 4);
 #pragma unroll
-        for (int j = 0; j < NJ; ++j) bfr[kk][j] = read_frag<BK>(Bs, wc * WN + j * 16 + (l & 15), chunk);
+        for (int j = 0; j < NJ; ++j) {
+          if constexpr (KN) bfr[kk][j] = read_frag_kn_fr(Bs, kk * 32, wc * WN + j * 16, l);
+          else bfr[kk][j] = read_frag<BK>(Bs, wc * WN + j * 16 + (l & 15), chunk);
+        }
 #pragma unroll
         for (int i = 0; i < 4; ++i) af[kk][i] = read_frag<BK>(As, wr * 64 + i * 16 + (l & 15), chunk);
       }
@@ -435,8 +451,18 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 #pragma unroll
           for (int j = 0; j < NJ; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
-      __builtin_amdgcn_sched_group_barrier(0x100, (BK / 32) * (4 + NJ), 0);  // every DS read first
-      __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ, 0);    // then the MFMAs
+      // every DS read first, the first half's before the second's (at most 16 in flight, and the
+      // first MFMAs wait on the first half only), then the MFMAs
+      if constexpr (KN) {  // 16 reads: the second half's go out after the first MFMAs (lgkmcnt <= 15)
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * NJ, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+        __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * NJ, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ - 2, 0);
+      } else {
+#pragma unroll
+        for (int kk = 0; kk < BK / 32; ++kk) __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);
+        __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ, 0);
+      }
       return;
     }
 #pragma unroll
@@ -747,7 +773,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 }
 
 // variant: 0 = pick by shape, 1 = 128x128 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase,
-// 3 = variant 4 with front-loaded fragment reads (FR; NT operands, else as 4),
+// 3 = variant 4 with front-loaded fragment reads (FR),
 // 4 = 128x128 4-stage with 8 waves (1 block / CU).  The round-2 variants measured slower or no
 // better inside the MLP step (3, 5-9) live in csrc/diag/gemm_variants_r2.h.
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
@@ -767,10 +793,11 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // a grid that fits the chip at one block per CU gains nothing from 2 blocks / CU: spend the LDS on
   // a deep (4-stage) pipeline and 8 waves instead (measured: 8 waves beat 4 on one-wave grids)
   const bool eight = !big && (variant == 3 || variant == 4 || (variant == 0 && grid <= 256));
-  const bool fr = eight && !kn && variant == 3;
+  const bool fr = eight && variant == 3;
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
-    if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
+    if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, true>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;
 #define DGT_EPI_CASE(E)                                                                           \

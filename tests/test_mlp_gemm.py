@@ -55,6 +55,7 @@ gpu = pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 1), (512, 256, 1024, 1),
                                            (256, 256, 128, 2), (512, 768, 256, 2), (768, 512, 1152, 2),
                                            (128, 128, 64, 4), (384, 256, 192, 4), (512, 256, 1024, 4),
+                                           (128, 128, 64, 3), (384, 256, 192, 3), (512, 256, 1024, 3),
                                            (256, 128, 128, 0), (1024, 512, 256, 0)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "bias_T", "bias", "mask_T", "f32", "f32_acc", "bf16_acc"])
 def test_gemm_nt_matches_reference(M, N, K, variant, epi):
@@ -151,6 +152,29 @@ def test_transpose_rowsum_head():
 
 
 @gpu
+@pytest.mark.parametrize("kn", [False, True])
+def test_gemm_variant3_is_bitwise_variant4(kn):
+    """Front-loaded fragment reads (variant 3) change the schedule only: same MFMAs in the same order,
+    so every epilogue output equals variant 4's bit for bit."""
+    g = torch.Generator().manual_seed(11 + kn)
+    M, N, K = 512, 384, 1024
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    B = torch.randn(*((K, N) if kn else (N, K)), generator=g).to(torch.bfloat16).cuda()
+    mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).cuda()
+    bias = torch.randn(N, generator=g).cuda()
+    outs = []
+    for v in (4, 3):
+        C = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+        CT = torch.empty(N, M, dtype=torch.bfloat16).cuda()
+        if kn:
+            gemm_nt(A, B, C=C, CT=CT, mask=mask, b_kn=True, variant=v)
+        else:
+            gemm_nt(A, B, C=C, CT=CT, bias=bias, relu=True, variant=v)
+        outs.append((C, CT))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+
+
+@gpu
 @pytest.mark.parametrize("N,mask", [(1, True), (3, False)])
 def test_skinny_head_matches_reference_and_is_reproducible(N, mask):
     """skinny_fwd/bwd_bf16 (the engine chain's Linear(K, N <= 4) head) against the fp32 reference;
@@ -224,7 +248,8 @@ def test_trainer_overlap_schedule_is_bitwise_serial():
 
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 1), (128, 128, 64, 4),
-                                           (384, 256, 192, 4), (512, 256, 1024, 4), (256, 512, 512, 0)])
+                                           (384, 256, 192, 4), (512, 256, 1024, 4), (256, 512, 512, 0),
+                                           (128, 128, 64, 3), (384, 256, 192, 3), (512, 256, 1024, 3)])
 @pytest.mark.parametrize("epi", ["plain", "mask_T", "T", "f32"])
 def test_gemm_b_kn_matches_reference(M, N, K, variant, epi):
     """B given as [K, N] (the dgrad reading W[out, in] directly through transposed LDS reads)."""
@@ -245,7 +270,7 @@ def test_gemm_b_kn_matches_reference(M, N, K, variant, epi):
 
 
 @gpu
-@pytest.mark.parametrize("variant", [1, 4])
+@pytest.mark.parametrize("variant", [1, 3, 4])
 def test_gemm_b_kn_identity_asymmetric(variant):
     # A = I: C must equal B exactly, catching any transposed / swizzled fragment read
     n = 256
@@ -272,7 +297,8 @@ def test_trainer_comm_dtype_selects_gradient_wire(comm, want):
 
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 4), (512, 256, 1024, 4),
-                                           (256, 256, 128, 2), (512, 768, 256, 2), (1024, 1024, 1024, 0)])
+                                           (512, 256, 1024, 3), (256, 256, 128, 2), (512, 768, 256, 2),
+                                           (1024, 1024, 1024, 0)])
 @pytest.mark.parametrize("wd,adamw", [(0.0, False), (0.01, True)])
 def test_gemm_nt_adam_matches_reference(M, N, K, variant, wd, adamw):
     """wgrad + Adam in one launch (kEpiAdam epilogue through LDS, both kernels) against an fp32
