@@ -402,7 +402,9 @@ DGT_DEVICE void wait_vmcnt() {
 // fragments land.  After the per-K-tile barrier all waves otherwise move in lockstep through
 // read -> lgkmcnt(0) -> 4 MFMAs phases, so the LDS and the matrix cores take turns instead of
 // overlapping.
-template <int EPI, int S, int NW = 4, bool FR = false>
+// FR = 2: the same reads, with ONE barrier per two K-tiles (K % 128 == 0): the pair's both tiles
+// land behind one vmcnt(0) + barrier, the next pair is staged, then the two tiles are computed.
+template <int EPI, int S, int NW = 4, int FR = 0>
 __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(S == 2 || S == 4, "two stages (2 blocks / CU) or four (1 block / CU)");
   constexpr int BK = GBK;
@@ -513,8 +515,31 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
   } else {
     constexpr int PER_TILE = 2 * (16 / NW);  // glds per thread per K-tile (A and B)
     constexpr int AHEAD = S - 2;             // K-tiles left in flight past the one being retired
-    Stager<NW, false, FR> sa(A, g.lda, m0, w, l);
-    Stager<NW, KN, FR> sb(B, g.ldb, n0, w, l);
+    Stager<NW, false, FR != 0> sa(A, g.lda, m0, w, l);
+    Stager<NW, KN, FR != 0> sb(B, g.ldb, n0, w, l);
+    if constexpr (FR == 2) {
+      static_assert(S == 4, "pairs of K-tiles in a 4-stage ring");
+      sa.issue(lds[0][0]);
+      sb.issue(lds[0][1]);
+      sa.issue(lds[1][0]);
+      sb.issue(lds[1][1]);
+      for (int kt = 0; kt < nk; kt += 2) {  // nk even (checked by the dispatcher)
+        const int b0 = kt & 3;
+        wait_vmcnt<0>();                    // this pair landed (the only loads in flight)
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();       // ... for every wave; the previous pair's buffers are free
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 2 < nk) {
+          sa.issue(lds[b0 ^ 2][0]);
+          sb.issue(lds[b0 ^ 2][1]);
+          sa.issue(lds[(b0 ^ 2) + 1][0]);
+          sb.issue(lds[(b0 ^ 2) + 1][1]);
+        }
+        compute(b0);
+        compute(b0 + 1);
+      }
+      __builtin_amdgcn_s_barrier();
+    } else {
 #pragma unroll
     for (int p = 0; p < S - 1; ++p) {
       if (p < nk) {
@@ -543,6 +568,7 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       buf = (buf + 1 == S) ? 0 : buf + 1;
     }
     __builtin_amdgcn_s_barrier();
+    }
   }
 
   // ---- epilogue: D col = l&15 (n), row = 4*(l>>4) + r (m)
@@ -773,18 +799,19 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 }
 
 // variant: 0 = pick by shape, 1 = 128x128 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase,
-// 3 = variant 4 with front-loaded fragment reads (FR),
+// 3 = variant 4 with front-loaded fragment reads (FR), 5 = FR with one barrier per two K-tiles
+// (K % 128 == 0, else 3),
 // 4 = 128x128 4-stage with 8 waves (1 block / CU).  The round-2 variants measured slower or no
 // better inside the MLP step (3, 5-9) live in csrc/diag/gemm_variants_r2.h.
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 4) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 5) return hipErrorInvalidValue;
   const bool kn = (epi & kEpiBKN) != 0;  // only the 128x128 kernels read a [K, N] B operand
   const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0;
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks)
   // wins
   bool big = fits256 && !kn && (g.M / 256) * (g.N / 256) >= 200;
-  if (variant == 1 || variant == 3 || variant == 4) big = false;
+  if (variant == 1 || variant >= 3) big = false;
   if (variant == 2) {
     if (!fits256 || kn) return hipErrorInvalidValue;
     big = true;
@@ -792,18 +819,21 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   const int grid = big ? (g.M / 256) * (g.N / 256) : (g.M / GBM) * (g.N / GBN);
   // a grid that fits the chip at one block per CU gains nothing from 2 blocks / CU: spend the LDS on
   // a deep (4-stage) pipeline and 8 waves instead (measured: 8 waves beat 4 on one-wave grids)
-  const bool eight = !big && (variant == 3 || variant == 4 || (variant == 0 && grid <= 256));
-  const bool fr = eight && variant == 3;
+  const bool eight = !big && (variant >= 3 || (variant == 0 && grid <= 256));
+  const bool fr2 = eight && variant == 5 && g.K % 128 == 0;
+  const bool fr = eight && (variant == 3 || (variant == 5 && !fr2));
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
-    if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, true>), dim3(grid), dim3(512), 0, stream, g); \
+    if (fr2) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 2>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
     if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
-    else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, true>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (fr2) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 2>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;

@@ -47,8 +47,9 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
             out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0,
             b_kn: bool = False) -> None:
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage (2 blocks per CU),
-    2 = 256x256 8-phase pipeline, 3 = variant 4 with front-loaded LDS fragment reads (NT operands;
-    a [K, N] B runs as 4), 4 = 128x128 tiles 4-stage with 8 waves (1 block per CU).
+    2 = 256x256 8-phase pipeline, 3 = variant 4 with front-loaded LDS fragment reads,
+    4 = 128x128 tiles 4-stage with 8 waves (1 block per CU), 5 = 3 with one barrier per two K-tiles
+    (K % 128 == 0, else 3).
     ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
     the shape rule gives to the 128x128 kernels).
 
