@@ -240,16 +240,19 @@ DGT_DEVICE void tile_of_block(int bid, int nbm, int nbn, int& tm, int& tn) {
 // bf16-output epilogue staged through the (then idle) operand LDS, for a TM x TN block tile of NT
 // threads whose waves own WM x WN sub-tiles: the MFMA layout gives each lane 4 rows of ONE column,
 // so direct stores are 2-byte scatters; staged, every global access (C rows, C^T rows, mask rows)
-// is a 16-byte vector and 16 lanes cover one 256-byte row piece.  The low 4 bits of a row's
-// 16-byte chunk index are XOR-swizzled by (row / 8) ^ bit 2 of the row, so the row reads (C: 16
-// lanes per row, row pairs never straddling a 4-row group), the column reads (C^T: 16 lanes at
-// rows 8k + e of one column) and the MFMA-layout writes (rows 4 apart in one 32-lane half, which
-// the row / 8 term alone put on one bank) all hit distinct bank groups.  Values are rounded to
-// bf16 once (after bias / ReLU) and masked after rounding (identical results: the mask only zeroes).
+// is a 16-byte vector.  Tile rows are whole multiples of 32 banks, so only the 16-byte chunk index
+// can separate rows: its low 4 bits are XOR-swizzled by (row / 8) ^ (bit 2 of the row << 1).
+//   MFMA-layout writes (2-byte, banks mod 32): a 32-lane half writes 16 columns (chunks {x, x^1}) of
+//     rows r and r + 4; bit 2 moves row r + 4 to chunks {x^2, x^3}: disjoint banks.
+//   C row reads (16 B, banks mod 64): 16 lanes per row, 2 rows per 16-lane group with equal swizzle.
+//   C^T column reads (2-byte, banks mod 32): a 32-lane half reads 4 adjacent columns (one chunk) of 8
+//     row blocks 8k + e, k = 8 consecutive values: 8 distinct chunk residues mod 8.
+// Values are rounded to bf16 once (after bias / ReLU) and masked after rounding (identical results:
+// the mask only zeroes).
 template <int TN>
 DGT_DEVICE int etile(int r, int n) {
   const int c = n >> 3;
-  return r * TN + ((((c ^ (r >> 3) ^ ((r >> 2) & 1)) & 15) | (c & ~15)) << 3) + (n & 7);
+  return r * TN + ((((c ^ (r >> 3) ^ (((r >> 2) & 1) << 1)) & 15) | (c & ~15)) << 3) + (n & 7);
 }
 
 // kEpiAdam epilogue: the block's fp32 gradient tile goes through LDS (the operand stages are idle)
@@ -371,9 +374,13 @@ DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][W
     if (EPI & kEpiMask) __syncthreads();
     u16* CT = static_cast<u16*>(g.CT);
     constexpr int CPC = TM / 8;  // 8-row chunks per column
+    static_assert(CPC % 16 == 0 && NT % 64 == 0, "C^T read mapping: 16-chunk blocks per wave");
 #pragma unroll
     for (int it = 0; it < TN * CPC / NT; ++it) {
-      const int idx = tid + NT * it, n = idx / CPC, mc = (idx % CPC) * 8;
+      // a wave reads 4 columns x 16 row chunks; each 32-lane half 4 columns x 8 row chunks
+      const int idx = tid + NT * it, sub = idx % (4 * CPC), q = sub & 63;
+      const int n = (idx / (4 * CPC)) * 4 + ((q & 31) >> 3);
+      const int mc = ((q & 7) + 8 * (q >> 5) + 16 * (sub >> 6)) * 8;
       unsigned w[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e)
