@@ -101,9 +101,10 @@ DGT_DEVICE void stage_b(const u16* __restrict__ src, int ld, int n0, int k0, u16
 // the first MFMA that uses one; hidden in asm it counts the reads (lgkmcnt(N)).  The caller owns
 // the DMA's vmcnt accounting (wait_vmcnt) and its ordering against LDS reads (s_barrier).  M0 is
 // saved and restored around the DMA's use of it.
-DGT_DEVICE void glds_asm(const u16* gptr, const u16* lds) {
-  const unsigned la =
-      __builtin_amdgcn_readfirstlane((unsigned)(uintptr_t)((__attribute__((address_space(3))) const u16*)(lds)));
+DGT_DEVICE unsigned lds_byte_addr(const void* p) {
+  return (unsigned)(uintptr_t)((__attribute__((address_space(3))) const char*)(p));
+}
+DGT_DEVICE void glds_asm(const u16* gptr, unsigned la) {  // la: wave-uniform LDS byte address
   unsigned saved;
   asm volatile(
       "s_mov_b32 %0, m0\n\t"
@@ -138,14 +139,26 @@ struct Stager {
       }
     }
     step = KN ? (long long)GBK * ld : GBK;
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) lds_b[i] = __builtin_amdgcn_readfirstlane((unsigned)lds_off[i] * 2u);
   }
+  unsigned lds_b[PER_WAVE];  // ASM: byte offsets of the pieces, in SGPRs
   DGT_DEVICE void issue(u16* lds) {
+    if constexpr (ASM) {  // one address-space cast per tile; the pieces are scalar adds
+      issue_at(__builtin_amdgcn_readfirstlane(lds_byte_addr(lds)));
+      return;
+    }
 #pragma unroll
     for (int i = 0; i < PER_WAVE; ++i) {
-      if constexpr (ASM) glds_asm(p[i], lds + lds_off[i]);
-      else
-        __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(p[i]), reinterpret_cast<int*>(lds + lds_off[i]),
-                                         16, 0, 0);
+      __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(p[i]), reinterpret_cast<int*>(lds + lds_off[i]),
+                                       16, 0, 0);
+      p[i] += step;
+    }
+  }
+  DGT_DEVICE void issue_at(unsigned tile_base) {  // ASM only: LDS byte address of the operand tile
+#pragma unroll
+    for (int i = 0; i < PER_WAVE; ++i) {
+      glds_asm(p[i], tile_base + lds_b[i]);
       p[i] += step;
     }
   }
@@ -524,12 +537,15 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
     constexpr int AHEAD = S - 2;             // K-tiles left in flight past the one being retired
     Stager<NW, false, FR != 0> sa(A, g.lda, m0, w, l);
     Stager<NW, KN, FR != 0> sb(B, g.ldb, n0, w, l);
+    // LDS byte address of operand tile (stage b, operand o): integer arithmetic on one base
+    const unsigned lds0 = FR ? __builtin_amdgcn_readfirstlane(lds_byte_addr(&lds[0][0][0])) : 0u;
+    auto tile_at = [&](int b, int o) { return lds0 + (unsigned)((b * 2 + o) * GBM * BK * 2); };
     if constexpr (FR == 2) {
       static_assert(S == 4, "pairs of K-tiles in a 4-stage ring");
-      sa.issue(lds[0][0]);
-      sb.issue(lds[0][1]);
-      sa.issue(lds[1][0]);
-      sb.issue(lds[1][1]);
+      sa.issue_at(tile_at(0, 0));
+      sb.issue_at(tile_at(0, 1));
+      sa.issue_at(tile_at(1, 0));
+      sb.issue_at(tile_at(1, 1));
       for (int kt = 0; kt < nk; kt += 2) {  // nk even (checked by the dispatcher)
         const int b0 = kt & 3;
         wait_vmcnt<0>();                    // this pair landed (the only loads in flight)
@@ -537,10 +553,10 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
         __builtin_amdgcn_s_barrier();       // ... for every wave; the previous pair's buffers are free
         __builtin_amdgcn_sched_barrier(0);
         if (kt + 2 < nk) {
-          sa.issue(lds[b0 ^ 2][0]);
-          sb.issue(lds[b0 ^ 2][1]);
-          sa.issue(lds[(b0 ^ 2) + 1][0]);
-          sb.issue(lds[(b0 ^ 2) + 1][1]);
+          sa.issue_at(tile_at(b0 ^ 2, 0));
+          sb.issue_at(tile_at(b0 ^ 2, 1));
+          sa.issue_at(tile_at((b0 ^ 2) + 1, 0));
+          sb.issue_at(tile_at((b0 ^ 2) + 1, 1));
         }
         compute(b0);
         compute(b0 + 1);
@@ -550,8 +566,13 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 #pragma unroll
     for (int p = 0; p < S - 1; ++p) {
       if (p < nk) {
-        sa.issue(lds[p][0]);
-        sb.issue(lds[p][1]);
+        if constexpr (FR != 0) {
+          sa.issue_at(tile_at(p, 0));
+          sb.issue_at(tile_at(p, 1));
+        } else {
+          sa.issue(lds[p][0]);
+          sb.issue(lds[p][1]);
+        }
       }
     }
     int buf = 0, nb = S - 1;  // buffer of tile kt, buffer the next staged tile lands in (tile % S)
@@ -566,8 +587,13 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       __builtin_amdgcn_sched_barrier(0);
 #if !(defined(DGT_GEMM_ABLATE) && DGT_GEMM_ABLATE == 1)  // diag: 1 = no staging inside the loop
       if (kt + S - 1 < nk) {
-        sa.issue(lds[nb][0]);
-        sb.issue(lds[nb][1]);
+        if constexpr (FR != 0) {
+          sa.issue_at(tile_at(nb, 0));
+          sb.issue_at(tile_at(nb, 1));
+        } else {
+          sa.issue(lds[nb][0]);
+          sb.issue(lds[nb][1]);
+        }
       }
       nb = (nb + 1 == S) ? 0 : nb + 1;
 #endif
@@ -805,7 +831,8 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   }
 }
 
-// variant: 0 = pick by shape, 1 = 128x128 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase,
+// variant: 0 = pick by shape (256x256 for >= 200 tiles, else 128x128 variant 3 for one-wave
+// grids, else variant 1), 1 = 128x128 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase,
 // 3 = variant 4 with front-loaded fragment reads (FR), 5 = FR with one barrier per two K-tiles
 // (K % 128 == 0, else 3),
 // 4 = 128x128 4-stage with 8 waves (1 block / CU).  The round-2 variants measured slower or no
@@ -828,7 +855,9 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // a deep (4-stage) pipeline and 8 waves instead (measured: 8 waves beat 4 on one-wave grids)
   const bool eight = !big && (variant >= 3 || (variant == 0 && grid <= 256));
   const bool fr2 = eight && variant == 5 && g.K % 128 == 0;
-  const bool fr = eight && (variant == 3 || (variant == 5 && !fr2));
+  // the shape rule's 128x128 choice is the front-loaded-reads form (variant 3): bit-identical to 4,
+  // faster hot and cold and inside the MLP step (profiles/r3_gemm_m1024.jsonl)
+  const bool fr = eight && (variant == 0 || variant == 3 || (variant == 5 && !fr2));
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
     if (fr2) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 2>), dim3(grid), dim3(512), 0, stream, g); \
