@@ -320,10 +320,13 @@ def test_fused_chain_frozen_layer_stays_frozen():
 
 @pytest.mark.gpu
 def test_graph_module_keeps_buffers_and_rng_and_guards_double_forward():
-    """graph_module's capture warmup leaves BatchNorm running stats as they were, and a second forward of one signature before the first one's backward runs eagerly
-    (the pending backward keeps its activations): the trajectory equals the eager engine's.  Both
-    runs use F.linear (fused_linear off): the graphs must change the schedule, not the kernels --
-    under Adam two GEMM implementations' last-bit differences grow past any tight tolerance."""
+    """graph_module's capture warmup leaves BatchNorm running stats as they were, and a
+    second forward of one signature before the first one's backward runs eagerly (the pending
+    backward keeps its activations): both calls' gradients reach the buckets, as in the eager engine.
+    Both runs use F.linear (fused_linear off); the captured GEMMs may still pick other hipBLASLt
+    algorithms than eager ones (other stream, other workspace), so the first step's gradients are
+    compared at fp32-reassociation tolerance and the Adam trajectory at a loose one -- a lost or
+    doubled contribution of either call would be off by tens of percent."""
     def net(seed):
         torch.manual_seed(seed)
         return torch.nn.Sequential(torch.nn.Linear(64, 128), torch.nn.BatchNorm1d(128), torch.nn.ReLU(),
@@ -333,21 +336,25 @@ def test_graph_module_keeps_buffers_and_rng_and_guards_double_forward():
     for amd in ({"graph_module": False, "fused_linear": False}, {"graph_module": True, "fused_linear": False}):
         e, _, _, _ = dgt.initialize(model=net(17), config={"train_batch_size": 32, "amd": amd})
         torch.manual_seed(5)
-        losses = []
+        losses, first_grad = [], None
         for x, y in _batches(6, 18):
             out1 = e(x)
             out2 = e(x * 0.5)  # same signature, before out1's backward
             loss = crit(out1, y) + crit(out2, y)
             e.backward(loss)
+            if first_grad is None:
+                first_grad = torch.cat([p.grad.detach().reshape(-1).clone() for p in e.module.parameters()])
             e.step()
             losses.append(float(loss))
-        res.append((losses, e.store.param_buf.detach().clone(), [b.detach().clone() for b in e.module.buffers()]))
+        res.append((losses, first_grad, e.store.param_buf.detach().clone(),
+                    [b.detach().clone() for b in e.module.buffers()]))
         e.close()
-    (l1, p1, b1), (l2, p2, b2) = res
-    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=1e-5, atol=1e-6)
-    torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
-    for u, v in zip(b1, b2):
-        torch.testing.assert_close(u.float(), v.float(), rtol=1e-5, atol=1e-6)
+    (l1, g1, p1, b1), (l2, g2, p2, b2) = res
+    torch.testing.assert_close(g2, g1, rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=2e-2, atol=1e-4)
+    torch.testing.assert_close(p2, p1, rtol=0, atol=2e-2)
+    for u, v in zip(b1, b2):  # running stats: 12 updates in both runs, none from the capture warmup
+        torch.testing.assert_close(u.float(), v.float(), rtol=2e-2, atol=1e-3)
 
 
 def _bf16_mlp_engine(fused, seed=41, width=512, depth=3, B=256, steps=4, extra=None):
@@ -451,5 +458,10 @@ def test_engine_bf16_matches_mlp_trainer():
     for i in range(3):
         w_eng = eng.engine.module.layers[i].weight.detach().float()
         w_mt = mt.W[i].float()
-        torch.testing.assert_close(w_eng, w_mt, rtol=0, atol=4e-3)
+        d = (w_eng - w_mt).abs()
+        # three Adam steps of lr 1e-3 move a weight by at most ~3e-3: an element whose tiny gradient
+        # has opposite signs in the two paths' roundings may differ by up to twice that; the bulk of
+        # the weights must agree to within bf16 rounding of the updates
+        assert float(d.max()) <= 7e-3, float(d.max())
+        assert float((d > 2e-3).float().mean()) < 1e-3 and float(d.mean()) < 2e-4, (float(d.mean()), i)
     eng.close()
