@@ -325,6 +325,8 @@ class Engine:
 
     def step(self, lr_kwargs=None) -> None:
         self.micro_steps += 1
+        for fn in self._graphed_fwd.values():  # a forward whose backward never came: its activations are dead
+            fn.pending = False
         if not self._boundary_pending:
             return
         self._boundary_pending = False

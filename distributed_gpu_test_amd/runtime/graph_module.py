@@ -102,7 +102,9 @@ class GraphedModule:
         self.pending = False  # a replayed forward whose backward has not run yet
 
     def __call__(self, *args):
+        grad = torch.is_grad_enabled()  # the caller's mode: inside Function.forward it is always off
         outs = _Replay.apply(self, *args, *self.params)
+        self.pending = grad  # under no_grad no backward will come
         return outs[0] if self.single else outs
 
 
@@ -114,7 +116,6 @@ class _Replay(torch.autograd.Function):
                 dst.copy_(src)
         runner.fwd.replay()
         runner.replays += 1
-        runner.pending = torch.is_grad_enabled()  # under no_grad no backward will come
         ctx.runner = runner
         outs = tuple(o.detach() for o in runner.static_out)
         for i, o in enumerate(outs):
