@@ -48,7 +48,8 @@ dgt::AdamHyper make_hyper(double lr, double beta1, double beta2, double eps, dou
 // zero1 / line: the fused kernel's exchange shape (ZeRO-1 or one-shot) and line format (3 = LL3,
 // 2 = LL2), chosen by the trainer (runtime/tiny_trainer.py) and the same on every rank
 dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank, int64_t world_size, int64_t stride,
-                            int64_t seq_base, int64_t timeout_ticks, int64_t zero1 = 0, int64_t line = 3) {
+                            int64_t seq_base, int64_t timeout_ticks, int64_t zero1 = 0, int64_t line = 3,
+                            int64_t xsum = 0) {
   dgt::Exchange ex;
   std::memset(&ex, 0, sizeof(ex));
   TORCH_CHECK(world_size >= 1 && world_size <= dgt::kMaxRanks, "dgt: world_size must be in [1, 8], got ", world_size);
@@ -62,6 +63,8 @@ dgt::Exchange make_exchange(c10::ArrayRef<int64_t> data_ptrs, int64_t rank, int6
   TORCH_CHECK(line == 2 || line == 3, "dgt: exchange line format must be 2 (LL2) or 3 (LL3), got ", line);
   ex.zero1 = zero1 ? 1 : 0;
   ex.line = (int)line;
+  TORCH_CHECK(xsum % 4 == 0, "dgt: misaligned ZeRO-1 checksum buffer");
+  ex.xsum = reinterpret_cast<unsigned*>(xsum);  // caller-owned int32 [2 * threads] on the device (0 = off)
   if (world_size > 1) {
     TORCH_CHECK((int64_t)data_ptrs.size() == world_size, "dgt: need one mailbox pointer per rank");
     TORCH_CHECK(stride > 0 && stride % 256 == 0, "dgt: mailbox stride must be a positive multiple of 256 floats");
@@ -94,7 +97,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
                     int64_t adam_step0, c10::ArrayRef<int64_t> data_ptrs,
                     int64_t rank, int64_t world_size, int64_t stride, int64_t seq_base, int64_t timeout_ticks,
                     int64_t corrupt_step, const std::optional<at::Tensor>& workspace, int64_t zero1,
-                    int64_t line) {
+                    int64_t line, int64_t xsum) {
   TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
               " H=", hidden);
   TORCH_CHECK(beta1 > 0.5 && beta1 < 1.0 && beta2 > 0.0 && beta2 < 1.0, "dgt: fused kernel needs 0.5 < beta1 < 1");
@@ -144,7 +147,7 @@ void tiny_mlp_train(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& 
   a.bc = bc.data_ptr<float>();
   a.loss_acc = loss_acc.data_ptr<double>();
   a.status = status.data_ptr<int>();
-  a.ex = make_exchange(data_ptrs, rank, world_size, stride, seq_base, timeout_ticks, zero1, line);
+  a.ex = make_exchange(data_ptrs, rank, world_size, stride, seq_base, timeout_ticks, zero1, line, xsum);
   a.ex.corrupt_step = corrupt_step;
   a.stamps = nullptr;
   if (world_size > 1) {
@@ -172,7 +175,8 @@ int64_t tiny_launcher_create(const at::Tensor& X, const at::Tensor& Y, const at:
                              const at::Tensor& status, int64_t n_features, int64_t hidden, double lr, double beta1,
                              double beta2, double eps, double weight_decay, bool adamw,
                              c10::ArrayRef<int64_t> data_ptrs, int64_t rank, int64_t world_size, int64_t stride,
-                             int64_t timeout_ticks, int64_t corrupt_step, int64_t zero1, int64_t line) {
+                             int64_t timeout_ticks, int64_t corrupt_step, int64_t zero1, int64_t line,
+                             int64_t xsum) {
   TORCH_CHECK(dgt::tiny_mlp_supported((int)n_features, (int)hidden), "dgt: no fused kernel for F=", n_features,
               " H=", hidden);
   TORCH_CHECK(beta1 > 0.5 && beta1 < 1.0 && beta2 > 0.0 && beta2 < 1.0, "dgt: fused kernel needs 0.5 < beta1 < 1");
@@ -205,7 +209,7 @@ int64_t tiny_launcher_create(const at::Tensor& X, const at::Tensor& Y, const at:
   L->a.beta2 = beta2;
   L->a.loss_acc = loss_acc.data_ptr<double>();
   L->a.status = status.data_ptr<int>();
-  L->a.ex = make_exchange(data_ptrs, rank, world_size, stride, 0, timeout_ticks, zero1, line);
+  L->a.ex = make_exchange(data_ptrs, rank, world_size, stride, 0, timeout_ticks, zero1, line, xsum);
   L->a.ex.corrupt_step = corrupt_step;
   L->a.stamps = nullptr;
   L->f = (int)n_features;
@@ -734,13 +738,13 @@ TORCH_LIBRARY(dgt, m) {
       "Tensor(c!) exp_avg_sq, Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, "
       "float beta1, float beta2, float eps, float weight_decay, bool adamw, int adam_step0, int[] data_ptrs, "
       "int rank, int world_size, int stride, int seq_base, int timeout_ticks, int corrupt_step=-1, "
-      "Tensor(f!)? workspace=None, int zero1=0, int line=3) -> ()",
+      "Tensor(f!)? workspace=None, int zero1=0, int line=3, int xsum=0) -> ()",
       &tiny_mlp_train);
   m.def(
       "tiny_launcher_create(Tensor X, Tensor Y, Tensor(a!) params, Tensor(b!) exp_avg, Tensor(c!) exp_avg_sq, "
       "Tensor(d!) loss_acc, Tensor(e!) status, int n_features, int hidden, float lr, float beta1, float beta2, "
       "float eps, float weight_decay, bool adamw, int[] data_ptrs, int rank, int world_size, int stride, "
-      "int timeout_ticks, int corrupt_step, int zero1=0, int line=3) -> int",
+      "int timeout_ticks, int corrupt_step, int zero1=0, int line=3, int xsum=0) -> int",
       &tiny_launcher_create);
   m.def("tiny_launcher_destroy(int handle) -> ()", &tiny_launcher_destroy);
   m.def(

@@ -55,6 +55,12 @@ struct Exchange {
                                     // owners, owners update, parameters all-gathered) instead of the
                                     // one-shot all-to-all of gradients
   int line;                         // fused kernel line format: 3 = LL3 (16-byte lines), 2 = LL2 (8-byte pairs)
+  unsigned* xsum;                   // ZeRO-1 transfer checksums (null = off): per thread t, [2t] ^= every
+                                    // parameter word its lane sent (owner) or received (all-gather) and
+                                    // [2t + 1] ^= every gradient word it sent (non-owner) or received
+                                    // from peers (owner), over the launch.  A transfer fault ZeRO-1 would
+                                    // heal at the next all-gather still shows up as a mismatch between
+                                    // ranks (runtime/tiny_trainer.py: verify_replicas).
 };
 
 typedef unsigned u32x4 __attribute__((ext_vector_type(4)));

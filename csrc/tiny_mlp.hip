@@ -376,7 +376,8 @@ DGT_DEVICE float line_payload(const u32x4 (&v)[LinesOf<NPAY, LN>::NL], int k) {
 // the same bits, on every rank)
 template <int NPAY, int NP, int LN>
 DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, unsigned tag,
-                               const float (&pay)[NPAY], float (&sum)[NPAY], unsigned long long t0, bool& late) {
+                               const float (&pay)[NPAY], float (&sum)[NPAY], unsigned long long t0, bool& late,
+                               unsigned& rx) {
   u32x4 v[NP][LinesOf<NPAY, LN>::NL];
   unsigned pend = 0;
 #pragma unroll
@@ -387,8 +388,20 @@ DGT_DEVICE void poll_sum_peers(const Exchange& ex, int parity, long long wofs, u
   for (int p = 0; p < NP; ++p) {
     if (p >= ex.world_size) continue;
 #pragma unroll
-    for (int k = 0; k < NPAY; ++k) sum[k] += p == ex.rank ? pay[k] : line_payload<NPAY, LN>(v[p], k);
+    for (int k = 0; k < NPAY; ++k) {
+      const float r = line_payload<NPAY, LN>(v[p], k);
+      if (p != ex.rank) rx ^= __float_as_uint(r);  // (ZeRO-1 checksum; dead code in the one-shot kernel)
+      sum[k] += p == ex.rank ? pay[k] : r;
+    }
   }
+}
+
+template <int NPAY>
+DGT_DEVICE unsigned xor_words(const float (&pay)[NPAY]) {
+  unsigned x = 0;
+#pragma unroll
+  for (int k = 0; k < NPAY; ++k) x ^= __float_as_uint(pay[k]);
+  return x;
 }
 
 // push this lane's payload into one peer's mailbox as LN-payload lines (c0 replaces pay[0]: fault
@@ -401,6 +414,14 @@ DGT_DEVICE void push_payload(unsigned* dst, const float (&pay)[NPAY], float c0, 
     LLine<LN>::put(dst + j * 256, j == 0 ? c0 : pay[k], k + 1 < NPAY ? pay[k + 1] : 0.f,
                    k + 2 < NPAY ? pay[k + 2] : 0.f, tag);
   }
+}
+
+// x * y rounded on its own: never contracted into a following add (an FMA there would round
+// differently depending on how the compiler inlined the caller -- the one-shot and ZeRO-1 kernels
+// must scale the summed gradients to the same bits)
+DGT_DEVICE float mul_rounded(float x, float y) {
+#pragma clang fp contract(off)
+  return x * y;
 }
 
 // ZeRO-1 payload (plain layout, either direction): the lane's W1 slots, its W2 element and b2
@@ -418,9 +439,9 @@ DGT_DEVICE void unpack_plain(const float (&pay)[TinyCfg<F, H>::NPAYZ], float sca
                              float (&w1)[TinyCfg<F, H>::NSP], float& bw, float& b2) {
   using C = TinyCfg<F, H>;
 #pragma unroll
-  for (int i = 0; i < C::NSP; ++i) w1[i] = i < C::NSL ? pay[i] * scale : 0.f;
-  bw = pay[C::NSL] * scale;
-  b2 = pay[C::NSL + 1] * scale;
+  for (int i = 0; i < C::NSP; ++i) w1[i] = i < C::NSL ? mul_rounded(pay[i], scale) : 0.f;
+  bw = mul_rounded(pay[C::NSL], scale);
+  b2 = mul_rounded(pay[C::NSL + 1], scale);
 }
 
 // gradients of one lane -> exchange payload (see TinyCfg::DENSE for the dense layout)
@@ -455,14 +476,14 @@ DGT_DEVICE void unpack_payload(const float (&sum)[TinyCfg<F, H>::NPAY], float in
     const float last = sum[C::NSL - 1];
     const float back = __shfl(last, (l + 20) & 63);  // lanes 0-3 take their W2 sums back from 20-23
 #pragma unroll
-    for (int i = 0; i < C::NSL - 1; ++i) gw1[i] = sum[i] * inv_ws;
-    gw1[C::NSL - 1] = lq == 0 ? last * inv_ws : 0.f;
-    gbw = lr < 4 ? (lq == 0 ? back : last) * inv_ws : 0.f;
-    gb2 = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(last), 24)) * inv_ws;
+    for (int i = 0; i < C::NSL - 1; ++i) gw1[i] = mul_rounded(sum[i], inv_ws);
+    gw1[C::NSL - 1] = lq == 0 ? mul_rounded(last, inv_ws) : 0.f;
+    gbw = lr < 4 ? mul_rounded(lq == 0 ? back : last, inv_ws) : 0.f;
+    gb2 = mul_rounded(__int_as_float(__builtin_amdgcn_readlane(__float_as_int(last), 24)), inv_ws);
   } else {
 #pragma unroll
     for (int i = 0; i < C::NPAY; ++i) {
-      const float v = sum[i] * inv_ws;
+      const float v = mul_rounded(sum[i], inv_ws);
       if (i < C::NSL) gw1[i] = v;
       else if (i == C::NSL) gbw = v;
       else if (i == C::NSL + 1) gb2 = v;
@@ -549,6 +570,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
 #endif
 
   double loss_total = 0.0;
+  unsigned xs_ag = 0, xs_rs = 0;  // ZeRO-1 transfer checksums (Exchange::xsum)
   float zs = 0.f, ys = 0.f, ibs = 0.f;  // deferred-loss ring (wave 0)
   const float inv_ws = 1.0f / (float)ex.world_size;
   // Adam bias corrections of the current step, loaded a step ahead: the scalar load of step s+1's
@@ -638,7 +660,8 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
         }
         // every peer's lines in flight at once: ONE local round trip per poll whatever the world
         // size (polling in batches of 4 peers cost a second round trip per step at 5-8 ranks)
-        poll_sum_peers<NPX, NP, LN>(ex, parity, wofs, tag, pay, sum, t0, late);
+        unsigned rx_unused = 0;
+        poll_sum_peers<NPX, NP, LN>(ex, parity, wofs, tag, pay, sum, t0, late, rx_unused);
         if (late) sm.err = 1;
         unpack_payload<F, H>(sum, inv_ws, l, gw1, gbw, gb2);
         adam_lane<F, H, WD>(st, gw1, gbw, gb2, a.hp, step_size_neg, inv_bc2_sqrt);
@@ -653,15 +676,19 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
         // optimizer state is current only for its 1/P of the lanes (its checkpoint shard).
         pack_plain<F, H>(gw1, gbw, gb2, pay);
         const int own = l % ex.world_size;
-        if (own != ex.rank) push_payload<NPX, LN>(ex.data[own] + mine, pay, pay[0], tag);
+        if (own != ex.rank) {
+          push_payload<NPX, LN>(ex.data[own] + mine, pay, pay[0], tag);
+          xs_rs ^= xor_words<NPX>(pay);
+        }
         // owner lanes FIRST, in program order: a lane waiting for an all-gather must never run
         // ahead of its own wave's owner lanes, which other ranks wait on
         if (own == ex.rank) {
-          poll_sum_peers<NPX, NP, LN>(ex, parity, wofs, tag, pay, sum, t0, late);
+          poll_sum_peers<NPX, NP, LN>(ex, parity, wofs, tag, pay, sum, t0, late, xs_rs);
           if (!late) {
             unpack_plain<F, H>(sum, inv_ws, gw1, gbw, gb2);
             adam_lane<F, H, WD>(st, gw1, gbw, gb2, a.hp, step_size_neg, inv_bc2_sqrt);
             pack_plain<F, H>(st.w1, st.bw, st.b2, pay);
+            xs_ag ^= xor_words<NPX>(pay);  // what every peer must receive
             for (int p = 0; p < ex.world_size; ++p) {
               if (p == ex.rank) continue;
               push_payload<NPX, LN>(ex.data[p] + mine, pay, (p == victim && l == ex.rank) ? pay[0] + 1.0f : pay[0],
@@ -684,6 +711,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
           } while (!ready && !late);
 #pragma unroll
           for (int k = 0; k < NPX; ++k) sum[k] = line_payload<NPX, LN>(v, k);
+          xs_ag ^= xor_words<NPX>(sum);
           unpack_plain<F, H>(sum, 1.0f, st.w1, st.bw, st.b2);
         }
         if (late) sm.err = 1;
@@ -699,6 +727,12 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     idx_next = idx_next2;
     idx_next2 = idx_next3;
     DGT_STAMP(5);
+  }
+  if constexpr (Z) {
+    if (ex.xsum) {  // one thread per word pair, XOR-accumulated across the epoch's launches
+      ex.xsum[2 * t] ^= xs_ag;
+      ex.xsum[2 * t + 1] ^= xs_rs;
+    }
   }
   loss_total += (double)deferred_loss(zs, ys, ibs);  // the partial last ring (empty rings add 0)
   if (l == 0) sm.loss[w] = loss_total;

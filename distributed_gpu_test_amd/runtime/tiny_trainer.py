@@ -109,6 +109,31 @@ class ReplicaDivergence(RuntimeError):
     """Data-parallel replicas ended an epoch with different parameters (a corrupted exchange)."""
 
 
+XSUM_WORDS = 2048  # 2 per thread of the fused kernel (<= 1024 threads); unused threads stay 0
+
+
+def zero1_checksum_mismatch(per_rank: List[torch.Tensor], world_size: int) -> Optional[str]:
+    """Check the ZeRO-1 kernel's transfer checksums (csrc/dgt_common.h Exchange::xsum) of every rank.
+    Thread t's lane l = t % 64 is owned by rank l % world_size.  Word 2t: the owner's XOR of the
+    parameters it all-gathered must equal every other rank's XOR of what it received.  Word 2t + 1:
+    the owner's XOR of the gradients it received must equal the XOR over the other ranks of what
+    they sent.  Returns a description of the first mismatch, or None."""
+    xs = torch.stack([t.view(-1, 2) for t in per_rank])  # [ranks, threads, 2]
+    for t in range(xs.shape[1]):
+        o = (t % 64) % world_size
+        ag = xs[:, t, 0]
+        if bool((ag != ag[o]).any()):
+            r = int(torch.nonzero(ag != ag[o])[0])
+            return f"parameters all-gathered by rank {o} arrived altered on rank {r} (thread {t})"
+        sent = 0
+        for p in range(world_size):
+            if p != o:
+                sent ^= int(xs[p, t, 1])
+        if sent != int(xs[o, t, 1]):
+            return f"gradients reduce-scattered to rank {o} arrived altered (thread {t})"
+    return None
+
+
 class ExchangeFailure(RuntimeError):
     """The fused kernel's in-kernel exchange failed on some rank (timeout or replica divergence)."""
 
@@ -194,6 +219,7 @@ class TinyMLPTrainer:
         self._lh = None  # lean fused launcher (created on the first fused launch)
         self._lh_stream = None
         self._ws = None  # the fused kernel's bias-correction workspace (it fills it itself)
+        self._xsum = None  # ZeRO-1 transfer checksums (zero1_checksum_mismatch)
         if self.impl == "fused":
             self.reserve(self.steps_per_epoch())
         if self.impl == "graph":
@@ -393,7 +419,7 @@ class TinyMLPTrainer:
                                ch.data_ptrs if ch else [], self.rank,
                                self.world_size, ch.stride if ch else 0, seq,
                                ch.timeout_ticks if ch else 0, self.faults.corrupt_step(), self._ws,
-                               int(self.zero1), self.line)
+                               int(self.zero1), self.line, self._xsum_ptr())
             self.global_steps += n
         elif self.impl == "graph":
             self.step_dev.fill_(self.global_steps)
@@ -455,7 +481,8 @@ class TinyMLPTrainer:
                 self.x, self.y, self.params, self.exp_avg, self.exp_avg_sq, self.loss_acc, self.status, self.F,
                 self.H, self.lr, self.betas[0], self.betas[1], self.eps, self.weight_decay, self.adamw,
                 ch.data_ptrs if ch else [], self.rank, self.world_size, ch.stride if ch else 0,
-                ch.timeout_ticks if ch else 0, self.faults.corrupt_step(), int(self.zero1), self.line))
+                ch.timeout_ticks if ch else 0, self.faults.corrupt_step(), int(self.zero1), self.line,
+                self._xsum_ptr()))
             self._lh_stream = _raw_stream(self.device.index)  # the launcher was bound to it
             self._clib = _ext.c_lib()
         return True
@@ -490,7 +517,9 @@ class TinyMLPTrainer:
 
     def verify_replicas(self) -> None:
         """Raise ReplicaDivergence on EVERY rank unless all ranks hold bit-identical parameters
-        (data-parallel training keeps them identical; only a corrupted exchange breaks that)."""
+        (data-parallel training keeps them identical; only a corrupted exchange breaks that) and,
+        on the ZeRO-1 kernel, every transfer arrived as sent (a corrupted parameter all-gather is
+        overwritten by the next step's, so identical replicas alone do not prove a clean epoch)."""
         if self.world_size == 1:
             return
         ref = self.params.clone()
@@ -499,6 +528,19 @@ class TinyMLPTrainer:
         if bad > 0:
             raise ReplicaDivergence(f"data-parallel replicas diverged by optimizer step {self.global_steps} "
                                     f"(impl={self.impl}, exchange={self.exchange})")
+        if self._xsum is not None and self.zero1 and self.impl == "fused":
+            why = zero1_checksum_mismatch(comm.all_gather_object(self._xsum.cpu()), self.world_size)
+            if why:
+                raise ReplicaDivergence(f"ZeRO-1 exchange transfer corrupted by optimizer step {self.global_steps}: "
+                                        f"{why} (exchange={self.exchange})")
+
+    def _xsum_ptr(self) -> int:
+        """Device address of the ZeRO-1 transfer checksums (0 = not on the ZeRO-1 kernel)."""
+        if not (self.zero1 and self.impl == "fused" and self.device.type == "cuda"):
+            return 0
+        if self._xsum is None:
+            self._xsum = torch.zeros(XSUM_WORDS, dtype=torch.int32, device=self.device)
+        return self._xsum.data_ptr()
 
     def _torch_corrupt_spec(self):
         spec = self.faults.spec
@@ -551,6 +593,8 @@ class TinyMLPTrainer:
         plan, counts = self.epoch_plan(epoch)
         snap = self._snapshot() if self._can_fall_back() else None
         self.loss_acc.zero_()
+        if self._xsum is not None:
+            self._xsum.zero_()  # this epoch's transfers only
         with tracing.range(f"dgt.{self.impl}.epoch{epoch}"):  # the fused path: ONE kernel launch
             self.run_plan(plan, counts)
         with tracing.range("dgt.epoch_sync"):

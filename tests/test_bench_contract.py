@@ -81,3 +81,32 @@ def test_zero1_owner_map_partitions_every_element():
             counts = torch.bincount(own, minlength=ws)
             assert int(counts.max() - counts.min()) <= (simple_net_numel(f, h) // ws) // 2 + 16, counts
             assert int(own[-1]) == 0
+
+
+def test_zero1_checksum_mismatch_detects_altered_transfers():
+    """The ZeRO-1 kernel's transfer checksums: a clean epoch passes; an all-gathered parameter or a
+    reduce-scattered gradient that arrived altered is named (csrc/dgt_common.h Exchange::xsum)."""
+    import torch
+    from distributed_gpu_test_amd.runtime.tiny_trainer import XSUM_WORDS, zero1_checksum_mismatch
+    ws = 3
+    g = torch.Generator().manual_seed(0)
+    words = torch.randint(-2**31, 2**31 - 1, (ws, XSUM_WORDS // 2), generator=g, dtype=torch.int64)
+    xs = [torch.zeros(XSUM_WORDS, dtype=torch.int32) for _ in range(ws)]
+    for t in range(XSUM_WORDS // 2):
+        o = (t % 64) % ws
+        ag = int(words[0, t]) & 0x7fffffff
+        acc = 0
+        for p in range(ws):
+            xs[p][2 * t] = ag  # every rank received what the owner sent
+            if p != o:
+                s = int(words[p, t]) & 0x7fffffff
+                xs[p][2 * t + 1] = s
+                acc ^= s
+        xs[o][2 * t + 1] = acc
+    assert zero1_checksum_mismatch(xs, ws) is None
+    bad = [x.clone() for x in xs]
+    bad[2][2 * 5 + 1] ^= 1  # thread 5's lane is owned by rank 2 (5 % 3): its received gradients differ
+    assert "reduce-scattered to rank 2" in zero1_checksum_mismatch(bad, ws)
+    bad = [x.clone() for x in xs]
+    bad[1][2 * 6] ^= 1 << 20  # thread 6 owned by rank 0: rank 1 received an altered parameter
+    assert "arrived altered on rank 1" in zero1_checksum_mismatch(bad, ws)
