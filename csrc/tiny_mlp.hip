@@ -758,7 +758,10 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
     a.exp_avg[bi] = st.mbw;
     a.exp_avg_sq[bi] = st.vbw;
   }
-  if (t == 0) {
+  // b2 is replicated in every lane and stored once: under ZeRO-1 a lane's moments are current only
+  // on the rank that owns it, so each rank stores b2's state from a lane it owns (lane = rank of
+  // wave 0); the next launch loads it into every lane, and the owners carry on from current moments
+  if (t == (Z ? ex.rank : 0)) {
     a.params[C::G_B2] = st.b2;
     a.exp_avg[C::G_B2] = st.mb2;
     a.exp_avg_sq[C::G_B2] = st.vb2;

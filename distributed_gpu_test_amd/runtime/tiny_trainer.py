@@ -82,7 +82,8 @@ def zero1_owner_map(n_features: int, hidden: int, world_size: int) -> torch.Tens
     """Owning rank of every flat parameter under the fused kernel's ZeRO-1 exchange: the kernel
     keeps W1[j][k] / b1[j] in lane (j % 16, slot) of wave j // 16 and W2 in lanes 0-3 of each DPP
     row (``csrc/tiny_mlp.hip`` TinyCfg::slot_index / bw_index); lane l is owned by rank l % world;
-    b2 is replicated and written back by lane 0 (rank 0)."""
+    b2 is replicated; each rank writes its state back from a lane it owns (lane = rank), so every
+    rank's copy is current and rank 0's stands for the shard."""
     F, H = n_features, hidden
     nkt = (F + 1 + 15) // 16
     rem = F + 1 - 16 * (nkt - 1)
