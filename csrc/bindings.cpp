@@ -505,8 +505,11 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
   }
   if (epi & dgt::kEpiBias) {
     TORCH_CHECK(bias.has_value() && bias->defined() && bias->numel() == N, "dgt: bias must have N elements");
-    check_gpu(*bias, "bias", at::kFloat);
-    g.bias = bias->data_ptr<float>();
+    const bool bf = bias->scalar_type() == at::kBFloat16;
+    check_gpu(*bias, "bias", bf ? at::kBFloat16 : at::kFloat);
+    TORCH_CHECK(bias->is_contiguous(), "dgt: bias must be contiguous");
+    g.bias = bias->data_ptr();
+    g.bias_bf16 = bf ? 1 : 0;  // a bf16 module's bias as it is: no per-call fp32 copy
   }
   if (epi & dgt::kEpiMask) {
     TORCH_CHECK(mask.has_value() && mask->defined(), "dgt: kEpiMask needs mask");

@@ -128,7 +128,8 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   const void* B;
   void* C;             // bf16 or fp32 [M, ldc]; may be null when only C^T is wanted
   void* CT;            // bf16 [N, ldct]
-  const float* bias;
+  const void* bias;     // fp32, or bf16 when bias_bf16
+  int bias_bf16;
   const void* mask;
   int M, N, K;
   int lda, ldb, ldc, ldct, ldmask;

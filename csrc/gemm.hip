@@ -204,10 +204,14 @@ DGT_DEVICE bf16x8 read_frag_kn_fr(const u16* lds, int kb, int nb, int l) {
   return __builtin_bit_cast(bf16x8, v);
 }
 
+DGT_DEVICE float bias_at(const GemmArgs& g, int n) {
+  return g.bias_bf16 ? bf2f(static_cast<const u16*>(g.bias)[n]) : static_cast<const float*>(g.bias)[n];
+}
+
 // One MFMA accumulator (rows mb..mb+3 of column n) through the fused epilogue.
 template <int EPI>
 DGT_DEVICE void epi_store(const GemmArgs& g, const f32x4& acc, int mb, int n) {
-  const float bn = (EPI & kEpiBias) ? g.bias[n] : 0.f;
+  const float bn = (EPI & kEpiBias) ? bias_at(g, n) : 0.f;
   const u16* mask = static_cast<const u16*>(g.mask);
   float v[4];
 #pragma unroll
@@ -333,7 +337,7 @@ DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][W
 #pragma unroll
   for (int j = 0; j < WN / 16; ++j) {
     const int nl = wc * WN + j * 16 + (l & 15);
-    const float bn = (EPI & kEpiBias) ? g.bias[n0 + nl] : 0.f;
+    const float bn = (EPI & kEpiBias) ? bias_at(g, n0 + nl) : 0.f;
 #pragma unroll
     for (int i = 0; i < WM / 16; ++i) {
       const int ml = wr * WM + i * 16 + 4 * (l >> 4);

@@ -93,7 +93,7 @@ class _MfmaChainFn(torch.autograd.Function):
             yT = None
             if i + 1 < L and need[4 + 2 * (i + 1)]:
                 yT = xTs[i + 1] = torch.empty(w.shape[0], M, dtype=BF16, device=dev)
-            gemm_nt(h, w, C=y, CT=yT, bias=None if b is None else b.float(), relu=relus[i])
+            gemm_nt(h, w, C=y, CT=yT, bias=b, relu=relus[i])  # a bf16 bias is read as it is
             xs.append(y)
             h = y
         out = h

@@ -46,9 +46,12 @@ class GradReducer:
         self._launched = [False] * nb
         self._works: List = []
         self.armed = False
-        # staging buffer when the wire dtype differs from the gradient dtype (e.g. bf16 grads, fp32 comm)
+        # staging buffer when the wire dtype differs from the gradient dtype (e.g. bf16 grads, fp32 comm);
+        # a rank that sends nothing (world size 1, collectives not forced) has no wire: the optimizer
+        # reads the gradient buffer as it is (no 6 B/param conversion pass, half the optimizer's reads)
         self.comm_buf = (torch.zeros(layout.total, dtype=self.comm_dtype, device=grad_buf.device)
-                         if self.comm_dtype != grad_buf.dtype else None)
+                         if self.comm_dtype != grad_buf.dtype and (stage >= 1 or comm.collectives_on(world_size))
+                         else None)
         if stage >= 1:
             self.shard_offsets = []
             off = 0

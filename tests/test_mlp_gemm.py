@@ -58,12 +58,15 @@ gpu = pytest.mark.gpu
                                            (128, 128, 64, 3), (384, 256, 192, 3), (512, 256, 1024, 3),
                                            (128, 128, 64, 5), (384, 256, 256, 5), (512, 256, 1024, 5),
                                            (256, 128, 128, 0), (1024, 512, 256, 0)])
-@pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "bias_T", "bias", "mask_T", "f32", "f32_acc", "bf16_acc"])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "bias_T", "bias", "bf16bias_relu_T", "mask_T", "f32", "f32_acc",
+                                 "bf16_acc"])
 def test_gemm_nt_matches_reference(M, N, K, variant, epi):
     g = torch.Generator().manual_seed(M + N + K)
     A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
     B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
     bias = torch.randn(N, generator=g).cuda()
+    if epi.startswith("bf16bias"):  # a bf16 module's bias, read as it is
+        bias, epi = bias.to(torch.bfloat16), epi[4:]
     mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).cuda()
     kw = {}
     if epi == "bias_relu_T":
