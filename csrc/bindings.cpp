@@ -611,7 +611,8 @@ void skinny_fwd_bf16(const at::Tensor& a, const at::Tensor& W, const std::option
 
 // its backward: g = (dz . W) * 1[a > 0] (mask) and g^T; dW / db accumulate in fp32
 void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor& W, bool mask, const at::Tensor& g,
-                     const std::optional<at::Tensor>& gT, const at::Tensor& dW, const at::Tensor& db) {
+                     const std::optional<at::Tensor>& gT, const at::Tensor& dW, const at::Tensor& db,
+                     bool accumulate) {
   const int64_t M = a.size(0), K = a.size(1), N = W.size(0);
   TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && W.size(1) == K && N >= 1 && N <= 4 && M % 64 == 0 && K % 64 == 0,
               "dgt: skinny_bwd needs a [M, K], W [N <= 4, K], M, K % 64 == 0");
@@ -625,15 +626,16 @@ void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor
     check_2d(*gT, "gT", at::kBFloat16, K, M);
     gTp = gT->data_ptr();
   }
-  check_gpu(dW, "dW", at::kFloat);
-  check_gpu(db, "db", at::kFloat);
-  TORCH_CHECK(dW.numel() == N * K && db.numel() == N, "dgt: skinny_bwd dW [N, K] and db [N] (fp32)");
+  const bool bf = dW.scalar_type() == at::kBFloat16;  // the bucket's bf16 gradient views, or fp32
+  check_gpu(dW, "dW", bf ? at::kBFloat16 : at::kFloat);
+  check_gpu(db, "db", bf ? at::kBFloat16 : at::kFloat);
+  TORCH_CHECK(dW.numel() == N * K && db.numel() == N, "dgt: skinny_bwd dW [N, K] and db [N] (one dtype)");
   TORCH_CHECK(dW.is_contiguous(), "dgt: skinny_bwd dW must be contiguous");
   c10::DeviceGuard guard(a.device());
   at::Tensor ws = at::empty({M / 64, N, K}, a.options().dtype(at::kFloat));  // per-row-tile dW partials
   DGT_CHECK_HIP(dgt::skinny_bwd_bf16(dz.data_ptr(), a.data_ptr(), W.data_ptr(), mask ? 1 : 0, g.data_ptr(), gTp,
-                                     dW.data_ptr<float>(), db.data_ptr<float>(), ws.data_ptr<float>(), (int)M,
-                                     (int)N, (int)K, stream_of(a)));
+                                     dW.data_ptr(), db.data_ptr(), bf ? 1 : 0, accumulate ? 1 : 0,
+                                     ws.data_ptr<float>(), (int)M, (int)N, (int)K, stream_of(a)));
 }
 
 void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& y,
@@ -782,7 +784,7 @@ TORCH_LIBRARY(dgt, m) {
   m.def("skinny_fwd_bf16(Tensor a, Tensor W, Tensor? b, Tensor(a!) z) -> ()", &skinny_fwd_bf16);
   m.def(
       "skinny_bwd_bf16(Tensor dz, Tensor a, Tensor W, bool mask, Tensor(a!) g, Tensor(b!)? gT, Tensor(c!) dW, "
-      "Tensor(d!) db) -> ()",
+      "Tensor(d!) db, bool accumulate=True) -> ()",
       &skinny_bwd_bf16);
   m.def(
       "mlp_head(Tensor a, Tensor w, Tensor b0, Tensor y, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!) db, "

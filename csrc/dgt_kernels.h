@@ -149,16 +149,20 @@ hipError_t rowsum_bf16(const void* in, void* out, int out_bf16, int rows, int co
 // The binary head of an MLP (Linear(K, N), N <= 4) in bf16 for the engine's MFMA chain:
 //   forward   z[M, N] = a[M, K] . W[N, K]^T + b           (bf16 in / out, fp32 accumulation)
 //   backward  g[M, K] = (dz . W) * 1[a > 0] (mask optional), g^T[K, M] (optional),
-//             dW[N, K] += dz^T . a (fp32), db[N] += sum_m dz (fp32); part_ws: fp32 [M / 64, N, K]
-//             workspace (per-row-tile dW partials, summed in a fixed order: no atomics)
+//             dW[N, K] (+)= dz^T . a, db[N] (+)= sum_m dz (fp32, or bf16 when dw_bf16: summed in fp32,
+//             rounded once; accumulate = 0 stores); part_ws: fp32 [M / 64, N, K] workspace (per-row-tile
+//             dW partials, summed in a fixed order: no atomics)
 hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z, int M, int N, int K,
                            hipStream_t stream);
-hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, float* dW,
-                           float* db, float* part_ws, int M, int N, int K, hipStream_t stream);
+hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, void* dW,
+                           void* db, int dw_bf16, int accumulate, float* part_ws, int M, int N, int K,
+                           hipStream_t stream);
 
 // out[i] (+)= sum over t = 0 .. tiles-1 (in this order) of part[t * n + i]: the fixed-order reduction of
-// per-tile partials that replaces float atomics (bit-reproducible gradients); n % 4 == 0, 16-B aligned
-hipError_t partials_reduce(const float* part, float* out, int tiles, int n, int accumulate, hipStream_t stream);
+// per-tile partials that replaces float atomics (bit-reproducible gradients); out fp32 or bf16
+// (out_bf16); n % 4 == 0, aligned
+hipError_t partials_reduce(const float* part, void* out, int out_bf16, int tiles, int n, int accumulate,
+                           hipStream_t stream);
 
 struct HeadArgs {      // binary head of the synthetic MLP: Linear(D, 1) + BCE-with-logits (mean)
   const void* a;       // bf16 [B, D] last hidden activation

@@ -1148,7 +1148,7 @@ hipError_t mlp_head(const HeadArgs& h, hipStream_t stream) {
                      h.scratch + h.B, h.db, h.loss_acc);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return partials_reduce(h.scratch + h.B, h.dw, h.B / 64, h.D, 0, stream);
+  return partials_reduce(h.scratch + h.B, h.dw, 0, h.B / 64, h.D, 0, stream);
 }
 
 }  // namespace dgt

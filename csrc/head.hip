@@ -71,7 +71,7 @@ template <int N>
 __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__ dz, const u16* __restrict__ a,
                                                          const u16* __restrict__ W, int mask, u16* __restrict__ g,
                                                          u16* __restrict__ gT, float* __restrict__ part_ws,
-                                                         float* __restrict__ db, int M, int K) {
+                                                         void* __restrict__ db, int db_bf16, int acc, int M, int K) {
   const int l = threadIdx.x & 63, cg = l & 7, rb = l >> 3, wv = threadIdx.x >> 6;
   const int r = blockIdx.y * 64 + rb * 8, c = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + cg * 8;
   float w[N][8];
@@ -143,34 +143,61 @@ __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__
       float s = 0.f;
       for (int i = l; i < M; i += 64) s += b2f(dz[(long long)i * N + n]);
       s = wave_sum(s);
-      if (l == 0) db[n] += s;
+      if (l == 0) {
+        if (db_bf16) {
+          u16* d = static_cast<u16*>(db) + n;
+          *d = f2b((acc ? b2f(*d) : 0.f) + s);
+        } else {
+          float* d = static_cast<float*>(db) + n;
+          *d = (acc ? *d : 0.f) + s;
+        }
+      }
     }
   }
 }
 
-// out[i] (+)= sum over row tiles t (in order) of part[t][i], i < n
-__global__ __launch_bounds__(256) void partials_reduce_kernel(const float* __restrict__ part_ws,
-                                                              float* __restrict__ dW, int tiles, int nk, int acc) {
-  const int i = (blockIdx.x * 256 + threadIdx.x) * 4;
+// out[i] (+)= sum over row tiles t (in order) of part[t][i], i < n; out fp32 or bf16 (the sum in
+// fp32, rounded once).  One float4 column group per thread, its tiles' loads issued 8 at a time
+// (independent), then added in tile order.
+template <bool BF>
+__global__ __launch_bounds__(64) void partials_reduce_kernel(const float* __restrict__ part_ws, void* __restrict__ out,
+                                                             int tiles, int nk, int acc) {
+  const int i = (blockIdx.x * 64 + threadIdx.x) * 4;
   if (i >= nk) return;
-  float4 s = *reinterpret_cast<const float4*>(part_ws + i);
-  for (int t = 1; t < tiles; ++t) {
-    const float4 p = *reinterpret_cast<const float4*>(part_ws + (long long)t * nk + i);
-    s.x += p.x, s.y += p.y, s.z += p.z, s.w += p.w;
+  float4 s = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int t0 = 0; t0 < tiles; t0 += 8) {
+    float4 p[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (t0 + j < tiles) p[j] = *reinterpret_cast<const float4*>(part_ws + (long long)(t0 + j) * nk + i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (t0 + j < tiles) s.x += p[j].x, s.y += p[j].y, s.z += p[j].z, s.w += p[j].w;
   }
-  float4* d = reinterpret_cast<float4*>(dW + i);
-  if (acc) {
-    const float4 o = *d;
-    s = make_float4(o.x + s.x, o.y + s.y, o.z + s.z, o.w + s.w);
+  if constexpr (BF) {
+    u16* d = static_cast<u16*>(out) + i;
+    if (acc) s = make_float4(b2f(d[0]) + s.x, b2f(d[1]) + s.y, b2f(d[2]) + s.z, b2f(d[3]) + s.w);
+    const unsigned lo = (unsigned)f2b(s.x) | ((unsigned)f2b(s.y) << 16);
+    const unsigned hi = (unsigned)f2b(s.z) | ((unsigned)f2b(s.w) << 16);
+    *reinterpret_cast<uint2*>(d) = make_uint2(lo, hi);
+  } else {
+    float4* d = reinterpret_cast<float4*>(static_cast<float*>(out) + i);
+    if (acc) {
+      const float4 o = *d;
+      s = make_float4(o.x + s.x, o.y + s.y, o.z + s.z, o.w + s.w);
+    }
+    *d = s;
   }
-  *d = s;
 }
 
-hipError_t partials_reduce(const float* part, float* out, int tiles, int n, int accumulate, hipStream_t stream) {
-  if (n % 4 || tiles < 1 || ((reinterpret_cast<uintptr_t>(part) | reinterpret_cast<uintptr_t>(out)) & 15))
+hipError_t partials_reduce(const float* part, void* out, int out_bf16, int tiles, int n, int accumulate,
+                           hipStream_t stream) {
+  if (n % 4 || tiles < 1 || (reinterpret_cast<uintptr_t>(part) & 15) ||
+      (reinterpret_cast<uintptr_t>(out) & (out_bf16 ? 7 : 15)))
     return hipErrorInvalidValue;
-  hipLaunchKernelGGL(partials_reduce_kernel, dim3((n / 4 + 255) / 256), dim3(256), 0, stream, part, out, tiles, n,
-                     accumulate);
+  const dim3 grid((n / 4 + 63) / 64), blk(64);
+  if (out_bf16) hipLaunchKernelGGL(partials_reduce_kernel<true>, grid, blk, 0, stream, part, out, tiles, n, accumulate);
+  else hipLaunchKernelGGL(partials_reduce_kernel<false>, grid, blk, 0, stream, part, out, tiles, n, accumulate);
   return hipGetLastError();
 }
 
@@ -189,22 +216,23 @@ hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z,
   return hipGetLastError();
 }
 
-hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, float* dW,
-                           float* db, float* part_ws, int M, int N, int K, hipStream_t stream) {
+hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, void* dW,
+                           void* db, int dw_bf16, int accumulate, float* part_ws, int M, int N, int K,
+                           hipStream_t stream) {
   if (N < 1 || N > 4 || M % 64 || K % 64 || M <= 0 || K <= 0) return hipErrorInvalidValue;
   const int wpb = K % 256 == 0 ? 4 : 1;  // 4 tiles per block side by side when the width allows
   const dim3 grid(K / (64 * wpb), M / 64), blk(64 * wpb);
   const u16 *dp = static_cast<const u16*>(dz), *ap = static_cast<const u16*>(a), *wp = static_cast<const u16*>(W);
   u16 *gp = static_cast<u16*>(g), *gtp = static_cast<u16*>(gT);
   switch (N) {
-    case 1: hipLaunchKernelGGL(skinny_bwd_kernel<1>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, M, K); break;
-    case 2: hipLaunchKernelGGL(skinny_bwd_kernel<2>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, M, K); break;
-    case 3: hipLaunchKernelGGL(skinny_bwd_kernel<3>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, M, K); break;
-    default: hipLaunchKernelGGL(skinny_bwd_kernel<4>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, M, K);
+    case 1: hipLaunchKernelGGL(skinny_bwd_kernel<1>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K); break;
+    case 2: hipLaunchKernelGGL(skinny_bwd_kernel<2>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K); break;
+    case 3: hipLaunchKernelGGL(skinny_bwd_kernel<3>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K); break;
+    default: hipLaunchKernelGGL(skinny_bwd_kernel<4>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  return partials_reduce(part_ws, dW, M / 64, N * K, 1, stream);  // K % 64 == 0: whole float4 groups
+  return partials_reduce(part_ws, dW, dw_bf16, M / 64, N * K, accumulate, stream);  // K % 64: whole float4s
 }
 
 }  // namespace dgt

@@ -114,11 +114,11 @@ def skinny_fwd_bf16(a: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
 
 
 def skinny_bwd_bf16(dz: torch.Tensor, a: torch.Tensor, w: torch.Tensor, mask: bool, g: torch.Tensor,
-                    gT: Optional[torch.Tensor], dw: torch.Tensor, db: torch.Tensor) -> None:
-    """Its backward: g = (dz . w) * 1[a > 0] (if mask) and g^T (bf16); dw [N, K] and db [N] (fp32)
-    accumulate dz^T . a and the column sums of dz."""
+                    gT: Optional[torch.Tensor], dw: torch.Tensor, db: torch.Tensor, accumulate: bool = True) -> None:
+    """Its backward: g = (dz . w) * 1[a > 0] (if mask) and g^T (bf16); dw [N, K] and db [N] (both fp32
+    or both bf16) receive dz^T . a and the column sums of dz: added (``accumulate``) or stored."""
     if a.is_cuda:
-        require().skinny_bwd_bf16(dz, a, w, mask, g, gT, dw, db)
+        require().skinny_bwd_bf16(dz, a, w, mask, g, gT, dw, db, bool(accumulate))
         return
     d = dz.float().reshape(a.shape[0], w.shape[0])
     gg = d @ w.float()
@@ -127,8 +127,12 @@ def skinny_bwd_bf16(dz: torch.Tensor, a: torch.Tensor, w: torch.Tensor, mask: bo
     g.copy_(gg.to(g.dtype))
     if gT is not None:
         gT.copy_(gg.t().to(gT.dtype))
-    dw.add_(d.t() @ a.float())
-    db.add_(d.sum(0))
+    if accumulate:
+        dw.copy_((dw.float() + d.t() @ a.float()).to(dw.dtype))
+        db.copy_((db.float() + d.sum(0)).to(db.dtype))
+    else:
+        dw.copy_((d.t() @ a.float()).to(dw.dtype))
+        db.copy_(d.sum(0).to(db.dtype))
 
 
 def mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT) -> None:

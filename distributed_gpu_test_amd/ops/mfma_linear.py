@@ -128,20 +128,33 @@ class _MfmaChainFn(torch.autograd.Function):
             kh = wh.shape[1]
             g = torch.empty(M, kh, dtype=BF16, device=dev)
             gT = torch.empty(kh, M, dtype=BF16, device=dev)
-            dw = torch.zeros(wh.shape, dtype=torch.float32, device=dev)
-            db = torch.zeros(wh.shape[0], dtype=torch.float32, device=dev)
-            skinny_bwd_bf16(dout, xs[L], wh, relus[L - 1] if L > 0 else False, g, gT, dw, db)
             jw, jb = 2 * L, 2 * L + 1
-            for j, val in ((jw, dw), (jb, db)):
-                if j == jb and not ctx.has_bias[L]:
-                    continue
-                if not need[4 + j]:
-                    continue
-                p = leaf(j)
-                if p is not None and _grad_view_ok(p, BF16):
-                    p.grad.add_(val)  # tiny: [N <= 4, K] and [N]
-                else:
-                    grads[j] = val.to(BF16)
+            pw, pb = leaf(jw), (leaf(jb) if ctx.has_bias[L] else None)
+            mask_h = relus[L - 1] if L > 0 else False
+            direct = (need[4 + jw] and pw is not None and _grad_view_ok(pw, BF16)
+                      and (not ctx.has_bias[L] or (need[4 + jb] and pb is not None and _grad_view_ok(pb, BF16))))
+            if direct:
+                store_w = _first_write(pw.grad)
+                store_b = _first_write(pb.grad) if pb is not None else store_w
+                direct = store_w == store_b  # (else: the add path below, right for zeroed views too)
+            if direct:
+                # straight into the bucket's bf16 views, stored on their first write of this backward
+                db = pb.grad if pb is not None else torch.zeros(wh.shape[0], dtype=BF16, device=dev)
+                skinny_bwd_bf16(dout, xs[L], wh, mask_h, g, gT, pw.grad, db, accumulate=not store_w)
+            else:
+                dw = torch.zeros(wh.shape, dtype=torch.float32, device=dev)
+                db = torch.zeros(wh.shape[0], dtype=torch.float32, device=dev)
+                skinny_bwd_bf16(dout, xs[L], wh, mask_h, g, gT, dw, db)
+                for j, val in ((jw, dw), (jb, db)):
+                    if j == jb and not ctx.has_bias[L]:
+                        continue
+                    if not need[4 + j]:
+                        continue
+                    p = leaf(j)
+                    if p is not None and _grad_view_ok(p, BF16):
+                        p.grad.add_(val)  # tiny: [N <= 4, K] and [N]
+                    else:
+                        grads[j] = val.to(BF16)
         else:
             y = xs[L]
             g = (dout * (y > 0)).contiguous() if relus[L - 1] else dout

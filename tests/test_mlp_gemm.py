@@ -209,6 +209,14 @@ def test_skinny_head_matches_reference_and_is_reproducible(N, mask):
     torch.testing.assert_close(runs[0][3], 0.25 + dz.float().sum(0), rtol=1e-4, atol=1e-4)
     for x, y in zip(*runs):
         assert torch.equal(x, y)
+    # straight into bf16 gradient views: stored (first write of a backward), then accumulated
+    dWh, dbh = torch.full((N, K), 7.0, dtype=torch.bfloat16).cuda(), torch.full((N,), 7.0, dtype=torch.bfloat16).cuda()
+    g2, gT2 = torch.empty(M, K, dtype=torch.bfloat16).cuda(), torch.empty(K, M, dtype=torch.bfloat16).cuda()
+    skinny_bwd_bf16(dz.cuda(), a.cuda(), W.cuda(), mask, g2, gT2, dWh, dbh, accumulate=False)
+    torch.testing.assert_close(dWh.cpu().float(), (dz.float().t() @ a.float()).bfloat16().float(), rtol=1e-2, atol=1e-3)
+    torch.testing.assert_close(dbh.cpu().float(), dz.float().sum(0).bfloat16().float(), rtol=1e-2, atol=1e-3)
+    skinny_bwd_bf16(dz.cuda(), a.cuda(), W.cuda(), mask, g2, gT2, dWh, dbh, accumulate=True)
+    torch.testing.assert_close(dWh.cpu().float(), 2 * (dz.float().t() @ a.float()), rtol=2e-2, atol=2e-3)
 
 
 @gpu
