@@ -123,8 +123,11 @@ template <int F, int H>
 struct LaneState {
   using C = TinyCfg<F, H>;
   float w1[C::NSP], m1[C::NSP], v1[C::NSP];  // [W1 | b1][16w + (l&15)][slot_k(i, l>>4)]
-  float bw, mbw, vbw;                      // W2 element (lanes 0-3 of each DPP row)
-  float b2, mb2, vb2;                      // replicated in every lane
+  // {W2 element (lanes 0-3 of each DPP row), b2 (replicated in every lane)}: value, exp_avg,
+  // exp_avg_sq as 2-vectors, the form the packed Adam update works on.  (Six scalar fields read
+  // pairwise made the compiler combine overlapping vector loads of the struct, which kept it in
+  // memory -- promoted to LDS -- and put an LDS round trip into every step.)
+  f32x2 p2, m2, v2;
 };
 
 template <int F, int H>
@@ -140,12 +143,9 @@ DGT_DEVICE void load_state(LaneState<F, H>& st, const float* __restrict__ p, con
     st.v1[i] = (ok && v) ? v[gi] : 0.f;
   }
   const int bi = C::bw_index(w, lr, lq);
-  st.bw = bi >= 0 ? p[bi] : 0.f;
-  st.mbw = (bi >= 0 && m) ? m[bi] : 0.f;
-  st.vbw = (bi >= 0 && v) ? v[bi] : 0.f;
-  st.b2 = p[C::G_B2];
-  st.mb2 = m ? m[C::G_B2] : 0.f;
-  st.vb2 = v ? v[C::G_B2] : 0.f;
+  st.p2 = f32x2{bi >= 0 ? p[bi] : 0.f, p[C::G_B2]};
+  st.m2 = f32x2{(bi >= 0 && m) ? m[bi] : 0.f, m ? m[C::G_B2] : 0.f};
+  st.v2 = f32x2{(bi >= 0 && v) ? v[bi] : 0.f, v ? v[C::G_B2] : 0.f};
 }
 
 // Minibatch values for the lane's row b = l&15: x[b][slot_k(i, l>>4)] and y[b].  A padding row
@@ -192,10 +192,10 @@ DGT_DEVICE void wave_forward(const LaneState<F, H>& st, WaveSmem<F, H>& ws, floa
   // stage this step's rows for the weight-gradient MFMA (row-major, conflict-free stride)
 #pragma unroll
   for (int i = 0; i < C::NSL; ++i) ws.X[lr * C::SX + C::slot_k(i, lq)] = x[i];
-  w2v[0] = dpp_mov<0x150>(st.bw);  // row_newbcast: W2[4lq + r] from lane r of the DPP row
-  w2v[1] = dpp_mov<0x151>(st.bw);
-  w2v[2] = dpp_mov<0x152>(st.bw);
-  w2v[3] = dpp_mov<0x153>(st.bw);
+  w2v[0] = dpp_mov<0x150>(st.p2.x);  // row_newbcast: W2[4lq + r] from lane r of the DPP row
+  w2v[1] = dpp_mov<0x151>(st.p2.x);
+  w2v[2] = dpp_mov<0x152>(st.p2.x);
+  w2v[3] = dpp_mov<0x153>(st.p2.x);
   float pz = 0.f;
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
@@ -229,7 +229,7 @@ DGT_DEVICE StepGrads wave_backward(const LaneState<F, H>& st, WaveSmem<F, H>& ws
   float s = 0.f;
 #pragma unroll
   for (int ww = 0; ww < C::NW; ++ww) s += Zbuf[ww * 16 + lr];
-  const float z = s + st.b2;
+  const float z = s + st.p2.y;
   const bool valid = lr < Bt;
   // BCE-with-logits (torch: (1-y)*z - log_sigmoid(z)); d/dz = sigmoid(z) - y, times 1/B (mean)
   const float e = __expf(-fabsf(z));
@@ -514,14 +514,10 @@ DGT_DEVICE void adam_lane(LaneState<F, H>& st, const float (&gw1)[TinyCfg<F, H>:
     st.v1[i] = v.x;
     st.v1[i + 1] = v.y;
   }
-  f32x2 m = {st.mbw, st.mb2}, v = {st.vbw, st.vb2};
-  const f32x2 pn = adam_update_fast2<WD>(f32x2{st.bw, st.b2}, f32x2{gbw, gb2}, m, v, hp, step_size_neg, inv_bc2_sqrt);
-  st.bw = pn.x;
-  st.b2 = pn.y;
-  st.mbw = m.x;
-  st.mb2 = m.y;
-  st.vbw = v.x;
-  st.vb2 = v.y;
+  f32x2 m = st.m2, v = st.v2;
+  st.p2 = adam_update_fast2<WD>(st.p2, f32x2{gbw, gb2}, m, v, hp, step_size_neg, inv_bc2_sqrt);
+  st.m2 = m;
+  st.v2 = v;
 }
 
 template <int F, int H, bool SMALLB, int NP, bool WD, int LN, bool Z>
@@ -687,7 +683,7 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
           if (!late) {
             unpack_plain<F, H>(sum, inv_ws, gw1, gbw, gb2);
             adam_lane<F, H, WD>(st, gw1, gbw, gb2, a.hp, step_size_neg, inv_bc2_sqrt);
-            pack_plain<F, H>(st.w1, st.bw, st.b2, pay);
+            pack_plain<F, H>(st.w1, st.p2.x, st.p2.y, pay);
             xs_ag ^= xor_words<NPX>(pay);  // what every peer must receive
             for (int p = 0; p < ex.world_size; ++p) {
               if (p == ex.rank) continue;
@@ -712,7 +708,9 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
 #pragma unroll
           for (int k = 0; k < NPX; ++k) sum[k] = line_payload<NPX, LN>(v, k);
           xs_ag ^= xor_words<NPX>(sum);
-          unpack_plain<F, H>(sum, 1.0f, st.w1, st.bw, st.b2);
+          float bw, b2;
+          unpack_plain<F, H>(sum, 1.0f, st.w1, bw, b2);
+          st.p2 = f32x2{bw, b2};
         }
         if (late) sm.err = 1;
       }
@@ -754,17 +752,17 @@ __global__ __launch_bounds__((TinyCfg<F, H>::T)) void tiny_mlp_train_kernel(Tiny
   }
   const int bi = C::bw_index(w, lr, lq);
   if (bi >= 0) {
-    a.params[bi] = st.bw;
-    a.exp_avg[bi] = st.mbw;
-    a.exp_avg_sq[bi] = st.vbw;
+    a.params[bi] = st.p2.x;
+    a.exp_avg[bi] = st.m2.x;
+    a.exp_avg_sq[bi] = st.v2.x;
   }
   // b2 is replicated in every lane and stored once: under ZeRO-1 a lane's moments are current only
   // on the rank that owns it, so each rank stores b2's state from a lane it owns (lane = rank of
   // wave 0); the next launch loads it into every lane, and the owners carry on from current moments
   if (t == (Z ? ex.rank : 0)) {
-    a.params[C::G_B2] = st.b2;
-    a.exp_avg[C::G_B2] = st.mb2;
-    a.exp_avg_sq[C::G_B2] = st.vb2;
+    a.params[C::G_B2] = st.p2.y;
+    a.exp_avg[C::G_B2] = st.m2.y;
+    a.exp_avg_sq[C::G_B2] = st.v2.y;
   }
   __syncthreads();
   if (t == 0) {
