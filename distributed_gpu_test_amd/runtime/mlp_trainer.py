@@ -63,6 +63,7 @@ from __future__ import annotations
 
 from typing import Dict, List, Optional
 
+import contextlib
 import os
 
 import torch
@@ -197,8 +198,10 @@ class MLPTrainer:
         B, D = self.B, self.D
         self.a = [None] + [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(self.L)]
         self.aT = [None] + [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(self.L)]
-        self.g = [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(2)]
-        self.gT = [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(2)]
+        # three gradient buffers: with the side-stream wgrad+Adam (below) a layer's g^T is still being
+        # read while the next two dgrads write theirs
+        self.g = [torch.empty(B, D, dtype=torch.bfloat16, device=dev) for _ in range(3)]
+        self.gT = [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(3)]
         self.dz = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
 
@@ -219,6 +222,17 @@ class MLPTrainer:
         self._overlap = self.schedule == "overlap"
         self._opt_pending = False
         self.s_main = None
+        # A/B knobs of the fused single-rank step: the wgrad+Adam launches on a side stream beside the
+        # dgrads (DGT_MLP_WGA_SIDE=1), and the GEMM variant of each product (ops/gemm.py gemm_nt:
+        # 1 = 128x128 2-stage, 64 KiB of LDS, so two different kernels' blocks can share a CU)
+        self._wga_side = (dev.type == "cuda" and os.environ.get("DGT_MLP_WGA_SIDE", "0") == "1")
+        self._v_wga = int(os.environ.get("DGT_MLP_WGA_VARIANT", "0") or 0)
+        self._v_dgrad = int(os.environ.get("DGT_MLP_DGRAD_VARIANT", "0") or 0)
+        self._v_fwd = int(os.environ.get("DGT_MLP_FWD_VARIANT", "0") or 0)
+        if self._wga_side:
+            self.s_opt = torch.cuda.Stream(dev)
+            self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
+            self.ev_opt = [torch.cuda.Event() for _ in range(self.L)]
         if self._overlap:
             self.s_opt = torch.cuda.Stream(dev)
             self.s_comm = torch.cuda.Stream(dev)
@@ -310,13 +324,15 @@ class MLPTrainer:
         xT = self.XT[:, j * B:(j + 1) * B]
         y = self.Y[j * B:(j + 1) * B]
         ov = self._overlap
-        main = torch.cuda.current_stream(self.device) if ov else None
-        # forward: layer i waits only on its own update of the previous step
+        main = torch.cuda.current_stream(self.device) if (ov or self._wga_side) else None
+        # forward: layer i waits only on its own update of the previous step (and, on the side
+        # stream, every later layer's, which read aT[i + 1] and were enqueued first)
         prev = x
         for i in range(L):
             if self._opt_pending:
                 main.wait_event(self.ev_opt[i])
-            gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True)
+            gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True,
+                    variant=self._v_fwd)
             prev = self.a[i + 1]
         # head (+ its gradients, written in place: no zero fills)
         cur = 0
@@ -347,7 +363,8 @@ class MLPTrainer:
                 else:
                     self._reduce_layer(i, works)
             if i > 0:
-                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True)
+                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True,
+                        variant=self._v_dgrad)
                 cur ^= 1
             if ov:
                 self.ev_bwd[i].record(main)
@@ -382,19 +399,31 @@ class MLPTrainer:
         region moves 26 B/param (12 read + 14 written) instead of the wgrad store + flat Adam's
         2 + 28 B/param, and the update overlaps the other blocks' MFMA work."""
         args = self._adam_args()
+        side = self._wga_side
+        main = torch.cuda.current_stream(self.device) if side else None
         for i in reversed(range(self.L)):
             a_prevT = xT if i == 0 else self.aT[i]
+            nxt = (cur + 1) % 3
             rowsum_bf16(self.gT[cur], self.gb[i])
             if i > 0:
-                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True)
+                gemm_nt(self.g[cur], self.W[i], C=self.g[nxt], CT=self.gT[nxt], mask=self.a[i], b_kn=True,
+                        variant=self._v_dgrad)
             R, Cc = self.shapes[i]
             sl = slice(self.w_off[i], self.w_off[i] + R * Cc)
-            gemm_nt_adam_(self.gT[cur], a_prevT, self.master_w[sl].view(R, Cc), self.m_w[sl].view(R, Cc),
-                          self.v_w[sl].view(R, Cc), self.params_bf16[sl].view(R, Cc), *args,
-                          grad_scale=1.0 / self.world_size)
+            if side:  # after the dgrad (it read W_i) and with gT[cur] complete
+                self.ev_bwd[i].record(main)
+                self.s_opt.wait_event(self.ev_bwd[i])
+            with torch.cuda.stream(self.s_opt) if side else contextlib.nullcontext():
+                gemm_nt_adam_(self.gT[cur], a_prevT, self.master_w[sl].view(R, Cc), self.m_w[sl].view(R, Cc),
+                              self.v_w[sl].view(R, Cc), self.params_bf16[sl].view(R, Cc), *args,
+                              grad_scale=1.0 / self.world_size, variant=self._v_wga)
+                if side:
+                    self.ev_opt[i].record(self.s_opt)
             if i > 0:
-                cur ^= 1
+                cur = nxt
         adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *args, grad_scale=1.0 / self.world_size)
+        if side:
+            self._opt_pending = True
 
     # ------------------------------------------------------------------ checkpoints
     def _param_names(self) -> List[str]:
