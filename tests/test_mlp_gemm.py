@@ -354,3 +354,23 @@ def test_mlp_fused_adam_matches_unfused_fp32_grads():
     for a, b in zip(outs[0][:4], outs[1][:4]):
         assert torch.equal(a, b)
     assert outs[0][4] == outs[1][4]
+
+
+@gpu
+def test_mlp_side_stream_wgrad_adam_is_bitwise_in_line(monkeypatch):
+    """DGT_MLP_WGA_SIDE=1 moves each fused wgrad+Adam launch to a side stream beside the dgrads
+    (three rotating gradient buffers, the next forward waits per layer): a schedule change only."""
+    def run(side):
+        monkeypatch.setenv("DGT_MLP_WGA_SIDE", "1" if side else "0")
+        torch.manual_seed(0)
+        tr = MLPTrainer(SyntheticMLP(width=256, depth=3), batch_size=256, n_batches=2, lr=1e-3,
+                        device=torch.device("cuda"))
+        for s in range(4):
+            tr.step(s)
+        tr.join()
+        torch.cuda.synchronize()
+        return tr
+    a, b = run(False), run(True)
+    assert b._wga_side and not a._wga_side
+    assert torch.equal(a.master_w, b.master_w) and torch.equal(a.params_bf16, b.params_bf16)
+    assert torch.equal(a.m_w, b.m_w) and torch.equal(a.loss_acc, b.loss_acc)
