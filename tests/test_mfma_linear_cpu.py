@@ -76,3 +76,21 @@ def test_injected_module_on_cpu_falls_back_and_counts():
     n0 = sum(lin_ops.FALLBACKS.values())
     assert torch.equal(m(x), ref(x))
     assert sum(lin_ops.FALLBACKS.values()) == n0 + 1
+
+
+def test_first_write_stores_once_per_backward():
+    """engine_backward(grads_zero=True): the first write of a gradient view in that backward may
+    store (the bucket is zero), every later write of the same view must add -- a module called
+    twice before one backward writes its gradients twice; nested / later backwards start afresh."""
+    import torch
+    from distributed_gpu_test_amd.ops.linear import _first_write, engine_backward
+    buf = torch.zeros(64)
+    a, b = buf[:32], buf[32:]
+    assert not _first_write(a)  # outside an engine backward: always accumulate
+    with engine_backward(grads_zero=True):
+        assert _first_write(a) and _first_write(b)
+        assert not _first_write(a) and not _first_write(b)
+    with engine_backward(grads_zero=True):
+        assert _first_write(a)  # a new backward
+    with engine_backward(grads_zero=False):
+        assert not _first_write(a)  # the bucket already holds gradients (accumulation step)
