@@ -565,6 +565,11 @@ void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& ma
   const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
   g.adam.step_size_neg = (float)(-(lr / bc1));
   g.adam.bc2_sqrt = (float)std::sqrt(bc2);
+  static const int adam_nt = [] {  // nontemporal optimizer-state streams (A/B: DGT_ADAM_EPI_NT=0)
+    const char* e = std::getenv("DGT_ADAM_EPI_NT");
+    return e ? std::atoi(e) : 1;
+  }();
+  g.adam_nt = adam_nt;
   c10::DeviceGuard guard(A.device());
   DGT_CHECK_HIP(dgt::gemm_nt(g, dgt::kEpiAdam, stream_of(A), (int)variant));
 }

@@ -130,6 +130,7 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   void* CT;            // bf16 [N, ldct]
   const void* bias;     // fp32, or bf16 when bias_bf16
   int bias_bf16;
+  int adam_nt;         // kEpiAdam: nontemporal optimizer-state accesses
   const void* mask;
   int M, N, K;
   int lda, ldb, ldc, ldct, ldmask;

@@ -310,9 +310,18 @@ DGT_DEVICE void epilogue_adam(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN 
       const int idx = tid + NT * it, r = idx / (TN / 4), c = (idx % (TN / 4)) * 4;
       const f32x4 gr = *reinterpret_cast<const f32x4*>(tile + adam_slot<TN>(r, c));
       const long long o = (long long)(m0 + h * RP + r) * g.ldc + n0 + c;
-      f32x4 p = *reinterpret_cast<const f32x4*>(a.master + o);
-      f32x4 m = *reinterpret_cast<const f32x4*>(a.m + o);
-      f32x4 v = *reinterpret_cast<const f32x4*>(a.v + o);
+      // the optimizer state streams through once per step: nontemporal loads and stores keep it
+      // from evicting the GEMM operands other blocks are still reading (DGT_ADAM_EPI_NT=0: plain)
+      f32x4 p, m, v;
+      if (g.adam_nt) {
+        p = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.master + o));
+        m = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.m + o));
+        v = __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(a.v + o));
+      } else {
+        p = *reinterpret_cast<const f32x4*>(a.master + o);
+        m = *reinterpret_cast<const f32x4*>(a.m + o);
+        v = *reinterpret_cast<const f32x4*>(a.v + o);
+      }
       __hip_bfloat16 b[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
@@ -322,10 +331,16 @@ DGT_DEVICE void epilogue_adam(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN 
         v[e] = vv;
         b[e] = __float2bfloat16(p[e]);
       }
-      *reinterpret_cast<f32x4*>(a.master + o) = p;
-      *reinterpret_cast<f32x4*>(a.m + o) = m;
-      *reinterpret_cast<f32x4*>(a.v + o) = v;
-      *reinterpret_cast<uint2*>(lp + o) = *reinterpret_cast<const uint2*>(b);
+      if (g.adam_nt) {
+        __builtin_nontemporal_store(p, reinterpret_cast<f32x4*>(a.master + o));
+        __builtin_nontemporal_store(m, reinterpret_cast<f32x4*>(a.m + o));
+        __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(a.v + o));
+      } else {
+        *reinterpret_cast<f32x4*>(a.master + o) = p;
+        *reinterpret_cast<f32x4*>(a.m + o) = m;
+        *reinterpret_cast<f32x4*>(a.v + o) = v;
+      }
+      *reinterpret_cast<uint2*>(lp + o) = *reinterpret_cast<const uint2*>(b);  // read by the next forward
     }
   }
 }
