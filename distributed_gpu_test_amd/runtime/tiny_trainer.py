@@ -119,19 +119,23 @@ def zero1_checksum_mismatch(per_rank: List[torch.Tensor], world_size: int) -> Op
     parameters it all-gathered must equal every other rank's XOR of what it received.  Word 2t + 1:
     the owner's XOR of the gradients it received must equal the XOR over the other ranks of what
     they sent.  Returns a description of the first mismatch, or None."""
-    xs = torch.stack([t.view(-1, 2) for t in per_rank])  # [ranks, threads, 2]
-    for t in range(xs.shape[1]):
-        o = (t % 64) % world_size
-        ag = xs[:, t, 0]
-        if bool((ag != ag[o]).any()):
-            r = int(torch.nonzero(ag != ag[o])[0])
-            return f"parameters all-gathered by rank {o} arrived altered on rank {r} (thread {t})"
-        sent = 0
-        for p in range(world_size):
-            if p != o:
-                sent ^= int(xs[p, t, 1])
-        if sent != int(xs[o, t, 1]):
-            return f"gradients reduce-scattered to rank {o} arrived altered (thread {t})"
+    xs = torch.stack([t.view(-1, 2).to(torch.int64) for t in per_rank])  # [ranks, threads, 2]
+    n = xs.shape[1]
+    owner = (torch.arange(n) % 64) % world_size
+    ag = xs[:, :, 0]
+    bad_ag = (ag != ag.gather(0, owner.view(1, -1)).expand_as(ag)).any(0)
+    acc = torch.zeros(n, dtype=torch.int64)
+    for p in range(world_size):  # XOR over every rank: the owner's received word cancels the senders'
+        acc ^= xs[p, :, 1]
+    bad_rs = acc != 0
+    if bool(bad_ag.any()):
+        t = int(torch.nonzero(bad_ag)[0])
+        o = int(owner[t])
+        r = int(torch.nonzero(ag[:, t] != ag[o, t])[0])
+        return f"parameters all-gathered by rank {o} arrived altered on rank {r} (thread {t})"
+    if bool(bad_rs.any()):
+        t = int(torch.nonzero(bad_rs)[0])
+        return f"gradients reduce-scattered to rank {int(owner[t])} arrived altered (thread {t})"
     return None
 
 
