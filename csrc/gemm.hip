@@ -675,11 +675,31 @@ DGT_DEVICE int lane_off(bool is_a, int ld, int w, int i, int l) {
   return row * ld + swz(u, l & 7) * 8;
 }
 
+// One unit's two LDS-DMAs per thread, issued from asm in the saddr form: the unit's base in SGPRs,
+// the lane's 32-bit byte offset in a VGPR, so the register-full loop (128 accumulator VGPRs + 64 of
+// fragments) holds no 64-bit address temporaries.  Through the compiler builtin every 256x256
+// kernel spilled 1-3 VGPRs to scratch; from asm none does, 4-6 % faster at every size
+// (profiles/r3_gemm256_asm_ab.jsonl).  With every DMA of the loop in asm, the compiler tracks none
+// of them; the phase's explicit vmcnt waits and barriers order them (as in the 128x128 FR kernel).
 DGT_DEVICE void stage(const u16* ubase, const int (&off)[2], u16* unit_lds, int w) {
+  const unsigned long long b = reinterpret_cast<unsigned long long>(ubase);
+  // (readfirstlane returns int: each half goes through unsigned, or the low half would be
+  // sign-extended into the high one)
+  const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b), hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
+  const unsigned long long sb = ((unsigned long long)hi << 32) | lo;
+  const unsigned l0 = __builtin_amdgcn_readfirstlane(lds_byte_addr(unit_lds + w * 2 * 8 * BK));
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
-    __builtin_amdgcn_global_load_lds(reinterpret_cast<const int*>(ubase + off[i]),
-                                     reinterpret_cast<int*>(unit_lds + (w * 2 + i) * 8 * BK), 16, 0, 0);
+  for (int i = 0; i < 2; ++i) {
+    unsigned saved;
+    asm volatile(
+        "s_mov_b32 %0, m0\n\t"
+        "s_mov_b32 m0, %3\n\t"
+        "global_load_lds_dwordx4 %1, %2\n\t"
+        "s_mov_b32 m0, %0"
+        : "=&s"(saved)
+        : "v"((unsigned)off[i] * 2u), "s"(sb), "s"(l0 + (unsigned)(i * 8 * BK * 2))
+        : "memory");
+  }
 }
 
 DGT_DEVICE bf16x8 frag(const u16* unit_lds, int u, int c) {
@@ -793,7 +813,7 @@ DGT_DEVICE void iteration(const Ctx& c, int it, Frags& f, f32x4 (&acc)[8][4]) {
 template <int EPI>
 __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   using namespace g256;
-  __shared__ __attribute__((aligned(16))) u16 lds[2 * 4 * UNIT];  // ONE array (no extra vmcnt(0) waits)
+  __shared__ __attribute__((aligned(16))) u16 lds[2 * 4 * UNIT];
   const int tid = threadIdx.x;
   int tm, tn;
   tile_of_block(blockIdx.x, g.M / BM, g.N / BN, tm, tn);

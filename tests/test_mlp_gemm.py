@@ -122,6 +122,29 @@ def test_gemm_256_large_k_repeated():
 
 
 @gpu
+def test_gemm_256_asm_staging_high_address():
+    """The 256x256 kernel's asm DMAs take their base from SGPRs as two 32-bit halves: operands whose
+    address has bit 31 of the low word set (a sign-extension bug there faulted only on such
+    addresses) must give the fp32 reference's result."""
+    M, N, K = 512, 512, 1024
+    nbytes = (M + N) * K * 2
+    buf = torch.empty((1 << 32) + nbytes + 4096, dtype=torch.uint8, device="cuda")
+    low = buf.data_ptr() & 0xFFFFFFFF
+    off = 0 if (low >= 0x80000000 and low + nbytes < (1 << 32)) else ((0x80000000 - low) % (1 << 32))
+    off = (off + 255) // 256 * 256
+    A = buf[off:off + M * K * 2].view(torch.bfloat16).view(M, K)
+    B = buf[off + M * K * 2:off + nbytes].view(torch.bfloat16).view(N, K)
+    assert (A.data_ptr() & 0xFFFFFFFF) >= 0x80000000 and (B.data_ptr() & 0xFFFFFFFF) >= 0x80000000
+    g = torch.Generator().manual_seed(3)
+    A.copy_(torch.randn(M, K, generator=g).bfloat16())
+    B.copy_(torch.randn(N, K, generator=g).bfloat16())
+    C = torch.empty(M, N, dtype=torch.float32, device="cuda")
+    gemm_nt(A, B, C=C, out_f32=True, variant=2)
+    torch.testing.assert_close(C, A.float() @ B.float().t(), rtol=1e-3, atol=1e-2)
+    del buf
+
+
+@gpu
 def test_gemm_strided_operand():
     A = torch.randn(128, 64).to(torch.bfloat16).cuda()
     wide = torch.randn(128, 256).to(torch.bfloat16).cuda()
@@ -314,7 +337,7 @@ def test_trainer_comm_dtype_selects_gradient_wire(comm, want):
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 4), (512, 256, 1024, 4),
                                            (512, 256, 1024, 3), (512, 256, 1024, 5), (512, 256, 1024, 6), (256, 256, 128, 2),
-                                           (512, 768, 256, 2),
+                                           (512, 768, 256, 2), (512, 768, 1024, 2),
                                            (1024, 1024, 1024, 0)])
 @pytest.mark.parametrize("wd,adamw", [(0.0, False), (0.01, True)])
 def test_gemm_nt_adam_matches_reference(M, N, K, variant, wd, adamw):
