@@ -441,11 +441,12 @@ DGT_DEVICE void wait_vmcnt() {
 // fragments land.  After the per-K-tile barrier all waves otherwise move in lockstep through
 // read -> lgkmcnt(0) -> 4 MFMAs phases, so the LDS and the matrix cores take turns instead of
 // overlapping.
-// FR = 2: the same reads, with ONE barrier per two K-tiles (K % 128 == 0): the pair's both tiles
-// land behind one vmcnt(0) + barrier, the next pair is staged, then the two tiles are computed.
+// (Round-3 forms measured and removed, records in profiles/r3_gemm_m1024.jsonl: one barrier per two
+// K-tiles -- fastest hot, loses cold and in the MLP step; five stages, three K-tiles in flight -- no
+// gain in the step.  Source: git history, commits fd01625 and 45106c5.)
 template <int EPI, int S, int NW = 4, int FR = 0>
 __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
-  static_assert(S == 2 || S == 4 || (S == 5 && FR == 1), "two stages (2 blocks / CU), four, or five (FR: all 160 KiB)");
+  static_assert(S == 2 || S == 4, "two stages (2 blocks / CU) or four (1 block / CU)");
   constexpr int BK = GBK;
   constexpr bool KN = (EPI & kEpiBKN) != 0;      // B is [K, N]: staged as is, transposed reads
   constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
@@ -559,29 +560,6 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
     // LDS byte address of operand tile (stage b, operand o): integer arithmetic on one base
     const unsigned lds0 = FR ? __builtin_amdgcn_readfirstlane(lds_byte_addr(&lds[0][0][0])) : 0u;
     auto tile_at = [&](int b, int o) { return lds0 + (unsigned)((b * 2 + o) * GBM * BK * 2); };
-    if constexpr (FR == 2) {
-      static_assert(S == 4, "pairs of K-tiles in a 4-stage ring");
-      sa.issue_at(tile_at(0, 0));
-      sb.issue_at(tile_at(0, 1));
-      sa.issue_at(tile_at(1, 0));
-      sb.issue_at(tile_at(1, 1));
-      for (int kt = 0; kt < nk; kt += 2) {  // nk even (checked by the dispatcher)
-        const int b0 = kt & 3;
-        wait_vmcnt<0>();                    // this pair landed (the only loads in flight)
-        __builtin_amdgcn_sched_barrier(0);
-        __builtin_amdgcn_s_barrier();       // ... for every wave; the previous pair's buffers are free
-        __builtin_amdgcn_sched_barrier(0);
-        if (kt + 2 < nk) {
-          sa.issue_at(tile_at(b0 ^ 2, 0));
-          sb.issue_at(tile_at(b0 ^ 2, 1));
-          sa.issue_at(tile_at((b0 ^ 2) + 1, 0));
-          sb.issue_at(tile_at((b0 ^ 2) + 1, 1));
-        }
-        compute(b0);
-        compute(b0 + 1);
-      }
-      __builtin_amdgcn_s_barrier();
-    } else {
 #pragma unroll
     for (int p = 0; p < S - 1; ++p) {
       if (p < nk) {
@@ -599,7 +577,6 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       // tiles kt .. min(kt + S - 2, nk - 1) are in flight; retire tile kt
       const int ahead = min(AHEAD, nk - kt - 1);
       if (ahead >= AHEAD) wait_vmcnt<AHEAD * PER_TILE>();
-      else if (AHEAD > 2 && ahead == 2) wait_vmcnt<2 * PER_TILE>();
       else if (ahead == 1) wait_vmcnt<PER_TILE>();
       else wait_vmcnt<0>();
       __builtin_amdgcn_sched_barrier(0);
@@ -621,7 +598,6 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       buf = (buf + 1 == S) ? 0 : buf + 1;
     }
     __builtin_amdgcn_s_barrier();
-    }
   }
 
   // ---- epilogue: D col = l&15 (n), row = 4*(l>>4) + r (m)
@@ -873,13 +849,12 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 
 // variant: 0 = pick by shape (256x256 for >= 200 tiles, else 128x128 variant 3 for one-wave
 // grids, else variant 1), 1 = 128x128 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase,
-// 3 = variant 4 with front-loaded fragment reads (FR), 5 = FR with one barrier per two K-tiles
-// (K % 128 == 0, else 3), 6 = FR with five stages (160 KiB of LDS, 3 K-tiles in flight),
-// 4 = 128x128 4-stage with 8 waves (1 block / CU).  The round-2 variants measured slower or no
+// 3 = variant 4 with front-loaded fragment reads (FR), 4 = 128x128 4-stage with 8 waves (1 block /
+// CU; the FR kernel's bitwise oracle).  The round-2 variants measured slower or no
 // better inside the MLP step (3, 5-9) live in csrc/diag/gemm_variants_r2.h.
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 6) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 4) return hipErrorInvalidValue;
   const bool kn = (epi & kEpiBKN) != 0;  // only the 128x128 kernels read a [K, N] B operand
   const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0;
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks)
@@ -894,24 +869,18 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // a grid that fits the chip at one block per CU gains nothing from 2 blocks / CU: spend the LDS on
   // a deep (4-stage) pipeline and 8 waves instead (measured: 8 waves beat 4 on one-wave grids)
   const bool eight = !big && (variant >= 3 || (variant == 0 && grid <= 256));
-  const bool fr2 = eight && variant == 5 && g.K % 128 == 0;
-  const bool s5 = eight && variant == 6;  // FR with five stages (all 160 KiB of LDS): 3 K-tiles ahead
   // the shape rule's 128x128 choice is the front-loaded-reads form (variant 3): bit-identical to 4,
   // faster hot and cold and inside the MLP step (profiles/r3_gemm_m1024.jsonl)
-  const bool fr = eight && (variant == 0 || variant == 3 || (variant == 5 && !fr2));
+  const bool fr = eight && (variant == 0 || variant == 3);
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
-    if (fr2) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 2>), dim3(grid), dim3(512), 0, stream, g); \
-    else if (s5) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
-    else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
+    if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
     if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
-    else if (fr2) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 2>), dim3(grid), dim3(512), 0, stream, g); \
-    else if (s5) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
