@@ -18,8 +18,11 @@ One optimizer step, all on the GPU, no host sync:
 
 Schedules (``schedule=`` or ``DGT_MLP_SCHEDULE``):
 
-* ``"flat"``: after backward, ONE Adam launch over every weight (one rank: each layer's wgrad GEMM
-  applies Adam in its epilogue instead, ``gemm_nt_adam_``, so no gradient reaches memory);
+* ``"flat"``: after backward, ONE Adam launch over every weight (one rank, opt-in
+  ``fuse_adam=True`` / ``DGT_MLP_FUSED_ADAM=1``: each layer's wgrad GEMM applies Adam in its
+  epilogue instead, ``gemm_nt_adam_``, so no gradient reaches memory -- measured slower in round 3:
+  the epilogue streams the optimizer state at ~4.8 TB/s from one 8-wave block per CU, the flat
+  launch at ~5.6 TB/s, 1,153-1,168 vs 1,233-1,281 iters/s, profiles/r3_mlp_fused_vs_flat_adam.txt);
 * ``"overlap"`` (default for N > 1): layer l's update runs on a side HIP stream as soon as its
   collective has landed and backward no longer reads W_l, so the Adam of the upper layers
   overlaps the collectives of the lower ones and only the first layer's update is left after
@@ -188,10 +191,10 @@ class MLPTrainer:
         self.ghw, self.ghb = sview(self.grads_s, "head.weight"), sview(self.grads_s, "head.bias")
         # dgrad g_{l-1} = g_l . W_l: the GEMM reads W_l[out, in] as a [K, N] operand through
         # transposed LDS reads (gemm_nt(..., b_kn=True)), so no W^T exists at all
-        # single rank, ZeRO-0: nothing reduces the weight gradients, so each wgrad GEMM applies Adam
-        # to its tile in its epilogue (gemm_nt_adam_) and no gradient ever reaches memory
-        if fuse_adam is None:
-            fuse_adam = os.environ.get("DGT_MLP_FUSED_ADAM", "1") != "0"
+        # single rank, ZeRO-0, opt-in: nothing reduces the weight gradients, so each wgrad GEMM can
+        # apply Adam to its tile in its epilogue (gemm_nt_adam_) and no gradient reaches memory
+        if fuse_adam is None:  # measured: the flat Adam launch wins (module docstring)
+            fuse_adam = os.environ.get("DGT_MLP_FUSED_ADAM", "0") == "1"
         self.fused_adam = bool(fuse_adam and dev.type == "cuda" and not self.coll and self.zero_stage == 0)
 
         # ---- activations (both layouts) and gradient scratch
