@@ -856,7 +856,9 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   if (variant < 0 || variant > 4) return hipErrorInvalidValue;
   const bool kn = (epi & kEpiBKN) != 0;  // only the 128x128 kernels read a [K, N] B operand
-  const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0;
+  // (the 256x256 kernel's DMAs carry a 32-bit per-lane byte offset of up to 255 rows: row strides
+  // past 4M elements take the 128x128 kernels)
+  const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0 && g.lda <= (1 << 22) && g.ldb <= (1 << 22);
   // the big tile needs most of the 256 CUs busy: below ~200 tiles the 128 kernel (4x the blocks)
   // wins
   bool big = fits256 && !kn && (g.M / 256) * (g.N / 256) >= 200;
