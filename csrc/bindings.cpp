@@ -461,7 +461,8 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
 
 void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
-             const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant) {
+             const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
+             const std::optional<at::Tensor>& colsum) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
   TORCH_CHECK(variant >= 0 && variant <= 4,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
@@ -516,6 +517,13 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
     check_2d(*mask, "mask", at::kBFloat16, M, N);
     g.mask = mask->data_ptr();
     g.ldmask = (int)N;
+  }
+  if (colsum.has_value() && colsum->defined()) {  // bias-gradient partials of the (masked) output
+    TORCH_CHECK((epi & dgt::kEpiStoreT) && (epi & dgt::kEpiBKN) && (epi & dgt::kEpiMask) && variant != 2,
+                "dgt: colsum is formed by the [K, N] dgrad epilogue (mask + C^T) of the 128x128 kernels");
+    check_2d(*colsum, "colsum", at::kFloat, M / 128, N);
+    g.colsum = colsum->data_ptr<float>();
+    epi |= dgt::kEpiColSum;
   }
   c10::DeviceGuard guard(A.device());
   if (variant == 2)
@@ -645,7 +653,8 @@ void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor
 
 void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& y,
               const at::Tensor& dz, const at::Tensor& dw, const at::Tensor& db, const at::Tensor& loss_acc,
-              const at::Tensor& g, const at::Tensor& gT) {
+              const at::Tensor& g, const at::Tensor& gT, const std::optional<at::Tensor>& dw_part,
+              const std::optional<at::Tensor>& bias_part) {
   TORCH_CHECK(a.dim() == 2, "dgt: head activation must be 2-d");
   const int64_t B = a.size(0), D = a.size(1);
   TORCH_CHECK(B % 64 == 0 && D % 64 == 0, "dgt: head needs B, D % 64 == 0");
@@ -677,7 +686,42 @@ void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, co
   // stream-ordered workspace from the caching allocator (reused in place on later calls)
   at::Tensor scratch = at::empty({B + (B / 64) * D}, dz.options());
   h.scratch = scratch.data_ptr<float>();
+  h.dw_part = nullptr;
+  h.bias_part = nullptr;
+  // caller-owned partials (reduced later by partials_reduce_multi, so never in this call's scratch)
+  if (dw_part.has_value() && dw_part->defined()) {
+    check_2d(*dw_part, "dw_part", at::kFloat, B / 64, D);
+    h.dw_part = dw_part->data_ptr<float>();
+  }
+  if (bias_part.has_value() && bias_part->defined()) {
+    check_2d(*bias_part, "bias_part", at::kFloat, B / 64, D);
+    h.bias_part = bias_part->data_ptr<float>();
+  }
   DGT_CHECK_HIP(dgt::mlp_head(h, stream_of(a)));
+}
+
+// out_s (+ nothing: stored) = sum over t of part_s[t] for every segment, in one launch
+void partials_reduce_multi(at::TensorList parts, at::TensorList outs) {
+  TORCH_CHECK(parts.size() == outs.size() && parts.size() >= 1 && (int)parts.size() <= dgt::kMaxReduceSegs,
+              "dgt: partials_reduce_multi needs 1..", dgt::kMaxReduceSegs, " (part, out) pairs");
+  dgt::ReduceSegs r;
+  std::memset(&r, 0, sizeof(r));
+  r.count = (int)parts.size();
+  for (size_t s = 0; s < parts.size(); ++s) {
+    const at::Tensor &p = parts[s], &o = outs[s];
+    TORCH_CHECK(p.dim() == 2 && p.is_contiguous() && o.is_contiguous() && o.numel() == p.size(1) && p.size(1) % 4 == 0,
+                "dgt: partials_reduce_multi segment ", s, ": part [tiles, n] (n % 4 == 0) and a contiguous out [n]");
+    check_gpu(p, "part", at::kFloat);
+    check_gpu(o, "out", at::kFloat);
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(p.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(o.data_ptr()) % 16 == 0,
+                "dgt: partials_reduce_multi tensors must be 16-byte aligned");
+    r.part[s] = p.data_ptr<float>();
+    r.out[s] = o.data_ptr<float>();
+    r.tiles[s] = (int)p.size(0);
+    r.n[s] = (int)p.size(1);
+  }
+  c10::DeviceGuard guard(parts[0].device());
+  DGT_CHECK_HIP(dgt::partials_reduce_multi(r, stream_of(parts[0])));
 }
 
 // ------------------------------------------------------------------------------ IPC runtime
@@ -782,7 +826,7 @@ TORCH_LIBRARY(dgt, m) {
       &oneshot_allreduce);
   m.def(
       "gemm_nt(Tensor A, Tensor B, Tensor(a!)? C, Tensor(b!)? CT, Tensor? bias, Tensor? mask, int epi, "
-      "float alpha, int variant=0) -> ()",
+      "float alpha, int variant=0, Tensor(c!)? colsum=None) -> ()",
       &gemm_nt);
   m.def("transpose_bf16(Tensor inp, Tensor(a!) out) -> ()", &transpose_bf16);
   m.def("rowsum_bf16(Tensor inp, Tensor(a!) out, bool accumulate) -> ()", &rowsum_bf16);
@@ -793,8 +837,9 @@ TORCH_LIBRARY(dgt, m) {
       &skinny_bwd_bf16);
   m.def(
       "mlp_head(Tensor a, Tensor w, Tensor b0, Tensor y, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!) db, "
-      "Tensor(d!) loss_acc, Tensor(e!) g, Tensor(f!) gT) -> ()",
+      "Tensor(d!) loss_acc, Tensor(e!) g, Tensor(f!) gT, Tensor(g!)? dw_part=None, Tensor(h!)? bias_part=None) -> ()",
       &mlp_head);
+  m.def("partials_reduce_multi(Tensor[] parts, Tensor(a!)[] outs) -> ()", &partials_reduce_multi);
   m.def("ipc_alloc(int nbytes, int kind, int device) -> int", &ipc_alloc);
   m.def("ipc_handle(int ptr) -> Tensor", &ipc_handle);
   m.def("ipc_open(Tensor handle, int device) -> int", &ipc_open);

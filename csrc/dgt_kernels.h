@@ -110,6 +110,8 @@ enum GemmEpilogue : int {
   kEpiBKN = 64,        // B is given as [K, N] (N contiguous): C = A . B, read with transposed LDS reads
   kEpiAdam = 128,      // C is a weight GRADIENT consumed in place: Adam updates adam.master / m / v [M, ldc]
                        // and writes the bf16 copy adam.lp; no gradient is stored (single-rank ZeRO-0)
+  kEpiColSum = 256,    // with kEpiStoreT, 128x128 kernels: colsum[m0 / 128][n] = sum over the tile's 128
+                       // rows of the (bf16-rounded, masked) output: bias-gradient partials, fixed order
 };
 
 struct GemmAdam {      // kEpiAdam: fp32 master, moments and the bf16 compute copy of the [M, N] weight
@@ -136,6 +138,7 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   int lda, ldb, ldc, ldct, ldmask;
   float alpha;
   GemmAdam adam;       // kEpiAdam only (the gradient is alpha * A . B^T; ldc = row stride of the weight)
+  float* colsum;       // kEpiColSum: fp32 [M / 128, N]
   float* sk_slab;      // diag split-K kernel only (csrc/diag/gemm_variants_r2.h): fp32 partial tiles
   int* sk_flags;       // diag split-K kernel only: 2 ints per tile (arrivals, slab ready)
 };
@@ -178,8 +181,24 @@ struct HeadArgs {      // binary head of the synthetic MLP: Linear(D, 1) + BCE-w
   float* scratch;      // fp32 [B + (B / 64) * D] workspace: per-row loss terms, then per-row-tile dw partials
   void* g;             // bf16 [B, D] gradient wrt the last pre-activation
   void* gT;            // bf16 [D, B]
+  float* dw_part;      // optional fp32 [B / 64, D]: the dw partials land here and are NOT reduced (the
+                       // caller's partials_reduce_multi does it, with other sums, in one launch)
+  float* bias_part;    // optional fp32 [B / 64, D]: per-row-tile column sums of g (the gradient of the
+                       // last hidden layer's bias, before its reduction)
 };
 
 hipError_t mlp_head(const HeadArgs& h, hipStream_t stream);
+
+// Several fixed-order partial reductions in ONE launch: out_s[i] = sum over t (in order) of
+// part_s[t][i] (fp32), for up to kMaxReduceSegs segments s (n_s % 4 == 0, 16-byte aligned).
+constexpr int kMaxReduceSegs = 8;
+struct ReduceSegs {
+  const float* part[kMaxReduceSegs];
+  float* out[kMaxReduceSegs];
+  int tiles[kMaxReduceSegs];
+  int n[kMaxReduceSegs];
+  int count;
+};
+hipError_t partials_reduce_multi(const ReduceSegs& r, hipStream_t stream);
 
 }  // namespace dgt

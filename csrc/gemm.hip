@@ -407,6 +407,7 @@ DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][W
     u16* CT = static_cast<u16*>(g.CT);
     constexpr int CPC = TM / 8;  // 8-row chunks per column
     static_assert(CPC % 16 == 0 && NT % 64 == 0, "C^T read mapping: 16-chunk blocks per wave");
+    static_assert(!(EPI & kEpiColSum) || CPC == 16, "column sums: one 16-chunk block (128 rows) per column");
 #pragma unroll
     for (int it = 0; it < TN * CPC / NT; ++it) {
       // a wave reads 4 columns x 16 row chunks; each 32-lane half 4 columns x 8 row chunks
@@ -418,6 +419,18 @@ DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][W
       for (int e = 0; e < 4; ++e)
         w[e] = (unsigned)tile[etile<TN>(mc + 2 * e, n)] | ((unsigned)tile[etile<TN>(mc + 2 * e + 1, n)] << 16);
       *reinterpret_cast<uint4*>(CT + (long long)(n0 + n) * g.ldct + m0 + mc) = make_uint4(w[0], w[1], w[2], w[3]);
+      if constexpr ((EPI & kEpiColSum) != 0) {
+        // the column's 16 chunks sit in the 16 lanes that differ in lane bits 0-2 and 5: sum the
+        // lane's 8 values, then a fixed xor tree over those bits (the same order on every call)
+        float cs = 0.f;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) cs += bf2f((u16)(w[e] & 0xffff)) + __uint_as_float(w[e] & 0xffff0000u);
+        cs += __shfl_xor(cs, 1);
+        cs += __shfl_xor(cs, 2);
+        cs += __shfl_xor(cs, 4);
+        cs += __shfl_xor(cs, 32);
+        if ((q & 0x27) == 0) g.colsum[(long long)(m0 / TM) * g.N + n0 + n] = cs;
+      }
     }
   }
 }
@@ -855,7 +868,9 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   if (variant < 0 || variant > 4) return hipErrorInvalidValue;
-  const bool kn = (epi & kEpiBKN) != 0;  // only the 128x128 kernels read a [K, N] B operand
+  // only the 128x128 kernels read a [K, N] B operand or form column sums
+  const bool kn = (epi & (kEpiBKN | kEpiColSum)) != 0;
+  if ((epi & kEpiColSum) && (!(epi & kEpiStoreT) || !g.colsum)) return hipErrorInvalidValue;
   // (the 256x256 kernel's DMAs carry a 32-bit per-lane byte offset of up to 255 rows: row strides
   // past 4M elements take the 128x128 kernels)
   const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0 && g.lda <= (1 << 22) && g.ldb <= (1 << 22);
@@ -900,6 +915,7 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
     DGT_EPI_CASE(kEpiOutF32 | kEpiBias)                            // generic fp32 out
     DGT_EPI_CASE(kEpiAdam)                                         // wgrad consumed by Adam in place
     DGT_EPI_CASE_KN(kEpiMask | kEpiStoreT | kEpiBKN)               // dgrad straight from W[out, in]
+    DGT_EPI_CASE_KN(kEpiMask | kEpiStoreT | kEpiBKN | kEpiColSum)  // + the bias-gradient partials
     DGT_EPI_CASE_KN(kEpiBKN)                                       // plain A . B (input gradient)
     DGT_EPI_CASE_KN(kEpiStoreT | kEpiBKN)                          // dgrad, no ReLU below
     DGT_EPI_CASE_KN(kEpiOutF32 | kEpiBKN)
@@ -1082,7 +1098,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
                                                       const float* __restrict__ lrow, int B, int D,
                                                       u16* __restrict__ g, u16* __restrict__ gT,
                                                       float* __restrict__ dw_part, float* __restrict__ db,
-                                                      double* __restrict__ loss_acc) {
+                                                      double* __restrict__ loss_acc, float* __restrict__ bias_part) {
   // one wave per 64 x 64 tile; lane (rb, cg) owns the 8 x 8 block rows r0 + 8rb.., cols c0 + 8cg..:
   // eight 16-byte row loads of a, eight 16-byte g row stores (8 lanes = one 128-byte line) and
   // eight 16-byte g^T row stores (8 consecutive rows of one column): no LDS
@@ -1094,6 +1110,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
 #pragma unroll
   for (int k = 0; k < 8; ++k) v[k] = *reinterpret_cast<const uint4*>(a + (long long)(r + k) * D + c);
   float part[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+  float gsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of g (bias_part)
   u16 gb[8][8];
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
@@ -1105,6 +1122,7 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
       const float av = bf2f((u16)(e & 1 ? u[e >> 1] >> 16 : u[e >> 1] & 0xffff));
       part[e] += d * av;
       gb[k][e] = f2bf(av > 0.f ? d * wc[e] : 0.f);
+      gsum[e] += bf2f(gb[k][e]);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) o[q] = (unsigned)gb[k][2 * q] | ((unsigned)gb[k][2 * q + 1] << 16);
@@ -1132,6 +1150,21 @@ __global__ __launch_bounds__(256) void head_bwd_kernel(const u16* __restrict__ a
     o[0] = make_float4(part[0], part[1], part[2], part[3]);
     o[1] = make_float4(part[4], part[5], part[6], part[7]);
   }
+  if (bias_part) {  // the same fixed tree over the tile's 8 row blocks, for the column sums of g
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = gsum[e];
+      x += __shfl_xor(x, 8);
+      x += __shfl_xor(x, 16);
+      x += __shfl_xor(x, 32);
+      gsum[e] = x;
+    }
+    if (rb == 0) {
+      float4* o = reinterpret_cast<float4*>(bias_part + (long long)blockIdx.y * D + c);
+      o[0] = make_float4(gsum[0], gsum[1], gsum[2], gsum[3]);
+      o[1] = make_float4(gsum[4], gsum[5], gsum[6], gsum[7]);
+    }
+  }
   if (blockIdx.x == 0 && blockIdx.y == 0 && wv == 0) {  // db and the step's loss, in a fixed order
     float sd = 0.f, sl = 0.f;
     for (int i = l; i < B; i += 64) {
@@ -1152,12 +1185,14 @@ hipError_t mlp_head(const HeadArgs& h, hipStream_t stream) {
   hipLaunchKernelGGL(head_fwd_kernel, dim3(h.B / 4), dim3(256), 0, stream, static_cast<const u16*>(h.a), h.w,
                      h.b0, h.y, h.B, h.D, h.dz, h.scratch, h.dw);
   const int wpb = h.D % 256 == 0 ? 4 : 1;  // 4 tiles per block side by side when the width allows
+  float* dwp = h.dw_part ? h.dw_part : h.scratch + h.B;
   hipLaunchKernelGGL(head_bwd_kernel, dim3(h.D / (64 * wpb), h.B / 64), dim3(64 * wpb), 0, stream,
                      static_cast<const u16*>(h.a),
                      h.w, h.dz, h.scratch, h.B, h.D, static_cast<u16*>(h.g), static_cast<u16*>(h.gT),
-                     h.scratch + h.B, h.db, h.loss_acc);
+                     dwp, h.db, h.loss_acc, h.bias_part);
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (h.dw_part) return hipSuccess;  // the caller reduces the partials (partials_reduce_multi)
   return partials_reduce(h.scratch + h.B, h.dw, 0, h.B / 64, h.D, 0, stream);
 }
 

@@ -190,6 +190,43 @@ __global__ __launch_bounds__(64) void partials_reduce_kernel(const float* __rest
   }
 }
 
+// ReduceSegs: every segment's float4 columns in one grid; each thread finds its segment by a
+// uniform scan of <= kMaxReduceSegs prefix sums, then sums its column's tiles in order (the
+// partials_reduce order, so the same bits as separate launches).
+__global__ __launch_bounds__(64) void partials_reduce_multi_kernel(ReduceSegs r) {
+  int i = (blockIdx.x * 64 + threadIdx.x) * 4;
+  int s = 0;
+  while (s < r.count && i >= r.n[s]) i -= r.n[s++];
+  if (s >= r.count) return;
+  const float* part = r.part[s];
+  const int tiles = r.tiles[s], n = r.n[s];
+  float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+  for (int t0 = 0; t0 < tiles; t0 += 8) {
+    float4 p[8];
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (t0 + j < tiles) p[j] = *reinterpret_cast<const float4*>(part + (long long)(t0 + j) * n + i);
+#pragma unroll
+    for (int j = 0; j < 8; ++j)
+      if (t0 + j < tiles) acc.x += p[j].x, acc.y += p[j].y, acc.z += p[j].z, acc.w += p[j].w;
+  }
+  *reinterpret_cast<float4*>(r.out[s] + i) = acc;
+}
+
+hipError_t partials_reduce_multi(const ReduceSegs& r, hipStream_t stream) {
+  if (r.count < 1 || r.count > kMaxReduceSegs) return hipErrorInvalidValue;
+  long long total = 0;
+  for (int s = 0; s < r.count; ++s) {
+    if (r.n[s] <= 0 || r.n[s] % 4 || r.tiles[s] < 1 || (reinterpret_cast<uintptr_t>(r.part[s]) & 15) ||
+        (reinterpret_cast<uintptr_t>(r.out[s]) & 15))
+      return hipErrorInvalidValue;
+    total += r.n[s];
+  }
+  const dim3 grid((unsigned)((total / 4 + 63) / 64)), blk(64);
+  hipLaunchKernelGGL(partials_reduce_multi_kernel, grid, blk, 0, stream, r);
+  return hipGetLastError();
+}
+
 hipError_t partials_reduce(const float* part, void* out, int out_bf16, int tiles, int n, int accumulate,
                            hipStream_t stream) {
   if (n % 4 || tiles < 1 || (reinterpret_cast<uintptr_t>(part) & 15) ||

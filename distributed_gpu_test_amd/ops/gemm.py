@@ -21,7 +21,7 @@ EPI_BIAS, EPI_RELU, EPI_MASK, EPI_STORE_T, EPI_OUT_F32, EPI_ACCUMULATE, EPI_B_KN
 
 
 def gemm_nt_reference(A, B, C=None, CT=None, bias=None, mask=None, relu=False, out_f32=False,
-                      accumulate=False, alpha=1.0, b_kn=False):
+                      accumulate=False, alpha=1.0, b_kn=False, colsum=None):
     r = (A.float() @ (B.float() if b_kn else B.float().t())) * alpha
     if bias is not None:
         r = r + bias.float()
@@ -29,6 +29,8 @@ def gemm_nt_reference(A, B, C=None, CT=None, bias=None, mask=None, relu=False, o
         r = torch.relu(r)
     if mask is not None:
         r = torch.where(mask.float() > 0, r, torch.zeros_like(r))
+    if colsum is not None:  # per-128-row-tile column sums of the bf16-rounded output
+        colsum.copy_(r.to(torch.bfloat16).float().view(r.shape[0] // 128, 128, r.shape[1]).sum(1))
     if C is not None:
         if accumulate:
             C.copy_((C.float() + r).to(C.dtype))
@@ -45,7 +47,7 @@ _ENV_VARIANT = int(os.environ.get("DGT_GEMM_VARIANT", "0") or 0)
 def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, CT: Optional[torch.Tensor] = None,
             bias: Optional[torch.Tensor] = None, mask: Optional[torch.Tensor] = None, relu: bool = False,
             out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0,
-            b_kn: bool = False) -> None:
+            b_kn: bool = False, colsum: Optional[torch.Tensor] = None) -> None:
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage (2 blocks per CU),
     2 = 256x256 8-phase pipeline, 3 = variant 4 with front-loaded LDS fragment reads,
     4 = 128x128 tiles 4-stage with 8 waves (1 block per CU; variant 3's bitwise oracle).
@@ -54,16 +56,35 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
 
     ``b_kn=True``: B is given as ``[K, N]`` (N contiguous) and ``C = alpha * A @ B`` — the operand is
     staged as it lies and read with transposed LDS reads (128x128 kernels only).  ``accumulate``
-    adds into C (fp32, or bf16 summed in fp32 and rounded once)."""
+    adds into C (fp32, or bf16 summed in fp32 and rounded once).
+
+    ``colsum`` (fp32 ``[M // 128, N]``, the ``[K, N]`` dgrad with ``mask`` and ``CT`` only): each
+    128-row tile's column sums of the bf16 output -- the next layer's bias-gradient partials, formed
+    in the epilogue from the values already staged for ``CT`` (``partials_reduce_multi`` finishes
+    them)."""
     if not A.is_cuda:
-        gemm_nt_reference(A, B, C, CT, bias, mask, relu, out_f32, accumulate, alpha, b_kn)
+        gemm_nt_reference(A, B, C, CT, bias, mask, relu, out_f32, accumulate, alpha, b_kn, colsum)
         return
     epi = ((EPI_BIAS if bias is not None else 0) | (EPI_RELU if relu else 0) | (EPI_MASK if mask is not None else 0)
            | (EPI_STORE_T if CT is not None else 0) | (EPI_OUT_F32 if out_f32 else 0)
            | (EPI_ACCUMULATE if accumulate else 0) | (EPI_B_KN if b_kn else 0))
     if variant == 0 and _ENV_VARIANT and (A.shape[0] // 128) * ((B.shape[1] if b_kn else B.shape[0]) // 128) <= 256:
         variant = _ENV_VARIANT
-    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant))
+    require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant), colsum)
+
+
+def partials_reduce_multi(pairs) -> None:
+    """For every ``(part [tiles, n], out [n])`` pair (fp32): ``out = part.sum(0)``, the tiles
+    added in order -- all pairs in ONE launch (at most 8)."""
+    pairs = list(pairs)
+    if pairs[0][0].is_cuda:
+        require().partials_reduce_multi([p for p, _ in pairs], [o for _, o in pairs])
+        return
+    for p, o in pairs:
+        acc = torch.zeros_like(p[0])
+        for t in range(p.shape[0]):
+            acc += p[t]
+        o.copy_(acc.view(o.shape))
 
 
 def gemm_nt_adam_(A: torch.Tensor, B: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor,
@@ -134,11 +155,14 @@ def skinny_bwd_bf16(dz: torch.Tensor, a: torch.Tensor, w: torch.Tensor, mask: bo
         db.copy_(d.sum(0).to(db.dtype))
 
 
-def mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT) -> None:
+def mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT, dw_part=None, bias_part=None) -> None:
     """Linear(D,1) + BCE-with-logits (mean) forward and backward; dw, db are overwritten with the
-    head's gradients, loss_acc accumulates the mean loss."""
+    head's gradients, loss_acc accumulates the mean loss.  ``dw_part`` (fp32 ``[B // 64, D]``): the
+    per-64-row-tile dw partials are left there and dw is NOT written (``partials_reduce_multi``
+    finishes it); ``bias_part`` (same shape): per-tile column sums of g, the last hidden layer's
+    bias-gradient partials."""
     if a.is_cuda:
-        require().mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT)
+        require().mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT, dw_part, bias_part)
         return
     af = a.float()
     z = af @ w + b0
@@ -151,3 +175,8 @@ def mlp_head(a, w, b0, y, dz, dw, db, loss_acc, g, gT) -> None:
     gg = torch.outer(d, w) * (af > 0)
     g.copy_(gg.to(g.dtype))
     gT.copy_(gg.t().to(gT.dtype))
+    B, D = a.shape
+    if dw_part is not None:
+        dw_part.copy_((d.view(B // 64, 64, 1) * af.view(B // 64, 64, D)).sum(1))
+    if bias_part is not None:
+        bias_part.copy_(g.float().view(B // 64, 64, D).sum(1))

@@ -7,8 +7,9 @@ One optimizer step, all on the GPU, no host sync:
     forward   a_l = relu(a_{l-1} W_l^T + b_l)   gemm_nt epilogue: bias + ReLU + bf16 a_l and a_l^T
     head      z = a_L w + b, BCE, dz, g_L = dz w^T * 1[a_L > 0] (+ g_L^T), dw, db      (mlp_head)
     backward  dW_l = g_l^T a_{l-1}   -> bf16 (or fp32) gradient buffer                  (gemm_nt)
-              db_l = row sums of g_l^T                                              (rowsum_bf16)
               g_{l-1} = (g_l W_l) * 1[a_{l-1} > 0] (+ g_{l-1}^T)   epilogue: mask  (gemm_nt, b_kn)
+                        + per-128-row-tile column sums of g_{l-1}: db_{l-1} partials (colsum)
+              db_l, head dw: ONE fixed-order reduction of the partials (partials_reduce_multi)
               each layer's weight gradient leaves for its collective as soon as its wgrad is
               enqueued (RCCL over xGMI on the process group's stream): the collective overlaps
               the remaining backward GEMMs
@@ -75,7 +76,7 @@ import torch.distributed as dist
 from ..accelerator import get_accelerator
 from ..models.synthetic_mlp import SyntheticMLP, synthetic_batch_data
 from ..ops.adam import adam_flat_
-from ..ops.gemm import gemm_nt, gemm_nt_adam_, mlp_head, rowsum_bf16, transpose_bf16
+from ..ops.gemm import gemm_nt, gemm_nt_adam_, mlp_head, partials_reduce_multi, rowsum_bf16, transpose_bf16
 from ..parallel import comm
 from . import checkpoint as ckpt
 
@@ -207,6 +208,16 @@ class MLPTrainer:
         self.gT = [torch.empty(D, B, dtype=torch.bfloat16, device=dev) for _ in range(3)]
         self.dz = torch.empty(B, dtype=torch.float32, device=dev)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=dev)
+        # bias-gradient and head-dw partials: the dgrad epilogue leaves per-128-row-tile column sums
+        # of g_{l-1} (colsum), the head per-64-row-tile sums of g_{L-1} and of dz a; ONE fixed-order
+        # reduction launch after backward turns them into the small region's gradients (instead of
+        # a row-sum launch per layer and the head's own reduction)
+        # (the GPU kernels need B % 128 == 0 anyway; a CPU run with another batch takes per-layer row sums)
+        self._partials = B % 128 == 0
+        self.bpart = [torch.empty(B // 128, D, dtype=torch.float32, device=dev) if self._partials else None
+                      for _ in range(self.L - 1)]
+        self.bpart_top = torch.empty(B // 64, D, dtype=torch.float32, device=dev) if self._partials else None
+        self.hw_part = torch.empty(B // 64, D, dtype=torch.float32, device=dev) if self._partials else None
 
         # ---- synthetic data (different stream per rank: weak-scaling data parallelism)
         n = B * n_batches
@@ -340,7 +351,7 @@ class MLPTrainer:
         # head (+ its gradients, written in place: no zero fills)
         cur = 0
         mlp_head(self.a[L], self.hw, self.hb, y, self.dz, self.ghw, self.ghb, self.loss_acc, self.g[cur],
-                 self.gT[cur])
+                 self.gT[cur], dw_part=self.hw_part, bias_part=self.bpart_top)
         self.global_steps += 1
         if self.fused_adam:
             self._backward_fused_adam(xT, cur)
@@ -352,7 +363,8 @@ class MLPTrainer:
         for i in reversed(range(L)):
             a_prevT = xT if i == 0 else self.aT[i]
             gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=self.grad_dtype == torch.float32)
-            rowsum_bf16(self.gT[cur], self.gb[i])
+            if not self._partials:
+                rowsum_bf16(self.gT[cur], self.gb[i])
             if self.coll:
                 if ov:
                     self.ev_wgrad[i].record(main)
@@ -367,7 +379,7 @@ class MLPTrainer:
                     self._reduce_layer(i, works)
             if i > 0:
                 gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True,
-                        variant=self._v_dgrad)
+                        variant=self._v_dgrad, colsum=self.bpart[i - 1])
                 cur ^= 1
             if ov:
                 self.ev_bwd[i].record(main)
@@ -377,6 +389,7 @@ class MLPTrainer:
                 with torch.cuda.stream(self.s_opt):
                     self._update_layer(i)
                     self.ev_opt[i].record(self.s_opt)
+        self._reduce_small()
         if self.coll:  # biases + head: one small replicated bucket
             self._collective(dist.all_reduce, self.grads_s, works=works)
         for w in works:
@@ -395,6 +408,15 @@ class MLPTrainer:
             if self.zero_stage == 1:
                 self._allgather_params()
 
+    def _reduce_small(self) -> None:
+        """The small region's gradients from their partials, in one launch: every hidden bias (the
+        dgrads' and the head's column sums of g) and the head weight (the head's dz a partials)."""
+        L = self.L
+        if not self._partials:
+            return
+        partials_reduce_multi([(self.bpart_top, self.gb[L - 1])] + [(self.bpart[i], self.gb[i]) for i in range(L - 1)]
+                              + [(self.hw_part, self.ghw)])
+
     def _backward_fused_adam(self, xT: torch.Tensor, cur: int) -> None:
         """Single-rank backward + update: per layer, the bias-gradient row sums, the dgrad (it
         reads W_l, so it runs BEFORE W_l changes), then ONE launch that computes dW_l and applies
@@ -407,10 +429,11 @@ class MLPTrainer:
         for i in reversed(range(self.L)):
             a_prevT = xT if i == 0 else self.aT[i]
             nxt = (cur + 1) % 3
-            rowsum_bf16(self.gT[cur], self.gb[i])
+            if not self._partials:
+                rowsum_bf16(self.gT[cur], self.gb[i])
             if i > 0:
                 gemm_nt(self.g[cur], self.W[i], C=self.g[nxt], CT=self.gT[nxt], mask=self.a[i], b_kn=True,
-                        variant=self._v_dgrad)
+                        variant=self._v_dgrad, colsum=self.bpart[i - 1])
             R, Cc = self.shapes[i]
             sl = slice(self.w_off[i], self.w_off[i] + R * Cc)
             if side:  # after the dgrad (it read W_i) and with gT[cur] complete
@@ -424,6 +447,7 @@ class MLPTrainer:
                     self.ev_opt[i].record(self.s_opt)
             if i > 0:
                 cur = nxt
+        self._reduce_small()
         adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *args, grad_scale=1.0 / self.world_size)
         if side:
             self._opt_pending = True

@@ -396,3 +396,47 @@ def test_mlp_side_stream_wgrad_adam_is_bitwise_in_line(monkeypatch):
     assert b._wga_side and not a._wga_side
     assert torch.equal(a.master_w, b.master_w) and torch.equal(a.params_bf16, b.params_bf16)
     assert torch.equal(a.m_w, b.m_w) and torch.equal(a.loss_acc, b.loss_acc)
+
+
+@gpu
+def test_dgrad_colsum_and_head_partials():
+    """The bias-gradient partials: the [K, N] dgrad epilogue's per-128-row-tile column sums of its
+    bf16 output (colsum), the head's per-64-row-tile sums of g and of dz a, and their one-launch
+    fixed-order reduction (partials_reduce_multi: bitwise the in-order sum)."""
+    from distributed_gpu_test_amd.ops.gemm import partials_reduce_multi
+    g_ = torch.Generator().manual_seed(5)
+    M, N, K = 1024, 512, 256
+    A = torch.randn(M, K, generator=g_).bfloat16().cuda()
+    W = torch.randn(K, N, generator=g_).bfloat16().cuda()
+    mask = (torch.randn(M, N, generator=g_) > 0).bfloat16().cuda()
+    C = torch.empty(M, N, dtype=torch.bfloat16, device="cuda")
+    CT = torch.empty(N, M, dtype=torch.bfloat16, device="cuda")
+    cs = torch.full((M // 128, N), float("nan"), device="cuda")
+    gemm_nt(A, W, C=C, CT=CT, mask=mask, b_kn=True, colsum=cs)
+    want = C.float().view(M // 128, 128, N).sum(1)  # the kernel's own output, tile by tile
+    torch.testing.assert_close(cs, want, rtol=1e-5, atol=1e-4)
+    cs2 = torch.empty_like(cs)
+    gemm_nt(A, W, C=C, CT=CT, mask=mask, b_kn=True, colsum=cs2)
+    assert torch.equal(cs, cs2)  # fixed order
+    # head partials
+    B, D = 256, 512
+    a = torch.relu(torch.randn(B, D, generator=g_)).bfloat16().cuda()
+    w, b0 = (torch.randn(D, generator=g_) * 0.1).cuda(), torch.tensor([0.05]).cuda()
+    y = (torch.rand(B, generator=g_) > 0.5).float().cuda()
+    outs = [torch.zeros(B, device="cuda"), torch.zeros(D, device="cuda"), torch.zeros(1, device="cuda"),
+            torch.zeros(1, dtype=torch.float64, device="cuda"), torch.empty(B, D, dtype=torch.bfloat16, device="cuda"),
+            torch.empty(D, B, dtype=torch.bfloat16, device="cuda")]
+    dwp, bp = torch.empty(B // 64, D, device="cuda"), torch.empty(B // 64, D, device="cuda")
+    mlp_head(a, w, b0, y, *outs, dw_part=dwp, bias_part=bp)
+    dz, gh = outs[0], outs[4]
+    torch.testing.assert_close(bp, gh.float().view(B // 64, 64, D).sum(1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(dwp, (dz.view(B // 64, 64, 1) * a.float().view(B // 64, 64, D)).sum(1),
+                               rtol=1e-4, atol=1e-7)
+    # one launch, several segments, the tiles added in order
+    o1, o2, o3 = torch.empty(N, device="cuda"), torch.empty(D, device="cuda"), torch.empty(D, device="cuda")
+    partials_reduce_multi([(cs, o1), (bp, o2), (dwp, o3)])
+    for p, o in ((cs, o1), (bp, o2), (dwp, o3)):
+        acc = torch.zeros_like(p[0])
+        for t in range(p.shape[0]):
+            acc += p[t]
+        assert torch.equal(o, acc)
