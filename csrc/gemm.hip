@@ -641,10 +641,10 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 //   q0: A_lo x B_lo (reads A_lo, B_lo)   q1: A_lo x B_hi (reads B_hi)
 //   q2: A_hi x B_hi (reads A_hi)         q3: A_hi x B_lo (no reads)
 // Two LDS buffers (even / odd K-tile) = 128 KiB; one loop iteration = 8 phases = 2 K-tiles.  Each
-// phase issues ONE unit of staging (2 global_load_lds per thread), its LDS reads, then
-// `s_waitcnt vmcnt(10)` (every unit but the 5 newest has landed), barrier, MFMAs, barrier.  The
-// unit order below restages a unit at least one phase after its last read (WAR) and reads it at
-// least one phase after the wait that retires it (RAW), so loads stay in flight across 5 phases
+// phase issues ONE unit of staging (2 LDS-DMAs per thread), its LDS reads, then `s_waitcnt
+// vmcnt(8)` (every unit but the 4 newest has landed), ONE barrier, MFMAs.  The unit order below
+// restages a unit at least two phases after its last read (WAR, so no second barrier) and reads it
+// at least one phase after the wait that retires it (RAW), so loads stay in flight across 4 phases
 // and never drain in the main loop (cdna_hip_programming.md §5, "8-phase template").
 namespace g256 {
 constexpr int BM = 256, BN = 256, BK = 64, UNIT = 128 * BK;  // elements per unit
@@ -725,14 +725,20 @@ DGT_DEVICE void stage_unit(const Ctx& c, int kt, int buf) {
   stage(ubase, is_a ? c.offa : c.offb, c.lds + (buf * 4 + U) * UNIT, c.w);
 }
 
-// unit staged in phase P (1..8) of an iteration: ph1 -> the odd tile's A_hi; ph2..5 -> the next
-// even tile; ph6..8 -> the next odd tile's A_lo, B_lo, B_hi
+// unit staged in phase P (1..8) of an iteration: ph1, ph2 -> the odd tile's B_hi, A_hi; ph3..6 ->
+// the next even tile's A_lo, B_lo, B_hi, A_hi; ph7, ph8 -> the next odd tile's A_lo, B_lo.  Every
+// unit is restaged at least TWO phases after its last read and read at least five phases after it
+// is staged (four units in flight: vmcnt(8)).  A wave staging in phase S has passed barrier S-1,
+// which every wave reaches only after its reads of phase S-2 have landed (lgkmcnt(0) before its
+// MFMAs), so no WAR barrier after the MFMAs is needed: ONE barrier per 16 MFMAs.  (Round 2's order
+// -- one phase between a unit's last read and its restaging, five units in flight -- needed a
+// second barrier per phase and was 10-13 % slower at every size: profiles/r3_gemm256_asm_ab.jsonl.)
 template <int P>
 DGT_DEVICE void stage_phase(const Ctx& c, int it) {
-  constexpr int unit = P == 1 ? kAHi : P == 2 ? kALo : P == 3 ? kBLo : P == 4 ? kBHi : P == 5 ? kAHi
-                     : P == 6 ? kALo : P == 7 ? kBLo : kBHi;
-  constexpr int buf = (P == 1 || P >= 6) ? 1 : 0;
-  const int kt = P == 1 ? 2 * it + 1 : (P <= 5 ? 2 * it + 2 : 2 * it + 3);
+  constexpr int unit = P == 1 ? kBHi : P == 2 ? kAHi : P == 3 ? kALo : P == 4 ? kBLo : P == 5 ? kBHi
+                     : P == 6 ? kAHi : P == 7 ? kALo : kBLo;
+  constexpr int buf = (P <= 2 || P >= 7) ? 1 : 0;
+  const int kt = P <= 2 ? 2 * it + 1 : (P <= 6 ? 2 * it + 2 : 2 * it + 3);
   stage_unit<unit>(c, kt, buf);
 }
 
@@ -742,7 +748,8 @@ DGT_DEVICE void phase(const Ctx& c, int it, Frags& f, f32x4 (&acc)[8][4]) {
   constexpr int q = (P - 1) & 3;
   const u16* base = c.lds + buf * 4 * UNIT;
   const int lr = c.l & 15, lc = c.l >> 4;
-  if (!LAST || P == 1) stage_phase<P>(c, it);
+  // the last iteration stages only its own odd tile's remaining two units
+  if (!LAST || P <= 2) stage_phase<P>(c, it);
   if (q == 0 || q == 2) {
     const u16* ul = base + (q == 0 ? kALo : kAHi) * UNIT;
 #pragma unroll
@@ -762,9 +769,9 @@ DGT_DEVICE void phase(const Ctx& c, int it, Frags& f, f32x4 (&acc)[8][4]) {
       }
   }
   // retire the unit read next phase (see the schedule above); the last iteration stages nothing
-  // after phase 1, so its counts shrink as the pipeline drains
-  if (!LAST) wait_vm<10>();
-  else wait_vm<P == 1 ? 10 : P == 2 ? 8 : P == 3 ? 6 : P == 4 ? 4 : P == 5 ? 2 : 0>();
+  // after phase 2, so its counts shrink as the pipeline drains
+  if (!LAST) wait_vm<8>();
+  else wait_vm<P <= 3 ? 8 : P == 4 ? 4 : P == 5 ? 2 : 0>();
   __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
@@ -781,8 +788,6 @@ DGT_DEVICE void phase(const Ctx& c, int it, Frags& f, f32x4 (&acc)[8][4]) {
         acc[i0 + i][(hi_b ? 2 : 0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
             f.a[i][kk], hi_b ? f.bhi[j][kk] : f.blo[j][kk], acc[i0 + i][(hi_b ? 2 : 0) + j], 0, 0, 0);
   __builtin_amdgcn_s_setprio(0);
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_sched_barrier(0);
 }
 
@@ -838,8 +843,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   stage_unit<kAHi>(c, 0, 0);
   stage_unit<kALo>(c, 1, 1);
   stage_unit<kBLo>(c, 1, 1);
-  stage_unit<kBHi>(c, 1, 1);
-  wait_vm<10>();
+  wait_vm<8>();
   __builtin_amdgcn_s_barrier();
 
   const int nit = g.K / (2 * BK);

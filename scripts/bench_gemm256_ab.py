@@ -18,14 +18,17 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 from bench_gemm import bench  # noqa: E402
 
 variants = [int(x) for x in os.environ.get("VARIANTS", "2").split(",")]
+reps = int(os.environ.get("REPS", "1"))
 for M, N, K in [(4096, 4096, 4096), (8192, 8192, 8192), (4096, 4096, 1024)]:
     A = torch.randn(M, K, device="cuda").bfloat16()
     B = torch.randn(N, K, device="cuda").bfloat16()
     C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
     fl = 2.0 * M * N * K
-    for v in variants:
-        t = bench(lambda: gemm_nt(A, B, C=C, variant=v), iters=30, warmup=5)
-        print(json.dumps({"shape": [M, N, K], "arm": f"v{v}", "us": round(t * 1e6, 1), "TFLOPs": round(fl / t / 1e12, 1)}), flush=True)
+    for r in range(reps):
+        for v in variants:
+            t = bench(lambda: gemm_nt(A, B, C=C, variant=v), iters=30, warmup=5)
+            print(json.dumps({"shape": [M, N, K], "arm": f"v{v}", "rep": r, "us": round(t * 1e6, 1),
+                              "TFLOPs": round(fl / t / 1e12, 1)}), flush=True)
     t = bench(lambda: torch.matmul(A, B.t(), out=C), iters=30, warmup=5)
     print(json.dumps({"shape": [M, N, K], "arm": "hipBLASLt", "us": round(t * 1e6, 1), "TFLOPs": round(fl / t / 1e12, 1)}), flush=True)
     del A, B, C

@@ -54,6 +54,7 @@ gpu = pytest.mark.gpu
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 1), (512, 256, 1024, 1),
                                            (256, 256, 128, 2), (512, 768, 256, 2), (768, 512, 1152, 2),
+                                           (2048, 1024, 4096, 2),
                                            (128, 128, 64, 4), (384, 256, 192, 4), (512, 256, 1024, 4),
                                            (128, 128, 64, 3), (384, 256, 192, 3), (512, 256, 1024, 3),
                                            (256, 128, 128, 0), (1024, 512, 256, 0)])
