@@ -1,7 +1,8 @@
 // Flat fused Adam/AdamW: ONE launch over the engine's flat fp32 master buffer replaces torch's
 // seven _foreach_* multi-tensor launches plus the DeepSpeed 1/world_size scale and the host-side
 // bias-correction .item() syncs.  Memory-bound: 16-byte vector accesses on
-// every stream (Guideline 13), nontemporal hints (each byte is touched once), one float4 group per
+// every stream (Guideline 13), nontemporal hints on the state streams (each byte is touched once;
+// not on the 16-bit compute copy, which the next forward reads), one float4 group per
 // thread over a full grid.  On the bench MLP's 67M parameters (profiles/r1_adam_v8_ab.txt): 5.41 TB/s
 // with fp32 gradients, 6.43 TB/s with bf16 gradients where the streaming hints pay (6.12 without).
 // The round-1/2 loop-shape variants (two groups per thread, 8-element groups, the Adam + W^T matrix
@@ -69,7 +70,7 @@ template <bool NT> struct Vec4<__half, NT> {
   }
 };
 
-template <typename GT, typename LT, bool NT>
+template <typename GT, typename LT, bool NT, bool LPNT = NT>
 DGT_DEVICE f32x4 adam_group(const AdamFlatArgs& a, const GT* __restrict__ grad, LT* __restrict__ lp, long long o,
                             float scale, float step_size_neg, float bc2_sqrt) {
   f32x4 p = Vec4<float, NT>::load(a.master + o), g = Vec4<GT, NT>::load(grad + o);
@@ -84,7 +85,7 @@ DGT_DEVICE f32x4 adam_group(const AdamFlatArgs& a, const GT* __restrict__ grad, 
   Vec4<float, NT>::store(a.master + o, p);
   Vec4<float, NT>::store(a.exp_avg + o, m);
   Vec4<float, NT>::store(a.exp_avg_sq + o, v);
-  if (lp) Vec4<LT, NT>::store(lp + o, p);
+  if (lp) Vec4<LT, LPNT>::store(lp + o, p);
   return p;
 }
 
@@ -117,8 +118,12 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   const GT* __restrict__ grad = static_cast<const GT*>(a.grad);
   LT* __restrict__ lp = static_cast<LT*>(a.param_lp);
   const long long stride = (long long)gridDim.x * blockDim.x;
+  // the state streams are nontemporal; the 16-bit compute copy is stored with the default policy:
+  // its 8-byte lane pieces then merge into whole lines in L2 (streamed, they went out as partial-line
+  // writes) and it stays in the Infinity Cache for the next forward -- 302 -> 280 us over the bench
+  // MLP's 67M weights (profiles/r3_adam_lp_policy_ab.txt)
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride)
-    adam_group<GT, LT, true>(a, grad, lp, 4 * i, scale, step_size_neg, bc2_sqrt);
+    adam_group<GT, LT, true, false>(a, grad, lp, 4 * i, scale, step_size_neg, bc2_sqrt);
 }
 
 template <typename GT, typename LT>

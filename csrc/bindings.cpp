@@ -464,10 +464,10 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
              const std::optional<at::Tensor>& colsum) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK(variant >= 0 && variant <= 4,
+  TORCH_CHECK(variant >= 0 && variant <= 5,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
-              "fragment reads) or 4 (128x128, 4 stages, 8 waves); the round-2 variants live in "
-              "csrc/diag/gemm_variants_r2.h");
+              "fragment reads), 4 (128x128, 4 stages, 8 waves) or 5 (software-pipelined reads); the round-2 "
+              "variants live in csrc/diag/gemm_variants_r2.h");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
@@ -536,7 +536,7 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
 void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& master, const at::Tensor& exp_avg,
                   const at::Tensor& exp_avg_sq, const at::Tensor& param_lp, int64_t step, double lr, double beta1,
                   double beta2, double eps, double weight_decay, bool adamw, double grad_scale, int64_t variant) {
-  TORCH_CHECK(variant >= 0 && variant <= 4 && step >= 1, "dgt: gemm_nt_adam needs variant 0 .. 4 and step >= 1");
+  TORCH_CHECK(variant >= 0 && variant <= 5 && step >= 1, "dgt: gemm_nt_adam needs variant 0 .. 5 and step >= 1");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt_adam needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {

@@ -457,9 +457,13 @@ DGT_DEVICE void wait_vmcnt() {
 // (Round-3 forms measured and removed, records in profiles/r3_gemm_m1024.jsonl: one barrier per two
 // K-tiles -- fastest hot, loses cold and in the MLP step; five stages, three K-tiles in flight -- no
 // gain in the step.  Source: git history, commits fd01625 and 45106c5.)
+// FR = 3 (SP, software-pipelined reads; S = 5, all 160 KiB of LDS): K-tile kt+1's fragments are read
+// into a second register set while tile kt's MFMAs run, so no MFMA waits on an LDS round trip of
+// its own K-tile; the barrier of step kt publishes tile kt+1 (one K-tile earlier than FR = 1), and
+// five stages keep the same two to three K-tiles of staging in flight.
 template <int EPI, int S, int NW = 4, int FR = 0>
 __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
-  static_assert(S == 2 || S == 4, "two stages (2 blocks / CU) or four (1 block / CU)");
+  static_assert(S == 2 || S == 4 || (S == 5 && FR == 3), "two stages (2 blocks / CU), four (1 block / CU), or SP");
   constexpr int BK = GBK;
   constexpr bool KN = (EPI & kEpiBKN) != 0;      // B is [K, N]: staged as is, transposed reads
   constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
@@ -565,6 +569,92 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
     }
+  } else if constexpr (FR == 3) {
+    static_assert(S == 5 && NW == 8, "SP: five stages, eight waves");
+    constexpr int PER_TILE = 2 * (16 / NW);
+    Stager<NW, false, true> sa(A, g.lda, m0, w, l);
+    Stager<NW, KN, true> sb(B, g.ldb, n0, w, l);
+    const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_byte_addr(&lds[0][0][0]));
+    auto tile_at = [&](int b, int o) { return lds0 + (unsigned)((b * 2 + o) * GBM * BK * 2); };
+    struct Fr {
+      bf16x8 a[BK / 32][4];
+      bf16x8 b[BK / 32][NJ];
+    };
+    auto read_frags = [&](int buf, Fr& fr) {
+      const u16* As = lds[buf][0];
+      const u16* Bs = lds[buf][1];
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        const int chunk = kk * 4 + (l >> 4);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) {
+          if constexpr (KN) fr.b[kk][j] = read_frag_kn_fr(Bs, kk * 32, wc * WN + j * 16, l);
+          else fr.b[kk][j] = read_frag<BK>(Bs, wc * WN + j * 16 + (l & 15), chunk);
+        }
+#pragma unroll
+        for (int i = 0; i < 4; ++i) fr.a[kk][i] = read_frag<BK>(As, wr * 64 + i * 16 + (l & 15), chunk);
+      }
+    };
+    auto mfmas = [&](const Fr& fr) {
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(fr.a[kk][i], fr.b[kk][j], acc[i][j], 0, 0, 0);
+    };
+    // prologue: tiles 0..3 staged, tile 0 retired and published, its fragments read
+#pragma unroll
+    for (int p = 0; p < 4; ++p) {
+      if (p < nk) {
+        sa.issue_at(tile_at(p, 0));
+        sb.issue_at(tile_at(p, 1));
+      }
+    }
+    {
+      const int newer = min(3, nk - 1);  // tiles staged after tile 0
+      if (newer >= 3) wait_vmcnt<3 * PER_TILE>();
+      else if (newer == 2) wait_vmcnt<2 * PER_TILE>();
+      else if (newer == 1) wait_vmcnt<PER_TILE>();
+      else wait_vmcnt<0>();
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();
+    __builtin_amdgcn_sched_barrier(0);
+    Fr f0, f1;
+    read_frags(0, f0);
+    int rb = 1, nb = 4;  // stage of tile kt + 1, stage the next staged tile lands in (tile % 5)
+    // one step: publish tile kt + 1 (its own wait + the barrier), stage tile kt + 4 into the stage
+    // tile kt - 1 left (its fragments were consumed by step kt - 1, which every wave has finished),
+    // read tile kt + 1 into `nxt`, then tile kt's MFMAs from `cur`
+    auto step = [&](int kt, const Fr& cur, Fr& nxt) {
+      if (kt + 1 < nk) {
+        const int newer = min(2, nk - kt - 2);  // tiles staged after tile kt + 1
+        if (newer >= 2) wait_vmcnt<2 * PER_TILE>();
+        else if (newer == 1) wait_vmcnt<PER_TILE>();
+        else wait_vmcnt<0>();
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        __builtin_amdgcn_sched_barrier(0);
+        if (kt + 4 < nk) {
+          sa.issue_at(tile_at(nb, 0));
+          sb.issue_at(tile_at(nb, 1));
+        }
+        nb = (nb + 1 == S) ? 0 : nb + 1;
+        read_frags(rb, nxt);
+        rb = (rb + 1 == S) ? 0 : rb + 1;
+        // (the MFMAs inside each branch: after a join the compiler could only wait lgkmcnt(0))
+        mfmas(cur);
+      } else {
+        mfmas(cur);
+      }
+    };
+    for (int kt = 0; kt < nk; kt += 2) {  // nk even (the dispatcher's condition): static register sets
+      step(kt, f0, f1);
+      step(kt + 1, f1, f0);
+    }
+    __builtin_amdgcn_s_barrier();
   } else {
     constexpr int PER_TILE = 2 * (16 / NW);  // glds per thread per K-tile (A and B)
     constexpr int AHEAD = S - 2;             // K-tiles left in flight past the one being retired
@@ -864,14 +954,15 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   }
 }
 
-// variant: 0 = pick by shape (256x256 for >= 200 tiles, else 128x128 variant 3 for one-wave
-// grids, else variant 1), 1 = 128x128 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase,
-// 3 = variant 4 with front-loaded fragment reads (FR), 4 = 128x128 4-stage with 8 waves (1 block /
-// CU; the FR kernel's bitwise oracle).  The round-2 variants measured slower or no
+// variant: 0 = pick by shape (256x256 for >= 200 tiles, else for one-wave grids the 128x128 variant
+// 5 for a [K, N] B operand with K % 128 == 0 and variant 3 otherwise, else variant 1), 1 = 128x128
+// 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase, 3 = variant 4 with front-loaded fragment
+// reads (FR), 4 = 128x128 4-stage with 8 waves (1 block / CU; the FR kernels' bitwise oracle),
+// 5 = software-pipelined fragment reads (SP, five stages; K % 128 == 0, else 3).  The round-2 variants measured slower or no
 // better inside the MLP step (3, 5-9) live in csrc/diag/gemm_variants_r2.h.
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 4) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 5) return hipErrorInvalidValue;
   // only the 128x128 kernels read a [K, N] B operand or form column sums
   const bool kn = (epi & (kEpiBKN | kEpiColSum)) != 0;
   if ((epi & kEpiColSum) && (!(epi & kEpiStoreT) || !g.colsum)) return hipErrorInvalidValue;
@@ -892,16 +983,22 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   const bool eight = !big && (variant >= 3 || (variant == 0 && grid <= 256));
   // the shape rule's 128x128 choice is the front-loaded-reads form (variant 3): bit-identical to 4,
   // faster hot and cold and inside the MLP step (profiles/r3_gemm_m1024.jsonl)
-  const bool fr = eight && (variant == 0 || variant == 3);
+  // the [K, N] dgrad takes the software-pipelined reads (variant 5: in the MLP step 46.1 vs 48.0 us,
+  // hot 41.2 vs 47.1); the NT forward keeps the front-loaded reads (44.5 vs 43.6 us in the step)
+  // (profiles/r3_gemm_sp_ab.txt)
+  const bool sp = eight && g.K % 128 == 0 && (variant == 5 || (variant == 0 && (epi & kEpiBKN) != 0));
+  const bool fr = eight && !sp && (variant == 0 || variant == 3 || variant == 5);
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
-    if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
+    if (sp) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 3>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \
     break;
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
     if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
+    else if (sp) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 3>), dim3(grid), dim3(512), 0, stream, g); \
     else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \

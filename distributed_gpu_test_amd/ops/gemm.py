@@ -50,7 +50,9 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
             b_kn: bool = False, colsum: Optional[torch.Tensor] = None) -> None:
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage (2 blocks per CU),
     2 = 256x256 8-phase pipeline, 3 = variant 4 with front-loaded LDS fragment reads,
-    4 = 128x128 tiles 4-stage with 8 waves (1 block per CU; variant 3's bitwise oracle).
+    4 = 128x128 tiles 4-stage with 8 waves (1 block per CU; variant 3's bitwise oracle),
+    5 = software-pipelined fragment reads (the next K-tile's fragments read during this one's MFMAs,
+    five LDS stages; K % 128 == 0, else 3) -- the shape rule's choice for the ``b_kn`` dgrad.
     ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
     the shape rule gives to the 128x128 kernels).
 

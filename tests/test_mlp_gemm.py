@@ -57,6 +57,8 @@ gpu = pytest.mark.gpu
                                            (2048, 1024, 4096, 2),
                                            (128, 128, 64, 4), (384, 256, 192, 4), (512, 256, 1024, 4),
                                            (128, 128, 64, 3), (384, 256, 192, 3), (512, 256, 1024, 3),
+                                           (128, 128, 128, 5), (384, 256, 256, 5), (512, 256, 1024, 5),
+                                           (384, 256, 192, 5),
                                            (256, 128, 128, 0), (1024, 512, 256, 0)])
 @pytest.mark.parametrize("epi", ["plain", "bias_relu_T", "bias_T", "bias", "bf16bias_relu_T", "mask_T", "f32", "f32_acc",
                                  "bf16_acc"])
@@ -180,7 +182,7 @@ def test_transpose_rowsum_head():
 
 @gpu
 @pytest.mark.parametrize("kn", [False, True])
-@pytest.mark.parametrize("fr", [3])
+@pytest.mark.parametrize("fr", [3, 5])
 def test_gemm_variant3_is_bitwise_variant4(kn, fr):
     """Front-loaded fragment reads (variant 3) change the schedule only: same MFMAs in the same
     order, so every epilogue output equals variant 4's bit for bit."""
@@ -285,7 +287,8 @@ def test_trainer_overlap_schedule_is_bitwise_serial():
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 1), (128, 128, 64, 4),
                                            (384, 256, 192, 4), (512, 256, 1024, 4), (256, 512, 512, 0),
-                                           (128, 128, 64, 3), (384, 256, 192, 3), (512, 256, 1024, 3)])
+                                           (128, 128, 64, 3), (384, 256, 192, 3), (512, 256, 1024, 3),
+                                           (128, 128, 128, 5), (384, 256, 256, 5), (512, 256, 1024, 5)])
 @pytest.mark.parametrize("epi", ["plain", "mask_T", "T", "f32"])
 def test_gemm_b_kn_matches_reference(M, N, K, variant, epi):
     """B given as [K, N] (the dgrad reading W[out, in] directly through transposed LDS reads)."""
@@ -306,7 +309,7 @@ def test_gemm_b_kn_matches_reference(M, N, K, variant, epi):
 
 
 @gpu
-@pytest.mark.parametrize("variant", [1, 3, 4])
+@pytest.mark.parametrize("variant", [1, 3, 4, 5])
 def test_gemm_b_kn_identity_asymmetric(variant):
     # A = I: C must equal B exactly, catching any transposed / swizzled fragment read
     n = 256
@@ -333,7 +336,7 @@ def test_trainer_comm_dtype_selects_gradient_wire(comm, want):
 
 @gpu
 @pytest.mark.parametrize("M,N,K,variant", [(128, 128, 64, 1), (256, 384, 128, 4), (512, 256, 1024, 4),
-                                           (512, 256, 1024, 3), (256, 256, 128, 2),
+                                           (512, 256, 1024, 3), (512, 256, 1024, 5), (256, 256, 128, 2),
                                            (512, 768, 256, 2), (512, 768, 1024, 2),
                                            (1024, 1024, 1024, 0)])
 @pytest.mark.parametrize("wd,adamw", [(0.0, False), (0.01, True)])
