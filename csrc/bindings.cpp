@@ -700,8 +700,13 @@ void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, co
   DGT_CHECK_HIP(dgt::mlp_head(h, stream_of(a)));
 }
 
-// out_s (+ nothing: stored) = sum over t of part_s[t] for every segment, in one launch
-void partials_reduce_multi(at::TensorList parts, at::TensorList outs) {
+// out_s (+ nothing: stored) = sum over t of part_s[t] for every segment, in one launch; with
+// `grads` given, also the Adam step of master / exp_avg / exp_avg_sq on the outs' elements (their
+// offsets inside `grads`), as adam_flat would over that region
+void partials_reduce_multi(at::TensorList parts, at::TensorList outs, const std::optional<at::Tensor>& grads,
+                           const std::optional<at::Tensor>& master, const std::optional<at::Tensor>& exp_avg,
+                           const std::optional<at::Tensor>& exp_avg_sq, int64_t step, double lr, double beta1,
+                           double beta2, double eps, double weight_decay, bool adamw, double grad_scale) {
   TORCH_CHECK(parts.size() == outs.size() && parts.size() >= 1 && (int)parts.size() <= dgt::kMaxReduceSegs,
               "dgt: partials_reduce_multi needs 1..", dgt::kMaxReduceSegs, " (part, out) pairs");
   dgt::ReduceSegs r;
@@ -720,8 +725,33 @@ void partials_reduce_multi(at::TensorList parts, at::TensorList outs) {
     r.tiles[s] = (int)p.size(0);
     r.n[s] = (int)p.size(1);
   }
+  dgt::ReduceAdam ad;
+  std::memset(&ad, 0, sizeof(ad));
+  if (grads.has_value() && grads->defined()) {
+    TORCH_CHECK(master.has_value() && exp_avg.has_value() && exp_avg_sq.has_value() && step >= 1,
+                "dgt: partials_reduce_multi's Adam needs master, exp_avg, exp_avg_sq and step >= 1");
+    for (const at::Tensor* t : {&*grads, &*master, &*exp_avg, &*exp_avg_sq}) {
+      check_gpu(*t, "adam region", at::kFloat);
+      TORCH_CHECK(t->is_contiguous() && t->numel() == grads->numel() && reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0,
+                  "dgt: partials_reduce_multi's Adam region tensors must be contiguous, equal-sized, 16-byte aligned");
+    }
+    const float* gb = grads->data_ptr<float>();
+    for (int s = 0; s < r.count; ++s)
+      TORCH_CHECK(r.out[s] >= gb && r.out[s] + r.n[s] <= gb + grads->numel(),
+                  "dgt: partials_reduce_multi with Adam: every out must lie inside grads");
+    ad.on = 1;
+    ad.grads = gb;
+    ad.master = master->data_ptr<float>();
+    ad.m = exp_avg->data_ptr<float>();
+    ad.v = exp_avg_sq->data_ptr<float>();
+    ad.hp = make_hyper(lr, beta1, beta2, eps, weight_decay, adamw);
+    const double bc1 = 1.0 - std::pow(beta1, (double)step), bc2 = 1.0 - std::pow(beta2, (double)step);
+    ad.step_size_neg = (float)(-(lr / bc1));
+    ad.bc2_sqrt = (float)std::sqrt(bc2);
+    ad.grad_scale = (float)grad_scale;
+  }
   c10::DeviceGuard guard(parts[0].device());
-  DGT_CHECK_HIP(dgt::partials_reduce_multi(r, stream_of(parts[0])));
+  DGT_CHECK_HIP(dgt::partials_reduce_multi(r, ad, stream_of(parts[0])));
 }
 
 // ------------------------------------------------------------------------------ IPC runtime
@@ -839,7 +869,11 @@ TORCH_LIBRARY(dgt, m) {
       "mlp_head(Tensor a, Tensor w, Tensor b0, Tensor y, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!) db, "
       "Tensor(d!) loss_acc, Tensor(e!) g, Tensor(f!) gT, Tensor(g!)? dw_part=None, Tensor(h!)? bias_part=None) -> ()",
       &mlp_head);
-  m.def("partials_reduce_multi(Tensor[] parts, Tensor(a!)[] outs) -> ()", &partials_reduce_multi);
+  m.def(
+      "partials_reduce_multi(Tensor[] parts, Tensor(a!)[] outs, Tensor? grads=None, Tensor(b!)? master=None, "
+      "Tensor(c!)? exp_avg=None, Tensor(d!)? exp_avg_sq=None, int step=1, float lr=0., float beta1=0.9, "
+      "float beta2=0.999, float eps=1e-8, float weight_decay=0., bool adamw=False, float grad_scale=1.) -> ()",
+      &partials_reduce_multi);
   m.def("ipc_alloc(int nbytes, int kind, int device) -> int", &ipc_alloc);
   m.def("ipc_handle(int ptr) -> Tensor", &ipc_handle);
   m.def("ipc_open(Tensor handle, int device) -> int", &ipc_open);

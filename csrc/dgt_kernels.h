@@ -199,6 +199,18 @@ struct ReduceSegs {
   int n[kMaxReduceSegs];
   int count;
 };
-hipError_t partials_reduce_multi(const ReduceSegs& r, hipStream_t stream);
+// Optional Adam on the reduced values (a single-rank small region: nothing reduces it across
+// ranks): element o = (out_s - grads) + i of master / m / v takes torch's Adam step with gradient
+// grad_scale * sum, exactly as adam_flat would over the same region.
+struct ReduceAdam {
+  int on;
+  const float* grads;  // base of the region the outs live in
+  float* master;
+  float* m;
+  float* v;
+  AdamHyper hp;
+  float step_size_neg, bc2_sqrt, grad_scale;
+};
+hipError_t partials_reduce_multi(const ReduceSegs& r, const ReduceAdam& adam, hipStream_t stream);
 
 }  // namespace dgt

@@ -193,7 +193,7 @@ __global__ __launch_bounds__(64) void partials_reduce_kernel(const float* __rest
 // ReduceSegs: every segment's float4 columns in one grid; each thread finds its segment by a
 // uniform scan of <= kMaxReduceSegs prefix sums, then sums its column's tiles in order (the
 // partials_reduce order, so the same bits as separate launches).
-__global__ __launch_bounds__(64) void partials_reduce_multi_kernel(ReduceSegs r) {
+__global__ __launch_bounds__(64) void partials_reduce_multi_kernel(ReduceSegs r, ReduceAdam ad) {
   int i = (blockIdx.x * 64 + threadIdx.x) * 4;
   int s = 0;
   while (s < r.count && i >= r.n[s]) i -= r.n[s++];
@@ -211,9 +211,24 @@ __global__ __launch_bounds__(64) void partials_reduce_multi_kernel(ReduceSegs r)
       if (t0 + j < tiles) acc.x += p[j].x, acc.y += p[j].y, acc.z += p[j].z, acc.w += p[j].w;
   }
   *reinterpret_cast<float4*>(r.out[s] + i) = acc;
+  if (ad.on) {  // the region's Adam step on these four elements (adam_flat's per-element op order)
+    const long long o = (long long)(r.out[s] - ad.grads) + i;
+    float4 p = *reinterpret_cast<const float4*>(ad.master + o);
+    float4 m = *reinterpret_cast<const float4*>(ad.m + o);
+    float4 v = *reinterpret_cast<const float4*>(ad.v + o);
+    float* pp = &p.x;
+    float* mp = &m.x;
+    float* vp = &v.x;
+    const float* gp = &acc.x;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) pp[e] = adam_update(pp[e], gp[e] * ad.grad_scale, mp[e], vp[e], ad.hp, ad.step_size_neg, ad.bc2_sqrt);
+    *reinterpret_cast<float4*>(ad.master + o) = p;
+    *reinterpret_cast<float4*>(ad.m + o) = m;
+    *reinterpret_cast<float4*>(ad.v + o) = v;
+  }
 }
 
-hipError_t partials_reduce_multi(const ReduceSegs& r, hipStream_t stream) {
+hipError_t partials_reduce_multi(const ReduceSegs& r, const ReduceAdam& adam, hipStream_t stream) {
   if (r.count < 1 || r.count > kMaxReduceSegs) return hipErrorInvalidValue;
   long long total = 0;
   for (int s = 0; s < r.count; ++s) {
@@ -223,7 +238,7 @@ hipError_t partials_reduce_multi(const ReduceSegs& r, hipStream_t stream) {
     total += r.n[s];
   }
   const dim3 grid((unsigned)((total / 4 + 63) / 64)), blk(64);
-  hipLaunchKernelGGL(partials_reduce_multi_kernel, grid, blk, 0, stream, r);
+  hipLaunchKernelGGL(partials_reduce_multi_kernel, grid, blk, 0, stream, r, adam);
   return hipGetLastError();
 }
 

@@ -75,18 +75,34 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     require().gemm_nt(A, B, C, CT, bias, mask, epi, float(alpha), int(variant), colsum)
 
 
-def partials_reduce_multi(pairs) -> None:
+def partials_reduce_multi(pairs, adam=None) -> None:
     """For every ``(part [tiles, n], out [n])`` pair (fp32): ``out = part.sum(0)``, the tiles
-    added in order -- all pairs in ONE launch (at most 8)."""
+    added in order -- all pairs in ONE launch (at most 8).  ``adam`` = ``(grads, master, exp_avg,
+    exp_avg_sq, step, lr, beta1, beta2, eps, weight_decay, adamw, grad_scale)``: the outs are views of
+    ``grads`` and the same launch applies Adam to their elements of master / exp_avg / exp_avg_sq
+    (adam_flat's arithmetic: the same bits as a separate adam_flat over the region)."""
     pairs = list(pairs)
     if pairs[0][0].is_cuda:
-        require().partials_reduce_multi([p for p, _ in pairs], [o for _, o in pairs])
+        if adam is None:
+            require().partials_reduce_multi([p for p, _ in pairs], [o for _, o in pairs])
+        else:
+            g, p_, m, v, step, lr, b1, b2, eps, wd, adamw, scale = adam
+            require().partials_reduce_multi([p for p, _ in pairs], [o for _, o in pairs], g, p_, m, v, int(step),
+                                            float(lr), float(b1), float(b2), float(eps), float(wd), bool(adamw),
+                                            float(scale))
         return
     for p, o in pairs:
         acc = torch.zeros_like(p[0])
         for t in range(p.shape[0]):
             acc += p[t]
         o.copy_(acc.view(o.shape))
+    if adam is not None:
+        from .reference import adam_flat_reference_
+        g, p_, m, v, step, lr, b1, b2, eps, wd, adamw, scale = adam
+        for _, o in pairs:
+            off = (o.data_ptr() - g.data_ptr()) // 4
+            sl = slice(off, off + o.numel())
+            adam_flat_reference_(p_[sl], g[sl], m[sl], v[sl], step, lr, b1, b2, eps, wd, adamw, grad_scale=scale)
 
 
 def gemm_nt_adam_(A: torch.Tensor, B: torch.Tensor, master: torch.Tensor, exp_avg: torch.Tensor,

@@ -389,13 +389,14 @@ class MLPTrainer:
                 with torch.cuda.stream(self.s_opt):
                     self._update_layer(i)
                     self.ev_opt[i].record(self.s_opt)
-        self._reduce_small()
+        small_done = self._reduce_small(with_adam=True)
         if self.coll:  # biases + head: one small replicated bucket
             self._collective(dist.all_reduce, self.grads_s, works=works)
         for w in works:
             w.wait()
-        adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *self._adam_args(),
-                   grad_scale=1.0 / self.world_size)
+        if not small_done:
+            adam_flat_(self.master_s, self.grads_s, self.m_s, self.v_s, *self._adam_args(),
+                       grad_scale=1.0 / self.world_size)
         if ov:
             self._opt_pending = True
         elif self.schedule == "serial":
@@ -408,14 +409,27 @@ class MLPTrainer:
             if self.zero_stage == 1:
                 self._allgather_params()
 
-    def _reduce_small(self) -> None:
+    def _reduce_small(self, with_adam: bool = False) -> bool:
         """The small region's gradients from their partials, in one launch: every hidden bias (the
-        dgrads' and the head's column sums of g) and the head weight (the head's dz a partials)."""
+        dgrads' and the head's column sums of g) and the head weight (the head's dz a partials).
+        ``with_adam`` (one rank, GPU): the same launch also applies the region's Adam step -- the head
+        bias (written by the head itself, padded to 4) rides along as a one-tile segment -- and
+        True is returned (the caller skips its adam_flat over the region)."""
         L = self.L
         if not self._partials:
-            return
-        partials_reduce_multi([(self.bpart_top, self.gb[L - 1])] + [(self.bpart[i], self.gb[i]) for i in range(L - 1)]
-                              + [(self.hw_part, self.ghw)])
+            return False
+        pairs = ([(self.bpart_top, self.gb[L - 1])] + [(self.bpart[i], self.gb[i]) for i in range(L - 1)]
+                 + [(self.hw_part, self.ghw)])
+        fuse = with_adam and self.device.type == "cuda" and not self.coll
+        if fuse:
+            o = self.s_off["head.bias"]
+            hb4 = self.grads_s[o:o + 4]  # the head bias and three padding zeros (never written)
+            pairs.append((hb4.view(1, 4), hb4))
+            partials_reduce_multi(pairs, adam=(self.grads_s, self.master_s, self.m_s, self.v_s, *self._adam_args(),
+                                               1.0 / self.world_size))
+            return True
+        partials_reduce_multi(pairs)
+        return False
 
     def _backward_fused_adam(self, xT: torch.Tensor, cur: int) -> None:
         """Single-rank backward + update: per layer, the bias-gradient row sums, the dgrad (it

@@ -444,3 +444,24 @@ def test_dgrad_colsum_and_head_partials():
         for t in range(p.shape[0]):
             acc += p[t]
         assert torch.equal(o, acc)
+
+
+@gpu
+def test_partials_reduce_with_adam_is_bitwise_adam_flat():
+    """The small region's reduction + Adam in one launch gives adam_flat's bits (and the gradients)."""
+    from distributed_gpu_test_amd.ops.adam import adam_flat_
+    from distributed_gpu_test_amd.ops.gemm import partials_reduce_multi
+    g_ = torch.Generator().manual_seed(9)
+    n = 1028  # exactly the three segments: adam_flat over it touches the same elements
+    grads = torch.zeros(n, device="cuda")
+    parts = [torch.randn(8, 512, generator=g_).cuda() for _ in range(2)]
+    master = torch.randn(n, generator=g_).cuda()
+    m, v = (torch.randn(n, generator=g_) * 1e-2).cuda(), (torch.rand(n, generator=g_) * 1e-3).cuda()
+    grads[1024:1028] = torch.tensor([0.5, 0.0, 0.0, 0.0], device="cuda")  # a one-tile in-place segment
+    ref = [t.clone() for t in (grads, master, m, v)]
+    pairs = lambda g: [(parts[0], g[0:512]), (parts[1], g[512:1024]), (g[1024:1028].view(1, 4), g[1024:1028])]
+    partials_reduce_multi(pairs(grads), adam=(grads, master, m, v, 3, 1e-3, 0.9, 0.999, 1e-8, 0.01, True, 0.5))
+    partials_reduce_multi(pairs(ref[0]))
+    adam_flat_(ref[1], ref[0], ref[2], ref[3], 3, 1e-3, 0.9, 0.999, 1e-8, 0.01, True, grad_scale=0.5)
+    for a, b in zip((grads, master, m, v), ref):
+        assert torch.equal(a, b)
