@@ -141,7 +141,13 @@ __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__
 #pragma unroll
     for (int n = 0; n < N; ++n) {
       float s = 0.f;
-      for (int i = l; i < M; i += 64) s += b2f(dz[(long long)i * N + n]);
+      for (int i0 = l; i0 < M; i0 += 64 * 8) {  // 8 loads per lane in flight, added in row order
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) v[u] = i0 + 64 * u < M ? b2f(dz[(long long)(i0 + 64 * u) * N + n]) : 0.f;
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+      }
       s = wave_sum(s);
       if (l == 0) {
         if (db_bf16) {
