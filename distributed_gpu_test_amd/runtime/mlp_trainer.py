@@ -345,8 +345,9 @@ class MLPTrainer:
         for i in range(L):
             if self._opt_pending:
                 main.wait_event(self.ev_opt[i])
-            gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1], bias=self.b[i], relu=True,
-                    variant=self._v_fwd)
+            # a_{i+1}^T feeds the wgrad of layer i+1: the last layer's output has none (the head reads a_L)
+            gemm_nt(prev, self.W[i], C=self.a[i + 1], CT=self.aT[i + 1] if i + 1 < L else None, bias=self.b[i],
+                    relu=True, variant=self._v_fwd)
             prev = self.a[i + 1]
         # head (+ its gradients, written in place: no zero fills)
         cur = 0
@@ -378,8 +379,9 @@ class MLPTrainer:
                 else:
                     self._reduce_layer(i, works)
             if i > 0:
-                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1], CT=self.gT[cur ^ 1], mask=self.a[i], b_kn=True,
-                        variant=self._v_dgrad, colsum=self.bpart[i - 1])
+                # g_{i-1} row-major feeds the next dgrad only: the last one (i == 1) writes just g_0^T
+                gemm_nt(self.g[cur], self.W[i], C=self.g[cur ^ 1] if i > 1 else None, CT=self.gT[cur ^ 1],
+                        mask=self.a[i], b_kn=True, variant=self._v_dgrad, colsum=self.bpart[i - 1])
                 cur ^= 1
             if ov:
                 self.ev_bwd[i].record(main)
@@ -446,8 +448,8 @@ class MLPTrainer:
             if not self._partials:
                 rowsum_bf16(self.gT[cur], self.gb[i])
             if i > 0:
-                gemm_nt(self.g[cur], self.W[i], C=self.g[nxt], CT=self.gT[nxt], mask=self.a[i], b_kn=True,
-                        variant=self._v_dgrad, colsum=self.bpart[i - 1])
+                gemm_nt(self.g[cur], self.W[i], C=self.g[nxt] if i > 1 else None, CT=self.gT[nxt], mask=self.a[i],
+                        b_kn=True, variant=self._v_dgrad, colsum=self.bpart[i - 1])
             R, Cc = self.shapes[i]
             sl = slice(self.w_off[i], self.w_off[i] + R * Cc)
             if side:  # after the dgrad (it read W_i) and with gT[cur] complete
