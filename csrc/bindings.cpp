@@ -625,7 +625,7 @@ void skinny_fwd_bf16(const at::Tensor& a, const at::Tensor& W, const std::option
 // its backward: g = (dz . W) * 1[a > 0] (mask) and g^T; dW / db accumulate in fp32
 void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor& W, bool mask, const at::Tensor& g,
                      const std::optional<at::Tensor>& gT, const at::Tensor& dW, const at::Tensor& db,
-                     bool accumulate) {
+                     bool accumulate, const std::optional<at::Tensor>& bias_part) {
   const int64_t M = a.size(0), K = a.size(1), N = W.size(0);
   TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && W.size(1) == K && N >= 1 && N <= 4 && M % 64 == 0 && K % 64 == 0,
               "dgt: skinny_bwd needs a [M, K], W [N <= 4, K], M, K % 64 == 0");
@@ -645,10 +645,15 @@ void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor
   TORCH_CHECK(dW.numel() == N * K && db.numel() == N, "dgt: skinny_bwd dW [N, K] and db [N] (one dtype)");
   TORCH_CHECK(dW.is_contiguous(), "dgt: skinny_bwd dW must be contiguous");
   c10::DeviceGuard guard(a.device());
+  float* bp = nullptr;  // caller-owned [M / 64, K] column sums of g (the layer below's bias partials)
+  if (bias_part.has_value() && bias_part->defined()) {
+    check_2d(*bias_part, "bias_part", at::kFloat, M / 64, K);
+    bp = bias_part->data_ptr<float>();
+  }
   at::Tensor ws = at::empty({M / 64, N, K}, a.options().dtype(at::kFloat));  // per-row-tile dW partials
   DGT_CHECK_HIP(dgt::skinny_bwd_bf16(dz.data_ptr(), a.data_ptr(), W.data_ptr(), mask ? 1 : 0, g.data_ptr(), gTp,
                                      dW.data_ptr(), db.data_ptr(), bf ? 1 : 0, accumulate ? 1 : 0,
-                                     ws.data_ptr<float>(), (int)M, (int)N, (int)K, stream_of(a)));
+                                     ws.data_ptr<float>(), (int)M, (int)N, (int)K, stream_of(a), bp));
 }
 
 void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& y,
@@ -700,15 +705,19 @@ void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, co
   DGT_CHECK_HIP(dgt::mlp_head(h, stream_of(a)));
 }
 
-// out_s (+ nothing: stored) = sum over t of part_s[t] for every segment, in one launch; with
+// out_s (+)= sum over t of part_s[t] for every segment, in one launch (out fp32 or bf16; accumulate[s]
+// adds to it instead of storing); with
 // `grads` given, also the Adam step of master / exp_avg / exp_avg_sq on the outs' elements (their
 // offsets inside `grads`), as adam_flat would over that region
 void partials_reduce_multi(at::TensorList parts, at::TensorList outs, const std::optional<at::Tensor>& grads,
                            const std::optional<at::Tensor>& master, const std::optional<at::Tensor>& exp_avg,
                            const std::optional<at::Tensor>& exp_avg_sq, int64_t step, double lr, double beta1,
-                           double beta2, double eps, double weight_decay, bool adamw, double grad_scale) {
+                           double beta2, double eps, double weight_decay, bool adamw, double grad_scale,
+                           at::OptionalIntArrayRef accumulate) {
   TORCH_CHECK(parts.size() == outs.size() && parts.size() >= 1 && (int)parts.size() <= dgt::kMaxReduceSegs,
               "dgt: partials_reduce_multi needs 1..", dgt::kMaxReduceSegs, " (part, out) pairs");
+  TORCH_CHECK(!accumulate.has_value() || accumulate->size() == parts.size(),
+              "dgt: partials_reduce_multi accumulate needs one flag per segment");
   dgt::ReduceSegs r;
   std::memset(&r, 0, sizeof(r));
   r.count = (int)parts.size();
@@ -717,11 +726,14 @@ void partials_reduce_multi(at::TensorList parts, at::TensorList outs, const std:
     TORCH_CHECK(p.dim() == 2 && p.is_contiguous() && o.is_contiguous() && o.numel() == p.size(1) && p.size(1) % 4 == 0,
                 "dgt: partials_reduce_multi segment ", s, ": part [tiles, n] (n % 4 == 0) and a contiguous out [n]");
     check_gpu(p, "part", at::kFloat);
-    check_gpu(o, "out", at::kFloat);
-    TORCH_CHECK(reinterpret_cast<uintptr_t>(p.data_ptr()) % 16 == 0 && reinterpret_cast<uintptr_t>(o.data_ptr()) % 16 == 0,
-                "dgt: partials_reduce_multi tensors must be 16-byte aligned");
+    const bool bf = o.scalar_type() == at::kBFloat16;
+    check_gpu(o, "out", bf ? at::kBFloat16 : at::kFloat);
+    TORCH_CHECK(reinterpret_cast<uintptr_t>(p.data_ptr()) % 16 == 0 &&
+                    reinterpret_cast<uintptr_t>(o.data_ptr()) % (bf ? 8 : 16) == 0,
+                "dgt: partials_reduce_multi parts must be 16-byte, outs 16 (fp32) / 8 (bf16) byte aligned");
     r.part[s] = p.data_ptr<float>();
-    r.out[s] = o.data_ptr<float>();
+    r.out[s] = o.data_ptr();
+    r.flags[s] = (bf ? 1 : 0) | ((accumulate.has_value() && (*accumulate)[s]) ? 2 : 0);
     r.tiles[s] = (int)p.size(0);
     r.n[s] = (int)p.size(1);
   }
@@ -736,9 +748,11 @@ void partials_reduce_multi(at::TensorList parts, at::TensorList outs, const std:
                   "dgt: partials_reduce_multi's Adam region tensors must be contiguous, equal-sized, 16-byte aligned");
     }
     const float* gb = grads->data_ptr<float>();
-    for (int s = 0; s < r.count; ++s)
-      TORCH_CHECK(r.out[s] >= gb && r.out[s] + r.n[s] <= gb + grads->numel(),
-                  "dgt: partials_reduce_multi with Adam: every out must lie inside grads");
+    for (int s = 0; s < r.count; ++s) {
+      const float* o = static_cast<const float*>(r.out[s]);
+      TORCH_CHECK(r.flags[s] == 0 && o >= gb && o + r.n[s] <= gb + grads->numel(),
+                  "dgt: partials_reduce_multi with Adam: every out must be a stored fp32 slice of grads");
+    }
     ad.on = 1;
     ad.grads = gb;
     ad.master = master->data_ptr<float>();
@@ -863,7 +877,7 @@ TORCH_LIBRARY(dgt, m) {
   m.def("skinny_fwd_bf16(Tensor a, Tensor W, Tensor? b, Tensor(a!) z) -> ()", &skinny_fwd_bf16);
   m.def(
       "skinny_bwd_bf16(Tensor dz, Tensor a, Tensor W, bool mask, Tensor(a!) g, Tensor(b!)? gT, Tensor(c!) dW, "
-      "Tensor(d!) db, bool accumulate=True) -> ()",
+      "Tensor(d!) db, bool accumulate=True, Tensor(e!)? bias_part=None) -> ()",
       &skinny_bwd_bf16);
   m.def(
       "mlp_head(Tensor a, Tensor w, Tensor b0, Tensor y, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!) db, "
@@ -872,7 +886,8 @@ TORCH_LIBRARY(dgt, m) {
   m.def(
       "partials_reduce_multi(Tensor[] parts, Tensor(a!)[] outs, Tensor? grads=None, Tensor(b!)? master=None, "
       "Tensor(c!)? exp_avg=None, Tensor(d!)? exp_avg_sq=None, int step=1, float lr=0., float beta1=0.9, "
-      "float beta2=0.999, float eps=1e-8, float weight_decay=0., bool adamw=False, float grad_scale=1.) -> ()",
+      "float beta2=0.999, float eps=1e-8, float weight_decay=0., bool adamw=False, float grad_scale=1., "
+      "int[]? accumulate=None) -> ()",
       &partials_reduce_multi);
   m.def("ipc_alloc(int nbytes, int kind, int device) -> int", &ipc_alloc);
   m.def("ipc_handle(int ptr) -> Tensor", &ipc_handle);

@@ -155,12 +155,13 @@ hipError_t rowsum_bf16(const void* in, void* out, int out_bf16, int rows, int co
 //   backward  g[M, K] = (dz . W) * 1[a > 0] (mask optional), g^T[K, M] (optional),
 //             dW[N, K] (+)= dz^T . a, db[N] (+)= sum_m dz (fp32, or bf16 when dw_bf16: summed in fp32,
 //             rounded once; accumulate = 0 stores); part_ws: fp32 [M / 64, N, K] workspace (per-row-tile
-//             dW partials, summed in a fixed order: no atomics)
+//             dW partials, summed in a fixed order: no atomics); bias_part (optional): fp32 [M / 64, K]
+//             per-row-tile column sums of g (the layer below's bias-gradient partials)
 hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z, int M, int N, int K,
                            hipStream_t stream);
 hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, void* dW,
                            void* db, int dw_bf16, int accumulate, float* part_ws, int M, int N, int K,
-                           hipStream_t stream);
+                           hipStream_t stream, float* bias_part = nullptr);
 
 // out[i] (+)= sum over t = 0 .. tiles-1 (in this order) of part[t * n + i]: the fixed-order reduction of
 // per-tile partials that replaces float atomics (bit-reproducible gradients); out fp32 or bf16
@@ -189,14 +190,16 @@ struct HeadArgs {      // binary head of the synthetic MLP: Linear(D, 1) + BCE-w
 
 hipError_t mlp_head(const HeadArgs& h, hipStream_t stream);
 
-// Several fixed-order partial reductions in ONE launch: out_s[i] = sum over t (in order) of
-// part_s[t][i] (fp32), for up to kMaxReduceSegs segments s (n_s % 4 == 0, 16-byte aligned).
+// Several fixed-order partial reductions in ONE launch: out_s[i] (+)= sum over t (in order) of
+// part_s[t][i] (fp32 partials; fp32 or bf16 out), for up to kMaxReduceSegs segments s (n_s % 4 == 0,
+// partials 16-byte aligned, outs 16 (fp32) or 8 (bf16) byte aligned).
 constexpr int kMaxReduceSegs = 8;
 struct ReduceSegs {
   const float* part[kMaxReduceSegs];
-  float* out[kMaxReduceSegs];
+  void* out[kMaxReduceSegs];     // fp32, or bf16 (flag 1: the sum in fp32, rounded once)
   int tiles[kMaxReduceSegs];
   int n[kMaxReduceSegs];
+  int flags[kMaxReduceSegs];     // 1 = bf16 out, 2 = accumulate into out
   int count;
 };
 // Optional Adam on the reduced values (a single-rank small region: nothing reduces it across

@@ -71,7 +71,8 @@ template <int N>
 __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__ dz, const u16* __restrict__ a,
                                                          const u16* __restrict__ W, int mask, u16* __restrict__ g,
                                                          u16* __restrict__ gT, float* __restrict__ part_ws,
-                                                         void* __restrict__ db, int db_bf16, int acc, int M, int K) {
+                                                         void* __restrict__ db, int db_bf16, int acc, int M, int K,
+                                                         float* __restrict__ bias_part) {
   const int l = threadIdx.x & 63, cg = l & 7, rb = l >> 3, wv = threadIdx.x >> 6;
   const int r = blockIdx.y * 64 + rb * 8, c = (blockIdx.x * (blockDim.x >> 6) + wv) * 64 + cg * 8;
   float w[N][8];
@@ -86,6 +87,7 @@ __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__
 #pragma unroll
     for (int e = 0; e < 8; ++e) part[n][e] = 0.f;
   u16 gb[8][8];
+  float gsum[8] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};  // column sums of g (bias_part)
 #pragma unroll
   for (int k = 0; k < 8; ++k) {
     float d[N];
@@ -103,6 +105,7 @@ __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__
         part[n][e] = fmaf(d[n], x[e], part[n][e]);
       }
       gb[k][e] = f2b((!mask || x[e] > 0.f) ? s : 0.f);
+      gsum[e] += b2f(gb[k][e]);
     }
 #pragma unroll
     for (int q = 0; q < 4; ++q) o[q] = (unsigned)gb[k][2 * q] | ((unsigned)gb[k][2 * q + 1] << 16);
@@ -129,6 +132,21 @@ __global__ __launch_bounds__(256) void skinny_bwd_kernel(const u16* __restrict__
       x += __shfl_xor(x, 32);
       part[n][e] = x;
     }
+  if (bias_part) {  // per-64-row-tile column sums of g: the layer below's bias-gradient partials
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      float x = gsum[e];
+      x += __shfl_xor(x, 8);
+      x += __shfl_xor(x, 16);
+      x += __shfl_xor(x, 32);
+      gsum[e] = x;
+    }
+    if (rb == 0) {
+      float4* o = reinterpret_cast<float4*>(bias_part + (long long)blockIdx.y * K + c);
+      o[0] = make_float4(gsum[0], gsum[1], gsum[2], gsum[3]);
+      o[1] = make_float4(gsum[4], gsum[5], gsum[6], gsum[7]);
+    }
+  }
   if (rb == 0) {
 #pragma unroll
     for (int n = 0; n < N; ++n) {
@@ -216,9 +234,23 @@ __global__ __launch_bounds__(64) void partials_reduce_multi_kernel(ReduceSegs r,
     for (int j = 0; j < 8; ++j)
       if (t0 + j < tiles) acc.x += p[j].x, acc.y += p[j].y, acc.z += p[j].z, acc.w += p[j].w;
   }
-  *reinterpret_cast<float4*>(r.out[s] + i) = acc;
+  const int fl = r.flags[s];
+  if (fl & 1) {  // bf16 out (the engine's gradient bucket views): the sum in fp32, rounded once
+    u16* d = static_cast<u16*>(r.out[s]) + i;
+    if (fl & 2) acc = make_float4(b2f(d[0]) + acc.x, b2f(d[1]) + acc.y, b2f(d[2]) + acc.z, b2f(d[3]) + acc.w);
+    const unsigned lo = (unsigned)f2b(acc.x) | ((unsigned)f2b(acc.y) << 16);
+    const unsigned hi = (unsigned)f2b(acc.z) | ((unsigned)f2b(acc.w) << 16);
+    *reinterpret_cast<uint2*>(d) = make_uint2(lo, hi);
+    return;
+  }
+  float4* d = reinterpret_cast<float4*>(static_cast<float*>(r.out[s]) + i);
+  if (fl & 2) {
+    const float4 o = *d;
+    acc = make_float4(o.x + acc.x, o.y + acc.y, o.z + acc.z, o.w + acc.w);
+  }
+  *d = acc;
   if (ad.on) {  // the region's Adam step on these four elements (adam_flat's per-element op order)
-    const long long o = (long long)(r.out[s] - ad.grads) + i;
+    const long long o = (long long)(static_cast<const float*>(r.out[s]) - ad.grads) + i;
     float4 p = *reinterpret_cast<const float4*>(ad.master + o);
     float4 m = *reinterpret_cast<const float4*>(ad.m + o);
     float4 v = *reinterpret_cast<const float4*>(ad.v + o);
@@ -239,7 +271,7 @@ hipError_t partials_reduce_multi(const ReduceSegs& r, const ReduceAdam& adam, hi
   long long total = 0;
   for (int s = 0; s < r.count; ++s) {
     if (r.n[s] <= 0 || r.n[s] % 4 || r.tiles[s] < 1 || (reinterpret_cast<uintptr_t>(r.part[s]) & 15) ||
-        (reinterpret_cast<uintptr_t>(r.out[s]) & 15))
+        (reinterpret_cast<uintptr_t>(r.out[s]) & ((r.flags[s] & 1) ? 7 : 15)) || (adam.on && r.flags[s]))
       return hipErrorInvalidValue;
     total += r.n[s];
   }
@@ -276,17 +308,17 @@ hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z,
 
 hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, void* dW,
                            void* db, int dw_bf16, int accumulate, float* part_ws, int M, int N, int K,
-                           hipStream_t stream) {
+                           hipStream_t stream, float* bias_part) {
   if (N < 1 || N > 4 || M % 64 || K % 64 || M <= 0 || K <= 0) return hipErrorInvalidValue;
   const int wpb = K % 256 == 0 ? 4 : 1;  // 4 tiles per block side by side when the width allows
   const dim3 grid(K / (64 * wpb), M / 64), blk(64 * wpb);
   const u16 *dp = static_cast<const u16*>(dz), *ap = static_cast<const u16*>(a), *wp = static_cast<const u16*>(W);
   u16 *gp = static_cast<u16*>(g), *gtp = static_cast<u16*>(gT);
   switch (N) {
-    case 1: hipLaunchKernelGGL(skinny_bwd_kernel<1>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K); break;
-    case 2: hipLaunchKernelGGL(skinny_bwd_kernel<2>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K); break;
-    case 3: hipLaunchKernelGGL(skinny_bwd_kernel<3>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K); break;
-    default: hipLaunchKernelGGL(skinny_bwd_kernel<4>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K);
+    case 1: hipLaunchKernelGGL(skinny_bwd_kernel<1>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K, bias_part); break;
+    case 2: hipLaunchKernelGGL(skinny_bwd_kernel<2>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K, bias_part); break;
+    case 3: hipLaunchKernelGGL(skinny_bwd_kernel<3>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K, bias_part); break;
+    default: hipLaunchKernelGGL(skinny_bwd_kernel<4>, grid, blk, 0, stream, dp, ap, wp, mask, gp, gtp, part_ws, db, dw_bf16, accumulate, M, K, bias_part);
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -76,30 +76,35 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
 
 
 def partials_reduce_multi(pairs, adam=None) -> None:
-    """For every ``(part [tiles, n], out [n])`` pair (fp32): ``out = part.sum(0)``, the tiles
-    added in order -- all pairs in ONE launch (at most 8).  ``adam`` = ``(grads, master, exp_avg,
+    """For every ``(part [tiles, n], out [n])`` pair (part fp32, out fp32 or bf16): ``out =
+    part.sum(0)``, the tiles added in order -- all pairs in ONE launch (at most 8).  A pair may carry a
+    third element ``accumulate``: ``out += part.sum(0)`` (a bf16 out: the sum in fp32, rounded once).
+    ``adam`` = ``(grads, master, exp_avg,
     exp_avg_sq, step, lr, beta1, beta2, eps, weight_decay, adamw, grad_scale)``: the outs are views of
     ``grads`` and the same launch applies Adam to their elements of master / exp_avg / exp_avg_sq
     (adam_flat's arithmetic: the same bits as a separate adam_flat over the region)."""
-    pairs = list(pairs)
-    if pairs[0][0].is_cuda:
+    pairs = [(q[0], q[1], bool(q[2]) if len(q) > 2 else False) for q in pairs]
+    parts, outs = [q[0] for q in pairs], [q[1] for q in pairs]
+    acc_flags = [int(q[2]) for q in pairs] if any(q[2] for q in pairs) else None
+    if parts[0].is_cuda:
         if adam is None:
-            require().partials_reduce_multi([p for p, _ in pairs], [o for _, o in pairs])
+            require().partials_reduce_multi(parts, outs, accumulate=acc_flags)
         else:
             g, p_, m, v, step, lr, b1, b2, eps, wd, adamw, scale = adam
-            require().partials_reduce_multi([p for p, _ in pairs], [o for _, o in pairs], g, p_, m, v, int(step),
-                                            float(lr), float(b1), float(b2), float(eps), float(wd), bool(adamw),
-                                            float(scale))
+            require().partials_reduce_multi(parts, outs, g, p_, m, v, int(step), float(lr), float(b1), float(b2),
+                                            float(eps), float(wd), bool(adamw), float(scale), acc_flags)
         return
-    for p, o in pairs:
+    for p, o, accumulate in pairs:
         acc = torch.zeros_like(p[0])
         for t in range(p.shape[0]):
             acc += p[t]
-        o.copy_(acc.view(o.shape))
+        if accumulate:  # the kernel's order: the tiles' sum, then added to the out
+            acc = o.float().reshape(-1) + acc
+        o.copy_(acc.view(o.shape).to(o.dtype))
     if adam is not None:
         from .reference import adam_flat_reference_
         g, p_, m, v, step, lr, b1, b2, eps, wd, adamw, scale = adam
-        for _, o in pairs:
+        for _, o, _ in pairs:
             off = (o.data_ptr() - g.data_ptr()) // 4
             sl = slice(off, off + o.numel())
             adam_flat_reference_(p_[sl], g[sl], m[sl], v[sl], step, lr, b1, b2, eps, wd, adamw, grad_scale=scale)
@@ -152,17 +157,22 @@ def skinny_fwd_bf16(a: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
 
 
 def skinny_bwd_bf16(dz: torch.Tensor, a: torch.Tensor, w: torch.Tensor, mask: bool, g: torch.Tensor,
-                    gT: Optional[torch.Tensor], dw: torch.Tensor, db: torch.Tensor, accumulate: bool = True) -> None:
+                    gT: Optional[torch.Tensor], dw: torch.Tensor, db: torch.Tensor, accumulate: bool = True,
+                    bias_part: Optional[torch.Tensor] = None) -> None:
     """Its backward: g = (dz . w) * 1[a > 0] (if mask) and g^T (bf16); dw [N, K] and db [N] (both fp32
-    or both bf16) receive dz^T . a and the column sums of dz: added (``accumulate``) or stored."""
+    or both bf16) receive dz^T . a and the column sums of dz: added (``accumulate``) or stored.
+    ``bias_part`` (fp32 ``[M // 64, K]``): the per-64-row-tile column sums of the bf16 g (the layer
+    below's bias-gradient partials, for ``partials_reduce_multi``)."""
     if a.is_cuda:
-        require().skinny_bwd_bf16(dz, a, w, mask, g, gT, dw, db, bool(accumulate))
+        require().skinny_bwd_bf16(dz, a, w, mask, g, gT, dw, db, bool(accumulate), bias_part)
         return
     d = dz.float().reshape(a.shape[0], w.shape[0])
     gg = d @ w.float()
     if mask:
         gg = gg * (a.float() > 0)
     g.copy_(gg.to(g.dtype))
+    if bias_part is not None:
+        bias_part.copy_(g.float().view(-1, 64, g.shape[1]).sum(1))
     if gT is not None:
         gT.copy_(gg.t().to(gT.dtype))
     if accumulate:

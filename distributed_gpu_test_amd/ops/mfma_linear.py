@@ -14,7 +14,11 @@ node whose kernels are this framework's (``csrc/gemm.hip``, ``csrc/head.hip``):
               dW_i = g_i^T x_i  -> the .grad view   gemm_nt (stores into the engine's flat bf16
                                                    gradient bucket; accumulates after the first
                                                    micro-step of an accumulation window)
-              db_i = row sums of g_i^T              rowsum_bf16 (bf16 out)
+              db_i = column sums of g_i             per-row-tile partials from the kernel that forms
+                                                   g_i (skinny_bwd / the dgrad epilogue's colsum),
+                                                   all layers reduced by ONE partials_reduce_multi
+                                                   (fixed order, bf16 out); rowsum_bf16 of g_i^T when
+                                                   no partials exist (no ReLU below the layer)
               g_{i-1} = (g_i W_i) * 1[x_i > 0], g^T  gemm_nt reading W_i[out, in] as a [K, N] operand
                                                    (transposed LDS reads), mask + C^T epilogue
 
@@ -33,7 +37,7 @@ import torch
 import torch.nn as nn
 
 from ..models.synthetic_mlp import SyntheticMLP
-from .gemm import gemm_nt, rowsum_bf16, skinny_bwd_bf16, skinny_fwd_bf16, transpose_bf16
+from .gemm import gemm_nt, partials_reduce_multi, rowsum_bf16, skinny_bwd_bf16, skinny_fwd_bf16, transpose_bf16
 from .linear import _first_write, _grad_view_ok, _in_place_active, count_fallback
 
 MAX_HEAD = 4
@@ -123,6 +127,11 @@ class _MfmaChainFn(torch.autograd.Function):
         def leaf(j):
             return ctx.params[j] if active else None
 
+        def wants_bias(i):  # layer i's bias gradient is needed
+            return ctx.has_bias[i] and need[4 + 2 * i + 1]
+
+        bpart = None  # column-sum partials of the current g (fp32 [row tiles, features]), if formed
+        segs = []     # (partials, bias-gradient target, accumulate): reduced together at the end
         if head:
             wh = ws[L]
             kh = wh.shape[1]
@@ -131,6 +140,7 @@ class _MfmaChainFn(torch.autograd.Function):
             jw, jb = 2 * L, 2 * L + 1
             pw, pb = leaf(jw), (leaf(jb) if ctx.has_bias[L] else None)
             mask_h = relus[L - 1] if L > 0 else False
+            hb = torch.empty(M // 64, kh, dtype=torch.float32, device=dev) if L > 0 and wants_bias(L - 1) else None
             direct = (need[4 + jw] and pw is not None and _grad_view_ok(pw, BF16)
                       and (not ctx.has_bias[L] or (need[4 + jb] and pb is not None and _grad_view_ok(pb, BF16))))
             if direct:
@@ -140,11 +150,11 @@ class _MfmaChainFn(torch.autograd.Function):
             if direct:
                 # straight into the bucket's bf16 views, stored on their first write of this backward
                 db = pb.grad if pb is not None else torch.zeros(wh.shape[0], dtype=BF16, device=dev)
-                skinny_bwd_bf16(dout, xs[L], wh, mask_h, g, gT, pw.grad, db, accumulate=not store_w)
+                skinny_bwd_bf16(dout, xs[L], wh, mask_h, g, gT, pw.grad, db, accumulate=not store_w, bias_part=hb)
             else:
                 dw = torch.zeros(wh.shape, dtype=torch.float32, device=dev)
                 db = torch.zeros(wh.shape[0], dtype=torch.float32, device=dev)
-                skinny_bwd_bf16(dout, xs[L], wh, mask_h, g, gT, dw, db)
+                skinny_bwd_bf16(dout, xs[L], wh, mask_h, g, gT, dw, db, bias_part=hb)
                 for j, val in ((jw, dw), (jb, db)):
                     if j == jb and not ctx.has_bias[L]:
                         continue
@@ -155,6 +165,7 @@ class _MfmaChainFn(torch.autograd.Function):
                         p.grad.add_(val)  # tiny: [N <= 4, K] and [N]
                     else:
                         grads[j] = val.to(BF16)
+            bpart = hb
         else:
             y = xs[L]
             g = (dout * (y > 0)).contiguous() if relus[L - 1] else dout
@@ -171,22 +182,32 @@ class _MfmaChainFn(torch.autograd.Function):
                 else:
                     grads[jw] = torch.empty_like(w)
                     gemm_nt(gT, xTs[i], C=grads[jw])
-            if ctx.has_bias[i] and need[4 + jb]:
+            if wants_bias(i):
                 p = leaf(jb)
-                if p is not None and _grad_view_ok(p, BF16):
-                    rowsum_bf16(gT, p.grad, accumulate=not _first_write(p.grad))
+                if p is not None and _grad_view_ok(p, BF16) and (bpart is None or p.grad.data_ptr() % 8 == 0):
+                    tgt, acc = p.grad, not _first_write(p.grad)
                 else:
-                    grads[jb] = torch.empty(w.shape[0], dtype=BF16, device=dev)
-                    rowsum_bf16(gT, grads[jb])
+                    tgt = grads[jb] = torch.empty(w.shape[0], dtype=BF16, device=dev)
+                    acc = False
+                if bpart is not None:
+                    segs.append((bpart, tgt, acc))
+                else:
+                    rowsum_bf16(gT, tgt, accumulate=acc)
             if i > 0:
                 k = w.shape[1]
                 g_prev = torch.empty(M, k, dtype=BF16, device=dev)
                 gT_prev = torch.empty(k, M, dtype=BF16, device=dev)
-                gemm_nt(g, w, C=g_prev, CT=gT_prev, mask=xs[i] if relus[i - 1] else None, b_kn=True)
+                bpart = None
+                if relus[i - 1] and wants_bias(i - 1):  # the epilogue's colsum needs the ReLU mask
+                    bpart = torch.empty(M // 128, k, dtype=torch.float32, device=dev)
+                gemm_nt(g, w, C=g_prev, CT=gT_prev, mask=xs[i] if relus[i - 1] else None, b_kn=True,
+                        colsum=bpart)
                 g, gT = g_prev, gT_prev
             elif need[0]:
                 dx = torch.empty_like(xs[0])
                 gemm_nt(g, w, C=dx, b_kn=True)
+        for s0 in range(0, len(segs), 8):
+            partials_reduce_multi(segs[s0:s0 + 8])
         return (dx, None, None, None, *grads)
 
 

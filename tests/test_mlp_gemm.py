@@ -447,6 +447,39 @@ def test_dgrad_colsum_and_head_partials():
 
 
 @gpu
+def test_skinny_bias_part_and_bf16_accumulating_reduce():
+    """The engine chain's bias gradients: skinny_bwd's per-64-row-tile column sums of its bf16 g,
+    reduced with the dgrad colsum into bf16 gradient views (stored, or added to what is there: the
+    sum in fp32, rounded once) -- the CPU reference's bits."""
+    from distributed_gpu_test_amd.ops.gemm import partials_reduce_multi, skinny_bwd_bf16
+    g_ = torch.Generator().manual_seed(9)
+    M, K, N = 512, 384, 2
+    dz = torch.randn(M, N, generator=g_).bfloat16()
+    a = torch.relu(torch.randn(M, K, generator=g_)).bfloat16()
+    w = torch.randn(N, K, generator=g_).bfloat16()
+    outs = {}
+    for dev in ("cpu", "cuda"):
+        g = torch.empty(M, K, dtype=torch.bfloat16, device=dev)
+        dw, db = torch.zeros(N, K, device=dev), torch.zeros(N, device=dev)
+        bp = torch.full((M // 64, K), float("nan"), device=dev)
+        skinny_bwd_bf16(dz.to(dev), a.to(dev), w.to(dev), True, g, None, dw, db, bias_part=bp)
+        outs[dev] = (g, bp)
+    torch.testing.assert_close(outs["cuda"][0].cpu(), outs["cpu"][0], rtol=1e-2, atol=1e-2)
+    gc, bpc = outs["cuda"]
+    torch.testing.assert_close(bpc, gc.float().view(M // 64, 64, K).sum(1), rtol=1e-5, atol=1e-5)
+    # bf16 outs (stored / accumulated), an fp32 accumulate, one launch; every out against the CPU path
+    base = torch.randn(K, generator=g_)
+    views = {dev: (torch.zeros(K, dtype=torch.bfloat16, device=dev), base.bfloat16().to(dev),
+                   base.clone().to(dev)) for dev in ("cpu", "cuda")}
+    p = bpc.cpu()
+    for dev in ("cpu", "cuda"):
+        o1, o2, o3 = views[dev]
+        partials_reduce_multi([(p.to(dev), o1), (p.to(dev), o2, True), (p.to(dev), o3, True)])
+    for x, y in zip(views["cuda"], views["cpu"]):
+        assert torch.equal(x.cpu(), y)
+
+
+@gpu
 def test_partials_reduce_with_adam_is_bitwise_adam_flat():
     """The small region's reduction + Adam in one launch gives adam_flat's bits (and the gradients)."""
     from distributed_gpu_test_amd.ops.adam import adam_flat_
