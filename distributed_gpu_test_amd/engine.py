@@ -164,6 +164,14 @@ class Engine:
         self._timers: Dict[str, float] = {}
         self._seed_one: Optional[torch.Tensor] = None
         self._grads_dirty = False  # the flat gradient buffer holds something since the last zero_grad
+        # Deferred zeroing (one GPU): when the last backward that began on a zeroed buffer STORED every
+        # parameter's gradient view (the bf16 MFMA chain's first writes), the step's zero fill of the
+        # flat buffer (a whole-buffer pass: 18.5 us of 800 for the bench MLP) is skipped -- the next
+        # backward overwrites every view anyway.  A forward that leaves the kernels (a counted
+        # fallback: F.linear would ADD into the stale view) fills the buffer before its backward, and
+        # a view the next backward does not store is zeroed right after it (it got no gradient).
+        self._stored_all = False
+        self._zero_deferred = False
         self._grad_norm: Optional[torch.Tensor] = None
         self._boundary_pending = False
         self.training = True
@@ -218,6 +226,17 @@ class Engine:
     def zero_grad(self) -> None:
         self.store.zero_grad()
         self._grads_dirty = False
+        self._zero_deferred = False
+
+    def _zero_after_step(self) -> None:
+        if self._stored_all and self.world_size == 1 and self.device.type == "cuda":
+            self._zero_deferred = True
+            self._grads_dirty = False
+        else:
+            self.zero_grad()
+
+    def _grad_views(self):
+        return [(p, (p.grad.data_ptr(), p.grad.numel())) for p in self.params if p.grad is not None]
 
     @property
     def linear_fallbacks(self) -> Dict[str, int]:
@@ -233,6 +252,17 @@ class Engine:
         if self.dtype != torch.float32:
             args = tuple(a.to(self.dtype) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)
         self.tput.start()
+        if self._zero_deferred:
+            from .ops.linear import FALLBACKS
+            n_fb = sum(FALLBACKS.values())
+            try:
+                return self._forward(args, kwargs)
+            finally:
+                if sum(FALLBACKS.values()) != n_fb:  # F.linear ran: its backward adds into the views
+                    self.zero_grad()
+        return self._forward(args, kwargs)
+
+    def _forward(self, args, kwargs):
         with tracing.range("dgt.forward"):
             if self.graph_module and self.training and not kwargs and args and all(torch.is_tensor(a) for a in args):
                 fn = self._graphed_forward(args)
@@ -280,8 +310,17 @@ class Engine:
             scaled = scaled * self.loss_scaler.scale
         t0 = time.perf_counter() if self.config.wall_clock_breakdown else 0.0
         from .ops.linear import engine_backward
-        with tracing.range("dgt.backward"), engine_backward(grads_zero=not self._grads_dirty):
+        from_zero, deferred = not self._grads_dirty, self._zero_deferred
+        self._zero_deferred = False
+        with tracing.range("dgt.backward"), engine_backward(grads_zero=from_zero) as stored:
             scaled.backward(self._backward_seed(scaled, loss), retain_graph=retain_graph)
+        if from_zero:
+            views = self._grad_views()
+            missing = [p for p, key in views if key not in stored]
+            if deferred:
+                for p in missing:  # stale from the last step and not written by this backward
+                    p.grad.zero_()
+            self._stored_all = len(views) == len(self.params) and not missing
         self._grads_dirty = True
         if boundary:
             with tracing.range("dgt.allreduce_wait"):
@@ -435,7 +474,7 @@ class Engine:
 
     def _finish_step(self, skipped: bool, zero: bool = True) -> None:
         if zero:
-            self.zero_grad()
+            self._zero_after_step()
         self.global_steps += 1
         self.global_samples += self.config.train_batch_size
         if self.lr_scheduler is not None and not skipped:

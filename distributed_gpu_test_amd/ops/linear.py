@@ -44,12 +44,13 @@ _WRITTEN: set = set()
 
 @contextlib.contextmanager
 def engine_backward(grads_zero: bool = False):
+    """Yields the set of ``(data_ptr, numel)`` gradient views STORED (first-written) in this backward."""
     global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN
     _ENGINE_BACKWARD += 1
     prev, _GRADS_ZERO = _GRADS_ZERO, bool(grads_zero)
     prev_written, _WRITTEN = _WRITTEN, set()
     try:
-        yield
+        yield _WRITTEN
     finally:
         _ENGINE_BACKWARD -= 1
         _GRADS_ZERO = prev

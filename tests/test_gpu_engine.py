@@ -424,6 +424,37 @@ def test_engine_bf16_chain_called_twice_before_backward():
 
 
 @pytest.mark.gpu
+def test_engine_bf16_deferred_zero_grad_matches_autograd_engine():
+    """After a backward that stored every gradient view, the step skips the bucket's zero fill; a
+    forward that falls back to F.linear (batch 192: not a multiple of 128) fills it before its
+    backward, and each step's gradients still match the autograd engine's."""
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    engines = []
+    for fused in (True, False):
+        torch.manual_seed(11)
+        cfg = {"train_micro_batch_size_per_gpu": 256, "bf16": {"enabled": True},
+               "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "amd": {"fused_linear": fused}}
+        engines.append(dgt.initialize(model=SyntheticMLP(256, 2), config=cfg)[0])
+    crit = torch.nn.BCEWithLogitsLoss()
+    g = torch.Generator().manual_seed(4)
+    deferred = []
+    for B in (256, 256, 256, 192, 256, 256):
+        x = torch.randn(B, 256, generator=g).to(torch.bfloat16).cuda()
+        y = (torch.rand(B, generator=g) > 0.5).float().cuda()
+        grads = []
+        for e in engines:
+            deferred.append(e._zero_deferred)
+            e.backward(crit(e(x).view(-1).float(), y))
+            grads.append(torch.cat([p.grad.float().reshape(-1) for p in e.module.parameters()]))
+            e.step()
+        torch.testing.assert_close(grads[0], grads[1], rtol=3e-2, atol=3e-4)
+    assert deferred[0::2] == [False, True, True, True, False, True]  # fused: the fallback step re-arms
+    assert not any(deferred[1::2])  # autograd's F.linear path adds: never deferred
+    for e in engines:
+        e.close()
+
+
+@pytest.mark.gpu
 def test_engine_bf16_step_runs_no_vendor_gemm():
     """The bf16 engine step launches this framework's GEMM / head / Adam kernels and no hipBLASLt
     (Cijk_*) or rocBLAS kernel (torch profiler kernel names of two steps)."""
