@@ -147,10 +147,15 @@ class Engine:
                                    comm_dtype=comm_dtype, oneshot=self.oneshot,
                                    oneshot_max_bytes=config.amd.oneshot_max_bytes,
                                    debug_sync=config.amd.debug_sync_streams)
+        # deferred zeroing needs a writer that STORES gradients (the bf16 MFMA chain) and no collective
+        self._defer_capable = (device.type == "cuda" and self.world_size == 1 and self.dtype == torch.bfloat16
+                               and self.fused_linear_layers > 0)
         self._hooks = []
         for i, p in enumerate(self.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(
                 lambda _p, i=i: self.reducer.on_grad_ready(i)))
+            if self._defer_capable:
+                self._hooks.append(p.register_hook(lambda g, p=p: self._before_accumulate(p)))
 
         # ---- schedules, loss scaling, logging, fault injection
         self.lr_scheduler = lr_scheduler
@@ -167,11 +172,14 @@ class Engine:
         # Deferred zeroing (one GPU): when the last backward that began on a zeroed buffer STORED every
         # parameter's gradient view (the bf16 MFMA chain's first writes), the step's zero fill of the
         # flat buffer (a whole-buffer pass: 18.5 us of 800 for the bench MLP) is skipped -- the next
-        # backward overwrites every view anyway.  A forward that leaves the kernels (a counted
-        # fallback: F.linear would ADD into the stale view) fills the buffer before its backward, and
-        # a view the next backward does not store is zeroed right after it (it got no gradient).
+        # backward overwrites every view anyway.  Should autograd itself accumulate into a view in that
+        # backward (a forward that fell back to F.linear, a parameter outside the chains), the view is
+        # zeroed just before (a tensor hook runs ahead of AccumulateGrad), and a view nothing writes is
+        # zeroed right after the backward (it got no gradient).
         self._stored_all = False
         self._zero_deferred = False
+        self._deferred_active = False
+        self._hook_zeroed = 0  # views zeroed by that hook in the current backward
         self._grad_norm: Optional[torch.Tensor] = None
         self._boundary_pending = False
         self.training = True
@@ -229,11 +237,20 @@ class Engine:
         self._zero_deferred = False
 
     def _zero_after_step(self) -> None:
-        if self._stored_all and self.world_size == 1 and self.device.type == "cuda":
+        if self._stored_all and self._defer_capable:
             self._zero_deferred = True
             self._grads_dirty = False
         else:
             self.zero_grad()
+
+    def _before_accumulate(self, p) -> None:
+        """Autograd is about to ADD into p.grad: in a backward over a deferred (stale) buffer, zero the
+        view first unless this backward already wrote it (then the add is the accumulation)."""
+        if self._deferred_active and p.grad is not None:
+            from .ops.linear import _first_write
+            if _first_write(p.grad):
+                p.grad.zero_()
+                self._hook_zeroed += 1
 
     def _grad_views(self):
         return [(p, (p.grad.data_ptr(), p.grad.numel())) for p in self.params if p.grad is not None]
@@ -252,17 +269,6 @@ class Engine:
         if self.dtype != torch.float32:
             args = tuple(a.to(self.dtype) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)
         self.tput.start()
-        if self._zero_deferred:
-            from .ops.linear import FALLBACKS
-            n_fb = sum(FALLBACKS.values())
-            try:
-                return self._forward(args, kwargs)
-            finally:
-                if sum(FALLBACKS.values()) != n_fb:  # F.linear ran: its backward adds into the views
-                    self.zero_grad()
-        return self._forward(args, kwargs)
-
-    def _forward(self, args, kwargs):
         with tracing.range("dgt.forward"):
             if self.graph_module and self.training and not kwargs and args and all(torch.is_tensor(a) for a in args):
                 fn = self._graphed_forward(args)
@@ -312,15 +318,21 @@ class Engine:
         from .ops.linear import engine_backward
         from_zero, deferred = not self._grads_dirty, self._zero_deferred
         self._zero_deferred = False
-        with tracing.range("dgt.backward"), engine_backward(grads_zero=from_zero) as stored:
-            scaled.backward(self._backward_seed(scaled, loss), retain_graph=retain_graph)
+        self._deferred_active, self._hook_zeroed = deferred, 0
+        try:
+            with tracing.range("dgt.backward"), engine_backward(grads_zero=from_zero) as stored:
+                scaled.backward(self._backward_seed(scaled, loss), retain_graph=retain_graph)
+        finally:
+            self._deferred_active = False
         if from_zero:
             views = self._grad_views()
             missing = [p for p, key in views if key not in stored]
             if deferred:
                 for p in missing:  # stale from the last step and not written by this backward
                     p.grad.zero_()
-            self._stored_all = len(views) == len(self.params) and not missing
+            # defer again only when the KERNELS stored every view (an autograd-written view costs a
+            # zero launch of its own in a deferred backward)
+            self._stored_all = len(views) == len(self.params) and not missing and self._hook_zeroed == 0
         self._grads_dirty = True
         if boundary:
             with tracing.range("dgt.allreduce_wait"):

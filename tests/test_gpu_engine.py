@@ -425,9 +425,10 @@ def test_engine_bf16_chain_called_twice_before_backward():
 
 @pytest.mark.gpu
 def test_engine_bf16_deferred_zero_grad_matches_autograd_engine():
-    """After a backward that stored every gradient view, the step skips the bucket's zero fill; a
-    forward that falls back to F.linear (batch 192: not a multiple of 128) fills it before its
-    backward, and each step's gradients still match the autograd engine's."""
+    """After a backward that stored every gradient view, the step skips the bucket's zero fill; in
+    a step that falls back to F.linear (batch 192: not a multiple of 128) autograd's accumulation
+    into the stale views is preceded by a zero of each view (tensor hook), the next step fills the
+    bucket again, and every step's gradients match the autograd engine's."""
     from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
     engines = []
     for fused in (True, False):
