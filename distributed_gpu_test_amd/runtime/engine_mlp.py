@@ -12,6 +12,7 @@ import torch
 
 from .. import initialize
 from ..models.synthetic_mlp import SyntheticMLP, synthetic_batch_data
+from ..ops import BCEWithLogitsLoss
 from ..parallel import comm
 
 
@@ -24,7 +25,9 @@ class EngineMLPTrainer:
         x, y = synthetic_batch_data(batch_size * n_batches, model.in_features, seed + comm.get_rank())
         self.X, self.Y = x.to(self.device), y.to(self.device)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.device)
-        self.crit = torch.nn.BCEWithLogitsLoss()
+        # the framework's drop-in for nn.BCEWithLogitsLoss (one HIP kernel: loss + d loss / d logits),
+        # as train.py uses on the engine path; it reads the bf16 logits as they are
+        self.crit = BCEWithLogitsLoss()
         world = comm.get_world_size()
         self.exchange = "none" if world == 1 else f"{comm.backend_name()}-bucketed"
         self.impl = f"dgt-engine+mfma{self.engine.fused_linear_layers}+zero{self.engine.stage}"
@@ -42,7 +45,7 @@ class EngineMLPTrainer:
         for _ in range(int(plan.shape[0])):
             j = self.global_steps % self.n_batches
             x, y = self.X[j * self.B:(j + 1) * self.B], self.Y[j * self.B:(j + 1) * self.B]
-            loss = self.crit(self.engine(x).view(-1).float(), y)
+            loss = self.crit(self.engine(x).view(-1), y)
             self.engine.backward(loss)
             self.engine.step()
             self.loss_acc += loss.detach().double()
