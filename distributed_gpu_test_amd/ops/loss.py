@@ -30,8 +30,10 @@ class _FusedBCEWithLogits(torch.autograd.Function):
     @staticmethod
     def backward(ctx, g: torch.Tensor):
         (dz,) = ctx.saved_tensors
-        gz = (dz * g).view(ctx.shape)
-        return (gz if ctx.dtype == torch.float32 else gz.to(ctx.dtype)), None
+        # scaled and cast to the logits' dtype in one pass (the fp32 product, rounded once)
+        gz = torch.empty(ctx.shape, dtype=ctx.dtype, device=dz.device)
+        torch.mul(dz.view(ctx.shape), g, out=gz)
+        return gz, None
 
 
 def bce_with_logits(z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:

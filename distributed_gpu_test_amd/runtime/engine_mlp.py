@@ -23,7 +23,8 @@ class EngineMLPTrainer:
         self.device = self.engine.device
         self.B, self.n_batches = batch_size, n_batches
         x, y = synthetic_batch_data(batch_size * n_batches, model.in_features, seed + comm.get_rank())
-        self.X, self.Y = x.to(self.device), y.to(self.device)
+        # the dataset held in the compute dtype (as MLPTrainer holds it): no per-step input cast
+        self.X, self.Y = x.to(self.device, self.engine.dtype), y.to(self.device)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.device)
         # the framework's drop-in for nn.BCEWithLogitsLoss (one HIP kernel: loss + d loss / d logits),
         # as train.py uses on the engine path; it reads the bf16 logits as they are
@@ -48,7 +49,7 @@ class EngineMLPTrainer:
             loss = self.crit(self.engine(x).view(-1), y)
             self.engine.backward(loss)
             self.engine.step()
-            self.loss_acc += loss.detach().double()
+            self.loss_acc.add_(loss.detach())  # fp32 loss added into the fp64 accumulator: one kernel
             self.global_steps += 1
 
     @property
