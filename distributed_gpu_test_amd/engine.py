@@ -175,7 +175,8 @@ class Engine:
         # backward overwrites every view anyway.  Should autograd itself accumulate into a view in that
         # backward (a forward that fell back to F.linear, a parameter outside the chains), the view is
         # zeroed just before (a tensor hook runs ahead of AccumulateGrad), and a view nothing writes is
-        # zeroed right after the backward (it got no gradient).
+        # zeroed right after the backward (it got no gradient).  So after step() such an engine's .grad
+        # views may still hold the last gradients until the next backward: engine.zero_grad() zeroes them.
         self._stored_all = False
         self._zero_deferred = False
         self._deferred_active = False
@@ -306,6 +307,8 @@ class Engine:
     def backward(self, loss: torch.Tensor, retain_graph: bool = False) -> torch.Tensor:
         loss = self.faults.maybe_corrupt_loss(loss, self.global_steps)
         boundary = self.is_gradient_accumulation_boundary()
+        if self._zero_deferred and self.store.user_set_grads():
+            self.zero_grad()  # a user gradient folds into the buffer below: it must be zero first
         if self.store.rebind_grads():
             self._grads_dirty = True
         self.reducer.arm(boundary and self.training)

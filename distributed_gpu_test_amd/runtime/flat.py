@@ -109,6 +109,14 @@ class FlatParamStore:
                 self.grad_views.append(self.grad_buf[off:off + n].view(shape))
                 p.grad = self.grad_views[-1]
 
+    def user_set_grads(self) -> bool:
+        """True if user code replaced some parameter's .grad (not None) since the last rebind."""
+        for p, view in zip(self.params, self.grad_views):
+            g = p.grad
+            if g is not None and g is not view and (g.data_ptr() != view.data_ptr() or g.shape != view.shape):
+                return True
+        return False
+
     def rebind_grads(self) -> bool:
         """Re-attach gradient views (after user code set ``.grad = None``).  Called every backward:
         the common case (every .grad still IS its cached view) costs one identity test per

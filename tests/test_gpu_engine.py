@@ -439,17 +439,20 @@ def test_engine_bf16_deferred_zero_grad_matches_autograd_engine():
     crit = torch.nn.BCEWithLogitsLoss()
     g = torch.Generator().manual_seed(4)
     deferred = []
-    for B in (256, 256, 256, 192, 256, 256):
+    for k, B in enumerate((256, 256, 256, 192, 256, 256)):
         x = torch.randn(B, 256, generator=g).to(torch.bfloat16).cuda()
         y = (torch.rand(B, generator=g) > 0.5).float().cuda()
         grads = []
         for e in engines:
             deferred.append(e._zero_deferred)
+            if k == 2:  # a user-set gradient on a deferred step folds into a zeroed buffer
+                p0 = next(e.module.parameters())
+                p0.grad = torch.full_like(p0, 0.01)
             e.backward(crit(e(x).view(-1).float(), y))
             grads.append(torch.cat([p.grad.float().reshape(-1) for p in e.module.parameters()]))
             e.step()
         torch.testing.assert_close(grads[0], grads[1], rtol=3e-2, atol=3e-4)
-    assert deferred[0::2] == [False, True, True, True, False, True]  # fused: the fallback step re-arms
+    assert deferred[0::2] == [False, True, True, True, False, True]  # the fallback step: a real fill after it
     assert not any(deferred[1::2])  # autograd's F.linear path adds: never deferred
     for e in engines:
         e.close()
