@@ -625,7 +625,8 @@ void skinny_fwd_bf16(const at::Tensor& a, const at::Tensor& W, const std::option
 // its backward: g = (dz . W) * 1[a > 0] (mask) and g^T; dW / db accumulate in fp32
 void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor& W, bool mask, const at::Tensor& g,
                      const std::optional<at::Tensor>& gT, const at::Tensor& dW, const at::Tensor& db,
-                     bool accumulate, const std::optional<at::Tensor>& bias_part) {
+                     bool accumulate, const std::optional<at::Tensor>& bias_part,
+                     const std::optional<at::Tensor>& dw_part) {
   const int64_t M = a.size(0), K = a.size(1), N = W.size(0);
   TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && W.size(1) == K && N >= 1 && N <= 4 && M % 64 == 0 && K % 64 == 0,
               "dgt: skinny_bwd needs a [M, K], W [N <= 4, K], M, K % 64 == 0");
@@ -650,9 +651,17 @@ void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor
     check_2d(*bias_part, "bias_part", at::kFloat, M / 64, K);
     bp = bias_part->data_ptr<float>();
   }
-  at::Tensor ws = at::empty({M / 64, N, K}, a.options().dtype(at::kFloat));  // per-row-tile dW partials
+  at::Tensor ws;  // per-row-tile dW partials: the caller's (reduced by it later) or this call's scratch
+  void* dwp = dW.data_ptr();
+  if (dw_part.has_value() && dw_part->defined()) {
+    check_2d(*dw_part, "dw_part", at::kFloat, M / 64, N * K);
+    ws = *dw_part;
+    dwp = nullptr;
+  } else {
+    ws = at::empty({M / 64, N, K}, a.options().dtype(at::kFloat));
+  }
   DGT_CHECK_HIP(dgt::skinny_bwd_bf16(dz.data_ptr(), a.data_ptr(), W.data_ptr(), mask ? 1 : 0, g.data_ptr(), gTp,
-                                     dW.data_ptr(), db.data_ptr(), bf ? 1 : 0, accumulate ? 1 : 0,
+                                     dwp, db.data_ptr(), bf ? 1 : 0, accumulate ? 1 : 0,
                                      ws.data_ptr<float>(), (int)M, (int)N, (int)K, stream_of(a), bp));
 }
 
@@ -877,7 +886,7 @@ TORCH_LIBRARY(dgt, m) {
   m.def("skinny_fwd_bf16(Tensor a, Tensor W, Tensor? b, Tensor(a!) z) -> ()", &skinny_fwd_bf16);
   m.def(
       "skinny_bwd_bf16(Tensor dz, Tensor a, Tensor W, bool mask, Tensor(a!) g, Tensor(b!)? gT, Tensor(c!) dW, "
-      "Tensor(d!) db, bool accumulate=True, Tensor(e!)? bias_part=None) -> ()",
+      "Tensor(d!) db, bool accumulate=True, Tensor(e!)? bias_part=None, Tensor(f!)? dw_part=None) -> ()",
       &skinny_bwd_bf16);
   m.def(
       "mlp_head(Tensor a, Tensor w, Tensor b0, Tensor y, Tensor(a!) dz, Tensor(b!) dw, Tensor(c!) db, "

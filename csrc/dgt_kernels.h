@@ -156,7 +156,8 @@ hipError_t rowsum_bf16(const void* in, void* out, int out_bf16, int rows, int co
 //             dW[N, K] (+)= dz^T . a, db[N] (+)= sum_m dz (fp32, or bf16 when dw_bf16: summed in fp32,
 //             rounded once; accumulate = 0 stores); part_ws: fp32 [M / 64, N, K] workspace (per-row-tile
 //             dW partials, summed in a fixed order: no atomics); bias_part (optional): fp32 [M / 64, K]
-//             per-row-tile column sums of g (the layer below's bias-gradient partials)
+//             per-row-tile column sums of g (the layer below's bias-gradient partials); dW == nullptr:
+//             part_ws is left to the caller to reduce (db is still formed)
 hipError_t skinny_fwd_bf16(const void* a, const void* W, const void* b, void* z, int M, int N, int K,
                            hipStream_t stream);
 hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mask, void* g, void* gT, void* dW,

@@ -322,6 +322,7 @@ hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mas
   }
   const hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
+  if (!dW) return hipSuccess;  // part_ws is the caller's: it reduces the partials (partials_reduce_multi)
   return partials_reduce(part_ws, dW, dw_bf16, M / 64, N * K, accumulate, stream);  // K % 64: whole float4s
 }
 

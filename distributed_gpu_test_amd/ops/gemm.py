@@ -158,13 +158,14 @@ def skinny_fwd_bf16(a: torch.Tensor, w: torch.Tensor, b: Optional[torch.Tensor],
 
 def skinny_bwd_bf16(dz: torch.Tensor, a: torch.Tensor, w: torch.Tensor, mask: bool, g: torch.Tensor,
                     gT: Optional[torch.Tensor], dw: torch.Tensor, db: torch.Tensor, accumulate: bool = True,
-                    bias_part: Optional[torch.Tensor] = None) -> None:
+                    bias_part: Optional[torch.Tensor] = None, dw_part: Optional[torch.Tensor] = None) -> None:
     """Its backward: g = (dz . w) * 1[a > 0] (if mask) and g^T (bf16); dw [N, K] and db [N] (both fp32
     or both bf16) receive dz^T . a and the column sums of dz: added (``accumulate``) or stored.
     ``bias_part`` (fp32 ``[M // 64, K]``): the per-64-row-tile column sums of the bf16 g (the layer
-    below's bias-gradient partials, for ``partials_reduce_multi``)."""
+    below's bias-gradient partials, for ``partials_reduce_multi``).  ``dw_part`` (fp32 ``[M // 64, N * K]``):
+    dw's per-64-row-tile partials are left there for the caller to reduce, and dw is not written."""
     if a.is_cuda:
-        require().skinny_bwd_bf16(dz, a, w, mask, g, gT, dw, db, bool(accumulate), bias_part)
+        require().skinny_bwd_bf16(dz, a, w, mask, g, gT, dw, db, bool(accumulate), bias_part, dw_part)
         return
     d = dz.float().reshape(a.shape[0], w.shape[0])
     gg = d @ w.float()
@@ -175,6 +176,11 @@ def skinny_bwd_bf16(dz: torch.Tensor, a: torch.Tensor, w: torch.Tensor, mask: bo
         bias_part.copy_(g.float().view(-1, 64, g.shape[1]).sum(1))
     if gT is not None:
         gT.copy_(gg.t().to(gT.dtype))
+    if dw_part is not None:
+        t = a.shape[0] // 64
+        dw_part.copy_(torch.einsum("trn,trk->tnk", d.view(t, 64, -1), a.float().view(t, 64, -1)).reshape(t, -1))
+        db.copy_(((db.float() + d.sum(0)) if accumulate else d.sum(0)).to(db.dtype))
+        return
     if accumulate:
         dw.copy_((dw.float() + d.t() @ a.float()).to(dw.dtype))
         db.copy_((db.float() + d.sum(0)).to(db.dtype))

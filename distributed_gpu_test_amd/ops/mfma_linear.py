@@ -150,7 +150,13 @@ class _MfmaChainFn(torch.autograd.Function):
             if direct:
                 # straight into the bucket's bf16 views, stored on their first write of this backward
                 db = pb.grad if pb is not None else torch.zeros(wh.shape[0], dtype=BF16, device=dev)
-                skinny_bwd_bf16(dout, xs[L], wh, mask_h, g, gT, pw.grad, db, accumulate=not store_w, bias_part=hb)
+                # dW's row-tile partials join the one reduction launch at the end (bias gradients)
+                hw = (torch.empty(M // 64, wh.numel(), dtype=torch.float32, device=dev)
+                      if pw.grad.data_ptr() % 8 == 0 else None)
+                skinny_bwd_bf16(dout, xs[L], wh, mask_h, g, gT, pw.grad, db, accumulate=not store_w, bias_part=hb,
+                                dw_part=hw)
+                if hw is not None:
+                    segs.append((hw, pw.grad.view(-1), not store_w))
             else:
                 dw = torch.zeros(wh.shape, dtype=torch.float32, device=dev)
                 db = torch.zeros(wh.shape[0], dtype=torch.float32, device=dev)

@@ -467,6 +467,17 @@ def test_skinny_bias_part_and_bf16_accumulating_reduce():
     torch.testing.assert_close(outs["cuda"][0].cpu(), outs["cpu"][0], rtol=1e-2, atol=1e-2)
     gc, bpc = outs["cuda"]
     torch.testing.assert_close(bpc, gc.float().view(M // 64, 64, K).sum(1), rtol=1e-5, atol=1e-5)
+    # dW left as per-row-tile partials for the caller (dw itself untouched; db still formed)
+    parts = {}
+    for dev in ("cpu", "cuda"):
+        g = torch.empty(M, K, dtype=torch.bfloat16, device=dev)
+        dw, db = torch.full((N, K), 7.0, device=dev), torch.zeros(N, device=dev)
+        dwp = torch.empty(M // 64, N * K, device=dev)
+        skinny_bwd_bf16(dz.to(dev), a.to(dev), w.to(dev), True, g, None, dw, db, accumulate=False, dw_part=dwp)
+        assert bool((dw == 7.0).all())
+        parts[dev] = (dwp, db)
+    torch.testing.assert_close(parts["cuda"][0].cpu(), parts["cpu"][0], rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(parts["cuda"][1].cpu(), parts["cpu"][1], rtol=1e-4, atol=1e-4)
     # bf16 outs (stored / accumulated), an fp32 accumulate, one launch; every out against the CPU path
     base = torch.randn(K, generator=g_)
     views = {dev: (torch.zeros(K, dtype=torch.bfloat16, device=dev), base.bfloat16().to(dev),
