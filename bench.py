@@ -271,8 +271,30 @@ def params_consistent(params, world: int) -> bool:
     return flag.item() == 0.0
 
 
+def self_launch(args, argv) -> "int | None":
+    """``python bench.py --gpus N`` (N > 1) with no launcher around it: start the N ranks the way the
+    reference's job does (``slurm_train.sbatch:18-23,36`` spawns ``nproc_per_node`` workers) -- one
+    torchrun CHILD process (never an exec: nothing here has touched the GPU yet, and nothing will in
+    this process), static rendezvous on 127.0.0.1, the same argv.  Rank 0's JSON line reaches our
+    stdout unchanged (inherited stdio); the return value is the child's exit code.  Returns None when
+    this process already is a rank (torchrun / SLURM / mpirun variables present) or N == 1."""
+    from distributed_gpu_test_amd.launch import free_port, resolve_rank_info
+    if args.gpus <= 1 or resolve_rank_info().source != "bare":
+        return None
+    import subprocess
+    argv = list(sys.argv[1:] if argv is None else argv)
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes", "1", "--nproc-per-node", str(args.gpus),
+           "--master-addr", "127.0.0.1", "--master-port", str(free_port()), os.path.abspath(__file__), *argv]
+    print(f"[bench] --gpus {args.gpus} without a launcher: starting {args.gpus} ranks under torchrun",
+          file=sys.stderr, flush=True)
+    return subprocess.call(cmd)
+
+
 def main(argv=None):
     args = parse_args(argv)
+    rc = self_launch(args, argv)
+    if rc is not None:
+        return rc
     os.environ.setdefault("DGT_QUIET", "1")  # the engine's steps_per_print lines would be timed too
     from distributed_gpu_test_amd.data import make_synthetic_data
     from distributed_gpu_test_amd.models import SimpleNet

@@ -85,7 +85,9 @@ _WARNED: set = set()
 
 def count_fallback(reason: str) -> None:
     FALLBACKS[reason] += 1
-    if reason not in _WARNED and os.environ.get("RANK", "0") == "0":
+    import torch.distributed as dist
+    rank0 = not (dist.is_available() and dist.is_initialized()) or dist.get_rank() == 0
+    if reason not in _WARNED and rank0:
         _WARNED.add(reason)
         print(f"[dgt] WARNING: Linear falls back to F.linear (vendor BLAS): {reason}", file=sys.stderr, flush=True)
 

@@ -10,16 +10,16 @@ from __future__ import annotations
 
 import datetime
 import os
-from dataclasses import replace
 from typing import Any, List, Optional
 
 import torch
 import torch.distributed as dist
 
 from ..accelerator import get_accelerator
-from ..launch import RankInfo, free_port, resolve_rank_info
+from ..launch import RankInfo, resolve_rank_info
 
 _RANK_INFO: Optional[RankInfo] = None
+_ENV_SET: List[str] = []  # os.environ keys init_distributed added (destroy() removes them)
 
 
 def default_backend() -> str:
@@ -32,12 +32,16 @@ def default_backend() -> str:
 
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
                      rank_info: Optional[RankInfo] = None, set_device: bool = True) -> RankInfo:
-    """Create the default process group (idempotent) and bind this rank's GPU."""
+    """Create the default process group (idempotent) and bind this rank's GPU.
+
+    The caller's ``os.environ`` is left alone: the rank variables are never exported (a child
+    process that inherited them would believe it was a torchrun rank).  A world-size-1 job, however
+    it was started, rendezvouses on an in-memory ``HashStore`` and opens no TCP port; a multi-rank
+    job started by SLURM or mpirun gets an explicit ``TCPStore`` built from the resolved rank info,
+    so ``env://`` (which reads ``RANK``/``MASTER_*``) is only used when torchrun already set them.
+    """
     global _RANK_INFO
     info = rank_info or resolve_rank_info()
-    if info.source == "bare" and not info.master_port:
-        info = replace(info, master_port=free_port(info.master_addr))
-    info.export()
     backend = backend or default_backend()
     accel = get_accelerator()
     if backend == "nccl":
@@ -46,12 +50,20 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
                                f"{accel.name!r} (no GPU visible, or DGT_ACCELERATOR=cpu)")
         if set_device:  # the reference's get_accelerator().set_device(local_rank) (train.py:61)
             accel.set_device(info.local_rank)
-        # hangs become errors instead of silent stalls
-        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        # hangs become errors instead of silent stalls; a torch knob read when the
+        # process group is created, restored by destroy()
+        if "TORCH_NCCL_ASYNC_ERROR_HANDLING" not in os.environ:
+            os.environ["TORCH_NCCL_ASYNC_ERROR_HANDLING"] = "1"
+            _ENV_SET.append("TORCH_NCCL_ASYNC_ERROR_HANDLING")
     if not dist.is_initialized():
         timeout = datetime.timedelta(seconds=timeout_s)
         restart = int(os.environ.get("TORCHELASTIC_RESTART_COUNT", "0") or 0)
-        if restart > 0 and info.world_size > 1:
+        if info.world_size == 1:
+            # a lone process has nobody to rendezvous with: an in-memory store, no TCP port to race
+            # for, whatever launcher variables the environment happens to carry
+            dist.init_process_group(backend=backend, store=dist.HashStore(), rank=0, world_size=1,
+                                    timeout=timeout)
+        elif restart > 0:
             # elastic restart (torchrun --max-restarts): the agent's store still holds the previous
             # attempt's keys (dead peers' addresses); rendezvous under a per-attempt prefix instead
             agent_store = os.environ.get("TORCHELASTIC_USE_AGENT_STORE") == "True"
@@ -60,14 +72,17 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
             store = dist.PrefixStore(f"/dgt/attempt_{restart}", store)
             dist.init_process_group(backend=backend, store=store, rank=info.rank, world_size=info.world_size,
                                     timeout=timeout)
-        elif info.source == "bare" and info.world_size == 1:
-            # a lone process has nobody to rendezvous with: an in-memory store, no TCP port to race
-            # for (MASTER_ADDR / MASTER_PORT are still exported for tools that read them)
-            dist.init_process_group(backend=backend, store=dist.HashStore(), rank=0, world_size=1,
-                                    timeout=timeout)
-        else:
+        elif info.source == "torchrun":
+            # torchrun exported RANK / MASTER_*; env:// also honours its agent-hosted store
             dist.init_process_group(backend=backend, init_method="env://", rank=info.rank,
                                     world_size=info.world_size, timeout=timeout)
+        else:
+            # SLURM / mpirun / explicit rank info: the rendezvous store straight from the resolved
+            # info (rank 0 hosts it), nothing written into the environment
+            store = dist.TCPStore(info.master_addr, info.master_port, info.world_size,
+                                  is_master=(info.rank == 0), timeout=timeout)
+            dist.init_process_group(backend=backend, store=store, rank=info.rank, world_size=info.world_size,
+                                    timeout=timeout)
     _RANK_INFO = info
     return info
 
@@ -170,3 +185,7 @@ def destroy() -> None:
             dist.destroy_process_group()
     except Exception:
         pass
+    global _RANK_INFO
+    _RANK_INFO = None
+    while _ENV_SET:
+        os.environ.pop(_ENV_SET.pop(), None)

@@ -23,6 +23,17 @@ def pytest_collection_modifyitems(config, items):
             item.add_marker(skip)
 
 
+@pytest.fixture(autouse=True)
+def _restore_environ():
+    """Every test sees (and leaves) the session's environment: nothing a test or the code under
+    test writes into os.environ leaks into a later test or the subprocesses it starts."""
+    saved = dict(os.environ)
+    yield
+    if dict(os.environ) != saved:
+        os.environ.clear()
+        os.environ.update(saved)
+
+
 @pytest.fixture(scope="session", autouse=True)
 def _teardown_process_group():
     """Tests that initialise the default process group in-process (engine, graph impl, native RCCL)

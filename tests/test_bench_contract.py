@@ -56,6 +56,22 @@ def test_bench_two_ranks_gloo_cpu():
     assert lines[0]["config"]["closing_barrier"] == "process-group"
 
 
+def test_bench_self_launches_n_ranks_cpu():
+    """``python bench.py --gpus 2`` with no launcher env starts its own 2 ranks (a torchrun child
+    process) and relays rank 0's single JSON line; the exit code is the child's."""
+    env = dict(os.environ, DGT_QUIET="1", OMP_NUM_THREADS="1")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        env.pop(k, None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "30",
+                        "--warmup", "3"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    _check(lines[0], 2, 30, 3)
+    assert lines[0]["ranks"] == 2 and lines[0]["config"]["parallelism"] == "dp2"
+    assert "starting 2 ranks under torchrun" in r.stderr
+
+
 def test_exchange_line_selection(monkeypatch):
     import pytest
     from distributed_gpu_test_amd.runtime.tiny_trainer import line_candidates

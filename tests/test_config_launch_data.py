@@ -1,5 +1,7 @@
 """T0 unit tests: config schema + batch assertion, rank discovery, sampler parity."""
 import json
+import os
+import socket
 
 import pytest
 import torch
@@ -97,6 +99,45 @@ def test_rank_info_bare():
     assert (ri.rank, ri.world_size, ri.source) == (0, 1, "bare")
     env = ri.export({})
     assert env["WORLD_SIZE"] == "1" and env["RANK"] == "0"
+
+
+_LAUNCH_VARS = ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "GROUP_RANK", "MASTER_ADDR",
+                "MASTER_PORT", "TORCH_NCCL_ASYNC_ERROR_HANDLING")
+
+
+def test_init_distributed_leaves_environ_unchanged(monkeypatch):
+    """In-process init + destroy writes nothing into os.environ (a later child process must not
+    inherit rank variables and believe it is a torchrun rank)."""
+    from distributed_gpu_test_amd.parallel import comm
+    comm.destroy()
+    for k in _LAUNCH_VARS:
+        monkeypatch.delenv(k, raising=False)
+    before = dict(os.environ)
+    info = comm.init_distributed(backend="gloo")
+    assert (info.world_size, info.source) == (1, "bare")
+    assert dict(os.environ) == before
+    assert resolve_rank_info().source == "bare"
+    comm.destroy()
+    assert dict(os.environ) == before and not comm.is_initialized()
+
+
+def test_world_size_one_never_opens_a_tcp_port(monkeypatch):
+    """RANK=0 WORLD_SIZE=1 with MASTER_PORT pointing at a port another process holds (the
+    GPUTEST_r03 EADDRINUSE failure): a 1-rank job rendezvouses on a HashStore and starts anyway."""
+    from distributed_gpu_test_amd.parallel import comm
+    comm.destroy()
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as busy:
+        busy.bind(("127.0.0.1", 0))
+        busy.listen(1)
+        port = busy.getsockname()[1]
+        monkeypatch.setenv("RANK", "0")
+        monkeypatch.setenv("WORLD_SIZE", "1")
+        monkeypatch.setenv("MASTER_ADDR", "127.0.0.1")
+        monkeypatch.setenv("MASTER_PORT", str(port))
+        info = comm.init_distributed(backend="gloo", timeout_s=20)
+        assert (info.world_size, info.source) == (1, "torchrun")
+        assert comm.get_world_size() == 1
+        comm.destroy()
 
 
 # ------------------------------------------------------------------ data

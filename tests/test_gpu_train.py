@@ -73,8 +73,14 @@ def test_train_py_zero1_config_runs_on_fused_kernel(tmp_path):
 
 
 def test_bench_zero1_driver_shape():
-    """bench.py --zero-stage 1 at the driver's shape on one GPU: the fused kernel, >= 300k it/s."""
+    """bench.py --zero-stage 1 at the driver's shape on one GPU: the CLI's ZeRO-1 selection reaches
+    the fused kernel and keeps >= 300k it/s.  At one rank nothing is sharded (the owner shard is the
+    whole vector), so this pins the plumbing only; the sharded exchange itself is covered by the
+    multi-rank rehearsals in tests/test_gpu_multiproc.py.  The launcher variables are scrubbed: the
+    child must resolve as a bare single process whatever this pytest process carries."""
     env = dict(os.environ, DGT_QUIET="1")
+    for k in ("RANK", "LOCAL_RANK", "WORLD_SIZE", "LOCAL_WORLD_SIZE", "MASTER_PORT", "GROUP_RANK"):
+        env.pop(k, None)
     r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "20", "--warmup", "5",
                         "--zero-stage", "1"], cwd=ROOT, env=env, capture_output=True, text=True, timeout=240)
     assert r.returncode == 0, r.stderr[-3000:]
