@@ -391,9 +391,9 @@ def main(argv=None):
     global_steps_per_s = args.steps / elapsed_max
     if args.model == "mlp":
         tflops = trainer.flops_per_step() * world * global_steps_per_s / 1e12
+        dtype = getattr(trainer, "dtype_name", "bf16")
         model_desc = (f"SyntheticMLP {args.depth}x[Linear({args.width},{args.width})+ReLU] + Linear({args.width},1) "
-                      f"+ BCEWithLogits + Adam, bf16 MFMA")
-        dtype = "bf16"
+                      f"+ BCEWithLogits + Adam, {dtype} MFMA")
     else:
         tflops = None
         model_desc = "SimpleNet Linear(20,64)-ReLU-Linear(64,1) + BCEWithLogits + Adam(1e-3)"

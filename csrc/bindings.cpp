@@ -317,6 +317,85 @@ void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, 
                                 stream_of(x)));
 }
 
+// Exact-fp32 MFMA GEMM (gemm_f32.hip): C[M, N] (+)= epi(A . B) with A [M, K] (la 0) or [K, M] (la 1),
+// B [N, K] (lb 0) or [K, N] (lb 1), all contiguous; split-K partials in a caching-allocator workspace.
+void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& maskA,
+              const std::optional<at::Tensor>& bias, const at::Tensor& C, int64_t la, int64_t lb, bool relu,
+              bool accumulate) {
+  check_gpu(A, "A", at::kFloat);
+  check_gpu(B, "B", at::kFloat);
+  check_gpu(C, "C", at::kFloat);
+  TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && C.dim() == 2 && (la == 0 || la == 1) && (lb == 0 || lb == 1),
+              "dgt: gemm_f32 takes 2-D operands and layouts 0 / 1");
+  const int64_t M = la == 0 ? A.size(0) : A.size(1), K = la == 0 ? A.size(1) : A.size(0);
+  const int64_t N = lb == 0 ? B.size(0) : B.size(1), Kb = lb == 0 ? B.size(1) : B.size(0);
+  TORCH_CHECK(K == Kb && C.size(0) == M && C.size(1) == N, "dgt: gemm_f32 shapes: A ", A.sizes(), " (layout ", la,
+              "), B ", B.sizes(), " (layout ", lb, "), C ", C.sizes());
+  TORCH_CHECK(M < (1LL << 31) && N < (1LL << 31) && K < (1LL << 31), "dgt: gemm_f32 dims must fit in int32");
+  dgt::GemmF32Args a{};
+  a.A = A.data_ptr<float>();
+  a.B = B.data_ptr<float>();
+  if (maskA.has_value() && maskA->defined()) {
+    check_gpu(*maskA, "maskA", at::kFloat);
+    TORCH_CHECK(maskA->sizes() == A.sizes(), "dgt: gemm_f32 maskA must have A's shape");
+    a.maskA = maskA->data_ptr<float>();
+  }
+  if (bias.has_value() && bias->defined()) {
+    check_gpu(*bias, "bias", at::kFloat);
+    TORCH_CHECK(bias->numel() == N, "dgt: gemm_f32 bias must have N elements");
+    a.bias = bias->data_ptr<float>();
+  }
+  a.C = C.data_ptr<float>();
+  a.M = (int)M;
+  a.N = (int)N;
+  a.K = (int)K;
+  a.lda = A.size(1);
+  a.ldb = B.size(1);
+  a.ldc = N;
+  a.relu = relu ? 1 : 0;
+  a.accumulate = accumulate ? 1 : 0;
+  if (M == 0 || N == 0) return;
+  c10::DeviceGuard guard(A.device());
+  if (K == 0) {  // an empty sum: the epilogue of zero
+    at::Tensor z = at::zeros_like(C);
+    if (a.bias) z.add_(*bias);
+    if (relu) z.clamp_min_(0.f);
+    if (accumulate) C.add_(z); else C.copy_(z);
+    return;
+  }
+  const dgt::GemmF32Plan plan = dgt::gemm_f32_plan(a.M, a.N, a.K);
+  at::Tensor ws;
+  if (plan.splits > 1) {
+    ws = at::empty({(int64_t)plan.splits * M * N}, A.options());
+    a.ws = ws.data_ptr<float>();
+  }
+  DGT_CHECK_HIP(dgt::gemm_f32(a, (int)la, (int)lb, plan, stream_of(A)));
+}
+
+// db[n] (+)= sum_m dy[m][n] (* 1[y[m][n] > 0]), deterministic two-pass column sum
+void colsum_f32(const at::Tensor& dy, const std::optional<at::Tensor>& y, const at::Tensor& db, bool accumulate) {
+  check_gpu(dy, "dy", at::kFloat);
+  check_gpu(db, "db", at::kFloat);
+  TORCH_CHECK(dy.dim() == 2 && db.numel() == dy.size(1), "dgt: colsum_f32 shapes: dy [M, N], db [N]");
+  const float* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    check_gpu(*y, "y", at::kFloat);
+    TORCH_CHECK(y->sizes() == dy.sizes(), "dgt: colsum_f32 mask must have dy's shape");
+    yp = y->data_ptr<float>();
+  }
+  const int M = (int)dy.size(0), N = (int)dy.size(1);
+  if (N == 0) return;
+  c10::DeviceGuard guard(dy.device());
+  if (M == 0) {
+    if (!accumulate) db.zero_();
+    return;
+  }
+  const int slices = dgt::colsum_f32_slices(M, N);
+  at::Tensor part = at::empty({(int64_t)slices * N}, dy.options());
+  DGT_CHECK_HIP(dgt::colsum_f32(dy.data_ptr<float>(), yp, db.data_ptr<float>(), part.data_ptr<float>(), M, N, slices,
+                                accumulate, stream_of(dy)));
+}
+
 void bce_logits(const at::Tensor& z, const at::Tensor& y, const at::Tensor& loss, const at::Tensor& dz) {
   TORCH_CHECK(z.is_cuda() && z.is_contiguous() && (z.scalar_type() == at::kFloat || z.scalar_type() == at::kBFloat16),
               "dgt: bce_logits needs contiguous fp32 / bf16 GPU logits");
@@ -870,6 +949,10 @@ TORCH_LIBRARY(dgt, m) {
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz) -> ()", &bce_logits);
   m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
+  m.def("gemm_f32(Tensor A, Tensor B, Tensor? maskA, Tensor? bias, Tensor(a!) C, int la, int lb, bool relu=False, "
+        "bool accumulate=False) -> ()",
+        &gemm_f32);
+  m.def("colsum_f32(Tensor dy, Tensor? y, Tensor(a!) db, bool accumulate=False) -> ()", &colsum_f32);
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor W, Tensor? y, Tensor(a!)? dx, Tensor(b!) dW, Tensor(c!)? db, "
         "bool accumulate=False) -> ()",
         &linear_bwd);

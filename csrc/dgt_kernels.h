@@ -93,6 +93,33 @@ hipError_t linear_bwd(const float* dy, const float* x, const float* W, const flo
 hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz,
                       hipStream_t stream);
 
+// ---------------------------------------------------------------- exact-fp32 MFMA GEMM (gemm_f32.hip)
+// C[M, N] (+)= epi(sum_k A(m, k) B(n, k)); A layout la: 0 = [M][K] (lda), 1 = [K][M]; B layout
+// lb: 0 = [N][K] (ldb), 1 = [K][N].  maskA (same layout / ld as A, optional): A(m, k) counts only
+// where maskA > 0 (the ReLU mask of a backward).  Epilogue: + bias[n], ReLU, accumulate into C.
+struct GemmF32Args {
+  const float* A;
+  const float* B;
+  const float* maskA;
+  const float* bias;
+  float* C;
+  float* ws;  // split-K partials, splits * M * N floats (plan.splits > 1 only)
+  int M, N, K;
+  long long lda, ldb, ldc;
+  int relu;
+  int accumulate;
+};
+struct GemmF32Plan {
+  bool big;    // 128x128 block tile (else 64x64)
+  int splits;  // split-K slices (1 = none)
+};
+GemmF32Plan gemm_f32_plan(int M, int N, int K);
+hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& plan, hipStream_t stream);
+// db[n] (+)= sum_m dy[m][n] * (y ? 1[y[m][n] > 0] : 1) over row slices (part: slices * N floats)
+int colsum_f32_slices(int M, int N);
+hipError_t colsum_f32(const float* dy, const float* y, float* db, float* part, int M, int N, int slices,
+                      bool accumulate, hipStream_t stream);
+
 // ---------------------------------------------------------------- IPC one-shot all-reduce
 // in[n] (fp32) from every rank -> out[n] = scale * sum over ranks (rank order, identical bits on
 // every rank).  Uses the Exchange mailboxes; n <= ex.stride.

@@ -1,0 +1,360 @@
+// Exact-fp32 GEMM on the CDNA4 matrix cores (v_mfma_f32_32x32x2_f32) for the engine's fp32
+// nn.Linear layers beyond the small-batch kernels of linear.hip ("bf16 + fp32").
+//
+//   C[M, N] (op)= epi( sum_k A(m, k) * B(n, k) )
+//
+// Each operand is read in whichever of its two row-major layouts it already has, so no Linear
+// product needs a transposed copy:
+//   A: LA = 0 "MK" A[m * lda + k]   (k contiguous)       LA = 1 "KM" A[k * lda + m]   (m contiguous)
+//   B: LB = 0 "NK" B[n * ldb + k]                        LB = 1 "KN" B[k * ldb + n]
+// The three products of a Linear layer y = x W^T + b (x [M, K], W [N, K], dy [M, N]):
+//   forward  y  = x . W^T          A = x  (MK), B = W  (NK)     epilogue: + bias, ReLU
+//   dgrad    dx = g . W            A = g  (MK), B = W  (KN)     g = dy * 1[y > 0] (ReLU mask on A)
+//   wgrad    dW = g^T . x          A = g  (KM), B = x  (KN)     epilogue: accumulate into .grad
+//
+// Numerics: v_mfma_f32_32x32x2_f32 is bitwise an fp32 fmaf chain (cdna_hip_programming.md §3
+// "FP32-input MFMA"): no TF32-style rounding of the inputs, so results agree with an fp32 reference
+// to summation-order rounding only.
+//
+// Block: BM x BN (128 x 128 or 64 x 64), BK = 32, 256 threads = 4 waves in 2 x 2, each wave
+// (BM/2) x (BN/2) = TM x TN 32 x 32 accumulators.  The MFMA takes ONE f32 per lane per operand:
+// lane l holds A[row l & 31][k-slot l >> 5].  Every 8-deep k group is consumed as 4 MFMA steps in
+// which lane half h takes physical k = 8g + 4h + s (s = 0..3), the same map for both operands, so:
+//   an MK/NK tile sits in LDS as [row][32 k] (128-B rows) and a lane fetches its 4 k values of a
+//     group with ONE ds_read_b128; the 16-B chunk is XOR-swizzled by (row >> 1) & 7, which makes
+//     all four 16-lane groups of the b128 read conflict-free (checked exhaustively for the gfx950
+//     lane groups of MI355X_MICROARCH.md §LDS);
+//   a KM/KN tile sits in LDS as [32 k][rows] as it lies in memory, and a lane fetches k = 8g+4h+s
+//     with ds_read_b32 (each 32-lane half reads 32 consecutive rows of one k: conflict-free).
+// Staging is global -> VGPR -> LDS (16-B loads, zero-filled outside M / N / K, which is what makes
+// ragged shapes exact), double-buffered: the next K-tile's loads are in flight while the current
+// one feeds the MFMAs, one barrier per K-tile.  fp32 MFMA runs at 1/16 of the bf16 rate, so the
+// staging path is far from the bound; what matters is keeping 2+ waves per SIMD (two 128x128 blocks
+// or four 64x64 blocks per CU) and enough blocks for 256 CUs, hence the 64x64 tile and split-K for
+// small grids.  Block ids go through the XCD-aware remap (T1) so an XCD's blocks share panels in L2.
+// Reference: the fp32 nn.Linear layers of train.py:29-33 (forward train.py:107, backward :113).
+#include "dgt_common.h"
+#include "dgt_kernels.h"
+
+namespace dgt {
+namespace f32g {
+
+constexpr int BK = 32;
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+// ----------------------------------------------------------------------------- staging
+// One operand tile of ROWS rows x BK k.  MK form: ROWS*BK/4 16-byte chunks, chunk c of row r ->
+// LDS [r][c ^ ((r >> 1) & 7)].  KM form: chunk = 4 consecutive rows of one k -> LDS [k][rows].
+template <bool KMAJ, int ROWS, bool VEC>
+struct Tile {
+  static constexpr int CHUNKS = ROWS * BK / 4;
+  static constexpr int PER = CHUNKS / 256;  // chunks per thread (256 threads)
+  f32x4 v[PER];
+
+  // rows [r0, r0 + ROWS) of the operand, k-tile [k0, k0 + BK); extent nr rows, nk k; ld elements
+  DGT_DEVICE void load(const float* __restrict__ p, const float* __restrict__ mask, long long ld, int r0, int k0,
+                       int nr, int nk, int tid) {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + 256 * i;
+      int r, k;  // first element of the chunk
+      if (!KMAJ) {
+        r = c / (BK / 4);
+        k = (c % (BK / 4)) * 4;
+      } else {
+        k = c / (ROWS / 4);
+        r = (c % (ROWS / 4)) * 4;
+      }
+      const int gr = r0 + r, gk = k0 + k;
+      f32x4 x = {0.f, 0.f, 0.f, 0.f};
+      if (VEC) {
+        // extents of the contiguous dim are multiples of 4 here, so a chunk is all in or all out
+        const bool ok = KMAJ ? (gk < nk && gr < nr) : (gr < nr && gk < nk);
+        if (ok) {
+          const long long off = KMAJ ? (long long)gk * ld + gr : (long long)gr * ld + gk;
+          x = *reinterpret_cast<const f32x4*>(p + off);
+          if (mask) {
+            const f32x4 mk = *reinterpret_cast<const f32x4*>(mask + off);
+#pragma unroll
+            for (int e = 0; e < 4; ++e) x[e] = mk[e] > 0.f ? x[e] : 0.f;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = KMAJ ? gr + e : gr, kk = KMAJ ? gk : gk + e;
+          if (rr < nr && kk < nk) {
+            const long long off = KMAJ ? (long long)kk * ld + rr : (long long)rr * ld + kk;
+            float val = p[off];
+            if (mask && !(mask[off] > 0.f)) val = 0.f;
+            x[e] = val;
+          }
+        }
+      }
+      v[i] = x;
+    }
+  }
+
+  DGT_DEVICE void store(float* lds, int tid) const {
+#pragma unroll
+    for (int i = 0; i < PER; ++i) {
+      const int c = tid + 256 * i;
+      int off;
+      if (!KMAJ) {
+        const int r = c / (BK / 4), ch = c % (BK / 4);
+        off = r * BK + ((ch ^ ((r >> 1) & 7)) << 2);
+      } else {
+        off = c * 4;  // [k][ROWS], chunks in memory order
+      }
+      *reinterpret_cast<f32x4*>(lds + off) = v[i];
+    }
+  }
+};
+
+// A lane's 4 values (s = 0..3) of k group g for the 32-row MFMA tile starting at row rb.
+template <bool KMAJ, int ROWS>
+DGT_DEVICE f32x4 frag(const float* lds, int rb, int g, int lane) {
+  const int r = rb + (lane & 31), h = lane >> 5;
+  if (!KMAJ) {
+    const int ch = 2 * g + h;
+    return *reinterpret_cast<const f32x4*>(lds + r * BK + ((ch ^ ((r >> 1) & 7)) << 2));
+  } else {
+    const int k = 8 * g + 4 * h;
+    f32x4 x;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) x[s] = lds[(k + s) * ROWS + r];
+    return x;
+  }
+}
+
+// XCD-aware bijective remap (T1): blocks b and b + 8 run on one XCD; each XCD gets a contiguous run
+// of tile ids, walked in groups of GROUP block-rows so neighbours reuse B panels in the XCD's L2.
+DGT_DEVICE void tile_of(int bid, int nbm, int nbn, int& tm, int& tn) {
+  const int nwg = nbm * nbn, xcd = bid % 8, q = nwg / 8, rm = nwg % 8;
+  const int wgid = (xcd < rm ? xcd * (q + 1) : rm * (q + 1) + (xcd - rm) * q) + bid / 8;
+  constexpr int GROUP = 8;
+  const int group = wgid / (GROUP * nbn), first = group * GROUP;
+  const int gsize = min(nbm - first, GROUP);
+  tm = first + (wgid % (GROUP * nbn)) % gsize;
+  tn = (wgid % (GROUP * nbn)) / gsize;
+}
+
+// grid.x = tiles, grid.y = split-K slices.  Split slices write raw partial sums to ws[z][M][N]
+// (epilogue in gemm_f32_splitk_reduce); an unsplit launch applies the epilogue itself.
+template <int LA, int LB, int BM, int BN, bool VEC>
+__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args a) {
+  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+  constexpr int A_SZ = BM * BK, B_SZ = BN * BK;
+  __shared__ __attribute__((aligned(16))) float lds[2][A_SZ + B_SZ];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+  int tm, tn;
+  tile_of(blockIdx.x, nbm, nbn, tm, tn);
+  const int m0 = tm * BM, n0 = tn * BN;
+  // this slice's k range (whole K-tiles)
+  const int ktiles = (a.K + BK - 1) / BK;
+  const int per = (ktiles + gridDim.y - 1) / gridDim.y;
+  const int kt0 = blockIdx.y * per, kt1 = min(ktiles, kt0 + per);
+
+  f32x16 acc[TM][TN];
+#pragma unroll
+  for (int i = 0; i < TM; ++i)
+#pragma unroll
+    for (int j = 0; j < TN; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  Tile<LA == 1, BM, VEC> ta;
+  Tile<LB == 1, BN, VEC> tb;
+  if (kt0 < kt1) {
+    ta.load(a.A, a.maskA, a.lda, m0, kt0 * BK, a.M, a.K, tid);
+    tb.load(a.B, nullptr, a.ldb, n0, kt0 * BK, a.N, a.K, tid);
+    ta.store(lds[0], tid);
+    tb.store(lds[0] + A_SZ, tid);
+  }
+  __syncthreads();
+  for (int kt = kt0; kt < kt1; ++kt) {
+    const int buf = (kt - kt0) & 1;
+    const bool more = kt + 1 < kt1;
+    if (more) {  // next K-tile in flight while this one is consumed
+      ta.load(a.A, a.maskA, a.lda, m0, (kt + 1) * BK, a.M, a.K, tid);
+      tb.load(a.B, nullptr, a.ldb, n0, (kt + 1) * BK, a.N, a.K, tid);
+    }
+    const float* la = lds[buf];
+    const float* lb = lds[buf] + A_SZ;
+#pragma unroll
+    for (int g = 0; g < BK / 8; ++g) {
+      f32x4 fa[TM], fb[TN];
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[i] = frag<LA == 1, BM>(la, wm * WM + 32 * i, g, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[j] = frag<LB == 1, BN>(lb, wn * WN + 32 * j, g, lane);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
+#pragma unroll
+        for (int i = 0; i < TM; ++i)
+#pragma unroll
+          for (int j = 0; j < TN; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+    }
+    if (more) {
+      ta.store(lds[buf ^ 1], tid);
+      tb.store(lds[buf ^ 1] + A_SZ, tid);
+    }
+    __syncthreads();
+  }
+
+  // epilogue: 32x32 accumulator layout col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
+  const bool split = gridDim.y > 1;
+  float* out = split ? a.ws + (long long)blockIdx.y * a.M * a.N : a.C;
+  const long long ldo = split ? a.N : a.ldc;
+#pragma unroll
+  for (int j = 0; j < TN; ++j) {
+    const int n = n0 + wn * WN + 32 * j + (lane & 31);
+    if (n >= a.N) continue;
+    const float bias = (!split && a.bias) ? a.bias[n] : 0.f;
+#pragma unroll
+    for (int i = 0; i < TM; ++i) {
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = m0 + wm * WM + 32 * i + (e & 3) + 8 * (e >> 2) + 4 * (lane >> 5);
+        if (m >= a.M) continue;
+        float v = acc[i][j][e];
+        float* dst = out + (long long)m * ldo + n;
+        if (!split) {
+          v += bias;
+          if (a.relu) v = fmaxf(v, 0.f);
+          if (a.accumulate) v += *dst;
+        }
+        *dst = v;
+      }
+    }
+  }
+}
+
+// C = epi(sum over z of ws[z]) in slice order (deterministic), 4 elements per thread.
+__global__ __launch_bounds__(256) void gemm_f32_splitk_reduce(GemmF32Args a, int splits) {
+  const long long total = (long long)a.M * a.N;
+  const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= total) return;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const long long i = i0 + e;
+    if (i >= total) break;
+    float v = 0.f;
+    for (int z = 0; z < splits; ++z) v += a.ws[(long long)z * total + i];
+    const int m = (int)(i / a.N), n = (int)(i % a.N);
+    if (a.bias) v += a.bias[n];
+    if (a.relu) v = fmaxf(v, 0.f);
+    float* dst = a.C + (long long)m * a.ldc + n;
+    if (a.accumulate) v += *dst;
+    *dst = v;
+  }
+}
+
+// ----------------------------------------------------------------------------- bias gradient
+// part[s][n] = sum over rows m of slice s of dy[m][n] * (y ? 1[y[m][n] > 0] : 1); 64 columns x 4
+// row lanes per block, rows strided by 4, combined in LDS in a fixed order.
+__global__ __launch_bounds__(256) void colsum_f32_partial(const float* __restrict__ dy, const float* __restrict__ y,
+                                                         float* __restrict__ part, int M, int N, int rows_per) {
+  __shared__ float red[4][64];
+  const int c = threadIdx.x & 63, rl = threadIdx.x >> 6;
+  const int n = blockIdx.x * 64 + c;
+  const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
+  float s = 0.f;
+  if (n < N) {
+    for (int m = r0 + rl; m < r1; m += 4) {
+      const long long off = (long long)m * N + n;
+      const float d = dy[off];
+      s += (y && !(y[off] > 0.f)) ? 0.f : d;
+    }
+  }
+  red[rl][c] = s;
+  __syncthreads();
+  if (rl == 0 && n < N) part[(long long)blockIdx.y * N + n] = ((red[0][c] + red[1][c]) + red[2][c]) + red[3][c];
+}
+
+__global__ __launch_bounds__(256) void colsum_f32_final(const float* __restrict__ part, float* __restrict__ db,
+                                                       int N, int slices, int accumulate) {
+  const int n = blockIdx.x * 256 + threadIdx.x;
+  if (n >= N) return;
+  float s = 0.f;
+  for (int z = 0; z < slices; ++z) s += part[(long long)z * N + n];
+  db[n] = accumulate ? db[n] + s : s;
+}
+
+template <int LA, int LB, int BM, int BN>
+hipError_t launch(const GemmF32Args& a, bool vec, int splits, hipStream_t stream) {
+  const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
+  const dim3 grid((unsigned)tiles, (unsigned)splits);
+  if (vec)
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true>), grid, dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false>), grid, dim3(256), 0, stream, a);
+  return hipGetLastError();
+}
+
+template <int LA, int LB>
+hipError_t dispatch(const GemmF32Args& a, bool big, bool vec, int splits, hipStream_t stream) {
+  return big ? launch<LA, LB, 128, 128>(a, vec, splits, stream) : launch<LA, LB, 64, 64>(a, vec, splits, stream);
+}
+
+}  // namespace f32g
+
+GemmF32Plan gemm_f32_plan(int M, int N, int K) {
+  GemmF32Plan p;
+  const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
+  const long long t64 = (long long)((M + 63) / 64) * ((N + 63) / 64);
+  p.big = t128 >= 256;  // a full wave of 128x128 blocks; else 4x the blocks at 64x64
+  const long long tiles = p.big ? t128 : t64;
+  const int ktiles = (K + f32g::BK - 1) / f32g::BK;
+  p.splits = 1;
+  // small grid, long K (e.g. a wgrad whose reduction runs over a large batch): split K so the
+  // launch covers the chip; partial sums are combined in slice order (deterministic)
+  while (tiles * p.splits < 256 && ktiles / (2 * p.splits) >= 8 && p.splits < 16) p.splits *= 2;
+  return p;
+}
+
+hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& p, hipStream_t stream) {
+  if (a.M <= 0 || a.N <= 0 || a.K <= 0 || la < 0 || la > 1 || lb < 0 || lb > 1) return hipErrorInvalidValue;
+  if (p.splits > 1 && a.ws == nullptr) return hipErrorInvalidValue;
+  // 16-byte loads need the contiguous extent, the leading dims and the bases aligned to 4 floats
+  const int ca = la == 0 ? a.K : a.M, cb = lb == 0 ? a.K : a.N;
+  const bool vec = (ca % 4 == 0) && (cb % 4 == 0) && (a.lda % 4 == 0) && (a.ldb % 4 == 0) &&
+                   ((uintptr_t)a.A % 16 == 0) && ((uintptr_t)a.B % 16 == 0) &&
+                   (a.maskA == nullptr || (uintptr_t)a.maskA % 16 == 0);
+  hipError_t e;
+  const int code = la * 2 + lb;
+  switch (code) {
+    case 0: e = f32g::dispatch<0, 0>(a, p.big, vec, p.splits, stream); break;
+    case 1: e = f32g::dispatch<0, 1>(a, p.big, vec, p.splits, stream); break;
+    case 3: e = f32g::dispatch<1, 1>(a, p.big, vec, p.splits, stream); break;
+    default: e = f32g::dispatch<1, 0>(a, p.big, vec, p.splits, stream); break;
+  }
+  if (e != hipSuccess || p.splits == 1) return e;
+  const long long total = (long long)a.M * a.N;
+  hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce, dim3((unsigned)((total + 1023) / 1024)), dim3(256), 0, stream, a,
+                     p.splits);
+  return hipGetLastError();
+}
+
+int colsum_f32_slices(int M, int N) {
+  const int cb = (N + 63) / 64;
+  int s = 1;
+  while (cb * s < 512 && M / (s * 2) >= 64) s *= 2;
+  return s;
+}
+
+hipError_t colsum_f32(const float* dy, const float* y, float* db, float* part, int M, int N, int slices,
+                      bool accumulate, hipStream_t stream) {
+  if (M <= 0 || N <= 0 || slices <= 0) return hipErrorInvalidValue;
+  const int rows_per = (M + slices - 1) / slices;
+  hipLaunchKernelGGL(f32g::colsum_f32_partial, dim3((unsigned)((N + 63) / 64), (unsigned)slices), dim3(256), 0, stream,
+                     dy, y, part, M, N, rows_per);
+  hipLaunchKernelGGL(f32g::colsum_f32_final, dim3((unsigned)((N + 255) / 256)), dim3(256), 0, stream, part, db, N,
+                     slices, accumulate ? 1 : 0);
+  return hipGetLastError();
+}
+
+}  // namespace dgt

@@ -528,6 +528,9 @@ class Engine:
             # the optimizer state (DeepSpeed's bf16 optimizer keeps its fp32 groups there too) --
             # without them a resumed run restarts from rounded weights and drifts off the original
             st["single_partition_of_fp32_groups"] = [self.master.detach().cpu().clone()]
+            # where each named parameter sits in that flat master (zero_to_fp32 unflattens it)
+            st["fp32_param_names"] = list(self.param_names)
+            st["fp32_param_segments"] = [(int(o), tuple(int(d) for d in s)) for o, s in self.layout.segments()]
         return st
 
     def _zero_shard_state(self) -> Dict[str, Any]:

@@ -11,9 +11,14 @@ launch forward (bias and ReLU folded in) and one launch backward (ReLU mask, dx,
 ``nn.ReLU`` that directly follows it in an ``nn.Sequential`` — keeping the same Parameter objects
 and state_dict keys, so checkpoints, the engine's flat buffers and optimizers are unaffected.
 
-Taken only for fp32 GPU tensors of small shapes (``SMALL``); anything else runs ``F.linear`` and is
-counted (``FALLBACKS``).  bf16 models get the MFMA GEMM chain of ``ops/mfma_linear.py`` instead:
-``inject_fused_linear`` dispatches on the parameters' dtype.
+Every fp32 GPU shape runs a hand-written kernel: small shapes (``SMALL_M`` / ``SMALL_WORK``) the
+one-launch dot-product kernels of ``csrc/linear.hip``; larger ones the exact-fp32 MFMA GEMM of
+``csrc/gemm_f32.hip`` (v_mfma_f32_32x32x2_f32, LDS-tiled, split-K for small grids) -- forward with
+bias / ReLU in the epilogue, dgrad and wgrad reading dy, W and x in their stored layouts with the
+ReLU mask applied while staging, and a deterministic column sum for the bias gradient.  Only
+non-fp32 / non-contiguous / CPU inputs run ``F.linear``, and those are counted (``FALLBACKS``).  bf16
+models get the MFMA GEMM chain of ``ops/mfma_linear.py`` instead: ``inject_fused_linear``
+dispatches on the parameters' dtype.
 """
 from __future__ import annotations
 
@@ -92,14 +97,41 @@ def count_fallback(reason: str) -> None:
         print(f"[dgt] WARNING: Linear falls back to F.linear (vendor BLAS): {reason}", file=sys.stderr, flush=True)
 
 SMALL_M = 256            # rows per call (batch)
-SMALL_WORK = 1 << 22     # M * N * K: beyond this a tiled GEMM (hipBLASLt / csrc/gemm.hip) wins
+SMALL_WORK = 1 << 22     # M * N * K: beyond this the tiled MFMA GEMM (csrc/gemm_f32.hip) wins
+
+
+def _small(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    return x.shape[0] <= SMALL_M and x.shape[0] * weight.shape[0] * weight.shape[1] <= SMALL_WORK
+
+
+def _fwd(ops, x, weight, bias, relu: bool) -> torch.Tensor:
+    """y = act(x W^T + b): the small-batch kernel or the tiled fp32 MFMA GEMM (bias/ReLU epilogue)."""
+    y = torch.empty(x.shape[0], weight.shape[0], dtype=torch.float32, device=x.device)
+    if _small(x, weight):
+        ops.linear_fwd(x, weight, bias, y, relu)
+    else:
+        ops.gemm_f32(x, weight, None, bias, y, 0, 0, relu, False)
+    return y
+
+
+def _bwd(ops, dy, x, weight, y, dx, dW, db, accumulate: bool = False) -> None:
+    """g = dy * 1[y > 0] (y given: the layer had a ReLU) or dy; dx = g W, dW (+)= g^T x, db (+)= sum_m g.
+    Tiled: dgrad A = g [M, N] (k = N contiguous), B = W [N, K] read as [k][n]; wgrad A = g read as
+    [k = M][n], B = x [M, K] read as [k][col]; the mask is applied while g is staged."""
+    if _small(x, weight):
+        ops.linear_bwd(dy, x, weight, y, dx, dW, db, accumulate)
+        return
+    if dx is not None:
+        ops.gemm_f32(dy, weight, y, None, dx, 0, 1, False, False)
+    ops.gemm_f32(dy, x, y, None, dW, 1, 1, False, accumulate)
+    if db is not None:
+        ops.colsum_f32(dy, y, db, accumulate)
 
 
 class _FusedLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, relu: bool, grad_in_place: bool = False):
-        y = torch.empty(x.shape[0], weight.shape[0], dtype=torch.float32, device=x.device)
-        _ext.require().linear_fwd(x, weight, bias, y, relu)
+        y = _fwd(_ext.require(), x, weight, bias, relu)
         ctx.relu = relu
         ctx.has_bias = bias is not None
         # leaf parameters only (no reference cycle through ctx)
@@ -120,12 +152,11 @@ class _FusedLinearFn(torch.autograd.Function):
             # separate AccumulateGrad add kernel per parameter.  Autograd still runs the leaves'
             # AccumulateGrad nodes with an undefined gradient, which fire the post-accumulate hooks
             # (the engine's bucket reducer) after this kernel is queued
-            _ext.require().linear_bwd(dy, x, weight, y, dx, w_leaf.grad,
-                                      None if b_leaf is None else b_leaf.grad, True)
+            _bwd(_ext.require(), dy, x, weight, y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad, True)
             return dx, None, None, None, None
         dw = torch.empty_like(weight)
         db = torch.empty(weight.shape[0], dtype=torch.float32, device=x.device) if ctx.has_bias else None
-        _ext.require().linear_bwd(dy, x, weight, y, dx, dw, db)
+        _bwd(_ext.require(), dy, x, weight, y, dx, dw, db)
         return dx, dw, db, None, None
 
 
@@ -135,9 +166,9 @@ def _grad_view_ok(p, dtype=torch.float32) -> bool:
             and g.shape == p.shape and not torch.is_grad_enabled())
 
 
-def _fusable(x: torch.Tensor, weight: torch.Tensor) -> bool:
+def _fusable(x: torch.Tensor, weight: torch.Tensor, bias=None) -> bool:
     return (x.is_cuda and x.dim() == 2 and x.dtype == torch.float32 and weight.dtype == torch.float32
-            and x.shape[0] <= SMALL_M and x.shape[0] * weight.shape[0] * weight.shape[1] <= SMALL_WORK
+            and weight.is_contiguous() and (bias is None or (bias.dtype == torch.float32 and bias.is_contiguous()))
             and _ext.require() is not None)  # a GPU shape we own: a missing extension is an error
 
 
@@ -146,11 +177,11 @@ def fused_linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = 
     """``grad_in_place``: inside the engine's backward (``engine_backward``), backward adds dW / db
     into the existing ``.grad`` tensors of leaf parameters instead of returning them to autograd
     (their post-accumulate hooks still fire); any other backward gets them returned as usual."""
-    if _fusable(x, weight):
+    if _fusable(x, weight, bias):
         return _FusedLinearFn.apply(x.contiguous(), weight, bias, relu, grad_in_place)
     if x.is_cuda:
-        count_fallback(f"fp32 Linear({weight.shape[1]}, {weight.shape[0]}) on {tuple(x.shape)} {x.dtype} input is "
-                       "beyond the small-batch kernels")
+        count_fallback(f"Linear({weight.shape[1]}, {weight.shape[0]}) with {weight.dtype} weights on "
+                       f"{tuple(x.shape)} {x.dtype} input (fp32, contiguous parameters only)")
     y = F.linear(x, weight, bias)
     return F.relu(y) if relu else y
 
@@ -197,9 +228,7 @@ class _FusedChainFn(torch.autograd.Function):
         acts = [x]
         h = x
         for i, relu in enumerate(relus):
-            w = wb[2 * i]
-            y = torch.empty(h.shape[0], w.shape[0], dtype=torch.float32, device=h.device)
-            ops.linear_fwd(h, w, wb[2 * i + 1], y, relu)
+            y = _fwd(ops, h, wb[2 * i], wb[2 * i + 1], relu)
             acts.append(y)
             h = y
         ctx.relus = relus
@@ -229,11 +258,11 @@ class _FusedChainFn(torch.autograd.Function):
             in_place = (active and w_need and _grad_view_ok(w_leaf)
                         and (not ctx.has_bias[i] or (b_need and _grad_view_ok(b_leaf))))
             if in_place:
-                ops.linear_bwd(dy, acts[i], ws[i], y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad, True)
+                _bwd(ops, dy, acts[i], ws[i], y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad, True)
             else:
                 dw = torch.empty_like(ws[i])
                 db = torch.empty(ws[i].shape[0], dtype=torch.float32, device=dy.device) if ctx.has_bias[i] else None
-                ops.linear_bwd(dy, acts[i], ws[i], y, dx, dw, db)
+                _bwd(ops, dy, acts[i], ws[i], y, dx, dw, db)
                 grads[2 * i] = dw if w_need else None
                 grads[2 * i + 1] = db if b_need else None
             dy = dx
@@ -254,7 +283,7 @@ class FusedChain(nn.Sequential):
         if layers is None:
             layers = self._chain() or []
             self.__dict__["_dgt_layers"] = layers
-        if len(layers) > 1 and x.dim() == 2 and all(_fusable(x, m.weight) for m in layers):
+        if len(layers) > 1 and x.dim() == 2 and all(_fusable(x, m.weight, m.bias) for m in layers):
             wb = []
             for m in layers:
                 wb.append(m.weight)

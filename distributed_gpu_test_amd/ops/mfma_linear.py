@@ -68,6 +68,17 @@ def chain_layout(linears: Sequence[nn.Linear], relus: Sequence[bool]) -> Optiona
     return head
 
 
+_ZERO_BIAS: dict = {}
+
+
+def _zero_bias(n: int, device) -> torch.Tensor:
+    key = (n, str(device))
+    z = _ZERO_BIAS.get(key)
+    if z is None:
+        z = _ZERO_BIAS[key] = torch.zeros(n, dtype=BF16, device=device)
+    return z
+
+
 def _runtime_reason(x: torch.Tensor, params: Sequence[Optional[torch.Tensor]]) -> Optional[str]:
     if not x.is_cuda or x.dtype != BF16 or x.dim() != 2:
         return f"input {tuple(x.shape)} {x.dtype} on {x.device.type} is not a 2-D bf16 GPU tensor"
@@ -97,7 +108,9 @@ class _MfmaChainFn(torch.autograd.Function):
             yT = None
             if i + 1 < L and need[4 + 2 * (i + 1)]:
                 yT = xTs[i + 1] = torch.empty(w.shape[0], M, dtype=BF16, device=dev)
-            gemm_nt(h, w, C=y, CT=yT, bias=b, relu=relus[i])  # a bf16 bias is read as it is
+            # a bf16 bias is read as it is; a bias-less Linear reads a zero bias (the GEMM's epilogue
+            # set has every ReLU / C^T form only with the bias add: x + 0 is x)
+            gemm_nt(h, w, C=y, CT=yT, bias=b if b is not None else _zero_bias(w.shape[0], dev), relu=relus[i])
             xs.append(y)
             h = y
         out = h
@@ -143,10 +156,13 @@ class _MfmaChainFn(torch.autograd.Function):
             hb = torch.empty(M // 64, kh, dtype=torch.float32, device=dev) if L > 0 and wants_bias(L - 1) else None
             direct = (need[4 + jw] and pw is not None and _grad_view_ok(pw, BF16)
                       and (not ctx.has_bias[L] or (need[4 + jb] and pb is not None and _grad_view_ok(pb, BF16))))
+            firsts = {}  # _first_write decisions already taken (each view is asked once per backward)
             if direct:
-                store_w = _first_write(pw.grad)
+                store_w = firsts[jw] = _first_write(pw.grad)
                 store_b = _first_write(pb.grad) if pb is not None else store_w
-                direct = store_w == store_b  # (else: the add path below, right for zeroed views too)
+                if pb is not None:
+                    firsts[jb] = store_b
+                direct = store_w == store_b  # (else: the per-tensor store / add path below)
             if direct:
                 # straight into the bucket's bf16 views, stored on their first write of this backward
                 db = pb.grad if pb is not None else torch.zeros(wh.shape[0], dtype=BF16, device=dev)
@@ -168,7 +184,13 @@ class _MfmaChainFn(torch.autograd.Function):
                         continue
                     p = leaf(j)
                     if p is not None and _grad_view_ok(p, BF16):
-                        p.grad.add_(val)  # tiny: [N <= 4, K] and [N]
+                        # tiny: [N <= 4, K] and [N].  A first write of this backward STORES: the
+                        # view may be a deferred (stale) buffer the engine has not zeroed
+                        first = firsts[j] if j in firsts else _first_write(p.grad)
+                        if first:
+                            p.grad.copy_(val)
+                        else:
+                            p.grad.add_(val)
                     else:
                         grads[j] = val.to(BF16)
             bpart = hb

@@ -32,6 +32,7 @@ class EngineMLPTrainer:
         world = comm.get_world_size()
         self.exchange = "none" if world == 1 else f"{comm.backend_name()}-bucketed"
         self.impl = f"dgt-engine+mfma{self.engine.fused_linear_layers}+zero{self.engine.stage}"
+        self.dtype_name = {torch.float32: "fp32", torch.bfloat16: "bf16", torch.float16: "fp16"}[self.engine.dtype]
         self.zero_stage = self.engine.stage
         self.global_steps = 0
 

@@ -447,6 +447,10 @@ class MLPTrainer:
             nxt = (cur + 1) % 3
             if not self._partials:
                 rowsum_bf16(self.gT[cur], self.gb[i])
+            if side and i + 2 < self.L:
+                # the buffers rotate mod 3: this dgrad writes gT[nxt], which layer i + 2's side-stream
+                # wgrad + Adam may still be reading (WAR); wait for that update first
+                main.wait_event(self.ev_opt[i + 2])
             if i > 0:
                 gemm_nt(self.g[cur], self.W[i], C=self.g[nxt] if i > 1 else None, CT=self.gT[nxt], mask=self.a[i],
                         b_kn=True, variant=self._v_dgrad, colsum=self.bpart[i - 1])

@@ -29,7 +29,22 @@ def consolidate(ckpt_dir, tag=None):
     model = torch.load(os.path.join(path, "mp_rank_00_model_states.pt"), map_location="cpu", weights_only=True)
     files = glob.glob(os.path.join(path, "zero_pp_rank_*_mp_rank_00_optim_states.pt"))
     if not files:
-        return {k: v.float() for k, v in model["module"].items()}
+        out = {}
+        opt = model.get("optimizer") or {}
+        fp32 = opt.get("single_partition_of_fp32_groups")
+        if fp32 and "fp32_param_names" in opt:
+            # stage 0 of a bf16 / fp16 run: the exact fp32 masters, not the module's rounded copy
+            flat = fp32[0].float()
+            for name, (off, shape) in zip(opt["fp32_param_names"], opt["fp32_param_segments"]):
+                if name is None:
+                    continue
+                numel = 1
+                for d in shape:
+                    numel *= d
+                out[name] = flat[off:off + numel].view(tuple(shape)).clone()
+        for k, v in model["module"].items():
+            out.setdefault(k, v.float())
+        return out
     shards = {}
     for f in files:
         r = int(re.search(r"zero_pp_rank_(\d+)_", os.path.basename(f)).group(1))
@@ -42,8 +57,9 @@ def consolidate(ckpt_dir, tag=None):
     if "index" in meta:  # element-wise ownership: every element exactly once over the ranks
         seen = torch.zeros(meta["total"], dtype=torch.int64)
         for r in range(ws):
-            full[shards[r]["index"]] = shards[r]["fp32_flat"].float()
-            seen[shards[r]["index"]] += 1
+            idx = shards[r]["index"].long()
+            full[idx] = shards[r]["fp32_flat"].float()
+            seen.index_add_(0, idx, torch.ones_like(idx))  # counts repeated indices too
         if not bool((seen == 1).all()):
             raise RuntimeError("index shards do not cover every element exactly once")
     else:

@@ -1,0 +1,174 @@
+"""Exact-fp32 MFMA GEMM (csrc/gemm_f32.hip) against fp32/fp64 PyTorch references of the same ops.
+
+Every layout pair the Linear layers use (forward MK.NK, dgrad MK.KN, wgrad KM.KN; plus KM.NK),
+aligned and ragged shapes (the 16-byte staging path and the scalar one), the 128x128 and 64x64 tiles,
+split-K, and the epilogues (bias, ReLU, accumulate, ReLU mask on A).  Then the engine-facing ops:
+FusedLinear / FusedChain at shapes beyond the small-batch kernels, with autograd gradients compared
+to nn.Linear in fp32."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _ops():
+    from distributed_gpu_test_amd.ops import _ext
+    return _ext.require()
+
+
+def _operands(M, N, K, la, lb, seed=0):
+    g = torch.Generator(device="cuda").manual_seed(seed)
+    a = torch.randn(M, K, device="cuda", generator=g)   # logical A[m][k]
+    b = torch.randn(N, K, device="cuda", generator=g)   # logical B[n][k]
+    A = a if la == 0 else a.t().contiguous()
+    B = b if lb == 0 else b.t().contiguous()
+    return a, b, A, B
+
+
+def _ref(a, b, bias=None, relu=False, mask=None):
+    a64 = a.double() if mask is None else (a * (mask > 0)).double()
+    out = a64 @ b.double().t()
+    if bias is not None:
+        out = out + bias.double()
+    if relu:
+        out = out.clamp_min(0)
+    return out
+
+
+def _close(got, ref, a, b):
+    # fp32 fma chain vs fp64: error bounded by ~K * 2^-24 * sum|a b|; rtol 1e-5 on that scale
+    scale = (a.abs().double() @ b.abs().double().t()).clamp_min(1.0)
+    err = ((got.double() - ref).abs() / scale).max().item()
+    assert err <= 1e-5, err
+
+
+SHAPES = [
+    (256, 256, 256),      # aligned, 64x64 tiles
+    (1024, 1024, 1024),   # aligned, 64x64 tiles (64 x 128^2 tiles < 256)
+    (2048, 2048, 512),    # aligned, 128x128 tiles
+    (1000, 999, 1004),    # ragged M / N, K % 4 == 0 (16-byte staging with zero fill)
+    (77, 130, 67),        # everything ragged, K odd (scalar staging)
+    (64, 64, 8192),       # tiny grid, long K: split-K
+    (3, 5, 7),            # degenerate
+]
+
+
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1), (1, 0)])
+@pytest.mark.parametrize("M,N,K", SHAPES)
+def test_gemm_f32_layouts(M, N, K, la, lb):
+    ops = _ops()
+    a, b, A, B = _operands(M, N, K, la, lb)
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm_f32(A, B, None, None, C, la, lb, False, False)
+    _close(C, _ref(a, b), a, b)
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (1000, 999, 1004), (64, 64, 8192), (77, 130, 67)])
+def test_gemm_f32_epilogues(M, N, K):
+    ops = _ops()
+    a, b, A, B = _operands(M, N, K, 0, 0, seed=1)
+    bias = torch.randn(N, device="cuda")
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm_f32(A, B, None, bias, C, 0, 0, True, False)
+    _close(C, _ref(a, b, bias, relu=True), a, b)
+    assert (C >= 0).all()
+    # accumulate into an existing C (gradient accumulation into .grad views)
+    C0 = torch.randn(M, N, device="cuda")
+    C = C0.clone()
+    ops.gemm_f32(A, B, None, None, C, 0, 0, False, True)
+    _close(C, C0.double() + _ref(a, b), a, b)
+    # ReLU mask on A (the backward's g = dy * 1[y > 0]), in both A layouts
+    mask = torch.randn(M, K, device="cuda")
+    for la in (0, 1):
+        Aa = a if la == 0 else a.t().contiguous()
+        Ma = mask if la == 0 else mask.t().contiguous()
+        C = torch.empty(M, N, device="cuda")
+        ops.gemm_f32(Aa, B, Ma, None, C, la, 0, False, False)
+        _close(C, _ref(a, b, mask=mask), a, b)
+
+
+def test_gemm_f32_asymmetric_identity():
+    """A = I with an asymmetric B catches a row/column swap of the epilogue (guide §3)."""
+    ops = _ops()
+    n = 192
+    A = torch.eye(n, device="cuda")
+    B = torch.arange(n * n, device="cuda", dtype=torch.float32).view(n, n) * 1e-3  # B[n][k]
+    C = torch.empty(n, n, device="cuda")
+    ops.gemm_f32(A, B, None, None, C, 0, 0, False, False)
+    assert torch.equal(C, B.t())
+
+
+@pytest.mark.parametrize("M,N", [(1024, 1024), (4096, 64), (1000, 999), (33, 7), (5000, 1)])
+def test_colsum_f32(M, N):
+    ops = _ops()
+    dy = torch.randn(M, N, device="cuda")
+    y = torch.randn(M, N, device="cuda")
+    db = torch.empty(N, device="cuda")
+    ops.colsum_f32(dy, None, db, False)
+    torch.testing.assert_close(db.double(), dy.double().sum(0), rtol=1e-5, atol=1e-4)
+    ops.colsum_f32(dy, y, db, True)
+    want = dy.double().sum(0) + (dy * (y > 0)).double().sum(0)
+    torch.testing.assert_close(db.double(), want, rtol=1e-5, atol=2e-4)
+
+
+@pytest.mark.parametrize("M,K,N,relu", [(1024, 1024, 1024, True), (512, 300, 700, False), (1000, 2048, 1, False)])
+def test_fused_linear_tiled_matches_nn_linear(M, K, N, relu):
+    """FusedLinear beyond the small-batch kernels: forward, dx, dW, db vs nn.Linear in fp32."""
+    from distributed_gpu_test_amd.ops import linear as L
+    torch.manual_seed(0)
+    lin = torch.nn.Linear(K, N).cuda()
+    fl = L.FusedLinear.from_linear(lin, relu=relu)
+    x = torch.randn(M, K, device="cuda", requires_grad=True)
+    x2 = x.detach().clone().requires_grad_(True)
+    before = dict(L.FALLBACKS)
+    y = fl(x)
+    ref = lin(x2)
+    ref = torch.relu(ref) if relu else ref
+    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+    gy = torch.randn_like(y)
+    gx, gw, gb = torch.autograd.grad(y, (x, lin.weight, lin.bias), gy)
+    rx, rw, rb = torch.autograd.grad(ref, (x2, lin.weight, lin.bias), gy)
+    torch.testing.assert_close(gx, rx, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(gw, rw, rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(gb, rb, rtol=1e-5, atol=1e-4)
+    assert dict(L.FALLBACKS) == before, L.FALLBACKS
+
+
+def test_engine_fp32_mlp_runs_no_vendor_gemm():
+    """The DeepSpeed-style engine on a fp32 SyntheticMLP(1024, 4) at batch 1024 with kernel
+    injection: every Linear runs a hand-written kernel (no F.linear fallback), and the first steps
+    match the same model trained by plain PyTorch fp32 + torch Adam."""
+    import copy
+    from distributed_gpu_test_amd import initialize
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP, synthetic_batch_data
+    torch.manual_seed(0)
+    model = SyntheticMLP(1024, 4)
+    ref = copy.deepcopy(model).cuda()
+    cfg = {"train_micro_batch_size_per_gpu": 1024, "gradient_accumulation_steps": 1,
+           "zero_optimization": {"stage": 0}, "optimizer": {"type": "Adam", "params": {"lr": 1e-4}},
+           "amd": {"fused_linear": True}}
+    from distributed_gpu_test_amd.ops.linear import FALLBACKS
+    before = dict(FALLBACKS)
+    engine, _, _, _ = initialize(model=model, config=cfg)
+    assert engine.fused_linear_layers == 5
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-4)
+    x, y = synthetic_batch_data(1024, 1024, 7)
+    x, y = x.cuda(), y.cuda()
+    crit = torch.nn.BCEWithLogitsLoss()
+    for step in range(3):
+        loss = crit(engine(x).view(-1), y)
+        engine.backward(loss)
+        rl = crit(ref(x).view(-1), y)
+        opt.zero_grad()
+        rl.backward()
+        torch.testing.assert_close(loss, rl, rtol=1e-4, atol=1e-5)
+        if step == 0:  # the gradients themselves (Adam's first step is ~lr * sign(g): compare before it)
+            for (name, p), q in zip(model.named_parameters(), ref.parameters()):
+                torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-6, msg=lambda m: f"{name}: {m}")
+        engine.step()
+        opt.step()
+    assert engine.linear_fallbacks == before, engine.linear_fallbacks
+    got = torch.nn.utils.parameters_to_vector(model.parameters())
+    want = torch.nn.utils.parameters_to_vector(ref.parameters())
+    torch.testing.assert_close(got, want, rtol=0, atol=5e-4)
+    engine.close()

@@ -502,3 +502,37 @@ def test_engine_bf16_matches_mlp_trainer():
         # paths' roundings -- a gradient that nearly cancels -- is a 2e-3 gap from step 1 on)
         assert float((d > 2e-3).float().mean()) < 2e-2 and float(d.mean()) < 3e-4, (float(d.mean()), i)
     eng.close()
+
+
+@pytest.mark.gpu
+def test_engine_bf16_mfma_chain_bias_free_linears():
+    """a bf16 chain whose Linears have no bias runs the MFMA chain (zero-bias epilogue)
+    and follows the autograd engine."""
+    import torch.nn as nn
+
+    def run(fused):
+        from distributed_gpu_test_amd import initialize
+        torch.manual_seed(5)
+        model = nn.Sequential(nn.Linear(256, 256, bias=False), nn.ReLU(), nn.Linear(256, 256, bias=False),
+                              nn.ReLU(), nn.Linear(256, 1))
+        cfg = {"train_micro_batch_size_per_gpu": 128, "bf16": {"enabled": True},
+               "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "amd": {"fused_linear": fused}}
+        eng, _, _, _ = initialize(model=model, config=cfg)
+        g = torch.Generator().manual_seed(0)
+        x = torch.randn(128, 256, generator=g).cuda()
+        y = (torch.randn(128, generator=g) > 0).float().cuda()
+        losses = []
+        for _ in range(3):
+            loss = torch.nn.functional.binary_cross_entropy_with_logits(eng(x).view(-1).float(), y)
+            eng.backward(loss)
+            eng.step()
+            losses.append(float(loss))
+        return eng, losses
+
+    a, la = run(True)
+    b, lb = run(False)
+    assert a.fused_linear_layers == 3
+    torch.testing.assert_close(torch.tensor(la), torch.tensor(lb), rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(a.master, b.master, rtol=0, atol=2e-3)
+    a.close()
+    b.close()
