@@ -546,7 +546,7 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
   TORCH_CHECK(variant >= 0 && variant <= 5,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
               "fragment reads), 4 (128x128, 4 stages, 8 waves) or 5 (software-pipelined reads); the round-2 "
-              "variants live in csrc/diag/gemm_variants_r2.h");
+              "variants live in git history (commit c0371a5)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");

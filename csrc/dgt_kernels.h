@@ -166,7 +166,7 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   float alpha;
   GemmAdam adam;       // kEpiAdam only (the gradient is alpha * A . B^T; ldc = row stride of the weight)
   float* colsum;       // kEpiColSum: fp32 [M / 128, N]
-  float* sk_slab;      // diag split-K kernel only (csrc/diag/gemm_variants_r2.h): fp32 partial tiles
+  float* sk_slab;      // diag split-K kernel only (removed; git history c0371a5): fp32 partial tiles
   int* sk_flags;       // diag split-K kernel only: 2 ints per tile (arrivals, slab ready)
 };
 

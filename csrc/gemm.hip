@@ -448,7 +448,7 @@ DGT_DEVICE void wait_vmcnt() {
 // NW = 4: waves 2 (M) x 2 (N), 64 x 64 each (4 x 4 accumulators).  NW = 8: waves 2 x 4, 64 x 32
 // each: two waves per SIMD, so one wave's LDS fragment reads overlap the other's MFMAs (the
 // 4-wave block leaves the matrix core idle while its only wave waits on LDS).
-// (Round-2 BK = 128 / two-K-tiles-per-barrier forms of this loop: csrc/diag/gemm_variants_r2.h.)
+// (Round-2 BK = 128 / two-K-tiles-per-barrier forms of this loop: git history, commit c0371a5.)
 // FR (front-loaded fragment reads): each wave issues ALL its ds_reads of a K-tile
 // (both 32-deep halves) before its first MFMA and lets counted lgkmcnt waits release the MFMAs as
 // fragments land.  After the per-K-tile barrier all waves otherwise move in lockstep through
@@ -959,7 +959,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 // 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase, 3 = variant 4 with front-loaded fragment
 // reads (FR), 4 = 128x128 4-stage with 8 waves (1 block / CU; the FR kernels' bitwise oracle),
 // 5 = software-pipelined fragment reads (SP, five stages; K % 128 == 0, else 3).  The round-2 variants measured slower or no
-// better inside the MLP step (3, 5-9) live in csrc/diag/gemm_variants_r2.h.
+// better inside the MLP step (3, 5-9) live in git history (commit c0371a5, csrc/diag/gemm_variants_r2.h).
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
   if (variant < 0 || variant > 5) return hipErrorInvalidValue;

@@ -82,14 +82,19 @@ class AMDConfig:
     hip_graph: bool = False
     # extra sync between comm and compute streams: validates overlap logic
     debug_sync_streams: bool = False
-    # kernel injection: nn.Linear (+ following nn.ReLU) -> one fused HIP launch forward and one
-    # backward for small fp32 batches (ops/linear.py).  None = auto: on for an fp32 GPU engine
-    # unless graph_module is asked for (torch's F.linear costs ~37 us of host dispatch per call on
-    # ROCm at these shapes: eager engine 2,450 -> 4,300 it/s, profiles/r2_engine_host_profile.txt)
+    # kernel injection: nn.Linear (+ following nn.ReLU) -> hand-written HIP kernels (ops/linear.py:
+    # fp32 small-batch fused launches or the fp32 MFMA GEMM; bf16 the MFMA chain).  None = auto: on
+    # for a GPU engine (torch's F.linear costs ~37 us of host dispatch per call on ROCm at the
+    # reference's shapes: eager engine 2,450 -> 4,300 it/s, profiles/r2_engine_host_profile.txt);
+    # with graph_module the graphs capture these kernels
     fused_linear: Optional[bool] = None
     # the module's forward and backward replayed from HIP graphs (one pair per input shape) under
     # the ordinary engine(x) / engine.backward(loss) / engine.step() calls (engine.py)
     graph_module: bool = False
+    # with graph_module: when the loss is the framework's fused BCE of the graphed output,
+    # engine.backward replays backward + gradient collective + clip + Adam as ONE graph and
+    # engine.step() only does the bookkeeping (so parameters are updated when backward returns)
+    graph_tail: bool = True
 
 
 @dataclass
@@ -218,7 +223,8 @@ def parse_config(config: Union[str, os.PathLike, Dict[str, Any], None], world_si
                     hip_graph=bool(a.get("hip_graph", False)),
                     debug_sync_streams=bool(a.get("debug_sync_streams", False)),
                     fused_linear=None if a.get("fused_linear") is None else bool(a["fused_linear"]),
-                    graph_module=bool(a.get("graph_module", False)))
+                    graph_module=bool(a.get("graph_module", False)),
+                    graph_tail=bool(a.get("graph_tail", True)))
     if amd.allreduce not in ("auto", "rccl", "oneshot"):
         raise ConfigError(f"amd.allreduce={amd.allreduce!r}: expected auto|rccl|oneshot")
 

@@ -83,8 +83,8 @@ class Engine:
         self.module = model.to(device=device, dtype=self.dtype)
         self.fused_linear_layers = 0
         fused_linear = config.amd.fused_linear
-        if fused_linear is None:  # auto: kernel injection unless the graphed module is asked for
-            fused_linear = not config.amd.graph_module
+        if fused_linear is None:  # auto: kernel injection (the graphed module captures the kernels too)
+            fused_linear = True
         if fused_linear and device.type == "cuda" and self.dtype in (torch.float32, torch.bfloat16):
             # fp32: the small-batch fused Linear kernels (csrc/linear.hip); bf16: the MFMA GEMM chain
             # (ops/mfma_linear.py: gemm.hip + head.hip, no vendor BLAS)
@@ -190,9 +190,14 @@ class Engine:
         self.graph_module = bool(config.amd.graph_module and device.type == "cuda")
         self.graph_module_reason = ""
         self._graphed_fwd: Dict[tuple, Any] = {}
-        if self.graph_module and self.fused_linear_layers:
-            self.graph_module = False
-            self.graph_module_reason = "fused_linear kernels accumulate gradients outside autograd"
+        # graphed tail (runtime/graph_module.py): backward + collective + Adam as one replay when
+        # the loss is the framework's own; the step counter Adam reads lives on the device
+        self._tail_rccl = None
+        self._tail_step_dev: Optional[torch.Tensor] = None
+        self._tail_step_host = -1   # what _tail_step_dev holds (host mirror, no sync)
+        self._tail_done = False     # backward ran the whole step: step() only does the bookkeeping
+        self.tail_steps = 0
+        self.tail_reason = ""       # why the graphed tail is not used (empty: in use or not asked)
 
     # ------------------------------------------------------------------ helpers
     def _names(self, params):
@@ -294,7 +299,7 @@ class Engine:
             return fn
         self.store.rebind_grads()
         try:
-            fn = GraphedModule(self.module, self.params, args)
+            fn = GraphedModule(self.module, self.params, args, tail=self._tail_callable())
         except Exception as e:  # data-dependent control flow, host syncs, ...: stay eager
             self.graph_module = False
             self.graph_module_reason = f"capture failed: {type(e).__name__}: {e}"
@@ -304,7 +309,98 @@ class Engine:
 
     __call__ = forward
 
+    # ------------------------------------------------------------------ graphed tail
+    def _tail_callable(self):
+        """The capturable optimizer tail for GraphedModule (None when the config needs host
+        decisions between backward and the update: see runtime/graph_step.supported)."""
+        if not self.config.amd.graph_tail:
+            self.tail_reason = "amd.graph_tail is off"
+            return None
+        from .runtime.graph_step import optimizer_tail, supported
+        ok, why = supported(self)
+        if not ok:
+            self.tail_reason = why
+            return None
+        if self._tail_step_dev is None:
+            self._tail_step_dev = torch.zeros((), dtype=torch.int64, device=self.device)
+            if comm.collectives_on(self.world_size):
+                from .parallel.rccl import RcclComm
+                self._tail_rccl = RcclComm(self.device)
+        lr = self.optimizer.param_groups[0]["lr"]
+
+        def tail():
+            optimizer_tail(self, self._tail_rccl, self._tail_step_dev)
+            self.store.grad_buf.zero_()  # consumed: the next step's backward starts from zero
+        tail.lr = lr
+        return tail
+
+    _VIEW_NODES = ("ViewBackward0", "ReshapeAliasBackward0", "UnsafeViewBackward0", "SqueezeBackward0",
+                   "SqueezeBackward1", "SqueezeBackward2", "UnsqueezeBackward0")
+
+    def _tail_runner(self, loss: torch.Tensor):
+        """(GraphedModule, dL/dout) when ``loss`` is the framework's fused BCE (``ops/loss.py``) of a
+        graphed forward's output, through reshapes / a dtype cast only -- a gradient the engine can
+        form without autograd: the BCE kernel already wrote it (d loss / d logits), and with no loss
+        scaling and one micro-step the backward seed is 1.  Else None (the autograd path)."""
+        node = loss.grad_fn
+        if node is None or type(node).__name__ != "_FusedBCEWithLogitsBackward":
+            return None
+        nxt = node.next_functions
+        if len(nxt) != 2 or nxt[1][0] is not None:
+            return None  # the targets need a gradient too
+        cur = nxt[0][0]
+        while cur is not None and type(cur).__name__ in self._VIEW_NODES + ("ToCopyBackward0",):
+            nn_ = cur.next_functions
+            if len(nn_) != 1:
+                return None
+            cur = nn_[0][0]
+        runner = getattr(cur, "runner", None)
+        if runner is None or getattr(runner, "bwd_tail", None) is None or not runner.pending:
+            return None
+        if len(runner.static_out) != 1 or runner.grad_out_idx != [0]:
+            return None
+        (dz,) = node.saved_tensors
+        gout = runner.static_gout[0]
+        if dz.numel() != gout.numel() or gout.device != dz.device:
+            return None
+        return runner, dz
+
+    def _try_graphed_tail(self, loss: torch.Tensor) -> bool:
+        if (not self.graph_module or not self.training or self.gas != 1 or self.loss_scaler is not None
+                or self._grads_dirty or self.faults.spec is not None or self.config.wall_clock_breakdown):
+            return False
+        found = self._tail_runner(loss)
+        if found is None:
+            return False
+        runner, dz = found
+        g = self.optimizer.param_groups[0]
+        if self.client_optimizer is not None and not isinstance(self.client_optimizer, FlatAdamOptimizer):
+            g["lr"] = float(self.client_optimizer.param_groups[0]["lr"])
+        if g["lr"] != runner.tail_lr:
+            self.tail_reason = "the lr changed since the tail was captured"
+            return False
+        self.store.rebind_grads()
+        if self._zero_deferred:  # the last eager step left its gradients in place (deferred zeroing)
+            self.store.grad_buf.zero_()
+            self._zero_deferred = False
+        want = self.global_steps - self.skipped_steps  # the graph adds 1 before its Adam launch
+        if self._tail_step_host != want:
+            self._tail_step_dev.fill_(want)
+        with torch.no_grad():
+            runner.static_gout[0].view(-1).copy_(dz.view(-1))
+        with tracing.range("dgt.graphed_tail"):
+            runner.bwd_tail.replay()
+        runner.pending = False
+        self._tail_step_host = want + 1
+        self._tail_done = True
+        self.tail_steps += 1
+        return True
+
     def backward(self, loss: torch.Tensor, retain_graph: bool = False) -> torch.Tensor:
+        if self._tail_done:
+            raise RuntimeError("engine.backward called twice without engine.step() after a graphed-tail step")
+        if self._try_graphed_tail(loss):
+            return loss
         loss = self.faults.maybe_corrupt_loss(loss, self.global_steps)
         boundary = self.is_gradient_accumulation_boundary()
         if self._zero_deferred and self.store.user_set_grads():
@@ -381,6 +477,10 @@ class Engine:
         self.micro_steps += 1
         for fn in self._graphed_fwd.values():  # a forward whose backward never came: its activations are dead
             fn.pending = False
+        if self._tail_done:  # the graphed tail already reduced, clipped, updated and zeroed
+            self._tail_done = False
+            self._finish_step(skipped=False, zero=False)
+            return
         if not self._boundary_pending:
             return
         self._boundary_pending = False

@@ -27,7 +27,7 @@ signature before that runs eagerly instead of overwriting the first one's activa
 """
 from __future__ import annotations
 
-from typing import List, Sequence, Tuple
+from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
 
@@ -42,7 +42,7 @@ def _as_tuple(out) -> Tuple[torch.Tensor, ...]:
 
 class GraphedModule:
     def __init__(self, module: torch.nn.Module, params: Sequence[torch.nn.Parameter], args: Sequence[torch.Tensor],
-                 warmup: int = 2):
+                 warmup: int = 2, tail: Optional[Callable[[], None]] = None):
         self.params: List[torch.nn.Parameter] = list(params)
         self.grad_views = [p.grad for p in self.params]
         if any(g is None or g.shape != p.shape for g, p in zip(self.grad_views, self.params)):
@@ -89,14 +89,34 @@ class GraphedModule:
         self.grad_out_idx = [i for i, o in enumerate(out) if o.requires_grad]
         self.static_gout = [torch.empty_like(out[i]) for i in self.grad_out_idx]
         self.bwd = torch.cuda.CUDAGraph()
+        # a tail (below) captures this backward a second time, so keep the autograd graph for it
+        with_tail = tail is not None and not self.in_rg
         with torch.cuda.graph(self.bwd, pool=self.pool):
             gs = torch.autograd.grad([out[i] for i in self.grad_out_idx], targets, grad_outputs=self.static_gout,
-                                     allow_unused=True)
+                                     allow_unused=True, retain_graph=with_tail)
             with torch.no_grad():
                 for gv, g in zip(self.grad_views, gs[:len(self.params)]):
                     if g is not None:
                         gv.add_(g)
         self.static_gin = gs[len(self.params):]
+        # The graphed tail: the same backward followed by ``tail()`` (the engine's gradient
+        # collective, clip coefficient, fused Adam, ZeRO-1 all-gather and the bucket's zero fill) in
+        # ONE graph, replayed by Engine.backward when the loss is one it can differentiate itself
+        # (the framework's fused BCE on this module's output): a training step is then the forward
+        # replay, the loss kernel and this replay, with no autograd engine call at all.
+        self.bwd_tail = None
+        self.tail_lr = getattr(tail, "lr", None)  # baked into the captured Adam launch
+        if with_tail:
+            self.bwd_tail = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(self.bwd_tail, pool=self.pool):
+                gs2 = torch.autograd.grad([out[i] for i in self.grad_out_idx], targets[:len(self.params)],
+                                          grad_outputs=self.static_gout, allow_unused=True)
+                with torch.no_grad():
+                    for gv, g in zip(self.grad_views, gs2):
+                        if g is not None:
+                            gv.add_(g)
+                    tail()
+            del gs2
         self.single = torch.is_tensor(out) or len(out) == 1
         self.replays = 0
         self.pending = False  # a replayed forward whose backward has not run yet

@@ -48,6 +48,68 @@ def supported(engine) -> Tuple[bool, str]:
     return True, ""
 
 
+def reduce_grads(e, rccl) -> torch.Tensor:
+    """What GradReducer does at the boundary, on the current (capture) stream: the optimizer then
+    reads ``reducer.reduced`` (the flat bucket, its wire-dtype copy, or the ZeRO shard)."""
+    red = e.reducer
+    src = red.grad_buf
+    if red.comm_buf is not None:
+        red.comm_buf.copy_(src)
+        src = red.comm_buf
+    for bi, b in enumerate(e.layout.buckets):
+        view = src[b.start:b.start + b.numel]
+        if e.stage >= 1:
+            n = b.numel // e.world_size
+            out = red.shard_grad[red.shard_offsets[bi]:red.shard_offsets[bi] + n]
+            if rccl is not None:
+                rccl.reduce_scatter(out, view)
+            else:
+                out.copy_(view)
+        elif rccl is not None:
+            rccl.all_reduce(view)
+    return red.reduced
+
+
+def clip_coef(e, rccl, grads: torch.Tensor, scale: float) -> Optional[torch.Tensor]:
+    """Device-side global-norm clip coefficient (never read on the host)."""
+    clip = e.config.gradient_clipping
+    if clip <= 0:
+        return None
+    sq = grads.float().pow(2).sum() * (scale * scale)
+    if e.stage >= 1 and rccl is not None:
+        rccl.all_reduce(sq.reshape(1))
+    return torch.clamp(clip / (sq.sqrt() + 1e-6), max=1.0).reshape(1).float()
+
+
+def allgather_params(e, rccl) -> None:
+    src = e.param_lp if e.param_lp is not None else e.master
+    off = 0
+    for b in e.layout.buckets:
+        n = b.numel // e.world_size
+        out = e.store.param_buf[b.start:b.start + b.numel]
+        if rccl is not None:
+            rccl.all_gather(out, src[off:off + n])
+        else:
+            out.copy_(src[off:off + n])
+        off += n
+
+
+def optimizer_tail(e, rccl, step_dev: torch.Tensor) -> None:
+    """Everything after the gradients are in the flat bucket, capturable: gradient collective ->
+    clip coefficient -> device step counter + 1 -> fused flat Adam -> [ZeRO-1] parameter all-gather.
+    The lr and Adam constants are baked into the captured launch."""
+    grads = reduce_grads(e, rccl)
+    scale = 1.0 / e.world_size
+    coef = clip_coef(e, rccl, grads, scale)
+    g = e.optimizer.param_groups[0]
+    step_dev.add_(1)
+    adam_flat_(e.master, grads, e.exp_avg, e.exp_avg_sq, 1, g["lr"], g["betas"][0], g["betas"][1], g["eps"],
+               g["weight_decay"], g["adamw"], grad_scale=scale, grad_scale_dev=coef, param_lp=e.param_lp,
+               step_dev=step_dev)
+    if e.stage >= 1:
+        allgather_params(e, rccl)
+
+
 class GraphedStep:
     def __init__(self, engine, loss_fn: Callable[..., torch.Tensor], warmup: int = 2, max_graphs: int = 4):
         ok, why = supported(engine)
@@ -74,50 +136,6 @@ class GraphedStep:
         engine.reducer.arm(False)  # the hooks stay silent: the step issues its own collectives
 
     # ------------------------------------------------------------------ the step body
-    def _reduce(self) -> torch.Tensor:
-        """What GradReducer does at the boundary, on the capture stream: the optimizer then reads
-        ``reducer.reduced`` (the flat bucket, its wire-dtype copy, or the ZeRO shard)."""
-        e = self.e
-        red = e.reducer
-        src = red.grad_buf
-        if red.comm_buf is not None:
-            red.comm_buf.copy_(src)
-            src = red.comm_buf
-        for bi, b in enumerate(e.layout.buckets):
-            view = src[b.start:b.start + b.numel]
-            if e.stage >= 1:
-                n = b.numel // e.world_size
-                out = red.shard_grad[red.shard_offsets[bi]:red.shard_offsets[bi] + n]
-                if self.rccl is not None:
-                    self.rccl.reduce_scatter(out, view)
-                else:
-                    out.copy_(view)
-            elif self.rccl is not None:
-                self.rccl.all_reduce(view)
-        return red.reduced
-
-    def _clip(self, grads: torch.Tensor, scale: float) -> Optional[torch.Tensor]:
-        clip = self.e.config.gradient_clipping
-        if clip <= 0:
-            return None
-        sq = grads.float().pow(2).sum() * (scale * scale)
-        if self.e.stage >= 1 and self.rccl is not None:
-            self.rccl.all_reduce(sq.reshape(1))
-        return torch.clamp(clip / (sq.sqrt() + 1e-6), max=1.0).reshape(1).float()
-
-    def _allgather(self) -> None:
-        e = self.e
-        src = e.param_lp if e.param_lp is not None else e.master
-        off = 0
-        for b in e.layout.buckets:
-            n = b.numel // e.world_size
-            out = e.store.param_buf[b.start:b.start + b.numel]
-            if self.rccl is not None:
-                self.rccl.all_gather(out, src[off:off + n])
-            else:
-                out.copy_(src[off:off + n])
-            off += n
-
     def _body(self, *args) -> torch.Tensor:
         e = self.e
         e.store.rebind_grads()  # .grad views into the flat bucket (host-side binding, no kernel)
@@ -126,16 +144,7 @@ class GraphedStep:
         from ..ops.linear import engine_backward
         with engine_backward(grads_zero=True):  # zeroed just above
             loss.float().backward(self._seed(loss))
-        grads = self._reduce()
-        scale = 1.0 / e.world_size
-        coef = self._clip(grads, scale)
-        g = e.optimizer.param_groups[0]
-        self.step_dev.add_(1)
-        adam_flat_(e.master, grads, e.exp_avg, e.exp_avg_sq, 1, g["lr"], g["betas"][0], g["betas"][1], g["eps"],
-                   g["weight_decay"], g["adamw"], grad_scale=scale, grad_scale_dev=coef, param_lp=e.param_lp,
-                   step_dev=self.step_dev)
-        if e.stage >= 1:
-            self._allgather()
+        optimizer_tail(e, self.rccl, self.step_dev)
         return loss.detach()
 
     def _seed(self, loss: torch.Tensor) -> Optional[torch.Tensor]:

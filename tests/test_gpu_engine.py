@@ -59,10 +59,10 @@ def test_engine_gpu_bf16():
     engine.close()
 
 
-def _run_engine(cfg, batches, seed=4, graph=False):
+def _run_engine(cfg, batches, seed=4, graph=False, crit=None):
     m = _mlp(seed)
     engine, _, _, _ = dgt.initialize(model=m, optimizer=torch.optim.Adam(m.parameters(), lr=1e-3), config=cfg)
-    crit = torch.nn.BCEWithLogitsLoss()
+    crit = crit or torch.nn.BCEWithLogitsLoss()
     losses = []
     if graph:
         step = engine.graph_step(lambda bx, by: crit(engine(bx).float(), by))
@@ -113,6 +113,54 @@ def test_engine_graph_module_matches_eager(extra):
     torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
     e1.close()
     e2.close()
+
+
+@pytest.mark.parametrize("extra", [{}, {"gradient_clipping": 0.5}, {"zero_optimization": {"stage": 1}},
+                                   {"bf16": {"enabled": True}}, {"gradient_accumulation_steps": 2,
+                                                                 "train_batch_size": 64}])
+def test_engine_graph_tail_matches_eager(extra):
+    """amd.graph_module with the framework's fused BCE: engine.backward replays backward + collective +
+    clip + Adam as one graph (engine.step() only counts), across two input shapes; the trajectory
+    matches the eager engine.  gas = 2 needs a host decision per micro-step: no tail, same results."""
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    batches = _batches(10, 5) + _batches(1, 6, bs=8) + _batches(10, 7) + _batches(3, 8, bs=8)
+    cfg = {"train_batch_size": 32, **extra}
+    e1, l1, p1 = _run_engine(dict(cfg), batches, crit=BCEWithLogitsLoss())
+    e2, l2, p2 = _run_engine(dict(cfg, amd={"graph_module": True}), batches, crit=BCEWithLogitsLoss())
+    assert e2.graph_module, e2.graph_module_reason
+    if "gradient_accumulation_steps" in extra:
+        assert e2.tail_steps == 0 and "gradient_accumulation" in e2.tail_reason
+    else:
+        assert e2.tail_steps == len(batches), (e2.tail_steps, e2.tail_reason)
+    assert e1.global_steps == e2.global_steps
+    tol = dict(rtol=2e-2, atol=2e-3) if "bf16" in extra else dict(rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), **tol)
+    torch.testing.assert_close(p2.float(), p1.float(), **tol)
+    # after the tail the gradient bucket is zero, as after an eager step
+    assert not e2.store.grad_buf.any()
+    e1.close()
+    e2.close()
+
+
+def test_engine_graph_tail_falls_back_for_other_losses_and_lr_changes():
+    """A loss the engine cannot differentiate itself (torch's BCE, a sum) takes the autograd path;
+    a changed lr disables the captured tail (its lr is baked in) -- results still match eager."""
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    m = _mlp(3)
+    opt = torch.optim.Adam(m.parameters(), lr=1e-3)
+    e, _, _, _ = dgt.initialize(model=m, optimizer=opt, config={"train_batch_size": 32, "amd": {"graph_module": True}})
+    fused, torch_bce = BCEWithLogitsLoss(), torch.nn.BCEWithLogitsLoss()
+    for i, (x, y) in enumerate(_batches(6, 9)):
+        loss = (fused if i % 2 == 0 else torch_bce)(e(x), y)
+        e.backward(loss)
+        e.step()
+    assert e.tail_steps == 3
+    opt.param_groups[0]["lr"] = 5e-4
+    x, y = _batches(1, 10)[0]
+    e.backward(fused(e(x), y))
+    e.step()
+    assert e.tail_steps == 3 and "lr" in e.tail_reason
+    e.close()
 
 
 def test_engine_graph_module_shape_cap_and_eval():
@@ -222,7 +270,7 @@ def test_fused_linear_grad_in_place_accumulates_and_fires_hooks():
 def test_engine_fused_linear_auto_default():
     """fused_linear unset = auto: an fp32 GPU engine injects the fused Linear kernels, a bf16 one
     and a graph_module one do not."""
-    cases = [({}, 2), ({"amd": {"graph_module": True}}, 0), ({"bf16": {"enabled": True}}, 0),
+    cases = [({}, 2), ({"amd": {"graph_module": True}}, 2), ({"bf16": {"enabled": True}}, 0),
              ({"amd": {"fused_linear": False}}, 0)]
     for extra, want in cases:
         m = _mlp(4)
