@@ -588,8 +588,18 @@ class DgtEngineBench(EngineBench):
         graphed = self.engine.graphed is not None
         self.exchange = ("none" if self.world == 1 else
                          ("rccl-native-in-hipgraph" if graphed else f"{comm.backend_name()}-bucketed"))
-        self.impl = ("dgt-engine" + ("+hipgraph" if graphed else "") + ("+fusedlinear" if self.engine.fused_linear_layers else "")
-                     + ("+graphmodule" if self.engine.graph_module else "") + f"+zero{self.engine.stage}")
+        self._impl = ("dgt-engine" + ("+hipgraph" if graphed else "") + ("+fusedlinear" if self.engine.fused_linear_layers else "")
+                      + ("+graphmodule" if self.engine.graph_module else ""))
+
+    @property
+    def impl(self) -> str:
+        """Named after the paths the steps actually took (the graphed tail is chosen per step)."""
+        tail = "+graphtail" if getattr(self.engine, "tail_steps", 0) else ""
+        return f"{self._impl}{tail}+zero{self.engine.stage}"
+
+    @impl.setter
+    def impl(self, value):
+        pass
 
     def run_plan(self, plan, counts):
         plan_d = plan.to(self.device).long()

@@ -84,7 +84,8 @@ def run_mlp(args, cfg, ds_config, world: int, local_rank: int) -> None:
     synthetic batches (weak scaling, as bench.py --model mlp), the DeepSpeed JSON's micro-batch,
     Adam hyper-parameters, ZeRO stage and communication dtype, epoch loss lines and per-epoch
     checkpoints in the reference's layout.  ``--impl auto`` runs MLPTrainer (hand-written MFMA
-    GEMMs, fused wgrad+Adam, per-layer RCCL buckets); ``--impl engine`` runs the same model through
+    GEMMs with fused bias / ReLU / mask / transposed-copy epilogues, one flat fused Adam over the
+    fp32 masters after backward, per-layer RCCL buckets); ``--impl engine`` runs the same model through
     ``initialize`` (the engine's bf16 MFMA Linear chain)."""
     from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
     from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
