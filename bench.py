@@ -573,7 +573,8 @@ class DgtEngineBench(EngineBench):
         def loss_fn(rows):
             # the batch gather and the device-side loss log (the reference's loss.item() sum,
             # train.py:115) are part of the step, so a HIP graph captures them with it
-            loss = crit(self.engine(self.x[rows]).float(), self.y[rows])
+            # the batch gather as index_select (one kernel; advanced indexing costs ~3x the host time)
+            loss = crit(self.engine(torch.index_select(self.x, 0, rows)).float(), torch.index_select(self.y, 0, rows))
             self.loss_acc.add_(loss.detach())
             return loss
 
@@ -603,8 +604,10 @@ class DgtEngineBench(EngineBench):
 
     def run_plan(self, plan, counts):
         plan_d = plan.to(self.device).long()
-        for s in range(plan.shape[0]):
-            self.step(plan_d[s, : int(counts[s])])
+        # the per-step row views, sliced before the loop (the DataLoader's batches of the reference)
+        batches = [plan_d[s, :c] for s, c in enumerate(counts.tolist())]
+        for rows in batches:
+            self.step(rows)
 
     @property
     def params(self):

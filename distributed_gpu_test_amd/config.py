@@ -95,6 +95,10 @@ class AMDConfig:
     # engine.backward replays backward + gradient collective + clip + Adam as ONE graph and
     # engine.step() only does the bookkeeping (so parameters are updated when backward returns)
     graph_tail: bool = True
+    # eager: engine.backward runs the backward of its own loss -> Linear-chain graph (fused BCE of an
+    # injected chain's output) by calling the two backward functions directly, without the autograd
+    # engine; any other graph goes through autograd (engine.py Engine._direct_backward)
+    direct_backward: bool = True
 
 
 @dataclass
@@ -224,7 +228,8 @@ def parse_config(config: Union[str, os.PathLike, Dict[str, Any], None], world_si
                     debug_sync_streams=bool(a.get("debug_sync_streams", False)),
                     fused_linear=None if a.get("fused_linear") is None else bool(a["fused_linear"]),
                     graph_module=bool(a.get("graph_module", False)),
-                    graph_tail=bool(a.get("graph_tail", True)))
+                    graph_tail=bool(a.get("graph_tail", True)),
+                    direct_backward=bool(a.get("direct_backward", True)))
     if amd.allreduce not in ("auto", "rccl", "oneshot"):
         raise ConfigError(f"amd.allreduce={amd.allreduce!r}: expected auto|rccl|oneshot")
 

@@ -197,6 +197,7 @@ class Engine:
         self._tail_step_host = -1   # what _tail_step_dev holds (host mirror, no sync)
         self._tail_done = False     # backward ran the whole step: step() only does the bookkeeping
         self.tail_steps = 0
+        self.direct_backwards = 0   # eager backwards run without the autograd engine (_direct_backward)
         self.tail_reason = ""       # why the graphed tail is not used (empty: in use or not asked)
 
     # ------------------------------------------------------------------ helpers
@@ -420,7 +421,8 @@ class Engine:
         self._deferred_active, self._hook_zeroed = deferred, 0
         try:
             with tracing.range("dgt.backward"), engine_backward(grads_zero=from_zero) as stored:
-                scaled.backward(self._backward_seed(scaled, loss), retain_graph=retain_graph)
+                if retain_graph or not self._direct_backward(scaled, loss):
+                    scaled.backward(self._backward_seed(scaled, loss), retain_graph=retain_graph)
         finally:
             self._deferred_active = False
         if from_zero:
@@ -442,6 +444,79 @@ class Engine:
                 torch.cuda.synchronize()
             self._timers["backward_ms"] = (time.perf_counter() - t0) * 1e3
         return loss
+
+    def _direct_backward(self, scaled: torch.Tensor, loss: torch.Tensor) -> bool:
+        """The backward of the engine's own two-node graph without the autograd engine.
+
+        When the loss is the framework's fused BCE (``ops/loss.py``) of the output of an injected
+        Linear chain (``ops/linear.py`` FusedChain / FusedLinear), through reshapes only, and the
+        chain's input needs no gradient, the whole graph is two Python backward functions: the BCE's
+        (d loss / d logits is already computed: one multiply by the seed) and the chain's (one fused
+        backward launch per layer, writing dW / db into the flat bucket).  Calling them directly and
+        then running the parameters' post-accumulate hooks (the bucket reducer) the way autograd's
+        AccumulateGrad nodes would saves autograd's graph walk and its hand-off to the device's
+        worker thread -- most of a host-bound eager step (profiles/r2_engine_host_profile.txt).
+        Anything else (another loss, an input that needs a gradient, tensor hooks on a parameter,
+        loss scaling or 1/gas nodes) returns False: the caller runs ``scaled.backward``."""
+        if (scaled is not loss or not self.config.amd.direct_backward or self._defer_capable
+                or self.device.type != "cuda" or loss.dim() != 0):
+            return False
+        node = loss.grad_fn
+        if node is None or type(node).__name__ != "_FusedBCEWithLogitsBackward":
+            return False
+        nxt = node.next_functions
+        if len(nxt) != 2 or nxt[1][0] is not None:
+            return False
+        views = []
+        cur = nxt[0][0]
+        while cur is not None and type(cur).__name__ in self._VIEW_NODES + ("ToCopyBackward0",):
+            if len(cur.next_functions) != 1:
+                return False
+            views.append(cur)
+            cur = cur.next_functions[0][0]
+        kind = type(cur).__name__ if cur is not None else ""
+        if kind not in ("_FusedChainFnBackward", "_FusedLinearFnBackward"):
+            return False
+        edges = cur.next_functions
+        if not edges or edges[0][0] is not None:
+            return False  # the chain's input wants a gradient too
+        accs = [e[0] for e in edges[1:]]
+        if any(a is None or type(a).__name__ != "AccumulateGrad" for a in accs):
+            return False
+        leaves = [a.variable for a in accs]
+        if any(p._backward_hooks for p in leaves):
+            return False  # a tensor hook sees the gradient before accumulation: autograd's job
+        seed = self._seed_one
+        if seed is None or seed.device != loss.device:
+            seed = self._seed_one = torch.ones((), dtype=torch.float32, device=loss.device)
+        g = node.apply(seed)
+        g = g[0] if isinstance(g, tuple) else g
+        for v in views:  # reshapes / casts back to the chain's output
+            g = v(g)
+            g = g[0] if isinstance(g, tuple) else g
+        res = cur.apply(g)
+        # backward outputs -> the tensor inputs the edges belong to (weights, then present biases)
+        if kind == "_FusedChainFnBackward":
+            grads = [gr for j, gr in enumerate(res[3:]) if j % 2 == 0 or cur.has_bias[j // 2]]
+        else:
+            grads = [res[1]] + ([res[2]] if cur.has_bias else [])
+        if len(grads) != len(leaves):
+            raise RuntimeError("dgt: direct backward: gradient / parameter count mismatch")
+        with torch.no_grad():
+            for p, gr in zip(leaves, grads):
+                if gr is None:
+                    continue  # written in place into p.grad by the kernels
+                if p.grad is None:
+                    p.grad = gr.detach()
+                else:
+                    p.grad.add_(gr)
+        for p in leaves:  # what AccumulateGrad does after accumulating: the post-accumulate hooks
+            hooks = p._post_accumulate_grad_hooks
+            if hooks:
+                for h in list(hooks.values()):
+                    h(p)
+        self.direct_backwards += 1
+        return True
 
     def _backward_seed(self, scaled: torch.Tensor, loss: torch.Tensor) -> Optional[torch.Tensor]:
         """A persistent fp32 scalar 1 as the backward seed, saving autograd's per-step ``ones_like``

@@ -584,3 +584,24 @@ def test_engine_bf16_mfma_chain_bias_free_linears():
     torch.testing.assert_close(a.master, b.master, rtol=0, atol=2e-3)
     a.close()
     b.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [{}, {"gradient_clipping": 0.5}, {"zero_optimization": {"stage": 1}}])
+def test_engine_direct_backward_matches_autograd(extra):
+    """Eager engine + fused BCE of an injected Linear chain: engine.backward calls the two backward
+    functions itself (no autograd engine) and fires the bucket hooks; bit-identical to autograd."""
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    batches = _batches(8, 11) + _batches(2, 12, bs=8)
+    cfg = {"train_batch_size": 32, **extra}
+    e1, l1, p1 = _run_engine(dict(cfg, amd={"direct_backward": False}), batches, crit=BCEWithLogitsLoss())
+    e2, l2, p2 = _run_engine(dict(cfg), batches, crit=BCEWithLogitsLoss())
+    assert e1.direct_backwards == 0 and e2.direct_backwards == len(batches)
+    assert l1 == l2
+    assert torch.equal(p1, p2)
+    # torch's own loss keeps the autograd path
+    e3, l3, p3 = _run_engine(dict(cfg), batches)
+    assert e3.direct_backwards == 0
+    torch.testing.assert_close(p3, p2, rtol=1e-5, atol=1e-6)
+    for e in (e1, e2, e3):
+        e.close()
