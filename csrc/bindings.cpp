@@ -543,9 +543,10 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
              const std::optional<at::Tensor>& colsum) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK(variant >= 0 && variant <= 5,
+  TORCH_CHECK(variant >= 0 && variant <= 7,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
-              "fragment reads), 4 (128x128, 4 stages, 8 waves) or 5 (software-pipelined reads); the round-2 "
+              "fragment reads), 4 (128x128, 4 stages, 8 waves), 5 (software-pipelined reads) or 6 / 7 (register "
+              "prefetch, 2 / 4 K-tiles); the round-2 "
               "variants live in git history (commit c0371a5)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),

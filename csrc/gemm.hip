@@ -719,6 +719,118 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
   }
 }
 
+// ------------------------------------------------------------------ 128 x 128, register prefetch (RP)
+// Variant 6 (NT operands): the K-tiles in flight live in VGPRs instead of LDS.  Each thread loads its
+// four 16-byte pieces of a K-tile (A rows tid/8 and tid/8 + 64, B likewise, chunk tid % 8) with
+// plain global loads D K-tiles ahead, and writes them into one of two LDS stages (ds_write_b128, the
+// same XOR-swizzled image the LDS-DMA produces) just before the tile is consumed: LDS holds 64 KiB,
+// the registers another D x 32 KiB per block, so D + 1 K-tiles are in flight against the 4-stage
+// kernel's two -- the per-CU operand stream of the one-wave M = 1024 grids is latency x bytes in
+// flight bound (profiles/r3_gemm_pmc.txt: MFMA ~40 % busy in ours and hipBLASLt's alike).  The
+// fragment reads and MFMA order are the FR kernel's (variant 3): results are bit-identical to it.
+// One barrier per K-tile: the write of tile kt + 1 goes into the stage tile kt - 1 was read from,
+// which every wave finished before the previous barrier.
+template <int EPI, int D>
+__global__ __launch_bounds__(512, 1) void gemm_nt_rp_kernel(GemmArgs g) {
+  constexpr int BK = GBK, NW = 8, WN = 32, WCOLS = GBN / WN, NJ = WN / 16;
+  static_assert(!(EPI & (kEpiBKN | kEpiColSum | kEpiAdam)), "RP: NT operands, staged or fp32 epilogues");
+  __shared__ __attribute__((aligned(16))) u16 lds[2][2][GBM * BK];  // [stage][A|B], 32 KiB per stage
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  int tm, tn;
+  tile_of_block(blockIdx.x, g.M / GBM, g.N / GBN, tm, tn);
+  const int m0 = tm * GBM, n0 = tn * GBN;
+  const int wr = w / WCOLS, wc = w % WCOLS;
+  const int prow = tid >> 3, pch = tid & 7;
+  const u16* ga[2];
+  const u16* gb[2];
+  int loff[2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int row = prow + 64 * i;
+    ga[i] = static_cast<const u16*>(g.A) + (long long)(m0 + row) * g.lda + pch * 8;
+    gb[i] = static_cast<const u16*>(g.B) + (long long)(n0 + row) * g.ldb + pch * 8;
+    loff[i] = row * BK + ((pch ^ (row & 7)) << 3);  // read_frag<BK>'s image
+  }
+  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
+  u32x4 rg[D][4];
+  auto gload = [&](int kt, u32x4 (&r)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      r[i] = *reinterpret_cast<const u32x4*>(ga[i] + (long long)kt * BK);
+      r[2 + i] = *reinterpret_cast<const u32x4*>(gb[i] + (long long)kt * BK);
+    }
+  };
+  auto lwrite = [&](int st, const u32x4 (&r)[4]) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      *reinterpret_cast<u32x4*>(&lds[st][0][loff[i]]) = r[i];
+      *reinterpret_cast<u32x4*>(&lds[st][1][loff[i]]) = r[2 + i];
+    }
+  };
+  f32x4 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto compute = [&](int buf) {  // the FR kernel's K-tile (gemm_nt_kernel, FR != 0, NT)
+    const u16* As = lds[buf][0];
+    const u16* Bs = lds[buf][1];
+    bf16x8 af[BK / 32][4], bfr[BK / 32][NJ];
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int chunk = kk * 4 + (l >> 4);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[kk][j] = read_frag<BK>(Bs, wc * WN + j * 16 + (l & 15), chunk);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = read_frag<BK>(As, wr * 64 + i * 16 + (l & 15), chunk);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);
+    __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ, 0);
+  };
+
+  // nk % D == 0 (the dispatcher's condition).  Every iteration issues exactly four loads and four
+  // LDS writes, past the end on clamped tile indices (re-reads of the last tile, never consumed):
+  // with a conditional load the compiler's vmcnt accounting takes the shorter path's count at the
+  // loop header and waits for every load in flight, leaving one K-tile of prefetch instead of D.
+  const int nk = g.K / BK;
+#pragma unroll
+  for (int d = 0; d < D; ++d) gload(min(d, nk - 1), rg[d]);
+  lwrite(0, rg[0]);
+  gload(min(D, nk - 1), rg[0]);
+  __syncthreads();
+  // iteration kt: tile kt + 1 (in rg[(kt + 1) % D]) -> LDS stage (kt + 1) & 1, its registers refilled
+  // with tile kt + 1 + D, then tile kt's MFMAs; unrolled by D so every register index is static
+  for (int kt0 = 0; kt0 < nk; kt0 += D) {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int kt = kt0 + d;
+      const int nx = (d + 1) % D;  // static after the unroll
+      lwrite((kt + 1) & 1, rg[nx]);
+      gload(min(kt + 1 + D, nk - 1), rg[nx]);
+      compute(kt & 1);
+      __syncthreads();
+    }
+  }
+
+  if constexpr (!(EPI & kEpiOutF32)) {
+    epilogue_staged<EPI, GBM, GBN, 64, WN, 64 * NW>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
+  } else {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        epi_store<EPI>(g, acc[i][j], m0 + wr * 64 + i * 16 + 4 * (l >> 4), n0 + wc * WN + j * 16 + (l & 15));
+  }
+}
+
 // ------------------------------------------------------------------ 256 x 256 tile, 8-phase pipeline
 // For large M x N (>= ~200 tiles): 512 threads = 8 waves in 2 (M) x 4 (N), each wave 128 x 64 =
 // 8 x 4 accumulators of 16x16 (128 VGPRs).  A K-tile (BK = 64) of A and of B is staged as four
@@ -960,12 +1072,30 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 // reads (FR), 4 = 128x128 4-stage with 8 waves (1 block / CU; the FR kernels' bitwise oracle),
 // 5 = software-pipelined fragment reads (SP, five stages; K % 128 == 0, else 3).  The round-2 variants measured slower or no
 // better inside the MLP step (3, 5-9) live in git history (commit c0371a5, csrc/diag/gemm_variants_r2.h).
+// the RP kernel for the forward-type epilogues (others: false, the dispatcher reports it)
+template <int E>
+bool launch_rp(int grid, const GemmArgs& g, hipStream_t stream, int depth) {
+  if constexpr ((E & ~(kEpiBias | kEpiRelu | kEpiStoreT | kEpiOutF32)) == 0) {
+    if (depth == 4) hipLaunchKernelGGL((gemm_nt_rp_kernel<E, 4>), dim3(grid), dim3(512), 0, stream, g);
+    else hipLaunchKernelGGL((gemm_nt_rp_kernel<E, 2>), dim3(grid), dim3(512), 0, stream, g);
+    return true;
+  } else {
+    return false;
+  }
+}
+
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 5) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 7) return hipErrorInvalidValue;
   // only the 128x128 kernels read a [K, N] B operand or form column sums
   const bool kn = (epi & (kEpiBKN | kEpiColSum)) != 0;
   if ((epi & kEpiColSum) && (!(epi & kEpiStoreT) || !g.colsum)) return hipErrorInvalidValue;
+  // variants 6 / 7: the register-prefetch 128x128 kernel (2 / 4 K-tiles in VGPRs) for NT products
+  // with forward-type epilogues and K a multiple of 2 / 4 K-tiles; any other product asked for it
+  // (a DGT_GEMM_VARIANT A/B run reaches the dgrads too) keeps the shape rule
+  const int rp_depth = variant == 7 ? 4 : 2;
+  if (variant >= 6 && (kn || (epi & kEpiAdam) || (g.K / GBK) % rp_depth)) variant = 0;
+  const bool rp = variant >= 6;
   // (the 256x256 kernel's DMAs carry a 32-bit per-lane byte offset of up to 255 rows: row strides
   // past 4M elements take the 128x128 kernels)
   const bool fits256 = g.M % 256 == 0 && g.N % 256 == 0 && g.K % 128 == 0 && g.lda <= (1 << 22) && g.ldb <= (1 << 22);
@@ -997,7 +1127,9 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
     break;
 #define DGT_EPI_CASE(E)                                                                           \
   case E:                                                                                         \
-    if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g);    \
+    if (rp) {                                                                                     \
+      if (!launch_rp<E>(grid, g, stream, rp_depth)) return hipErrorInvalidValue;                  \
+    } else if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g); \
     else if (sp) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 3>), dim3(grid), dim3(512), 0, stream, g); \
     else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \

@@ -52,7 +52,9 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     2 = 256x256 8-phase pipeline, 3 = variant 4 with front-loaded LDS fragment reads,
     4 = 128x128 tiles 4-stage with 8 waves (1 block per CU; variant 3's bitwise oracle),
     5 = software-pipelined fragment reads (the next K-tile's fragments read during this one's MFMAs,
-    five LDS stages; K % 128 == 0, else 3) -- the shape rule's choice for the ``b_kn`` dgrad.
+    five LDS stages; K % 128 == 0, else 3) -- the shape rule's choice for the ``b_kn`` dgrad,
+    6 / 7 = register prefetch (2 / 4 K-tiles of operands in flight in VGPRs, two LDS stages; NT
+    forward-type products, bit-identical to 3; other products keep the shape rule).
     ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
     the shape rule gives to the 128x128 kernels).
 

@@ -205,6 +205,42 @@ def test_gemm_variant3_is_bitwise_variant4(kn, fr):
 
 
 @gpu
+@pytest.mark.parametrize("rp", [6, 7])
+@pytest.mark.parametrize("epi", ["bias_relu_t", "bias", "f32"])
+def test_gemm_register_prefetch_is_bitwise_variant3(rp, epi):
+    """The register-prefetch kernels (6: 2 K-tiles in VGPRs, 7: 4) stage the same LDS image and run
+    variant 3's fragment reads and MFMAs: every epilogue output equals variant 3's bit for bit; a
+    [K, N] product asked for variant 6 keeps the shape rule."""
+    g = torch.Generator().manual_seed(rp)
+    M, N, K = 512, 384, 1024
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
+    bias = torch.randn(N, generator=g).cuda()
+    outs = []
+    for v in (3, rp):
+        if epi == "f32":
+            C = torch.empty(M, N, dtype=torch.float32).cuda()
+            gemm_nt(A, B, C=C, out_f32=True, variant=v)
+            outs.append((C, C))
+            continue
+        C = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+        CT = torch.empty(N, M, dtype=torch.bfloat16).cuda()
+        if epi == "bias_relu_t":
+            gemm_nt(A, B, C=C, CT=CT, bias=bias, relu=True, variant=v)
+        else:
+            gemm_nt(A, B, C=C, bias=bias, variant=v)
+            CT = C
+        outs.append((C, CT))
+    assert torch.equal(outs[0][0], outs[1][0]) and torch.equal(outs[0][1], outs[1][1])
+    Bkn = torch.randn(K, N, generator=g).to(torch.bfloat16).cuda()
+    C0 = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+    C1 = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+    gemm_nt(A, Bkn, C=C0, b_kn=True, variant=0)
+    gemm_nt(A, Bkn, C=C1, b_kn=True, variant=rp)
+    assert torch.equal(C0, C1)
+
+
+@gpu
 @pytest.mark.parametrize("N,mask", [(1, True), (3, False)])
 def test_skinny_head_matches_reference_and_is_reproducible(N, mask):
     """skinny_fwd/bwd_bf16 (the engine chain's Linear(K, N <= 4) head) against the fp32 reference;
