@@ -489,12 +489,13 @@ class Engine:
         seed = self._seed_one
         if seed is None or seed.device != loss.device:
             seed = self._seed_one = torch.ones((), dtype=torch.float32, device=loss.device)
-        g = node.apply(seed)
-        g = g[0] if isinstance(g, tuple) else g
-        for v in views:  # reshapes / casts back to the chain's output
-            g = v(g)
+        with torch.no_grad():  # autograd runs backward functions with grad mode off (no create_graph)
+            g = node.apply(seed)
             g = g[0] if isinstance(g, tuple) else g
-        res = cur.apply(g)
+            for v in views:  # reshapes / casts back to the chain's output
+                g = v(g)
+                g = g[0] if isinstance(g, tuple) else g
+            res = cur.apply(g)
         # backward outputs -> the tensor inputs the edges belong to (weights, then present biases)
         if kind == "_FusedChainFnBackward":
             grads = [gr for j, gr in enumerate(res[3:]) if j % 2 == 0 or cur.has_bias[j // 2]]

@@ -124,13 +124,24 @@ def test_fused_linear_tiled_matches_nn_linear(M, K, N, relu):
     y = fl(x)
     ref = lin(x2)
     ref = torch.relu(ref) if relu else ref
-    torch.testing.assert_close(y, ref, rtol=1e-5, atol=1e-5)
+    # against fp64 on the fp32 error scale (as _close): forward, then dx = g W, dW = g^T x, db
+    w64, b64 = lin.weight.detach().double(), lin.bias.detach().double()
+    x64 = x.detach().double()
+    z64 = x64 @ w64.t() + b64
+    y64 = z64.clamp_min(0) if relu else z64
+    _close(y, y64, x.detach(), lin.weight.detach())
+    torch.testing.assert_close(y, ref, rtol=1e-4, atol=5e-5)  # and hipBLASLt's fp32 within rounding
     gy = torch.randn_like(y)
     gx, gw, gb = torch.autograd.grad(y, (x, lin.weight, lin.bias), gy)
     rx, rw, rb = torch.autograd.grad(ref, (x2, lin.weight, lin.bias), gy)
-    torch.testing.assert_close(gx, rx, rtol=1e-5, atol=1e-4)
-    torch.testing.assert_close(gw, rw, rtol=1e-5, atol=1e-4)
-    torch.testing.assert_close(gb, rb, rtol=1e-5, atol=1e-4)
+    # the ReLU mask from the fp32 forward itself (a z within rounding of 0 may differ in fp64)
+    g64 = gy.double() * (y.detach() > 0) if relu else gy.double()
+    _close(gx, g64 @ w64, g64.float(), lin.weight.detach().t())
+    _close(gw, g64.t() @ x64, g64.float().t(), x.detach().t())
+    torch.testing.assert_close(gb.double(), g64.sum(0), rtol=1e-5, atol=1e-4)
+    torch.testing.assert_close(gx, rx, rtol=1e-4, atol=1e-4)
+    torch.testing.assert_close(gw, rw, rtol=1e-4, atol=1e-3)
+    torch.testing.assert_close(gb, rb, rtol=1e-4, atol=1e-3)
     assert dict(L.FALLBACKS) == before, L.FALLBACKS
 
 
@@ -170,5 +181,7 @@ def test_engine_fp32_mlp_runs_no_vendor_gemm():
     assert engine.linear_fallbacks == before, engine.linear_fallbacks
     got = torch.nn.utils.parameters_to_vector(model.parameters())
     want = torch.nn.utils.parameters_to_vector(ref.parameters())
-    torch.testing.assert_close(got, want, rtol=0, atol=5e-4)
+    # Adam's first steps move each weight by ~lr * sign(g): a near-zero gradient component whose sign
+    # differs between two fp32 summation orders moves apart by up to 2 lr per step
+    torch.testing.assert_close(got, want, rtol=0, atol=1e-3)
     engine.close()
