@@ -45,53 +45,56 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // ----------------------------------------------------------------------------- staging
 // One operand tile of ROWS rows x BK k.  MK form: ROWS*BK/4 16-byte chunks, chunk c of row r ->
 // LDS [r][c ^ ((r >> 1) & 7)].  KM form: chunk = 4 consecutive rows of one k -> LDS [k][rows].
-template <bool KMAJ, int ROWS, bool VEC>
+// load() only ISSUES the global loads (every load unconditional, out-of-range ones on a clamped
+// in-range address, their lanes remembered in `oob`); store() zero-fills those lanes, applies the
+// ReLU mask (MASKED) and writes LDS.  Nothing reads the loaded values until store(), so a tile's
+// loads stay in flight while earlier tiles are consumed, and every path through the loop issues the
+// same number of loads (the compiler's vmcnt accounting then keeps all prefetched tiles in flight).
+template <bool KMAJ, int ROWS, bool VEC, bool MASKED>
 struct Tile {
   static constexpr int CHUNKS = ROWS * BK / 4;
   static constexpr int PER = CHUNKS / 256;  // chunks per thread (256 threads)
   f32x4 v[PER];
+  f32x4 m[MASKED ? PER : 1];
+  unsigned oob;  // bit 4i+e: element e of chunk i is outside the operand
+
+  DGT_DEVICE static void chunk_pos(int c, int& r, int& k) {
+    if (!KMAJ) {
+      r = c / (BK / 4);
+      k = (c % (BK / 4)) * 4;
+    } else {
+      k = c / (ROWS / 4);
+      r = (c % (ROWS / 4)) * 4;
+    }
+  }
 
   // rows [r0, r0 + ROWS) of the operand, k-tile [k0, k0 + BK); extent nr rows, nk k; ld elements
   DGT_DEVICE void load(const float* __restrict__ p, const float* __restrict__ mask, long long ld, int r0, int k0,
                        int nr, int nk, int tid) {
+    oob = 0u;
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int c = tid + 256 * i;
-      int r, k;  // first element of the chunk
-      if (!KMAJ) {
-        r = c / (BK / 4);
-        k = (c % (BK / 4)) * 4;
-      } else {
-        k = c / (ROWS / 4);
-        r = (c % (ROWS / 4)) * 4;
-      }
+      int r, k;
+      chunk_pos(tid + 256 * i, r, k);
       const int gr = r0 + r, gk = k0 + k;
-      f32x4 x = {0.f, 0.f, 0.f, 0.f};
       if (VEC) {
-        // extents of the contiguous dim are multiples of 4 here, so a chunk is all in or all out
-        const bool ok = KMAJ ? (gk < nk && gr < nr) : (gr < nr && gk < nk);
-        if (ok) {
-          const long long off = KMAJ ? (long long)gk * ld + gr : (long long)gr * ld + gk;
-          x = *reinterpret_cast<const f32x4*>(p + off);
-          if (mask) {
-            const f32x4 mk = *reinterpret_cast<const f32x4*>(mask + off);
-#pragma unroll
-            for (int e = 0; e < 4; ++e) x[e] = mk[e] > 0.f ? x[e] : 0.f;
-          }
-        }
+        // the contiguous extent is a multiple of 4 here: a chunk is all in or all out
+        const bool ok = gr < nr && gk < nk;
+        const long long off = ok ? (KMAJ ? (long long)gk * ld + gr : (long long)gr * ld + gk) : 0;
+        v[i] = *reinterpret_cast<const f32x4*>(p + off);
+        if constexpr (MASKED) m[i] = *reinterpret_cast<const f32x4*>(mask + off);
+        oob |= ok ? 0u : (15u << (4 * i));
       } else {
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const int rr = KMAJ ? gr + e : gr, kk = KMAJ ? gk : gk + e;
-          if (rr < nr && kk < nk) {
-            const long long off = KMAJ ? (long long)kk * ld + rr : (long long)rr * ld + kk;
-            float val = p[off];
-            if (mask && !(mask[off] > 0.f)) val = 0.f;
-            x[e] = val;
-          }
+          const bool ok = rr < nr && kk < nk;
+          const long long off = ok ? (KMAJ ? (long long)kk * ld + rr : (long long)rr * ld + kk) : 0;
+          v[i][e] = p[off];
+          if constexpr (MASKED) m[i][e] = mask[off];
+          oob |= ok ? 0u : (1u << (4 * i + e));
         }
       }
-      v[i] = x;
     }
   }
 
@@ -106,7 +109,14 @@ struct Tile {
       } else {
         off = c * 4;  // [k][ROWS], chunks in memory order
       }
-      *reinterpret_cast<f32x4*>(lds + off) = v[i];
+      f32x4 x = v[i];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        bool keep = !((oob >> (4 * i + e)) & 1u);
+        if constexpr (MASKED) keep = keep && m[i][e] > 0.f;
+        x[e] = keep ? x[e] : 0.f;
+      }
+      *reinterpret_cast<f32x4*>(lds + off) = x;
     }
   }
 };
@@ -141,7 +151,7 @@ DGT_DEVICE void tile_of(int bid, int nbm, int nbn, int& tm, int& tn) {
 
 // grid.x = tiles, grid.y = split-K slices.  Split slices write raw partial sums to ws[z][M][N]
 // (epilogue in gemm_f32_splitk_reduce); an unsplit launch applies the epilogue itself.
-template <int LA, int LB, int BM, int BN, bool VEC>
+template <int LA, int LB, int BM, int BN, bool VEC, bool MASKED>
 __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args a) {
   constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
   constexpr int A_SZ = BM * BK, B_SZ = BN * BK;
@@ -165,22 +175,24 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args a) {
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  Tile<LA == 1, BM, VEC> ta;
-  Tile<LB == 1, BN, VEC> tb;
-  if (kt0 < kt1) {
-    ta.load(a.A, a.maskA, a.lda, m0, kt0 * BK, a.M, a.K, tid);
-    tb.load(a.B, nullptr, a.ldb, n0, kt0 * BK, a.N, a.K, tid);
-    ta.store(lds[0], tid);
-    tb.store(lds[0] + A_SZ, tid);
-  }
-  __syncthreads();
-  for (int kt = kt0; kt < kt1; ++kt) {
-    const int buf = (kt - kt0) & 1;
-    const bool more = kt + 1 < kt1;
-    if (more) {  // next K-tile in flight while this one is consumed
-      ta.load(a.A, a.maskA, a.lda, m0, (kt + 1) * BK, a.M, a.K, tid);
-      tb.load(a.B, nullptr, a.ldb, n0, (kt + 1) * BK, a.N, a.K, tid);
-    }
+  // P K-tiles of loads in flight in registers (the 64x64 tile's one-block-per-CU grids have no other
+  // wave to cover the global latency with), two LDS stages, one barrier per K-tile: iteration i
+  // writes tile i + 1 into the stage tile i - 1 was read from, refills its registers with tile
+  // i + 1 + P (clamped to the slice: re-reads of the last tile, never consumed), then consumes tile i.
+  constexpr int P = BM == 64 ? 3 : 2;
+  Tile<LA == 1, BM, VEC, MASKED> ta[P];
+  Tile<LB == 1, BN, VEC, false> tb[P];
+  const int nkt = kt1 - kt0;
+  auto load = [&](int p, int i) {
+    const int kt = kt0 + min(i, nkt - 1);
+    ta[p].load(a.A, a.maskA, a.lda, m0, kt * BK, a.M, a.K, tid);
+    tb[p].load(a.B, nullptr, a.ldb, n0, kt * BK, a.N, a.K, tid);
+  };
+  auto stage = [&](int p, int buf) {
+    ta[p].store(lds[buf], tid);
+    tb[p].store(lds[buf] + A_SZ, tid);
+  };
+  auto consume = [&](int buf) {
     const float* la = lds[buf];
     const float* lb = lds[buf] + A_SZ;
 #pragma unroll
@@ -198,11 +210,34 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args a) {
           for (int j = 0; j < TN; ++j)
             acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
     }
-    if (more) {
-      ta.store(lds[buf ^ 1], tid);
-      tb.store(lds[buf ^ 1] + A_SZ, tid);
+  };
+  // (the loop sits inside the nkt > 0 branch: a path into the loop header that skipped the prologue
+  // loads would make the compiler wait for every prefetched tile at the header)
+  if (nkt > 0) {
+    // the prologue's loads stay in tile order (sched_barrier): the loop header's wait counts assume
+    // the oldest tile in flight is the one staged next
+#pragma unroll
+    for (int p = 0; p < P; ++p) {
+      load(p, p);
+      __builtin_amdgcn_sched_barrier(0);
     }
+    stage(0, 0);
+    load(0, P);
+    __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
+    // whole groups of P iterations: the ones past the slice stage and load (clamped) but consume
+    // nothing -- a `break` would again give the header a path with fewer loads in flight
+    for (int i0 = 0; i0 < nkt; i0 += P) {
+#pragma unroll
+      for (int d = 0; d < P; ++d) {
+        const int i = i0 + d;
+        const int nx = (d + 1) % P;  // static after the unroll
+        stage(nx, (i + 1) & 1);
+        load(nx, i + 1 + P);
+        if (i < nkt) consume(i & 1);
+        __syncthreads();
+      }
+    }
   }
 
   // epilogue: 32x32 accumulator layout col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
@@ -284,14 +319,22 @@ __global__ __launch_bounds__(256) void colsum_f32_final(const float* __restrict_
   db[n] = accumulate ? db[n] + s : s;
 }
 
+template <int LA, int LB, int BM, int BN, bool MASKED>
+void launch_masked(const GemmF32Args& a, bool vec, const dim3& grid, hipStream_t stream) {
+  if (vec)
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true, MASKED>), grid, dim3(256), 0, stream, a);
+  else
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false, MASKED>), grid, dim3(256), 0, stream, a);
+}
+
 template <int LA, int LB, int BM, int BN>
 hipError_t launch(const GemmF32Args& a, bool vec, int splits, hipStream_t stream) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
-  if (vec)
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true>), grid, dim3(256), 0, stream, a);
+  if (a.maskA)
+    launch_masked<LA, LB, BM, BN, true>(a, vec, grid, stream);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false>), grid, dim3(256), 0, stream, a);
+    launch_masked<LA, LB, BM, BN, false>(a, vec, grid, stream);
   return hipGetLastError();
 }
 
