@@ -1094,7 +1094,8 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // with forward-type epilogues and K a multiple of 2 / 4 K-tiles; any other product asked for it
   // (a DGT_GEMM_VARIANT A/B run reaches the dgrads too) keeps the shape rule
   const int rp_depth = variant == 7 ? 4 : 2;
-  if (variant >= 6 && (kn || (epi & kEpiAdam) || (g.K / GBK) % rp_depth)) variant = 0;
+  if (variant >= 6 && (kn || (epi & ~(kEpiBias | kEpiRelu | kEpiStoreT | kEpiOutF32)) || (g.K / GBK) % rp_depth))
+    variant = 0;
   const bool rp = variant >= 6;
   // (the 256x256 kernel's DMAs carry a 32-bit per-lane byte offset of up to 255 rows: row strides
   // past 4M elements take the 128x128 kernels)
