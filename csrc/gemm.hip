@@ -730,10 +730,14 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 // fragment reads and MFMA order are the FR kernel's (variant 3): results are bit-identical to it.
 // One barrier per K-tile: the write of tile kt + 1 goes into the stage tile kt - 1 was read from,
 // which every wave finished before the previous barrier.
+// A [K, N] B operand (the dgrad's W, kEpiBKN) is loaded as it lies -- thread tid fetches chunk tid % 16
+// of k-rows tid / 16 and tid / 16 + 32 -- into stage_tile_kn's image, and read with the FR kernel's
+// transposed ds_read_b64_tr_b16 fragments.
 template <int EPI, int D>
 __global__ __launch_bounds__(512, 1) void gemm_nt_rp_kernel(GemmArgs g) {
   constexpr int BK = GBK, NW = 8, WN = 32, WCOLS = GBN / WN, NJ = WN / 16;
-  static_assert(!(EPI & (kEpiBKN | kEpiColSum | kEpiAdam)), "RP: NT operands, staged or fp32 epilogues");
+  constexpr bool KN = (EPI & kEpiBKN) != 0;
+  static_assert(!(EPI & kEpiAdam), "RP: no in-epilogue Adam");
   __shared__ __attribute__((aligned(16))) u16 lds[2][2][GBM * BK];  // [stage][A|B], 32 KiB per stage
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
   int tm, tn;
@@ -743,28 +747,36 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_rp_kernel(GemmArgs g) {
   const int prow = tid >> 3, pch = tid & 7;
   const u16* ga[2];
   const u16* gb[2];
-  int loff[2];
+  int loff[2], lboff[2];
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     const int row = prow + 64 * i;
     ga[i] = static_cast<const u16*>(g.A) + (long long)(m0 + row) * g.lda + pch * 8;
-    gb[i] = static_cast<const u16*>(g.B) + (long long)(n0 + row) * g.ldb + pch * 8;
     loff[i] = row * BK + ((pch ^ (row & 7)) << 3);  // read_frag<BK>'s image
+    if constexpr (KN) {
+      const int kr = (tid >> 4) + 32 * i, c = tid & 15;  // k-row, 16-byte chunk of the 128 n
+      gb[i] = static_cast<const u16*>(g.B) + (long long)kr * g.ldb + n0 + c * 8;
+      lboff[i] = kr * GBN + ((c ^ kn_swz(kr)) << 3);  // stage_tile_kn's image
+    } else {
+      gb[i] = static_cast<const u16*>(g.B) + (long long)(n0 + row) * g.ldb + pch * 8;
+      lboff[i] = loff[i];
+    }
   }
+  const long long bstep = KN ? (long long)BK * g.ldb : BK;  // elements per K-tile of B
   typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   u32x4 rg[D][4];
   auto gload = [&](int kt, u32x4 (&r)[4]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       r[i] = *reinterpret_cast<const u32x4*>(ga[i] + (long long)kt * BK);
-      r[2 + i] = *reinterpret_cast<const u32x4*>(gb[i] + (long long)kt * BK);
+      r[2 + i] = *reinterpret_cast<const u32x4*>(gb[i] + kt * bstep);
     }
   };
   auto lwrite = [&](int st, const u32x4 (&r)[4]) {
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       *reinterpret_cast<u32x4*>(&lds[st][0][loff[i]]) = r[i];
-      *reinterpret_cast<u32x4*>(&lds[st][1][loff[i]]) = r[2 + i];
+      *reinterpret_cast<u32x4*>(&lds[st][1][lboff[i]]) = r[2 + i];
     }
   };
   f32x4 acc[4][NJ];
@@ -772,7 +784,7 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_rp_kernel(GemmArgs g) {
   for (int i = 0; i < 4; ++i)
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  auto compute = [&](int buf) {  // the FR kernel's K-tile (gemm_nt_kernel, FR != 0, NT)
+  auto compute = [&](int buf) {  // the FR kernel's K-tile (gemm_nt_kernel, FR != 0)
     const u16* As = lds[buf][0];
     const u16* Bs = lds[buf][1];
     bf16x8 af[BK / 32][4], bfr[BK / 32][NJ];
@@ -780,7 +792,10 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_rp_kernel(GemmArgs g) {
     for (int kk = 0; kk < BK / 32; ++kk) {
       const int chunk = kk * 4 + (l >> 4);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[kk][j] = read_frag<BK>(Bs, wc * WN + j * 16 + (l & 15), chunk);
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (KN) bfr[kk][j] = read_frag_kn_fr(Bs, kk * 32, wc * WN + j * 16, l);
+        else bfr[kk][j] = read_frag<BK>(Bs, wc * WN + j * 16 + (l & 15), chunk);
+      }
 #pragma unroll
       for (int i = 0; i < 4; ++i) af[kk][i] = read_frag<BK>(As, wr * 64 + i * 16 + (l & 15), chunk);
     }
@@ -791,9 +806,16 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_rp_kernel(GemmArgs g) {
 #pragma unroll
         for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+    if constexpr (KN) {  // as the FR kernel: the second half's reads go out after the first MFMAs
+      __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * NJ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * NJ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ - 2, 0);
+    } else {
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);
-    __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ, 0);
+      for (int kk = 0; kk < BK / 32; ++kk) __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ, 0);
+    }
   };
 
   // nk % D == 0 (the dispatcher's condition).  Every iteration issues exactly four loads and four
@@ -1075,9 +1097,15 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 // the RP kernel for the forward-type epilogues (others: false, the dispatcher reports it)
 template <int E>
 bool launch_rp(int grid, const GemmArgs& g, hipStream_t stream, int depth) {
-  if constexpr ((E & ~(kEpiBias | kEpiRelu | kEpiStoreT | kEpiOutF32)) == 0) {
-    if (depth == 4) hipLaunchKernelGGL((gemm_nt_rp_kernel<E, 4>), dim3(grid), dim3(512), 0, stream, g);
-    else hipLaunchKernelGGL((gemm_nt_rp_kernel<E, 2>), dim3(grid), dim3(512), 0, stream, g);
+  if constexpr (!(E & kEpiAdam)) {
+    // depth 4 for the forward-type epilogues only (the others: 2)
+    if constexpr ((E & ~(kEpiBias | kEpiRelu | kEpiStoreT | kEpiOutF32)) == 0) {
+      if (depth == 4) {
+        hipLaunchKernelGGL((gemm_nt_rp_kernel<E, 4>), dim3(grid), dim3(512), 0, stream, g);
+        return true;
+      }
+    }
+    hipLaunchKernelGGL((gemm_nt_rp_kernel<E, 2>), dim3(grid), dim3(512), 0, stream, g);
     return true;
   } else {
     return false;
@@ -1093,9 +1121,9 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // variants 6 / 7: the register-prefetch 128x128 kernel (2 / 4 K-tiles in VGPRs) for NT products
   // with forward-type epilogues and K a multiple of 2 / 4 K-tiles; any other product asked for it
   // (a DGT_GEMM_VARIANT A/B run reaches the dgrads too) keeps the shape rule
-  const int rp_depth = variant == 7 ? 4 : 2;
-  if (variant >= 6 && (kn || (epi & ~(kEpiBias | kEpiRelu | kEpiStoreT | kEpiOutF32)) || (g.K / GBK) % rp_depth))
-    variant = 0;
+  const bool fwd_type = (epi & ~(kEpiBias | kEpiRelu | kEpiStoreT | kEpiOutF32)) == 0;
+  const int rp_depth = (variant == 7 && fwd_type) ? 4 : 2;
+  if (variant >= 6 && ((epi & kEpiAdam) || (g.K / GBK) % rp_depth)) variant = 0;
   const bool rp = variant >= 6;
   // (the 256x256 kernel's DMAs carry a 32-bit per-lane byte offset of up to 255 rows: row strides
   // past 4M elements take the 128x128 kernels)
@@ -1121,7 +1149,9 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   const bool fr = eight && !sp && (variant == 0 || variant == 3 || variant == 5);
 #define DGT_EPI_CASE_KN(E)                                                                        \
   case E:                                                                                         \
-    if (sp) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 3>), dim3(grid), dim3(512), 0, stream, g); \
+    if (rp) {                                                                                     \
+      if (!launch_rp<E>(grid, g, stream, rp_depth)) return hipErrorInvalidValue;                  \
+    } else if (sp) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 3>), dim3(grid), dim3(512), 0, stream, g); \
     else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \
     else hipLaunchKernelGGL((gemm_nt_kernel<E, 2>), dim3(grid), dim3(256), 0, stream, g);         \

@@ -209,8 +209,9 @@ def test_gemm_variant3_is_bitwise_variant4(kn, fr):
 @pytest.mark.parametrize("epi", ["bias_relu_t", "bias", "f32"])
 def test_gemm_register_prefetch_is_bitwise_variant3(rp, epi):
     """The register-prefetch kernels (6: 2 K-tiles in VGPRs, 7: 4) stage the same LDS image and run
-    variant 3's fragment reads and MFMAs: every epilogue output equals variant 3's bit for bit; a
-    [K, N] product asked for variant 6 keeps the shape rule."""
+    variant 3's fragment reads and MFMAs: every epilogue output equals variant 3's bit for bit, and
+    a [K, N] product (the dgrad, plain and with the mask + C^T + column-sum epilogue) equals the
+    shape rule's (variant 5, itself bitwise variant 4)."""
     g = torch.Generator().manual_seed(rp)
     M, N, K = 512, 384, 1024
     A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
@@ -238,6 +239,15 @@ def test_gemm_register_prefetch_is_bitwise_variant3(rp, epi):
     gemm_nt(A, Bkn, C=C0, b_kn=True, variant=0)
     gemm_nt(A, Bkn, C=C1, b_kn=True, variant=rp)
     assert torch.equal(C0, C1)
+    mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).cuda()
+    outs = []
+    for v in (5, rp):
+        C = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+        CT = torch.empty(N, M, dtype=torch.bfloat16).cuda()
+        cs = torch.empty(M // 128, N, dtype=torch.float32).cuda()
+        gemm_nt(A, Bkn, C=C, CT=CT, mask=mask, b_kn=True, variant=v, colsum=cs)
+        outs.append((C, CT, cs))
+    assert all(torch.equal(x, y) for x, y in zip(*outs))
 
 
 @gpu
