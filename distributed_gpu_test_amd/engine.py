@@ -31,6 +31,7 @@ import torch.distributed as dist
 
 from .config import DSConfig, parse_config
 from .ops.adam import adam_flat_
+from .ops.linear import engine_backward
 from .accelerator import get_accelerator
 from .parallel import comm
 from .parallel.reducer import GradReducer
@@ -415,7 +416,6 @@ class Engine:
         if self.loss_scaler is not None:
             scaled = scaled * self.loss_scaler.scale
         t0 = time.perf_counter() if self.config.wall_clock_breakdown else 0.0
-        from .ops.linear import engine_backward
         from_zero, deferred = not self._grads_dirty, self._zero_deferred
         self._zero_deferred = False
         self._deferred_active, self._hook_zeroed = deferred, 0

@@ -17,16 +17,29 @@ import torch
 _ENABLED = os.environ.get("DGT_ROCTX", "0") not in ("", "0")
 
 
-@contextlib.contextmanager
+class _Range:
+    __slots__ = ("name",)
+
+    def __init__(self, name: str):
+        self.name = name
+
+    def __enter__(self):
+        torch.cuda.nvtx.range_push(self.name)
+
+    def __exit__(self, *exc):
+        torch.cuda.nvtx.range_pop()
+        return False
+
+
+_NULL = contextlib.nullcontext()
+
+
 def range(name: str):  # noqa: A001 - mirrors nvtx.range
+    """A roctx range when tracing is on; otherwise one shared no-op context (the engine's host-bound
+    eager step enters several per step: no generator object per call)."""
     if _ENABLED and torch.cuda.is_available():
-        torch.cuda.nvtx.range_push(name)
-        try:
-            yield
-        finally:
-            torch.cuda.nvtx.range_pop()
-    else:
-        yield
+        return _Range(name)
+    return _NULL
 
 
 def enable(flag: bool = True) -> None:
