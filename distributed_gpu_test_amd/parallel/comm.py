@@ -30,6 +30,12 @@ def default_backend() -> str:
     return get_accelerator().communication_backend_name()
 
 
+def _oversubscribed(info: RankInfo) -> bool:
+    from ..accelerator import allow_oversubscribe
+    return (info.world_size > 1 and allow_oversubscribe() and get_accelerator().name == "hip"
+            and info.local_world_size > torch.cuda.device_count())
+
+
 def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
                      rank_info: Optional[RankInfo] = None, set_device: bool = True) -> RankInfo:
     """Create the default process group (idempotent) and bind this rank's GPU.
@@ -42,7 +48,16 @@ def init_distributed(backend: Optional[str] = None, timeout_s: float = 1800.0,
     """
     global _RANK_INFO
     info = rank_info or resolve_rank_info()
-    backend = backend or default_backend()
+    if backend is None:
+        backend = default_backend()
+        if backend == "nccl" and not os.environ.get("DGT_BACKEND") and _oversubscribed(info):
+            # RCCL refuses two ranks on one device ("invalid usage"): a rehearsal that shares cards on
+            # purpose (DGT_ALLOW_OVERSUBSCRIBE=1) runs its process group on gloo, host-staged
+            backend = "gloo"
+            if info.rank == 0:
+                import sys
+                print(f"[dgt] {info.local_world_size} ranks share {torch.cuda.device_count()} GPU(s): process "
+                      "group on gloo (RCCL needs one device per rank)", file=sys.stderr, flush=True)
     accel = get_accelerator()
     if backend == "nccl":
         if accel.name != "hip":

@@ -19,3 +19,7 @@ for v in 0 6 7; do
 done
 done
 echo done
+echo "== self-launched 4-rank rehearsal on one card (process group on gloo: RCCL needs one device per rank)"
+DGT_ALLOW_OVERSUBSCRIBE=1 timeout -k 10 400 python bench.py --gpus 4 --steps 20 --warmup 5 > gpurun_out/r4s/bench_self4.json 2> gpurun_out/r4s/bench_self4.err || { tail -30 gpurun_out/r4s/bench_self4.err; exit 1; }
+python -c "import json; d=json.load(open('gpurun_out/r4s/bench_self4.json')); print(d['value'], d['ranks'], d['config']['parallelism'], len(d['oneshot_xgmi_sweep']), d['config']['exchange'])"
+echo done
