@@ -16,9 +16,9 @@ tail -1 $O/smoke.log
 echo "== bench, the driver's command"
 for i in 1 2 3; do
   timeout -k 10 120 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_driver_$i.json 2> $O/bench_driver_$i.err || { tail -20 $O/bench_driver_$i.err; exit 1; }
-  python -c "import json; d=json.load(open('$O/bench_driver_$i.json')); print(d['value'], d['ms_per_step'])"
+  python -c "import json; d=json.loads(open('$O/bench_driver_$i.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])"
 done
 echo "== self-launched 4-rank rehearsal on one card"
 DGT_ALLOW_OVERSUBSCRIBE=1 timeout -k 10 400 python bench.py --gpus 4 --steps 20 --warmup 5 > $O/bench_self4.json 2> $O/bench_self4.err || { tail -30 $O/bench_self4.err; exit 1; }
-python -c "import json; d=json.load(open('$O/bench_self4.json')); print(d['value'], d['ranks'], d['config']['parallelism'], len(d['oneshot_xgmi_sweep']), d['allreduce_busbw_GBps'])"
+python -c "import json; d=json.loads(open('$O/bench_self4.json').read().strip().splitlines()[-1]); print(d['value'], d['ranks'], d['config']['parallelism'], len(d['oneshot_xgmi_sweep']), d['allreduce_busbw_GBps'])"
 echo done

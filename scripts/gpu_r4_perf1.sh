@@ -21,5 +21,5 @@ done
 echo done
 echo "== self-launched 4-rank rehearsal on one card (process group on gloo: RCCL needs one device per rank)"
 DGT_ALLOW_OVERSUBSCRIBE=1 timeout -k 10 400 python bench.py --gpus 4 --steps 20 --warmup 5 > gpurun_out/r4s/bench_self4.json 2> gpurun_out/r4s/bench_self4.err || { tail -30 gpurun_out/r4s/bench_self4.err; exit 1; }
-python -c "import json; d=json.load(open('gpurun_out/r4s/bench_self4.json')); print(d['value'], d['ranks'], d['config']['parallelism'], len(d['oneshot_xgmi_sweep']), d['config']['exchange'])"
+python -c "import json; d=json.loads(open('gpurun_out/r4s/bench_self4.json').read().strip().splitlines()[-1]); print(d['value'], d['ranks'], d['config']['parallelism'], len(d['oneshot_xgmi_sweep']), d['config']['exchange'])"
 echo done
