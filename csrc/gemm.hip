@@ -894,13 +894,15 @@ DGT_DEVICE int lane_off(bool is_a, int ld, int w, int i, int l) {
 // kernel spilled 1-3 VGPRs to scratch; from asm none does, 4-6 % faster at every size
 // (profiles/r3_gemm256_asm_ab.jsonl).  With every DMA of the loop in asm, the compiler tracks none
 // of them; the phase's explicit vmcnt waits and barriers order them (as in the 128x128 FR kernel).
-DGT_DEVICE void stage(const u16* ubase, const int (&off)[2], u16* unit_lds, int w) {
+// unit_la: the unit's LDS byte address, wave-uniform (kept in SGPRs: a generic LDS pointer per unit
+// costs two VGPRs each, and the cross-phase variant below has none to spare)
+DGT_DEVICE void stage(const u16* ubase, const int (&off)[2], unsigned unit_la, int w) {
   const unsigned long long b = reinterpret_cast<unsigned long long>(ubase);
   // (readfirstlane returns int: each half goes through unsigned, or the low half would be
   // sign-extended into the high one)
   const unsigned lo = __builtin_amdgcn_readfirstlane((unsigned)b), hi = __builtin_amdgcn_readfirstlane((unsigned)(b >> 32));
   const unsigned long long sb = ((unsigned long long)hi << 32) | lo;
-  const unsigned l0 = __builtin_amdgcn_readfirstlane(lds_byte_addr(unit_lds + w * 2 * 8 * BK));
+  const unsigned l0 = __builtin_amdgcn_readfirstlane(unit_la + (unsigned)(w * 2 * 8 * BK * 2));
 #pragma unroll
   for (int i = 0; i < 2; ++i) {
     unsigned saved;
@@ -939,6 +941,7 @@ struct Ctx {
   int lda, ldb, w, l, wr, wc;
   int offa[2], offb[2];
   u16* lds;
+  unsigned lds0;     // lds's LDS byte address (wave-uniform)
 };
 
 template <int U>
@@ -946,7 +949,7 @@ DGT_DEVICE void stage_unit(const Ctx& c, int kt, int buf) {
   const bool is_a = (U == kALo || U == kAHi);
   const u16* ubase = is_a ? c.A + (U == kAHi ? 64 * c.lda : 0) + kt * BK
                           : c.B + (U == kBHi ? 32 * c.ldb : 0) + kt * BK;
-  stage(ubase, is_a ? c.offa : c.offb, c.lds + (buf * 4 + U) * UNIT, c.w);
+  stage(ubase, is_a ? c.offa : c.offb, c.lds0 + (unsigned)((buf * 4 + U) * UNIT * 2), c.w);
 }
 
 // unit staged in phase P (1..8) of an iteration: ph1, ph2 -> the odd tile's B_hi, A_hi; ph3..6 ->
@@ -1026,9 +1029,120 @@ DGT_DEVICE void iteration(const Ctx& c, int it, Frags& f, f32x4 (&acc)[8][4]) {
   phase<7, LAST>(c, it, f, acc);
   phase<8, LAST>(c, it, f, acc);
 }
+
+// ---- cross-phase fragment prefetch (variant 8).  Above, every phase reads its fragments and then
+// waits for them before its MFMAs; the barrier lines all 8 waves up, so the CU's LDS reads (up to 96
+// KiB in q0) and its MFMAs take turns instead of overlapping.  Here phase P issues the reads of phase
+// P + 1 right after its barrier, interleaved with its own 16 MFMAs, and waits for them (lgkmcnt(0))
+// only before the next barrier.  The staging order and vmcnt waits are unchanged: the unit phase P+1
+// reads is exactly the one phase P's wait retires, and a read issued after barrier P has completed
+// before barrier P+1, so a unit may be restaged from phase P+2 on (every restage above is >= 2 phases
+// after the old last read, so >= 3 after the new one).  Each operand half keeps one register set:
+// q0 reads B_hi (free since the last tile's q2), q1 A_hi (free since q3), q2 the next tile's A_lo
+// (free since q1); B_lo is still being multiplied in q3 when the next tile's is read, so q3 issues
+// its kk = 0 MFMAs, then the reads that overwrite B_lo's kk = 0 fragments, then the kk = 1 MFMAs and
+// the remaining reads.  Same MFMAs in the same order per accumulator: bit-identical to phase<>.
+struct FragsX {
+  bf16x8 alo[4][2], ahi[4][2];
+  bf16x8 blo[2][2], bhi[2][2];
+};
+
+template <int U>
+DGT_DEVICE void read_a(const Ctx& c, int buf, bf16x8 (&dst)[4][2]) {  // A unit: the wave's 64 rows
+  const u16* ul = c.lds + (buf * 4 + U) * UNIT;
+  const int lr = c.l & 15, lc = c.l >> 4;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) dst[i][kk] = frag(ul, c.wr * 64 + i * 16 + lr, kk * 4 + lc);
+}
+template <int U>
+DGT_DEVICE void read_b(const Ctx& c, int buf, int kk, bf16x8 (&dst)[2][2]) {  // B unit: 32 cols, one kk
+  const u16* ul = c.lds + (buf * 4 + U) * UNIT;
+  const int lr = c.l & 15, lc = c.l >> 4;
+#pragma unroll
+  for (int j = 0; j < 2; ++j) dst[j][kk] = frag(ul, c.wc * 32 + j * 16 + lr, kk * 4 + lc);
+}
+
+template <int Q>
+DGT_DEVICE void mfma_half(FragsX& f, f32x4 (&acc)[8][4], int kk) {  // quadrant Q's 8 MFMAs of one kk
+  constexpr int i0 = (Q == 0 || Q == 1) ? 0 : 4;
+  constexpr bool hi_b = (Q == 1 || Q == 2);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+      acc[i0 + i][(hi_b ? 2 : 0) + j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+          i0 == 0 ? f.alo[i][kk] : f.ahi[i][kk], hi_b ? f.bhi[j][kk] : f.blo[j][kk],
+          acc[i0 + i][(hi_b ? 2 : 0) + j], 0, 0, 0);
+}
+
+template <int P, bool LAST>
+DGT_DEVICE void phase_x(const Ctx& c, int it, FragsX& f, f32x4 (&acc)[8][4]) {
+  constexpr int q = (P - 1) & 3;
+  constexpr int buf = P <= 4 ? 0 : 1;
+  if (!LAST || P <= 2) stage_phase<P>(c, it);
+  if (!LAST) wait_vm<8>();
+  else wait_vm<P <= 3 ? 8 : P == 4 ? 4 : P == 5 ? 2 : 0>();
+  wait_lgkm0();  // this phase's fragments (read during the previous phase) have landed
+  __builtin_amdgcn_sched_barrier(0);
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_sched_barrier(0);
+  constexpr bool reads = !(LAST && P >= 7);  // the last tile's q2 / q3 have no next tile to read
+  __builtin_amdgcn_s_setprio(1);
+  if constexpr (q == 3) {
+    mfma_half<3>(f, acc, 0);
+    if constexpr (reads) read_b<kBLo>(c, buf ^ 1, 0, f.blo);
+    mfma_half<3>(f, acc, 1);
+    if constexpr (reads) {
+      read_b<kBLo>(c, buf ^ 1, 1, f.blo);
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 8, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);
+    }
+  } else {
+    // q0: B_hi (4 reads), q1: A_hi (8), q2: the next tile's A_lo (8)
+    constexpr int nreads = q == 0 ? 4 : 8;
+    if constexpr (reads) {
+      if constexpr (q == 0) {
+        read_b<kBHi>(c, buf, 0, f.bhi);
+        read_b<kBHi>(c, buf, 1, f.bhi);
+      } else if constexpr (q == 1) {
+        read_a<kAHi>(c, buf, f.ahi);
+      } else {
+        read_a<kALo>(c, buf ^ 1, f.alo);
+      }
+    }
+    mfma_half<q>(f, acc, 0);
+    mfma_half<q>(f, acc, 1);
+    if constexpr (reads) {
+#pragma unroll
+      for (int r = 0; r < nreads; ++r) {
+        __builtin_amdgcn_sched_group_barrier(0x008, 1, 0);  // MFMA
+        __builtin_amdgcn_sched_group_barrier(0x100, 1, 0);  // DS read
+      }
+      __builtin_amdgcn_sched_group_barrier(0x008, 16 - nreads, 0);
+    }
+  }
+  __builtin_amdgcn_s_setprio(0);
+  __builtin_amdgcn_sched_barrier(0);
+}
+
+template <bool LAST>
+DGT_DEVICE void iteration_x(const Ctx& c, int it, FragsX& f, f32x4 (&acc)[8][4]) {
+  phase_x<1, LAST>(c, it, f, acc);
+  phase_x<2, LAST>(c, it, f, acc);
+  phase_x<3, LAST>(c, it, f, acc);
+  phase_x<4, LAST>(c, it, f, acc);
+  phase_x<5, LAST>(c, it, f, acc);
+  phase_x<6, LAST>(c, it, f, acc);
+  phase_x<7, LAST>(c, it, f, acc);
+  phase_x<8, LAST>(c, it, f, acc);
+}
 }  // namespace g256
 
-template <int EPI>
+template <int EPI, bool XP = false>
 __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   using namespace g256;
   __shared__ __attribute__((aligned(16))) u16 lds[2 * 4 * UNIT];
@@ -1041,7 +1155,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   c.B = static_cast<const u16*>(g.B) + (long long)n0 * g.ldb;
   c.lda = g.lda;
   c.ldb = g.ldb;
-  c.w = tid >> 6;
+  c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
   c.l = tid & 63;
   c.wr = c.w >> 2;
   c.wc = c.w & 3;
@@ -1051,6 +1165,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
     c.offb[i] = lane_off(false, g.ldb, c.w, i, c.l);
   }
   c.lds = lds;
+  c.lds0 = __builtin_amdgcn_readfirstlane(lds_byte_addr(lds));
 
   f32x4 acc[8][4];
 #pragma unroll
@@ -1071,8 +1186,18 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   __builtin_amdgcn_s_barrier();
 
   const int nit = g.K / (2 * BK);
-  for (int it = 0; it + 1 < nit; ++it) iteration<false>(c, it, f, acc);
-  iteration<true>(c, nit - 1, f, acc);
+  if constexpr (XP) {
+    // phase 1's fragments (tile 0's A_lo and B_lo, retired by the wait above)
+    FragsX fx;
+    read_a<kALo>(c, 0, fx.alo);
+    read_b<kBLo>(c, 0, 0, fx.blo);
+    read_b<kBLo>(c, 0, 1, fx.blo);
+    for (int it = 0; it + 1 < nit; ++it) iteration_x<false>(c, it, fx, acc);
+    iteration_x<true>(c, nit - 1, fx, acc);
+  } else {
+    for (int it = 0; it + 1 < nit; ++it) iteration<false>(c, it, f, acc);
+    iteration<true>(c, nit - 1, f, acc);
+  }
 
   if constexpr ((EPI & kEpiAdam) != 0) {
     // fp32 256 x 256 tile = 256 KiB: two passes of 128 rows through the 128 KiB of operand LDS
@@ -1090,10 +1215,12 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
 
 // variant: 0 = pick by shape (256x256 for >= 200 tiles, else for one-wave grids the 128x128 variant
 // 5 for a [K, N] B operand with K % 128 == 0 and variant 3 otherwise, else variant 1), 1 = 128x128
-// 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase, 3 = variant 4 with front-loaded fragment
-// reads (FR), 4 = 128x128 4-stage with 8 waves (1 block / CU; the FR kernels' bitwise oracle),
-// 5 = software-pipelined fragment reads (SP, five stages; K % 128 == 0, else 3).  The round-2 variants measured slower or no
-// better inside the MLP step (3, 5-9) live in git history (commit c0371a5, csrc/diag/gemm_variants_r2.h).
+// 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase (the bitwise oracle of 8), 3 = variant 4 with
+// front-loaded fragment reads (FR), 4 = 128x128 4-stage with 8 waves (1 block / CU; the FR kernels'
+// bitwise oracle), 5 = software-pipelined fragment reads (SP, five stages; K % 128 == 0, else 3),
+// 6 / 7 = register prefetch, 8 = 256x256 with cross-phase fragment prefetch (the shape rule's
+// 256x256 kernel).  The round-2 variants measured slower or no better inside the MLP step live in
+// git history (commit c0371a5).
 // the RP kernel for the forward-type epilogues (others: false, the dispatcher reports it)
 template <int E>
 bool launch_rp(int grid, const GemmArgs& g, hipStream_t stream, int depth) {
@@ -1114,7 +1241,12 @@ bool launch_rp(int grid, const GemmArgs& g, hipStream_t stream, int depth) {
 
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 7) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 8) return hipErrorInvalidValue;
+  // the 256x256 kernel runs the cross-phase fragment prefetch (g256::phase_x) unless variant 2 asks
+  // for the 8-phase pipeline it is bitwise-checked against: 8192^3 1.51-1.52 vs 1.39-1.47 PF, the
+  // MLP's wgrad 31.6-31.9 vs 33.0-33.7 us (profiles/r4_gemm256_xp.jsonl)
+  const bool xp = variant != 2;
+  if (variant == 8) variant = 2;
   // only the 128x128 kernels read a [K, N] B operand or form column sums
   const bool kn = (epi & (kEpiBKN | kEpiColSum)) != 0;
   if ((epi & kEpiColSum) && (!(epi & kEpiStoreT) || !g.colsum)) return hipErrorInvalidValue;
@@ -1160,7 +1292,8 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   case E:                                                                                         \
     if (rp) {                                                                                     \
       if (!launch_rp<E>(grid, g, stream, rp_depth)) return hipErrorInvalidValue;                  \
-    } else if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g); \
+    } else if (big && xp) hipLaunchKernelGGL((gemm_nt_256_kernel<E, true>), dim3(grid), dim3(512), 0, stream, g); \
+    else if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g); \
     else if (sp) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 3>), dim3(grid), dim3(512), 0, stream, g); \
     else if (fr) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1>), dim3(grid), dim3(512), 0, stream, g); \
     else if (eight) hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8>), dim3(grid), dim3(512), 0, stream, g); \

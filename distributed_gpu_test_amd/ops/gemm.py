@@ -49,12 +49,16 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
             out_f32: bool = False, accumulate: bool = False, alpha: float = 1.0, variant: int = 0,
             b_kn: bool = False, colsum: Optional[torch.Tensor] = None) -> None:
     """variant: 0 = pick the kernel by shape, 1 = 128x128 tiles 2-stage (2 blocks per CU),
-    2 = 256x256 8-phase pipeline, 3 = variant 4 with front-loaded LDS fragment reads,
+    2 = 256x256 8-phase pipeline (variant 8's bitwise oracle), 3 = variant 4 with front-loaded LDS
+    fragment reads,
     4 = 128x128 tiles 4-stage with 8 waves (1 block per CU; variant 3's bitwise oracle),
     5 = software-pipelined fragment reads (the next K-tile's fragments read during this one's MFMAs,
     five LDS stages; K % 128 == 0, else 3) -- the shape rule's choice for the ``b_kn`` dgrad,
     6 / 7 = register prefetch (2 / 4 K-tiles of operands in flight in VGPRs, two LDS stages; NT
-    forward-type products, bit-identical to 3; other products keep the shape rule).
+    forward-type products, bit-identical to 3; other products keep the shape rule),
+    8 = the 256x256 kernel with cross-phase fragment prefetch (phase P's MFMAs overlap the LDS
+    reads of phase P + 1; bit-identical to 2) -- the kernel the shape rule runs for >= 200 tiles of
+    256x256.
     ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
     the shape rule gives to the 128x128 kernels).
 

@@ -243,6 +243,7 @@ class MLPTrainer:
         self._v_wga = int(os.environ.get("DGT_MLP_WGA_VARIANT", "0") or 0)
         self._v_dgrad = int(os.environ.get("DGT_MLP_DGRAD_VARIANT", "0") or 0)
         self._v_fwd = int(os.environ.get("DGT_MLP_FWD_VARIANT", "0") or 0)
+        self._v_wgrad = int(os.environ.get("DGT_MLP_WGRAD_VARIANT", "0") or 0)
         if self._wga_side:
             self.s_opt = torch.cuda.Stream(dev)
             self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
@@ -363,7 +364,8 @@ class MLPTrainer:
         # s_opt once backward no longer reads W_i^T (after its dgrad) and the collective is done
         for i in reversed(range(L)):
             a_prevT = xT if i == 0 else self.aT[i]
-            gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=self.grad_dtype == torch.float32)
+            gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=self.grad_dtype == torch.float32,
+                    variant=self._v_wgrad)
             if not self._partials:
                 rowsum_bf16(self.gT[cur], self.gb[i])
             if self.coll:

@@ -35,6 +35,7 @@ the updated parameters; checkpoints hold one ``zero_pp_rank_{r}`` shard of owned
 """
 from __future__ import annotations
 
+import functools
 import os
 import sys
 from typing import Any, Dict, List, Optional
@@ -464,6 +465,31 @@ class TinyMLPTrainer:
                                      self.adamw, grad_scale=1.0 / self.world_size)
         self.global_samples += n * self.B * self.world_size
         self.faults.maybe_fire(self.global_steps)
+
+    def bind_launch(self, plan: torch.Tensor, counts: torch.Tensor):
+        """``run_plan(plan, counts)`` as a zero-argument callable whose per-call host work is the
+        ctypes call into ``dgt_tiny_launch`` (hipLaunchKernel) and the step bookkeeping: the plan
+        checks, the stream lookup, the workspace sizing and the argument packing happen here, once.
+        Valid while the current stream stays the one bound here.  Paths other than the
+        dispatcher-free fused launch get ``run_plan`` itself."""
+        n = int(plan.shape[0])
+        if not (self.impl == "fused" and n and self._lean_ok(plan, counts, n)):
+            return functools.partial(self.run_plan, plan, counts)
+        self.reserve(n)
+        stream = _raw_stream(self.device.index)
+        if stream != self._lh_stream:
+            self._clib.dgt_tiny_launcher_set_stream(self._lh, stream)
+            self._lh_stream = stream
+        fn, lh, ch = self._clib.dgt_tiny_launch, self._lh, self.channel
+        pp, cp, bmax, ws = plan.data_ptr(), counts.data_ptr(), int(plan.shape[1]), self._ws_ptr
+
+        def launch() -> None:
+            seq = ch.next_seq(n) if ch is not None else 0
+            rc = fn(lh, pp, cp, n, bmax, self.global_steps, seq, ws)
+            if rc != 0:
+                raise RuntimeError(f"dgt: fused training kernel launch failed (hipError {rc})")
+            self.global_steps += n
+        return launch
 
     def reserve(self, n_steps: int) -> None:
         """Size the fused kernel's workspace for launches of up to ``n_steps`` steps (the kernel fills

@@ -116,10 +116,51 @@ def test_gemm_256_large_k_repeated():
     B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
     ref = A.float() @ B.float().t()
     C = torch.empty(M, N, dtype=torch.float32).cuda()
-    for _ in range(5):
-        C.fill_(float("nan"))
-        gemm_nt(A, B, C=C, out_f32=True, variant=2)
-        torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
+    for v in (2, 8):
+        for _ in range(5):
+            C.fill_(float("nan"))
+            gemm_nt(A, B, C=C, out_f32=True, variant=v)
+            torch.testing.assert_close(C, ref, rtol=1e-3, atol=1e-2)
+
+
+@gpu
+@pytest.mark.parametrize("K", [128, 256, 384, 1024])
+@pytest.mark.parametrize("epi", ["plain", "bias_relu_t", "f32_acc", "adam"])
+def test_gemm_256_cross_phase_prefetch_is_bitwise_variant2(K, epi):
+    """Variant 8 (the 256x256 kernel reading phase P + 1's fragments during phase P's MFMAs) runs
+    variant 2's MFMAs in the same order per accumulator: every epilogue's output, the fused Adam's
+    state included, equals variant 2's bit for bit -- at one loop iteration (K = 128: only the
+    drain iteration), two, three and eight."""
+    from distributed_gpu_test_amd.ops.gemm import gemm_nt_adam_
+    g = torch.Generator().manual_seed(K)
+    M, N = 512, 768
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
+    bias = torch.randn(N, generator=g).cuda()
+    base = torch.randn(M, N, generator=g).cuda()
+    outs = []
+    for v in (2, 8):
+        if epi == "plain":
+            C = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+            gemm_nt(A, B, C=C, variant=v)
+            outs.append([C])
+        elif epi == "bias_relu_t":
+            C = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+            CT = torch.empty(N, M, dtype=torch.bfloat16).cuda()
+            gemm_nt(A, B, C=C, CT=CT, bias=bias, relu=True, variant=v)
+            outs.append([C, CT])
+        elif epi == "f32_acc":
+            C = base.clone()
+            gemm_nt(A, B, C=C, out_f32=True, accumulate=True, variant=v)
+            outs.append([C])
+        else:
+            p, m, s = base.clone(), torch.zeros(M, N).cuda(), torch.zeros(M, N).cuda()
+            pb = torch.empty(M, N, dtype=torch.bfloat16).cuda()
+            gemm_nt_adam_(A, B, p, m, s, pb, 3, 1e-3, 0.9, 0.999, 1e-8, variant=v)
+            outs.append([p, m, s, pb])
+    assert all(torch.equal(x, y) for x, y in zip(*outs))
+    if epi == "f32_acc":
+        torch.testing.assert_close(outs[1][0], base + A.float() @ B.float().t(), rtol=1e-3, atol=1e-2)
 
 
 @gpu
