@@ -199,17 +199,18 @@ def timed_run(trainer, plan, counts, args, device, comm):
     # microsecond of each other on every rank, so the hosts leave their syncs nearly together.
     use_dev = comm.collectives_on() and not os.environ.get("DGT_BENCH_PG_BARRIER")
     multi = comm.collectives_on()  # decided outside the timed region: the lookup costs microseconds
+    # the launch's host-side preparation (plan checks, stream lookup, argument packing) is done here,
+    # outside the bracket; the bracket holds the launch call itself and all K steps.  The held-back
+    # warmup step goes through the same bound-launch code, so the timed call is not its first.
+    bind = getattr(trainer, "bind_launch", None) or (lambda p, c: functools.partial(trainer.run_plan, p, c))
+    launch = bind(timed_plan, timed_counts)
     barrier()
     warm_loss = None
     if warm_last:  # the held-back warmup step; its loss is taken back out of the timed mean below
-        trainer.run_plan(last_plan, last_counts)
+        bind(last_plan, last_counts)()
         warm_loss = trainer.loss_acc.clone()
     if use_dev:
         getattr(trainer, "device_barrier", lambda: False)()
-    # the launch's host-side preparation (plan checks, stream lookup, argument packing) is done here,
-    # outside the bracket; the bracket holds the launch call itself and all K steps
-    bind = getattr(trainer, "bind_launch", None)
-    launch = bind(timed_plan, timed_counts) if bind else functools.partial(trainer.run_plan, timed_plan, timed_counts)
     if gpu:
         torch.cuda.synchronize()
     t0 = time.perf_counter()

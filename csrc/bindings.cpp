@@ -170,6 +170,15 @@ struct TinyLauncher {
   hipStream_t stream;
 };
 
+// dgt_tiny_prepare: one plan's complete argument block and the resolved kernel, so that
+// dgt_tiny_launch_prepared passes only the step base and sequence number
+struct TinyPrepared {
+  dgt::TinyTrainArgs a;
+  hipFunction_t fn;
+  int threads, device;
+  hipStream_t stream;
+};
+
 int64_t tiny_launcher_create(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& params,
                              const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq, const at::Tensor& loss_acc,
                              const at::Tensor& status, int64_t n_features, int64_t hidden, double lr, double beta1,
@@ -262,6 +271,50 @@ extern "C" int dgt_tiny_launch(int64_t handle, int64_t plan, int64_t counts, int
   if (cur != L->device) (void)hipSetDevice(cur);
   return (int)e;
 }
+
+// Bind one plan (device pointers, step count, row bound, workspace) and the launcher's stream into a
+// TinyPrepared and resolve its kernel once; dgt_tiny_launch_prepared then launches it with the
+// kernel-argument block passed as a buffer (no per-argument marshalling, no host-function lookup).
+// Returns the handle (0 on failure, *err = the hipError_t); free with dgt_tiny_prepared_free.
+extern "C" int64_t dgt_tiny_prepare(int64_t handle, int64_t plan, int64_t counts, int n_steps, int bmax,
+                                    int64_t workspace, int* err) {
+  auto* L = reinterpret_cast<TinyLauncher*>(handle);
+  *err = (int)hipErrorInvalidValue;
+  if (!L || !plan || !counts || !workspace || n_steps < 1 || bmax < 1 || bmax > 16) return 0;
+  auto* P = new TinyPrepared();
+  P->a = L->a;
+  P->a.plan = reinterpret_cast<const int*>(plan);
+  P->a.counts = reinterpret_cast<const int*>(counts);
+  P->a.n_steps = n_steps;
+  P->a.bmax = bmax;
+  P->a.bc = reinterpret_cast<float*>(workspace);
+  P->device = L->device;
+  P->stream = L->stream;
+  const void* k = dgt::tiny_mlp_train_symbol(L->f, L->h, P->a, &P->threads);
+  int cur = -1;
+  hipError_t e = k ? hipGetDevice(&cur) : hipErrorInvalidValue;
+  if (e == hipSuccess && cur != L->device) e = hipSetDevice(L->device);
+  if (e == hipSuccess) e = hipGetFuncBySymbol(&P->fn, k);
+  if (cur >= 0 && cur != L->device) (void)hipSetDevice(cur);
+  *err = (int)e;
+  if (e != hipSuccess) {
+    delete P;
+    return 0;
+  }
+  return reinterpret_cast<int64_t>(P);
+}
+
+extern "C" int dgt_tiny_launch_prepared(int64_t prepared, long long step0, long long seq_base) {
+  auto* P = reinterpret_cast<TinyPrepared*>(prepared);
+  if (!P) return (int)hipErrorInvalidValue;
+  P->a.adam_step0 = step0;
+  P->a.ex.seq_base = seq_base;
+  size_t size = sizeof(dgt::TinyTrainArgs);
+  void* extra[] = {HIP_LAUNCH_PARAM_BUFFER_POINTER, &P->a, HIP_LAUNCH_PARAM_BUFFER_SIZE, &size, HIP_LAUNCH_PARAM_END};
+  return (int)hipModuleLaunchKernel(P->fn, 1, 1, 1, (unsigned)P->threads, 1, 1, 0, P->stream, nullptr, extra);
+}
+
+extern "C" void dgt_tiny_prepared_free(int64_t prepared) { delete reinterpret_cast<TinyPrepared*>(prepared); }
 
 // Re-target a launcher at another HIP stream (the caller's current stream changed).
 extern "C" void dgt_tiny_launcher_set_stream(int64_t handle, int64_t stream) {

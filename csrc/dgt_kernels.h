@@ -35,6 +35,8 @@ struct TinyTrainArgs {
 };
 
 hipError_t tiny_mlp_train(int n_features, int hidden, const TinyTrainArgs& a, hipStream_t stream);
+// the instantiation tiny_mlp_train would launch for these arguments (nullptr: none) and its block size
+const void* tiny_mlp_train_symbol(int n_features, int hidden, const TinyTrainArgs& a, int* threads);
 
 // n_steps exchanges of the fused kernel's mailbox layout and line format (ex.line) with payloads that
 // expose any torn or lost line: bad words are added to *errors, a timeout sets *status.

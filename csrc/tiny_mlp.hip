@@ -924,17 +924,18 @@ int tiny_mlp_exchange_floats(int f, int h) {
   return 0;
 }
 
-hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
-  if (!a.bc) return hipErrorInvalidValue;
+// The kernel instantiation a launch of shape (f, h) with these arguments runs, and its block size;
+// nullptr if none (bad shape or line format).  Shared by the per-call launch and the prepared
+// launcher (bindings.cpp), which resolves it once.
+const void* tiny_mlp_train_symbol(int f, int h, const TinyTrainArgs& a, int* threads) {
+  if (!a.bc) return nullptr;
   const bool wd = a.hp.weight_decay != 0.f;
   const bool ll2 = a.ex.line == 2, z = a.ex.zero1 != 0;
-  if (a.ex.world_size > 1 && a.ex.line != 2 && a.ex.line != 3) return hipErrorInvalidValue;
+  if (a.ex.world_size > 1 && a.ex.line != 2 && a.ex.line != 3) return nullptr;
 #define DGT_TINY_LAUNCH_K(F_, H_, SB, NP_, LN_, Z_)                                                   \
   do {                                                                                             \
-    if (wd)                                                                                        \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, true, LN_, Z_>), dim3(1), blk, 0, stream, a); \
-    else                                                                                           \
-      hipLaunchKernelGGL((tiny_mlp_train_kernel<F_, H_, SB, NP_, false, LN_, Z_>), dim3(1), blk, 0, stream, a); \
+    if (wd) return reinterpret_cast<const void*>(&tiny_mlp_train_kernel<F_, H_, SB, NP_, true, LN_, Z_>); \
+    return reinterpret_cast<const void*>(&tiny_mlp_train_kernel<F_, H_, SB, NP_, false, LN_, Z_>);      \
   } while (0)
 // exchange kernels: line format x ZeRO-1, for 2, 4 or 8 compiled ranks
 #define DGT_TINY_LAUNCH_NP(F_, H_, SB, NP_)                                                        \
@@ -953,20 +954,27 @@ hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stre
   } while (0)
 #define X_(F_, H_)                                                                            \
   if (f == F_ && h == H_) {                                                                   \
-    const dim3 blk(TinyCfg<F_, H_>::T);                                                       \
+    *threads = TinyCfg<F_, H_>::T;                                                            \
     const bool xch = a.ex.world_size > 1;                                                     \
     if (a.bmax <= 4 && !xch) DGT_TINY_LAUNCH(F_, H_, true, false);                            \
     else if (a.bmax <= 4) DGT_TINY_LAUNCH(F_, H_, true, true);                                \
     else if (!xch) DGT_TINY_LAUNCH(F_, H_, false, false);                                     \
     else DGT_TINY_LAUNCH(F_, H_, false, true);                                                \
-    return hipGetLastError();                                                                 \
   }
   DGT_TINY_SHAPES(X_)
 #undef X_
 #undef DGT_TINY_LAUNCH
 #undef DGT_TINY_LAUNCH_NP
 #undef DGT_TINY_LAUNCH_K
-  return hipErrorInvalidValue;
+  return nullptr;
+}
+
+hipError_t tiny_mlp_train(int f, int h, const TinyTrainArgs& a, hipStream_t stream) {
+  int threads = 0;
+  const void* k = tiny_mlp_train_symbol(f, h, a, &threads);
+  if (!k) return hipErrorInvalidValue;
+  void* args[] = {const_cast<TinyTrainArgs*>(&a)};
+  return hipLaunchKernel(k, dim3(1), dim3(threads), args, 0, stream);
 }
 
 hipError_t tiny_mlp_grad(int f, int h, const TinyGradArgs& a, hipStream_t stream) {

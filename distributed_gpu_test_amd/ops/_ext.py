@@ -62,6 +62,12 @@ def c_lib():
         i64, i32 = ctypes.c_int64, ctypes.c_int
         lib.dgt_tiny_launch.argtypes = [i64, i64, i64, i32, i32, ctypes.c_longlong, ctypes.c_longlong, i64]
         lib.dgt_tiny_launch.restype = i32
+        lib.dgt_tiny_prepare.argtypes = [i64, i64, i64, i32, i32, i64, ctypes.POINTER(i32)]
+        lib.dgt_tiny_prepare.restype = i64
+        lib.dgt_tiny_prepared_free.argtypes = [i64]
+        lib.dgt_tiny_prepared_free.restype = None
+        lib.dgt_tiny_launch_prepared.argtypes = [i64, ctypes.c_longlong, ctypes.c_longlong]
+        lib.dgt_tiny_launch_prepared.restype = i32
         lib.dgt_tiny_launcher_set_stream.argtypes = [i64, i64]
         lib.dgt_tiny_launcher_set_stream.restype = None
         _clib = lib

@@ -466,12 +466,14 @@ class TinyMLPTrainer:
         self.global_samples += n * self.B * self.world_size
         self.faults.maybe_fire(self.global_steps)
 
-    def bind_launch(self, plan: torch.Tensor, counts: torch.Tensor):
-        """``run_plan(plan, counts)`` as a zero-argument callable whose per-call host work is the
-        ctypes call into ``dgt_tiny_launch`` (hipLaunchKernel) and the step bookkeeping: the plan
-        checks, the stream lookup, the workspace sizing and the argument packing happen here, once.
-        Valid while the current stream stays the one bound here.  Paths other than the
-        dispatcher-free fused launch get ``run_plan`` itself."""
+    def bind_launch(self, plan: torch.Tensor, counts: torch.Tensor, prepared: bool = True):
+        """``run_plan(plan, counts)`` as a zero-argument callable whose per-call host work is one
+        ctypes call and the step bookkeeping: the plan checks, the stream lookup, the workspace
+        sizing, the argument block and (``prepared``) the kernel lookup happen here, once, and the
+        launch passes the whole argument block as one buffer (``dgt_tiny_launch_prepared`` ->
+        hipModuleLaunchKernel); ``prepared=False`` keeps the per-launch entry point
+        (``dgt_tiny_launch`` -> hipLaunchKernel).  Valid while the current stream stays the one
+        bound here.  Paths other than the dispatcher-free fused launch get ``run_plan`` itself."""
         n = int(plan.shape[0])
         if not (self.impl == "fused" and n and self._lean_ok(plan, counts, n)):
             return functools.partial(self.run_plan, plan, counts)
@@ -480,8 +482,28 @@ class TinyMLPTrainer:
         if stream != self._lh_stream:
             self._clib.dgt_tiny_launcher_set_stream(self._lh, stream)
             self._lh_stream = stream
-        fn, lh, ch = self._clib.dgt_tiny_launch, self._lh, self.channel
+        ch = self.channel
         pp, cp, bmax, ws = plan.data_ptr(), counts.data_ptr(), int(plan.shape[1]), self._ws_ptr
+        if prepared:
+            import ctypes
+            import weakref
+            err = ctypes.c_int(0)
+            handle = self._clib.dgt_tiny_prepare(self._lh, pp, cp, n, bmax, ws, ctypes.byref(err))
+            if not handle:
+                raise RuntimeError(f"dgt: preparing the fused training kernel launch failed (hipError {err.value})")
+            fn = self._clib.dgt_tiny_launch_prepared
+            keep = (plan, counts, self._ws)  # the prepared block holds their device addresses
+
+            def launch() -> None:
+                seq = ch.next_seq(n) if ch is not None else 0
+                rc = fn(handle, self.global_steps, seq)
+                if rc != 0:
+                    raise RuntimeError(f"dgt: fused training kernel launch failed (hipError {rc})")
+                self.global_steps += n
+            launch.keep = keep
+            weakref.finalize(launch, self._clib.dgt_tiny_prepared_free, handle)
+            return launch
+        fn, lh = self._clib.dgt_tiny_launch, self._lh
 
         def launch() -> None:
             seq = ch.next_seq(n) if ch is not None else 0

@@ -60,6 +60,36 @@ def test_fused_reproduces_reference_oracle_ws1():
     assert losses == ORACLE_WS1
 
 
+@pytest.mark.parametrize("prepared", [True, False])
+def test_bound_launch_is_bitwise_run_plan(prepared):
+    """bench.py's bound launch (``bind_launch``: the argument block prepared once, launched through
+    hipModuleLaunchKernel, or the per-argument entry point) trains exactly as ``run_plan``: same
+    parameters, moments, loss and step count, bit for bit, over several launches of one plan and a
+    launch of another."""
+    x, y, m1 = _setup()
+    _, _, m2 = _setup()
+    a = TinyMLPTrainer(m1, x, y, 4, impl="fused")
+    b = TinyMLPTrainer(m2, x, y, 4, impl="fused")
+    plan, counts = a.epoch_plan(1)
+    p20, c20 = plan[:20], counts[:20]
+    a.reserve(20)
+    b.reserve(20)
+    launch = b.bind_launch(p20, c20, prepared=prepared)
+    other = b.bind_launch(plan[20:23], counts[20:23], prepared=prepared)
+    for _ in range(3):
+        a.run_plan(p20, c20)
+        launch()
+    a.run_plan(plan[20:23], counts[20:23])
+    other()
+    torch.cuda.synchronize()
+    assert a.global_steps == b.global_steps == 63
+    for ta, tb in ((a.params, b.params), (a.exp_avg, b.exp_avg), (a.exp_avg_sq, b.exp_avg_sq),
+                   (a.loss_acc, b.loss_acc)):
+        assert torch.equal(ta, tb)
+    a.check()
+    b.check()
+
+
 def test_stepwise_matches_fused():
     x, y, m1 = _setup()
     _, _, m2 = _setup()
