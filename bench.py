@@ -174,15 +174,19 @@ def timed_run(trainer, plan, counts, args, device, comm):
     # the last warmup step is held back and launched right before the opening sync (below), so the
     # host launch path is as hot for the timed launch as in a steady-state loop
     warm_last = args.warmup > 0 and os.environ.get("DGT_BENCH_WARM_LAST", "1") == "1"
+    # the launch's host-side preparation (plan checks, stream lookup, argument packing) is done
+    # outside the bracket; the bracket holds the launch call itself and all K steps
+    bind = getattr(trainer, "bind_launch", None) or (lambda p, c: functools.partial(trainer.run_plan, p, c))
     if args.warmup:
-        # the last few warmup steps run as single-step launches: the launch path itself (HIP
-        # runtime, dispatcher, Python) is then as warm for the timed launch as in steady state
+        # the last few warmup steps run as single-step launches through the same bound-launch path
+        # the timed region uses: that path (HIP runtime, ctypes, Python) is then as warm for the
+        # timed launch as in steady state, not on its first or second call
         tail = min(args.warmup, 4)
         head = args.warmup - tail
         if head:
             trainer.run_plan(plan[:head], counts[:head])
         for s in range(head, args.warmup - (1 if warm_last else 0)):
-            trainer.run_plan(plan[s:s + 1], counts[s:s + 1])
+            bind(plan[s:s + 1], counts[s:s + 1])()
     timed_plan, timed_counts = plan[args.warmup:], counts[args.warmup:]  # views; the upload happened in build_plan
     last_plan, last_counts = plan[args.warmup - 1:args.warmup], counts[args.warmup - 1:args.warmup]
     trainer.loss_acc.zero_()  # queued behind the warmup: the bracket's opening sync has nothing left to wait on
@@ -199,10 +203,6 @@ def timed_run(trainer, plan, counts, args, device, comm):
     # microsecond of each other on every rank, so the hosts leave their syncs nearly together.
     use_dev = comm.collectives_on() and not os.environ.get("DGT_BENCH_PG_BARRIER")
     multi = comm.collectives_on()  # decided outside the timed region: the lookup costs microseconds
-    # the launch's host-side preparation (plan checks, stream lookup, argument packing) is done here,
-    # outside the bracket; the bracket holds the launch call itself and all K steps.  The held-back
-    # warmup step goes through the same bound-launch code, so the timed call is not its first.
-    bind = getattr(trainer, "bind_launch", None) or (lambda p, c: functools.partial(trainer.run_plan, p, c))
     launch = bind(timed_plan, timed_counts)
     barrier()
     warm_loss = None

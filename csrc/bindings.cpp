@@ -416,7 +416,12 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     if (accumulate) C.add_(z); else C.copy_(z);
     return;
   }
-  const dgt::GemmF32Plan plan = dgt::gemm_f32_plan(a.M, a.N, a.K);
+  // DGT_F32_MIN_BLOCKS (A/B knob, read once): the grid size split-K fills small products up to
+  static const int min_blocks = [] {
+    const char* e = std::getenv("DGT_F32_MIN_BLOCKS");
+    return e && *e ? std::max(1, std::atoi(e)) : 0;
+  }();
+  const dgt::GemmF32Plan plan = dgt::gemm_f32_plan(a.M, a.N, a.K, min_blocks);
   at::Tensor ws;
   if (plan.splits > 1) {
     ws = at::empty({(int64_t)plan.splits * M * N}, A.options());

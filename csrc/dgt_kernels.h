@@ -115,7 +115,9 @@ struct GemmF32Plan {
   bool big;    // 128x128 block tile (else 64x64)
   int splits;  // split-K slices (1 = none)
 };
-GemmF32Plan gemm_f32_plan(int M, int N, int K);
+// min_blocks: split K until the grid holds at least this many blocks (0 = auto: 2 blocks per CU for
+// 128x128 tiles, 4 for 64x64)
+GemmF32Plan gemm_f32_plan(int M, int N, int K, int min_blocks = 0);
 hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& plan, hipStream_t stream);
 // db[n] (+)= sum_m dy[m][n] * (y ? 1[y[m][n] > 0] : 1) over row slices (part: slices * N floats)
 int colsum_f32_slices(int M, int N);

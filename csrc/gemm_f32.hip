@@ -110,11 +110,15 @@ struct Tile {
         off = c * 4;  // [k][ROWS], chunks in memory order
       }
       f32x4 x = v[i];
+      // interior chunks (every chunk of an interior tile) need no select: the zero-fill is for the
+      // ragged edges only, and the VALU it costs per K-tile showed up in the counters (PMC)
+      if (MASKED || ((oob >> (4 * i)) & 15u) != 0u) {
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        bool keep = !((oob >> (4 * i + e)) & 1u);
-        if constexpr (MASKED) keep = keep && m[i][e] > 0.f;
-        x[e] = keep ? x[e] : 0.f;
+        for (int e = 0; e < 4; ++e) {
+          bool keep = !((oob >> (4 * i + e)) & 1u);
+          if constexpr (MASKED) keep = keep && m[i][e] > 0.f;
+          x[e] = keep ? x[e] : 0.f;
+        }
       }
       *reinterpret_cast<f32x4*>(lds + off) = x;
     }
@@ -192,23 +196,30 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args a) {
     ta[p].store(lds[buf], tid);
     tb[p].store(lds[buf] + A_SZ, tid);
   };
+  // the k groups' fragments are read one group ahead: group g + 1's LDS reads are in flight while
+  // group g's MFMAs run (reading each group just before its MFMAs left the waves waiting on LDS
+  // ~30x as long as hipBLASLt's: SQ_WAIT_INST_LDS, profiles/r4_gemm_f32_pmc.txt)
   auto consume = [&](int buf) {
     const float* la = lds[buf];
     const float* lb = lds[buf] + A_SZ;
+    f32x4 fa[2][TM], fb[2][TN];
+    auto read = [&](int g, int d) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i) fa[d][i] = frag<LA == 1, BM>(la, wm * WM + 32 * i, g, lane);
+#pragma unroll
+      for (int j = 0; j < TN; ++j) fb[d][j] = frag<LB == 1, BN>(lb, wn * WN + 32 * j, g, lane);
+    };
+    read(0, 0);
 #pragma unroll
     for (int g = 0; g < BK / 8; ++g) {
-      f32x4 fa[TM], fb[TN];
-#pragma unroll
-      for (int i = 0; i < TM; ++i) fa[i] = frag<LA == 1, BM>(la, wm * WM + 32 * i, g, lane);
-#pragma unroll
-      for (int j = 0; j < TN; ++j) fb[j] = frag<LB == 1, BN>(lb, wn * WN + 32 * j, g, lane);
+      if (g + 1 < BK / 8) read(g + 1, (g + 1) & 1);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[i][s], fb[j][s], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[g & 1][i][s], fb[g & 1][j][s], acc[i][j], 0, 0, 0);
     }
   };
   // (the loop sits inside the nkt > 0 branch: a path into the loop header that skipped the prologue
@@ -345,7 +356,7 @@ hipError_t dispatch(const GemmF32Args& a, bool big, bool vec, int splits, hipStr
 
 }  // namespace f32g
 
-GemmF32Plan gemm_f32_plan(int M, int N, int K) {
+GemmF32Plan gemm_f32_plan(int M, int N, int K, int min_blocks) {
   GemmF32Plan p;
   const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
   const long long t64 = (long long)((M + 63) / 64) * ((N + 63) / 64);
@@ -354,8 +365,11 @@ GemmF32Plan gemm_f32_plan(int M, int N, int K) {
   const int ktiles = (K + f32g::BK - 1) / f32g::BK;
   p.splits = 1;
   // small grid, long K (e.g. a wgrad whose reduction runs over a large batch): split K so the
-  // launch covers the chip; partial sums are combined in slice order (deterministic)
-  while (tiles * p.splits < 256 && ktiles / (2 * p.splits) >= 8 && p.splits < 16) p.splits *= 2;
+  // launch covers the chip with 2 (128x128) or 4 (64x64) blocks per CU -- more blocks in flight
+  // measured faster in the fp32 engine step even where a hot repeat of one product is not
+  // (profiles/r4_gemm_f32_split_ab.txt); partial sums are combined in slice order (deterministic)
+  if (min_blocks <= 0) min_blocks = p.big ? 512 : 1024;
+  while (tiles * p.splits < min_blocks && ktiles / (2 * p.splits) >= 8 && p.splits < 16) p.splits *= 2;
   return p;
 }
 

@@ -244,14 +244,6 @@ class MLPTrainer:
         self._v_dgrad = int(os.environ.get("DGT_MLP_DGRAD_VARIANT", "0") or 0)
         self._v_fwd = int(os.environ.get("DGT_MLP_FWD_VARIANT", "0") or 0)
         self._v_wgrad = int(os.environ.get("DGT_MLP_WGRAD_VARIANT", "0") or 0)
-        # DGT_MLP_WGRAD_SIDE=1 (one rank, flat Adam): each layer's wgrad runs on a side stream beside
-        # the same layer's dgrad (they read g_i / g_i^T and write disjoint buffers); the next dgrad,
-        # which overwrites the g^T buffer the wgrad reads, and the optimizer wait for it
-        self._wgrad_side = (dev.type == "cuda" and os.environ.get("DGT_MLP_WGRAD_SIDE", "0") == "1")
-        if self._wgrad_side:
-            self.s_wgrad = torch.cuda.Stream(dev)
-            self.ev_wg_in = [torch.cuda.Event() for _ in range(self.L)]
-            self.ev_wg_out = [torch.cuda.Event() for _ in range(self.L)]
         if self._wga_side:
             self.s_opt = torch.cuda.Stream(dev)
             self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
@@ -370,23 +362,13 @@ class MLPTrainer:
         # backward, last layer first; each weight bucket leaves for its collective as soon as its
         # wgrad is enqueued; with the overlap schedule the layer's optimizer update follows on
         # s_opt once backward no longer reads W_i^T (after its dgrad) and the collective is done
-        wside = self._wgrad_side and not ov and not self.coll and self._partials
-        if wside:
-            main = torch.cuda.current_stream(self.device)
         for i in reversed(range(L)):
             a_prevT = xT if i == 0 else self.aT[i]
-            if wside:
-                self.ev_wg_in[i].record(main)
-                self.s_wgrad.wait_event(self.ev_wg_in[i])
-                with torch.cuda.stream(self.s_wgrad):
-                    gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=self.grad_dtype == torch.float32,
-                            variant=self._v_wgrad)
-                    self.ev_wg_out[i].record(self.s_wgrad)
-                if i + 1 < L:  # the previous layer's wgrad read the g^T buffer this dgrad overwrites
-                    main.wait_event(self.ev_wg_out[i + 1])
-            else:
-                gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=self.grad_dtype == torch.float32,
-                        variant=self._v_wgrad)
+            # (a side stream running this wgrad beside the same layer's dgrad measured 8 % slower per
+            # step: two one-wave grids of one-block-per-CU kernels compete for the CUs,
+            # profiles/r4_mlp_wgrad_side_ab.txt)
+            gemm_nt(self.gT[cur], a_prevT, C=self.gW[i], out_f32=self.grad_dtype == torch.float32,
+                    variant=self._v_wgrad)
             if not self._partials:
                 rowsum_bf16(self.gT[cur], self.gb[i])
             if self.coll:
@@ -414,10 +396,6 @@ class MLPTrainer:
                 with torch.cuda.stream(self.s_opt):
                     self._update_layer(i)
                     self.ev_opt[i].record(self.s_opt)
-        if wside:  # every wgrad done before the optimizer reads the gradients
-            main.wait_event(self.ev_wg_out[0])
-            if L > 1:
-                main.wait_event(self.ev_wg_out[1])
         small_done = self._reduce_small(with_adam=True)
         if self.coll:  # biases + head: one small replicated bucket
             self._collective(dist.all_reduce, self.grads_s, works=works)

@@ -490,28 +490,6 @@ def test_mlp_side_stream_wgrad_adam_is_bitwise_in_line(monkeypatch):
 
 
 @gpu
-@pytest.mark.parametrize("depth", [1, 2, 4])
-def test_mlp_wgrad_side_stream_is_bitwise_in_line(monkeypatch, depth):
-    """DGT_MLP_WGRAD_SIDE=1 runs each layer's wgrad on a side stream beside its dgrad (the next
-    dgrad and the optimizer wait for it): a schedule change only, at every depth (depth 1: one
-    wgrad, no dgrad)."""
-    def run(side):
-        monkeypatch.setenv("DGT_MLP_WGRAD_SIDE", "1" if side else "0")
-        torch.manual_seed(0)
-        tr = MLPTrainer(SyntheticMLP(width=512, depth=depth), batch_size=256, n_batches=2, lr=1e-3,
-                        device=torch.device("cuda"))
-        for s in range(4):
-            tr.step(s)
-        tr.join()
-        torch.cuda.synchronize()
-        return tr
-    a, b = run(False), run(True)
-    assert b._wgrad_side and not a._wgrad_side
-    assert torch.equal(a.master_w, b.master_w) and torch.equal(a.params_bf16, b.params_bf16)
-    assert torch.equal(a.m_w, b.m_w) and torch.equal(a.v_w, b.v_w) and torch.equal(a.loss_acc, b.loss_acc)
-
-
-@gpu
 def test_dgrad_colsum_and_head_partials():
     """The bias-gradient partials: the [K, N] dgrad epilogue's per-128-row-tile column sums of its
     bf16 output (colsum), the head's per-64-row-tile sums of g and of dz a, and their one-launch
