@@ -421,7 +421,12 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     const char* e = std::getenv("DGT_F32_MIN_BLOCKS");
     return e && *e ? std::max(1, std::atoi(e)) : 0;
   }();
-  const dgt::GemmF32Plan plan = dgt::gemm_f32_plan(a.M, a.N, a.K, min_blocks);
+  dgt::GemmF32Plan plan = dgt::gemm_f32_plan(a.M, a.N, a.K, min_blocks);
+  static const int big_threads = [] {  // DGT_F32_BIG_THREADS=256|512 (A/B knob, read once)
+    const char* e = std::getenv("DGT_F32_BIG_THREADS");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  if (big_threads == 256 || big_threads == 512) plan.threads = big_threads;
   at::Tensor ws;
   if (plan.splits > 1) {
     ws = at::empty({(int64_t)plan.splits * M * N}, A.options());

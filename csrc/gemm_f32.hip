@@ -50,10 +50,10 @@ typedef float f32x16 __attribute__((ext_vector_type(16)));
 // ReLU mask (MASKED) and writes LDS.  Nothing reads the loaded values until store(), so a tile's
 // loads stay in flight while earlier tiles are consumed, and every path through the loop issues the
 // same number of loads (the compiler's vmcnt accounting then keeps all prefetched tiles in flight).
-template <bool KMAJ, int ROWS, bool VEC, bool MASKED>
+template <bool KMAJ, int ROWS, bool VEC, bool MASKED, int NT>
 struct Tile {
   static constexpr int CHUNKS = ROWS * BK / 4;
-  static constexpr int PER = CHUNKS / 256;  // chunks per thread (256 threads)
+  static constexpr int PER = CHUNKS / NT;  // chunks per thread (NT threads)
   f32x4 v[PER];
   f32x4 m[MASKED ? PER : 1];
   unsigned oob;  // bit 4i+e: element e of chunk i is outside the operand
@@ -75,7 +75,7 @@ struct Tile {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       int r, k;
-      chunk_pos(tid + 256 * i, r, k);
+      chunk_pos(tid + NT * i, r, k);
       const int gr = r0 + r, gk = k0 + k;
       if (VEC) {
         // the contiguous extent is a multiple of 4 here: a chunk is all in or all out
@@ -101,7 +101,7 @@ struct Tile {
   DGT_DEVICE void store(float* lds, int tid) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
-      const int c = tid + 256 * i;
+      const int c = tid + NT * i;
       int off;
       if (!KMAJ) {
         const int r = c / (BK / 4), ch = c % (BK / 4);
@@ -155,13 +155,17 @@ DGT_DEVICE void tile_of(int bid, int nbm, int nbn, int& tm, int& tn) {
 
 // grid.x = tiles, grid.y = split-K slices.  Split slices write raw partial sums to ws[z][M][N]
 // (epilogue in gemm_f32_splitk_reduce); an unsplit launch applies the epilogue itself.
-template <int LA, int LB, int BM, int BN, bool VEC, bool MASKED>
-__global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args a) {
-  constexpr int WM = BM / 2, WN = BN / 2, TM = WM / 32, TN = WN / 32;
+template <int LA, int LB, int BM, int BN, bool VEC, bool MASKED, int NT>
+__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
+  // NT = 256: 4 waves in 2 x 2; NT = 512: 8 waves in 2 x 4 (each wave BM/2 x BN/4: four waves per
+  // SIMD at two blocks per CU, so one wave's staging and barrier wait hide behind three others' MFMAs)
+  constexpr int NW = NT / 64, WCOLS = NW / 2;
+  constexpr int WM = BM / 2, WN = BN / WCOLS, TM = WM / 32, TN = WN / 32;
+  static_assert(TN >= 1 && TM >= 1, "fp32 GEMM wave tile below one 32x32 MFMA");
   constexpr int A_SZ = BM * BK, B_SZ = BN * BK;
   __shared__ __attribute__((aligned(16))) float lds[2][A_SZ + B_SZ];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave >> 1, wn = wave & 1;
+  const int wm = wave / WCOLS, wn = wave % WCOLS;
   const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
   int tm, tn;
   tile_of(blockIdx.x, nbm, nbn, tm, tn);
@@ -184,8 +188,8 @@ __global__ __launch_bounds__(256, 2) void gemm_f32_kernel(GemmF32Args a) {
   // writes tile i + 1 into the stage tile i - 1 was read from, refills its registers with tile
   // i + 1 + P (clamped to the slice: re-reads of the last tile, never consumed), then consumes tile i.
   constexpr int P = BM == 64 ? 3 : 2;
-  Tile<LA == 1, BM, VEC, MASKED> ta[P];
-  Tile<LB == 1, BN, VEC, false> tb[P];
+  Tile<LA == 1, BM, VEC, MASKED, NT> ta[P];
+  Tile<LB == 1, BN, VEC, false, NT> tb[P];
   const int nkt = kt1 - kt0;
   auto load = [&](int p, int i) {
     const int kt = kt0 + min(i, nkt - 1);
@@ -330,28 +334,30 @@ __global__ __launch_bounds__(256) void colsum_f32_final(const float* __restrict_
   db[n] = accumulate ? db[n] + s : s;
 }
 
-template <int LA, int LB, int BM, int BN, bool MASKED>
+template <int LA, int LB, int BM, int BN, bool MASKED, int NT>
 void launch_masked(const GemmF32Args& a, bool vec, const dim3& grid, hipStream_t stream) {
   if (vec)
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true, MASKED>), grid, dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true, MASKED, NT>), grid, dim3(NT), 0, stream, a);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false, MASKED>), grid, dim3(256), 0, stream, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false, MASKED, NT>), grid, dim3(NT), 0, stream, a);
 }
 
-template <int LA, int LB, int BM, int BN>
+template <int LA, int LB, int BM, int BN, int NT>
 hipError_t launch(const GemmF32Args& a, bool vec, int splits, hipStream_t stream) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
   if (a.maskA)
-    launch_masked<LA, LB, BM, BN, true>(a, vec, grid, stream);
+    launch_masked<LA, LB, BM, BN, true, NT>(a, vec, grid, stream);
   else
-    launch_masked<LA, LB, BM, BN, false>(a, vec, grid, stream);
+    launch_masked<LA, LB, BM, BN, false, NT>(a, vec, grid, stream);
   return hipGetLastError();
 }
 
 template <int LA, int LB>
-hipError_t dispatch(const GemmF32Args& a, bool big, bool vec, int splits, hipStream_t stream) {
-  return big ? launch<LA, LB, 128, 128>(a, vec, splits, stream) : launch<LA, LB, 64, 64>(a, vec, splits, stream);
+hipError_t dispatch(const GemmF32Args& a, const GemmF32Plan& p, bool vec, hipStream_t stream) {
+  if (!p.big) return launch<LA, LB, 64, 64, 256>(a, vec, p.splits, stream);
+  return p.threads == 512 ? launch<LA, LB, 128, 128, 512>(a, vec, p.splits, stream)
+                          : launch<LA, LB, 128, 128, 256>(a, vec, p.splits, stream);
 }
 
 }  // namespace f32g
@@ -369,6 +375,7 @@ GemmF32Plan gemm_f32_plan(int M, int N, int K, int min_blocks) {
   // measured faster in the fp32 engine step even where a hot repeat of one product is not
   // (profiles/r4_gemm_f32_split_ab.txt); partial sums are combined in slice order (deterministic)
   if (min_blocks <= 0) min_blocks = p.big ? 512 : 1024;
+  p.threads = 512;
   while (tiles * p.splits < min_blocks && ktiles / (2 * p.splits) >= 8 && p.splits < 16) p.splits *= 2;
   return p;
 }
@@ -384,10 +391,10 @@ hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& p, 
   hipError_t e;
   const int code = la * 2 + lb;
   switch (code) {
-    case 0: e = f32g::dispatch<0, 0>(a, p.big, vec, p.splits, stream); break;
-    case 1: e = f32g::dispatch<0, 1>(a, p.big, vec, p.splits, stream); break;
-    case 3: e = f32g::dispatch<1, 1>(a, p.big, vec, p.splits, stream); break;
-    default: e = f32g::dispatch<1, 0>(a, p.big, vec, p.splits, stream); break;
+    case 0: e = f32g::dispatch<0, 0>(a, p, vec, stream); break;
+    case 1: e = f32g::dispatch<0, 1>(a, p, vec, stream); break;
+    case 3: e = f32g::dispatch<1, 1>(a, p, vec, stream); break;
+    default: e = f32g::dispatch<1, 0>(a, p, vec, stream); break;
   }
   if (e != hipSuccess || p.splits == 1) return e;
   const long long total = (long long)a.M * a.N;
