@@ -31,6 +31,7 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from ..models.synthetic_mlp import SyntheticMLP
 from . import _ext
 
 # > 0 while the engine runs a backward (Engine.backward / the graphed step): only then do the
@@ -292,6 +293,35 @@ class FusedChain(nn.Sequential):
         return super().forward(x)
 
 
+class FusedSyntheticMLP(SyntheticMLP):
+    """``SyntheticMLP`` (``layers`` each followed by ReLU, then ``head``; its ReLU is a
+    ``torch.relu`` call in ``forward``, not a module, so the Sequential folding above cannot see it)
+    as one ``_FusedChainFn``: the ReLUs go into the GEMM epilogues and the dgrads' staging masks,
+    and the whole model is one autograd node.  Installed by swapping the instance's class (same
+    children, keys and parameters); inputs the chain cannot take run layer
+    by layer (the layers are ``FusedLinear(relu=True)``, so no second ReLU is applied)."""
+
+    def forward(self, x):
+        layers = list(self.layers) + [self.head]
+        if x.dim() == 2 and all(isinstance(m, FusedLinear) and _fusable(x, m.weight, m.bias) for m in layers):
+            wb = []
+            for m in layers:
+                wb.append(m.weight)
+                wb.append(m.bias)
+            return _FusedChainFn.apply(x.contiguous(), tuple(m.relu for m in layers), layers[0].grad_in_place, *wb)
+        for m in self.layers:
+            x = m(x)
+        return self.head(x)
+
+
+def _fuse_synthetic_mlp(module: nn.Module, grad_in_place: bool) -> int:
+    for i, lin in enumerate(module.layers):
+        module.layers[i] = FusedLinear.from_linear(lin, relu=True, grad_in_place=grad_in_place)
+    module.head = FusedLinear.from_linear(module.head, grad_in_place=grad_in_place)
+    module.__class__ = FusedSyntheticMLP
+    return len(module.layers) + 1
+
+
 def inject_fused_linear(module: nn.Module, grad_in_place: bool = False) -> int:
     """Replace nn.Linear (+ a directly following nn.ReLU inside an nn.Sequential) in place,
     recursively; ``module`` itself may be the Sequential.  A plain ``nn.Sequential`` left holding
@@ -304,6 +334,9 @@ def inject_fused_linear(module: nn.Module, grad_in_place: bool = False) -> int:
     if p is not None and p.dtype == torch.bfloat16:
         from .mfma_linear import inject_mfma_linear
         return inject_mfma_linear(module, grad_in_place)
+    if type(module) is SyntheticMLP and all(type(m) is nn.Linear for m in module.layers) \
+            and type(module.head) is nn.Linear:
+        return _fuse_synthetic_mlp(module, grad_in_place)
     n = 0
     if isinstance(module, nn.Sequential):
         kids = list(module.children())

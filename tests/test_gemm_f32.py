@@ -147,8 +147,10 @@ def test_fused_linear_tiled_matches_nn_linear(M, K, N, relu):
 
 def test_engine_fp32_mlp_runs_no_vendor_gemm():
     """The DeepSpeed-style engine on a fp32 SyntheticMLP(1024, 4) at batch 1024 with kernel
-    injection: every Linear runs a hand-written kernel (no F.linear fallback), and the first steps
-    match the same model trained by plain PyTorch fp32 + torch Adam."""
+    injection: the model runs as ONE fused chain node (ReLUs in the GEMM epilogues and the dgrad
+    masks, not torch's clamp / threshold kernels), every Linear on a hand-written kernel (no
+    F.linear fallback), and the first steps match the same model trained by plain PyTorch fp32 +
+    torch Adam."""
     import copy
     from distributed_gpu_test_amd import initialize
     from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP, synthetic_batch_data
@@ -167,7 +169,9 @@ def test_engine_fp32_mlp_runs_no_vendor_gemm():
     x, y = x.cuda(), y.cuda()
     crit = torch.nn.BCEWithLogitsLoss()
     for step in range(3):
-        loss = crit(engine(x).view(-1), y)
+        out = engine(x)
+        assert type(out.grad_fn).__name__ == "_FusedChainFnBackward", type(out.grad_fn).__name__
+        loss = crit(out.view(-1), y)
         engine.backward(loss)
         rl = crit(ref(x).view(-1), y)
         opt.zero_grad()
