@@ -427,6 +427,11 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     return e && *e ? std::atoi(e) : 0;
   }();
   if (big_threads == 256 || big_threads == 512) plan.threads = big_threads;
+  static const int small_kg = [] {  // DGT_F32_SMALL_KGROUPS=1|2 (A/B knob, read once)
+    const char* e = std::getenv("DGT_F32_SMALL_KGROUPS");
+    return e && *e ? std::atoi(e) : 0;
+  }();
+  if (small_kg == 1 || small_kg == 2) plan.kgroups = small_kg;
   at::Tensor ws;
   if (plan.splits > 1) {
     ws = at::empty({(int64_t)plan.splits * M * N}, A.options());

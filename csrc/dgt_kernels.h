@@ -115,6 +115,7 @@ struct GemmF32Plan {
   bool big;     // 128x128 block tile (else 64x64)
   int splits;   // split-K slices (1 = none)
   int threads;  // 128x128 blocks: 512 (8 waves of 64 x 32) or 256 (4 waves of 64 x 64)
+  int kgroups;  // 64x64 blocks: 2 (8 waves, two k groups summed in LDS) or 1 (4 waves)
 };
 // min_blocks: split K until the grid holds at least this many blocks (0 = auto: 2 blocks per CU for
 // 128x128 tiles, 4 for 64x64)

@@ -155,16 +155,21 @@ DGT_DEVICE void tile_of(int bid, int nbm, int nbn, int& tm, int& tn) {
 
 // grid.x = tiles, grid.y = split-K slices.  Split slices write raw partial sums to ws[z][M][N]
 // (epilogue in gemm_f32_splitk_reduce); an unsplit launch applies the epilogue itself.
-template <int LA, int LB, int BM, int BN, bool VEC, bool MASKED, int NT>
+template <int LA, int LB, int BM, int BN, bool VEC, bool MASKED, int NT, int KG = 1>
 __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
   // NT = 256: 4 waves in 2 x 2; NT = 512: 8 waves in 2 x 4 (each wave BM/2 x BN/4: four waves per
-  // SIMD at two blocks per CU, so one wave's staging and barrier wait hide behind three others' MFMAs)
-  constexpr int NW = NT / 64, WCOLS = NW / 2;
+  // SIMD at two blocks per CU, so one wave's staging and barrier wait hide behind three others' MFMAs).
+  // KG = 2 (the 64 x 64 tile at NT = 512): two groups of 4 waves in 2 x 2 share each K-tile, group g
+  // taking its k groups 2g, 2g + 1; group 1's sums are added to group 0's through LDS at the end
+  // (the 64 x 64 tile has only four 32 x 32 MFMA tiles, so more waves need a split of K, and inside
+  // the block it costs 16 KiB of LDS traffic instead of a partial-sum pass through memory)
+  static_assert(KG == 1 || KG == 2, "one or two k groups per block");
+  constexpr int NW = NT / 64 / KG, WCOLS = NW / 2;
   constexpr int WM = BM / 2, WN = BN / WCOLS, TM = WM / 32, TN = WN / 32;
   static_assert(TN >= 1 && TM >= 1, "fp32 GEMM wave tile below one 32x32 MFMA");
   constexpr int A_SZ = BM * BK, B_SZ = BN * BK;
   __shared__ __attribute__((aligned(16))) float lds[2][A_SZ + B_SZ];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) % NW, kg = (tid >> 6) / NW;
   const int wm = wave / WCOLS, wn = wave % WCOLS;
   const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
   int tm, tn;
@@ -213,17 +218,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[d][j] = frag<LB == 1, BN>(lb, wn * WN + 32 * j, g, lane);
     };
-    read(0, 0);
+    constexpr int GPK = BK / 8 / KG;  // k groups per wave group
+    const int g0 = kg * GPK;
+    read(g0, 0);
 #pragma unroll
-    for (int g = 0; g < BK / 8; ++g) {
-      if (g + 1 < BK / 8) read(g + 1, (g + 1) & 1);
+    for (int gi = 0; gi < GPK; ++gi) {
+      if (gi + 1 < GPK) read(g0 + gi + 1, (gi + 1) & 1);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int i = 0; i < TM; ++i)
 #pragma unroll
           for (int j = 0; j < TN; ++j)
-            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[g & 1][i][s], fb[g & 1][j][s], acc[i][j], 0, 0, 0);
+            acc[i][j] = __builtin_amdgcn_mfma_f32_32x32x2f32(fa[gi & 1][i][s], fb[gi & 1][j][s], acc[i][j], 0, 0, 0);
     }
   };
   // (the loop sits inside the nkt > 0 branch: a path into the loop header that skipped the prologue
@@ -255,6 +262,28 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
     }
   }
 
+  if constexpr (KG == 2) {
+    // group 1's sums into group 0's through the (now idle) operand LDS: lane-contiguous, conflict-free
+    static_assert(NW * TM * TN * 16 * 64 <= 2 * (A_SZ + B_SZ), "k-group exchange fits the operand LDS");
+    float* xs = &lds[0][0];
+    if (nkt <= 0) __syncthreads();  // (with K-tiles the loop's last barrier already passed every read)
+    if (kg == 1) {
+#pragma unroll
+      for (int i = 0; i < TM; ++i)
+#pragma unroll
+        for (int j = 0; j < TN; ++j)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) xs[(((wave * TM + i) * TN + j) * 16 + e) * 64 + lane] = acc[i][j][e];
+    }
+    __syncthreads();
+    if (kg == 1) return;
+#pragma unroll
+    for (int i = 0; i < TM; ++i)
+#pragma unroll
+      for (int j = 0; j < TN; ++j)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[i][j][e] += xs[(((wave * TM + i) * TN + j) * 16 + e) * 64 + lane];
+  }
   // epilogue: 32x32 accumulator layout col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
   const bool split = gridDim.y > 1;
   float* out = split ? a.ws + (long long)blockIdx.y * a.M * a.N : a.C;
@@ -283,7 +312,34 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
   }
 }
 
-// C = epi(sum over z of ws[z]) in slice order (deterministic), 4 elements per thread.
+// C = epi(sum over z of ws[z]) in slice order (deterministic), 4 consecutive elements of one row per
+// thread with 16-byte accesses (N and ldc multiples of 4, C 16-byte aligned): every slice's load is in
+// flight before the sum, one row / column split per thread instead of a 64-bit division per element
+// (the scalar form below ran at ~2.5 TB/s, 13 launches = 105 us of the fp32 engine MLP step).
+// Bitwise the scalar form: the same left-to-right slice order from 0.
+template <int SPLITS>
+__global__ __launch_bounds__(256) void gemm_f32_splitk_reduce4(GemmF32Args a) {
+  const long long total = (long long)a.M * a.N;
+  const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= total) return;
+  const int m = (int)(i0 / a.N), n = (int)(i0 - (long long)m * a.N);
+  f32x4 w[SPLITS];
+#pragma unroll
+  for (int z = 0; z < SPLITS; ++z) w[z] = *reinterpret_cast<const f32x4*>(a.ws + (long long)z * total + i0);
+  f32x4 v = {0.f, 0.f, 0.f, 0.f};  // from +0, as the scalar form (a -0 partial sums to +0 alike)
+#pragma unroll
+  for (int z = 0; z < SPLITS; ++z) v += w[z];
+  if (a.bias) v += *reinterpret_cast<const f32x4*>(a.bias + n);
+  if (a.relu) {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+  }
+  f32x4* dst = reinterpret_cast<f32x4*>(a.C + (long long)m * a.ldc + n);
+  if (a.accumulate) v += *dst;
+  *dst = v;
+}
+
+// scalar form: any N / ldc / alignment
 __global__ __launch_bounds__(256) void gemm_f32_splitk_reduce(GemmF32Args a, int splits) {
   const long long total = (long long)a.M * a.N;
   const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
@@ -314,6 +370,9 @@ __global__ __launch_bounds__(256) void colsum_f32_partial(const float* __restric
   const int r0 = blockIdx.y * rows_per, r1 = min(M, r0 + rows_per);
   float s = 0.f;
   if (n < N) {
+    // unrolled so eight rows' loads are in flight before their (in-order) adds: one dependent
+    // memory round trip per row made this kernel latency-bound (~7 us for 8 MB)
+#pragma unroll 8
     for (int m = r0 + rl; m < r1; m += 4) {
       const long long off = (long long)m * N + n;
       const float d = dy[off];
@@ -334,28 +393,31 @@ __global__ __launch_bounds__(256) void colsum_f32_final(const float* __restrict_
   db[n] = accumulate ? db[n] + s : s;
 }
 
-template <int LA, int LB, int BM, int BN, bool MASKED, int NT>
+template <int LA, int LB, int BM, int BN, bool MASKED, int NT, int KG>
 void launch_masked(const GemmF32Args& a, bool vec, const dim3& grid, hipStream_t stream) {
   if (vec)
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true, MASKED, NT>), grid, dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true, MASKED, NT, KG>), grid, dim3(NT), 0, stream, a);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false, MASKED, NT>), grid, dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false, MASKED, NT, KG>), grid, dim3(NT), 0, stream, a);
 }
 
-template <int LA, int LB, int BM, int BN, int NT>
+template <int LA, int LB, int BM, int BN, int NT, int KG = 1>
 hipError_t launch(const GemmF32Args& a, bool vec, int splits, hipStream_t stream) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
   if (a.maskA)
-    launch_masked<LA, LB, BM, BN, true, NT>(a, vec, grid, stream);
+    launch_masked<LA, LB, BM, BN, true, NT, KG>(a, vec, grid, stream);
   else
-    launch_masked<LA, LB, BM, BN, false, NT>(a, vec, grid, stream);
+    launch_masked<LA, LB, BM, BN, false, NT, KG>(a, vec, grid, stream);
   return hipGetLastError();
 }
 
 template <int LA, int LB>
 hipError_t dispatch(const GemmF32Args& a, const GemmF32Plan& p, bool vec, hipStream_t stream) {
-  if (!p.big) return launch<LA, LB, 64, 64, 256>(a, vec, p.splits, stream);
+  if (!p.big) {
+    return p.kgroups == 2 ? launch<LA, LB, 64, 64, 512, 2>(a, vec, p.splits, stream)
+                          : launch<LA, LB, 64, 64, 256>(a, vec, p.splits, stream);
+  }
   return p.threads == 512 ? launch<LA, LB, 128, 128, 512>(a, vec, p.splits, stream)
                           : launch<LA, LB, 128, 128, 256>(a, vec, p.splits, stream);
 }
@@ -376,6 +438,7 @@ GemmF32Plan gemm_f32_plan(int M, int N, int K, int min_blocks) {
   // (profiles/r4_gemm_f32_split_ab.txt); partial sums are combined in slice order (deterministic)
   if (min_blocks <= 0) min_blocks = p.big ? 512 : 1024;
   p.threads = 512;
+  p.kgroups = 2;
   while (tiles * p.splits < min_blocks && ktiles / (2 * p.splits) >= 8 && p.splits < 16) p.splits *= 2;
   return p;
 }
@@ -398,8 +461,16 @@ hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& p, 
   }
   if (e != hipSuccess || p.splits == 1) return e;
   const long long total = (long long)a.M * a.N;
-  hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce, dim3((unsigned)((total + 1023) / 1024)), dim3(256), 0, stream, a,
-                     p.splits);
+  const dim3 grid((unsigned)((total + 1023) / 1024));
+  const bool v4 = a.N % 4 == 0 && a.ldc % 4 == 0 && (uintptr_t)a.C % 16 == 0 && (uintptr_t)a.ws % 16 == 0 &&
+                  (a.bias == nullptr || (uintptr_t)a.bias % 16 == 0);
+  switch (v4 ? p.splits : 0) {
+    case 2: hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce4<2>, grid, dim3(256), 0, stream, a); break;
+    case 4: hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce4<4>, grid, dim3(256), 0, stream, a); break;
+    case 8: hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce4<8>, grid, dim3(256), 0, stream, a); break;
+    case 16: hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce4<16>, grid, dim3(256), 0, stream, a); break;
+    default: hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce, grid, dim3(256), 0, stream, a, p.splits);
+  }
   return hipGetLastError();
 }
 
