@@ -280,6 +280,32 @@ def test_inject_fused_linear_keeps_parameters_and_falls_back_on_cpu():
     torch.testing.assert_close(nested(x20), nested_ref(x20))
 
 
+def test_inject_fused_linear_fuses_synthetic_mlp_relus():
+    """SyntheticMLP applies its ReLUs with torch.relu in forward (no ReLU modules to fold): the fp32
+    injection swaps in FusedSyntheticMLP, whose layers carry relu=True and whose head does not -- the
+    same Parameter objects and state_dict keys, still a SyntheticMLP, the same outputs and gradients
+    on the CPU fallback, and a second injection changes nothing."""
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.ops.linear import FusedLinear, FusedSyntheticMLP, inject_fused_linear
+    torch.manual_seed(0)
+    m = SyntheticMLP(32, 3)
+    ref = copy.deepcopy(m)
+    params, keys = [id(p) for p in m.parameters()], list(m.state_dict().keys())
+    assert inject_fused_linear(m) == 4
+    assert type(m) is FusedSyntheticMLP and isinstance(m, SyntheticMLP)
+    assert [id(p) for p in m.parameters()] == params and list(m.state_dict().keys()) == keys
+    assert all(isinstance(l, FusedLinear) and l.relu for l in m.layers)
+    assert isinstance(m.head, FusedLinear) and not m.head.relu
+    x = torch.randn(6, 32)
+    out, want = m(x), ref(x)
+    torch.testing.assert_close(out, want)
+    out.sum().backward()
+    want.sum().backward()
+    for p, q in zip(m.parameters(), ref.parameters()):
+        torch.testing.assert_close(p.grad, q.grad)
+    assert inject_fused_linear(m) == 0 and type(m) is FusedSyntheticMLP
+
+
 class _ScaleGradInPlace(torch.autograd.Function):
     """A user Function whose backward edits grad_output IN PLACE (legal autograd code)."""
 
