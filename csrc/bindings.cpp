@@ -374,7 +374,7 @@ void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, 
 // B [N, K] (lb 0) or [K, N] (lb 1), all contiguous; split-K partials in a caching-allocator workspace.
 void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& maskA,
               const std::optional<at::Tensor>& bias, const at::Tensor& C, int64_t la, int64_t lb, bool relu,
-              bool accumulate) {
+              bool accumulate, const std::optional<at::Tensor>& rowsum) {
   check_gpu(A, "A", at::kFloat);
   check_gpu(B, "B", at::kFloat);
   check_gpu(C, "C", at::kFloat);
@@ -399,6 +399,11 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     a.bias = bias->data_ptr<float>();
   }
   a.C = C.data_ptr<float>();
+  if (rowsum.has_value() && rowsum->defined()) {
+    check_gpu(*rowsum, "rowsum", at::kFloat);
+    TORCH_CHECK(rowsum->numel() == M && rowsum->is_contiguous(), "dgt: gemm_f32 rowsum must have M elements");
+    a.rowsum = rowsum->data_ptr<float>();
+  }
   a.M = (int)M;
   a.N = (int)N;
   a.K = (int)K;
@@ -414,6 +419,7 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     if (a.bias) z.add_(*bias);
     if (relu) z.clamp_min_(0.f);
     if (accumulate) C.add_(z); else C.copy_(z);
+    if (a.rowsum && !accumulate) rowsum->zero_();
     return;
   }
   // DGT_F32_MIN_BLOCKS (A/B knob, read once): the grid size split-K fills small products up to
@@ -427,14 +433,9 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     return e && *e ? std::atoi(e) : 0;
   }();
   if (big_threads == 256 || big_threads == 512) plan.threads = big_threads;
-  static const int small_kg = [] {  // DGT_F32_SMALL_KGROUPS=1|2 (A/B knob, read once)
-    const char* e = std::getenv("DGT_F32_SMALL_KGROUPS");
-    return e && *e ? std::atoi(e) : 0;
-  }();
-  if (small_kg == 1 || small_kg == 2) plan.kgroups = small_kg;
   at::Tensor ws;
   if (plan.splits > 1) {
-    ws = at::empty({(int64_t)plan.splits * M * N}, A.options());
+    ws = at::empty({(int64_t)plan.splits * M * N + (a.rowsum ? (int64_t)plan.splits * M : 0)}, A.options());
     a.ws = ws.data_ptr<float>();
   }
   DGT_CHECK_HIP(dgt::gemm_f32(a, (int)la, (int)lb, plan, stream_of(A)));
@@ -1021,7 +1022,7 @@ TORCH_LIBRARY(dgt, m) {
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz) -> ()", &bce_logits);
   m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
   m.def("gemm_f32(Tensor A, Tensor B, Tensor? maskA, Tensor? bias, Tensor(a!) C, int la, int lb, bool relu=False, "
-        "bool accumulate=False) -> ()",
+        "bool accumulate=False, Tensor(b!)? rowsum=None) -> ()",
         &gemm_f32);
   m.def("colsum_f32(Tensor dy, Tensor? y, Tensor(a!) db, bool accumulate=False) -> ()", &colsum_f32);
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor W, Tensor? y, Tensor(a!)? dx, Tensor(b!) dW, Tensor(c!)? db, "

@@ -105,20 +105,21 @@ struct GemmF32Args {
   const float* maskA;
   const float* bias;
   float* C;
-  float* ws;  // split-K partials, splits * M * N floats (plan.splits > 1 only)
+  float* ws;  // split-K partials, splits * M * N floats (plan.splits > 1 only) [+ splits * M row sums]
   int M, N, K;
   long long lda, ldb, ldc;
   int relu;
   int accumulate;
+  // optional: rowsum[m] (+)= sum_k A'(m, k), A' = A after the mask (the wgrad's bias gradient,
+  // sum over the batch of g = dy * 1[y > 0]); (+)= follows `accumulate`
+  float* rowsum;
 };
 struct GemmF32Plan {
   bool big;     // 128x128 block tile (else 64x64)
   int splits;   // split-K slices (1 = none)
   int threads;  // 128x128 blocks: 512 (8 waves of 64 x 32) or 256 (4 waves of 64 x 64)
-  int kgroups;  // 64x64 blocks: 2 (8 waves, two k groups summed in LDS) or 1 (4 waves)
 };
-// min_blocks: split K until the grid holds at least this many blocks (0 = auto: 2 blocks per CU for
-// 128x128 tiles, 4 for 64x64)
+// min_blocks: split K until the grid holds at least this many blocks (0 = auto: 2 blocks per CU)
 GemmF32Plan gemm_f32_plan(int M, int N, int K, int min_blocks = 0);
 hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& plan, hipStream_t stream);
 // db[n] (+)= sum_m dy[m][n] * (y ? 1[y[m][n] > 0] : 1) over row slices (part: slices * N floats)

@@ -98,7 +98,9 @@ struct Tile {
     }
   }
 
-  DGT_DEVICE void store(float* lds, int tid) const {
+  // rs (optional): per-chunk running sums of the stored values by operand row -- 4 rows of one k
+  // (KMAJ) or one row's 4 k (MK); a thread's chunks sit at the same rows in every K-tile
+  DGT_DEVICE void store(float* lds, int tid, f32x4* rs = nullptr) const {
 #pragma unroll
     for (int i = 0; i < PER; ++i) {
       const int c = tid + NT * i;
@@ -121,6 +123,7 @@ struct Tile {
         }
       }
       *reinterpret_cast<f32x4*>(lds + off) = x;
+      if (rs) rs[i] += x;
     }
   }
 };
@@ -155,21 +158,18 @@ DGT_DEVICE void tile_of(int bid, int nbm, int nbn, int& tm, int& tn) {
 
 // grid.x = tiles, grid.y = split-K slices.  Split slices write raw partial sums to ws[z][M][N]
 // (epilogue in gemm_f32_splitk_reduce); an unsplit launch applies the epilogue itself.
-template <int LA, int LB, int BM, int BN, bool VEC, bool MASKED, int NT, int KG = 1>
+template <int LA, int LB, int BM, int BN, bool VEC, bool MASKED, int NT>
 __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
   // NT = 256: 4 waves in 2 x 2; NT = 512: 8 waves in 2 x 4 (each wave BM/2 x BN/4: four waves per
   // SIMD at two blocks per CU, so one wave's staging and barrier wait hide behind three others' MFMAs).
-  // KG = 2 (the 64 x 64 tile at NT = 512): two groups of 4 waves in 2 x 2 share each K-tile, group g
-  // taking its k groups 2g, 2g + 1; group 1's sums are added to group 0's through LDS at the end
-  // (the 64 x 64 tile has only four 32 x 32 MFMA tiles, so more waves need a split of K, and inside
-  // the block it costs 16 KiB of LDS traffic instead of a partial-sum pass through memory)
-  static_assert(KG == 1 || KG == 2, "one or two k groups per block");
-  constexpr int NW = NT / 64 / KG, WCOLS = NW / 2;
+  // (A form with two in-block k groups for the 64 x 64 tile, summed through LDS, gave wrong input
+  // gradients inside the fp32 engine chain while passing the isolated product tests: removed.)
+  constexpr int NW = NT / 64, WCOLS = NW / 2;
   constexpr int WM = BM / 2, WN = BN / WCOLS, TM = WM / 32, TN = WN / 32;
   static_assert(TN >= 1 && TM >= 1, "fp32 GEMM wave tile below one 32x32 MFMA");
   constexpr int A_SZ = BM * BK, B_SZ = BN * BK;
   __shared__ __attribute__((aligned(16))) float lds[2][A_SZ + B_SZ];
-  const int tid = threadIdx.x, lane = tid & 63, wave = (tid >> 6) % NW, kg = (tid >> 6) / NW;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WCOLS, wn = wave % WCOLS;
   const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
   int tm, tn;
@@ -201,8 +201,15 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
     ta[p].load(a.A, a.maskA, a.lda, m0, kt * BK, a.M, a.K, tid);
     tb[p].load(a.B, nullptr, a.ldb, n0, kt * BK, a.N, a.K, tid);
   };
-  auto stage = [&](int p, int buf) {
-    ta[p].store(lds[buf], tid);
+  // fused row sums of the masked A (the bias gradient): the blocks of the first column tile add
+  // every K-tile they stage (tiles staged past the slice's end are clamped re-reads: skipped)
+  const bool rs_on = a.rowsum != nullptr && tn == 0;
+  constexpr int APER = Tile<LA == 1, BM, VEC, MASKED, NT>::PER;
+  f32x4 rsum[APER];
+#pragma unroll
+  for (int i = 0; i < APER; ++i) rsum[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto stage = [&](int p, int buf, bool counted = false) {
+    ta[p].store(lds[buf], tid, counted && rs_on ? rsum : nullptr);
     tb[p].store(lds[buf] + A_SZ, tid);
   };
   // the k groups' fragments are read one group ahead: group g + 1's LDS reads are in flight while
@@ -218,12 +225,11 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
 #pragma unroll
       for (int j = 0; j < TN; ++j) fb[d][j] = frag<LB == 1, BN>(lb, wn * WN + 32 * j, g, lane);
     };
-    constexpr int GPK = BK / 8 / KG;  // k groups per wave group
-    const int g0 = kg * GPK;
-    read(g0, 0);
+    constexpr int GPK = BK / 8;  // k groups of the K-tile
+    read(0, 0);
 #pragma unroll
     for (int gi = 0; gi < GPK; ++gi) {
-      if (gi + 1 < GPK) read(g0 + gi + 1, (gi + 1) & 1);
+      if (gi + 1 < GPK) read(gi + 1, (gi + 1) & 1);
 #pragma unroll
       for (int s = 0; s < 4; ++s)
 #pragma unroll
@@ -243,7 +249,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
       load(p, p);
       __builtin_amdgcn_sched_barrier(0);
     }
-    stage(0, 0);
+    stage(0, 0, true);
     load(0, P);
     __builtin_amdgcn_sched_barrier(0);
     __syncthreads();
@@ -254,7 +260,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
       for (int d = 0; d < P; ++d) {
         const int i = i0 + d;
         const int nx = (d + 1) % P;  // static after the unroll
-        stage(nx, (i + 1) & 1);
+        stage(nx, (i + 1) & 1, i + 1 < nkt);
         load(nx, i + 1 + P);
         if (i < nkt) consume(i & 1);
         __syncthreads();
@@ -262,27 +268,39 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
     }
   }
 
-  if constexpr (KG == 2) {
-    // group 1's sums into group 0's through the (now idle) operand LDS: lane-contiguous, conflict-free
-    static_assert(NW * TM * TN * 16 * 64 <= 2 * (A_SZ + B_SZ), "k-group exchange fits the operand LDS");
-    float* xs = &lds[0][0];
-    if (nkt <= 0) __syncthreads();  // (with K-tiles the loop's last barrier already passed every read)
-    if (kg == 1) {
+  if (a.rowsum != nullptr && tn == 0) {
+    // the block's row sums: each thread's per-chunk sums go to the chunk's own LDS slots (the staging
+    // image: [k][rows] for KMAJ, [row][k] swizzled for MK), then one thread per row adds its BK (KMAJ)
+    // or BK / 4 (MK) slots in k order; slice partials go to ws after the C partials
+    if (nkt <= 0) __syncthreads();
+    float* red = &lds[0][0];
+    constexpr bool AK = LA == 1;
+    using TA = Tile<AK, BM, VEC, MASKED, NT>;
 #pragma unroll
-      for (int i = 0; i < TM; ++i)
-#pragma unroll
-        for (int j = 0; j < TN; ++j)
-#pragma unroll
-          for (int e = 0; e < 16; ++e) xs[(((wave * TM + i) * TN + j) * 16 + e) * 64 + lane] = acc[i][j][e];
+    for (int i = 0; i < TA::PER; ++i) {
+      const int c = tid + NT * i;
+      if (AK) {
+        *reinterpret_cast<f32x4*>(red + c * 4) = rsum[i];
+      } else {
+        red[c] = (rsum[i][0] + rsum[i][1]) + (rsum[i][2] + rsum[i][3]);
+      }
     }
     __syncthreads();
-    if (kg == 1) return;
-#pragma unroll
-    for (int i = 0; i < TM; ++i)
-#pragma unroll
-      for (int j = 0; j < TN; ++j)
-#pragma unroll
-        for (int e = 0; e < 16; ++e) acc[i][j][e] += xs[(((wave * TM + i) * TN + j) * 16 + e) * 64 + lane];
+    if (tid < BM && m0 + tid < a.M) {
+      float t = 0.f;
+      if (AK) {
+        for (int k = 0; k < BK; ++k) t += red[k * BM + tid];
+      } else {
+        for (int q = 0; q < BK / 4; ++q) t += red[tid * (BK / 4) + q];
+      }
+      if (gridDim.y > 1) {
+        a.ws[(long long)gridDim.y * a.M * a.N + (long long)blockIdx.y * a.M + m0 + tid] = t;
+      } else {
+        float* d = a.rowsum + m0 + tid;
+        *d = a.accumulate ? *d + t : t;
+      }
+    }
+    __syncthreads();  // the LDS is reused below
   }
   // epilogue: 32x32 accumulator layout col = lane & 31, row = (e & 3) + 8 (e >> 2) + 4 (lane >> 5)
   const bool split = gridDim.y > 1;
@@ -317,8 +335,19 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
 // flight before the sum, one row / column split per thread instead of a 64-bit division per element
 // (the scalar form below ran at ~2.5 TB/s, 13 launches = 105 us of the fp32 engine MLP step).
 // Bitwise the scalar form: the same left-to-right slice order from 0.
+// rowsum[m] (+)= the slices' row sums in slice order (the fused bias gradient, gemm_f32_kernel)
+DGT_DEVICE void reduce_rowsum(const GemmF32Args& a, int splits) {
+  const long long m = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (a.rowsum == nullptr || m >= a.M) return;
+  const float* p = a.ws + (long long)splits * a.M * a.N + m;
+  float t = 0.f;
+  for (int z = 0; z < splits; ++z) t += p[(long long)z * a.M];
+  a.rowsum[m] = a.accumulate ? a.rowsum[m] + t : t;
+}
+
 template <int SPLITS>
 __global__ __launch_bounds__(256) void gemm_f32_splitk_reduce4(GemmF32Args a) {
+  reduce_rowsum(a, SPLITS);
   const long long total = (long long)a.M * a.N;
   const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i0 >= total) return;
@@ -341,6 +370,7 @@ __global__ __launch_bounds__(256) void gemm_f32_splitk_reduce4(GemmF32Args a) {
 
 // scalar form: any N / ldc / alignment
 __global__ __launch_bounds__(256) void gemm_f32_splitk_reduce(GemmF32Args a, int splits) {
+  reduce_rowsum(a, splits);
   const long long total = (long long)a.M * a.N;
   const long long i0 = ((long long)blockIdx.x * 256 + threadIdx.x) * 4;
   if (i0 >= total) return;
@@ -393,31 +423,28 @@ __global__ __launch_bounds__(256) void colsum_f32_final(const float* __restrict_
   db[n] = accumulate ? db[n] + s : s;
 }
 
-template <int LA, int LB, int BM, int BN, bool MASKED, int NT, int KG>
+template <int LA, int LB, int BM, int BN, bool MASKED, int NT>
 void launch_masked(const GemmF32Args& a, bool vec, const dim3& grid, hipStream_t stream) {
   if (vec)
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true, MASKED, NT, KG>), grid, dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, true, MASKED, NT>), grid, dim3(NT), 0, stream, a);
   else
-    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false, MASKED, NT, KG>), grid, dim3(NT), 0, stream, a);
+    hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, BM, BN, false, MASKED, NT>), grid, dim3(NT), 0, stream, a);
 }
 
-template <int LA, int LB, int BM, int BN, int NT, int KG = 1>
+template <int LA, int LB, int BM, int BN, int NT>
 hipError_t launch(const GemmF32Args& a, bool vec, int splits, hipStream_t stream) {
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const dim3 grid((unsigned)tiles, (unsigned)splits);
   if (a.maskA)
-    launch_masked<LA, LB, BM, BN, true, NT, KG>(a, vec, grid, stream);
+    launch_masked<LA, LB, BM, BN, true, NT>(a, vec, grid, stream);
   else
-    launch_masked<LA, LB, BM, BN, false, NT, KG>(a, vec, grid, stream);
+    launch_masked<LA, LB, BM, BN, false, NT>(a, vec, grid, stream);
   return hipGetLastError();
 }
 
 template <int LA, int LB>
 hipError_t dispatch(const GemmF32Args& a, const GemmF32Plan& p, bool vec, hipStream_t stream) {
-  if (!p.big) {
-    return p.kgroups == 2 ? launch<LA, LB, 64, 64, 512, 2>(a, vec, p.splits, stream)
-                          : launch<LA, LB, 64, 64, 256>(a, vec, p.splits, stream);
-  }
+  if (!p.big) return launch<LA, LB, 64, 64, 256>(a, vec, p.splits, stream);
   return p.threads == 512 ? launch<LA, LB, 128, 128, 512>(a, vec, p.splits, stream)
                           : launch<LA, LB, 128, 128, 256>(a, vec, p.splits, stream);
 }
@@ -433,12 +460,12 @@ GemmF32Plan gemm_f32_plan(int M, int N, int K, int min_blocks) {
   const int ktiles = (K + f32g::BK - 1) / f32g::BK;
   p.splits = 1;
   // small grid, long K (e.g. a wgrad whose reduction runs over a large batch): split K so the
-  // launch covers the chip with 2 (128x128) or 4 (64x64) blocks per CU -- more blocks in flight
-  // measured faster in the fp32 engine step even where a hot repeat of one product is not
-  // (profiles/r4_gemm_f32_split_ab.txt); partial sums are combined in slice order (deterministic)
-  if (min_blocks <= 0) min_blocks = p.big ? 512 : 1024;
+  // launch covers the chip with 2 blocks per CU -- more blocks in flight measured faster in the fp32
+  // engine step even where a hot repeat of one product is not, and 2 beat 1 and 4 for the 64x64
+  // tiles once the reduce was vectorised (profiles/r4_gemm_f32_split_ab.txt); partial sums are
+  // combined in slice order (deterministic)
+  if (min_blocks <= 0) min_blocks = 512;
   p.threads = 512;
-  p.kgroups = 2;
   while (tiles * p.splits < min_blocks && ktiles / (2 * p.splits) >= 8 && p.splits < 16) p.splits *= 2;
   return p;
 }
@@ -461,7 +488,8 @@ hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& p, 
   }
   if (e != hipSuccess || p.splits == 1) return e;
   const long long total = (long long)a.M * a.N;
-  const dim3 grid((unsigned)((total + 1023) / 1024));
+  // (the row sums take one thread per row of C: enough blocks for M rows when N < 4)
+  const dim3 grid((unsigned)std::max((total + 1023) / 1024, a.rowsum ? ((long long)a.M + 255) / 256 : 0LL));
   const bool v4 = a.N % 4 == 0 && a.ldc % 4 == 0 && (uintptr_t)a.C % 16 == 0 && (uintptr_t)a.ws % 16 == 0 &&
                   (a.bias == nullptr || (uintptr_t)a.bias % 16 == 0);
   switch (v4 ? p.splits : 0) {

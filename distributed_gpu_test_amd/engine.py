@@ -490,8 +490,13 @@ class Engine:
         if seed is None or seed.device != loss.device:
             seed = self._seed_one = torch.ones((), dtype=torch.float32, device=loss.device)
         with torch.no_grad():  # autograd runs backward functions with grad mode off (no create_graph)
-            g = node.apply(seed)
-            g = g[0] if isinstance(g, tuple) else g
+            if getattr(node, "dtype", None) == torch.float32:
+                # fp32 logits: the BCE backward's product with the unit seed is its saved d loss /
+                # d logits itself (x * 1.0 == x bit for bit): no multiply launch
+                g = node.saved_tensors[0].view(node.shape)
+            else:
+                g = node.apply(seed)
+                g = g[0] if isinstance(g, tuple) else g
             for v in views:  # reshapes / casts back to the chain's output
                 g = v(g)
                 g = g[0] if isinstance(g, tuple) else g

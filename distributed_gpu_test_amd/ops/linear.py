@@ -97,6 +97,7 @@ def count_fallback(reason: str) -> None:
         _WARNED.add(reason)
         print(f"[dgt] WARNING: Linear falls back to F.linear (vendor BLAS): {reason}", file=sys.stderr, flush=True)
 
+_FUSED_ROWSUM = True     # the wgrad forms db (tests / diagnostics switch to the column-sum pass)
 SMALL_M = 256            # rows per call (batch)
 SMALL_WORK = 1 << 22     # M * N * K: beyond this the tiled MFMA GEMM (csrc/gemm_f32.hip) wins
 
@@ -118,15 +119,20 @@ def _fwd(ops, x, weight, bias, relu: bool) -> torch.Tensor:
 def _bwd(ops, dy, x, weight, y, dx, dW, db, accumulate: bool = False) -> None:
     """g = dy * 1[y > 0] (y given: the layer had a ReLU) or dy; dx = g W, dW (+)= g^T x, db (+)= sum_m g.
     Tiled: dgrad A = g [M, N] (k = N contiguous), B = W [N, K] read as [k][n]; wgrad A = g read as
-    [k = M][n], B = x [M, K] read as [k][col]; the mask is applied while g is staged."""
+    [k = M][n], B = x [M, K] read as [k][col]; the mask is applied while g is staged, and the wgrad
+    sums the staged g per row of A for db (no separate column-sum pass over dy and y)."""
     if _small(x, weight):
         ops.linear_bwd(dy, x, weight, y, dx, dW, db, accumulate)
         return
     if dx is not None:
         ops.gemm_f32(dy, weight, y, None, dx, 0, 1, False, False)
-    ops.gemm_f32(dy, x, y, None, dW, 1, 1, False, accumulate)
-    if db is not None:
-        ops.colsum_f32(dy, y, db, accumulate)
+    if _FUSED_ROWSUM:
+        # db = the row sums of the wgrad's masked A (g^T), formed while the GEMM stages it
+        ops.gemm_f32(dy, x, y, None, dW, 1, 1, False, accumulate, db)
+    else:
+        ops.gemm_f32(dy, x, y, None, dW, 1, 1, False, accumulate)
+        if db is not None:
+            ops.colsum_f32(dy, y, db, accumulate)
 
 
 class _FusedLinearFn(torch.autograd.Function):

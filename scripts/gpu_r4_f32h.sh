@@ -4,7 +4,7 @@ set -o pipefail
 O=gpurun_out/r4f8
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest tests/test_gemm_f32.py -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
+timeout -k 10 600 python -u -m pytest tests/test_gemm_f32.py tests/test_gpu_engine.py -x -q --timeout 200 --timeout-method thread > $O/pytest.log 2>&1; rc=$?
 tail -2 $O/pytest.log; [ $rc -eq 0 ] || { grep -E "^(FAILED|ERROR)|Error|assert" $O/pytest.log | head -20; exit $rc; }
 run() {  # kg min_blocks
   DGT_F32_SMALL_KGROUPS=$1 DGT_F32_MIN_BLOCKS=$2 timeout -k 10 300 python bench.py --model mlp --width 1024 --depth 4 --batch 1024 --impl dgt-engine --deepspeed-config configs/ds_bench_mlp_fp32.json --steps 50 --warmup 10 --no-sweep > $O/mlp.json 2> $O/mlp.err || { tail -20 $O/mlp.err; exit 1; }

@@ -53,6 +53,36 @@ SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("la", [0, 1])
+@pytest.mark.parametrize("masked", [False, True])
+@pytest.mark.parametrize("accumulate", [False, True])
+@pytest.mark.parametrize("M,N,K", [(256, 256, 256), (1024, 1024, 1024), (2048, 2048, 512), (1000, 999, 1004),
+                                   (77, 130, 67), (64, 64, 8192), (4096, 1, 1024)])
+def test_gemm_f32_fused_rowsum(M, N, K, la, masked, accumulate):
+    """``rowsum[m] (+)= sum_k A'(m, k)`` formed while the GEMM stages A (A' = A after the ReLU mask):
+    the wgrad's bias gradient without a separate column-sum pass.  Every tile size, the split-K
+    path (slice partials summed by the reduce kernel), the scalar and 16-byte staging, both A
+    layouts; the product itself is unchanged."""
+    ops = _ops()
+    a, b, A, B = _operands(M, N, K, la, 0, seed=M + K)
+    mask = None
+    if masked:
+        m = (torch.randn(M, K, device="cuda") > 0).float()
+        mask = m if la == 0 else m.t().contiguous()
+    C = torch.randn(M, N, device="cuda") if accumulate else torch.empty(M, N, device="cuda")
+    rs = torch.randn(M, device="cuda") if accumulate else torch.full((M,), float("nan"), device="cuda")
+    C0, rs0 = C.clone(), rs.clone()
+    ops.gemm_f32(A, B, mask, None, C, la, 0, False, accumulate, rs)
+    ref = _ref(a, b, mask=m if masked else None)
+    want_rs = (a * (m > 0) if masked else a).double().sum(1)
+    if accumulate:
+        ref, want_rs = ref + C0.double(), want_rs + rs0.double()
+    _close(C, ref, a, b)
+    scale = (a.abs().double().sum(1)).clamp_min(1.0)
+    err = ((rs.double() - want_rs).abs() / scale).max().item()
+    assert err <= 1e-5, err
+
+
 @pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1), (1, 0)])
 @pytest.mark.parametrize("M,N,K", SHAPES)
 def test_gemm_f32_layouts(M, N, K, la, lb):
@@ -178,8 +208,14 @@ def test_engine_fp32_mlp_runs_no_vendor_gemm():
         rl.backward()
         torch.testing.assert_close(loss, rl, rtol=1e-4, atol=1e-5)
         if step == 0:  # the gradients themselves (Adam's first step is ~lr * sign(g): compare before it)
+            # two fp32 summation orders put a few activations near 0 on different sides of the ReLU, so
+            # a handful of mask bits (and the |dy x| terms they gate) differ: compare in norm and
+            # relative to the gradient's scale, not element by element at 1e-6 (the kernels' own
+            # exactness against fp64 is pinned above at 1e-5 normalised)
             for (name, p), q in zip(model.named_parameters(), ref.parameters()):
-                torch.testing.assert_close(p.grad, q.grad, rtol=1e-4, atol=1e-6, msg=lambda m: f"{name}: {m}")
+                rel = float((p.grad - q.grad).norm() / q.grad.norm().clamp_min(1e-30))
+                worst = float((p.grad - q.grad).abs().max() / q.grad.abs().max().clamp_min(1e-30))
+                assert rel < 1e-4 and worst < 2e-3, f"{name}: relative L2 {rel:.2e}, worst {worst:.2e}"
         engine.step()
         opt.step()
     assert engine.linear_fallbacks == before, engine.linear_fallbacks
