@@ -374,7 +374,7 @@ void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, 
 // B [N, K] (lb 0) or [K, N] (lb 1), all contiguous; split-K partials in a caching-allocator workspace.
 void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& maskA,
               const std::optional<at::Tensor>& bias, const at::Tensor& C, int64_t la, int64_t lb, bool relu,
-              bool accumulate, const std::optional<at::Tensor>& rowsum) {
+              bool accumulate, const std::optional<at::Tensor>& rowsum, const std::optional<at::Tensor>& maskC) {
   check_gpu(A, "A", at::kFloat);
   check_gpu(B, "B", at::kFloat);
   check_gpu(C, "C", at::kFloat);
@@ -404,6 +404,11 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     TORCH_CHECK(rowsum->numel() == M && rowsum->is_contiguous(), "dgt: gemm_f32 rowsum must have M elements");
     a.rowsum = rowsum->data_ptr<float>();
   }
+  if (maskC.has_value() && maskC->defined()) {
+    check_gpu(*maskC, "maskC", at::kFloat);
+    TORCH_CHECK(maskC->sizes() == C.sizes() && maskC->is_contiguous(), "dgt: gemm_f32 maskC must be C-shaped, contiguous");
+    a.maskC = maskC->data_ptr<float>();
+  }
   a.M = (int)M;
   a.N = (int)N;
   a.K = (int)K;
@@ -418,6 +423,7 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     at::Tensor z = at::zeros_like(C);
     if (a.bias) z.add_(*bias);
     if (relu) z.clamp_min_(0.f);
+    if (a.maskC) z.mul_(maskC->gt(0.f));
     if (accumulate) C.add_(z); else C.copy_(z);
     if (a.rowsum && !accumulate) rowsum->zero_();
     return;
@@ -1022,7 +1028,7 @@ TORCH_LIBRARY(dgt, m) {
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz) -> ()", &bce_logits);
   m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
   m.def("gemm_f32(Tensor A, Tensor B, Tensor? maskA, Tensor? bias, Tensor(a!) C, int la, int lb, bool relu=False, "
-        "bool accumulate=False, Tensor(b!)? rowsum=None) -> ()",
+        "bool accumulate=False, Tensor(b!)? rowsum=None, Tensor? maskC=None) -> ()",
         &gemm_f32);
   m.def("colsum_f32(Tensor dy, Tensor? y, Tensor(a!) db, bool accumulate=False) -> ()", &colsum_f32);
   m.def("linear_bwd(Tensor dy, Tensor x, Tensor W, Tensor? y, Tensor(a!)? dx, Tensor(b!) dW, Tensor(c!)? db, "

@@ -113,6 +113,9 @@ struct GemmF32Args {
   // optional: rowsum[m] (+)= sum_k A'(m, k), A' = A after the mask (the wgrad's bias gradient,
   // sum over the batch of g = dy * 1[y > 0]); (+)= follows `accumulate`
   float* rowsum;
+  // optional: the product masked by 1[maskC > 0] ([M, N], row stride N) before it is stored or
+  // accumulated -- a dgrad writing the ReLU-masked gradient of the layer below directly
+  const float* maskC;
 };
 struct GemmF32Plan {
   bool big;     // 128x128 block tile (else 64x64)

@@ -322,6 +322,7 @@ __global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
         if (!split) {
           v += bias;
           if (a.relu) v = fmaxf(v, 0.f);
+          if (a.maskC && !(a.maskC[(long long)m * a.N + n] > 0.f)) v = 0.f;
           if (a.accumulate) v += *dst;
         }
         *dst = v;
@@ -363,6 +364,11 @@ __global__ __launch_bounds__(256) void gemm_f32_splitk_reduce4(GemmF32Args a) {
 #pragma unroll
     for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
   }
+  if (a.maskC) {
+    const f32x4 mk = *reinterpret_cast<const f32x4*>(a.maskC + i0);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
+  }
   f32x4* dst = reinterpret_cast<f32x4*>(a.C + (long long)m * a.ldc + n);
   if (a.accumulate) v += *dst;
   *dst = v;
@@ -383,6 +389,7 @@ __global__ __launch_bounds__(256) void gemm_f32_splitk_reduce(GemmF32Args a, int
     const int m = (int)(i / a.N), n = (int)(i % a.N);
     if (a.bias) v += a.bias[n];
     if (a.relu) v = fmaxf(v, 0.f);
+    if (a.maskC && !(a.maskC[i] > 0.f)) v = 0.f;
     float* dst = a.C + (long long)m * a.ldc + n;
     if (a.accumulate) v += *dst;
     *dst = v;
@@ -491,7 +498,8 @@ hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& p, 
   // (the row sums take one thread per row of C: enough blocks for M rows when N < 4)
   const dim3 grid((unsigned)std::max((total + 1023) / 1024, a.rowsum ? ((long long)a.M + 255) / 256 : 0LL));
   const bool v4 = a.N % 4 == 0 && a.ldc % 4 == 0 && (uintptr_t)a.C % 16 == 0 && (uintptr_t)a.ws % 16 == 0 &&
-                  (a.bias == nullptr || (uintptr_t)a.bias % 16 == 0);
+                  (a.bias == nullptr || (uintptr_t)a.bias % 16 == 0) &&
+                  (a.maskC == nullptr || (uintptr_t)a.maskC % 16 == 0);
   switch (v4 ? p.splits : 0) {
     case 2: hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce4<2>, grid, dim3(256), 0, stream, a); break;
     case 4: hipLaunchKernelGGL(f32g::gemm_f32_splitk_reduce4<4>, grid, dim3(256), 0, stream, a); break;

@@ -116,16 +116,19 @@ def _fwd(ops, x, weight, bias, relu: bool) -> torch.Tensor:
     return y
 
 
-def _bwd(ops, dy, x, weight, y, dx, dW, db, accumulate: bool = False) -> None:
+def _bwd(ops, dy, x, weight, y, dx, dW, db, accumulate: bool = False, mask_dx=None) -> bool:
     """g = dy * 1[y > 0] (y given: the layer had a ReLU) or dy; dx = g W, dW (+)= g^T x, db (+)= sum_m g.
     Tiled: dgrad A = g [M, N] (k = N contiguous), B = W [N, K] read as [k][n]; wgrad A = g read as
     [k = M][n], B = x [M, K] read as [k][col]; the mask is applied while g is staged, and the wgrad
-    sums the staged g per row of A for db (no separate column-sum pass over dy and y)."""
+    sums the staged g per row of A for db (no separate column-sum pass over dy and y).
+    ``mask_dx`` (the layer below's ReLU output): the tiled dgrad stores dx * 1[mask_dx > 0], the
+    gradient the layer below needs, so that layer reads no mask.  Returns whether it did (the
+    small-batch kernel does not)."""
     if _small(x, weight):
         ops.linear_bwd(dy, x, weight, y, dx, dW, db, accumulate)
-        return
+        return False
     if dx is not None:
-        ops.gemm_f32(dy, weight, y, None, dx, 0, 1, False, False)
+        ops.gemm_f32(dy, weight, y, None, dx, 0, 1, False, False, None, mask_dx)
     if _FUSED_ROWSUM:
         # db = the row sums of the wgrad's masked A (g^T), formed while the GEMM stages it
         ops.gemm_f32(dy, x, y, None, dW, 1, 1, False, accumulate, db)
@@ -133,6 +136,7 @@ def _bwd(ops, dy, x, weight, y, dx, dW, db, accumulate: bool = False) -> None:
         ops.gemm_f32(dy, x, y, None, dW, 1, 1, False, accumulate)
         if db is not None:
             ops.colsum_f32(dy, y, db, accumulate)
+    return dx is not None and mask_dx is not None
 
 
 class _FusedLinearFn(torch.autograd.Function):
@@ -254,9 +258,12 @@ class _FusedChainFn(torch.autograd.Function):
         active = ctx.grad_in_place and _in_place_active()
         grads = [None] * (2 * L)
         dy = dy.contiguous()
+        masked = False  # dy already carries this layer's ReLU mask (stored so by the dgrad above)
         for i in reversed(range(L)):
             dx = torch.empty_like(acts[i]) if (i > 0 or ctx.needs_input_grad[0]) else None
-            y = acts[i + 1] if ctx.relus[i] else None
+            y = acts[i + 1] if ctx.relus[i] and not masked else None
+            # the layer below's ReLU mask goes into this dgrad's store (i > 0: dx feeds layer i - 1)
+            mask_dx = acts[i] if (i > 0 and ctx.relus[i - 1]) else None
             # per layer: a parameter frozen after injection (requires_grad False) gets nothing, and
             # only a layer whose trained tensors all have live .grad views accumulates in place
             w_need, b_need = ctx.needs_input_grad[3 + 2 * i], ctx.has_bias[i] and ctx.needs_input_grad[4 + 2 * i]
@@ -265,11 +272,12 @@ class _FusedChainFn(torch.autograd.Function):
             in_place = (active and w_need and _grad_view_ok(w_leaf)
                         and (not ctx.has_bias[i] or (b_need and _grad_view_ok(b_leaf))))
             if in_place:
-                _bwd(ops, dy, acts[i], ws[i], y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad, True)
+                masked = _bwd(ops, dy, acts[i], ws[i], y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad,
+                              True, mask_dx)
             else:
                 dw = torch.empty_like(ws[i])
                 db = torch.empty(ws[i].shape[0], dtype=torch.float32, device=dy.device) if ctx.has_bias[i] else None
-                _bwd(ops, dy, acts[i], ws[i], y, dx, dw, db)
+                masked = _bwd(ops, dy, acts[i], ws[i], y, dx, dw, db, mask_dx=mask_dx)
                 grads[2 * i] = dw if w_need else None
                 grads[2 * i + 1] = db if b_need else None
             dy = dx

@@ -53,6 +53,22 @@ SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 1024, 1024), (2048, 2048, 512), (1000, 999, 1004), (77, 130, 67),
+                                   (64, 64, 8192)])
+def test_gemm_f32_output_mask(M, N, K):
+    """``maskC``: the product stored as C * 1[maskC > 0] (a dgrad writing the ReLU-masked gradient of
+    the layer below), on the direct epilogue and through the split-K reduce, equal bit for bit to the
+    plain product masked afterwards."""
+    ops = _ops()
+    a, b, A, B = _operands(M, N, K, 0, 1, seed=K)
+    mk = torch.randn(M, N, device="cuda")
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm_f32(A, B, None, None, C, 0, 1, False, False, None, mk)
+    plain = torch.empty(M, N, device="cuda")
+    ops.gemm_f32(A, B, None, None, plain, 0, 1, False, False)
+    assert torch.equal(C, torch.where(mk > 0, plain, torch.zeros_like(plain)))
+
+
 @pytest.mark.parametrize("la", [0, 1])
 @pytest.mark.parametrize("masked", [False, True])
 @pytest.mark.parametrize("accumulate", [False, True])
