@@ -92,7 +92,7 @@ hipError_t linear_fwd(const float* x, const float* W, const float* b, float* y, 
                       hipStream_t stream);
 hipError_t linear_bwd(const float* dy, const float* x, const float* W, const float* y, float* dx, float* dW,
                       float* db, int M, int N, int K, bool accumulate, hipStream_t stream);
-hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz,
+hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz, void* dz_lp,
                       hipStream_t stream);
 
 // ---------------------------------------------------------------- exact-fp32 MFMA GEMM (gemm_f32.hip)

@@ -20,7 +20,8 @@ DGT_DEVICE float to_f<__hip_bfloat16>(__hip_bfloat16 v) { return __bfloat162floa
 
 template <typename T>
 __global__ __launch_bounds__(1024) void bce_logits_kernel(const T* __restrict__ z, const float* __restrict__ y, long long n,
-                                                          float* __restrict__ loss, float* __restrict__ dz) {
+                                                          float* __restrict__ loss, float* __restrict__ dz,
+                                                          __hip_bfloat16* __restrict__ dz_lp) {
   __shared__ float red[32];
   const float inv_n = 1.f / (float)n;
   float acc = 0.f;
@@ -30,7 +31,9 @@ __global__ __launch_bounds__(1024) void bce_logits_kernel(const T* __restrict__ 
     const float r = 1.f / (1.f + e);
     const float sig = zi >= 0.f ? r : e * r;
     acc += (1.f - yi) * zi - (fminf(zi, 0.f) - log1pf(e));
-    dz[i] = (sig - yi) * inv_n;
+    const float d = (sig - yi) * inv_n;
+    dz[i] = d;
+    if (dz_lp) dz_lp[i] = __float2bfloat16(d);  // the product with a unit seed, rounded once
   }
   acc = wave_sum(acc);
   const int w = threadIdx.x >> 6, l = threadIdx.x & 63;
@@ -43,16 +46,17 @@ __global__ __launch_bounds__(1024) void bce_logits_kernel(const T* __restrict__ 
   }
 }
 
-hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz,
+hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz, void* dz_lp,
                       hipStream_t stream) {
   if (n < 1) return hipErrorInvalidValue;
   const int threads = n >= 1024 ? 1024 : (int)((n + 63) / 64 * 64);
   if (z_dtype == kBF16)
     hipLaunchKernelGGL(bce_logits_kernel<__hip_bfloat16>, dim3(1), dim3(threads), 0, stream,
-                       static_cast<const __hip_bfloat16*>(z), y, n, loss, dz);
+                       static_cast<const __hip_bfloat16*>(z), y, n, loss, dz,
+                       static_cast<__hip_bfloat16*>(dz_lp));
   else
     hipLaunchKernelGGL(bce_logits_kernel<float>, dim3(1), dim3(threads), 0, stream, static_cast<const float*>(z), y,
-                       n, loss, dz);
+                       n, loss, dz, static_cast<__hip_bfloat16*>(dz_lp));
   return hipGetLastError();
 }
 

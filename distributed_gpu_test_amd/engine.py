@@ -361,8 +361,10 @@ class Engine:
             return None
         if len(runner.static_out) != 1 or runner.grad_out_idx != [0]:
             return None
-        (dz,) = node.saved_tensors
+        dz, lp = node.saved_tensors
         gout = runner.static_gout[0]
+        if lp is not None and gout.dtype == lp.dtype:
+            dz = lp  # the kernel's once-rounded bf16 copy: a plain copy into the graph's input
         if dz.numel() != gout.numel() or gout.device != dz.device:
             return None
         return runner, dz
@@ -486,17 +488,10 @@ class Engine:
         leaves = [a.variable for a in accs]
         if any(p._backward_hooks for p in leaves):
             return False  # a tensor hook sees the gradient before accumulation: autograd's job
-        seed = self._seed_one
-        if seed is None or seed.device != loss.device:
-            seed = self._seed_one = torch.ones((), dtype=torch.float32, device=loss.device)
+        seed = self._unit_seed(loss.device)
         with torch.no_grad():  # autograd runs backward functions with grad mode off (no create_graph)
-            if getattr(node, "dtype", None) == torch.float32:
-                # fp32 logits: the BCE backward's product with the unit seed is its saved d loss /
-                # d logits itself (x * 1.0 == x bit for bit): no multiply launch
-                g = node.saved_tensors[0].view(node.shape)
-            else:
-                g = node.apply(seed)
-                g = g[0] if isinstance(g, tuple) else g
+            g = node.apply(seed)  # the unit seed: the saved d loss / d logits itself, no launch
+            g = g[0] if isinstance(g, tuple) else g
             for v in views:  # reshapes / casts back to the chain's output
                 g = v(g)
                 g = g[0] if isinstance(g, tuple) else g
@@ -530,16 +525,23 @@ class Engine:
         engine itself created (the 1/gas division or the loss-scale multiply), whose backward
         reads its incoming gradient without writing it.  A loss the user's code produced directly
         gets autograd's own fresh seed: a custom Function may edit grad_output in place, which
-        would corrupt a shared seed for every later step."""
-        if scaled is loss or scaled.grad_fn is None or scaled.grad_fn is loss.grad_fn:
+        would corrupt a shared seed for every later step.  The framework's own fused BCE is such a
+        node too: its backward only reads the seed (``ops/loss.py``)."""
+        own_loss = (scaled is loss and scaled.grad_fn is not None
+                    and type(scaled.grad_fn).__name__ == "_FusedBCEWithLogitsBackward")
+        if not own_loss and (scaled is loss or scaled.grad_fn is None or scaled.grad_fn is loss.grad_fn):
             return None
         if scaled.dim() != 0 or scaled.dtype != torch.float32:
             return None
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             return None
+        return self._unit_seed(scaled.device)
+
+    def _unit_seed(self, device: torch.device) -> torch.Tensor:
         seed = self._seed_one
-        if seed is None or seed.device != scaled.device:
-            seed = self._seed_one = torch.ones((), dtype=torch.float32, device=scaled.device)
+        if seed is None or seed.device != device:
+            from .ops.loss import unit_seed
+            seed = self._seed_one = unit_seed(device)  # the BCE backward then launches nothing
         return seed
 
     def _clip_coef(self, grads: torch.Tensor, scale: float) -> Optional[torch.Tensor]:

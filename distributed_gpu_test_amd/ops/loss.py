@@ -6,6 +6,10 @@ One HIP kernel computes the mean loss AND d loss / d logits (saved for backward)
 multiply by the incoming gradient.  torch's loss runs ~11 small kernels per step, and inside a
 HIP-graph-replayed step every node costs a few microseconds whatever it computes.  On CPU tensors
 (or without the extension) it is ``F.binary_cross_entropy_with_logits`` itself.
+
+Backward seeded with :func:`unit_seed` (the engine's persistent 1, never written) launches nothing:
+the gradient IS the saved d loss / d logits -- for bf16 logits the copy the kernel rounded once,
+bit for bit what ``dz * 1`` cast to bf16 gives.  Any other seed is one multiply.
 """
 from __future__ import annotations
 
@@ -13,6 +17,22 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext
+
+_UNIT: dict = {}
+
+
+def unit_seed(device: torch.device) -> torch.Tensor:
+    """A persistent fp32 scalar 1 on ``device``; callers must never write it (the BCE backward
+    recognises it and skips its multiply)."""
+    t = _UNIT.get(device)
+    if t is None:
+        t = _UNIT[device] = torch.ones((), dtype=torch.float32, device=device)
+    return t
+
+
+def _is_unit(g: torch.Tensor) -> bool:
+    t = _UNIT.get(g.device)
+    return t is not None and g.dim() == 0 and g.dtype == torch.float32 and g.data_ptr() == t.data_ptr()
 
 
 class _FusedBCEWithLogits(torch.autograd.Function):
@@ -22,14 +42,17 @@ class _FusedBCEWithLogits(torch.autograd.Function):
         yc = y.reshape(-1).to(torch.float32).contiguous()
         loss = torch.empty(1, dtype=torch.float32, device=z.device)
         dz = torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
-        _ext.require().bce_logits(zc, yc, loss, dz)
-        ctx.save_for_backward(dz)
+        lp = torch.empty(zc.numel(), dtype=torch.bfloat16, device=z.device) if z.dtype == torch.bfloat16 else None
+        _ext.require().bce_logits(zc, yc, loss, dz, lp)
+        ctx.save_for_backward(dz, lp)
         ctx.shape, ctx.dtype = z.shape, z.dtype
         return loss.view(())
 
     @staticmethod
     def backward(ctx, g: torch.Tensor):
-        (dz,) = ctx.saved_tensors
+        dz, lp = ctx.saved_tensors
+        if _is_unit(g):
+            return (lp if lp is not None else dz).view(ctx.shape), None
         # scaled and cast to the logits' dtype in one pass (the fp32 product, rounded once)
         gz = torch.empty(ctx.shape, dtype=ctx.dtype, device=dz.device)
         torch.mul(dz.view(ctx.shape), g, out=gz)

@@ -199,6 +199,26 @@ def test_fused_bce_matches_torch(n, dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("dtype", [torch.float32, torch.bfloat16])
+def test_fused_bce_unit_seed_is_bitwise_plain_seed(dtype):
+    """The engine's persistent unit seed returns the saved gradient (bf16: the kernel's once-rounded
+    copy) -- bit for bit autograd's dz * ones cast to the logits' dtype, and the seed stays 1."""
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    from distributed_gpu_test_amd.ops.loss import unit_seed
+    g = torch.Generator().manual_seed(7)
+    z0 = (torch.randn(3000, 1, generator=g) * 4).to(dtype).cuda()
+    y = (torch.rand(3000, 1, generator=g) > 0.5).float().cuda()
+    grads = []
+    for seed in (torch.ones((), device="cuda"), unit_seed(torch.device("cuda", 0))):
+        z = z0.clone().requires_grad_(True)
+        BCEWithLogitsLoss()(z, y).backward(seed)
+        assert z.grad.dtype == dtype
+        grads.append(z.grad)
+    assert torch.equal(grads[0], grads[1])
+    assert unit_seed(torch.device("cuda", 0)).item() == 1.0
+
+
+@pytest.mark.gpu
 @pytest.mark.parametrize("M,N,K,relu,bias,need_dx", [(4, 64, 20, True, True, False), (4, 1, 64, False, True, True),
                                                      (7, 33, 19, True, False, True), (256, 128, 96, True, True, True)])
 def test_fused_linear_matches_torch(M, N, K, relu, bias, need_dx):
