@@ -99,6 +99,9 @@ class AMDConfig:
     # injected chain's output) by calling the two backward functions directly, without the autograd
     # engine; any other graph goes through autograd (engine.py Engine._direct_backward)
     direct_backward: bool = True
+    # one GPU, injected kernels that STORE their first gradient writes: skip the step's zero fill of
+    # the gradient bucket (the next backward overwrites it; engine.py "Deferred zeroing")
+    defer_zero_grad: bool = True
 
 
 @dataclass
@@ -229,7 +232,8 @@ def parse_config(config: Union[str, os.PathLike, Dict[str, Any], None], world_si
                     fused_linear=None if a.get("fused_linear") is None else bool(a["fused_linear"]),
                     graph_module=bool(a.get("graph_module", False)),
                     graph_tail=bool(a.get("graph_tail", True)),
-                    direct_backward=bool(a.get("direct_backward", True)))
+                    direct_backward=bool(a.get("direct_backward", True)),
+                    defer_zero_grad=bool(a.get("defer_zero_grad", True)))
     if amd.allreduce not in ("auto", "rccl", "oneshot"):
         raise ConfigError(f"amd.allreduce={amd.allreduce!r}: expected auto|rccl|oneshot")
 

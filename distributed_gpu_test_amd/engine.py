@@ -148,15 +148,19 @@ class Engine:
                                    comm_dtype=comm_dtype, oneshot=self.oneshot,
                                    oneshot_max_bytes=config.amd.oneshot_max_bytes,
                                    debug_sync=config.amd.debug_sync_streams)
-        # deferred zeroing needs a writer that STORES gradients (the bf16 MFMA chain) and no collective
-        self._defer_capable = (device.type == "cuda" and self.world_size == 1 and self.dtype == torch.bfloat16
-                               and self.fused_linear_layers > 0)
+        # deferred zeroing needs a writer that STORES gradients (the bf16 MFMA chain, the fp32 fused
+        # Linear kernels) and no collective
+        self._defer_capable = (device.type == "cuda" and self.world_size == 1 and config.amd.defer_zero_grad
+                               and self.dtype in (torch.bfloat16, torch.float32) and self.fused_linear_layers > 0)
         self._hooks = []
+        self._own_tensor_hooks = set()  # ids of the engine's own tensor hooks (the direct backward runs them)
         for i, p in enumerate(self.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(
                 lambda _p, i=i: self.reducer.on_grad_ready(i)))
             if self._defer_capable:
-                self._hooks.append(p.register_hook(lambda g, p=p: self._before_accumulate(p)))
+                h = p.register_hook(lambda g, p=p: self._before_accumulate(p))
+                self._hooks.append(h)
+                self._own_tensor_hooks.add(h.id)
 
         # ---- schedules, loss scaling, logging, fault injection
         self.lr_scheduler = lr_scheduler
@@ -171,9 +175,10 @@ class Engine:
         self._seed_one: Optional[torch.Tensor] = None
         self._grads_dirty = False  # the flat gradient buffer holds something since the last zero_grad
         # Deferred zeroing (one GPU): when the last backward that began on a zeroed buffer STORED every
-        # parameter's gradient view (the bf16 MFMA chain's first writes), the step's zero fill of the
-        # flat buffer (a whole-buffer pass: 18.5 us of 800 for the bench MLP) is skipped -- the next
-        # backward overwrites every view anyway.  Should autograd itself accumulate into a view in that
+        # parameter's gradient view (the first writes of the bf16 MFMA chain or of the fp32 fused Linear
+        # kernels), the step's zero fill of the flat buffer (a whole-buffer pass: 18.5 us of 800 for
+        # the bench MLP; a launch of a host-bound eager step) is skipped -- the next backward
+        # overwrites every view anyway.  Should autograd itself accumulate into a view in that
         # backward (a forward that fell back to F.linear, a parameter outside the chains), the view is
         # zeroed just before (a tensor hook runs ahead of AccumulateGrad), and a view nothing writes is
         # zeroed right after the backward (it got no gradient).  So after step() such an engine's .grad
@@ -460,7 +465,7 @@ class Engine:
         worker thread -- most of a host-bound eager step (profiles/r2_engine_host_profile.txt).
         Anything else (another loss, an input that needs a gradient, tensor hooks on a parameter,
         loss scaling or 1/gas nodes) returns False: the caller runs ``scaled.backward``."""
-        if (scaled is not loss or not self.config.amd.direct_backward or self._defer_capable
+        if (scaled is not loss or not self.config.amd.direct_backward
                 or self.device.type != "cuda" or loss.dim() != 0):
             return False
         node = loss.grad_fn
@@ -486,8 +491,9 @@ class Engine:
         if any(a is None or type(a).__name__ != "AccumulateGrad" for a in accs):
             return False
         leaves = [a.variable for a in accs]
-        if any(p._backward_hooks for p in leaves):
-            return False  # a tensor hook sees the gradient before accumulation: autograd's job
+        own = self._own_tensor_hooks
+        if any(p._backward_hooks and any(k not in own for k in p._backward_hooks) for p in leaves):
+            return False  # a user's tensor hook sees the gradient before accumulation: autograd's job
         seed = self._unit_seed(loss.device)
         with torch.no_grad():  # autograd runs backward functions with grad mode off (no create_graph)
             g = node.apply(seed)  # the unit seed: the saved d loss / d logits itself, no launch
@@ -510,6 +516,8 @@ class Engine:
                 if p.grad is None:
                     p.grad = gr.detach()
                 else:
+                    if p._backward_hooks:
+                        self._before_accumulate(p)  # the engine's tensor hook, as autograd would run it
                     p.grad.add_(gr)
         for p in leaves:  # what AccumulateGrad does after accumulating: the post-accumulate hooks
             hooks = p._post_accumulate_grad_hooks

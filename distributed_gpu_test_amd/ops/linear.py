@@ -26,6 +26,7 @@ import collections
 import contextlib
 import os
 import sys
+from typing import Optional
 
 import torch
 import torch.nn as nn
@@ -81,6 +82,21 @@ def _first_write(grad: torch.Tensor) -> bool:
         return False
     _WRITTEN.add(key)
     return True
+
+
+def _store_both(w_grad: torch.Tensor, b_grad: Optional[torch.Tensor]) -> bool:
+    """One accumulate flag for a layer's dW and db (the fp32 kernels take one): True = STORE both
+    (their first write of a backward that began on a zeroed -- or deferred, stale -- buffer).  Each
+    view is asked once; a mix (a view shared with another layer) zeroes the first-written view and
+    accumulates into both."""
+    fw = _first_write(w_grad)
+    if b_grad is None:
+        return fw
+    fb = _first_write(b_grad)
+    if fw != fb:
+        (w_grad if fw else b_grad).zero_()
+        return False
+    return fw
 
 
 # Every call that leaves the hand-written kernels for F.linear (hipBLASLt / rocBLAS), by reason:
@@ -159,11 +175,13 @@ class _FusedLinearFn(torch.autograd.Function):
         w_leaf, b_leaf = ctx.params
         if (ctx.grad_in_place and _in_place_active() and ctx.needs_input_grad[1] and w_leaf.requires_grad
                 and _grad_view_ok(w_leaf) and (b_leaf is None or (b_leaf.requires_grad and _grad_view_ok(b_leaf)))):
-            # accumulate straight into the existing .grad views (the engine's flat bucket): no
-            # separate AccumulateGrad add kernel per parameter.  Autograd still runs the leaves'
+            # write straight into the existing .grad views (the engine's flat bucket; stored on
+            # their first write of a from-zero backward, else added): no separate AccumulateGrad
+            # add kernel per parameter.  Autograd still runs the leaves'
             # AccumulateGrad nodes with an undefined gradient, which fire the post-accumulate hooks
             # (the engine's bucket reducer) after this kernel is queued
-            _bwd(_ext.require(), dy, x, weight, y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad, True)
+            bg = None if b_leaf is None else b_leaf.grad
+            _bwd(_ext.require(), dy, x, weight, y, dx, w_leaf.grad, bg, not _store_both(w_leaf.grad, bg))
             return dx, None, None, None, None
         dw = torch.empty_like(weight)
         db = torch.empty(weight.shape[0], dtype=torch.float32, device=x.device) if ctx.has_bias else None
@@ -272,8 +290,9 @@ class _FusedChainFn(torch.autograd.Function):
             in_place = (active and w_need and _grad_view_ok(w_leaf)
                         and (not ctx.has_bias[i] or (b_need and _grad_view_ok(b_leaf))))
             if in_place:
-                masked = _bwd(ops, dy, acts[i], ws[i], y, dx, w_leaf.grad, None if b_leaf is None else b_leaf.grad,
-                              True, mask_dx)
+                bg = None if b_leaf is None else b_leaf.grad
+                masked = _bwd(ops, dy, acts[i], ws[i], y, dx, w_leaf.grad, bg, not _store_both(w_leaf.grad, bg),
+                              mask_dx)
             else:
                 dw = torch.empty_like(ws[i])
                 db = torch.empty(ws[i].shape[0], dtype=torch.float32, device=dy.device) if ctx.has_bias[i] else None

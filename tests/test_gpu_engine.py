@@ -625,3 +625,41 @@ def test_engine_direct_backward_matches_autograd(extra):
     assert e3.direct_backwards == 0 and all(v == v for v in l3)
     for e in (e1, e2, e3):
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("B,F", [(64, 64), (512, 256)])  # the small-batch kernels; the tiled fp32 GEMM
+def test_engine_fp32_deferred_zero_grad_direct_backward(B, F):
+    """fp32 fused Linear kernels STORE a gradient view on its first write of a backward, so the
+    engine defers the bucket's zero fill as for bf16; the direct backward still runs (it calls the
+    engine's own tensor hook), a user-set gradient folds into a zeroed buffer, and every step's
+    gradients match the autograd engine's on F.linear."""
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    engines = []
+    for fused in (True, False):
+        torch.manual_seed(12)
+        cfg = {"train_micro_batch_size_per_gpu": B,
+               "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "amd": {"fused_linear": fused}}
+        engines.append(dgt.initialize(model=SyntheticMLP(F, 2), config=cfg)[0])
+    crit = BCEWithLogitsLoss()
+    g = torch.Generator().manual_seed(5)
+    deferred = []
+    for k in range(5):
+        x = torch.randn(B, F, generator=g).cuda()
+        y = (torch.rand(B, generator=g) > 0.5).float().cuda()
+        grads = []
+        for e in engines:
+            deferred.append(e._zero_deferred)
+            if k == 2:
+                p0 = next(e.module.parameters())
+                p0.grad = torch.full_like(p0, 0.01)
+            e.backward(crit(e(x).view(-1), y))
+            grads.append(torch.cat([p.grad.reshape(-1) for p in e.module.parameters()]))
+            e.step()
+        torch.testing.assert_close(grads[0], grads[1], rtol=1e-4, atol=1e-6)
+    assert deferred[0::2] == [False, True, True, True, True]
+    assert not any(deferred[1::2])
+    assert engines[0].direct_backwards == 5
+    for e in engines:
+        e.close()
