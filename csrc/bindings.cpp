@@ -829,6 +829,65 @@ void skinny_bwd_bf16(const at::Tensor& dz, const at::Tensor& a, const at::Tensor
                                      ws.data_ptr<float>(), (int)M, (int)N, (int)K, stream_of(a), bp));
 }
 
+// skinny fp32 Linear(K, N <= 4) (the fp32 engine's MLP head): z = act(a . W^T + b)
+void skinny_f32_fwd(const at::Tensor& a, const at::Tensor& W, const std::optional<at::Tensor>& b, const at::Tensor& z,
+                    bool relu) {
+  TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && W.size(1) == a.size(1), "dgt: skinny_f32_fwd needs a [M, K], W [N, K]");
+  const int64_t M = a.size(0), K = a.size(1), N = W.size(0);
+  TORCH_CHECK(N >= 1 && N <= 4 && K % 4 == 0 && M > 0, "dgt: skinny_f32_fwd needs N <= 4, K % 4 == 0");
+  check_2d(a, "a", at::kFloat, M, K);
+  check_2d(W, "W", at::kFloat, N, K);
+  check_gpu(z, "z", at::kFloat);
+  TORCH_CHECK(z.numel() == M * N, "dgt: skinny_f32_fwd z must be [M, N]");
+  const float* bp = nullptr;
+  if (b.has_value() && b->defined()) {
+    check_gpu(*b, "b", at::kFloat);
+    TORCH_CHECK(b->numel() == N, "dgt: skinny_f32_fwd bias must have N elements");
+    bp = b->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(a.device());
+  DGT_CHECK_HIP(dgt::skinny_f32_fwd(a.data_ptr<float>(), W.data_ptr<float>(), bp, z.data_ptr<float>(), (int)M, (int)N,
+                                    (int)K, relu ? 1 : 0, stream_of(a)));
+}
+
+// its backward: g = dz * 1[y > 0] (y given), dx = (g . W) * 1[a > 0] (mask), dW / db (+)= in fixed order
+void skinny_f32_bwd(const at::Tensor& dz, const std::optional<at::Tensor>& y, const at::Tensor& a, const at::Tensor& W,
+                    bool mask, const std::optional<at::Tensor>& dx, const at::Tensor& dW,
+                    const std::optional<at::Tensor>& db, bool accumulate) {
+  const int64_t M = a.size(0), K = a.size(1), N = W.size(0);
+  TORCH_CHECK(a.dim() == 2 && W.dim() == 2 && W.size(1) == K && N >= 1 && N <= 4 && M % 64 == 0 && K % 32 == 0 && M > 0,
+              "dgt: skinny_f32_bwd needs a [M, K], W [N <= 4, K], M % 64 == 0, K % 32 == 0");
+  check_gpu(dz, "dz", at::kFloat);
+  TORCH_CHECK(dz.numel() == M * N, "dgt: skinny_f32_bwd dz must be [M, N]");
+  check_2d(a, "a", at::kFloat, M, K);
+  check_2d(W, "W", at::kFloat, N, K);
+  const float* yp = nullptr;
+  if (y.has_value() && y->defined()) {
+    check_gpu(*y, "y", at::kFloat);
+    TORCH_CHECK(y->numel() == M * N, "dgt: skinny_f32_bwd y must be [M, N]");
+    yp = y->data_ptr<float>();
+  }
+  float* dxp = nullptr;
+  if (dx.has_value() && dx->defined()) {
+    check_2d(*dx, "dx", at::kFloat, M, K);
+    dxp = dx->data_ptr<float>();
+  }
+  check_gpu(dW, "dW", at::kFloat);
+  TORCH_CHECK(dW.numel() == N * K && reinterpret_cast<uintptr_t>(dW.data_ptr()) % 16 == 0,
+              "dgt: skinny_f32_bwd dW must be [N, K], 16-byte aligned");
+  float* dbp = nullptr;
+  if (db.has_value() && db->defined()) {
+    check_gpu(*db, "db", at::kFloat);
+    TORCH_CHECK(db->numel() == N, "dgt: skinny_f32_bwd db must have N elements");
+    dbp = db->data_ptr<float>();
+  }
+  c10::DeviceGuard guard(a.device());
+  at::Tensor ws = at::empty({M / 64, N, K}, a.options());
+  DGT_CHECK_HIP(dgt::skinny_f32_bwd(dz.data_ptr<float>(), yp, a.data_ptr<float>(), W.data_ptr<float>(), mask ? 1 : 0,
+                                    dxp, dW.data_ptr<float>(), dbp, accumulate ? 1 : 0, ws.data_ptr<float>(), (int)M,
+                                    (int)N, (int)K, stream_of(a)));
+}
+
 void mlp_head(const at::Tensor& a, const at::Tensor& w, const at::Tensor& b0, const at::Tensor& y,
               const at::Tensor& dz, const at::Tensor& dw, const at::Tensor& db, const at::Tensor& loss_acc,
               const at::Tensor& g, const at::Tensor& gT, const std::optional<at::Tensor>& dw_part,
@@ -1052,6 +1111,11 @@ TORCH_LIBRARY(dgt, m) {
   m.def("transpose_bf16(Tensor inp, Tensor(a!) out) -> ()", &transpose_bf16);
   m.def("rowsum_bf16(Tensor inp, Tensor(a!) out, bool accumulate) -> ()", &rowsum_bf16);
   m.def("skinny_fwd_bf16(Tensor a, Tensor W, Tensor? b, Tensor(a!) z) -> ()", &skinny_fwd_bf16);
+  m.def("skinny_f32_fwd(Tensor a, Tensor W, Tensor? b, Tensor(a!) z, bool relu=False) -> ()", &skinny_f32_fwd);
+  m.def(
+      "skinny_f32_bwd(Tensor dz, Tensor? y, Tensor a, Tensor W, bool mask, Tensor(a!)? dx, Tensor(b!) dW, "
+      "Tensor(c!)? db, bool accumulate=False) -> ()",
+      &skinny_f32_bwd);
   m.def(
       "skinny_bwd_bf16(Tensor dz, Tensor a, Tensor W, bool mask, Tensor(a!) g, Tensor(b!)? gT, Tensor(c!) dW, "
       "Tensor(d!) db, bool accumulate=True, Tensor(e!)? bias_part=None, Tensor(f!)? dw_part=None) -> ()",

@@ -201,6 +201,16 @@ hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mas
                            void* db, int dw_bf16, int accumulate, float* part_ws, int M, int N, int K,
                            hipStream_t stream, float* bias_part = nullptr);
 
+// fp32 skinny Linear (N <= 4) for the engine's fp32 Linear path: z = act(a . W^T + b) (K % 4);
+// backward g = dz * 1[y > 0] (y optional), dx = (g . W) * 1[a > 0] (mask; dx optional),
+// dW (+)= g^T a via part_ws [M / 64, N, K] + the fixed-order partials_reduce, db (+)= sum g (optional);
+// M % 64, K % 32
+hipError_t skinny_f32_fwd(const float* a, const float* W, const float* b, float* z, int M, int N, int K, int relu,
+                          hipStream_t stream);
+hipError_t skinny_f32_bwd(const float* dz, const float* y, const float* a, const float* W, int mask, float* dx,
+                          float* dW, float* db, int accumulate, float* part_ws, int M, int N, int K,
+                          hipStream_t stream);
+
 // out[i] (+)= sum over t = 0 .. tiles-1 (in this order) of part[t * n + i]: the fixed-order reduction of
 // per-tile partials that replaces float atomics (bit-reproducible gradients); out fp32 or bf16
 // (out_bf16); n % 4 == 0, aligned

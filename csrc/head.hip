@@ -266,6 +266,130 @@ __global__ __launch_bounds__(64) void partials_reduce_multi_kernel(ReduceSegs r,
   }
 }
 
+// fp32 skinny Linear (N <= 4 outputs): the binary head of an fp32 MLP on the engine's fused Linear
+// path (ops/linear.py).  A 64 x 64 MFMA tile computing one useful column (forward, wgrad) or one
+// useful k step (dgrad) wastes the matrix cores and still pays a split-K reduce; these are the two
+// bandwidth-bound passes over the activation instead.
+//   forward   z[M, N] = act(a[M, K] . W[N, K]^T + b)            one wave per row, float4 loads
+//   backward  g = dz * 1[y > 0] (y: the head's own ReLU output, optional)
+//             dx = (g . W) * 1[a > 0] (mask: a is the layer below's ReLU output)
+//             dW (+)= g^T . a as per-64-row-tile partials + the fixed-order partials_reduce,
+//             db (+)= sum g in row order: deterministic, no atomics
+template <int N>
+__global__ __launch_bounds__(256) void skinny_f32_fwd_kernel(const float* __restrict__ a, const float* __restrict__ W,
+                                                             const float* __restrict__ b, float* __restrict__ z,
+                                                             int M, int K, int relu) {
+  const int l = threadIdx.x & 63, row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= M) return;
+  const float* ar = a + (long long)row * K;
+  float acc[N];
+#pragma unroll
+  for (int n = 0; n < N; ++n) acc[n] = 0.f;
+#pragma unroll 4
+  for (int c = l * 4; c < K; c += 64 * 4) {
+    const float4 av = *reinterpret_cast<const float4*>(ar + c);
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const float4 wv = *reinterpret_cast<const float4*>(W + (long long)n * K + c);
+      acc[n] = fmaf(av.x, wv.x, acc[n]);
+      acc[n] = fmaf(av.y, wv.y, acc[n]);
+      acc[n] = fmaf(av.z, wv.z, acc[n]);
+      acc[n] = fmaf(av.w, wv.w, acc[n]);
+    }
+  }
+#pragma unroll
+  for (int n = 0; n < N; ++n) acc[n] = wave_sum(acc[n]);
+  if (l < N) {
+    float v = acc[0];
+#pragma unroll
+    for (int n = 1; n < N; ++n) v = l == n ? acc[n] : v;
+    v += b ? b[l] : 0.f;
+    z[(long long)row * N + l] = relu ? fmaxf(v, 0.f) : v;
+  }
+}
+
+// one wave per 64 x 32 tile of a: lane (cg = l & 7, rb = l >> 3) owns rows rb*8 .. +7, columns cg*4 .. +3
+template <int N>
+__global__ __launch_bounds__(256) void skinny_f32_bwd_kernel(const float* __restrict__ dz, const float* __restrict__ y,
+                                                             const float* __restrict__ a, const float* __restrict__ W,
+                                                             int mask, float* __restrict__ dx,
+                                                             float* __restrict__ part_ws, float* __restrict__ db,
+                                                             int acc, int M, int K) {
+  const int l = threadIdx.x & 63, cg = l & 7, rb = l >> 3, wv = threadIdx.x >> 6;
+  const int r = blockIdx.y * 64 + rb * 8, c = (blockIdx.x * (blockDim.x >> 6) + wv) * 32 + cg * 4;
+  float w[N][4];
+#pragma unroll
+  for (int n = 0; n < N; ++n) {
+    const float4 t = *reinterpret_cast<const float4*>(W + (long long)n * K + c);
+    w[n][0] = t.x, w[n][1] = t.y, w[n][2] = t.z, w[n][3] = t.w;
+  }
+  float4 av[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) av[k] = *reinterpret_cast<const float4*>(a + (long long)(r + k) * K + c);
+  float part[N][4];
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) part[n][e] = 0.f;
+#pragma unroll
+  for (int k = 0; k < 8; ++k) {
+    float d[N];
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      const long long o = (long long)(r + k) * N + n;
+      d[n] = (y && !(y[o] > 0.f)) ? 0.f : dz[o];
+    }
+    const float x[4] = {av[k].x, av[k].y, av[k].z, av[k].w};
+    float o4[4];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float s = 0.f;
+#pragma unroll
+      for (int n = 0; n < N; ++n) {
+        s = fmaf(d[n], w[n][e], s);
+        part[n][e] = fmaf(d[n], x[e], part[n][e]);
+      }
+      o4[e] = (!mask || x[e] > 0.f) ? s : 0.f;
+    }
+    if (dx) *reinterpret_cast<float4*>(dx + (long long)(r + k) * K + c) = make_float4(o4[0], o4[1], o4[2], o4[3]);
+  }
+  // the tile's dW partial: its 8 row blocks (lanes cg, cg + 8, ..., cg + 56) summed
+#pragma unroll
+  for (int n = 0; n < N; ++n)
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      float x = part[n][e];
+      x += __shfl_xor(x, 8);
+      x += __shfl_xor(x, 16);
+      x += __shfl_xor(x, 32);
+      part[n][e] = x;
+    }
+  if (rb == 0) {
+#pragma unroll
+    for (int n = 0; n < N; ++n)
+      *reinterpret_cast<float4*>(part_ws + ((long long)blockIdx.y * N + n) * K + c) =
+          make_float4(part[n][0], part[n][1], part[n][2], part[n][3]);
+  }
+  if (db && blockIdx.x == 0 && blockIdx.y == 0 && wv == 0) {  // db, in a fixed order
+#pragma unroll
+    for (int n = 0; n < N; ++n) {
+      float s = 0.f;
+      for (int i0 = l; i0 < M; i0 += 64 * 8) {
+        float v[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const long long o = (long long)(i0 + 64 * u) * N + n;
+          v[u] = (i0 + 64 * u < M && !(y && !(y[o] > 0.f))) ? dz[o] : 0.f;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) s += v[u];
+      }
+      s = wave_sum(s);
+      if (l == 0) db[n] = (acc ? db[n] : 0.f) + s;
+    }
+  }
+}
+
 hipError_t partials_reduce_multi(const ReduceSegs& r, const ReduceAdam& adam, hipStream_t stream) {
   if (r.count < 1 || r.count > kMaxReduceSegs) return hipErrorInvalidValue;
   long long total = 0;
@@ -324,6 +448,36 @@ hipError_t skinny_bwd_bf16(const void* dz, const void* a, const void* W, int mas
   if (e != hipSuccess) return e;
   if (!dW) return hipSuccess;  // part_ws is the caller's: it reduces the partials (partials_reduce_multi)
   return partials_reduce(part_ws, dW, dw_bf16, M / 64, N * K, accumulate, stream);  // K % 64: whole float4s
+}
+
+hipError_t skinny_f32_fwd(const float* a, const float* W, const float* b, float* z, int M, int N, int K, int relu,
+                          hipStream_t stream) {
+  if (N < 1 || N > 4 || K % 4 || M <= 0) return hipErrorInvalidValue;
+  const dim3 grid((M + 3) / 4), blk(256);
+  switch (N) {
+    case 1: hipLaunchKernelGGL(skinny_f32_fwd_kernel<1>, grid, blk, 0, stream, a, W, b, z, M, K, relu); break;
+    case 2: hipLaunchKernelGGL(skinny_f32_fwd_kernel<2>, grid, blk, 0, stream, a, W, b, z, M, K, relu); break;
+    case 3: hipLaunchKernelGGL(skinny_f32_fwd_kernel<3>, grid, blk, 0, stream, a, W, b, z, M, K, relu); break;
+    default: hipLaunchKernelGGL(skinny_f32_fwd_kernel<4>, grid, blk, 0, stream, a, W, b, z, M, K, relu);
+  }
+  return hipGetLastError();
+}
+
+hipError_t skinny_f32_bwd(const float* dz, const float* y, const float* a, const float* W, int mask, float* dx,
+                          float* dW, float* db, int accumulate, float* part_ws, int M, int N, int K,
+                          hipStream_t stream) {
+  if (N < 1 || N > 4 || M % 64 || K % 32 || M <= 0 || K <= 0 || !dW) return hipErrorInvalidValue;
+  const int wpb = K % 128 == 0 ? 4 : 1;  // 4 tiles per block side by side when the width allows
+  const dim3 grid(K / (32 * wpb), M / 64), blk(64 * wpb);
+  switch (N) {
+    case 1: hipLaunchKernelGGL(skinny_f32_bwd_kernel<1>, grid, blk, 0, stream, dz, y, a, W, mask, dx, part_ws, db, accumulate, M, K); break;
+    case 2: hipLaunchKernelGGL(skinny_f32_bwd_kernel<2>, grid, blk, 0, stream, dz, y, a, W, mask, dx, part_ws, db, accumulate, M, K); break;
+    case 3: hipLaunchKernelGGL(skinny_f32_bwd_kernel<3>, grid, blk, 0, stream, dz, y, a, W, mask, dx, part_ws, db, accumulate, M, K); break;
+    default: hipLaunchKernelGGL(skinny_f32_bwd_kernel<4>, grid, blk, 0, stream, dz, y, a, W, mask, dx, part_ws, db, accumulate, M, K);
+  }
+  const hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  return partials_reduce(part_ws, dW, 0, M / 64, N * K, accumulate, stream);  // K % 32: whole float4s
 }
 
 }  // namespace dgt

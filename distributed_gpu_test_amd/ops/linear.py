@@ -122,11 +122,21 @@ def _small(x: torch.Tensor, weight: torch.Tensor) -> bool:
     return x.shape[0] <= SMALL_M and x.shape[0] * weight.shape[0] * weight.shape[1] <= SMALL_WORK
 
 
+def _skinny(x: torch.Tensor, weight: torch.Tensor) -> bool:
+    """A head Linear(K, N <= 4) beyond the small-batch kernels: two bandwidth passes over x
+    (``csrc/head.hip`` skinny_f32), not 64 x 64 MFMA tiles with one useful column plus a split-K reduce."""
+    return (weight.shape[0] <= 4 and x.shape[0] % 64 == 0 and x.shape[1] % 32 == 0
+            and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
+
+
 def _fwd(ops, x, weight, bias, relu: bool) -> torch.Tensor:
-    """y = act(x W^T + b): the small-batch kernel or the tiled fp32 MFMA GEMM (bias/ReLU epilogue)."""
+    """y = act(x W^T + b): the small-batch kernel, the skinny head kernel or the tiled fp32 MFMA GEMM
+    (bias/ReLU epilogue)."""
     y = torch.empty(x.shape[0], weight.shape[0], dtype=torch.float32, device=x.device)
     if _small(x, weight):
         ops.linear_fwd(x, weight, bias, y, relu)
+    elif _skinny(x, weight):
+        ops.skinny_f32_fwd(x, weight, bias, y, relu)
     else:
         ops.gemm_f32(x, weight, None, bias, y, 0, 0, relu, False)
     return y
@@ -143,6 +153,9 @@ def _bwd(ops, dy, x, weight, y, dx, dW, db, accumulate: bool = False, mask_dx=No
     if _small(x, weight):
         ops.linear_bwd(dy, x, weight, y, dx, dW, db, accumulate)
         return False
+    if _skinny(x, weight) and dW.data_ptr() % 16 == 0 and (mask_dx is None or mask_dx is x):
+        ops.skinny_f32_bwd(dy, y, x, weight, mask_dx is not None, dx, dW, db, accumulate)
+        return dx is not None and mask_dx is not None
     if dx is not None:
         ops.gemm_f32(dy, weight, y, None, dx, 0, 1, False, False, None, mask_dx)
     if _FUSED_ROWSUM:

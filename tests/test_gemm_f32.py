@@ -157,7 +157,8 @@ def test_colsum_f32(M, N):
     torch.testing.assert_close(db.double(), want, rtol=1e-5, atol=2e-4)
 
 
-@pytest.mark.parametrize("M,K,N,relu", [(1024, 1024, 1024, True), (512, 300, 700, False), (1000, 2048, 1, False)])
+@pytest.mark.parametrize("M,K,N,relu", [(1024, 1024, 1024, True), (512, 300, 700, False), (1000, 2048, 1, False),
+                                        (1024, 1024, 1, False), (512, 256, 3, True)])  # the last two: skinny
 def test_fused_linear_tiled_matches_nn_linear(M, K, N, relu):
     """FusedLinear beyond the small-batch kernels: forward, dx, dW, db vs nn.Linear in fp32."""
     from distributed_gpu_test_amd.ops import linear as L
@@ -189,6 +190,41 @@ def test_fused_linear_tiled_matches_nn_linear(M, K, N, relu):
     torch.testing.assert_close(gw, rw, rtol=1e-4, atol=1e-3)
     torch.testing.assert_close(gb, rb, rtol=1e-4, atol=1e-3)
     assert dict(L.FALLBACKS) == before, L.FALLBACKS
+
+
+@pytest.mark.parametrize("N", [1, 2, 4])
+@pytest.mark.parametrize("M,K", [(1024, 1024), (192, 96)])  # 4 tiles per block; 1 (K % 128 != 0)
+@pytest.mark.parametrize("mask,ymask,accumulate,with_dx", [(False, False, False, True), (True, False, False, True),
+                                                          (True, True, True, True), (False, True, False, False)])
+def test_skinny_f32_matches_fp64(N, M, K, mask, ymask, accumulate, with_dx):
+    """The fp32 head kernels (csrc/head.hip skinny_f32): z = relu?(a W^T + b); backward with the
+    head's own ReLU (y), the layer below's mask on dx, store or accumulate into dW / db."""
+    ops = _ops()
+    g = torch.Generator(device="cuda").manual_seed(N * 7 + M)
+    a = torch.randn(M, K, device="cuda", generator=g).clamp_min(0) if mask else torch.randn(M, K, device="cuda", generator=g)
+    W = torch.randn(N, K, device="cuda", generator=g)
+    b = torch.randn(N, device="cuda", generator=g)
+    z = torch.empty(M, N, device="cuda")
+    ops.skinny_f32_fwd(a, W, b, z, ymask)
+    z64 = a.double() @ W.double().t() + b.double()
+    if ymask:
+        z64 = z64.clamp_min(0)
+    _close(z, z64, a, W)
+    dz = torch.randn(M, N, device="cuda", generator=g)
+    dW0, db0 = torch.randn(N, K, device="cuda", generator=g), torch.randn(N, device="cuda", generator=g)
+    dW, db = dW0.clone(), db0.clone()
+    dx = torch.full((M, K), float("nan"), device="cuda") if with_dx else None
+    ops.skinny_f32_bwd(dz, z if ymask else None, a, W, mask, dx, dW, db, accumulate)
+    g64 = dz.double() * (z > 0) if ymask else dz.double()
+    if with_dx:
+        dx64 = g64 @ W.double()
+        if mask:
+            dx64 = dx64 * (a > 0)
+        _close(dx, dx64, g64.float(), W.t())
+    dW64 = g64.t() @ a.double() + (dW0.double() if accumulate else 0)
+    db64 = g64.sum(0) + (db0.double() if accumulate else 0)
+    torch.testing.assert_close(dW.double(), dW64, rtol=1e-5, atol=1e-3)
+    torch.testing.assert_close(db.double(), db64, rtol=1e-5, atol=1e-4)
 
 
 def test_engine_fp32_mlp_runs_no_vendor_gemm():
