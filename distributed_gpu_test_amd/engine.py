@@ -699,10 +699,12 @@ class Engine:
                 msg += ", " + ", ".join(f"{k}={v:.3f}" for k, v in self._timers.items())
             if os.environ.get("DGT_QUIET", "0") == "0":
                 print(msg, flush=True)
-        self.metrics.log({"step": self.global_steps, "lr": self.lr, "skipped": int(skipped),
-                          "samples_per_sec": self.tput.samples_per_sec(),
-                          "comm_bytes": self.reducer.bytes_reduced, **self._timers})
-        self.faults.maybe_fire(self.global_steps)
+        if self.metrics.enabled:  # (no per-step record built for a disabled sink: host-bound eager steps)
+            self.metrics.log({"step": self.global_steps, "lr": self.lr, "skipped": int(skipped),
+                              "samples_per_sec": self.tput.samples_per_sec(),
+                              "comm_bytes": self.reducer.bytes_reduced, **self._timers})
+        if self.faults.spec is not None:
+            self.faults.maybe_fire(self.global_steps)
 
     # ------------------------------------------------------------------ state
     def module_state_dict(self) -> Dict[str, torch.Tensor]:

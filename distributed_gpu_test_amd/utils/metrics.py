@@ -67,6 +67,10 @@ class MetricsSink:
             os.makedirs(d, exist_ok=True)
         return cls(p)
 
+    @property
+    def enabled(self) -> bool:
+        return self._fh is not None
+
     def log(self, record: Dict[str, Any]) -> None:
         if self._fh is None:
             return
