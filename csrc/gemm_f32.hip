@@ -159,7 +159,7 @@ DGT_DEVICE void tile_of(int bid, int nbm, int nbn, int& tm, int& tn) {
 // grid.x = tiles, grid.y = split-K slices.  Split slices write raw partial sums to ws[z][M][N]
 // (epilogue in gemm_f32_splitk_reduce); an unsplit launch applies the epilogue itself.
 template <int LA, int LB, int BM, int BN, bool VEC, bool MASKED, int NT>
-__global__ __launch_bounds__(NT, BM == 64 ? 4 : 2) void gemm_f32_kernel(GemmF32Args a) {
+__global__ __launch_bounds__(NT, 2) void gemm_f32_kernel(GemmF32Args a) {
   // NT = 256: 4 waves in 2 x 2; NT = 512: 8 waves in 2 x 4 (each wave BM/2 x BN/4: four waves per
   // SIMD at two blocks per CU, so one wave's staging and barrier wait hide behind three others' MFMAs).
   // (A form with two in-block k groups for the 64 x 64 tile, summed through LDS, gave wrong input
@@ -188,10 +188,9 @@ __global__ __launch_bounds__(NT, BM == 64 ? 4 : 2) void gemm_f32_kernel(GemmF32A
 #pragma unroll
       for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
 
-  // P K-tiles of loads in flight in registers, two LDS stages, one barrier per K-tile (the 64x64 tile
-  // is compiled for 4 blocks per CU, <= 128 VGPRs, with 2 K-tiles in flight: 2,530-2,544 fp32 engine
-  // MLP iters/s against 2,410-2,465 with 3 in flight at 2 blocks per CU, r4_gemm_f32_occ4_ab.txt;
-  // splitting K further to fill those 4 slots measured slower): iteration i
+  // P K-tiles of loads in flight in registers, two LDS stages, one barrier per K-tile (2 K-tiles in
+  // flight for the 64x64 tile too: the fp32 engine MLP 2,551-2,562 iters/s against 2,410-2,465 with
+  // 3; compiled for 4 blocks per CU instead, 2,530-2,558: r4_gemm_f32_occ4_ab.txt): iteration i
   // writes tile i + 1 into the stage tile i - 1 was read from, refills its registers with tile
   // i + 1 + P (clamped to the slice: re-reads of the last tile, never consumed), then consumes tile i.
   constexpr int P = 2;
