@@ -1,0 +1,16 @@
+#!/bin/bash
+# Driver-shape headline on the final tree, 8 fresh processes (bench.py --gpus 1 --steps 20 --warmup 5).
+set -o pipefail
+O=gpurun_out/r4hf
+mkdir -p $O
+: > $O/driver8.txt
+for i in 1 2 3 4 5 6 7 8; do
+  DGT_BENCH_BREAKDOWN=1 timeout -k 10 200 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/drv_$i.json 2> $O/drv_$i.err || { tail -20 $O/drv_$i.err; exit 1; }
+  python -c "import json; d=json.loads(open('$O/drv_$i.json').read().strip().splitlines()[-1]); print(d['value'], d['ms_per_step'])" | tee -a $O/driver8.txt
+  grep "timed region" $O/drv_$i.err | tee -a $O/driver8.txt
+done
+python - <<'PY'
+import statistics
+v=[float(l.split()[0]) for l in open('gpurun_out/r4hf/driver8.txt') if l[0].isdigit()]
+print('median', statistics.median(v), 'min', min(v), 'max', max(v))
+PY
