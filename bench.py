@@ -573,16 +573,16 @@ class DgtEngineBench(EngineBench):
         opt = torch.optim.Adam(model.parameters(), lr=1e-3)
         self.engine, _, _, _ = initialize(model=model, optimizer=opt, model_parameters=model.parameters(), config=cfg)
         from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
-        crit = BCEWithLogitsLoss()  # fused HIP loss + gradient kernel
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=device)
+        # fused HIP loss + gradient kernel, which also adds the loss into the device-side loss log
+        # (the reference's loss.item() sum, train.py:115) -- no launch of its own
+        crit = BCEWithLogitsLoss(sum_into=self.loss_acc)
 
         def loss_fn(rows):
-            # the batch gather and the device-side loss log (the reference's loss.item() sum,
-            # train.py:115) are part of the step, so a HIP graph captures them with it
-            # the batch gather as index_select (one kernel; advanced indexing costs ~3x the host time)
-            loss = crit(self.engine(torch.index_select(self.x, 0, rows)).float(), torch.index_select(self.y, 0, rows))
-            self.loss_acc.add_(loss.detach())
-            return loss
+            # the batch gather and the loss log are part of the step, so a HIP graph captures them
+            # with it; the batch gather as index_select (one kernel; advanced indexing costs ~3x the
+            # host time)
+            return crit(self.engine(torch.index_select(self.x, 0, rows)).float(), torch.index_select(self.y, 0, rows))
 
         if self.engine.config.amd.hip_graph:
             self.step = self.engine.graph_step(loss_fn)

@@ -472,7 +472,7 @@ void colsum_f32(const at::Tensor& dy, const std::optional<at::Tensor>& y, const 
 }
 
 void bce_logits(const at::Tensor& z, const at::Tensor& y, const at::Tensor& loss, const at::Tensor& dz,
-                const std::optional<at::Tensor>& dz_lp) {
+                const std::optional<at::Tensor>& dz_lp, const std::optional<at::Tensor>& sum_into) {
   TORCH_CHECK(z.is_cuda() && z.is_contiguous() && (z.scalar_type() == at::kFloat || z.scalar_type() == at::kBFloat16),
               "dgt: bce_logits needs contiguous fp32 / bf16 GPU logits");
   check_gpu(y, "y", at::kFloat);
@@ -486,9 +486,15 @@ void bce_logits(const at::Tensor& z, const at::Tensor& y, const at::Tensor& loss
     TORCH_CHECK(dz_lp->numel() == z.numel(), "dgt: bce_logits dz_lp size mismatch");
     lp = dz_lp->data_ptr();
   }
+  double* acc = nullptr;
+  if (sum_into.has_value()) {
+    check_gpu(*sum_into, "sum_into", at::kDouble);
+    TORCH_CHECK(sum_into->numel() == 1, "dgt: bce_logits sum_into must hold one fp64 value");
+    acc = sum_into->data_ptr<double>();
+  }
   c10::DeviceGuard guard(z.device());
   DGT_CHECK_HIP(dgt::bce_logits(z.data_ptr(), dtype_code(z.scalar_type()), y.data_ptr<float>(), z.numel(),
-                                loss.data_ptr<float>(), dz.data_ptr<float>(), lp, stream_of(z)));
+                                loss.data_ptr<float>(), dz.data_ptr<float>(), lp, acc, stream_of(z)));
 }
 
 void tiny_mlp_grad(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& plan, const at::Tensor& counts,
@@ -1091,7 +1097,7 @@ TORCH_LIBRARY(dgt, m) {
       "Tensor? grad_scale_dev, Tensor? step_dev=None) -> ()",
       &adam_flat);
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
-  m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz, Tensor(c!)? dz_lp=None) -> ()", &bce_logits);
+  m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz, Tensor(c!)? dz_lp=None, Tensor(d!)? sum_into=None) -> ()", &bce_logits);
   m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
   m.def("gemm_f32(Tensor A, Tensor B, Tensor? maskA, Tensor? bias, Tensor(a!) C, int la, int lb, bool relu=False, "
         "bool accumulate=False, Tensor(b!)? rowsum=None, Tensor? maskC=None) -> ()",

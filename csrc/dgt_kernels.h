@@ -93,7 +93,7 @@ hipError_t linear_fwd(const float* x, const float* W, const float* b, float* y, 
 hipError_t linear_bwd(const float* dy, const float* x, const float* W, const float* y, float* dx, float* dW,
                       float* db, int M, int N, int K, bool accumulate, hipStream_t stream);
 hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz, void* dz_lp,
-                      hipStream_t stream);
+                      double* sum_into, hipStream_t stream);
 
 // ---------------------------------------------------------------- exact-fp32 MFMA GEMM (gemm_f32.hip)
 // C[M, N] (+)= epi(sum_k A(m, k) B(n, k)); A layout la: 0 = [M][K] (lda), 1 = [K][M]; B layout

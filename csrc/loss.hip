@@ -21,7 +21,8 @@ DGT_DEVICE float to_f<__hip_bfloat16>(__hip_bfloat16 v) { return __bfloat162floa
 template <typename T>
 __global__ __launch_bounds__(1024) void bce_logits_kernel(const T* __restrict__ z, const float* __restrict__ y, long long n,
                                                           float* __restrict__ loss, float* __restrict__ dz,
-                                                          __hip_bfloat16* __restrict__ dz_lp) {
+                                                          __hip_bfloat16* __restrict__ dz_lp,
+                                                          double* __restrict__ sum_into) {
   __shared__ float red[32];
   const float inv_n = 1.f / (float)n;
   float acc = 0.f;
@@ -42,21 +43,23 @@ __global__ __launch_bounds__(1024) void bce_logits_kernel(const T* __restrict__ 
   if (threadIdx.x == 0) {
     float s = 0.f;
     for (int i = 0; i < (int)(blockDim.x >> 6); ++i) s += red[i];
-    *loss = s * inv_n;
+    const float l = s * inv_n;
+    *loss = l;
+    if (sum_into) *sum_into += (double)l;  // the loss log (train.py:115's running sum), as loss_acc += loss
   }
 }
 
 hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz, void* dz_lp,
-                      hipStream_t stream) {
+                      double* sum_into, hipStream_t stream) {
   if (n < 1) return hipErrorInvalidValue;
   const int threads = n >= 1024 ? 1024 : (int)((n + 63) / 64 * 64);
   if (z_dtype == kBF16)
     hipLaunchKernelGGL(bce_logits_kernel<__hip_bfloat16>, dim3(1), dim3(threads), 0, stream,
                        static_cast<const __hip_bfloat16*>(z), y, n, loss, dz,
-                       static_cast<__hip_bfloat16*>(dz_lp));
+                       static_cast<__hip_bfloat16*>(dz_lp), sum_into);
   else
     hipLaunchKernelGGL(bce_logits_kernel<float>, dim3(1), dim3(threads), 0, stream, static_cast<const float*>(z), y,
-                       n, loss, dz, static_cast<__hip_bfloat16*>(dz_lp));
+                       n, loss, dz, static_cast<__hip_bfloat16*>(dz_lp), sum_into);
   return hipGetLastError();
 }
 

@@ -352,8 +352,8 @@ class Engine:
         node = loss.grad_fn
         if node is None or type(node).__name__ != "_FusedBCEWithLogitsBackward":
             return None
-        nxt = node.next_functions
-        if len(nxt) != 2 or nxt[1][0] is not None:
+        nxt = node.next_functions  # (logits, targets[, sum_into])
+        if len(nxt) < 2 or any(e[0] is not None for e in nxt[1:]):
             return None  # the targets need a gradient too
         cur = nxt[0][0]
         while cur is not None and type(cur).__name__ in self._VIEW_NODES + ("ToCopyBackward0",):
@@ -471,8 +471,8 @@ class Engine:
         node = loss.grad_fn
         if node is None or type(node).__name__ != "_FusedBCEWithLogitsBackward":
             return False
-        nxt = node.next_functions
-        if len(nxt) != 2 or nxt[1][0] is not None:
+        nxt = node.next_functions  # (logits, targets[, sum_into])
+        if len(nxt) < 2 or any(e[0] is not None for e in nxt[1:]):
             return False
         views = []
         cur = nxt[0][0]

@@ -13,6 +13,8 @@ bit for bit what ``dz * 1`` cast to bf16 gives.  Any other seed is one multiply.
 """
 from __future__ import annotations
 
+from typing import Optional
+
 import torch
 import torch.nn.functional as F
 
@@ -37,13 +39,13 @@ def _is_unit(g: torch.Tensor) -> bool:
 
 class _FusedBCEWithLogits(torch.autograd.Function):
     @staticmethod
-    def forward(ctx, z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    def forward(ctx, z: torch.Tensor, y: torch.Tensor, sum_into=None) -> torch.Tensor:
         zc = z.contiguous().reshape(-1)
         yc = y.reshape(-1).to(torch.float32).contiguous()
         loss = torch.empty(1, dtype=torch.float32, device=z.device)
         dz = torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
         lp = torch.empty(zc.numel(), dtype=torch.bfloat16, device=z.device) if z.dtype == torch.bfloat16 else None
-        _ext.require().bce_logits(zc, yc, loss, dz, lp)
+        _ext.require().bce_logits(zc, yc, loss, dz, lp, sum_into)
         ctx.save_for_backward(dz, lp)
         ctx.shape, ctx.dtype = z.shape, z.dtype
         return loss.view(())
@@ -52,23 +54,37 @@ class _FusedBCEWithLogits(torch.autograd.Function):
     def backward(ctx, g: torch.Tensor):
         dz, lp = ctx.saved_tensors
         if _is_unit(g):
-            return (lp if lp is not None else dz).view(ctx.shape), None
+            return (lp if lp is not None else dz).view(ctx.shape), None, None
         # scaled and cast to the logits' dtype in one pass (the fp32 product, rounded once)
         gz = torch.empty(ctx.shape, dtype=ctx.dtype, device=dz.device)
         torch.mul(dz.view(ctx.shape), g, out=gz)
-        return gz, None
+        return gz, None, None
 
 
-def bce_with_logits(z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-    """Mean BCE-with-logits; the fused HIP kernel on GPU fp32 / bf16 logits."""
+def bce_with_logits(z: torch.Tensor, y: torch.Tensor, sum_into: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """Mean BCE-with-logits; the fused HIP kernel on GPU fp32 / bf16 logits.  ``sum_into`` (one fp64
+    element on the logits' device): the loss is also added to it -- a training loop's running loss
+    log (the reference's per-step ``loss.item()`` sum, train.py:115) as ``sum_into += loss``, inside
+    the loss kernel instead of a launch of its own."""
+    if sum_into is not None and (sum_into.dtype != torch.float64 or sum_into.numel() != 1
+                                 or sum_into.device != z.device):
+        raise ValueError("bce_with_logits: sum_into must be one fp64 element on the logits' device")
     if (z.is_cuda and z.dtype in (torch.float32, torch.bfloat16) and z.numel() == y.numel() and z.numel() > 0
             and _ext.require() is not None):  # on the GPU a missing extension is an error, not a fallback
-        return _FusedBCEWithLogits.apply(z, y)
-    return F.binary_cross_entropy_with_logits(z, y.to(z.dtype))
+        return _FusedBCEWithLogits.apply(z, y, sum_into)
+    loss = F.binary_cross_entropy_with_logits(z, y.to(z.dtype))
+    if sum_into is not None:
+        sum_into.add_(loss.detach())
+    return loss
 
 
 class BCEWithLogitsLoss(torch.nn.Module):
-    """Drop-in for ``nn.BCEWithLogitsLoss()`` (mean reduction, no weights)."""
+    """Drop-in for ``nn.BCEWithLogitsLoss()`` (mean reduction, no weights); ``sum_into``: see
+    :func:`bce_with_logits`."""
+
+    def __init__(self, sum_into: Optional[torch.Tensor] = None):
+        super().__init__()
+        self.sum_into = sum_into
 
     def forward(self, z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
-        return bce_with_logits(z, y)
+        return bce_with_logits(z, y, self.sum_into)

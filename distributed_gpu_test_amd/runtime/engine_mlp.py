@@ -27,8 +27,9 @@ class EngineMLPTrainer:
         self.X, self.Y = x.to(self.device, self.engine.dtype), y.to(self.device)
         self.loss_acc = torch.zeros(1, dtype=torch.float64, device=self.device)
         # the framework's drop-in for nn.BCEWithLogitsLoss (one HIP kernel: loss + d loss / d logits),
-        # as train.py uses on the engine path; it reads the bf16 logits as they are
-        self.crit = BCEWithLogitsLoss()
+        # as train.py uses on the engine path; it reads the bf16 logits as they are and adds the loss
+        # into the fp64 loss log in the same kernel (sum_into)
+        self.crit = BCEWithLogitsLoss(sum_into=self.loss_acc)
         world = comm.get_world_size()
         self.exchange = "none" if world == 1 else f"{comm.backend_name()}-bucketed"
         self.impl = f"dgt-engine+mfma{self.engine.fused_linear_layers}+zero{self.engine.stage}"
@@ -50,7 +51,6 @@ class EngineMLPTrainer:
             loss = self.crit(self.engine(x).view(-1), y)
             self.engine.backward(loss)
             self.engine.step()
-            self.loss_acc.add_(loss.detach())  # fp32 loss added into the fp64 accumulator: one kernel
             self.global_steps += 1
 
     @property

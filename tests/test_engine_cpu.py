@@ -252,6 +252,13 @@ def test_fused_bce_falls_back_to_torch_on_cpu():
     loss.backward()
     ref.backward()
     assert torch.equal(loss, ref) and torch.equal(z.grad, ref_z.grad)
+    acc = torch.zeros(1, dtype=torch.float64)
+    BCEWithLogitsLoss(sum_into=acc)(z.detach(), y)
+    BCEWithLogitsLoss(sum_into=acc)(z.detach(), y)
+    assert torch.equal(acc, torch.zeros(1, dtype=torch.float64).add_(ref.detach()).add_(ref.detach()))
+    import pytest
+    with pytest.raises(ValueError):
+        BCEWithLogitsLoss(sum_into=torch.zeros(1))(z, y)  # fp64 only
 
 
 def test_inject_fused_linear_keeps_parameters_and_falls_back_on_cpu():
