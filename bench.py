@@ -25,9 +25,24 @@ queued behind the last step, then one sync), ``config.closing_barrier`` says whi
 the process count and ``oversubscribed`` is true when ranks share a device.  A run whose ranks end
 with different parameters exits non-zero and prints no headline line.
 
-``value`` is the whole-job aggregate: optimizer iterations per second summed over ranks
-(= N x global steps/s).  ``allreduce_busbw_GBps`` is the peak RCCL all-reduce bus bandwidth of a
-size sweep (8 B - 1 GiB) run after the timed region (rccl-tests convention, busbw = algbw x 2(n-1)/n).
+``value`` is the whole-job aggregate the driver contract asks for ("total tokens/s, not per-GPU";
+here: rank-iterations/s = N x global DP steps/s, i.e. samples/s / 4).  Under weak scaling it grows
+with N when the global step rate holds, so the driver's efficiency value_N / (N x value_1) is exactly
+global_steps_per_sec_N / global_steps_per_sec_1.  The reference's own iteration -- one synchronised DP
+step (``train.py:104-117``) -- is reported beside it as ``global_steps_per_sec``.
+
+``allreduce_busbw_GBps`` is the peak RCCL all-reduce bus bandwidth of a size sweep (8 B - 1 GiB) run
+after the timed region (rccl-tests convention, busbw = algbw x 2(n-1)/n).  The sweep runs in a
+worker thread under a wall-clock budget (``--sweep-budget-s``; it stops growing the size once the
+budget is spent) and a hard deadline: an RCCL error is recorded in ``allreduce_sweep_error`` and a
+hang ends the job after the headline line is printed, so neither can cost the headline.
+
+After the headline's timed region, and outside it, the same guarded runner times BASELINE config #2
+(``bf16_mlp``: SyntheticMLP(4096, 4), batch 1024 per GPU, bf16 MFMA GEMMs, MLPTrainer), the fp32
+engine MLP (``fp32_engine_mlp``: SyntheticMLP(1024, 4) through the DeepSpeed-style engine on the
+exact-fp32 MFMA GEMM) and, at N > 1, the ZeRO-1 variant of config #2 (``bf16_mlp_zero1``, config #5)
+-- each a short warmup + timed block with its own ms_per_step / iters_per_s / model_tflops
+(``--no-secondary`` turns them off; a failure is recorded as ``error`` in its block).
 """
 from __future__ import annotations
 
@@ -74,6 +89,27 @@ def parse_args(argv=None):
                     help="mlp: gradient wire dtype (DeepSpeed communication_data_type; default bf16)")
     ap.add_argument("--no-sweep", action="store_true", help="skip the all-reduce bus bandwidth sweep")
     ap.add_argument("--sweep-max-mb", type=int, default=1024)  # rccl-tests range: 8 B .. 1 GiB
+    ap.add_argument("--force-sweep", action="store_true",
+                    help="run the all-reduce sweep on any backend/device (gloo on the CPU: tests)")
+    ap.add_argument("--sweep-budget-s", type=float, default=60.0,
+                    help="stop growing the sweep's message size once this much wall time is spent")
+    ap.add_argument("--pg-timeout-s", type=float, default=180.0,
+                    help="process-group timeout (a hung collective becomes an error after this long)")
+    ap.add_argument("--no-secondary", action="store_true",
+                    help="skip the post-headline bf16 MLP / fp32 engine MLP blocks")
+    ap.add_argument("--secondary-steps", type=int, default=50)
+    ap.add_argument("--secondary-warmup", type=int, default=10)
+    ap.add_argument("--secondary-budget-s", type=float, default=90.0,
+                    help="hard deadline for each secondary block (setup + warmup + timed steps)")
+    # N > 1 knobs, echoed in the JSON config so a scaling run is self-describing
+    ap.add_argument("--schedule", default=None, choices=["auto", "overlap", "serial", "flat"],
+                    help="mlp: optimizer schedule (MLPTrainer; auto = flat at N=1, overlap at N>1)")
+    ap.add_argument("--bucket-mb", type=float, default=None,
+                    help="gradient bucket size in MiB: mlp = MLPTrainer's all-reduce buckets (default one per "
+                         "layer); dgt-engine = zero_optimization.reduce_bucket_size")
+    ap.add_argument("--oneshot-max-bytes", type=int, default=None,
+                    help="dgt-engine: amd.oneshot_max_bytes (buckets at or below go over the IPC one-shot "
+                         "all-reduce instead of RCCL)")
     return ap.parse_known_args(argv)[0]
 
 
@@ -139,11 +175,20 @@ def oneshot_sweep(device, world: int, max_bytes: int = 1024 * 1024):
         ch.close()
 
 
-def allreduce_sweep(device, max_mb: int, world: int):
-    """RCCL all-reduce bus bandwidth over message sizes (rccl-tests all_reduce_perf columns)."""
-    results = []
-    if world < 2:
+def allreduce_sweep(device, max_mb: int, world: int, budget_s: float = 60.0, out: "list | None" = None):
+    """RCCL all-reduce bus bandwidth over message sizes (rccl-tests all_reduce_perf columns).
+
+    Runs at N > 1, or at N = 1 under ``DGT_FORCE_COLLECTIVES=1`` (a 1-rank RCCL communicator: algbw
+    only, busbw is 0 by the 2(n-1)/n convention), so the code has run on hardware before a scaling
+    box runs it.  Once ``budget_s`` of wall time is spent the size stops growing; the decision is
+    all-reduced (MAX) so every rank leaves the loop at the same size.  Results are appended to
+    ``out`` as they come, so a caller that gave up waiting still has the finished sizes."""
+    from distributed_gpu_test_amd.parallel import comm
+    results = [] if out is None else out
+    if world < 2 and not comm.force_collectives():
         return results
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
+    start = time.perf_counter()
     size = 8
     while size <= max_mb * 1024 * 1024:
         n = max(1, size // 4)
@@ -151,18 +196,123 @@ def allreduce_sweep(device, max_mb: int, world: int):
         iters = 20 if size <= (1 << 22) else 5
         for _ in range(3):
             dist.all_reduce(t)
-        torch.cuda.synchronize()
+        sync()
         dist.barrier()
         t0 = time.perf_counter()
         for _ in range(iters):
             dist.all_reduce(t)
-        torch.cuda.synchronize()
+        sync()
         dt = (time.perf_counter() - t0) / iters
+        dt = comm.all_reduce_max(dt)  # the slowest rank's time, as rccl-tests reports
         algbw = n * 4 / dt / 1e9
         results.append({"bytes": n * 4, "us": dt * 1e6, "algbw_GBps": algbw,
                         "busbw_GBps": algbw * 2 * (world - 1) / world})
+        del t
+        if comm.all_reduce_max(float(time.perf_counter() - start > budget_s)) > 0:
+            break
         size *= 4
     return results
+
+
+def run_bounded(fn, deadline_s: float, device=None):
+    """Run ``fn()`` in a daemon thread with a hard deadline: returns (result, error, hung).
+
+    The informational parts of the bench (collective sweeps, secondary workloads) go through here so
+    that neither an exception nor a hung collective costs the headline line: an exception comes back
+    as ``error``; a call still running at the deadline comes back as ``hung`` -- the caller then
+    issues no further collective (they would queue behind the stuck one), prints its line and ends
+    the process with ``os._exit``."""
+    import threading
+    box = {}
+
+    def target():
+        try:
+            if device is not None and device.type == "cuda":
+                torch.cuda.set_device(device)  # the current device is per thread
+            box["r"] = fn()
+        except BaseException as e:  # noqa: BLE001 -- recorded, never raised into the headline path
+            box["e"] = f"{type(e).__name__}: {e}"[:500]
+
+    th = threading.Thread(target=target, daemon=True, name="dgt-bench-bounded")
+    th.start()
+    th.join(deadline_s)
+    if th.is_alive():
+        return None, f"timeout: still running after {deadline_s:.0f} s", True
+    return box.get("r"), box.get("e"), False
+
+
+def timed_block(trainer, steps: int, warmup: int, device) -> float:
+    """W untimed steps, then K steps between barrier + sync on both sides; max over ranks (s)."""
+    from distributed_gpu_test_amd.parallel import comm
+    sync = torch.cuda.synchronize if device.type == "cuda" else (lambda: None)
+    plan, counts = build_plan(trainer, warmup + steps)
+    if warmup:
+        trainer.run_plan(plan[:warmup], counts[:warmup])
+    sync()
+    comm.barrier()
+    sync()
+    t0 = time.perf_counter()
+    trainer.run_plan(plan[warmup:], counts[warmup:])
+    sync()
+    comm.barrier()
+    sync()
+    return comm.all_reduce_max(time.perf_counter() - t0)
+
+
+def secondary_specs(args, device, world: int):
+    """The post-headline blocks: (key, description, factory) -- BASELINE config #2 (bf16 MLP on the
+    MFMA GEMMs), the fp32 engine MLP, and at N > 1 config #5 (ZeRO-1 of config #2)."""
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+
+    def bf16_mlp(zero_stage):
+        def make():
+            from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
+            torch.manual_seed(1234)
+            model = SyntheticMLP(4096, 4)
+            return MLPTrainer(model, batch_size=1024, lr=1e-4, device=device, zero_stage=zero_stage,
+                              schedule=args.schedule, bucket_mb=args.bucket_mb if zero_stage == 0 else None)
+        return make
+
+    def fp32_engine_mlp():
+        from distributed_gpu_test_amd.runtime.engine_mlp import EngineMLPTrainer
+        torch.manual_seed(1234)
+        cfg = json.load(open(os.path.join(ROOT, "configs", "ds_bench_mlp_fp32.json")))
+        cfg = dict(cfg, train_micro_batch_size_per_gpu=1024)
+        cfg.pop("train_batch_size", None)
+        return EngineMLPTrainer(SyntheticMLP(1024, 4), 1024, 8, cfg)
+
+    specs = [("bf16_mlp", "SyntheticMLP 4x[Linear(4096,4096)+ReLU] + Linear(4096,1), batch 1024/GPU, bf16 MFMA, "
+              "MLPTrainer, ZeRO-0 (BASELINE config #2)", bf16_mlp(0)),
+             ("fp32_engine_mlp", "SyntheticMLP 4x[Linear(1024,1024)+ReLU] + Linear(1024,1), batch 1024/GPU, fp32 "
+              "(exact-fp32 MFMA GEMM), DeepSpeed-style engine, configs/ds_bench_mlp_fp32.json", fp32_engine_mlp)]
+    if world > 1:
+        specs.append(("bf16_mlp_zero1", "as bf16_mlp with ZeRO-1: reduce-scatter + sharded Adam + all-gather "
+                      "(BASELINE config #5)", bf16_mlp(1)))
+    return specs
+
+
+def run_secondary(key: str, desc: str, make, args, device, world: int) -> dict:
+    """One secondary block (setup + warmup + timed steps); raises on failure (run_bounded catches)."""
+    tr = make()
+    try:
+        elapsed = timed_block(tr, args.secondary_steps, args.secondary_warmup, device)
+        gsps = args.secondary_steps / elapsed
+        flops = tr.flops_per_step()
+        return {"model": desc, "steps": args.secondary_steps, "warmup": args.secondary_warmup,
+                "ms_per_step": round(elapsed / args.secondary_steps * 1e3, 6),
+                "iters_per_s": round(gsps, 2),  # global DP steps/s
+                "iters_per_s_sum_over_ranks": round(gsps * world, 2),
+                "model_tflops": round(flops * world * gsps / 1e12, 2),
+                "dtype": getattr(tr, "dtype_name", "bf16"), "impl": tr.impl, "exchange": tr.exchange,
+                "zero_stage": getattr(tr, "zero_stage", 0), "schedule": getattr(tr, "schedule", None),
+                "bucket_mb": getattr(tr, "bucket_mb", None),
+                "mean_loss": round(float(tr.loss_acc.item()) / max(1, args.secondary_steps + args.secondary_warmup), 6)}
+    finally:
+        tr.close()
+        del tr
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
 
 
 def timed_run(trainer, plan, counts, args, device, comm):
@@ -307,7 +457,9 @@ def main(argv=None):
     from distributed_gpu_test_amd.parallel import comm
     from distributed_gpu_test_amd.runtime.tiny_trainer import TinyMLPTrainer
 
-    info = comm.init_distributed()
+    # a short process-group timeout: one hung collective becomes an error within minutes, well
+    # inside any driver limit, instead of after torch's default 30 minutes
+    info = comm.init_distributed(timeout_s=args.pg_timeout_s)
     world, rank = comm.get_world_size(), comm.get_rank()
     if args.gpus != world:
         print(f"[bench] note: --gpus {args.gpus} but WORLD_SIZE={world}; using {world}", file=sys.stderr)
@@ -326,20 +478,19 @@ def main(argv=None):
         if args.impl == "engine":
             trainer = TorchMLPBench(model, B, device)
         elif args.impl == "dgt-engine":
-            import json as _json
             from distributed_gpu_test_amd.runtime.engine_mlp import EngineMLPTrainer
-            cfg = _json.load(open(args.ds_config or os.path.join(ROOT, "configs", "ds_bench_mlp_bf16.json")))
+            cfg = engine_config(args, os.path.join(ROOT, "configs", "ds_bench_mlp_bf16.json"))
             cfg = dict(cfg, train_micro_batch_size_per_gpu=B)
             cfg.pop("train_batch_size", None)
             trainer = EngineMLPTrainer(model, B, 8, cfg)
         else:
             cdt = {None: None, "bf16": torch.bfloat16, "fp32": torch.float32}[args.comm_dtype]
             trainer = MLPTrainer(model, batch_size=B, lr=1e-4, device=device, zero_stage=args.zero_stage,
-                                 comm_dtype=cdt)
+                                 comm_dtype=cdt, schedule=args.schedule, bucket_mb=args.bucket_mb)
     elif args.impl == "engine":
         trainer = EngineBench(model, x, y, B, device)
     elif args.impl == "dgt-engine":
-        trainer = DgtEngineBench(model, x, y, B, device, args.ds_config)
+        trainer = DgtEngineBench(model, x, y, B, device, engine_config(args, None))
     else:
         trainer = TinyMLPTrainer(model, x, y, B, lr=1e-3, impl=args.impl if device.type == "cuda" else "torch",
                                  device=device, zero_stage=args.zero_stage)
@@ -381,14 +532,44 @@ def main(argv=None):
     devices = comm.all_gather_object(device_identity(device))
     n_devices = len(set(devices))
 
-    gpu_sweeps = not args.no_sweep and device.type == "cuda" and world > 1
-    sweep = allreduce_sweep(device, args.sweep_max_mb, world) if gpu_sweeps and comm.backend_name() == "nccl" else []
+    # ---- informational parts, after the headline's timed region: every one runs through
+    # run_bounded, so an error is recorded and a hang ends the job only after the line is printed
+    hung = None
+    collectives = world > 1 or comm.force_collectives()
+    sweep, sweep_error = [], None
+    if not args.no_sweep and collectives and (args.force_sweep or (device.type == "cuda" and
+                                                                   comm.backend_name() == "nccl")):
+        _, sweep_error, h = run_bounded(
+            functools.partial(allreduce_sweep, device, args.sweep_max_mb, world, args.sweep_budget_s, sweep),
+            args.sweep_budget_s + 120.0, device)
+        if sweep_error:
+            print(f"[bench] RCCL all-reduce sweep stopped: {sweep_error}", file=sys.stderr, flush=True)
+        hung = "allreduce_sweep" if h else None
     oneshot = []
-    if gpu_sweeps and fallback_reason is None:  # after an IPC failure the mailboxes are not retried
-        try:
-            oneshot = oneshot_sweep(device, world)
-        except Exception as e:  # the sweep is informational; never lose the headline number to it
-            print(f"[bench] one-shot sweep skipped: {e}", file=sys.stderr)
+    if not hung and not args.no_sweep and device.type == "cuda" and world > 1 and fallback_reason is None:
+        # (after an IPC failure the mailboxes are not retried)
+        res, err, h = run_bounded(functools.partial(oneshot_sweep, device, world), 120.0, device)
+        oneshot = res or []
+        if err:
+            print(f"[bench] one-shot sweep skipped: {err}", file=sys.stderr)
+        hung = "oneshot_sweep" if h else None
+    secondary = {}
+    if not hung and not args.no_secondary and args.model == "simple" and device.type == "cuda":
+        for key, desc, make in secondary_specs(args, device, world):
+            t_block = time.perf_counter()
+            res, err, h = run_bounded(functools.partial(run_secondary, key, desc, make, args, device, world),
+                                      args.secondary_budget_s, device)
+            block = res if res is not None else {"model": desc, "error": err}
+            block["block_wall_s"] = round(time.perf_counter() - t_block, 2)
+            secondary[key] = block
+            if err:
+                print(f"[bench] secondary block {key} failed: {err}", file=sys.stderr, flush=True)
+            if h:
+                hung = key
+                break
+            # a block that failed on one rank may have left the others mid-collective: stop there
+            if comm.all_reduce_max(float(err is not None)) > 0:
+                break
     small_os = min(oneshot, key=lambda r: abs(r["bytes"] - 5632)) if oneshot else None
     peak_busbw = max((r["busbw_GBps"] for r in sweep), default=None)
     small = min(sweep, key=lambda r: abs(r["bytes"] - 5632)) if sweep else None
@@ -407,7 +588,7 @@ def main(argv=None):
     out = {
         "metric": METRIC,
         "value": round(world * global_steps_per_s, 2),
-        "unit": "iters/s (sum over ranks)",
+        "unit": "iters/s, whole job (N ranks x global DP steps/s)",
         "n_gpus": n_devices,
         "steps": args.steps,
         "warmup": args.warmup,
@@ -421,7 +602,9 @@ def main(argv=None):
         "config": {"model": model_desc,
                    "global_batch": B * world, "seq_len": 1, "parallelism": f"dp{world}",
                    "micro_batch_per_gpu": B, "impl": trainer.impl, "exchange": trainer.exchange,
-                   "zero_stage": args.zero_stage, "closing_barrier": closing_barrier_kind(trainer, world)},
+                   "zero_stage": args.zero_stage, "closing_barrier": closing_barrier_kind(trainer, world),
+                   "schedule": getattr(trainer, "schedule", None), "bucket_mb": args.bucket_mb,
+                   "oneshot_max_bytes": args.oneshot_max_bytes, "pg_timeout_s": args.pg_timeout_s},
         "global_steps_per_sec": round(global_steps_per_s, 2),
         "samples_per_sec": round(global_steps_per_s * B * world, 2),
         "mean_loss": round(mean_loss, 6),
@@ -437,12 +620,39 @@ def main(argv=None):
         "allreduce_sweep": [{k: round(v, 3) for k, v in r.items()} for r in sweep],
         "oneshot_xgmi_sweep": [{k: (round(v, 3) if isinstance(v, float) else v) for k, v in r.items()}
                                for r in oneshot],
+        "allreduce_sweep_error": sweep_error,
+        "hung": hung,
     }
+    out.update(secondary)
     if rank == 0:
         print(json.dumps(out), flush=True)
+    if hung:
+        # a collective is stuck in a worker thread: a barrier or destroy would queue behind it.  The
+        # line is out; end this rank now (every rank reaches its own deadline the same way)
+        print(f"[bench] {hung} hung; exiting without process-group teardown", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        sys.stderr.flush()
+        os._exit(0)
     trainer.close()
     comm.destroy()
     return 0
+
+
+def engine_config(args, default_path):
+    """The dgt-engine DeepSpeed config (``--deepspeed-config``, else ``default_path``, else the
+    reference's in-code dict) with the bench's N > 1 knobs applied."""
+    from distributed_gpu_test_amd.config import REFERENCE_DS_CONFIG
+    path = args.ds_config or default_path
+    cfg = json.load(open(path)) if path else json.loads(json.dumps(REFERENCE_DS_CONFIG))
+    if args.bucket_mb is not None:
+        z = dict(cfg.get("zero_optimization", {}))
+        z["reduce_bucket_size"] = z["allgather_bucket_size"] = max(1, int(args.bucket_mb * (1 << 20) / 4))
+        cfg["zero_optimization"] = z
+    if args.oneshot_max_bytes is not None:
+        a = dict(cfg.get("amd", {}))
+        a["oneshot_max_bytes"] = int(args.oneshot_max_bytes)
+        cfg["amd"] = a
+    return cfg
 
 
 class EngineBench:
@@ -558,13 +768,15 @@ class DgtEngineBench(EngineBench):
 
     impl = "dgt-engine"
 
-    def __init__(self, model, x, y, B, device, config_path=None):
-        import json
+    def __init__(self, model, x, y, B, device, cfg=None):
         from distributed_gpu_test_amd.config import REFERENCE_DS_CONFIG
         from distributed_gpu_test_amd.engine import initialize
         from distributed_gpu_test_amd.parallel import comm
         from distributed_gpu_test_amd import data as dgt_data
-        cfg = json.load(open(config_path)) if config_path else dict(REFERENCE_DS_CONFIG)
+        if cfg is None:
+            cfg = dict(REFERENCE_DS_CONFIG)
+        elif isinstance(cfg, str):
+            cfg = json.load(open(cfg))
         self._data = dgt_data
         self.device = device
         self.world, self.rank = comm.get_world_size(), comm.get_rank()

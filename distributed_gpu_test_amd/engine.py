@@ -148,10 +148,16 @@ class Engine:
                                    comm_dtype=comm_dtype, oneshot=self.oneshot,
                                    oneshot_max_bytes=config.amd.oneshot_max_bytes,
                                    debug_sync=config.amd.debug_sync_streams)
+        # ---- module forward/backward from HIP graphs under the eager API (amd.graph_module)
+        self.graph_module = bool(config.amd.graph_module and device.type == "cuda")
         # deferred zeroing needs a writer that STORES gradients (the bf16 MFMA chain, the fp32 fused
-        # Linear kernels) and no collective
+        # Linear kernels) and no collective.  Not with graph_module: a graphed backward ADDS into the
+        # flat buckets (its captured kernels cannot tell a stale buffer from a fresh one), so after an
+        # eager step that deferred its zero fill the next graphed step would add onto stale gradients
+        # (ADVICE r4); there the graphed tail zeroes the bucket inside its own replay instead
         self._defer_capable = (device.type == "cuda" and self.world_size == 1 and config.amd.defer_zero_grad
-                               and self.dtype in (torch.bfloat16, torch.float32) and self.fused_linear_layers > 0)
+                               and self.dtype in (torch.bfloat16, torch.float32) and self.fused_linear_layers > 0
+                               and not self.graph_module)
         self._hooks = []
         self._own_tensor_hooks = set()  # ids of the engine's own tensor hooks (the direct backward runs them)
         for i, p in enumerate(self.params):
@@ -192,8 +198,6 @@ class Engine:
         self.training = True
         self.graphed = None
         self.graph_fallback_reason = ""
-        # ---- module forward/backward from HIP graphs under the eager API (amd.graph_module)
-        self.graph_module = bool(config.amd.graph_module and device.type == "cuda")
         self.graph_module_reason = ""
         self._graphed_fwd: Dict[tuple, Any] = {}
         # graphed tail (runtime/graph_module.py): backward + collective + Adam as one replay when

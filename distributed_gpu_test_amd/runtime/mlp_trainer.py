@@ -95,7 +95,7 @@ class MLPTrainer:
                  betas=(0.9, 0.999), eps: float = 1e-8, weight_decay: float = 0.0, seed: int = 1234,
                  device: Optional[torch.device] = None, zero_stage: int = 0, schedule: Optional[str] = None,
                  grad_dtype: Optional[torch.dtype] = None, comm_dtype: Optional[torch.dtype] = None,
-                 fuse_adam: Optional[bool] = None):
+                 fuse_adam: Optional[bool] = None, bucket_mb: Optional[float] = None):
         if zero_stage not in (0, 1):
             raise ValueError("MLPTrainer supports zero_stage 0 or 1")
         if comm_dtype not in (None, torch.bfloat16, torch.float32):
@@ -175,6 +175,7 @@ class MLPTrainer:
             self.shard_grad = torch.zeros(self.master_w.numel(), dtype=grad_dtype, device=dev)
             del w_full
         self.m_w, self.v_w = torch.zeros_like(self.master_w), torch.zeros_like(self.master_w)
+        self._plan_buckets(bucket_mb)
 
         def wview(buf, i):
             shape = named[f"layers.{i}.weight"].shape
@@ -257,6 +258,44 @@ class MLPTrainer:
             self.ev_opt = [torch.cuda.Event() for _ in range(self.L)]
 
     # ------------------------------------------------------------------ helpers
+    def _plan_buckets(self, bucket_mb: Optional[float]) -> None:
+        """The weight region's communication buckets (``bucket_mb`` / ``DGT_MLP_BUCKET_MB``).
+
+        Default (None): one bucket per layer matrix (33.5 MB bf16 at width 4096).  With a size, the
+        region is cut into contiguous pieces of that many MiB from its top (the last layer's end,
+        where backward starts), each a multiple of ALIGN x world_size elements: a layer larger than
+        the size leaves in several collectives, smaller layers share one.  A bucket leaves once the
+        wgrad of the lowest layer it touches is enqueued (``bucket_ready[i]``: buckets issued after
+        layer i's wgrad), and layer i's update waits for the last bucket covering it
+        (``update_after[i]``: the backward iteration that issues it).  ZeRO-1 keeps per-layer
+        buckets (its shards are per layer)."""
+        if bucket_mb is None and os.environ.get("DGT_MLP_BUCKET_MB"):
+            bucket_mb = float(os.environ["DGT_MLP_BUCKET_MB"])
+        L, esize = self.L, (2 if self.grad_dtype == torch.bfloat16 else 4)
+        quantum = ALIGN * self.world_size
+        if bucket_mb is None or self.zero_stage == 1:
+            self.bucket_mb = None
+            spans = [(self.w_off[i], self.w_off[i] + self.w_len[i]) for i in reversed(range(L))]
+        else:
+            if bucket_mb <= 0:
+                raise ValueError("bucket_mb must be positive")
+            self.bucket_mb = float(bucket_mb)
+            cap = max(quantum, int(bucket_mb * (1 << 20)) // esize // quantum * quantum)
+            spans, hi = [], self.total_w
+            while hi > 0:
+                spans.append((max(0, hi - cap), hi))
+                hi = spans[-1][0]
+
+        def layer_of(e: int) -> int:
+            return max(i for i in range(L) if self.w_off[i] <= e)
+
+        self.buckets = spans  # in issue order (descending memory = backward order)
+        self.bucket_ready: List[List[int]] = [[] for _ in range(L)]
+        for b, (lo, _) in enumerate(spans):
+            self.bucket_ready[layer_of(lo)].append(b)
+        # layer i is complete once the bucket holding its lowest element has been reduced
+        self.update_after = [layer_of(next(lo for lo, hi in spans if lo <= self.w_off[i] < hi)) for i in range(L)]
+
     def flops_per_step(self) -> int:
         return self.model.flops_per_sample() * self.B
 
@@ -282,12 +321,15 @@ class MLPTrainer:
             works.append(fn(out, *inp, async_op=True))
 
     def _reduce_layer(self, i: int, works: list) -> None:
+        """The collectives of the buckets that become ready with layer i's wgrad."""
         if not self.coll:
             return
-        bucket = self.grads_w[self.w_off[i]:self.w_off[i] + self.w_len[i]]
         if self.zero_stage == 0:
-            self._collective(dist.all_reduce, bucket, works=works)
+            for b in self.bucket_ready[i]:
+                lo, hi = self.buckets[b]
+                self._collective(dist.all_reduce, self.grads_w[lo:hi], works=works)
         else:
+            bucket = self.grads_w[self.w_off[i]:self.w_off[i] + self.w_len[i]]
             out = self.shard_grad[self.shard_off[i]:self.shard_off[i] + self.shard_len[i]]
             self._collective(dist.reduce_scatter_tensor, out, bucket, works=works)
 
@@ -390,12 +432,17 @@ class MLPTrainer:
                 cur ^= 1
             if ov:
                 self.ev_bwd[i].record(main)
-                self.s_opt.wait_event(self.ev_bwd[i])
-                if self.coll:
-                    self.s_opt.wait_event(self.ev_comm[i])
-                with torch.cuda.stream(self.s_opt):
-                    self._update_layer(i)
-                    self.ev_opt[i].record(self.s_opt)
+                # the layers whose last bucket left at this iteration (per-layer buckets: layer i);
+                # their dgrads (which read W) ran at iterations >= i, all enqueued before ev_bwd[i]
+                for u in reversed(range(i, L)):
+                    if self.update_after[u] != i:
+                        continue
+                    self.s_opt.wait_event(self.ev_bwd[i])
+                    if self.coll:
+                        self.s_opt.wait_event(self.ev_comm[i])
+                    with torch.cuda.stream(self.s_opt):
+                        self._update_layer(u)
+                        self.ev_opt[u].record(self.s_opt)
         small_done = self._reduce_small(with_adam=True)
         if self.coll:  # biases + head: one small replicated bucket
             self._collective(dist.all_reduce, self.grads_s, works=works)

@@ -126,3 +126,82 @@ def test_zero1_checksum_mismatch_detects_altered_transfers():
     bad = [x.clone() for x in xs]
     bad[1][2 * 6] ^= 1 << 20  # thread 6 owned by rank 0: rank 1 received an altered parameter
     assert "arrived altered on rank 1" in zero1_checksum_mismatch(bad, ws)
+
+
+def test_sweep_error_keeps_the_headline(monkeypatch, capsys):
+    """An RCCL error in the middle of the all-reduce sweep (here: dist.all_reduce raising from the
+    128 KiB size on) is recorded in ``allreduce_sweep_error``; the run still exits 0 with one headline
+    line that carries the sizes measured before the error."""
+    import torch.distributed as dist
+    import bench
+    real = dist.all_reduce
+
+    def flaky(t, *a, **k):
+        if t.numel() >= 16384:
+            raise RuntimeError("injected RCCL failure")
+        return real(t, *a, **k)
+
+    monkeypatch.setattr(dist, "all_reduce", flaky)
+    monkeypatch.setenv("DGT_FORCE_COLLECTIVES", "1")
+    monkeypatch.setenv("DGT_QUIET", "1")
+    rc = bench.main(["--steps", "20", "--warmup", "3", "--force-sweep", "--sweep-max-mb", "1"])
+    assert rc == 0
+    lines = _json_lines(capsys.readouterr().out)
+    assert len(lines) == 1
+    d = lines[0]
+    assert "injected RCCL failure" in d["allreduce_sweep_error"] and d["hung"] is None
+    assert [r["bytes"] for r in d["allreduce_sweep"]] == [8, 32, 128, 512, 2048, 8192, 32768]
+    assert d["value"] > 0 and d["steps"] == 20
+
+
+def test_run_bounded_error_and_deadline():
+    import time
+    import bench
+    assert bench.run_bounded(lambda: 7, 5.0) == (7, None, False)
+    r, err, hung = bench.run_bounded(lambda: 1 / 0, 5.0)
+    assert r is None and "ZeroDivisionError" in err and not hung
+    t0 = time.perf_counter()
+    r, err, hung = bench.run_bounded(lambda: time.sleep(30), 0.5)
+    assert hung and "timeout" in err and time.perf_counter() - t0 < 5
+
+
+def test_sweep_budget_stops_growing(monkeypatch):
+    """The sweep stops growing the message size once its wall-clock budget is spent."""
+    import torch
+    import torch.distributed as dist
+    import bench
+    from distributed_gpu_test_amd.parallel import comm
+    monkeypatch.setenv("DGT_FORCE_COLLECTIVES", "1")
+    comm.init_distributed(backend="gloo")
+    try:
+        out = bench.allreduce_sweep(torch.device("cpu"), 1024, 1, budget_s=0.0)
+        assert len(out) == 1 and out[0]["bytes"] == 8 and out[0]["busbw_GBps"] == 0.0
+    finally:
+        if dist.is_initialized():
+            dist.destroy_process_group()
+
+
+def test_secondary_block_cpu():
+    """A secondary block (here a small MLPTrainer on the CPU) reports its own timing keys."""
+    import argparse
+    import torch
+    import bench
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
+    args = argparse.Namespace(secondary_steps=3, secondary_warmup=1)
+    dev = torch.device("cpu")
+    blk = bench.run_secondary("bf16_mlp", "small", lambda: MLPTrainer(SyntheticMLP(128, 2), batch_size=128,
+                                                                      device=dev, bucket_mb=0.01), args, dev, 1)
+    assert blk["steps"] == 3 and blk["ms_per_step"] > 0 and blk["iters_per_s"] > 0
+    assert blk["model_tflops"] >= 0 and blk["bucket_mb"] == 0.01 and blk["mean_loss"] > 0
+
+
+def test_engine_config_knobs():
+    import argparse
+    import bench
+    a = argparse.Namespace(ds_config=None, bucket_mb=8.0, oneshot_max_bytes=4096)
+    cfg = bench.engine_config(a, os.path.join(ROOT, "configs", "ds_bench_mlp_fp32.json"))
+    assert cfg["zero_optimization"]["reduce_bucket_size"] == 2 * 1024 * 1024
+    assert cfg["amd"]["oneshot_max_bytes"] == 4096 and cfg["amd"]["fused_linear"] is True
+    cfg = bench.engine_config(argparse.Namespace(ds_config=None, bucket_mb=None, oneshot_max_bytes=None), None)
+    assert cfg["train_batch_size"] == 64  # the reference's in-code dict

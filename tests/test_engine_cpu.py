@@ -399,3 +399,34 @@ def test_zero_to_fp32_rejects_duplicated_index_shards(tmp_path):
     shards([0, 2], [2, 3])  # element 2 from both ranks
     with pytest.raises(RuntimeError, match="exactly once"):
         consolidate(str(tmp_path))
+
+
+def test_mlp_trainer_bucket_plan_cpu():
+    """MLPTrainer's gradient buckets (bench.py --bucket-mb): contiguous pieces from the top of the
+    weight region, each a multiple of ALIGN x world_size elements, issued after the wgrad of the
+    lowest layer they touch; every layer's update waits for the last bucket covering it."""
+    import torch
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.runtime.mlp_trainer import ALIGN, MLPTrainer
+    torch.manual_seed(0)
+    model = SyntheticMLP(width=128, depth=3)
+    per_layer = MLPTrainer(model, batch_size=64, n_batches=1, device=torch.device("cpu"))
+    L, n = 3, 128 * 128
+    assert per_layer.buckets == [(per_layer.w_off[i], per_layer.w_off[i] + per_layer.w_len[i]) for i in (2, 1, 0)]
+    assert per_layer.update_after == [0, 1, 2] and per_layer.bucket_mb is None
+    # 0.01 MiB of bf16 = 5,242 elements -> 5,184 (a multiple of 64): each layer in 4 pieces, the
+    # cuts not aligned with the layer boundaries
+    t = MLPTrainer(model, batch_size=64, n_batches=1, device=torch.device("cpu"), bucket_mb=0.01)
+    spans = t.buckets
+    assert spans[0][1] == t.total_w and spans[-1][0] == 0
+    assert all(a[0] == b[1] for a, b in zip(spans, spans[1:]))  # contiguous, descending
+    assert all((hi - lo) % ALIGN == 0 and hi - lo <= 5184 for lo, hi in spans)
+    assert sorted(b for bs in t.bucket_ready for b in bs) == list(range(len(spans)))
+    for i in range(L):
+        lo_layer = t.w_off[i]
+        last = next(lo for lo, hi in spans if lo <= lo_layer < hi)
+        assert t.update_after[i] == max(j for j in range(L) if t.w_off[j] <= last) <= i
+    # one bucket for everything: issued after layer 0's wgrad, every update after it
+    big = MLPTrainer(model, batch_size=64, n_batches=1, device=torch.device("cpu"), bucket_mb=64)
+    assert big.buckets == [(0, big.total_w)] and big.update_after == [0, 0, 0] and big.bucket_ready[0] == [0]
+    assert n * L <= big.total_w

@@ -180,6 +180,28 @@ def test_engine_graph_module_shape_cap_and_eval():
     engine.close()
 
 
+@pytest.mark.parametrize("bf16", [False, True])
+def test_engine_graph_module_after_eager_step_keeps_gradients(bf16):
+    """graph_module + the injected kernels, an eager step (a 5th input shape, past
+    MAX_GRAPHED_SHAPES) followed by graphed steps whose loss is torch's BCE (no graphed tail): the
+    graphed backward must not add onto the eager step's gradients, nor lose its own.  The whole
+    trajectory matches the engine without graph_module."""
+    sizes = [32, 8, 12, 16, 20, 32, 8, 20, 32, 32, 12, 20, 16]
+    g = torch.Generator().manual_seed(11)
+    batches = [(torch.randn(bs, 64, generator=g).cuda(), (torch.rand(bs, 1, generator=g) > 0.5).float().cuda())
+               for bs in sizes]
+    cfg = {"train_batch_size": 32, **({"bf16": {"enabled": True}} if bf16 else {})}
+    e1, l1, p1 = _run_engine(dict(cfg), batches)
+    e2, l2, p2 = _run_engine(dict(cfg, amd={"graph_module": True}), batches)
+    assert e2.graph_module and len(e2._graphed_fwd) == e2.MAX_GRAPHED_SHAPES
+    assert e2.fused_linear_layers > 0 and not e2._defer_capable
+    tol = dict(rtol=2e-2, atol=2e-3) if bf16 else dict(rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), **tol)
+    torch.testing.assert_close(p2.float(), p1.float(), **tol)
+    e1.close()
+    e2.close()
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("n,dtype", [(4, torch.float32), (1000, torch.float32), (5000, torch.bfloat16)])
 def test_fused_bce_matches_torch(n, dtype):

@@ -122,6 +122,9 @@ def test_mlp_trainer_zero1_matches_zero0():
     assert float(m.group(1)) == 0.0 and float(m.group(2)) == 0.0
     assert int(m.group(3)) * 2 == int(m.group(4))
     assert "reducescatter+allgather" in m.group(5)
+    # --bucket-mb: other bucket cuts of the same all-reduce are bit-identical
+    b = re.search(r"bucket_diff=(\S+) small_buckets=(\d+)", r.stdout)
+    assert b and float(b.group(1)) == 0.0 and int(b.group(2)) > 2, r.stdout[-2000:]
 
 
 def test_mpirun_style_launch_matches_oracle(tmp_path):
