@@ -370,7 +370,9 @@ class Engine:
             return None
         if len(runner.static_out) != 1 or runner.grad_out_idx != [0]:
             return None
-        dz, lp = node.saved_tensors
+        if getattr(node, "freed", True):
+            return None
+        dz, lp = node.dz, node.lp
         gout = runner.static_gout[0]
         if lp is not None and gout.dtype == lp.dtype:
             dz = lp  # the kernel's once-rounded bf16 copy: a plain copy into the graph's input
@@ -378,9 +380,16 @@ class Engine:
             return None
         return runner, dz
 
-    def _try_graphed_tail(self, loss: torch.Tensor) -> bool:
-        if (not self.graph_module or not self.training or self.gas != 1 or self.loss_scaler is not None
-                or self._grads_dirty or self.faults.spec is not None or self.config.wall_clock_breakdown):
+    def _try_graphed_tail(self, loss: torch.Tensor, retain_graph: bool = False) -> bool:
+        """The graphed tail runs the whole update inside ``backward`` (the captured graph zeroes the
+        bucket after Adam): code between backward and step would see zeroed ``.grad``.  So it is
+        skipped when the caller keeps the graph for another backward (``retain_graph``) or has set a
+        ``.grad`` itself -- both mean gradients are still to be combined before the update."""
+        if (retain_graph or not self.graph_module or not self.training or self.gas != 1
+                or self.loss_scaler is not None or self._grads_dirty or self.faults.spec is not None
+                or self.config.wall_clock_breakdown):
+            return False
+        if self.store.user_set_grads():
             return False
         found = self._tail_runner(loss)
         if found is None:
@@ -412,7 +421,7 @@ class Engine:
     def backward(self, loss: torch.Tensor, retain_graph: bool = False) -> torch.Tensor:
         if self._tail_done:
             raise RuntimeError("engine.backward called twice without engine.step() after a graphed-tail step")
-        if self._try_graphed_tail(loss):
+        if self._try_graphed_tail(loss, retain_graph):
             return loss
         loss = self.faults.maybe_corrupt_loss(loss, self.global_steps)
         boundary = self.is_gradient_accumulation_boundary()
@@ -499,13 +508,19 @@ class Engine:
         if any(p._backward_hooks and any(k not in own for k in p._backward_hooks) for p in leaves):
             return False  # a user's tensor hook sees the gradient before accumulation: autograd's job
         seed = self._unit_seed(loss.device)
-        with torch.no_grad():  # autograd runs backward functions with grad mode off (no create_graph)
+        from .ops.loss import direct_backward, release
+        with torch.no_grad(), direct_backward():  # grad mode off as under autograd (no create_graph)
             g = node.apply(seed)  # the unit seed: the saved d loss / d logits itself, no launch
             g = g[0] if isinstance(g, tuple) else g
             for v in views:  # reshapes / casts back to the chain's output
                 g = v(g)
                 g = g[0] if isinstance(g, tuple) else g
             res = cur.apply(g)
+        # what autograd does after a backward that does not retain the graph: the activations and
+        # d loss / d logits are freed now (not when the caller drops ``loss``), and a second
+        # backward through this graph raises instead of adding the gradients again
+        release(node)
+        release(cur)
         # backward outputs -> the tensor inputs the edges belong to (weights, then present biases)
         if kind == "_FusedChainFnBackward":
             grads = [gr for j, gr in enumerate(res[3:]) if j % 2 == 0 or cur.has_bias[j // 2]]
@@ -543,8 +558,8 @@ class Engine:
                     and type(scaled.grad_fn).__name__ == "_FusedBCEWithLogitsBackward")
         if not own_loss and (scaled is loss or scaled.grad_fn is None or scaled.grad_fn is loss.grad_fn):
             return None
-        if scaled.dim() != 0 or scaled.dtype != torch.float32:
-            return None
+        if scaled.dim() != 0 or scaled.dtype != torch.float32 or scaled.retains_grad:
+            return None  # (a retained .grad would alias the persistent seed)
         if torch.cuda.is_available() and torch.cuda.is_current_stream_capturing():
             return None
         return self._unit_seed(scaled.device)

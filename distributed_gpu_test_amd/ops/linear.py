@@ -34,6 +34,7 @@ import torch.nn.functional as F
 
 from ..models.synthetic_mlp import SyntheticMLP
 from . import _ext
+from .loss import FREED, keep_graph, release
 
 # > 0 while the engine runs a backward (Engine.backward / the graphed step): only then do the
 # in-place kernels add dW / db straight into the parameters' .grad views (the engine's flat
@@ -177,12 +178,20 @@ class _FusedLinearFn(torch.autograd.Function):
         # leaf parameters only (no reference cycle through ctx)
         ctx.grad_in_place = grad_in_place and weight.is_leaf and (bias is None or bias.is_leaf)
         ctx.params = (weight, bias) if ctx.grad_in_place else (None, None)
-        ctx.save_for_backward(x, weight, y if relu else None)
+        # the input and the weight as attributes (freed by the direct backward: ops/loss.py
+        # release), the output through save_for_backward (an attribute would be a reference cycle)
+        ctx.x, ctx.w, ctx.freed = x, weight, False
+        ctx.save_for_backward(y if relu else None)
         return y
 
     @staticmethod
     def backward(ctx, dy):
-        x, weight, y = ctx.saved_tensors
+        if ctx.freed:
+            raise RuntimeError(FREED)
+        (y,) = ctx.saved_tensors
+        x, weight = ctx.x, ctx.w
+        if not keep_graph():
+            release(ctx)
         dy = dy.contiguous()
         dx = torch.empty_like(x) if ctx.needs_input_grad[0] else None
         w_leaf, b_leaf = ctx.params
@@ -277,15 +286,22 @@ class _FusedChainFn(torch.autograd.Function):
         ctx.has_bias = tuple(b is not None for b in wb[1::2])
         ctx.grad_in_place = grad_in_place and all(p is None or p.is_leaf for p in wb)
         ctx.params = wb if ctx.grad_in_place else ()
-        ctx.save_for_backward(*acts, *wb[0::2])
+        # the input, the hidden activations and the weights as attributes (none of them an output:
+        # no reference cycle; freed by the direct backward, ops/loss.py release), the chain's output
+        # through save_for_backward
+        ctx.acts, ctx.ws, ctx.freed = acts[:-1], wb[0::2], False
+        ctx.save_for_backward(h)
         return h
 
     @staticmethod
     def backward(ctx, dy):
         ops = _ext.require()
+        if ctx.freed:
+            raise RuntimeError(FREED)
         L = len(ctx.relus)
-        saved = ctx.saved_tensors
-        acts, ws = saved[:L + 1], saved[L + 1:]
+        acts, ws = list(ctx.acts) + list(ctx.saved_tensors), ctx.ws
+        if not keep_graph():
+            release(ctx)
         active = ctx.grad_in_place and _in_place_active()
         grads = [None] * (2 * L)
         dy = dy.contiguous()

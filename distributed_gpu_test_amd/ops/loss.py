@@ -10,9 +10,19 @@ HIP-graph-replayed step every node costs a few microseconds whatever it computes
 Backward seeded with :func:`unit_seed` (the engine's persistent 1, never written) launches nothing:
 the gradient IS the saved d loss / d logits -- for bf16 logits the copy the kernel rounded once,
 bit for bit what ``dz * 1`` cast to bf16 gives.  Any other seed is one multiply.
+
+d loss / d logits is kept on the node as a plain attribute (it is an intermediate, not an output:
+no reference cycle) rather than through ``save_for_backward``, so the engine's direct backward
+(``engine._direct_backward``, which calls the node without the autograd engine) can free it the way
+autograd frees saved tensors; a backward that does not retain the graph frees it itself.  A second
+backward through a freed node raises autograd's own error.  With ``retain_graph`` the unit-seed
+path hands out a copy, so a consumer that edits its incoming gradient in place cannot alter the
+value a later backward reads.
 """
 from __future__ import annotations
 
+import contextlib
+import threading
 from typing import Optional
 
 import torch
@@ -32,6 +42,45 @@ def unit_seed(device: torch.device) -> torch.Tensor:
     return t
 
 
+FREED = ("Trying to backward through the graph a second time (or directly access saved tensors after they "
+         "have already been freed). Saved intermediate values of the graph are freed when you call .backward() "
+         "or autograd.grad(). Specify retain_graph=True if you need to backward through the graph a second time "
+         "or if you need to access saved tensors after calling backward.")
+
+
+_DIRECT = threading.local()
+
+
+def keep_graph() -> bool:
+    """Whether the running backward retains the graph: False inside :func:`direct_backward` (the
+    engine calling the nodes itself, never retaining), else autograd's answer (True outside any
+    backward)."""
+    if getattr(_DIRECT, "on", False):
+        return False
+    return torch._C._autograd._get_current_graph_task_keep_graph()
+
+
+@contextlib.contextmanager
+def direct_backward():
+    """Marks the engine's own calls of the nodes' backward (``engine._direct_backward``): a
+    backward that does not retain the graph."""
+    _DIRECT.on = True
+    try:
+        yield
+    finally:
+        _DIRECT.on = False
+
+
+def release(node) -> None:
+    """Free what the framework's fused loss / Linear nodes hold for backward (the direct backward's
+    counterpart of autograd's release of saved tensors)."""
+    for attr in ("dz", "lp", "acts", "ws", "x", "w"):
+        if hasattr(node, attr):
+            setattr(node, attr, None)
+    if hasattr(node, "freed"):
+        node.freed = True
+
+
 def _is_unit(g: torch.Tensor) -> bool:
     t = _UNIT.get(g.device)
     return t is not None and g.dim() == 0 and g.dtype == torch.float32 and g.data_ptr() == t.data_ptr()
@@ -46,15 +95,21 @@ class _FusedBCEWithLogits(torch.autograd.Function):
         dz = torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
         lp = torch.empty(zc.numel(), dtype=torch.bfloat16, device=z.device) if z.dtype == torch.bfloat16 else None
         _ext.require().bce_logits(zc, yc, loss, dz, lp, sum_into)
-        ctx.save_for_backward(dz, lp)
+        ctx.dz, ctx.lp, ctx.freed = dz, lp, False
         ctx.shape, ctx.dtype = z.shape, z.dtype
         return loss.view(())
 
     @staticmethod
     def backward(ctx, g: torch.Tensor):
-        dz, lp = ctx.saved_tensors
+        if ctx.freed:
+            raise RuntimeError(FREED)
+        dz, lp = ctx.dz, ctx.lp
+        keep = keep_graph()
+        if not keep:
+            release(ctx)
         if _is_unit(g):
-            return (lp if lp is not None else dz).view(ctx.shape), None, None
+            out = (lp if lp is not None else dz).view(ctx.shape)
+            return (out.clone() if keep else out), None, None
         # scaled and cast to the logits' dtype in one pass (the fp32 product, rounded once)
         gz = torch.empty(ctx.shape, dtype=ctx.dtype, device=dz.device)
         torch.mul(dz.view(ctx.shape), g, out=gz)

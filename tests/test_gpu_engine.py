@@ -194,7 +194,7 @@ def test_engine_graph_module_after_eager_step_keeps_gradients(bf16):
     e1, l1, p1 = _run_engine(dict(cfg), batches)
     e2, l2, p2 = _run_engine(dict(cfg, amd={"graph_module": True}), batches)
     assert e2.graph_module and len(e2._graphed_fwd) == e2.MAX_GRAPHED_SHAPES
-    assert e2.fused_linear_layers > 0 and not e2._defer_capable
+    assert not e2._defer_capable and (bf16 or e2.fused_linear_layers > 0)
     tol = dict(rtol=2e-2, atol=2e-3) if bf16 else dict(rtol=1e-5, atol=1e-6)
     torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), **tol)
     torch.testing.assert_close(p2.float(), p1.float(), **tol)
@@ -706,3 +706,42 @@ def test_engine_fp32_deferred_zero_grad_direct_backward(B, F):
     assert engines[0].direct_backwards == 5
     for e in engines:
         e.close()
+
+
+@pytest.mark.gpu
+def test_engine_direct_backward_frees_activations_and_refuses_second_backward():
+    """the direct backward frees the chain's activations and d loss / d logits
+    at once, as autograd's backward does (not when the caller drops ``loss``), and a second
+    backward through the same graph raises instead of adding the gradients again.  With
+    retain_graph the autograd path keeps them (and hands out a copy of the unit-seed gradient)."""
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    torch.manual_seed(13)
+    B, F = 8192, 256
+    engine = dgt.initialize(model=SyntheticMLP(F, 3), config={
+        "train_micro_batch_size_per_gpu": B, "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}})[0]
+    crit = BCEWithLogitsLoss()
+    g = torch.Generator().manual_seed(6)
+    x = torch.randn(B, F, generator=g).cuda()
+    y = (torch.rand(B, generator=g) > 0.5).float().cuda()
+    engine.backward(crit(engine(x).view(-1), y))  # warm: buffers, kernels
+    engine.step()
+    torch.cuda.synchronize()
+    loss = crit(engine(x).view(-1), y)
+    before = torch.cuda.memory_allocated()
+    engine.backward(loss)
+    torch.cuda.synchronize()
+    after = torch.cuda.memory_allocated()
+    assert engine.direct_backwards == 2
+    # 2 hidden activations of B x F fp32 (+ d loss / d logits) no longer held by the graph
+    assert before - after >= 2 * B * F * 4, (before, after)
+    with pytest.raises(RuntimeError, match="second time"):
+        loss.backward()
+    engine.step()
+    # retain_graph: the autograd path, the graph stays usable
+    loss = crit(engine(x).view(-1), y)
+    engine.backward(loss, retain_graph=True)
+    node = loss.grad_fn
+    assert node.dz is not None and not node.freed
+    engine.step()
+    engine.close()
