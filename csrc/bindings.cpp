@@ -371,7 +371,7 @@ void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, 
 }
 
 // Exact-fp32 MFMA GEMM (gemm_f32.hip): C[M, N] (+)= epi(A . B) with A [M, K] (la 0) or [K, M] (la 1),
-// B [N, K] (lb 0) or [K, N] (lb 1), all contiguous; split-K partials in a caching-allocator workspace.
+// B [N, K] (lb 0) or [K, N] (lb 1), all contiguous; one launch (K splits inside the workgroup).
 void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& maskA,
               const std::optional<at::Tensor>& bias, const at::Tensor& C, int64_t la, int64_t lb, bool relu,
               bool accumulate, const std::optional<at::Tensor>& rowsum, const std::optional<at::Tensor>& maskC) {
@@ -428,22 +428,12 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     if (a.rowsum && !accumulate) rowsum->zero_();
     return;
   }
-  // DGT_F32_MIN_BLOCKS (A/B knob, read once): the grid size split-K fills small products up to
-  static const int min_blocks = [] {
-    const char* e = std::getenv("DGT_F32_MIN_BLOCKS");
-    return e && *e ? std::max(1, std::atoi(e)) : 0;
+  // DGT_F32_CFG (A/B knob, read once): force a tile configuration (dgt::GemmF32Cfg)
+  static const int force_cfg = [] {
+    const char* e = std::getenv("DGT_F32_CFG");
+    return e && *e ? std::atoi(e) : -1;
   }();
-  dgt::GemmF32Plan plan = dgt::gemm_f32_plan(a.M, a.N, a.K, min_blocks);
-  static const int big_threads = [] {  // DGT_F32_BIG_THREADS=256|512 (A/B knob, read once)
-    const char* e = std::getenv("DGT_F32_BIG_THREADS");
-    return e && *e ? std::atoi(e) : 0;
-  }();
-  if (big_threads == 256 || big_threads == 512) plan.threads = big_threads;
-  at::Tensor ws;
-  if (plan.splits > 1) {
-    ws = at::empty({(int64_t)plan.splits * M * N + (a.rowsum ? (int64_t)plan.splits * M : 0)}, A.options());
-    a.ws = ws.data_ptr<float>();
-  }
+  const dgt::GemmF32Plan plan = dgt::gemm_f32_plan(a.M, a.N, a.K, force_cfg);
   DGT_CHECK_HIP(dgt::gemm_f32(a, (int)la, (int)lb, plan, stream_of(A)));
 }
 

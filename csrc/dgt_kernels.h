@@ -105,7 +105,6 @@ struct GemmF32Args {
   const float* maskA;
   const float* bias;
   float* C;
-  float* ws;  // split-K partials, splits * M * N floats (plan.splits > 1 only) [+ splits * M row sums]
   int M, N, K;
   long long lda, ldb, ldc;
   int relu;
@@ -117,13 +116,15 @@ struct GemmF32Args {
   // accumulated -- a dgrad writing the ReLU-masked gradient of the layer below directly
   const float* maskC;
 };
+// wave tile / workgroup shape: 128x64 waves in 2x2 (256x128 tiles), 64x64 waves in 2x2 (128x128),
+// 64x64 waves 1x2 with K split 2 (64x128), 64x64 waves with K split 4 (64x64)
+enum GemmF32Cfg : int { kF32Wave128 = 0, kF32Wave64 = 1, kF32Wave64Split2 = 2, kF32Wave64Split4 = 3 };
 struct GemmF32Plan {
-  bool big;     // 128x128 block tile (else 64x64)
-  int splits;   // split-K slices (1 = none)
-  int threads;  // 128x128 blocks: 512 (8 waves of 64 x 32) or 256 (4 waves of 64 x 64)
+  int cfg = kF32Wave64Split4;
 };
-// min_blocks: split K until the grid holds at least this many blocks (0 = auto: 2 blocks per CU)
-GemmF32Plan gemm_f32_plan(int M, int N, int K, int min_blocks = 0);
+// force_cfg >= 0: that configuration (A/B knob); else the largest wave tile that still gives every
+// SIMD a wave
+GemmF32Plan gemm_f32_plan(int M, int N, int K, int force_cfg = -1);
 hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& plan, hipStream_t stream);
 // db[n] (+)= sum_m dy[m][n] * (y ? 1[y[m][n] > 0] : 1) over row slices (part: slices * N floats)
 int colsum_f32_slices(int M, int N);

@@ -1,8 +1,9 @@
 """Exact-fp32 MFMA GEMM (csrc/gemm_f32.hip) against fp32/fp64 PyTorch references of the same ops.
 
 Every layout pair the Linear layers use (forward MK.NK, dgrad MK.KN, wgrad KM.KN; plus KM.NK),
-aligned and ragged shapes (the 16-byte staging path and the scalar one), the 128x128 and 64x64 tiles,
-split-K, and the epilogues (bias, ReLU, accumulate, ReLU mask on A).  Then the engine-facing ops:
+aligned and ragged shapes (the 16-byte load path and the scalar one), every tile configuration the
+planner picks (128x64 and 64x64 wave tiles, the in-workgroup K splits), K tails that are not a
+multiple of the chunk, and the epilogues (bias, ReLU, accumulate, ReLU mask on A).  Then the engine-facing ops:
 FusedLinear / FusedChain at shapes beyond the small-batch kernels, with autograd gradients compared
 to nn.Linear in fp32."""
 import pytest
@@ -48,7 +49,7 @@ SHAPES = [
     (2048, 2048, 512),    # aligned, 128x128 tiles
     (1000, 999, 1004),    # ragged M / N, K % 4 == 0 (16-byte staging with zero fill)
     (77, 130, 67),        # everything ragged, K odd (scalar staging)
-    (64, 64, 8192),       # tiny grid, long K: split-K
+    (64, 64, 8192),       # tiny grid, long K: the in-workgroup K split
     (3, 5, 7),            # degenerate
 ]
 
