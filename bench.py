@@ -93,6 +93,8 @@ def parse_args(argv=None):
                     help="run the all-reduce sweep on any backend/device (gloo on the CPU: tests)")
     ap.add_argument("--sweep-budget-s", type=float, default=60.0,
                     help="stop growing the sweep's message size once this much wall time is spent")
+    ap.add_argument("--sweep-deadline-s", type=float, default=None,
+                    help="hard deadline of the sweep thread (default: the budget + 120 s)")
     ap.add_argument("--pg-timeout-s", type=float, default=180.0,
                     help="process-group timeout (a hung collective becomes an error after this long)")
     ap.add_argument("--no-secondary", action="store_true",
@@ -541,7 +543,7 @@ def main(argv=None):
                                                                    comm.backend_name() == "nccl")):
         _, sweep_error, h = run_bounded(
             functools.partial(allreduce_sweep, device, args.sweep_max_mb, world, args.sweep_budget_s, sweep),
-            args.sweep_budget_s + 120.0, device)
+            args.sweep_deadline_s if args.sweep_deadline_s is not None else args.sweep_budget_s + 120.0, device)
         if sweep_error:
             print(f"[bench] RCCL all-reduce sweep stopped: {sweep_error}", file=sys.stderr, flush=True)
         hung = "allreduce_sweep" if h else None
@@ -554,7 +556,8 @@ def main(argv=None):
             print(f"[bench] one-shot sweep skipped: {err}", file=sys.stderr)
         hung = "oneshot_sweep" if h else None
     secondary = {}
-    if not hung and not args.no_secondary and args.model == "simple" and device.type == "cuda":
+    # (the driver runs the default: the fused headline; other --impl / --model runs skip the blocks)
+    if not hung and not args.no_secondary and args.model == "simple" and args.impl == "fused" and device.type == "cuda":
         for key, desc, make in secondary_specs(args, device, world):
             t_block = time.perf_counter()
             res, err, h = run_bounded(functools.partial(run_secondary, key, desc, make, args, device, world),

@@ -205,3 +205,22 @@ def test_engine_config_knobs():
     assert cfg["amd"]["oneshot_max_bytes"] == 4096 and cfg["amd"]["fused_linear"] is True
     cfg = bench.engine_config(argparse.Namespace(ds_config=None, bucket_mb=None, oneshot_max_bytes=None), None)
     assert cfg["train_batch_size"] == 64  # the reference's in-code dict
+
+
+def test_bench_sweep_hang_still_prints_headline():
+    """A hung collective in the sweep (rank 1 wedged) ends every rank at the sweep's deadline; rank 0
+    prints the headline line with ``hung`` set and the job exits 0 -- the scaling point survives."""
+    import time
+    env = dict(os.environ, DGT_QUIET="1", OMP_NUM_THREADS="1")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
+           f"--master-port={free_port()}", os.path.join(ROOT, "tests", "bench_hang_worker.py"), "--gpus", "2",
+           "--steps", "20", "--warmup", "3", "--force-sweep", "--sweep-max-mb", "1", "--sweep-deadline-s", "8"]
+    t0 = time.perf_counter()
+    r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = _json_lines(r.stdout)
+    assert len(lines) == 1, r.stdout
+    d = lines[0]
+    assert d["hung"] == "allreduce_sweep" and "timeout" in d["allreduce_sweep_error"]
+    assert d["value"] > 0 and d["ranks"] == 2
+    assert time.perf_counter() - t0 < 120
