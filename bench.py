@@ -570,8 +570,14 @@ def main(argv=None):
             if h:
                 hung = key
                 break
-            # a block that failed on one rank may have left the others mid-collective: stop there
-            if comm.all_reduce_max(float(err is not None)) > 0:
+            # a block that failed on one rank may have left the others mid-collective: stop there.
+            # (The agreement is itself a collective: bounded too, a wedged peer must not keep this
+            # rank from printing)
+            bad, _, h = run_bounded(functools.partial(comm.all_reduce_max, float(err is not None)), 60.0, device)
+            if h:
+                hung = f"{key}:agreement"
+                break
+            if bad is None or bad > 0:
                 break
     small_os = min(oneshot, key=lambda r: abs(r["bytes"] - 5632)) if oneshot else None
     peak_busbw = max((r["busbw_GBps"] for r in sweep), default=None)
