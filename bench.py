@@ -557,7 +557,9 @@ def main(argv=None):
         hung = "oneshot_sweep" if h else None
     secondary = {}
     # (the driver runs the default: the fused headline; other --impl / --model runs skip the blocks)
-    if not hung and not args.no_secondary and args.model == "simple" and args.impl == "fused" and device.type == "cuda":
+    # (ranks sharing a card -- a rehearsal on gloo -- would time host-staged collectives: skipped)
+    if (not hung and not args.no_secondary and args.model == "simple" and args.impl == "fused" and device.type == "cuda"
+            and n_devices == world):
         for key, desc, make in secondary_specs(args, device, world):
             t_block = time.perf_counter()
             res, err, h = run_bounded(functools.partial(run_secondary, key, desc, make, args, device, world),

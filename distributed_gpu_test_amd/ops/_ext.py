@@ -12,7 +12,8 @@ import threading
 import torch
 
 _PKG = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(_PKG, "_C.so")
+# DGT_EXT_LIB: an A/B build of the extension (tools/build_ext.py --variant) instead of the in-tree one
+LIB_PATH = os.environ.get("DGT_EXT_LIB") or os.path.join(_PKG, "_C.so")
 _lock = threading.Lock()
 _loaded = False
 _error: Exception | None = None

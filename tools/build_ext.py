@@ -57,14 +57,25 @@ def _run(cmd, verbose):
 
 # the fused tiny kernel reads every MFMA result straight back into VALU math: accumulators in
 # VGPRs save the v_accvgpr_read round trips (the GEMMs keep the compiler's AGPR choice)
-PER_FILE_FLAGS = {"tiny_mlp.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-amdgpu-sched-strategy=max-ilp"]}
+# The exact-fp32 GEMM's loop-carried accumulators: in the default AGPR form the register allocator
+# rotates them through v_accvgpr moves at every loop back-edge (96-190 moves per 128-512 MFMAs);
+# in VGPR form the loops hold MFMAs, loads and address arithmetic only
+_F32_GEMM = ["-mllvm", "-amdgpu-mfma-vgpr-form"]
+PER_FILE_FLAGS = {"tiny_mlp.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm", "-amdgpu-sched-strategy=max-ilp"],
+                  **{f"gemm_f32_l{a}{b}.hip": _F32_GEMM for a in "01" for b in "01"}}
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int = 8) -> str:
+def build(verbose: bool = False, force: bool = False, jobs: int = 8, variant: str = "", defines=()) -> str:
+    """``variant``: an A/B build of the whole extension with extra ``defines`` (-D) into
+    build/variants/<variant>/_C.so (load it with DGT_EXT_LIB=<path>); the default build is untouched."""
+    global BUILD, OUT
+    if variant:
+        BUILD = os.path.join(ROOT, "build", "variants", variant, "obj")
+        OUT = os.path.join(ROOT, "build", "variants", variant, "_C.so")
     os.makedirs(BUILD, exist_ok=True)
     os.makedirs(BIN, exist_ok=True)
     headers = glob.glob(os.path.join(CSRC, "*.h"))
-    common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-Wno-unused-result"]
+    common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-Wno-unused-result", *[f"-D{d}" for d in defines]]
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
     inc, tlib, abi = _torch_paths()
     jobs_list = []
@@ -127,8 +138,10 @@ def main(argv=None):
     ap.add_argument("-j", "--jobs", type=int, default=8)
     ap.add_argument("--sanitize", action="store_true",
                     help="also build host-ASan/UBSan copies of the standalone tools (build/bin/*_asan)")
+    ap.add_argument("--variant", default="", help="A/B build into build/variants/<name>/_C.so")
+    ap.add_argument("-D", "--define", action="append", default=[], help="extra preprocessor define (variants)")
     a = ap.parse_args(argv)
-    out = build(verbose=a.verbose, force=a.force, jobs=a.jobs)
+    out = build(verbose=a.verbose, force=a.force, jobs=a.jobs, variant=a.variant, defines=a.define)
     print(f"built {out}")
     if a.sanitize:
         for exe in build_sanitized(verbose=a.verbose, force=a.force):
