@@ -344,6 +344,50 @@ void linear_fwd(const at::Tensor& x, const at::Tensor& W, const std::optional<at
                                 (int)W.size(0), (int)W.size(1), relu, stream_of(x)));
 }
 
+// the two-layer chain in one launch (linear.hip linear2_*): x [M, K], W1 [H, K], W2 [O, H]
+float* opt_f32(const std::optional<at::Tensor>& t, const char* name, int64_t numel) {
+  if (!t.has_value() || !t->defined()) return nullptr;
+  check_gpu(*t, name, at::kFloat);
+  TORCH_CHECK(t->numel() == numel, "dgt: linear2 ", name, " has ", t->numel(), " elements, expected ", numel);
+  return t->data_ptr<float>();
+}
+
+bool linear2_fits(int64_t M, int64_t K, int64_t H, int64_t O) {
+  return M < (1 << 30) && K < (1 << 30) && H < (1 << 30) && O < (1 << 30) &&
+         dgt::linear2_fits((int)M, (int)K, (int)H, (int)O);
+}
+
+void linear2_fwd(const at::Tensor& x, const at::Tensor& W1, const std::optional<at::Tensor>& b1, const at::Tensor& W2,
+                 const std::optional<at::Tensor>& b2, const at::Tensor& h, const at::Tensor& y, bool relu1, bool relu2) {
+  for (const at::Tensor* t : {&x, &W1, &W2, &h, &y}) check_gpu(*t, "linear2 operand", at::kFloat);
+  const int64_t M = x.size(0), K = x.size(1), H = W1.size(0), O = W2.size(0);
+  TORCH_CHECK(x.dim() == 2 && W1.dim() == 2 && W1.size(1) == K && W2.dim() == 2 && W2.size(1) == H &&
+                  h.numel() == M * H && y.numel() == M * O && linear2_fits(M, K, H, O),
+              "dgt: linear2_fwd shapes: x [M, K], W1 [H, K], W2 [O, H], h [M, H], y [M, O], M * H <= 4096");
+  c10::DeviceGuard guard(x.device());
+  DGT_CHECK_HIP(dgt::linear2_fwd(x.data_ptr<float>(), W1.data_ptr<float>(), opt_f32(b1, "b1", H), W2.data_ptr<float>(),
+                                 opt_f32(b2, "b2", O), h.data_ptr<float>(), y.data_ptr<float>(), (int)M, (int)K, (int)H,
+                                 (int)O, relu1, relu2, stream_of(x)));
+}
+
+void linear2_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W1, const at::Tensor& h,
+                 const at::Tensor& W2, const std::optional<at::Tensor>& y, const std::optional<at::Tensor>& dx,
+                 const at::Tensor& dW1, const std::optional<at::Tensor>& db1, const at::Tensor& dW2,
+                 const std::optional<at::Tensor>& db2, bool relu1, bool acc1, bool acc2) {
+  for (const at::Tensor* t : {&dy, &x, &W1, &h, &W2, &dW1, &dW2}) check_gpu(*t, "linear2 operand", at::kFloat);
+  const int64_t M = x.size(0), K = x.size(1), H = W1.size(0), O = W2.size(0);
+  TORCH_CHECK(x.dim() == 2 && W1.dim() == 2 && W1.size(1) == K && W2.dim() == 2 && W2.size(1) == H &&
+                  h.numel() == M * H && dy.numel() == M * O && dW1.sizes() == W1.sizes() &&
+                  dW2.sizes() == W2.sizes() && linear2_fits(M, K, H, O),
+              "dgt: linear2_bwd shapes: dy [M, O], x [M, K], W1 / dW1 [H, K], h [M, H], W2 / dW2 [O, H]");
+  c10::DeviceGuard guard(x.device());
+  DGT_CHECK_HIP(dgt::linear2_bwd(dy.data_ptr<float>(), x.data_ptr<float>(), W1.data_ptr<float>(), h.data_ptr<float>(),
+                                 W2.data_ptr<float>(), opt_f32(y, "y", M * O), opt_f32(dx, "dx", M * K),
+                                 dW1.data_ptr<float>(), opt_f32(db1, "db1", H), dW2.data_ptr<float>(),
+                                 opt_f32(db2, "db2", O), (int)M, (int)K, (int)H, (int)O, relu1, acc1, acc2,
+                                 stream_of(x)));
+}
+
 void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, const std::optional<at::Tensor>& y,
                 const std::optional<at::Tensor>& dx, const at::Tensor& dW, const std::optional<at::Tensor>& db,
                 bool accumulate) {
@@ -1089,6 +1133,12 @@ TORCH_LIBRARY(dgt, m) {
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz, Tensor(c!)? dz_lp=None, Tensor(d!)? sum_into=None) -> ()", &bce_logits);
   m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
+  m.def("linear2_fwd(Tensor x, Tensor W1, Tensor? b1, Tensor W2, Tensor? b2, Tensor(a!) h, Tensor(b!) y, bool relu1, "
+        "bool relu2) -> ()",
+        &linear2_fwd);
+  m.def("linear2_bwd(Tensor dy, Tensor x, Tensor W1, Tensor h, Tensor W2, Tensor? y, Tensor(a!)? dx, Tensor(b!) dW1, "
+        "Tensor(c!)? db1, Tensor(d!) dW2, Tensor(e!)? db2, bool relu1, bool acc1, bool acc2) -> ()",
+        &linear2_bwd);
   m.def("gemm_f32(Tensor A, Tensor B, Tensor? maskA, Tensor? bias, Tensor(a!) C, int la, int lb, bool relu=False, "
         "bool accumulate=False, Tensor(b!)? rowsum=None, Tensor? maskC=None) -> ()",
         &gemm_f32);

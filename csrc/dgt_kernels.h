@@ -92,6 +92,14 @@ hipError_t linear_fwd(const float* x, const float* W, const float* b, float* y, 
                       hipStream_t stream);
 hipError_t linear_bwd(const float* dy, const float* x, const float* W, const float* y, float* dx, float* dW,
                       float* db, int M, int N, int K, bool accumulate, hipStream_t stream);
+// a two-layer chain Linear(K, H)(+ReLU) -> Linear(H, O)(+ReLU) in ONE workgroup (small batches: M * H
+// <= 4096, bitwise the two per-layer launches)
+bool linear2_fits(int M, int K, int H, int O);
+hipError_t linear2_fwd(const float* x, const float* W1, const float* b1, const float* W2, const float* b2, float* h,
+                       float* y, int M, int K, int H, int O, bool relu1, bool relu2, hipStream_t stream);
+hipError_t linear2_bwd(const float* dy, const float* x, const float* W1, const float* h, const float* W2,
+                       const float* y, float* dx, float* dW1, float* db1, float* dW2, float* db2, int M, int K, int H,
+                       int O, bool relu1, bool acc1, bool acc2, hipStream_t stream);
 hipError_t bce_logits(const void* z, int z_dtype, const float* y, long long n, float* loss, float* dz, void* dz_lp,
                       double* sum_into, hipStream_t stream);
 

@@ -187,7 +187,8 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32Args a) {
     // condition inside (a consumer under a branch lets the compiler sink the prefetch into that
     // branch, right in front of its MFMAs); sched_barrier keeps each load group in front of the
     // MFMAs it must overlap (left alone, the scheduler moves loads down next to their consumers to
-    // shorten register lifetimes, exposing the load latency every chunk).
+    // shorten register lifetimes, exposing the load latency every chunk).  (Spreading the loads one
+    // per R MFMAs instead, with sched_group_barrier, measured level: profiles/r5_gemm_f32_interleave_ab.txt)
     Frag<TM, H> fa0, fa1;
     Frag<TN, H> fb0, fb1;
     load(fa0, fb0, c0);
@@ -219,25 +220,23 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32Args a) {
   constexpr int RED_FLOATS = (WGK > 1 ? 4 * NACC * 64 : 0) + (ROWSUM ? 4 * TM * 4 * 64 : 0);
   __shared__ __attribute__((aligned(16))) float red[RED_FLOATS > 0 ? RED_FLOATS : 1];
   if constexpr (WGK > 1) {
+    // one 16-byte LDS access per accumulator tile and lane ([wave][tile][lane] x float4)
+    f32x4v* red4 = reinterpret_cast<f32x4v*>(red);
 #pragma unroll
     for (int t = 0; t < TM; ++t)
 #pragma unroll
-      for (int u = 0; u < TN; ++u)
-#pragma unroll
-        for (int r = 0; r < 4; ++r) red[((size_t)wave * NACC + (t * TN + u) * 4 + r) * 64 + lane] = acc[t][u][r];
+      for (int u = 0; u < TN; ++u) red4[((size_t)wave * TM * TN + t * TN + u) * 64 + lane] = acc[t][u];
     __syncthreads();
 #pragma unroll
     for (int t = 0; t < TM; ++t) {
       if (t % WGK != wk) continue;
 #pragma unroll
-      for (int u = 0; u < TN; ++u)
+      for (int u = 0; u < TN; ++u) {
+        f32x4v v = {0.f, 0.f, 0.f, 0.f};  // slice order from +0 (deterministic)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) {
-          float v = 0.f;
-#pragma unroll
-          for (int k = 0; k < WGK; ++k) v += red[((size_t)(wmn * WGK + k) * NACC + (t * TN + u) * 4 + r) * 64 + lane];
-          acc[t][u][r] = v;
-        }
+        for (int k = 0; k < WGK; ++k) v += red4[((size_t)(wmn * WGK + k) * TM * TN + t * TN + u) * 64 + lane];
+        acc[t][u] = v;
+      }
     }
   }
 
@@ -279,61 +278,98 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32Args a) {
     }
   }
 
-  // ---- epilogue: bias, ReLU, output mask, accumulate; KN products store float4s of 4 columns
+  // ---- epilogue: bias, ReLU, output mask, accumulate, as float4s of 4 adjacent columns where C's
+  // row stride allows: a KN product's interleaved column tiles already hold 4 adjacent columns per
+  // lane; an NK product's 16x16 tile holds one column per lane, so each quad of lanes transposes
+  // its 4x4 blocks first (two DPP butterflies: lane b of a quad then holds row 4q + b, the quad's 4
+  // columns) -- a quarter of the store instructions of per-column stores
   const int q = lane >> 4, j = lane & 15;
+  const bool c4 = VEC && (a.N & 3) == 0 && (a.ldc & 3) == 0 && (a.maskC == nullptr || ((uintptr_t)a.maskC & 15) == 0);
+  auto store4 = [&](int m, int n, f32x4v v) {
+    float* crow = a.C + (long long)m * a.ldc;
+    if (a.bias) v += *reinterpret_cast<const f32x4v*>(a.bias + n);
+    if (a.relu) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
+    }
+    if (a.maskC) {
+      const f32x4v mk = *reinterpret_cast<const f32x4v*>(a.maskC + (long long)m * a.N + n);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
+    }
+    f32x4v* dst = reinterpret_cast<f32x4v*>(crow + n);
+    if (a.accumulate) v += *dst;
+    *dst = v;
+  };
+  auto store1 = [&](int m, int n, float x) {
+    float* crow = a.C + (long long)m * a.ldc;
+    if (a.bias) x += a.bias[n];
+    if (a.relu) x = fmaxf(x, 0.f);
+    if (a.maskC && !(a.maskC[(long long)m * a.N + n] > 0.f)) x = 0.f;
+    if (a.accumulate) x += crow[n];
+    crow[n] = x;
+  };
 #pragma unroll
   for (int t = 0; t < TM; ++t) {
     if (WGK > 1 && t % WGK != wk) continue;
+    if constexpr (BK) {
 #pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      const int m = row_of<AK>(m0, t, 4 * q + r);
-      if (m >= a.M) continue;
-      float* crow = a.C + (long long)m * a.ldc;
-      const float* mrow = a.maskC ? a.maskC + (long long)m * a.N : nullptr;
-      if constexpr (BK) {
+      for (int r = 0; r < 4; ++r) {
+        const int m = row_of<AK>(m0, t, 4 * q + r);
+        if (m >= a.M) continue;
 #pragma unroll
         for (int G = 0; G < TN / 4; ++G) {
           const int n = n0 + 64 * G + 4 * j;
-          f32x4v v = {acc[t][4 * G][r], acc[t][4 * G + 1][r], acc[t][4 * G + 2][r], acc[t][4 * G + 3][r]};
-          const bool vec_st = VEC && n + 3 < a.N && (a.ldc & 3) == 0 && (a.N & 3) == 0;
-          if (vec_st) {
-            if (a.bias) v += *reinterpret_cast<const f32x4v*>(a.bias + n);
-            if (a.relu) {
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = fmaxf(v[e], 0.f);
-            }
-            if (mrow) {
-              const f32x4v mk = *reinterpret_cast<const f32x4v*>(mrow + n);
-#pragma unroll
-              for (int e = 0; e < 4; ++e) v[e] = mk[e] > 0.f ? v[e] : 0.f;
-            }
-            f32x4v* dst = reinterpret_cast<f32x4v*>(crow + n);
-            if (a.accumulate) v += *dst;
-            *dst = v;
+          const f32x4v v = {acc[t][4 * G][r], acc[t][4 * G + 1][r], acc[t][4 * G + 2][r], acc[t][4 * G + 3][r]};
+          if (c4) {
+            if (n < a.N) store4(m, n, v);
           } else {
 #pragma unroll
-            for (int e = 0; e < 4; ++e) {
-              if (n + e >= a.N) continue;
-              float x = v[e];
-              if (a.bias) x += a.bias[n + e];
-              if (a.relu) x = fmaxf(x, 0.f);
-              if (mrow && !(mrow[n + e] > 0.f)) x = 0.f;
-              if (a.accumulate) x += crow[n + e];
-              crow[n + e] = x;
-            }
+            for (int e = 0; e < 4; ++e)
+              if (n + e < a.N) store1(m, n + e, v[e]);
           }
         }
-      } else {
+      }
+    } else if (c4) {
+      const int b = j & 3;
+#pragma unroll
+      for (int u = 0; u < TN; ++u) {
+        f32x4v x = acc[t][u];
+        // 4x4 transpose within the quad: M[lane b][reg r] = (row r, col b) -> T[lane b][c] = M[c][b]
+        f32x4v y;
+#pragma unroll
+        for (int e = 0; e < 4; ++e)  // xor 2: quad_perm [2, 3, 0, 1]
+          y[e] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x[e]), 0x4E, 0xF, 0xF, false));
+        if (b & 2) {
+          x[0] = y[2];
+          x[1] = y[3];
+        } else {
+          x[2] = y[0];
+          x[3] = y[1];
+        }
+#pragma unroll
+        for (int e = 0; e < 4; ++e)  // xor 1: quad_perm [1, 0, 3, 2]
+          y[e] = __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x[e]), 0xB1, 0xF, 0xF, false));
+        if (b & 1) {
+          x[0] = y[1];
+          x[2] = y[3];
+        } else {
+          x[1] = y[0];
+          x[3] = y[2];
+        }
+        const int m = row_of<AK>(m0, t, 4 * q + b);
+        const int n = n0 + 16 * u + 4 * (j >> 2);
+        if (m < a.M && n < a.N) store4(m, n, x);
+      }
+    } else {
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        const int m = row_of<AK>(m0, t, 4 * q + r);
+        if (m >= a.M) continue;
 #pragma unroll
         for (int u = 0; u < TN; ++u) {
           const int n = n0 + 16 * u + j;
-          if (n >= a.N) continue;
-          float x = acc[t][u][r];
-          if (a.bias) x += a.bias[n];
-          if (a.relu) x = fmaxf(x, 0.f);
-          if (mrow && !(mrow[n] > 0.f)) x = 0.f;
-          if (a.accumulate) x += crow[n];
-          crow[n] = x;
+          if (n < a.N) store1(m, n, acc[t][u][r]);
         }
       }
     }
@@ -342,9 +378,11 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32Args a) {
 
 // VEC_OK / SCALAR_OK: which load paths this configuration is instantiated for (the scalar one only
 // for the K-split-4 64x64 configuration: compile time)
-template <int LA, int LB, int WTM, int WTN, int WGM, int WGN, int WGK, int H>
+// PLAIN: only the unmasked, row-sum-free instantiations (the 128x64 wave tile: its masked and
+// row-sum forms spill; dispatch routes those products to the 64x64 tile)
+template <int LA, int LB, int WTM, int WTN, int WGM, int WGN, int WGK, int H, bool PLAIN = false>
 hipError_t launch(const GemmF32Args& a, bool vec, hipStream_t stream) {
-  constexpr bool VEC_OK = true, SCALAR_OK = WTM == 64 && WTN == 64 && WGK == 4;
+  constexpr bool VEC_OK = true, SCALAR_OK = WTM == 64 && WTN == 64 && WGK == 4 && !PLAIN;
   constexpr int BM = WGM * WTM, BN = WGN * WTN;
   const int tiles = ((a.M + BM - 1) / BM) * ((a.N + BN - 1) / BN);
   const dim3 grid((unsigned)tiles), block(256);
@@ -355,7 +393,11 @@ hipError_t launch(const GemmF32Args& a, bool vec, hipStream_t stream) {
   // (the ReLU-masked A and the fused row sums come together in a wgrad: MASKED and ROWSUM share
   // one instantiation pair)
   const bool rs = a.rowsum != nullptr;
-  if constexpr (VEC_OK) {
+  if constexpr (PLAIN) {
+    if (!vec || a.maskA || rs) return hipErrorInvalidValue;  // (dispatch never sends these here)
+    DGT_F32_LAUNCH(true, false, false)
+    return hipGetLastError();
+  } else if constexpr (VEC_OK) {
     if (vec) {
       if (a.maskA && rs) DGT_F32_LAUNCH(true, true, true)
       else if (a.maskA) DGT_F32_LAUNCH(true, true, false)
@@ -379,7 +421,9 @@ hipError_t dispatch(const GemmF32Args& a, const GemmF32Plan& p, bool vec, hipStr
   // ragged operands (scalar loads) are rare: one configuration serves them all (it takes any grid)
   if (!vec) return launch<LA, LB, 64, 64, 1, 1, 4, 1>(a, false, stream);
   switch (p.cfg) {
-    case kF32Wave128: return launch<LA, LB, 128, 64, 2, 2, 1, 2>(a, vec, stream);
+    case kF32Wave128:
+      if (a.maskA || a.rowsum) return launch<LA, LB, 64, 64, 2, 2, 1, 2>(a, vec, stream);
+      return launch<LA, LB, 128, 64, 2, 2, 1, 2, true>(a, vec, stream);
     case kF32Wave64: return launch<LA, LB, 64, 64, 2, 2, 1, 2>(a, vec, stream);
     case kF32Wave64Split2: return launch<LA, LB, 64, 64, 1, 2, 2, 2>(a, vec, stream);
     default: return launch<LA, LB, 64, 64, 1, 1, 4, 1>(a, vec, stream);

@@ -200,6 +200,7 @@ class Engine:
         self.graph_fallback_reason = ""
         self.graph_module_reason = ""
         self._graphed_fwd: Dict[tuple, Any] = {}
+        self._last_graphed = None  # (shape, dtype, requires_grad, GraphedModule) of the last hit
         # graphed tail (runtime/graph_module.py): backward + collective + Adam as one replay when
         # the loss is the framework's own; the step counter Adam reads lives on the device
         self._tail_rccl = None
@@ -287,7 +288,8 @@ class Engine:
             args = tuple(a.to(self.dtype) if torch.is_tensor(a) and a.is_floating_point() else a for a in args)
         self.tput.start()
         with tracing.range("dgt.forward"):
-            if self.graph_module and self.training and not kwargs and args and all(torch.is_tensor(a) for a in args):
+            if (self.graph_module and self.training and not kwargs and args
+                    and (torch.is_tensor(args[0]) if len(args) == 1 else all(torch.is_tensor(a) for a in args))):
                 fn = self._graphed_forward(args)
                 # a second forward of this signature before the first one's backward runs eagerly:
                 # replaying would overwrite the activations the pending backward still needs
@@ -303,9 +305,16 @@ class Engine:
         into the flat gradient buckets, so a step costs two graph launches instead of one launch
         per op, autograd node and parameter; the bucket hooks still fire.  Up to
         MAX_GRAPHED_SHAPES signatures are captured; others, and any capture failure, run eagerly."""
+        last = self._last_graphed  # the common case: the same single-input signature as last step
+        if last is not None and len(args) == 1:
+            a = args[0]
+            if a.shape == last[0] and a.dtype == last[1] and a.requires_grad == last[2]:
+                return last[3]
         from .runtime.graph_module import GraphedModule
         key = tuple((tuple(a.shape), a.dtype, a.requires_grad) for a in args)
         fn = self._graphed_fwd.get(key)
+        if fn is not None and len(args) == 1:
+            self._last_graphed = (args[0].shape, args[0].dtype, args[0].requires_grad, fn)
         if fn is not None or len(self._graphed_fwd) >= self.MAX_GRAPHED_SHAPES:
             return fn
         self.store.rebind_grads()
@@ -408,8 +417,9 @@ class Engine:
         want = self.global_steps - self.skipped_steps  # the graph adds 1 before its Adam launch
         if self._tail_step_host != want:
             self._tail_step_dev.fill_(want)
-        with torch.no_grad():
-            runner.static_gout[0].view(-1).copy_(dz.view(-1))
+        if dz.data_ptr() != runner.static_gout[0].data_ptr():  # (else the loss kernel wrote it there)
+            with torch.no_grad():
+                runner.static_gout[0].view(-1).copy_(dz.view(-1))
         with tracing.range("dgt.graphed_tail"):
             runner.bwd_tail.replay()
         runner.pending = False
@@ -825,6 +835,7 @@ class Engine:
             self.graphed.close()
             self.graphed = None
         self._graphed_fwd.clear()  # graph_module: the captured graphs and their memory pools
+        self._last_graphed = None
         for h in self._hooks:
             h.remove()
         self._hooks = []

@@ -130,6 +130,15 @@ def _skinny(x: torch.Tensor, weight: torch.Tensor) -> bool:
             and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
 
 
+def _chain2(x: torch.Tensor, wb) -> bool:
+    """A two-layer chain the one-launch kernels take (csrc/linear.hip linear2_*): both layers within the
+    small-batch kernels' range, the hidden activation within the kernel's LDS (M * H <= 4096)."""
+    if len(wb) != 4 or not _small(x, wb[0]):
+        return False
+    M, K, H, O = x.shape[0], x.shape[1], wb[0].shape[0], wb[2].shape[0]
+    return M * H <= 4096 and M * H * K + M * O * H <= (1 << 20) and wb[2].shape[1] == H
+
+
 def _fwd(ops, x, weight, bias, relu: bool) -> torch.Tensor:
     """y = act(x W^T + b): the small-batch kernel, the skinny head kernel or the tiled fp32 MFMA GEMM
     (bias/ReLU epilogue)."""
@@ -278,7 +287,16 @@ class _FusedChainFn(torch.autograd.Function):
         ops = _ext.require()
         acts = [x]
         h = x
-        for i, relu in enumerate(relus):
+        ctx.chain2 = _chain2(x, wb)
+        if ctx.chain2:
+            # the reference model's shape: both layers in ONE launch (csrc/linear.hip linear2_fwd,
+            # bitwise the two per-layer launches)
+            W1, b1, W2, b2 = wb
+            hid = torch.empty(x.shape[0], W1.shape[0], dtype=torch.float32, device=x.device)
+            h = torch.empty(x.shape[0], W2.shape[0], dtype=torch.float32, device=x.device)
+            ops.linear2_fwd(x, W1, b1, W2, b2, hid, h, relus[0], relus[1])
+            acts += [hid, h]
+        for i, relu in enumerate(relus if not ctx.chain2 else ()):
             y = _fwd(ops, h, wb[2 * i], wb[2 * i + 1], relu)
             acts.append(y)
             h = y
@@ -303,6 +321,19 @@ class _FusedChainFn(torch.autograd.Function):
         if not keep_graph():
             release(ctx)
         active = ctx.grad_in_place and _in_place_active()
+        if ctx.chain2 and active and all(ctx.needs_input_grad[3:3 + 2 * L:2]):
+            # both layers' gradients into their .grad views in ONE launch (csrc/linear.hip linear2_bwd)
+            W1, W2 = ctx.params[0], ctx.params[2]
+            B1, B2 = ctx.params[1], ctx.params[3]
+            if (all(_grad_view_ok(p) for p in (W1, W2)) and all(b is None or (b.requires_grad and _grad_view_ok(b))
+                                                                for b in (B1, B2))):
+                acc2 = not _store_both(W2.grad, None if B2 is None else B2.grad)
+                acc1 = not _store_both(W1.grad, None if B1 is None else B1.grad)
+                dx = torch.empty_like(acts[0]) if ctx.needs_input_grad[0] else None
+                ops.linear2_bwd(dy.contiguous(), acts[0], ws[0], acts[1], ws[1], acts[2] if ctx.relus[1] else None, dx,
+                                W1.grad, None if B1 is None else B1.grad, W2.grad, None if B2 is None else B2.grad,
+                                ctx.relus[0], acc1, acc2)
+                return (dx, None, None, *([None] * (2 * L)))
         grads = [None] * (2 * L)
         dy = dy.contiguous()
         masked = False  # dy already carries this layer's ReLU mask (stored so by the dgrad above)

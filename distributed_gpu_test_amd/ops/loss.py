@@ -81,6 +81,22 @@ def release(node) -> None:
         node.freed = True
 
 
+_GOUT_ALIAS: dict = {}  # data_ptr of a graphed module's static output -> weakref to its GraphedModule
+
+
+def register_gout_alias(out: torch.Tensor, runner) -> None:
+    """runtime/graph_module.py: logits at ``out``'s address may take their d loss / d logits buffer
+    from ``runner.claim_gout`` (the backward graph's static input)."""
+    import weakref
+    _GOUT_ALIAS[out.data_ptr()] = weakref.ref(runner)
+
+
+def _gout_buffer(z: torch.Tensor, dtype: torch.dtype) -> Optional[torch.Tensor]:
+    ref = _GOUT_ALIAS.get(z.data_ptr()) if _GOUT_ALIAS else None
+    runner = ref() if ref is not None else None
+    return None if runner is None else runner.claim_gout(z, dtype)
+
+
 def _is_unit(g: torch.Tensor) -> bool:
     t = _UNIT.get(g.device)
     return t is not None and g.dim() == 0 and g.dtype == torch.float32 and g.data_ptr() == t.data_ptr()
@@ -92,8 +108,15 @@ class _FusedBCEWithLogits(torch.autograd.Function):
         zc = z.contiguous().reshape(-1)
         yc = y.reshape(-1).to(torch.float32).contiguous()
         loss = torch.empty(1, dtype=torch.float32, device=z.device)
-        dz = torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
-        lp = torch.empty(zc.numel(), dtype=torch.bfloat16, device=z.device) if z.dtype == torch.bfloat16 else None
+        # the gradient a graphed module's backward replays from: written in place when z is that
+        # module's fresh output (fp32: dz itself, bf16: the once-rounded copy)
+        gbuf = _gout_buffer(zc, z.dtype)
+        if z.dtype == torch.bfloat16:
+            dz = torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
+            lp = gbuf.view(-1) if gbuf is not None else torch.empty(zc.numel(), dtype=torch.bfloat16, device=z.device)
+        else:
+            dz = gbuf.view(-1) if gbuf is not None else torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
+            lp = None
         _ext.require().bce_logits(zc, yc, loss, dz, lp, sum_into)
         ctx.dz, ctx.lp, ctx.freed = dz, lp, False
         ctx.shape, ctx.dtype = z.shape, z.dtype

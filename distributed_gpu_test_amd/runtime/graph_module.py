@@ -120,6 +120,23 @@ class GraphedModule:
         self.single = torch.is_tensor(out) or len(out) == 1
         self.replays = 0
         self.pending = False  # a replayed forward whose backward has not run yet
+        # the framework's fused BCE on this graph's (single, differentiable) output writes its
+        # d loss / d logits straight into the backward graph's static input (ops/loss.py
+        # claim_gout): no copy before the backward replay.  One claim per forward replay.
+        self.gout_claimable = False
+        if self.single and self.grad_out_idx == [0]:
+            from ..ops.loss import register_gout_alias
+            register_gout_alias(self.static_out[0], self)
+
+    def claim_gout(self, z: torch.Tensor, dtype: torch.dtype) -> Optional[torch.Tensor]:
+        """The static gradient input as the destination of d loss / d logits of ``z`` (this graph's
+        output of the latest replay, read by its first loss), else None."""
+        g = self.static_gout[0]
+        if (not self.gout_claimable or not self.pending or g.dtype != dtype or z.numel() != g.numel()
+                or z.data_ptr() != self.static_out[0].data_ptr()):
+            return None
+        self.gout_claimable = False
+        return g
 
     def __call__(self, *args):
         grad = torch.is_grad_enabled()  # the caller's mode: inside Function.forward it is always off
@@ -136,6 +153,7 @@ class _Replay(torch.autograd.Function):
                 dst.copy_(src)
         runner.fwd.replay()
         runner.replays += 1
+        runner.gout_claimable = True
         ctx.runner = runner
         outs = tuple(o.detach() for o in runner.static_out)
         for i, o in enumerate(outs):
@@ -151,7 +169,7 @@ class _Replay(torch.autograd.Function):
             g = gouts[i]
             if g is None:
                 dst.zero_()
-            else:
+            elif g.data_ptr() != dst.data_ptr():  # (the fused BCE may have written it in place)
                 dst.copy_(g)
         r.bwd.replay()
         grads_in: List = [None] * len(r.static_in)

@@ -46,7 +46,8 @@ def _close(got, ref, a, b):
 SHAPES = [
     (256, 256, 256),      # aligned, 64x64 tiles
     (1024, 1024, 1024),   # aligned, 64x64 tiles (64 x 128^2 tiles < 256)
-    (2048, 2048, 512),    # aligned, 128x128 tiles
+    (2048, 2048, 512),    # aligned, 64x64 wave tiles in 2 x 2 (128x128 workgroup tiles)
+    (4096, 2048, 256),    # aligned, 128x64 wave tiles (256x128 workgroup tiles)
     (1000, 999, 1004),    # ragged M / N, K % 4 == 0 (16-byte staging with zero fill)
     (77, 130, 67),        # everything ragged, K odd (scalar staging)
     (64, 64, 8192),       # tiny grid, long K: the in-workgroup K split
@@ -54,19 +55,20 @@ SHAPES = [
 ]
 
 
+@pytest.mark.parametrize("lb", [0, 1])
 @pytest.mark.parametrize("M,N,K", [(1024, 1024, 1024), (2048, 2048, 512), (1000, 999, 1004), (77, 130, 67),
-                                   (64, 64, 8192)])
-def test_gemm_f32_output_mask(M, N, K):
+                                   (64, 64, 8192), (4096, 1024, 256), (1000, 1000, 1000)])
+def test_gemm_f32_output_mask(M, N, K, lb):
     """``maskC``: the product stored as C * 1[maskC > 0] (a dgrad writing the ReLU-masked gradient of
     the layer below), on the direct epilogue and through the split-K reduce, equal bit for bit to the
     plain product masked afterwards."""
     ops = _ops()
-    a, b, A, B = _operands(M, N, K, 0, 1, seed=K)
+    a, b, A, B = _operands(M, N, K, 0, lb, seed=K)
     mk = torch.randn(M, N, device="cuda")
     C = torch.empty(M, N, device="cuda")
-    ops.gemm_f32(A, B, None, None, C, 0, 1, False, False, None, mk)
+    ops.gemm_f32(A, B, None, None, C, 0, lb, False, False, None, mk)
     plain = torch.empty(M, N, device="cuda")
-    ops.gemm_f32(A, B, None, None, plain, 0, 1, False, False)
+    ops.gemm_f32(A, B, None, None, plain, 0, lb, False, False)
     assert torch.equal(C, torch.where(mk > 0, plain, torch.zeros_like(plain)))
 
 
@@ -110,7 +112,8 @@ def test_gemm_f32_layouts(M, N, K, la, lb):
     _close(C, _ref(a, b), a, b)
 
 
-@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (1000, 999, 1004), (64, 64, 8192), (77, 130, 67)])
+@pytest.mark.parametrize("M,N,K", [(512, 384, 256), (1000, 999, 1004), (64, 64, 8192), (77, 130, 67),
+                                   (4096, 2048, 128)])
 def test_gemm_f32_epilogues(M, N, K):
     ops = _ops()
     a, b, A, B = _operands(M, N, K, 0, 0, seed=1)

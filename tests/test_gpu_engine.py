@@ -745,3 +745,72 @@ def test_engine_direct_backward_frees_activations_and_refuses_second_backward():
     assert node.dz is not None and not node.freed
     engine.step()
     engine.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("bf16", [False, True])
+def test_graph_module_fused_bce_writes_gradient_in_place(bf16):
+    """graph_module + the framework's fused BCE: the loss kernel writes d loss / d logits straight into
+    the backward graph's static input (no copy before the replay), only for the first loss on a fresh
+    forward replay; a second loss on the same output gets its own buffer.  Trajectory as eager."""
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    crit = BCEWithLogitsLoss()
+    cfg = {"train_batch_size": 32, **({"bf16": {"enabled": True}} if bf16 else {})}
+    batches = _batches(6, 21)
+    e1, l1, p1 = _run_engine(dict(cfg), batches, crit=crit)
+    m = _mlp(4)
+    e2 = dgt.initialize(model=m, optimizer=torch.optim.Adam(m.parameters(), lr=1e-3),
+                        config=dict(cfg, amd={"graph_module": True}))[0]
+    losses = []
+    for i, (x, y) in enumerate(batches):
+        out = e2(x)
+        loss = crit(out.float() if not bf16 else out, y)
+        runner = next(iter(e2._graphed_fwd.values()))
+        if i > 0:  # (the first forward of a signature captures; its output is not a replay)
+            buf = loss.grad_fn.lp if bf16 else loss.grad_fn.dz
+            assert buf.data_ptr() == runner.static_gout[0].data_ptr()
+            extra = crit(out.float() if not bf16 else out, y)  # a second loss: its own buffer
+            eb = extra.grad_fn.lp if bf16 else extra.grad_fn.dz
+            assert eb.data_ptr() != runner.static_gout[0].data_ptr()
+            del extra
+        e2.backward(loss)
+        e2.step()
+        losses.append(float(loss))
+    tol = dict(rtol=2e-2, atol=2e-3) if bf16 else dict(rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(torch.tensor(losses), torch.tensor(l1), **tol)
+    torch.testing.assert_close(e2.store.param_buf.float(), p1.float(), **tol)
+    e1.close()
+    e2.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("in_place", [False, True])
+@pytest.mark.parametrize("B,F,H,O,relu_out", [(4, 20, 64, 1, False), (16, 32, 128, 8, True), (3, 17, 40, 5, False)])
+def test_fused_chain2_one_launch_is_bitwise_per_layer(B, F, H, O, relu_out, in_place):
+    """A two-layer chain (the reference SimpleNet's shape among others) runs forward and backward as
+    ONE launch each (csrc/linear.hip linear2_*): outputs, input gradients and parameter gradients
+    bit-identical to the layer-by-layer kernels, in place into .grad views or returned."""
+    from distributed_gpu_test_amd.ops.linear import FusedChain, engine_backward, inject_fused_linear
+    torch.manual_seed(B + F)
+    layers = [torch.nn.Linear(F, H), torch.nn.ReLU(), torch.nn.Linear(H, O)] + ([torch.nn.ReLU()] if relu_out else [])
+    base = torch.nn.Sequential(*layers).cuda()
+    chain, layered = copy.deepcopy(base), copy.deepcopy(base)
+    assert inject_fused_linear(chain, grad_in_place=in_place) == 2 and type(chain) is FusedChain
+    inject_fused_linear(layered, grad_in_place=in_place)
+    for net in (chain, layered):
+        for p in net.parameters():
+            if in_place:
+                p.grad = torch.zeros_like(p)
+    x0 = torch.randn(B, F, device="cuda")
+    outs, dxs = [], []
+    for net in (chain, layered):
+        x = x0.clone().requires_grad_(True)
+        for _ in range(2):  # the second backward accumulates
+            y = net(x) if net is chain else _layer_by_layer(net, x)
+            with engine_backward():
+                (y * torch.linspace(-1, 1, y.numel(), device="cuda").view_as(y)).sum().backward()
+        outs.append(y.detach())
+        dxs.append(x.grad)
+    assert torch.equal(outs[0], outs[1]) and torch.equal(dxs[0], dxs[1])
+    for p, q in zip(chain.parameters(), layered.parameters()):
+        assert torch.equal(p.grad, q.grad)
