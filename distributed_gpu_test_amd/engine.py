@@ -46,6 +46,20 @@ from .utils.metrics import MetricsSink, ThroughputTimer
 _DTYPES = {"fp32": torch.float32, "bf16": torch.bfloat16, "fp16": torch.float16}
 
 
+_DIRECT_KINDS = None
+
+
+def _direct_node_classes():
+    """The autograd node classes of the framework's fused BCE, Linear chain and single Linear
+    (identity checks on the direct-backward path instead of class-name strings)."""
+    global _DIRECT_KINDS
+    if _DIRECT_KINDS is None:
+        from .ops.linear import _FusedChainFn, _FusedLinearFn
+        from .ops.loss import _FusedBCEWithLogits
+        _DIRECT_KINDS = (_FusedBCEWithLogits._backward_cls, _FusedChainFn._backward_cls, _FusedLinearFn._backward_cls)
+    return _DIRECT_KINDS
+
+
 class FlatAdamOptimizer:
     """Optimizer facade handed back by ``initialize`` (the engine drives the actual update)."""
 
@@ -491,54 +505,67 @@ class Engine:
         if (scaled is not loss or not self.config.amd.direct_backward
                 or self.device.type != "cuda" or loss.dim() != 0):
             return False
+        kinds = _direct_node_classes()
         node = loss.grad_fn
-        if node is None or type(node).__name__ != "_FusedBCEWithLogitsBackward":
+        if node is None or type(node) is not kinds[0]:
             return False
         nxt = node.next_functions  # (logits, targets[, sum_into])
-        if len(nxt) < 2 or any(e[0] is not None for e in nxt[1:]):
+        if len(nxt) < 2:
             return False
+        for e in nxt[1:]:
+            if e[0] is not None:
+                return False
         views = []
         cur = nxt[0][0]
-        while cur is not None and type(cur).__name__ in self._VIEW_NODES + ("ToCopyBackward0",):
+        while cur is not None and type(cur) is not kinds[1] and type(cur) is not kinds[2]:
+            if type(cur).__name__ not in self._VIEW_NODES + ("ToCopyBackward0",):
+                return False
             if len(cur.next_functions) != 1:
                 return False
             views.append(cur)
             cur = cur.next_functions[0][0]
-        kind = type(cur).__name__ if cur is not None else ""
-        if kind not in ("_FusedChainFnBackward", "_FusedLinearFnBackward"):
+        if cur is None:
             return False
+        chain = type(cur) is kinds[1]
         edges = cur.next_functions
         if not edges or edges[0][0] is not None:
             return False  # the chain's input wants a gradient too
-        accs = [e[0] for e in edges[1:]]
-        if any(a is None or type(a).__name__ != "AccumulateGrad" for a in accs):
-            return False
-        leaves = [a.variable for a in accs]
+        leaves = []
         own = self._own_tensor_hooks
-        if any(p._backward_hooks and any(k not in own for k in p._backward_hooks) for p in leaves):
-            return False  # a user's tensor hook sees the gradient before accumulation: autograd's job
+        for e in edges[1:]:
+            a = e[0]
+            if a is None or type(a).__name__ != "AccumulateGrad":
+                return False
+            p = a.variable
+            if p._backward_hooks:
+                for k in p._backward_hooks:
+                    if k not in own:
+                        return False  # a user's tensor hook sees the gradient before accumulation: autograd's job
+            leaves.append(p)
         seed = self._unit_seed(loss.device)
         from .ops.loss import direct_backward, release
-        with torch.no_grad(), direct_backward():  # grad mode off as under autograd (no create_graph)
-            g = node.apply(seed)  # the unit seed: the saved d loss / d logits itself, no launch
-            g = g[0] if isinstance(g, tuple) else g
-            for v in views:  # reshapes / casts back to the chain's output
-                g = v(g)
+        prev_grad = torch.is_grad_enabled()
+        torch.set_grad_enabled(False)  # grad mode off as under autograd (no create_graph)
+        try:
+            with direct_backward():
+                g = node.apply(seed)  # the unit seed: the saved d loss / d logits itself, no launch
                 g = g[0] if isinstance(g, tuple) else g
-            res = cur.apply(g)
-        # what autograd does after a backward that does not retain the graph: the activations and
-        # d loss / d logits are freed now (not when the caller drops ``loss``), and a second
-        # backward through this graph raises instead of adding the gradients again
-        release(node)
-        release(cur)
-        # backward outputs -> the tensor inputs the edges belong to (weights, then present biases)
-        if kind == "_FusedChainFnBackward":
-            grads = [gr for j, gr in enumerate(res[3:]) if j % 2 == 0 or cur.has_bias[j // 2]]
-        else:
-            grads = [res[1]] + ([res[2]] if cur.has_bias else [])
-        if len(grads) != len(leaves):
-            raise RuntimeError("dgt: direct backward: gradient / parameter count mismatch")
-        with torch.no_grad():
+                for v in views:  # reshapes / casts back to the chain's output
+                    g = v(g)
+                    g = g[0] if isinstance(g, tuple) else g
+                res = cur.apply(g)
+            # what autograd does after a backward that does not retain the graph: the activations and
+            # d loss / d logits are freed now (not when the caller drops ``loss``), and a second
+            # backward through this graph raises instead of adding the gradients again
+            release(node)
+            release(cur)
+            # backward outputs -> the tensor inputs the edges belong to (weights, then present biases)
+            if chain:
+                grads = [gr for j, gr in enumerate(res[3:]) if j % 2 == 0 or cur.has_bias[j // 2]]
+            else:
+                grads = [res[1]] + ([res[2]] if cur.has_bias else [])
+            if len(grads) != len(leaves):
+                raise RuntimeError("dgt: direct backward: gradient / parameter count mismatch")
             for p, gr in zip(leaves, grads):
                 if gr is None:
                     continue  # written in place into p.grad by the kernels
@@ -548,6 +575,8 @@ class Engine:
                     if p._backward_hooks:
                         self._before_accumulate(p)  # the engine's tensor hook, as autograd would run it
                     p.grad.add_(gr)
+        finally:
+            torch.set_grad_enabled(prev_grad)
         for p in leaves:  # what AccumulateGrad does after accumulating: the post-accumulate hooks
             hooks = p._post_accumulate_grad_hooks
             if hooks:

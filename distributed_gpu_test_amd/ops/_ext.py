@@ -42,11 +42,18 @@ def available() -> bool:
     return load()
 
 
+_OPS = None  # torch.ops.dgt once loaded: require() sits on every eager op call's path
+
+
 def require():
     """Return ``torch.ops.dgt``; raise if the extension cannot be loaded."""
+    global _OPS
+    if _OPS is not None:
+        return _OPS
     if not load():
         raise RuntimeError(f"distributed_gpu_test_amd native extension unavailable: {_error}")
-    return torch.ops.dgt
+    _OPS = torch.ops.dgt
+    return _OPS
 
 
 _clib = None

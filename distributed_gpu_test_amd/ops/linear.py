@@ -23,7 +23,6 @@ dispatches on the parameters' dtype.
 from __future__ import annotations
 
 import collections
-import contextlib
 import os
 import sys
 from typing import Optional
@@ -50,19 +49,29 @@ _GRADS_ZERO = False
 _WRITTEN: set = set()
 
 
-@contextlib.contextmanager
-def engine_backward(grads_zero: bool = False):
-    """Yields the set of ``(data_ptr, numel)`` gradient views STORED (first-written) in this backward."""
-    global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN
-    _ENGINE_BACKWARD += 1
-    prev, _GRADS_ZERO = _GRADS_ZERO, bool(grads_zero)
-    prev_written, _WRITTEN = _WRITTEN, set()
-    try:
-        yield _WRITTEN
-    finally:
+class engine_backward:
+    """``with engine_backward(grads_zero) as stored``: the engine's backward; ``stored`` is the set of
+    ``(data_ptr, numel)`` gradient views STORED (first-written) in it.  (A class, not a generator-based
+    context manager: entered once per eager step, where the host cost is the step's cost.)"""
+
+    __slots__ = ("grads_zero", "prev", "prev_written")
+
+    def __init__(self, grads_zero: bool = False):
+        self.grads_zero = bool(grads_zero)
+
+    def __enter__(self):
+        global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN
+        _ENGINE_BACKWARD += 1
+        self.prev, _GRADS_ZERO = _GRADS_ZERO, self.grads_zero
+        self.prev_written, _WRITTEN = _WRITTEN, set()
+        return _WRITTEN
+
+    def __exit__(self, *exc):
+        global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN
         _ENGINE_BACKWARD -= 1
-        _GRADS_ZERO = prev
-        _WRITTEN = prev_written
+        _GRADS_ZERO = self.prev
+        _WRITTEN = self.prev_written
+        return False
 
 
 def _in_place_active() -> bool:
@@ -189,7 +198,7 @@ class _FusedLinearFn(torch.autograd.Function):
         ctx.params = (weight, bias) if ctx.grad_in_place else (None, None)
         # the input and the weight as attributes (freed by the direct backward: ops/loss.py
         # release), the output through save_for_backward (an attribute would be a reference cycle)
-        ctx.x, ctx.w, ctx.freed = x, weight, False
+        ctx.x, ctx.w, ctx.freed, ctx.held = x, weight, False, ("x", "w")
         ctx.save_for_backward(y if relu else None)
         return y
 
@@ -224,6 +233,11 @@ def _grad_view_ok(p, dtype=torch.float32) -> bool:
     g = p.grad
     return (g is not None and g.is_cuda and g.dtype == dtype and g.is_contiguous()
             and g.shape == p.shape and not torch.is_grad_enabled())
+
+
+def _fusable_param(weight: torch.Tensor, bias=None) -> bool:
+    return (weight.dtype == torch.float32 and weight.is_contiguous()
+            and (bias is None or (bias.dtype == torch.float32 and bias.is_contiguous())))
 
 
 def _fusable(x: torch.Tensor, weight: torch.Tensor, bias=None) -> bool:
@@ -307,7 +321,7 @@ class _FusedChainFn(torch.autograd.Function):
         # the input, the hidden activations and the weights as attributes (none of them an output:
         # no reference cycle; freed by the direct backward, ops/loss.py release), the chain's output
         # through save_for_backward
-        ctx.acts, ctx.ws, ctx.freed = acts[:-1], wb[0::2], False
+        ctx.acts, ctx.ws, ctx.freed, ctx.held = acts[:-1], wb[0::2], False, ("acts", "ws")
         ctx.save_for_backward(h)
         return h
 
@@ -377,12 +391,23 @@ class FusedChain(nn.Sequential):
         if layers is None:
             layers = self._chain() or []
             self.__dict__["_dgt_layers"] = layers
-        if len(layers) > 1 and x.dim() == 2 and all(_fusable(x, m.weight, m.bias) for m in layers):
+        if len(layers) > 1 and x.dim() == 2 and x.is_cuda and x.dtype == torch.float32:
+            # (the parameters straight from each layer's _parameters: nn.Module.__getattr__ is a
+            # measurable part of a host-bound eager step)
             wb = []
+            ok = True
             for m in layers:
-                wb.append(m.weight)
-                wb.append(m.bias)
-            return _FusedChainFn.apply(x.contiguous(), tuple(m.relu for m in layers), layers[0].grad_in_place, *wb)
+                w, b = m._parameters["weight"], m._parameters["bias"]
+                if not _fusable_param(w, b):
+                    ok = False
+                    break
+                wb.append(w)
+                wb.append(b)
+            if ok and _ext.require() is not None:
+                relus = self.__dict__.get("_dgt_relus")
+                if relus is None:
+                    relus = self.__dict__["_dgt_relus"] = tuple(m.relu for m in layers)
+                return _FusedChainFn.apply(x.contiguous(), relus, layers[0].grad_in_place, *wb)
         return super().forward(x)
 
 

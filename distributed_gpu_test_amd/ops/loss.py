@@ -21,7 +21,6 @@ value a later backward reads.
 """
 from __future__ import annotations
 
-import contextlib
 import threading
 from typing import Optional
 
@@ -60,24 +59,27 @@ def keep_graph() -> bool:
     return torch._C._autograd._get_current_graph_task_keep_graph()
 
 
-@contextlib.contextmanager
-def direct_backward():
+class direct_backward:
     """Marks the engine's own calls of the nodes' backward (``engine._direct_backward``): a
     backward that does not retain the graph."""
-    _DIRECT.on = True
-    try:
-        yield
-    finally:
+
+    __slots__ = ()
+
+    def __enter__(self):
+        _DIRECT.on = True
+
+    def __exit__(self, *exc):
         _DIRECT.on = False
+        return False
 
 
 def release(node) -> None:
     """Free what the framework's fused loss / Linear nodes hold for backward (the direct backward's
-    counterpart of autograd's release of saved tensors)."""
-    for attr in ("dz", "lp", "acts", "ws", "x", "w"):
-        if hasattr(node, attr):
+    counterpart of autograd's release of saved tensors).  Each node lists its attributes in ``held``."""
+    held = getattr(node, "held", None)
+    if held is not None:
+        for attr in held:
             setattr(node, attr, None)
-    if hasattr(node, "freed"):
         node.freed = True
 
 
@@ -118,7 +120,7 @@ class _FusedBCEWithLogits(torch.autograd.Function):
             dz = gbuf.view(-1) if gbuf is not None else torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
             lp = None
         _ext.require().bce_logits(zc, yc, loss, dz, lp, sum_into)
-        ctx.dz, ctx.lp, ctx.freed = dz, lp, False
+        ctx.dz, ctx.lp, ctx.freed, ctx.held = dz, lp, False, ("dz", "lp")
         ctx.shape, ctx.dtype = z.shape, z.dtype
         return loss.view(())
 
