@@ -82,6 +82,9 @@ def parse_args(argv=None):
     ap.add_argument("--width", type=int, default=4096)
     ap.add_argument("--depth", type=int, default=4)
     ap.add_argument("--batch", type=int, default=1024, help="mlp: per-GPU micro-batch")
+    ap.add_argument("--torch-dtype", default="bf16", choices=["bf16", "fp32"],
+                    help="--model mlp --impl engine: the PyTorch stack's compute dtype (bf16 autocast, or plain fp32 on "
+                         "hipBLASLt's exact-fp32 GEMMs: the baseline for the fp32 engine MLP)")
     ap.add_argument("--zero-stage", type=int, default=0, choices=[0, 1],
                     help="0 = all-reduce the gradients; 1 = ZeRO-1: reduce-scatter them, shard Adam, all-gather "
                          "the parameters (simple: inside the fused kernel's exchange; mlp: per-layer RCCL)")
@@ -478,7 +481,7 @@ def main(argv=None):
         model = SyntheticMLP(args.width, args.depth)
         B = args.batch
         if args.impl == "engine":
-            trainer = TorchMLPBench(model, B, device)
+            trainer = TorchMLPBench(model, B, device, autocast=args.torch_dtype == "bf16")
         elif args.impl == "dgt-engine":
             from distributed_gpu_test_amd.runtime.engine_mlp import EngineMLPTrainer
             cfg = engine_config(args, os.path.join(ROOT, "configs", "ds_bench_mlp_bf16.json"))
@@ -725,7 +728,7 @@ class TorchMLPBench:
 
     impl = "torch-autocast-bf16"
 
-    def __init__(self, model, B, device, n_batches=8, seed=1234):
+    def __init__(self, model, B, device, n_batches=8, seed=1234, autocast=True):
         from distributed_gpu_test_amd.models.synthetic_mlp import synthetic_batch_data
         from distributed_gpu_test_amd.parallel import comm
         self.world, self.rank = comm.get_world_size(), comm.get_rank()
@@ -740,6 +743,9 @@ class TorchMLPBench:
         self.global_steps = 0
         self.exchange = f"{comm.backend_name()}-ddp" if self.world > 1 else "none"
         self._flops = model.flops_per_sample() * B
+        self.autocast = autocast
+        if not autocast:  # plain fp32: hipBLASLt's exact-fp32 GEMMs (TF32 is off by default in torch)
+            self.impl, self.dtype_name = "torch-fp32", "fp32"
 
     def flops_per_step(self):
         return self._flops
@@ -753,7 +759,7 @@ class TorchMLPBench:
         for _ in range(int(plan.shape[0])):
             j = self.global_steps % self.n_batches
             x, y = self.X[j * self.B:(j + 1) * self.B], self.Y[j * self.B:(j + 1) * self.B]
-            with torch.autocast(device_type=self.device.type, dtype=torch.bfloat16):
+            with torch.autocast(device_type=self.device.type, dtype=torch.bfloat16, enabled=self.autocast):
                 loss = crit(self.model(x).view(-1).float(), y)
             self.opt.zero_grad(set_to_none=True)
             loss.backward()
