@@ -102,8 +102,9 @@ def parse_args(argv=None):
                     help="process-group timeout (a hung collective becomes an error after this long)")
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the post-headline bf16 MLP / fp32 engine MLP blocks")
-    ap.add_argument("--secondary-steps", type=int, default=50)
-    ap.add_argument("--secondary-warmup", type=int, default=10)
+    # (200 timed steps: 0.06 s of the fp32 block, 0.14 s of the bf16 one -- past the first-steps ramp)
+    ap.add_argument("--secondary-steps", type=int, default=200)
+    ap.add_argument("--secondary-warmup", type=int, default=20)
     ap.add_argument("--secondary-budget-s", type=float, default=90.0,
                     help="hard deadline for each secondary block (setup + warmup + timed steps)")
     # N > 1 knobs, echoed in the JSON config so a scaling run is self-describing

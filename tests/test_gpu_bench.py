@@ -39,7 +39,7 @@ def test_driver_shape_with_secondary_blocks():
     for key in ("bf16_mlp", "fp32_engine_mlp"):
         blk = d[key]
         assert "error" not in blk, (key, blk, err[-2000:])
-        assert blk["iters_per_s"] > 0 and blk["model_tflops"] > 0 and blk["steps"] == 50
+        assert blk["iters_per_s"] > 0 and blk["model_tflops"] > 0 and blk["steps"] == 200
         assert blk["block_wall_s"] < 30, (key, blk)
     assert d["bf16_mlp"]["dtype"] == "bf16" and d["fp32_engine_mlp"]["dtype"] == "fp32"
     print(json.dumps({"wall_s": round(wall, 1), "value": d["value"],
