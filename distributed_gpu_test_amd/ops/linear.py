@@ -12,10 +12,11 @@ launch forward (bias and ReLU folded in) and one launch backward (ReLU mask, dx,
 and state_dict keys, so checkpoints, the engine's flat buffers and optimizers are unaffected.
 
 Every fp32 GPU shape runs a hand-written kernel: small shapes (``SMALL_M`` / ``SMALL_WORK``) the
-one-launch dot-product kernels of ``csrc/linear.hip``; larger ones the exact-fp32 MFMA GEMM of
-``csrc/gemm_f32.hip`` (v_mfma_f32_32x32x2_f32, LDS-tiled, split-K for small grids) -- forward with
-bias / ReLU in the epilogue, dgrad and wgrad reading dy, W and x in their stored layouts with the
-ReLU mask applied while staging, and a deterministic column sum for the bias gradient.  Only
+one-launch dot-product kernels of ``csrc/linear.hip`` (a two-layer chain in one launch each way);
+larger ones the exact-fp32 MFMA GEMM of ``csrc/gemm_f32_kernel.h`` (v_mfma_f32_16x16x4_f32,
+register-fed, K split inside the workgroup for small grids) -- forward with bias / ReLU in the
+epilogue, dgrad and wgrad reading dy, W and x in their stored layouts with the ReLU mask applied
+while loading, and the bias gradient as the wgrad's deterministic row sums.  Only
 non-fp32 / non-contiguous / CPU inputs run ``F.linear``, and those are counted (``FALLBACKS``).  bf16
 models get the MFMA GEMM chain of ``ops/mfma_linear.py`` instead: ``inject_fused_linear``
 dispatches on the parameters' dtype.
@@ -134,7 +135,7 @@ def _small(x: torch.Tensor, weight: torch.Tensor) -> bool:
 
 def _skinny(x: torch.Tensor, weight: torch.Tensor) -> bool:
     """A head Linear(K, N <= 4) beyond the small-batch kernels: two bandwidth passes over x
-    (``csrc/head.hip`` skinny_f32), not 64 x 64 MFMA tiles with one useful column plus a split-K reduce."""
+    (``csrc/head.hip`` skinny_f32), not 64 x 64 MFMA tiles with one useful column."""
     return (weight.shape[0] <= 4 and x.shape[0] % 64 == 0 and x.shape[1] % 32 == 0
             and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
 

@@ -60,8 +60,8 @@ SHAPES = [
                                    (64, 64, 8192), (4096, 1024, 256), (1000, 1000, 1000)])
 def test_gemm_f32_output_mask(M, N, K, lb):
     """``maskC``: the product stored as C * 1[maskC > 0] (a dgrad writing the ReLU-masked gradient of
-    the layer below), on the direct epilogue and through the split-K reduce, equal bit for bit to the
-    plain product masked afterwards."""
+    the layer below), in every epilogue form (per-column and float4 stores, the in-workgroup K-split
+    reduce), equal bit for bit to the plain product masked afterwards."""
     ops = _ops()
     a, b, A, B = _operands(M, N, K, 0, lb, seed=K)
     mk = torch.randn(M, N, device="cuda")
@@ -79,7 +79,7 @@ def test_gemm_f32_output_mask(M, N, K, lb):
                                    (77, 130, 67), (64, 64, 8192), (4096, 1, 1024)])
 def test_gemm_f32_fused_rowsum(M, N, K, la, masked, accumulate):
     """``rowsum[m] (+)= sum_k A'(m, k)`` formed while the GEMM stages A (A' = A after the ReLU mask):
-    the wgrad's bias gradient without a separate column-sum pass.  Every tile size, the split-K
+    the wgrad's bias gradient without a separate column-sum pass.  Every tile size, the in-workgroup K-split
     path (slice partials summed by the reduce kernel), the scalar and 16-byte staging, both A
     layouts; the product itself is unchanged."""
     ops = _ops()
