@@ -808,11 +808,13 @@ class DgtEngineBench(EngineBench):
         # (the reference's loss.item() sum, train.py:115) -- no launch of its own
         crit = BCEWithLogitsLoss(sum_into=self.loss_acc)
 
+        gather = dgt_data.gather_batch
+
         def loss_fn(rows):
             # the batch gather and the loss log are part of the step, so a HIP graph captures them
-            # with it; the batch gather as index_select (one kernel; advanced indexing costs ~3x the
-            # host time)
-            return crit(self.engine(torch.index_select(self.x, 0, rows)).float(), torch.index_select(self.y, 0, rows))
+            # with it; the gather is the data loader's (data.gather_batch: x and y rows in one launch)
+            xb, yb = gather(rows, self.x, self.y)
+            return crit(self.engine(xb).float(), yb)
 
         if self.engine.config.amd.hip_graph:
             self.step = self.engine.graph_step(loss_fn)

@@ -5,6 +5,7 @@
 #include <ATen/ATen.h>
 #include <ATen/hip/impl/HIPStreamMasqueradingAsCUDA.h>
 #include <c10/core/DeviceGuard.h>
+#include <torch/extension.h>
 #include <torch/library.h>
 
 #include <cstdlib>
@@ -529,6 +530,40 @@ void bce_logits(const at::Tensor& z, const at::Tensor& y, const at::Tensor& loss
   c10::DeviceGuard guard(z.device());
   DGT_CHECK_HIP(dgt::bce_logits(z.data_ptr(), dtype_code(z.scalar_type()), y.data_ptr<float>(), z.numel(),
                                 loss.data_ptr<float>(), dz.data_ptr<float>(), lp, acc, stream_of(z)));
+}
+
+std::vector<at::Tensor> gather_rows(const at::Tensor& idx, at::TensorList srcs) {
+  TORCH_CHECK(idx.is_cuda() && idx.scalar_type() == at::kLong && idx.dim() == 1 && idx.is_contiguous(),
+              "dgt: gather_rows needs a contiguous 1-D int64 GPU index");
+  TORCH_CHECK(!srcs.empty() && (int)srcs.size() <= dgt::kMaxGather, "dgt: gather_rows takes 1..", dgt::kMaxGather,
+              " tensors");
+  const int64_t n = srcs[0].dim() > 0 ? srcs[0].size(0) : 0;
+  dgt::GatherArgs a{};
+  a.idx = reinterpret_cast<const long long*>(idx.data_ptr<int64_t>());
+  a.n_rows = n;
+  a.count = (int)srcs.size();
+  std::vector<at::Tensor> outs;
+  for (size_t t = 0; t < srcs.size(); ++t) {
+    const at::Tensor& s = srcs[t];
+    TORCH_CHECK(s.device() == idx.device() && s.is_contiguous() && s.dim() >= 1 && s.size(0) == n,
+                "dgt: gather_rows tensors must be contiguous, on the index's device, with the same row count");
+    const int64_t row_bytes = n > 0 ? s.numel() / n * (int64_t)s.element_size() : 0;
+    TORCH_CHECK(row_bytes % 4 == 0 && row_bytes / 4 < (1 << 30), "dgt: gather_rows rows must be whole 4-byte words");
+    auto sizes = s.sizes().vec();
+    sizes[0] = idx.numel();
+    outs.push_back(at::empty(sizes, s.options()));
+    a.src[t] = s.data_ptr();
+    a.dst[t] = outs.back().data_ptr();
+    a.row_words[t] = (int)(row_bytes / 4);
+    if (row_bytes % 16 == 0 && reinterpret_cast<uintptr_t>(a.src[t]) % 16 == 0) a.vec_mask |= 1 << t;
+  }
+  if (idx.numel() == 0 || n == 0 || outs[0].numel() == 0) {
+    TORCH_CHECK(idx.numel() == 0, "dgt: gather_rows from an empty tensor");
+    return outs;
+  }
+  c10::DeviceGuard guard(idx.device());
+  DGT_CHECK_HIP(dgt::gather_rows(a, (int)idx.numel(), stream_of(idx)));
+  return outs;
 }
 
 void tiny_mlp_grad(const at::Tensor& X, const at::Tensor& Y, const at::Tensor& plan, const at::Tensor& counts,
@@ -1132,6 +1167,7 @@ TORCH_LIBRARY(dgt, m) {
       &adam_flat);
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz, Tensor(c!)? dz_lp=None, Tensor(d!)? sum_into=None) -> ()", &bce_logits);
+  m.def("gather_rows(Tensor idx, Tensor[] srcs) -> Tensor[]", &gather_rows);
   m.def("linear_fwd(Tensor x, Tensor W, Tensor? b, Tensor(a!) y, bool relu) -> ()", &linear_fwd);
   m.def("linear2_fwd(Tensor x, Tensor W1, Tensor? b1, Tensor W2, Tensor? b2, Tensor(a!) h, Tensor(b!) y, bool relu1, "
         "bool relu2) -> ()",
@@ -1183,4 +1219,20 @@ TORCH_LIBRARY(dgt, m) {
   m.def("ipc_free(int ptr) -> ()", &ipc_free);
   m.def("memset_device(int ptr, int value, int nbytes) -> ()", &memset_device);
   m.def("can_access_peer(int dev, int peer) -> bool", &can_access_peer);
+}
+
+// The same functions as a Python extension module (``distributed_gpu_test_amd._C``, loaded by
+// ops/_ext.py fast()): a pybind11 call unpacks its tensors directly, where a ``torch.ops.dgt`` call
+// goes through the boxed dispatcher (an IValue stack per call) -- ~2-3 us of host time per call on
+// the MI355X box, paid several times per step by the host-bound engine paths (gather, Linear chain,
+// loss, Adam).  Only the hot eager-path ops; everything else stays on torch.ops.dgt.
+PYBIND11_MODULE(_C, m) {
+  m.doc() = "dgt hot-path ops without the dispatcher (same C++ functions as torch.ops.dgt)";
+  m.def("gather_rows", [](const at::Tensor& idx, const std::vector<at::Tensor>& srcs) { return gather_rows(idx, srcs); });
+  m.def("bce_logits", &bce_logits);
+  m.def("linear_fwd", &linear_fwd);
+  m.def("linear_bwd", &linear_bwd);
+  m.def("linear2_fwd", &linear2_fwd);
+  m.def("linear2_bwd", &linear2_bwd);
+  m.def("adam_flat", &adam_flat);
 }

@@ -273,4 +273,19 @@ struct ReduceAdam {
 };
 hipError_t partials_reduce_multi(const ReduceSegs& r, const ReduceAdam& adam, hipStream_t stream);
 
+// data.hip: rows idx[0..n_out) of up to kMaxGather row-major tensors (row_words 4-byte words per
+// row, n_rows rows each) into contiguous outputs, one launch.
+constexpr int kMaxGather = 4;
+struct GatherArgs {
+  const long long* idx;
+  long long n_rows;
+  const void* src[kMaxGather];
+  void* dst[kMaxGather];
+  int row_words[kMaxGather];
+  int count;
+  int vec_mask;  // bit t: tensor t's rows are 16-byte words at 16-byte-aligned addresses
+  int* bad;  // optional: set to 1 when an index is out of range
+};
+hipError_t gather_rows(const GatherArgs& a, int n_out, hipStream_t stream);
+
 }  // namespace dgt

@@ -95,6 +95,10 @@ class AMDConfig:
     # engine.backward replays backward + gradient collective + clip + Adam as ONE graph and
     # engine.step() only does the bookkeeping (so parameters are updated when backward returns)
     graph_tail: bool = True
+    # with graph_module: an input that arrives at the same address step after step (a loader's
+    # fresh batch, recycled by the caching allocator) gets graphs that read it in place -- no copy
+    # into a static input (up to 2 addresses per input shape; others take the copying graph)
+    graph_bind_inputs: bool = True
     # eager: engine.backward runs the backward of its own loss -> Linear-chain graph (fused BCE of an
     # injected chain's output) by calling the two backward functions directly, without the autograd
     # engine; any other graph goes through autograd (engine.py Engine._direct_backward)
@@ -232,6 +236,7 @@ def parse_config(config: Union[str, os.PathLike, Dict[str, Any], None], world_si
                     fused_linear=None if a.get("fused_linear") is None else bool(a["fused_linear"]),
                     graph_module=bool(a.get("graph_module", False)),
                     graph_tail=bool(a.get("graph_tail", True)),
+                    graph_bind_inputs=bool(a.get("graph_bind_inputs", True)),
                     direct_backward=bool(a.get("direct_backward", True)),
                     defer_zero_grad=bool(a.get("defer_zero_grad", True)))
     if amd.allreduce not in ("auto", "rccl", "oneshot"):

@@ -82,6 +82,19 @@ def steps_per_epoch(n: int, world_size: int, batch_size: int) -> int:
     return math.ceil(math.ceil(n / world_size) / batch_size)
 
 
+def gather_batch(rows: torch.Tensor, *tensors: torch.Tensor) -> Tuple[torch.Tensor, ...]:
+    """The minibatch ``t[rows]`` of every dataset tensor (x, y, ...).  On the GPU: one HIP launch for
+    all of them (``csrc/data.hip``), fresh contiguous outputs, instead of one ``index_select`` per
+    tensor -- the generic engine's step is host-bound and each launch is ~4-5 us of it.  Indices must
+    lie in ``[0, rows)`` (an out-of-range index yields a zero row, as no check may sync the step)."""
+    if (rows.is_cuda and 0 < len(tensors) <= 4 and rows.dtype == torch.long and rows.dim() == 1
+            and all(t.is_cuda and t.dim() >= 1 and t.is_contiguous() and (t.stride(0) * t.element_size()) % 4 == 0
+                    for t in tensors)):
+        from .ops import _ext
+        return tuple(_ext.hot().gather_rows(rows.contiguous(), list(tensors)))  # (checks the devices)
+    return tuple(t.index_select(0, rows) for t in tensors)
+
+
 @dataclass
 class SyntheticDataset:
     """Device-resident dataset + per-rank sampler.  Iteration yields device tensors."""
@@ -117,5 +130,4 @@ class SyntheticDataset:
         idx = shard_indices(self.n, self.world_size, self.rank, self.epoch, self.sampler_seed)
         dev_idx = torch.tensor(idx, dtype=torch.long, device=self.x.device)
         for s in range(0, len(idx), self.batch_size):
-            sel = dev_idx[s:s + self.batch_size]
-            yield self.x.index_select(0, sel), self.y.index_select(0, sel)
+            yield gather_batch(dev_idx[s:s + self.batch_size], self.x, self.y)

@@ -24,7 +24,7 @@ from __future__ import annotations
 import math
 import os
 import time
-from typing import Any, Dict, Iterable, Optional, Tuple
+from typing import Any, Dict, Iterable, List, Optional, Tuple
 
 import torch
 import torch.distributed as dist
@@ -214,6 +214,7 @@ class Engine:
         self.graph_fallback_reason = ""
         self.graph_module_reason = ""
         self._graphed_fwd: Dict[tuple, Any] = {}
+        self._runners: List[Any] = []  # every GraphedModule: the copying ones above and their bound ones
         self._last_graphed = None  # (shape, dtype, requires_grad, GraphedModule) of the last hit
         # graphed tail (runtime/graph_module.py): backward + collective + Adam as one replay when
         # the loss is the framework's own; the step counter Adam reads lives on the device
@@ -305,13 +306,48 @@ class Engine:
             if (self.graph_module and self.training and not kwargs and args
                     and (torch.is_tensor(args[0]) if len(args) == 1 else all(torch.is_tensor(a) for a in args))):
                 fn = self._graphed_forward(args)
-                # a second forward of this signature before the first one's backward runs eagerly:
-                # replaying would overwrite the activations the pending backward still needs
-                if fn is not None and not fn.pending:
-                    return fn(*args)
+                if fn is not None:
+                    if len(args) == 1 and self.config.amd.graph_bind_inputs:
+                        b = self._bound_runner(fn, args[0])
+                        if b is not None and not b.pending:
+                            return b(*args)
+                    # a second forward of this signature before the first one's backward runs
+                    # eagerly: replaying would overwrite the activations the pending backward needs
+                    if not fn.pending:
+                        return fn(*args)
             return self.module(*args, **kwargs)
 
     MAX_GRAPHED_SHAPES = 4
+    MAX_BOUND_ADDRESSES = 4
+    BIND_BUDGET_BYTES = 1 << 30  # device memory the bound graph pairs of one signature may hold
+
+    def _bound_runner(self, fn, a: torch.Tensor):
+        """Graphs that read the input where it lies (``GraphedModule(bind_inputs=True)``): captured
+        for an address seen twice in this signature's last 8 calls -- a loader's fresh batch, whose
+        block the caching allocator hands back every few steps (the loop variable still holds the
+        previous batch while the next one is allocated, so a few addresses take turns) -- and
+        replayed whenever the input is there again, which saves the copy into the static input (one
+        launch of a host-bound step).  Up to MAX_BOUND_ADDRESSES pairs within BIND_BUDGET_BYTES of
+        device memory.  None: take the copying graph."""
+        p = a.data_ptr()
+        b = fn.bound.get(p)
+        if b is not None:
+            return b
+        seen, fn.recent = fn.recent, (p,) + fn.recent[:7]
+        if (seen.count(p) < 2 or len(fn.bound) >= self.MAX_BOUND_ADDRESSES or fn.bind_failed
+                or (len(fn.bound) + 1) * fn.footprint > self.BIND_BUDGET_BYTES
+                or a.requires_grad or not a.is_contiguous()):
+            return None
+        from .runtime.graph_module import GraphedModule
+        self.store.rebind_grads()
+        try:
+            b = GraphedModule(self.module, self.params, (a,), tail=self._tail_callable(), bind_inputs=True)
+        except Exception as e:  # keep the copying graph
+            fn.bind_failed = f"{type(e).__name__}: {e}"
+            return None
+        fn.bound[p] = b
+        self._runners.append(b)
+        return b
 
     def _graphed_forward(self, args):
         """The module as a graphed callable for this input signature (``runtime/graph_module.py``):
@@ -332,13 +368,18 @@ class Engine:
         if fn is not None or len(self._graphed_fwd) >= self.MAX_GRAPHED_SHAPES:
             return fn
         self.store.rebind_grads()
+        before = torch.cuda.memory_reserved(self.device)
         try:
             fn = GraphedModule(self.module, self.params, args, tail=self._tail_callable())
         except Exception as e:  # data-dependent control flow, host syncs, ...: stay eager
             self.graph_module = False
             self.graph_module_reason = f"capture failed: {type(e).__name__}: {e}"
             return None
+        fn.bound, fn.recent, fn.bind_failed = {}, (), None
+        # what one more graph pair of this signature costs (its pool: activations, outputs)
+        fn.footprint = max(0, torch.cuda.memory_reserved(self.device) - before)
         self._graphed_fwd[key] = fn
+        self._runners.append(fn)
         return fn
 
     __call__ = forward
@@ -436,7 +477,7 @@ class Engine:
                 runner.static_gout[0].view(-1).copy_(dz.view(-1))
         with tracing.range("dgt.graphed_tail"):
             runner.bwd_tail.replay()
-        runner.pending = False
+        runner.finish()
         self._tail_step_host = want + 1
         self._tail_done = True
         self.tail_steps += 1
@@ -624,8 +665,8 @@ class Engine:
 
     def step(self, lr_kwargs=None) -> None:
         self.micro_steps += 1
-        for fn in self._graphed_fwd.values():  # a forward whose backward never came: its activations are dead
-            fn.pending = False
+        for fn in self._runners:  # a forward whose backward never came: its activations are dead
+            fn.finish()
         if self._tail_done:  # the graphed tail already reduced, clipped, updated and zeroed
             self._tail_done = False
             self._finish_step(skipped=False, zero=False)
@@ -864,6 +905,7 @@ class Engine:
             self.graphed.close()
             self.graphed = None
         self._graphed_fwd.clear()  # graph_module: the captured graphs and their memory pools
+        self._runners = []
         self._last_graphed = None
         for h in self._hooks:
             h.remove()

@@ -56,6 +56,52 @@ def require():
     return _OPS
 
 
+_FAST = None
+
+
+def fast():
+    """The hot eager-path ops (gather_rows, bce_logits, linear_fwd / linear_bwd, linear2_fwd /
+    linear2_bwd, adam_flat) as plain pybind11 functions of the same library
+    (``csrc/bindings.cpp`` PYBIND11_MODULE): same C++ code and arguments as ``torch.ops.dgt``, without
+    the boxed dispatcher's per-call cost.  Positional arguments only."""
+    global _FAST
+    if _FAST is None:
+        require()
+        import importlib.util
+        spec = importlib.util.spec_from_file_location("distributed_gpu_test_amd._C", LIB_PATH)
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        _FAST = mod
+    return _FAST
+
+
+class _Hot:
+    """``torch.ops.dgt`` with the :func:`fast` functions in place of their dispatcher entries."""
+
+    def __init__(self, fast_mod, ops):
+        self._ops = ops
+        for name in dir(fast_mod):
+            if not name.startswith("_"):
+                setattr(self, name, getattr(fast_mod, name))
+
+    def __getattr__(self, name):  # any other op: the dispatcher's, cached on first use
+        op = getattr(self._ops, name)
+        setattr(self, name, op)
+        return op
+
+
+_HOT = None
+
+
+def hot():
+    """The op namespace of the hot eager paths: :func:`fast` entries where they exist, else
+    ``torch.ops.dgt`` (raises like :func:`require` when the extension is missing)."""
+    global _HOT
+    if _HOT is None:
+        _HOT = _Hot(fast(), require())
+    return _HOT
+
+
 _clib = None
 
 

@@ -8,7 +8,7 @@ from typing import Optional
 
 import torch
 
-from ._ext import require
+from ._ext import hot
 from .reference import adam_flat_reference_
 
 
@@ -25,9 +25,9 @@ def adam_flat_(master: torch.Tensor, grad: torch.Tensor, exp_avg: torch.Tensor, 
     device int64 holding this update's 1-based step) replaces ``step`` for HIP-graph replay.
     """
     if master.is_cuda:
-        require().adam_flat(master, param_lp, grad, exp_avg, exp_avg_sq, float(lr), float(beta1), float(beta2),
-                            float(eps), float(weight_decay), bool(adamw), int(step), float(grad_scale),
-                            grad_scale_dev, step_dev)
+        hot().adam_flat(master, param_lp, grad, exp_avg, exp_avg_sq, float(lr), float(beta1), float(beta2),
+                        float(eps), float(weight_decay), bool(adamw), int(step), float(grad_scale),
+                        grad_scale_dev, step_dev)
     else:
         if step_dev is not None:
             step = int(step_dev.item())

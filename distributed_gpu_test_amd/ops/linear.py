@@ -34,6 +34,7 @@ import torch.nn.functional as F
 
 from ..models.synthetic_mlp import SyntheticMLP
 from . import _ext
+from ..utils.fnapply import fast_apply
 from .loss import FREED, keep_graph, release
 
 # > 0 while the engine runs a backward (Engine.backward / the graphed step): only then do the
@@ -191,7 +192,7 @@ def _bwd(ops, dy, x, weight, y, dx, dW, db, accumulate: bool = False, mask_dx=No
 class _FusedLinearFn(torch.autograd.Function):
     @staticmethod
     def forward(ctx, x, weight, bias, relu: bool, grad_in_place: bool = False):
-        y = _fwd(_ext.require(), x, weight, bias, relu)
+        y = _fwd(_ext.hot(), x, weight, bias, relu)
         ctx.relu = relu
         ctx.has_bias = bias is not None
         # leaf parameters only (no reference cycle through ctx)
@@ -222,11 +223,11 @@ class _FusedLinearFn(torch.autograd.Function):
             # AccumulateGrad nodes with an undefined gradient, which fire the post-accumulate hooks
             # (the engine's bucket reducer) after this kernel is queued
             bg = None if b_leaf is None else b_leaf.grad
-            _bwd(_ext.require(), dy, x, weight, y, dx, w_leaf.grad, bg, not _store_both(w_leaf.grad, bg))
+            _bwd(_ext.hot(), dy, x, weight, y, dx, w_leaf.grad, bg, not _store_both(w_leaf.grad, bg))
             return dx, None, None, None, None
         dw = torch.empty_like(weight)
         db = torch.empty(weight.shape[0], dtype=torch.float32, device=x.device) if ctx.has_bias else None
-        _bwd(_ext.require(), dy, x, weight, y, dx, dw, db)
+        _bwd(_ext.hot(), dy, x, weight, y, dx, dw, db)
         return dx, dw, db, None, None
 
 
@@ -253,7 +254,7 @@ def fused_linear(x: torch.Tensor, weight: torch.Tensor, bias=None, relu: bool = 
     into the existing ``.grad`` tensors of leaf parameters instead of returning them to autograd
     (their post-accumulate hooks still fire); any other backward gets them returned as usual."""
     if _fusable(x, weight, bias):
-        return _FusedLinearFn.apply(x.contiguous(), weight, bias, relu, grad_in_place)
+        return _linear_apply(x.contiguous(), weight, bias, relu, grad_in_place)
     if x.is_cuda:
         count_fallback(f"Linear({weight.shape[1]}, {weight.shape[0]}) with {weight.dtype} weights on "
                        f"{tuple(x.shape)} {x.dtype} input (fp32, contiguous parameters only)")
@@ -299,7 +300,7 @@ class _FusedChainFn(torch.autograd.Function):
 
     @staticmethod
     def forward(ctx, x, relus, grad_in_place, *wb):
-        ops = _ext.require()
+        ops = _ext.hot()
         acts = [x]
         h = x
         ctx.chain2 = _chain2(x, wb)
@@ -328,7 +329,7 @@ class _FusedChainFn(torch.autograd.Function):
 
     @staticmethod
     def backward(ctx, dy):
-        ops = _ext.require()
+        ops = _ext.hot()
         if ctx.freed:
             raise RuntimeError(FREED)
         L = len(ctx.relus)
@@ -408,7 +409,7 @@ class FusedChain(nn.Sequential):
                 relus = self.__dict__.get("_dgt_relus")
                 if relus is None:
                     relus = self.__dict__["_dgt_relus"] = tuple(m.relu for m in layers)
-                return _FusedChainFn.apply(x.contiguous(), relus, layers[0].grad_in_place, *wb)
+                return _chain_apply(x.contiguous(), relus, layers[0].grad_in_place, *wb)
         return super().forward(x)
 
 
@@ -427,7 +428,7 @@ class FusedSyntheticMLP(SyntheticMLP):
             for m in layers:
                 wb.append(m.weight)
                 wb.append(m.bias)
-            return _FusedChainFn.apply(x.contiguous(), tuple(m.relu for m in layers), layers[0].grad_in_place, *wb)
+            return _chain_apply(x.contiguous(), tuple(m.relu for m in layers), layers[0].grad_in_place, *wb)
         for m in self.layers:
             x = m(x)
         return self.head(x)
@@ -478,3 +479,7 @@ def inject_fused_linear(module: nn.Module, grad_in_place: bool = False) -> int:
         elif not isinstance(child, FusedLinear):
             n += inject_fused_linear(child, grad_in_place)
     return n
+
+
+_linear_apply = fast_apply(_FusedLinearFn)
+_chain_apply = fast_apply(_FusedChainFn)

@@ -28,6 +28,7 @@ import torch
 import torch.nn.functional as F
 
 from . import _ext
+from ..utils.fnapply import fast_apply
 
 _UNIT: dict = {}
 
@@ -119,7 +120,7 @@ class _FusedBCEWithLogits(torch.autograd.Function):
         else:
             dz = gbuf.view(-1) if gbuf is not None else torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
             lp = None
-        _ext.require().bce_logits(zc, yc, loss, dz, lp, sum_into)
+        _ext.hot().bce_logits(zc, yc, loss, dz, lp, sum_into)
         ctx.dz, ctx.lp, ctx.freed, ctx.held = dz, lp, False, ("dz", "lp")
         ctx.shape, ctx.dtype = z.shape, z.dtype
         return loss.view(())
@@ -141,6 +142,9 @@ class _FusedBCEWithLogits(torch.autograd.Function):
         return gz, None, None
 
 
+_bce_apply = fast_apply(_FusedBCEWithLogits)
+
+
 def bce_with_logits(z: torch.Tensor, y: torch.Tensor, sum_into: Optional[torch.Tensor] = None) -> torch.Tensor:
     """Mean BCE-with-logits; the fused HIP kernel on GPU fp32 / bf16 logits.  ``sum_into`` (one fp64
     element on the logits' device): the loss is also added to it -- a training loop's running loss
@@ -151,7 +155,7 @@ def bce_with_logits(z: torch.Tensor, y: torch.Tensor, sum_into: Optional[torch.T
         raise ValueError("bce_with_logits: sum_into must be one fp64 element on the logits' device")
     if (z.is_cuda and z.dtype in (torch.float32, torch.bfloat16) and z.numel() == y.numel() and z.numel() > 0
             and _ext.require() is not None):  # on the GPU a missing extension is an error, not a fallback
-        return _FusedBCEWithLogits.apply(z, y, sum_into)
+        return _bce_apply(z, y, sum_into)
     loss = F.binary_cross_entropy_with_logits(z, y.to(z.dtype))
     if sum_into is not None:
         sum_into.add_(loss.detach())

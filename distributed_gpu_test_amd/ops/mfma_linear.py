@@ -38,6 +38,7 @@ import torch.nn as nn
 
 from ..models.synthetic_mlp import SyntheticMLP
 from .gemm import gemm_nt, partials_reduce_multi, rowsum_bf16, skinny_bwd_bf16, skinny_fwd_bf16, transpose_bf16
+from ..utils.fnapply import fast_apply
 from .linear import _first_write, _grad_view_ok, _in_place_active, count_fallback
 
 MAX_HEAD = 4
@@ -252,7 +253,7 @@ def run_chain(x: torch.Tensor, linears: Sequence[nn.Linear], relus: Sequence[boo
     if why is not None:
         count_fallback(f"bf16 MFMA chain: {why}")
         return None
-    return _MfmaChainFn.apply(x.contiguous(), tuple(relus), head, grad_in_place, *wb)
+    return _mfma_chain_apply(x.contiguous(), tuple(relus), head, grad_in_place, *wb)
 
 
 class MfmaSequential(nn.Sequential):
@@ -326,3 +327,6 @@ def inject_mfma_linear(module: nn.Module, grad_in_place: bool = False) -> int:
     if n == 0 and type(module) is nn.Linear:
         count_fallback(f"bf16 Linear({module.in_features}, {module.out_features}) outside a recognised chain")
     return n
+
+
+_mfma_chain_apply = fast_apply(_MfmaChainFn)

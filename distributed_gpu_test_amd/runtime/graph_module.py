@@ -42,12 +42,20 @@ def _as_tuple(out) -> Tuple[torch.Tensor, ...]:
 
 class GraphedModule:
     def __init__(self, module: torch.nn.Module, params: Sequence[torch.nn.Parameter], args: Sequence[torch.Tensor],
-                 warmup: int = 2, tail: Optional[Callable[[], None]] = None):
+                 warmup: int = 2, tail: Optional[Callable[[], None]] = None, bind_inputs: bool = False):
         self.params: List[torch.nn.Parameter] = list(params)
         self.grad_views = [p.grad for p in self.params]
         if any(g is None or g.shape != p.shape for g, p in zip(self.grad_views, self.params)):
             raise RuntimeError("graph_module needs the engine's gradient views bound (.grad) before capture")
-        self.static_in = tuple(a.detach().clone().requires_grad_(a.requires_grad) for a in args)
+        # bind_inputs: the graphs read the caller's input tensors where they lie (no static copy);
+        # replayed only for inputs at the same addresses (``bound_ptrs``), see Engine._graphed_forward
+        self.bound_ptrs = None
+        if bind_inputs:
+            if any(a.requires_grad or not a.is_contiguous() for a in args):
+                raise ValueError("bind_inputs needs contiguous inputs that do not require grad")
+            self.static_in = tuple(a.detach() for a in args)
+        else:
+            self.static_in = tuple(a.detach().clone().requires_grad_(a.requires_grad) for a in args)
         self.in_rg = [i for i, a in enumerate(self.static_in) if a.requires_grad]
         # The graphs run the module on ALIASES of its parameters (same storage, so optimizer updates
         # are seen, but separate autograd leaves): capture never touches the real parameters'
@@ -120,6 +128,12 @@ class GraphedModule:
         self.single = torch.is_tensor(out) or len(out) == 1
         self.replays = 0
         self.pending = False  # a replayed forward whose backward has not run yet
+        self.held = None  # bound inputs of the pending forward: alive (and unmoved) until its backward
+        if bind_inputs:
+            # keep no reference to the caller's tensors: their blocks go back to the caching
+            # allocator, which hands the same addresses to the next step's batch
+            self.bound_ptrs = tuple(a.data_ptr() for a in self.static_in)
+            self.static_in = None
         # the framework's fused BCE on this graph's (single, differentiable) output writes its
         # d loss / d logits straight into the backward graph's static input (ops/loss.py
         # claim_gout): no copy before the backward replay.  One claim per forward replay.
@@ -140,17 +154,27 @@ class GraphedModule:
 
     def __call__(self, *args):
         grad = torch.is_grad_enabled()  # the caller's mode: inside Function.forward it is always off
-        outs = _Replay.apply(self, *args, *self.params)
+        outs = _replay_apply(self, *args, *self.params)
         self.pending = grad  # under no_grad no backward will come
+        if self.bound_ptrs is not None:
+            self.held = args if grad else None
         return outs[0] if self.single else outs
+
+    def finish(self) -> None:
+        """The pending forward's backward has been replayed."""
+        self.pending = False
+        self.held = None
 
 
 class _Replay(torch.autograd.Function):
     @staticmethod
     def forward(ctx, runner: GraphedModule, *tensors):
-        for dst, src in zip(runner.static_in, tensors[:len(runner.static_in)]):
-            if dst.data_ptr() != src.data_ptr():
-                dst.copy_(src)
+        if runner.bound_ptrs is None:
+            for dst, src in zip(runner.static_in, tensors[:len(runner.static_in)]):
+                if dst.data_ptr() != src.data_ptr():
+                    dst.copy_(src)
+        elif any(p != t.data_ptr() for p, t in zip(runner.bound_ptrs, tensors)):
+            raise RuntimeError("graph_module: a bound graph replayed for inputs at other addresses")
         runner.fwd.replay()
         runner.replays += 1
         runner.gout_claimable = True
@@ -164,7 +188,6 @@ class _Replay(torch.autograd.Function):
     @staticmethod
     def backward(ctx, *gouts):
         r: GraphedModule = ctx.runner
-        r.pending = False
         for dst, i in zip(r.static_gout, r.grad_out_idx):
             g = gouts[i]
             if g is None:
@@ -172,7 +195,13 @@ class _Replay(torch.autograd.Function):
             elif g.data_ptr() != dst.data_ptr():  # (the fused BCE may have written it in place)
                 dst.copy_(g)
         r.bwd.replay()
-        grads_in: List = [None] * len(r.static_in)
+        r.finish()
+        grads_in: List = [None] * (len(r.bound_ptrs) if r.bound_ptrs is not None else len(r.static_in))
         for i, g in zip(r.in_rg, r.static_gin):
             grads_in[i] = None if g is None else g.detach().clone()
         return (None, *grads_in, *([None] * len(r.params)))
+
+
+from ..utils.fnapply import fast_apply  # noqa: E402
+
+_replay_apply = fast_apply(_Replay)

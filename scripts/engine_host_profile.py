@@ -28,6 +28,7 @@ def main():
     ap.add_argument("--steps", type=int, default=2000)
     ap.add_argument("--config", default=None)
     ap.add_argument("--top", type=int, default=30)
+    ap.add_argument("--no-cprofile", action="store_true", help="only the unprofiled timings")
     a = ap.parse_args()
     comm.init_distributed()
     dev = torch.device("cuda", 0) if torch.cuda.is_available() else torch.device("cpu")
@@ -42,10 +43,17 @@ def main():
         torch.cuda.synchronize()
     t0 = time.perf_counter()
     b.run_plan(plan, counts)
+    t1 = time.perf_counter()  # the host has enqueued every step
     if dev.type == "cuda":
         torch.cuda.synchronize()
     dt = time.perf_counter() - t0
-    print(f"[engine-host] impl={b.impl} {dt / a.steps * 1e6:.1f} us/step ({a.steps / dt:.0f} it/s) unprofiled")
+    # enqueue ~= total: host-bound; total >> enqueue: the device (or its dispatch) is the limit
+    print(f"[engine-host] impl={b.impl} {dt / a.steps * 1e6:.1f} us/step ({a.steps / dt:.0f} it/s) unprofiled, "
+          f"host enqueue {(t1 - t0) / a.steps * 1e6:.1f} us/step")
+    if a.no_cprofile:
+        b.close()
+        comm.destroy()
+        return
     pr = cProfile.Profile()
     pr.enable()
     b.run_plan(plan, counts)

@@ -205,3 +205,17 @@ def test_rank_info_mpi():
     assert (ri.rank, ri.local_rank, ri.node_rank, ri.master_addr) == (9, 1, 1, "127.0.0.1")
     # torchrun variables win when both are present
     assert resolve_rank_info({**ompi, "RANK": "0", "WORLD_SIZE": "1"}).source == "torchrun"
+
+
+def test_gather_batch_cpu_is_index_select():
+    """data.gather_batch off the GPU: index_select per tensor (the one-launch HIP gather is GPU-only,
+    tests/test_gpu_engine.py); SyntheticDataset yields through it."""
+    import torch
+    from distributed_gpu_test_amd.data import SyntheticDataset, gather_batch
+    x, y = torch.randn(30, 5), torch.randn(30, 1)
+    rows = torch.tensor([4, 0, 29, 4])
+    gx, gy = gather_batch(rows, x, y)
+    assert torch.equal(gx, x[rows]) and torch.equal(gy, y[rows])
+    ds = SyntheticDataset(x, y, 4, world_size=2, rank=1)
+    batches = list(ds)
+    assert len(batches) == len(ds) and batches[0][0].shape == (4, 5)

@@ -765,7 +765,9 @@ def test_graph_module_fused_bce_writes_gradient_in_place(bf16):
     for i, (x, y) in enumerate(batches):
         out = e2(x)
         loss = crit(out.float() if not bf16 else out, y)
-        runner = next(iter(e2._graphed_fwd.values()))
+        # the graph pair this forward replayed (bf16: the engine's cast of x recurs at one address,
+        # so a bound pair takes over)
+        runner = next((r for r in e2._runners if r.pending), None)
         if i > 0:  # (the first forward of a signature captures; its output is not a replay)
             buf = loss.grad_fn.lp if bf16 else loss.grad_fn.dz
             assert buf.data_ptr() == runner.static_gout[0].data_ptr()
@@ -814,3 +816,105 @@ def test_fused_chain2_one_launch_is_bitwise_per_layer(B, F, H, O, relu_out, in_p
     assert torch.equal(outs[0], outs[1]) and torch.equal(dxs[0], dxs[1])
     for p, q in zip(chain.parameters(), layered.parameters()):
         assert torch.equal(p.grad, q.grad)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("shape,dtype", [((50, 20), torch.float32), ((50, 1), torch.float32), ((40, 8, 4), torch.float32),
+                                         ((33, 6), torch.bfloat16), ((33, 3), torch.bfloat16), ((20, 5), torch.int32)])
+def test_gather_batch_matches_index_select(shape, dtype):
+    """data.gather_batch: the rows of every dataset tensor in one launch (csrc/data.hip), equal to
+    index_select, for 16-byte and 4-byte row words and for rows it cannot take (6-byte bf16 rows:
+    index_select itself)."""
+    from distributed_gpu_test_amd.data import gather_batch
+    g = torch.Generator().manual_seed(shape[0])
+    x = (torch.randn(shape, generator=g) * 100).to(dtype).cuda()
+    y = torch.randn(shape[0], 1, generator=g).cuda()
+    rows = torch.randint(0, shape[0], (17,), generator=g).cuda()
+    gx, gy = gather_batch(rows, x, y)
+    assert torch.equal(gx, x.index_select(0, rows)) and torch.equal(gy, y.index_select(0, rows))
+    assert gx.is_contiguous() and gx.data_ptr() != x.data_ptr()
+    e, = gather_batch(rows[:0], x)
+    assert e.shape == (0,) + tuple(shape[1:])
+
+
+@pytest.mark.gpu
+def test_gather_batch_out_of_range_is_a_zero_row():
+    from distributed_gpu_test_amd.data import gather_batch
+    x = torch.arange(1, 41, dtype=torch.float32, device="cuda").view(10, 4)
+    got, = gather_batch(torch.tensor([3, 10, -1, 0], device="cuda"), x)
+    assert torch.equal(got[0], x[3]) and torch.equal(got[3], x[0]) and not got[1:3].any()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [{}, {"zero_optimization": {"stage": 1}}, {"bf16": {"enabled": True}}])
+def test_graph_module_binds_recurring_input_addresses(extra):
+    """graph_module: a loader's fresh batch lands at the same address step after step (the caching
+    allocator recycles its block), so the engine captures graphs that read the input in place (no
+    copy into a static input) and replays them while the input is there; a batch elsewhere takes the
+    copying graph.  The trajectory matches the eager engine, with and without the graphed tail."""
+    from distributed_gpu_test_amd.data import gather_batch
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    g = torch.Generator().manual_seed(31)
+    X = torch.randn(400, 64, generator=g).cuda()
+    Y = (torch.rand(400, 1, generator=g) > 0.5).float().cuda()
+    plan = torch.randint(0, 400, (24, 32), generator=g).cuda()
+    cfg = {"train_batch_size": 32, **extra}
+    tol = dict(rtol=2e-2, atol=2e-3) if "bf16" in extra else dict(rtol=1e-5, atol=1e-6)
+    for crit in (BCEWithLogitsLoss(), torch.nn.BCEWithLogitsLoss()):
+        runs = []
+        for amd in ({}, {"graph_module": True}):
+            m = _mlp(12)
+            e = dgt.initialize(model=m, optimizer=torch.optim.Adam(m.parameters(), lr=1e-3),
+                               config=dict(cfg, amd=amd))[0]
+            losses, keep = [], []
+            for s in range(plan.shape[0]):
+                xb, yb = gather_batch(plan[s], X, Y)
+                if s in (20, 21):
+                    keep.append(xb)  # held across steps: the next batches land elsewhere
+                loss = crit(e(xb).float(), yb)
+                e.backward(loss)
+                e.step()
+                losses.append(float(loss))
+            runs.append((e, losses, e.store.param_buf.detach().float().clone()))
+        (e1, l1, p1), (e2, l2, p2) = runs
+        fn = next(iter(e2._graphed_fwd.values()))
+        assert fn.bound and fn.bind_failed is None, fn.bind_failed
+        bound_replays = sum(b.replays for b in fn.bound.values())
+        assert bound_replays >= 14 and fn.replays >= 1, (bound_replays, fn.replays)
+        assert all(b.held is None and not b.pending for b in fn.bound.values())
+        torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), **tol)
+        torch.testing.assert_close(p2, p1, **tol)
+        e1.close()
+        e2.close()
+
+
+@pytest.mark.gpu
+def test_graph_module_bound_graph_guards_double_forward_and_off_switch():
+    """A second forward of a bound input before its backward runs eagerly (its activations are
+    pending); amd.graph_bind_inputs=false never binds."""
+    from distributed_gpu_test_amd.data import gather_batch
+    X = torch.randn(64, 64, device="cuda")
+    Y = (torch.rand(64, 1, device="cuda") > 0.5).float()
+    rows = torch.arange(32, device="cuda")
+    for bind in (True, False):
+        m = _mlp(13)
+        e = dgt.initialize(model=m, config={"train_batch_size": 32,
+                                            "amd": {"graph_module": True, "graph_bind_inputs": bind}})[0]
+        crit = torch.nn.BCEWithLogitsLoss()
+        for _ in range(8):
+            xb, yb = gather_batch(rows, X, Y)
+            e.backward(crit(e(xb), yb))
+            e.step()
+        fn = next(iter(e._graphed_fwd.values()))
+        assert bool(fn.bound) == bind
+        if bind:
+            b = next(iter(fn.bound.values()))
+            xb, yb = gather_batch(rows, X, Y)
+            out1 = e(xb)
+            assert b.pending and b.held is not None
+            out2 = e(xb)  # eager: must not overwrite out1's activations
+            assert out2.data_ptr() != out1.data_ptr()
+            e.backward(crit(out1, yb) + crit(out2, yb))
+            e.step()
+            assert not b.pending and b.held is None
+        e.close()

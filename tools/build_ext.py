@@ -98,7 +98,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 8, variant: st
         list(ex.map(lambda c: _run(c, verbose), jobs_list))
     if force or jobs_list or _newer(OUT, objs):
         _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", *objs, "-o", OUT,
-              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-lrccl",
+              f"-L{tlib}", "-lc10", "-lc10_hip", "-ltorch_cpu", "-ltorch_hip", "-ltorch", "-ltorch_python", "-lrccl",
               f"-Wl,-rpath,{tlib}"], verbose)
 
     # standalone native tools (no torch): link straight against ROCm's HIP + RCCL
