@@ -638,6 +638,8 @@ def main(argv=None):
         "allreduce_sweep_error": sweep_error,
         "hung": hung,
     }
+    if getattr(trainer, "graph_stats", None) is not None:
+        out["engine_graph_replays"] = trainer.graph_stats
     out.update(secondary)
     if rank == 0:
         print(json.dumps(out), flush=True)
@@ -846,6 +848,17 @@ class DgtEngineBench(EngineBench):
         batches = [plan_d[s, :c] for s, c in enumerate(counts.tolist())]
         for rows in batches:
             self.step(rows)
+
+    @property
+    def graph_stats(self):
+        """graph_module: forward replays of the copying graphs and of the graphs bound to the
+        batch's recurring addresses (engine.py _bound_runner)."""
+        fns = list(self.engine._graphed_fwd.values())
+        if not fns:
+            return None
+        return {"copying": sum(f.replays for f in fns),
+                "bound": sum(b.replays for f in fns for b in f.bound.values()),
+                "bound_graphs": sum(len(f.bound) for f in fns), "evictions": sum(f.evictions for f in fns)}
 
     @property
     def params(self):

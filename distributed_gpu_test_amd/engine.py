@@ -60,6 +60,10 @@ def _direct_node_classes():
     return _DIRECT_KINDS
 
 
+def _bce_node_class():
+    return _direct_node_classes()[0]
+
+
 class FlatAdamOptimizer:
     """Optimizer facade handed back by ``initialize`` (the engine drives the actual update)."""
 
@@ -328,23 +332,40 @@ class Engine:
         previous batch while the next one is allocated, so a few addresses take turns) -- and
         replayed whenever the input is there again, which saves the copy into the static input (one
         launch of a host-bound step).  Up to MAX_BOUND_ADDRESSES pairs within BIND_BUDGET_BYTES of
-        device memory.  None: take the copying graph."""
+        device memory; a pair unused for 16 calls gives way to a new address.  None: take the
+        copying graph."""
         p = a.data_ptr()
+        fn.calls += 1
         b = fn.bound.get(p)
         if b is not None:
+            b.last_use = fn.calls
             return b
         seen, fn.recent = fn.recent, (p,) + fn.recent[:7]
-        if (seen.count(p) < 2 or len(fn.bound) >= self.MAX_BOUND_ADDRESSES or fn.bind_failed
-                or (len(fn.bound) + 1) * fn.footprint > self.BIND_BUDGET_BYTES
-                or a.requires_grad or not a.is_contiguous()):
+        if seen.count(p) < 2 or fn.bind_failed or a.requires_grad or not a.is_contiguous():
+            return None
+        if len(fn.bound) >= self.MAX_BOUND_ADDRESSES:
+            # addresses of an earlier phase (e.g. before another capture moved the allocator's
+            # blocks) make room once unused for a while; bounded, so a churning pattern stops binding
+            stale = [q for q, r in fn.bound.items() if not r.pending and fn.calls - r.last_use > 16]
+            if not stale:
+                return None
+            if fn.evictions >= 16:
+                fn.bind_failed = "input addresses keep changing"
+                return None
+            victim = fn.bound.pop(min(stale, key=lambda q: fn.bound[q].last_use))
+            self._runners.remove(victim)
+            fn.evictions += 1
+        if (len(fn.bound) + 1) * fn.footprint > self.BIND_BUDGET_BYTES:
             return None
         from .runtime.graph_module import GraphedModule
         self.store.rebind_grads()
         try:
-            b = GraphedModule(self.module, self.params, (a,), tail=self._tail_callable(), bind_inputs=True)
+            # no warmup: the copying pair of this signature already ran it (library handles, workspaces)
+            b = GraphedModule(self.module, self.params, (a,), warmup=0, tail=self._tail_callable(), bind_inputs=True)
         except Exception as e:  # keep the copying graph
             fn.bind_failed = f"{type(e).__name__}: {e}"
             return None
+        b.last_use = fn.calls
         fn.bound[p] = b
         self._runners.append(b)
         return b
@@ -375,7 +396,7 @@ class Engine:
             self.graph_module = False
             self.graph_module_reason = f"capture failed: {type(e).__name__}: {e}"
             return None
-        fn.bound, fn.recent, fn.bind_failed = {}, (), None
+        fn.bound, fn.recent, fn.bind_failed, fn.calls, fn.evictions = {}, (), None, 0, 0
         # what one more graph pair of this signature costs (its pool: activations, outputs)
         fn.footprint = max(0, torch.cuda.memory_reserved(self.device) - before)
         self._graphed_fwd[key] = fn
@@ -418,7 +439,7 @@ class Engine:
         form without autograd: the BCE kernel already wrote it (d loss / d logits), and with no loss
         scaling and one micro-step the backward seed is 1.  Else None (the autograd path)."""
         node = loss.grad_fn
-        if node is None or type(node).__name__ != "_FusedBCEWithLogitsBackward":
+        if node is None or type(node) is not _bce_node_class():
             return None
         nxt = node.next_functions  # (logits, targets[, sum_into])
         if len(nxt) < 2 or any(e[0] is not None for e in nxt[1:]):
@@ -453,7 +474,8 @@ class Engine:
                 or self.loss_scaler is not None or self._grads_dirty or self.faults.spec is not None
                 or self.config.wall_clock_breakdown):
             return False
-        if self.store.user_set_grads():
+        grads = self.store.grads_state()
+        if grads == 2:  # a user-set .grad
             return False
         found = self._tail_runner(loss)
         if found is None:
@@ -465,7 +487,8 @@ class Engine:
         if g["lr"] != runner.tail_lr:
             self.tail_reason = "the lr changed since the tail was captured"
             return False
-        self.store.rebind_grads()
+        if grads:
+            self.store.rebind_grads()
         if self._zero_deferred:  # the last eager step left its gradients in place (deferred zeroing)
             self.store.grad_buf.zero_()
             self._zero_deferred = False

@@ -108,22 +108,25 @@ def _is_unit(g: torch.Tensor) -> bool:
 class _FusedBCEWithLogits(torch.autograd.Function):
     @staticmethod
     def forward(ctx, z: torch.Tensor, y: torch.Tensor, sum_into=None) -> torch.Tensor:
-        zc = z.contiguous().reshape(-1)
-        yc = y.reshape(-1).to(torch.float32).contiguous()
-        loss = torch.empty(1, dtype=torch.float32, device=z.device)
+        # the kernel reads z and y as flat contiguous arrays of the same length (any shapes); the
+        # common case -- contiguous logits, fp32 targets -- passes both as they are (host-bound step)
+        zc = z if z.is_contiguous() else z.contiguous()
+        yc = y if (y.dtype == torch.float32 and y.is_contiguous()) else y.to(torch.float32).contiguous()
+        dev = z.device
+        loss = torch.empty((), dtype=torch.float32, device=dev)
         # the gradient a graphed module's backward replays from: written in place when z is that
         # module's fresh output (fp32: dz itself, bf16: the once-rounded copy)
-        gbuf = _gout_buffer(zc, z.dtype)
+        gbuf = _gout_buffer(zc, z.dtype) if _GOUT_ALIAS else None
         if z.dtype == torch.bfloat16:
-            dz = torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
-            lp = gbuf.view(-1) if gbuf is not None else torch.empty(zc.numel(), dtype=torch.bfloat16, device=z.device)
+            dz = torch.empty(zc.shape, dtype=torch.float32, device=dev)
+            lp = gbuf if gbuf is not None else torch.empty(zc.shape, dtype=torch.bfloat16, device=dev)
         else:
-            dz = gbuf.view(-1) if gbuf is not None else torch.empty(zc.numel(), dtype=torch.float32, device=z.device)
+            dz = gbuf if gbuf is not None else torch.empty(zc.shape, dtype=torch.float32, device=dev)
             lp = None
         _ext.hot().bce_logits(zc, yc, loss, dz, lp, sum_into)
         ctx.dz, ctx.lp, ctx.freed, ctx.held = dz, lp, False, ("dz", "lp")
         ctx.shape, ctx.dtype = z.shape, z.dtype
-        return loss.view(())
+        return loss
 
     @staticmethod
     def backward(ctx, g: torch.Tensor):

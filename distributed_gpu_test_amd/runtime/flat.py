@@ -117,6 +117,19 @@ class FlatParamStore:
                 return True
         return False
 
+    def grads_state(self) -> int:
+        """0: every .grad IS its view; 1: some are None or equivalent views (rebind_grads reattaches
+        them); 2: user code set a gradient of its own (``user_set_grads``).  One pass."""
+        state = 0
+        for p, view in zip(self.params, self.grad_views):
+            g = p.grad
+            if g is view:
+                continue
+            if g is not None and (g.data_ptr() != view.data_ptr() or g.shape != view.shape):
+                return 2
+            state = 1
+        return state
+
     def rebind_grads(self) -> bool:
         """Re-attach gradient views (after user code set ``.grad = None``).  Called every backward:
         the common case (every .grad still IS its cached view) costs one identity test per

@@ -40,6 +40,40 @@ def _as_tuple(out) -> Tuple[torch.Tensor, ...]:
     raise TypeError(f"graph_module needs a module returning a tensor or a tuple of tensors, got {type(out).__name__}")
 
 
+_CAPTURE_STREAMS: dict = {}
+
+
+class _capture:
+    """``torch.cuda.graph`` without its ``gc.collect()`` + ``empty_cache()`` on entry: emptying the
+    caching allocator moves every later allocation, so the addresses bound graphs were captured for
+    (``bind_inputs``) would never come back.  Captures on one side stream per device, ordered
+    after and before the caller's stream."""
+
+    __slots__ = ("graph", "pool", "stream", "ctx")
+
+    def __init__(self, graph: "torch.cuda.CUDAGraph", pool):
+        self.graph, self.pool = graph, pool
+        dev = torch.cuda.current_device()
+        self.stream = _CAPTURE_STREAMS.get(dev)
+        if self.stream is None:
+            self.stream = _CAPTURE_STREAMS[dev] = torch.cuda.Stream()
+
+    def __enter__(self):
+        self.stream.wait_stream(torch.cuda.current_stream())
+        self.ctx = torch.cuda.stream(self.stream)
+        self.ctx.__enter__()
+        self.graph.capture_begin(pool=self.pool)
+        return self
+
+    def __exit__(self, *exc):
+        try:
+            self.graph.capture_end()
+        finally:
+            self.ctx.__exit__(*exc)
+            torch.cuda.current_stream().wait_stream(self.stream)
+        return False
+
+
 class GraphedModule:
     def __init__(self, module: torch.nn.Module, params: Sequence[torch.nn.Parameter], args: Sequence[torch.Tensor],
                  warmup: int = 2, tail: Optional[Callable[[], None]] = None, bind_inputs: bool = False):
@@ -63,6 +97,7 @@ class GraphedModule:
         # created on a capture stream they would put a cross-stream wait into every later backward
         # (and, during capture, an event wait on a non-capturing stream).
         by_id = {id(p): n for n, p in module.named_parameters()}
+        self._param_ix = {id(p): i for i, p in enumerate(self.params)}
         if any(id(p) not in by_id for p in self.params):
             raise RuntimeError("graph_module: every trained tensor must be a parameter of the module")
         self.aliases = {n: p.detach().requires_grad_(p.requires_grad) for n, p in module.named_parameters()}
@@ -71,35 +106,46 @@ class GraphedModule:
         def run():
             return _as_tuple(torch.func.functional_call(module, self.aliases, self.static_in))
 
-        cur = torch.cuda.current_stream()
-        side = torch.cuda.Stream()
-        side.wait_stream(cur)
-        # the warmup executes the module: keep its buffers and the RNG streams as they were
-        bufs = [(b, b.detach().clone()) for b in module.buffers()]
-        cpu_rng, gpu_rng = torch.get_rng_state(), torch.cuda.get_rng_state()
-        with torch.cuda.stream(side):  # library handles / workspaces before capture
-            for _ in range(warmup):
-                outs = [o for o in run() if o.requires_grad]
-                torch.autograd.grad(outs, targets, grad_outputs=[torch.ones_like(o) for o in outs],
-                                    allow_unused=True)
-                del outs
-        cur.wait_stream(side)
-        with torch.no_grad():
-            for b, saved in bufs:
-                b.copy_(saved)
-        torch.set_rng_state(cpu_rng)
-        torch.cuda.set_rng_state(gpu_rng)
+        if warmup:
+            cur = torch.cuda.current_stream()
+            side = torch.cuda.Stream()
+            side.wait_stream(cur)
+            # the warmup executes the module: keep its buffers and the RNG streams as they were
+            bufs = [(b, b.detach().clone()) for b in module.buffers()]
+            cpu_rng, gpu_rng = torch.get_rng_state(), torch.cuda.get_rng_state()
+            with torch.cuda.stream(side):  # library handles / workspaces before capture
+                for _ in range(warmup):
+                    outs = [o for o in run() if o.requires_grad]
+                    torch.autograd.grad(outs, targets, grad_outputs=[torch.ones_like(o) for o in outs],
+                                        allow_unused=True)
+                    del outs
+            cur.wait_stream(side)
+            with torch.no_grad():
+                for b, saved in bufs:
+                    b.copy_(saved)
+            torch.set_rng_state(cpu_rng)
+            torch.cuda.set_rng_state(gpu_rng)
         self.pool = torch.cuda.graph_pool_handle()
         self.fwd = torch.cuda.CUDAGraph()
-        with torch.cuda.graph(self.fwd, pool=self.pool):
+        with _capture(self.fwd, self.pool):
             out = run()
+            self.grad_out_idx = [i for i, o in enumerate(out) if o.requires_grad]
+            # allocated in the graph's pool, not the caller's: a block taken from the caching
+            # allocator here would shift the addresses the caller's next batches land at
+            self.static_gout = [torch.empty_like(out[i]) for i in self.grad_out_idx]
         self.static_out = out
-        self.grad_out_idx = [i for i, o in enumerate(out) if o.requires_grad]
-        self.static_gout = [torch.empty_like(out[i]) for i in self.grad_out_idx]
         self.bwd = torch.cuda.CUDAGraph()
+        # The injected HIP Linear kernels (ops/linear.py, ops/mfma_linear.py) add dW / db straight into
+        # their parameter's .grad inside an engine backward: with the aliases' .grad bound to the
+        # engine's gradient views, the captured backward needs no separate add per parameter (one
+        # graph node each); parameters of other modules still come back from autograd and are added.
+        from ..ops.linear import engine_backward
+        for n, p in module.named_parameters():
+            if id(p) in self._param_ix:
+                self.aliases[n].grad = self.grad_views[self._param_ix[id(p)]]
         # a tail (below) captures this backward a second time, so keep the autograd graph for it
         with_tail = tail is not None and not self.in_rg
-        with torch.cuda.graph(self.bwd, pool=self.pool):
+        with _capture(self.bwd, self.pool), engine_backward(False):
             gs = torch.autograd.grad([out[i] for i in self.grad_out_idx], targets, grad_outputs=self.static_gout,
                                      allow_unused=True, retain_graph=with_tail)
             with torch.no_grad():
@@ -116,7 +162,7 @@ class GraphedModule:
         self.tail_lr = getattr(tail, "lr", None)  # baked into the captured Adam launch
         if with_tail:
             self.bwd_tail = torch.cuda.CUDAGraph()
-            with torch.cuda.graph(self.bwd_tail, pool=self.pool):
+            with _capture(self.bwd_tail, self.pool), engine_backward(False):
                 gs2 = torch.autograd.grad([out[i] for i in self.grad_out_idx], targets[:len(self.params)],
                                           grad_outputs=self.static_gout, allow_unused=True)
                 with torch.no_grad():
@@ -126,6 +172,7 @@ class GraphedModule:
                     tail()
             del gs2
         self.single = torch.is_tensor(out) or len(out) == 1
+        self.fwd_replay = torch._C._CUDAGraph.replay.__get__(self.fwd)  # (no Python wrapper frame per step)
         self.replays = 0
         self.pending = False  # a replayed forward whose backward has not run yet
         self.held = None  # bound inputs of the pending forward: alive (and unmoved) until its backward
@@ -154,11 +201,11 @@ class GraphedModule:
 
     def __call__(self, *args):
         grad = torch.is_grad_enabled()  # the caller's mode: inside Function.forward it is always off
-        outs = _replay_apply(self, *args, *self.params)
+        outs = _replay_apply(self, *args, *self.params)  # (a single output comes back as a tensor)
         self.pending = grad  # under no_grad no backward will come
         if self.bound_ptrs is not None:
             self.held = args if grad else None
-        return outs[0] if self.single else outs
+        return outs
 
     def finish(self) -> None:
         """The pending forward's backward has been replayed."""
@@ -175,15 +222,17 @@ class _Replay(torch.autograd.Function):
                     dst.copy_(src)
         elif any(p != t.data_ptr() for p, t in zip(runner.bound_ptrs, tensors)):
             raise RuntimeError("graph_module: a bound graph replayed for inputs at other addresses")
-        runner.fwd.replay()
+        runner.fwd_replay()
         runner.replays += 1
         runner.gout_claimable = True
         ctx.runner = runner
+        if runner.single and runner.grad_out_idx:
+            return runner.static_out[0].detach()
         outs = tuple(o.detach() for o in runner.static_out)
         for i, o in enumerate(outs):
             if i not in runner.grad_out_idx:
                 ctx.mark_non_differentiable(o)
-        return outs
+        return outs[0] if runner.single else outs
 
     @staticmethod
     def backward(ctx, *gouts):

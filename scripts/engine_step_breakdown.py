@@ -86,7 +86,8 @@ def main():
     base = min(ptrs)
     print(f"[breakdown] batch addresses (offsets): {[p - base for p in ptrs]}")
     for fn in eng._graphed_fwd.values():
-        print(f"[breakdown] copying-graph replays {fn.replays}, bound {[r.replays for r in fn.bound.values()]}"
+        print(f"[breakdown] copying-graph replays {fn.replays}, bound {[r.replays for r in fn.bound.values()]}, "
+              f"evictions {fn.evictions}"
               f"{' bind failed: ' + fn.bind_failed if fn.bind_failed else ''}", flush=True)
     b.close()
     comm.destroy()

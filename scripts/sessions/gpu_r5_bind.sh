@@ -14,7 +14,7 @@ done
 for rep in 1 2 3 4; do
 for cfg in "" configs/ds_graph_module.json; do
   timeout -k 10 200 python bench.py --impl dgt-engine ${cfg:+--deepspeed-config $cfg} --steps 3000 --warmup 200 --no-sweep > $O/eng.json 2> $O/eng.err || { tail -20 $O/eng.err; exit 1; }
-  python -c "import json; d=json.loads(open('$O/eng.json').read().splitlines()[-1]); print('${cfg:-eager}', d['value'], round(d['ms_per_step']*1e3,1), 'us/step', d['config']['impl'])" | tee -a $O/engine_paths.txt
+  python -c "import json; d=json.loads(open('$O/eng.json').read().splitlines()[-1]); print('${cfg:-eager}', d['value'], round(d['ms_per_step']*1e3,1), 'us/step', d['config']['impl'], d.get('engine_graph_replays'))" | tee -a $O/engine_paths.txt
 done
 done
 echo done
