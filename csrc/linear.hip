@@ -85,6 +85,7 @@ __global__ __launch_bounds__(256) void linear_bwd_kernel(const float* __restrict
 // LDS for the second layer.  Every output is the same fmaf chain in the same order as the per-layer
 // kernels above, so the chain is bitwise the per-layer path.
 constexpr int kChain2MaxHidden = 4096;  // M * H floats of the hidden activation / gradient in LDS
+constexpr int kChain2StageW2 = 4096;    // O * H floats of W2 staged in LDS by the forward
 
 // h = act1(x W1^T + b1) [M, H]; y = act2(h W2^T + b2) [M, O]
 __global__ __launch_bounds__(256) void linear2_fwd_kernel(const float* __restrict__ x, const float* __restrict__ W1,
@@ -93,6 +94,13 @@ __global__ __launch_bounds__(256) void linear2_fwd_kernel(const float* __restric
                                                            float* __restrict__ y, int M, int K, int H, int O,
                                                            int relu1, int relu2) {
   __shared__ float hs[kChain2MaxHidden];
+  __shared__ float w2s[kChain2StageW2];
+  // layer 2's few dot products each walk a whole W2 row in a dependent fma chain: read from global
+  // memory that chain waits on a batch of loads every few steps (~5 of the kernel's ~10 us in a
+  // graph-replayed step); staged into LDS by all 256 threads at once (same products, same order)
+  const bool stage = O * H <= kChain2StageW2;
+  if (stage)
+    for (int i = threadIdx.x; i < O * H; i += 256) w2s[i] = W2[i];
   for (int i = threadIdx.x; i < M * H; i += 256) {
     const int m = i / H, n = i % H;
     const float* xr = x + (long long)m * K;
@@ -108,9 +116,14 @@ __global__ __launch_bounds__(256) void linear2_fwd_kernel(const float* __restric
   for (int i = threadIdx.x; i < M * O; i += 256) {
     const int m = i / O, o = i % O;
     const float* hr = hs + m * H;
-    const float* wr = W2 + (long long)o * H;
     float acc = 0.f;
-    for (int k = 0; k < H; ++k) acc = fmaf(hr[k], wr[k], acc);
+    if (stage) {  // (separate loops: both operands as LDS reads, not flat loads)
+      const float* wr = w2s + o * H;
+      for (int k = 0; k < H; ++k) acc = fmaf(hr[k], wr[k], acc);
+    } else {
+      const float* wr = W2 + (long long)o * H;
+      for (int k = 0; k < H; ++k) acc = fmaf(hr[k], wr[k], acc);
+    }
     float v = acc + (b2 ? b2[o] : 0.f);
     if (relu2) v = fmaxf(v, 0.f);
     y[i] = v;

@@ -130,28 +130,45 @@ class GraphedStep:
         self.graphs: Dict[tuple, tuple] = {}  # shape key -> (graph, static inputs, static loss)
         self.seen: Dict[tuple, int] = {}
         self.seeds: Dict[tuple, torch.Tensor] = {}
+        self.all_stored: Dict[tuple, bool] = {}  # signature -> its eager step stored every gradient
+        from ..ops.loss import _FusedBCEWithLogits, unit_seed
+        self._bce_node = _FusedBCEWithLogits._backward_cls
+        self._unit = unit_seed(engine.device)  # (made here, outside any capture)
         self.replays = 0
         self.eager_steps = 0
         self.failed = ""
         engine.reducer.arm(False)  # the hooks stay silent: the step issues its own collectives
 
     # ------------------------------------------------------------------ the step body
-    def _body(self, *args) -> torch.Tensor:
+    def _body(self, *args, key=None, capturing: bool = False) -> torch.Tensor:
         e = self.e
         e.store.rebind_grads()  # .grad views into the flat bucket (host-side binding, no kernel)
-        e.store.grad_buf.zero_()
+        # The bucket is zeroed so the backward may STORE each gradient's first write.  When the
+        # eager runs of this signature saw every gradient view stored by the injected kernels, the
+        # captured step leaves the zero fill out (one graph node: ~3 us of a ~33 us step): the
+        # stores overwrite whatever the bucket holds, and nothing else writes it (the padding
+        # between views stays zero from the first fill).
+        if not (capturing and self.all_stored.get(key)):
+            e.store.grad_buf.zero_()
         loss = self.loss_fn(*args)
         from ..ops.linear import engine_backward
-        with engine_backward(grads_zero=True):  # zeroed just above
+        with engine_backward(grads_zero=True) as stored:  # zeroed just above
             loss.float().backward(self._seed(loss))
+        if not capturing:
+            self.all_stored[key] = all((v.data_ptr(), v.numel()) in stored for v in e.store.grad_views)
         optimizer_tail(e, self.rccl, self.step_dev)
         return loss.detach()
 
     def _seed(self, loss: torch.Tensor) -> Optional[torch.Tensor]:
-        """A persistent tensor for the backward seed.  Made only outside capture (a tensor from the
-        graph's private pool must not outlive its graph); a capture that finds none lets autograd
-        fill its own.  It is re-filled with 1 before every use (one fill node in the captured step):
-        the loss comes from user code, and a custom Function may edit its grad_output in place."""
+        """The backward seed.  The framework's fused BCE (ops/loss.py) only reads its incoming
+        gradient and recognises the persistent unit seed: its backward then launches nothing (no
+        fill, no multiply node).  Any other loss gets a persistent tensor made only outside capture
+        (a tensor from the graph's private pool must not outlive its graph; a capture that finds
+        none lets autograd fill its own), re-filled with 1 before every use (one fill node in the
+        captured step): a custom Function may edit its grad_output in place."""
+        if (loss.grad_fn is not None and type(loss.grad_fn) is self._bce_node and loss.dim() == 0
+                and loss.dtype == torch.float32 and not loss.retains_grad):
+            return self._unit
         key = (tuple(loss.shape), loss.device)
         seed = self.seeds.get(key)
         if seed is None and not torch.cuda.is_current_stream_capturing():
@@ -169,7 +186,7 @@ class GraphedStep:
             n = self.seen.get(key, 0)
             if n < self.warmup or len(self.graphs) >= self.max_graphs:
                 self.seen[key] = n + 1
-                loss = self._body(*args)
+                loss = self._body(*args, key=key)
                 self.eager_steps += 1
                 e._finish_graph_step()
                 return loss
@@ -199,7 +216,7 @@ class GraphedStep:
         # capture records the launches without running them: the step counter advance is replayed,
         # not double-counted
         with torch.cuda.graph(graph, pool=self.pool):
-            static_loss = self._body(*static_in)
+            static_loss = self._body(*static_in, key=key, capturing=True)
         entry = (graph, static_in, static_loss)
         self.graphs[key] = entry
         return entry

@@ -922,3 +922,23 @@ def test_graph_module_bound_graph_guards_double_forward_and_off_switch():
             e.step()
             assert not b.pending and b.held is None
         e.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("extra", [{}, {"zero_optimization": {"stage": 1}}, {"gradient_clipping": 0.5}])
+def test_hip_graph_step_with_fused_bce_drops_seed_and_zero_fill(extra):
+    """Whole-step HIP graph with the framework's fused BCE: the backward seed is the persistent unit
+    (the BCE backward launches nothing) and, since the injected kernels store every gradient view,
+    the captured step has no zero fill of the bucket.  Same trajectory as the eager engine; the
+    short batch signature as well."""
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    batches = _batches(10, 41) + _batches(1, 42, bs=8) + _batches(10, 43) + _batches(3, 44, bs=8)
+    cfg = {"train_batch_size": 32, **extra}
+    e1, l1, p1 = _run_engine(dict(cfg), batches, crit=BCEWithLogitsLoss())
+    e2, l2, p2 = _run_engine(dict(cfg, amd={"hip_graph": True}), batches, graph=True, crit=BCEWithLogitsLoss())
+    assert e2.graphed.replays >= 15 and not e2.graphed.failed, e2.graphed.failed
+    assert e2.graphed.all_stored and all(e2.graphed.all_stored.values()), e2.graphed.all_stored
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
+    e1.close()
+    e2.close()
