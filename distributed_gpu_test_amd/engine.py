@@ -419,13 +419,14 @@ class Engine:
             return None
         if self._tail_step_dev is None:
             self._tail_step_dev = torch.zeros((), dtype=torch.int64, device=self.device)
+            self._tail_ticket = torch.zeros((), dtype=torch.int32, device=self.device)  # (Adam advances the step)
             if comm.collectives_on(self.world_size):
                 from .parallel.rccl import RcclComm
                 self._tail_rccl = RcclComm(self.device)
         lr = self.optimizer.param_groups[0]["lr"]
 
         def tail():
-            optimizer_tail(self, self._tail_rccl, self._tail_step_dev)
+            optimizer_tail(self, self._tail_rccl, self._tail_step_dev, self._tail_ticket)
             self.store.grad_buf.zero_()  # consumed: the next step's backward starts from zero
         tail.lr = lr
         return tail

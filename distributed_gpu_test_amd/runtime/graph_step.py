@@ -94,18 +94,20 @@ def allgather_params(e, rccl) -> None:
         off += n
 
 
-def optimizer_tail(e, rccl, step_dev: torch.Tensor) -> None:
+def optimizer_tail(e, rccl, step_dev: torch.Tensor, step_ticket: Optional[torch.Tensor] = None) -> None:
     """Everything after the gradients are in the flat bucket, capturable: gradient collective ->
-    clip coefficient -> device step counter + 1 -> fused flat Adam -> [ZeRO-1] parameter all-gather.
-    The lr and Adam constants are baked into the captured launch."""
+    clip coefficient -> fused flat Adam (which advances the device step counter itself when given
+    ``step_ticket``, else one increment launch first) -> [ZeRO-1] parameter all-gather.  The lr and
+    Adam constants are baked into the captured launch; ``step_dev`` counts the updates done."""
     grads = reduce_grads(e, rccl)
     scale = 1.0 / e.world_size
     coef = clip_coef(e, rccl, grads, scale)
     g = e.optimizer.param_groups[0]
-    step_dev.add_(1)
+    if step_ticket is None:
+        step_dev.add_(1)
     adam_flat_(e.master, grads, e.exp_avg, e.exp_avg_sq, 1, g["lr"], g["betas"][0], g["betas"][1], g["eps"],
                g["weight_decay"], g["adamw"], grad_scale=scale, grad_scale_dev=coef, param_lp=e.param_lp,
-               step_dev=step_dev)
+               step_dev=step_dev, step_ticket=step_ticket)
     if e.stage >= 1:
         allgather_params(e, rccl)
 
@@ -126,6 +128,7 @@ class GraphedStep:
         # the Adam step counter the captured launch reads (the step number of THIS update, 1-based)
         self.step_dev = torch.full((), engine.global_steps - engine.skipped_steps, dtype=torch.int64,
                                    device=engine.device)
+        self.step_ticket = torch.zeros((), dtype=torch.int32, device=engine.device)  # (Adam advances step_dev)
         self.pool = torch.cuda.graph_pool_handle()
         self.graphs: Dict[tuple, tuple] = {}  # shape key -> (graph, static inputs, static loss)
         self.seen: Dict[tuple, int] = {}
@@ -136,6 +139,7 @@ class GraphedStep:
         self._unit = unit_seed(engine.device)  # (made here, outside any capture)
         self.replays = 0
         self.eager_steps = 0
+        self._last = None  # (shape, dtype, entry, bound replay) of the last replayed one-tensor signature
         self.failed = ""
         engine.reducer.arm(False)  # the hooks stay silent: the step issues its own collectives
 
@@ -156,7 +160,7 @@ class GraphedStep:
             loss.float().backward(self._seed(loss))
         if not capturing:
             self.all_stored[key] = all((v.data_ptr(), v.numel()) in stored for v in e.store.grad_views)
-        optimizer_tail(e, self.rccl, self.step_dev)
+        optimizer_tail(e, self.rccl, self.step_dev, self.step_ticket)
         return loss.detach()
 
     def _seed(self, loss: torch.Tensor) -> Optional[torch.Tensor]:
@@ -180,6 +184,16 @@ class GraphedStep:
     # ------------------------------------------------------------------ public
     def __call__(self, *args) -> torch.Tensor:
         e = self.e
+        last = self._last  # the common case: one tensor argument of last step's signature
+        if last is not None and len(args) == 1 and torch.is_tensor(args[0]):
+            a = args[0]
+            if a.shape == last[0] and a.dtype == last[1]:
+                graph, static_in, static_loss = last[2]
+                static_in[0].copy_(a, non_blocking=True)
+                last[3]()
+                self.replays += 1
+                e._finish_graph_step()
+                return static_loss
         key = tuple((tuple(a.shape), a.dtype) if torch.is_tensor(a) else ("py", a) for a in args)
         entry = self.graphs.get(key)
         if entry is None:
@@ -205,6 +219,8 @@ class GraphedStep:
             if torch.is_tensor(dst):
                 dst.copy_(src, non_blocking=True)
         graph.replay()
+        if len(args) == 1 and torch.is_tensor(args[0]):
+            self._last = (args[0].shape, args[0].dtype, entry, torch._C._CUDAGraph.replay.__get__(graph))
         self.replays += 1
         e._finish_graph_step()
         return static_loss
@@ -222,6 +238,7 @@ class GraphedStep:
         return entry
 
     def close(self) -> None:
+        self._last = None
         self.graphs.clear()
         if self.rccl is not None:
             self.rccl.close()

@@ -350,6 +350,7 @@ class TinyMLPTrainer:
             from ..parallel.rccl import RcclComm
             self.rccl = RcclComm(self.device)
         self.step_dev = torch.zeros((), dtype=torch.int64, device=self.device)
+        self.step_ticket = torch.zeros((), dtype=torch.int32, device=self.device)  # Adam advances step_dev
         self._gsteps = self.steps_per_epoch()
         self._gplan = torch.full((self._gsteps, self.B), -1, dtype=torch.int32, device=self.device)
         self._gcounts = torch.ones(self._gsteps, dtype=torch.int32, device=self.device)
@@ -359,9 +360,9 @@ class TinyMLPTrainer:
         ops.tiny_mlp_grad(self.x, self.y, plan, counts, s, self.params, self.grad, self.loss_acc, self.F, self.H)
         if self.rccl is not None:
             self.rccl.all_reduce(self.grad)
-        ops.step_increment(self.step_dev)
         adam_flat_(self.params, self.grad, self.exp_avg, self.exp_avg_sq, 1, self.lr, self.betas[0], self.betas[1],
-                   self.eps, self.weight_decay, self.adamw, grad_scale=1.0 / self.world_size, step_dev=self.step_dev)
+                   self.eps, self.weight_decay, self.adamw, grad_scale=1.0 / self.world_size, step_dev=self.step_dev,
+                   step_ticket=self.step_ticket)
 
     def _capture(self) -> None:
         # warm the kernels once outside capture, then restore the state they touched

@@ -4,7 +4,7 @@ set -o pipefail
 O=${OUT:-gpurun_out/r5t}
 mkdir -p $O
 export TMPDIR=/tmp
-timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_engine.py > $O/pytest_engine.log 2>&1 || { tail -40 $O/pytest_engine.log; exit 1; }
+timeout -k 10 600 python -u -m pytest -x -q --timeout 200 --timeout-method thread tests/test_gpu_engine.py tests/test_gpu_tiny_mlp.py > $O/pytest_engine.log 2>&1 || { tail -40 $O/pytest_engine.log; exit 1; }
 tail -1 $O/pytest_engine.log
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/gm -o run -- python3 scripts/engine_host_profile.py --steps 600 --config configs/ds_graph_module.json --no-cprofile > $O/gm.log 2>&1 || { tail -20 $O/gm.log; exit 1; }
 timeout -k 10 200 rocprofv3 --kernel-trace --output-format csv -d $O/whole -o run -- python3 scripts/engine_host_profile.py --steps 600 --config configs/ds_graph_fused.json --no-cprofile > $O/whole.log 2>&1 || { tail -20 $O/whole.log; exit 1; }
