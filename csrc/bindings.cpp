@@ -601,7 +601,8 @@ dgt::AdamFlatArgs adam_args(const at::Tensor& master, const std::optional<at::Te
                             const at::Tensor& grad, const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq,
                             double lr, double beta1, double beta2, double eps, double weight_decay, bool adamw,
                             int64_t step, double grad_scale, const std::optional<at::Tensor>& grad_scale_dev,
-                            const std::optional<at::Tensor>& step_dev) {
+                            const std::optional<at::Tensor>& step_dev,
+                            const std::optional<at::Tensor>& step_ticket = std::nullopt) {
   check_gpu(master, "master", at::kFloat);
   check_gpu(exp_avg, "exp_avg", at::kFloat);
   check_gpu(exp_avg_sq, "exp_avg_sq", at::kFloat);
@@ -617,7 +618,7 @@ dgt::AdamFlatArgs adam_args(const at::Tensor& master, const std::optional<at::Te
   TORCH_CHECK(grad.numel() == n && exp_avg.numel() == n && exp_avg_sq.numel() == n, "dgt: flat size mismatch");
   const bool dev_step = step_dev.has_value() && step_dev->defined();
   TORCH_CHECK(dev_step || step >= 1, "dgt: adam step must be >= 1");
-  dgt::AdamFlatArgs a;
+  dgt::AdamFlatArgs a{};
   a.master = master.data_ptr<float>();
   a.param_lp = nullptr;
   a.lp_dtype = dgt::kF32;
@@ -648,9 +649,15 @@ dgt::AdamFlatArgs adam_args(const at::Tensor& master, const std::optional<at::Te
   a.lr_d = lr;
   a.beta1_d = beta1;
   a.beta2_d = beta2;
+  a.step_ticket = nullptr;
   if (dev_step) {
     check_gpu(*step_dev, "step_dev", at::kLong);
-    a.step_dev = reinterpret_cast<const long long*>(step_dev->data_ptr<int64_t>());
+    a.step_dev = reinterpret_cast<long long*>(step_dev->data_ptr<int64_t>());
+  }
+  if (step_ticket.has_value() && step_ticket->defined()) {
+    TORCH_CHECK(dev_step, "dgt: adam_flat step_ticket needs step_dev");
+    check_gpu(*step_ticket, "step_ticket", at::kInt);
+    a.step_ticket = reinterpret_cast<unsigned*>(step_ticket->data_ptr<int32_t>());
   }
   return a;
 }
@@ -658,9 +665,10 @@ dgt::AdamFlatArgs adam_args(const at::Tensor& master, const std::optional<at::Te
 void adam_flat(const at::Tensor& master, const std::optional<at::Tensor>& param_lp, const at::Tensor& grad,
                const at::Tensor& exp_avg, const at::Tensor& exp_avg_sq, double lr, double beta1, double beta2,
                double eps, double weight_decay, bool adamw, int64_t step, double grad_scale,
-               const std::optional<at::Tensor>& grad_scale_dev, const std::optional<at::Tensor>& step_dev) {
+               const std::optional<at::Tensor>& grad_scale_dev, const std::optional<at::Tensor>& step_dev,
+               const std::optional<at::Tensor>& step_ticket) {
   const dgt::AdamFlatArgs a = adam_args(master, param_lp, grad, exp_avg, exp_avg_sq, lr, beta1, beta2, eps,
-                                        weight_decay, adamw, step, grad_scale, grad_scale_dev, step_dev);
+                                        weight_decay, adamw, step, grad_scale, grad_scale_dev, step_dev, step_ticket);
   c10::DeviceGuard guard(master.device());
   DGT_CHECK_HIP(dgt::adam_flat(a, stream_of(master)));
 }
@@ -1163,7 +1171,7 @@ TORCH_LIBRARY(dgt, m) {
   m.def(
       "adam_flat(Tensor(a!) master, Tensor(b!)? param_lp, Tensor grad, Tensor(c!) exp_avg, Tensor(d!) exp_avg_sq, "
       "float lr, float beta1, float beta2, float eps, float weight_decay, bool adamw, int step, float grad_scale, "
-      "Tensor? grad_scale_dev, Tensor? step_dev=None) -> ()",
+      "Tensor? grad_scale_dev, Tensor(e!)? step_dev=None, Tensor(f!)? step_ticket=None) -> ()",
       &adam_flat);
   m.def("step_increment(Tensor(a!) counter) -> ()", &step_increment);
   m.def("bce_logits(Tensor z, Tensor y, Tensor(a!) loss, Tensor(b!) dz, Tensor(c!)? dz_lp=None, Tensor(d!)? sum_into=None) -> ()", &bce_logits);

@@ -76,7 +76,11 @@ struct AdamFlatArgs {
   const float* grad_scale_dev;  // optional extra device-side multiplier (clip coefficient)
   // optional device-resident step counter (graph replay): when set, the kernel forms the bias
   // corrections from *step_dev (the 1-based step of THIS update) instead of the host scalars
-  const long long* step_dev;
+  long long* step_dev;
+  // with step_dev: advance the counter in this launch -- this update is step *step_dev + 1, and the
+  // last block to finish stores it back (a zeroed ticket it counts on and resets): a graph-replayed
+  // step needs no separate increment node
+  unsigned* step_ticket;
   double lr_d, beta1_d, beta2_d;
 };
 
