@@ -103,6 +103,8 @@ def parse_args(argv=None):
     ap.add_argument("--no-secondary", action="store_true",
                     help="skip the post-headline bf16 MLP / fp32 engine MLP blocks")
     # (200 timed steps: 0.06 s of the fp32 block, 0.14 s of the bf16 one -- past the first-steps ramp)
+    ap.add_argument("--force-secondary", action="store_true",
+                    help="run the secondary blocks also when ranks share a card (a rehearsal of the N > 1 blocks)")
     ap.add_argument("--secondary-steps", type=int, default=200)
     ap.add_argument("--secondary-warmup", type=int, default=20)
     ap.add_argument("--secondary-budget-s", type=float, default=90.0,
@@ -563,7 +565,7 @@ def main(argv=None):
     # (the driver runs the default: the fused headline; other --impl / --model runs skip the blocks)
     # (ranks sharing a card -- a rehearsal on gloo -- would time host-staged collectives: skipped)
     if (not hung and not args.no_secondary and args.model == "simple" and args.impl == "fused" and device.type == "cuda"
-            and n_devices == world):
+            and (n_devices == world or args.force_secondary)):
         for key, desc, make in secondary_specs(args, device, world):
             t_block = time.perf_counter()
             res, err, h = run_bounded(functools.partial(run_secondary, key, desc, make, args, device, world),

@@ -430,3 +430,18 @@ def test_mlp_trainer_bucket_plan_cpu():
     big = MLPTrainer(model, batch_size=64, n_batches=1, device=torch.device("cpu"), bucket_mb=64)
     assert big.buckets == [(0, big.total_w)] and big.update_after == [0, 0, 0] and big.bucket_ready[0] == [0]
     assert n * L <= big.total_w
+
+
+def test_adam_flat_step_ticket_cpu_advances_counter():
+    """adam_flat_ on CPU with step_dev + step_ticket: the update is step_dev + 1 and step_dev advances,
+    as the HIP kernel does (tests/test_gpu_tiny_mlp.py)."""
+    import torch
+    from distributed_gpu_test_amd.ops import adam_flat_
+    p = torch.randn(8)
+    m, v = torch.zeros(8), torch.zeros(8)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    step_dev = torch.full((), 2, dtype=torch.int64)
+    gr = torch.randn(8)
+    adam_flat_(p, gr, m, v, 1, 1e-3, step_dev=step_dev, step_ticket=torch.zeros((), dtype=torch.int32))
+    adam_flat_(p2, gr, m2, v2, 3, 1e-3)
+    assert int(step_dev) == 3 and torch.equal(p, p2)

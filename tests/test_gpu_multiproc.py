@@ -289,3 +289,17 @@ def test_fused_exchange_every_shape(ws):
         # LL2 and ZeRO-1 move the same gradients: bit-identical parameters
         assert row["ll2_equal"] and row["zero1_equal"] and row["zero1_ll2_equal"], (shape, row)
     print(json.dumps(res))
+
+
+def test_bench_secondary_blocks_two_ranks_one_gpu():
+    """The N > 1 secondary blocks (bf16 MLP config #2, the fp32 engine MLP, ZeRO-1 config #5) run
+    their multi-rank code paths before the first 8-GPU run does: two ranks on the card (gloo,
+    --force-secondary, a few steps each); every block reports steps and no error."""
+    import json
+    r = run(2, "bench.py", "--gpus", "2", "--steps", "20", "--warmup", "5", "--no-sweep", "--force-secondary",
+            "--secondary-steps", "3", "--secondary-warmup", "1", timeout=600)
+    assert r.returncode == 0, r.stderr[-4000:]
+    out = json.loads([l for l in r.stdout.splitlines() if l.startswith("{")][-1])
+    for key in ("bf16_mlp", "fp32_engine_mlp", "bf16_mlp_zero1"):
+        assert key in out and out[key].get("error") is None, (key, out.get(key))
+        assert out[key]["steps"] == 3 and out[key]["iters_per_s"] > 0, out[key]

@@ -214,3 +214,23 @@ def test_in_kernel_bias_corrections_are_launch_split_invariant():
     # the loss log folds 4-step groups in fp32 (deferred ring, aligned to the launch start) into a
     # double: only the grouping depends on the split
     assert abs(outs[0][3] - outs[1][3]) <= 1e-6 * abs(outs[0][3])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1412, 1 << 20])
+def test_adam_flat_advances_device_step_itself(n):
+    """adam_flat_ with step_ticket: the launch uses step_dev + 1 and stores it back from its last
+    block (a graph-replayed step needs no increment node); bitwise the host-step update, over one
+    block and over 1,024 blocks; the ticket returns to zero after every launch."""
+    g = torch.Generator(device="cuda").manual_seed(n)
+    p = torch.randn(n, device="cuda", generator=g)
+    m, v = torch.zeros_like(p), torch.zeros_like(p)
+    p2, m2, v2 = p.clone(), m.clone(), v.clone()
+    step_dev = torch.full((), 4, dtype=torch.int64, device="cuda")
+    ticket = torch.zeros((), dtype=torch.int32, device="cuda")
+    for t in range(5, 9):
+        gr = torch.randn(n, device="cuda", generator=g)
+        adam_flat_(p, gr, m, v, 1, 1e-3, 0.9, 0.999, 1e-8, 0.0, False, step_dev=step_dev, step_ticket=ticket)
+        adam_flat_(p2, gr, m2, v2, t, 1e-3, 0.9, 0.999, 1e-8, 0.0, False)
+        assert int(step_dev) == t and int(ticket) == 0
+    assert torch.equal(p, p2) and torch.equal(m, m2) and torch.equal(v, v2)
