@@ -445,3 +445,54 @@ def test_adam_flat_step_ticket_cpu_advances_counter():
     adam_flat_(p, gr, m, v, 1, 1e-3, step_dev=step_dev, step_ticket=torch.zeros((), dtype=torch.int32))
     adam_flat_(p2, gr, m2, v2, 3, 1e-3)
     assert int(step_dev) == 3 and torch.equal(p, p2)
+
+
+def test_fast_apply_matches_function_apply_and_functorch():
+    """utils/fnapply.fast_apply: the C++ Function.apply entry gives the same outputs and gradients as
+    Function.apply, and under a functorch transform it defers to Function.apply."""
+    import torch
+    from distributed_gpu_test_amd.utils.fnapply import fast_apply
+
+    class Sq(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, k):
+            ctx.save_for_backward(x)
+            ctx.k = k
+            return x * x * k
+
+        @staticmethod
+        def backward(ctx, g):
+            (x,) = ctx.saved_tensors
+            return 2 * x * ctx.k * g, None
+
+        @staticmethod
+        def setup_context(ctx, inputs, output):  # makes the class functorch-capable
+            x, k = inputs
+            ctx.save_for_backward(x)
+            ctx.k = k
+
+    class Plain(torch.autograd.Function):
+        @staticmethod
+        def forward(ctx, x, k):
+            ctx.save_for_backward(x)
+            ctx.k = k
+            return x * x * k
+
+        @staticmethod
+        def backward(ctx, g):
+            (x,) = ctx.saved_tensors
+            return 2 * x * ctx.k * g, None
+
+    fast = fast_apply(Plain)
+    x1 = torch.randn(5, requires_grad=True)
+    x2 = x1.detach().clone().requires_grad_(True)
+    fast(x1, 3.0).sum().backward()
+    Plain.apply(x2, 3.0).sum().backward()
+    assert torch.equal(x1.grad, x2.grad)
+    # a class with setup_context keeps Function.apply (it binds default arguments)
+    assert fast_apply(Sq) == Sq.apply
+    # under a functorch transform the wrapper defers to Function.apply (which raises for a class
+    # without setup_context, exactly as calling Function.apply directly would)
+    import pytest
+    with pytest.raises(RuntimeError):
+        torch.func.grad(lambda t: fast(t, 3.0).sum())(torch.randn(5))
