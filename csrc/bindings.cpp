@@ -709,10 +709,10 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
              const std::optional<at::Tensor>& colsum) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || (variant != 2 && variant != 8),
               "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK(variant >= 0 && variant <= 9,
+  TORCH_CHECK(variant >= 0 && variant <= 8,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
               "fragment reads), 4 (128x128, 4 stages, 8 waves), 5 (software-pipelined reads), 6 / 7 (register "
-              "prefetch, 2 / 4 K-tiles), 8 (256x256 with cross-phase fragment prefetch) or 9 (256x256, 4 waves of 128x128); the round-2 "
+              "prefetch, 2 / 4 K-tiles) or 8 (256x256 with cross-phase fragment prefetch); the round-2 "
               "variants live in git history (commit c0371a5)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
@@ -782,8 +782,8 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
 void gemm_nt_adam(const at::Tensor& A, const at::Tensor& B, const at::Tensor& master, const at::Tensor& exp_avg,
                   const at::Tensor& exp_avg_sq, const at::Tensor& param_lp, int64_t step, double lr, double beta1,
                   double beta2, double eps, double weight_decay, bool adamw, double grad_scale, int64_t variant) {
-  TORCH_CHECK(((variant >= 0 && variant <= 5) || variant == 8 || variant == 9) && step >= 1,
-              "dgt: gemm_nt_adam needs variant 0 .. 5, 8 or 9 (runs as 8) and step >= 1");
+  TORCH_CHECK(((variant >= 0 && variant <= 5) || variant == 8) && step >= 1,
+              "dgt: gemm_nt_adam needs variant 0 .. 5 or 8 and step >= 1");
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(1), "dgt: gemm_nt_adam needs A[M,K], B[N,K]");
   const int64_t M = A.size(0), N = B.size(0), K = A.size(1);
   for (const at::Tensor* t : {&A, &B}) {

@@ -1213,217 +1213,6 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   }
 }
 
-
-// ---- 256x256 tile with 4 waves of 128x128 (variant 9).  The 8-wave kernel above gives each wave
-// 128x64: per 64-deep K-tile the CU reads 192 KiB of fragments from LDS for 512 MFMAs.  With 4 waves
-// of 128x128 it reads 128 KiB for the same 512 MFMAs (1.5x fewer fragment bytes per MFMA).  The
-// accumulators (256 fp32 per lane) then fill the AGPR file: the MFMAs are issued from inline asm
-// with "+a" accumulator operands, so the compiler keeps them in AGPRs for the whole loop (with the
-// builtin it rotated ~30 of them through VGPRs per iteration: round 4's 4-wave attempt,
-// profiles/r4_gemm256_4wave_ab.jsonl.txt).  BK = 32 K-tiles in a four-stage LDS ring (32 KiB per
-// stage, tile t + 3 staged while t is multiplied), one barrier per K-tile, and the next K-tile's
-// fragments read during this one's MFMAs (two fragment sets, 128 VGPRs).  Per accumulator the
-// MFMAs run in k order, 32 at a time: bit-identical to variants 2 / 8.
-namespace gw4 {
-constexpr int BM = 256, BN = 256, BK = 32, STAGES = 5;
-constexpr int UNIT = 128 * BK;    // elements per unit: A rows 0-127 / 128-255, B cols 0-127 / 128-255
-constexpr int STAGE = 4 * UNIT;   // elements per ring stage (32 KiB)
-
-// LDS row u (64 bytes = four 16-byte chunks) holds global chunk c at slot c ^ ((u >> 2) & 3): the 16
-// lanes of a ds_read_b128 group (16 consecutive rows, one chunk) hit 16 distinct 16-byte bank slots.
-DGT_DEVICE int swz(int u, int c) { return c ^ ((u >> 2) & 3); }
-
-// one unit's two 1-KiB LDS-DMAs of this wave (rows 32w .. 32w + 31): the unit's base in SGPRs (the
-// saddr form, as g256::stage), the lane's byte offset in a VGPR, M0 = the wave's LDS destination
-DGT_DEVICE void dma_unit(const u16* base, const int (&off)[2], unsigned la) {
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    unsigned saved;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "global_load_lds_dwordx4 %1, %2\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(saved)
-        : "v"(off[i]), "s"(base), "s"(la + (unsigned)(i * 1024))
-        : "memory");
-  }
-}
-
-// acc += a . b^T on a 16x16x32 bf16 MFMA with the accumulator pinned in AGPRs.  Back-to-back MFMAs
-// on one accumulator need no wait states (the accumulate chain); the reader after the loop is
-// fenced by acc_fence.
-DGT_DEVICE void mfma_a(f32x4& acc, const bf16x8& a, const bf16x8& b) {
-  asm volatile("v_mfma_f32_16x16x32_bf16 %0, %1, %2, %0" : "+a"(acc) : "v"(a), "v"(b));
-}
-// an MFMA's result read by any other instruction: 8-pass XDL -> 12 wait states (padded to 32);
-// taking the last-written accumulators as operands keeps the compiler's reads of them below it
-DGT_DEVICE void acc_fence(f32x4 (&acc)[8][8]) {
-  asm volatile("s_nop 15\n\ts_nop 15"
-               : "+a"(acc[7][0]), "+a"(acc[7][1]), "+a"(acc[7][2]), "+a"(acc[7][3]), "+a"(acc[7][4]),
-                 "+a"(acc[7][5]), "+a"(acc[7][6]), "+a"(acc[7][7]));
-}
-
-template <int N>
-DGT_DEVICE void wait_vm() {
-  __builtin_amdgcn_s_waitcnt((N & 15) | ((N >> 4) << 14) | (7 << 4) | (15 << 8));
-}
-}  // namespace gw4
-
-template <int EPI>
-__global__ __launch_bounds__(256, 1) void gemm_nt_w4_kernel(GemmArgs g) {
-  using namespace gw4;
-  __shared__ __attribute__((aligned(16))) u16 lds[STAGES * STAGE];
-  const int tid = threadIdx.x, l = tid & 63, lr = l & 15, lc = l >> 4;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6), wr = w >> 1, wc = w & 1;
-  int tm, tn;
-  tile_of_block(blockIdx.x, g.M / BM, g.N / BN, tm, tn);
-  const int m0 = tm * BM, n0 = tn * BN;
-  const u16* A = static_cast<const u16*>(g.A) + (long long)m0 * g.lda;
-  const u16* B = static_cast<const u16*>(g.B) + (long long)n0 * g.ldb;
-  int offa[2], offb[2];  // byte offsets of the lane's 16-byte piece in its two DMAs of a unit
-#pragma unroll
-  for (int i = 0; i < 2; ++i) {
-    const int u = (w * 2 + i) * 16 + (l >> 2);
-    offa[i] = (u * g.lda + swz(u, l & 3) * 8) * 2;
-    offb[i] = (u * g.ldb + swz(u, l & 3) * 8) * 2;
-  }
-  const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_byte_addr(lds));
-  const int nk = g.K / BK;
-  const long long a_hi = 128LL * g.lda, b_hi = 128LL * g.ldb;
-
-  auto stage_tile = [&](int kt) __attribute__((always_inline)) {
-    const unsigned la = lds0 + (unsigned)((kt % STAGES) * STAGE * 2 + w * 2 * 1024);
-    dma_unit(A + kt * BK, offa, la);
-    dma_unit(A + a_hi + kt * BK, offa, la + UNIT * 2);
-    dma_unit(B + kt * BK, offb, la + 2 * UNIT * 2);
-    dma_unit(B + b_hi + kt * BK, offb, la + 3 * UNIT * 2);
-  };
-  // one of a tile's 8 DMAs of this wave (unit p >> 1, half p & 1)
-  auto stage_piece = [&](int kt, int p) __attribute__((always_inline)) {
-    const int U = p >> 1, i = p & 1;
-    const unsigned la = lds0 + (unsigned)((kt % STAGES) * STAGE * 2 + U * UNIT * 2 + w * 2 * 1024 + i * 1024);
-    const u16* base = (U < 2 ? A + (U ? a_hi : 0) : B + (U == 3 ? b_hi : 0)) + kt * BK;
-    unsigned saved;
-    asm volatile(
-        "s_mov_b32 %0, m0\n\t"
-        "s_mov_b32 m0, %3\n\t"
-        "global_load_lds_dwordx4 %1, %2\n\t"
-        "s_mov_b32 m0, %0"
-        : "=&s"(saved)
-        : "v"(U < 2 ? offa[i] : offb[i]), "s"(base), "s"(la)
-        : "memory");
-  };
-  auto read_one = [&](int kt, int f, bf16x8& dst) __attribute__((always_inline)) {  // fragment f: A row tile f (< 8) or B col tile f - 8
-    const u16* st = lds + (kt % STAGES) * STAGE + (f < 8 ? wr : 2 + wc) * UNIT;
-    dst = *reinterpret_cast<const bf16x8*>(st + ((f & 7) * 16 + lr) * BK + swz(lr, lc) * 8);
-  };
-  auto read_frags = [&](int kt, bf16x8 (&a)[8], bf16x8 (&b)[8]) {
-    const u16* st = lds + (kt % STAGES) * STAGE;
-    const u16* ua = st + wr * UNIT;
-    const u16* ub = st + (2 + wc) * UNIT;
-    const int slot = swz(lr, lc) * 8;  // (i * 16 + lr) >> 2 & 3 == lr >> 2 & 3: the same for every i
-#pragma unroll
-    for (int i = 0; i < 8; ++i) a[i] = *reinterpret_cast<const bf16x8*>(ua + (i * 16 + lr) * BK + slot);
-#pragma unroll
-    for (int j = 0; j < 8; ++j) b[j] = *reinterpret_cast<const bf16x8*>(ub + (j * 16 + lr) * BK + slot);
-  };
-
-  f32x4 acc[8][8];
-#pragma unroll
-  for (int i = 0; i < 8; ++i)
-#pragma unroll
-    for (int j = 0; j < 8; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  bf16x8 fa0[8], fb0[8], fa1[8], fb1[8];
-
-  // prologue: tiles 0-3 in flight, tile 0 landed (tiles 1-3's 8 DMAs each may pend), its fragments
-  // read.  (nk is a multiple of 4, >= 4: the dispatcher's 256-grid rule has K % 128 == 0)
-  stage_tile(0);
-  stage_tile(1);
-  stage_tile(2);
-  stage_tile(3);
-  wait_vm<24>();
-  __builtin_amdgcn_sched_barrier(0);
-  __builtin_amdgcn_s_barrier();
-  __builtin_amdgcn_sched_barrier(0);
-  read_frags(0, fa0, fb0);
-
-  // the barrier, then the fragments read before it counted in (issued a whole K-tile ago; with the
-  // next tile's reads issued first, the compiler's own wait before an MFMA could not tell them apart)
-  auto sync = [&]() __attribute__((always_inline)) {
-    __builtin_amdgcn_sched_barrier(0);
-    __builtin_amdgcn_s_barrier();
-    __builtin_amdgcn_s_waitcnt(15 | (3 << 14) | (7 << 4));  // lgkmcnt(0)
-    __builtin_amdgcn_sched_barrier(0);
-  };
-  // Iteration t.  At its barrier tile t + 1 has landed from every wave (this wave's DMAs of tiles
-  // t + 2 and t + 3 may pend: 3 K-tiles of cover for every DMA) and every wave has read tile t - 1's
-  // fragments, so that stage ((t + 4) % 5) takes tile t + 4.  Then, interleaved in program order
-  // (the MFMAs are volatile asm, which the compiler keeps in order against memory operations), tile
-  // t's 64 MFMAs with tile t + 1's 16 fragment reads and tile t + 4's 8 DMAs: the matrix pipe
-  // restarts right after the barrier instead of behind the read and DMA issues.  Straight-line
-  // bodies (a steady pair and a peeled tail): a branch between MFMAs would make the accumulators
-  // phis, which the compiler then copies through VGPRs.
-  auto iter = [&](int t, const bf16x8 (&ca)[8], const bf16x8 (&cb)[8], bf16x8 (&na)[8], bf16x8 (&nb)[8],
-                  int pend, bool do_sync, bool do_read, bool do_stage) __attribute__((always_inline)) {
-    if (do_sync) {
-      if (pend == 16) wait_vm<16>();
-      else if (pend == 8) wait_vm<8>();
-      else wait_vm<0>();
-      sync();
-    }
-    __builtin_amdgcn_s_setprio(1);
-#pragma unroll
-    for (int q = 0; q < 16; ++q) {
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        // column-major over the 8 x 8 accumulators: the next tile's first MFMAs need all A
-        // fragments and B fragment 0, read first; B fragment j (read 9 + j-th) is due 8 j MFMAs in
-        const int idx = q * 4 + e, j = idx >> 3, i = idx & 7;
-        mfma_a(acc[i][j], ca[i], cb[j]);
-      }
-      if (do_read) {
-        if (q < 8) read_one(t + 1, q, na[q]);
-        else read_one(t + 1, q, nb[q - 8]);
-      }
-      if (do_stage && (q & 1) == 0) stage_piece(t + 4, q >> 1);
-    }
-    __builtin_amdgcn_s_setprio(0);
-  };
-  int t = 0;
-  for (; t + 5 < nk; t += 2) {
-    iter(t, fa0, fb0, fa1, fb1, 16, true, true, true);
-    iter(t + 1, fa1, fb1, fa0, fb0, 16, true, true, true);
-  }
-  iter(t, fa0, fb0, fa1, fb1, 16, true, true, false);  // nk - 4
-  iter(t + 1, fa1, fb1, fa0, fb0, 8, true, true, false);  // nk - 3
-  iter(t + 2, fa0, fb0, fa1, fb1, 0, true, true, false);  // nk - 2
-  iter(t + 3, fa1, fb1, fa0, fb0, 0, false, false, false);  // nk - 1
-  acc_fence(acc);
-
-  if constexpr ((EPI & kEpiOutF32) != 0) {
-#pragma unroll
-    for (int i = 0; i < 8; ++i)
-#pragma unroll
-      for (int j = 0; j < 8; ++j)
-        epi_store<EPI>(g, acc[i][j], m0 + wr * 128 + i * 16 + 4 * lc, n0 + wc * 128 + j * 16 + lr);
-  } else {
-    // the 256 x 256 bf16 tile (128 KiB) staged through the ring's LDS (the helper's first barrier
-    // has every wave past its last fragment read)
-    epilogue_staged<EPI, BM, BN, 128, 128, 256>(g, acc, lds, m0, n0, wr, wc, l, tid);
-  }
-}
-
-template <int E>
-bool launch_w4(int grid, const GemmArgs& g, hipStream_t stream) {
-  if constexpr ((E & kEpiAdam) != 0) {
-    return false;
-  } else {
-    hipLaunchKernelGGL((gemm_nt_w4_kernel<E>), dim3(grid), dim3(256), 0, stream, g);
-    return true;
-  }
-}
-
 // variant: 0 = pick by shape (256x256 for >= 200 tiles, else for one-wave grids the 128x128 variant
 // 5 for a [K, N] B operand with K % 128 == 0 and variant 3 otherwise, else variant 1), 1 = 128x128
 // 2-stage (4 waves, 2 blocks / CU), 2 = 256x256 8-phase (the bitwise oracle of 8), 3 = variant 4 with
@@ -1452,15 +1241,12 @@ bool launch_rp(int grid, const GemmArgs& g, hipStream_t stream, int depth) {
 
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 9) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 8) return hipErrorInvalidValue;
   // the 256x256 kernel runs the cross-phase fragment prefetch (g256::phase_x) unless variant 2 asks
   // for the 8-phase pipeline it is bitwise-checked against: 8192^3 1.51-1.52 vs 1.39-1.47 PF, the
   // MLP's wgrad 31.6-31.9 vs 33.0-33.7 us (profiles/r4_gemm256_xp.jsonl)
   const bool xp = variant != 2;
-  // variant 9: the 4-wave 256x256 kernel; products it does not take (the fused Adam epilogue,
-  // [K, N] operands, shapes off the 256 grid) run variant 8
-  const bool w4req = variant == 9;
-  if (variant == 8 || variant == 9) variant = 2;
+  if (variant == 8) variant = 2;
   // only the 128x128 kernels read a [K, N] B operand or form column sums
   const bool kn = (epi & (kEpiBKN | kEpiColSum)) != 0;
   if ((epi & kEpiColSum) && (!(epi & kEpiStoreT) || !g.colsum)) return hipErrorInvalidValue;
@@ -1479,13 +1265,9 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   bool big = fits256 && !kn && (g.M / 256) * (g.N / 256) >= 200;
   if (variant == 1 || variant >= 3) big = false;
   if (variant == 2) {
-    if (!fits256 || kn) {
-      if (w4req) return gemm_nt(g, epi, stream, 0);
-      return hipErrorInvalidValue;
-    }
+    if (!fits256 || kn) return hipErrorInvalidValue;
     big = true;
   }
-  const bool w4 = w4req && big && (g.K % 128) == 0 && !(epi & kEpiAdam);
   const int grid = big ? (g.M / 256) * (g.N / 256) : (g.M / GBM) * (g.N / GBN);
   // a grid that fits the chip at one block per CU gains nothing from 2 blocks / CU: spend the LDS on
   // a deep (4-stage) pipeline and 8 waves instead (measured: 8 waves beat 4 on one-wave grids)
@@ -1510,7 +1292,6 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   case E:                                                                                         \
     if (rp) {                                                                                     \
       if (!launch_rp<E>(grid, g, stream, rp_depth)) return hipErrorInvalidValue;                  \
-    } else if (w4 && launch_w4<E>(grid, g, stream)) {                                              \
     } else if (big && xp) hipLaunchKernelGGL((gemm_nt_256_kernel<E, true>), dim3(grid), dim3(512), 0, stream, g); \
     else if (big) hipLaunchKernelGGL((gemm_nt_256_kernel<E>), dim3(grid), dim3(512), 0, stream, g); \
     else if (sp) hipLaunchKernelGGL((gemm_nt_kernel<E, 5, 8, 3>), dim3(grid), dim3(512), 0, stream, g); \

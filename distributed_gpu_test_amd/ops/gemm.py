@@ -58,10 +58,7 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     forward-type products, bit-identical to 3; other products keep the shape rule),
     8 = the 256x256 kernel with cross-phase fragment prefetch (phase P's MFMAs overlap the LDS
     reads of phase P + 1; bit-identical to 2) -- the kernel the shape rule runs for >= 200 tiles of
-    256x256,
-    9 = the 256x256 tile with 4 waves of 128x128 (accumulators pinned in AGPRs by inline-asm MFMAs,
-    a four-stage BK = 32 ring; bit-identical to 2 / 8); products it does not take (the fused Adam,
-    [K, N] operands, shapes off the 256 grid) run as variant 8 / the shape rule.
+    256x256.
     ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
     the shape rule gives to the 128x128 kernels).
 

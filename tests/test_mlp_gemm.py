@@ -164,56 +164,6 @@ def test_gemm_256_cross_phase_prefetch_is_bitwise_variant2(K, epi):
 
 
 @gpu
-@pytest.mark.parametrize("K", [128, 256, 384, 1024])
-@pytest.mark.parametrize("epi", ["plain", "bias_relu_t", "f32_acc", "bf16_acc", "mask_t", "adam"])
-def test_gemm_256_four_wave_is_bitwise_variant8(K, epi):
-    """Variant 9 (256x256 tile, 4 waves of 128x128 with the accumulators pinned in AGPRs by
-    inline-asm MFMAs, four-stage BK = 32 ring) runs each accumulator's MFMAs in k order, 32 at a
-    time, as variant 8 does: every epilogue's output equals variant 8's bit for bit, from the
-    shortest loop (K = 128: only the peeled tail) up; the fused Adam (not taken) falls back to 8."""
-    from distributed_gpu_test_amd.ops.gemm import gemm_nt_adam_
-    g = torch.Generator().manual_seed(K + len(epi))
-    M, N = 512, 768
-    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
-    B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
-    bias = torch.randn(N, generator=g).cuda()
-    base = torch.randn(M, N, generator=g).cuda()
-    mask = torch.randn(M, N, generator=g).to(torch.bfloat16).cuda()
-    outs = []
-    for v in (8, 9):
-        if epi == "plain":
-            C = torch.empty(M, N, dtype=torch.bfloat16).cuda()
-            gemm_nt(A, B, C=C, variant=v)
-            outs.append([C])
-        elif epi == "bias_relu_t":
-            C = torch.empty(M, N, dtype=torch.bfloat16).cuda()
-            CT = torch.empty(N, M, dtype=torch.bfloat16).cuda()
-            gemm_nt(A, B, C=C, CT=CT, bias=bias, relu=True, variant=v)
-            outs.append([C, CT])
-        elif epi == "f32_acc":
-            C = base.clone()
-            gemm_nt(A, B, C=C, out_f32=True, accumulate=True, variant=v)
-            outs.append([C])
-        elif epi == "bf16_acc":
-            C = base.to(torch.bfloat16)
-            gemm_nt(A, B, C=C, accumulate=True, variant=v)
-            outs.append([C])
-        elif epi == "mask_t":
-            C = torch.empty(M, N, dtype=torch.bfloat16).cuda()
-            CT = torch.empty(N, M, dtype=torch.bfloat16).cuda()
-            gemm_nt(A, B, C=C, CT=CT, mask=mask, variant=v)
-            outs.append([C, CT])
-        else:
-            p, m, s = base.clone(), torch.zeros(M, N).cuda(), torch.zeros(M, N).cuda()
-            pb = torch.empty(M, N, dtype=torch.bfloat16).cuda()
-            gemm_nt_adam_(A, B, p, m, s, pb, 3, 1e-3, 0.9, 0.999, 1e-8, variant=v)
-            outs.append([p, m, s, pb])
-    assert all(torch.equal(x, y) for x, y in zip(*outs))
-    if epi == "plain":
-        torch.testing.assert_close(outs[1][0].float(), A.float() @ B.float().t(), rtol=2e-2, atol=5e-1)
-
-
-@gpu
 def test_gemm_256_asm_staging_high_address():
     """The 256x256 kernel's asm DMAs take their base from SGPRs as two 32-bit halves: operands whose
     address has bit 31 of the low word set (a sign-extension bug there faulted only on such
