@@ -496,3 +496,68 @@ def test_fast_apply_matches_function_apply_and_functorch():
     import pytest
     with pytest.raises(RuntimeError):
         torch.func.grad(lambda t: fast(t, 3.0).sum())(torch.randn(5))
+
+
+def test_bound_runner_policy_lru_budget_and_churn(monkeypatch):
+    """Engine._bound_runner (graph_module's in-place input graphs), the host policy alone (a stand-in
+    for GraphedModule, no GPU): an address is bound once seen twice in the last 8 calls; at most
+    MAX_BOUND_ADDRESSES pairs; a pair unused for 16 calls makes room for a new address; a churning
+    pattern stops binding after 16 evictions; the memory budget caps the pairs."""
+    import types
+    from distributed_gpu_test_amd import engine as eng_mod
+    from distributed_gpu_test_amd.runtime import graph_module as gm
+
+    made = []
+
+    class FakeRunner:
+        def __init__(self, module, params, args, warmup=2, tail=None, bind_inputs=False):
+            assert bind_inputs and warmup == 0
+            self.pending = False
+            made.append(args[0].data_ptr())
+
+    monkeypatch.setattr(gm, "GraphedModule", FakeRunner)
+
+    class FakeTensor:
+        def __init__(self, p):
+            self.p = p
+            self.requires_grad = False
+
+        def data_ptr(self):
+            return self.p
+
+        def is_contiguous(self):
+            return True
+
+    def fresh_fn(footprint=0):
+        return types.SimpleNamespace(bound={}, recent=(), bind_failed=None, calls=0, evictions=0,
+                                     footprint=footprint)
+
+    eng = types.SimpleNamespace(MAX_BOUND_ADDRESSES=eng_mod.Engine.MAX_BOUND_ADDRESSES,
+                                BIND_BUDGET_BYTES=eng_mod.Engine.BIND_BUDGET_BYTES, _runners=[],
+                                module=None, params=[], store=types.SimpleNamespace(rebind_grads=lambda: False),
+                                _tail_callable=lambda: None)
+    call = lambda fn, p: eng_mod.Engine._bound_runner(eng, fn, FakeTensor(p))  # noqa: E731
+
+    fn = fresh_fn()
+    # a period-3 address cycle: each address is bound on its third appearance, then reused
+    seq = [0, 512, 1024] * 6
+    got = [call(fn, p) is not None for p in seq]
+    assert made == [0, 512, 1024] and sum(got) == len(seq) - 6
+    # a new phase of addresses: the old pairs go stale (unused for > 16 calls) and make room
+    made.clear()
+    for p in [4096, 8192] * 12:
+        call(fn, p)
+    assert made == [4096, 8192] and len(fn.bound) <= eng.MAX_BOUND_ADDRESSES and fn.evictions >= 1
+    # churn: every address new twice in a row -> evictions run out, binding stops
+    fn2 = fresh_fn()
+    for k in range(40):
+        for _ in range(3):  # a new address, bound on its third call
+            call(fn2, (1 << 20) + k * 64)
+        for _ in range(17):  # ... then aged past the 16-call window by another (bound) address
+            call(fn2, 7)
+    assert fn2.bind_failed == "input addresses keep changing" and fn2.evictions == 16
+    # budget: a pair the size of the budget leaves no room for a second one
+    fn3 = fresh_fn(footprint=eng.BIND_BUDGET_BYTES)
+    for q in [1, 1, 1, 2, 2, 2]:
+        call(fn3, q)
+    assert list(fn3.bound) == [1]
