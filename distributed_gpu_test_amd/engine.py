@@ -219,6 +219,7 @@ class Engine:
         self.graph_module_reason = ""
         self._graphed_fwd: Dict[tuple, Any] = {}
         self._runners: List[Any] = []  # every GraphedModule: the copying ones above and their bound ones
+        self._view_keys: Optional[list] = None  # _grad_views()
         self._last_graphed = None  # (shape, dtype, requires_grad, GraphedModule) of the last hit
         # graphed tail (runtime/graph_module.py): backward + collective + Adam as one replay when
         # the loss is the framework's own; the step counter Adam reads lives on the device
@@ -290,7 +291,13 @@ class Engine:
                 self._hook_zeroed += 1
 
     def _grad_views(self):
-        return [(p, (p.grad.data_ptr(), p.grad.numel())) for p in self.params if p.grad is not None]
+        """(parameter, (data_ptr, numel) of its gradient view): backward rebinds every .grad to its
+        flat-bucket view (or an equivalent one) first, so the keys are the store's views' -- built
+        once, not per step (the eager step is host-bound)."""
+        keys = self._view_keys
+        if keys is None:
+            keys = self._view_keys = [(p, (v.data_ptr(), v.numel())) for p, v in zip(self.params, self.store.grad_views)]
+        return keys
 
     @property
     def linear_fallbacks(self) -> Dict[str, int]:
@@ -613,12 +620,15 @@ class Engine:
         torch.set_grad_enabled(False)  # grad mode off as under autograd (no create_graph)
         try:
             with direct_backward():
-                g = node.apply(seed)  # the unit seed: the saved d loss / d logits itself, no launch
+                # the Functions' own backward on their nodes (what BackwardCFunction.apply calls,
+                # without its per-call vjp / backward lookup): the unit seed -> the saved d loss /
+                # d logits itself, no launch
+                g = node._forward_cls.backward(node, seed)
                 g = g[0] if isinstance(g, tuple) else g
                 for v in views:  # reshapes / casts back to the chain's output
                     g = v(g)
                     g = g[0] if isinstance(g, tuple) else g
-                res = cur.apply(g)
+                res = cur._forward_cls.backward(cur, g)
             # what autograd does after a backward that does not retain the graph: the activations and
             # d loss / d logits are freed now (not when the caller drops ``loss``), and a second
             # backward through this graph raises instead of adding the gradients again
