@@ -26,6 +26,7 @@ from typing import Optional
 
 import torch
 import torch.nn.functional as F
+import torch.nn.modules.module as _mod
 
 from . import _ext
 from ..utils.fnapply import fast_apply
@@ -174,4 +175,13 @@ class BCEWithLogitsLoss(torch.nn.Module):
         self.sum_into = sum_into
 
     def forward(self, z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        return bce_with_logits(z, y, self.sum_into)
+
+    def __call__(self, z: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+        # straight to forward when no hook could see the call (nn.Module's dispatch is ~1.5 us of a
+        # host-bound engine step); with any module or global hook, nn.Module's own call path
+        if (self._forward_hooks or self._forward_pre_hooks or self._backward_hooks or self._backward_pre_hooks
+                or _mod._global_forward_hooks or _mod._global_forward_pre_hooks or _mod._global_backward_hooks
+                or _mod._global_backward_pre_hooks):
+            return super().__call__(z, y)
         return bce_with_logits(z, y, self.sum_into)

@@ -220,7 +220,8 @@ class _Replay(torch.autograd.Function):
             for dst, src in zip(runner.static_in, tensors[:len(runner.static_in)]):
                 if dst.data_ptr() != src.data_ptr():
                     dst.copy_(src)
-        elif any(p != t.data_ptr() for p, t in zip(runner.bound_ptrs, tensors)):
+        elif (runner.bound_ptrs[0] != tensors[0].data_ptr() if len(runner.bound_ptrs) == 1
+              else any(p != t.data_ptr() for p, t in zip(runner.bound_ptrs, tensors))):
             raise RuntimeError("graph_module: a bound graph replayed for inputs at other addresses")
         runner.fwd_replay()
         runner.replays += 1

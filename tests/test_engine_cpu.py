@@ -561,3 +561,20 @@ def test_bound_runner_policy_lru_budget_and_churn(monkeypatch):
     for q in [1, 1, 1, 2, 2, 2]:
         call(fn3, q)
     assert list(fn3.bound) == [1]
+
+
+def test_bce_module_call_keeps_hooks():
+    """ops.BCEWithLogitsLoss skips nn.Module's call path only when no hook could observe the call:
+    with a forward hook registered the hook fires, and the value is torch's either way."""
+    import torch
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    z, y = torch.randn(6, 1), (torch.rand(6, 1) > 0.5).float()
+    crit = BCEWithLogitsLoss()
+    want = torch.nn.functional.binary_cross_entropy_with_logits(z, y)
+    assert torch.allclose(crit(z, y), want)
+    seen = []
+    h = crit.register_forward_hook(lambda m, args, out: seen.append(float(out)))
+    assert torch.allclose(crit(z, y), want) and len(seen) == 1
+    h.remove()
+    crit(z, y)
+    assert len(seen) == 1
