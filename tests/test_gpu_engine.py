@@ -902,7 +902,7 @@ def test_graph_module_bound_graph_guards_double_forward_and_off_switch():
         e = dgt.initialize(model=m, config={"train_batch_size": 32,
                                             "amd": {"graph_module": True, "graph_bind_inputs": bind}})[0]
         crit = torch.nn.BCEWithLogitsLoss()
-        for _ in range(8):
+        for _ in range(16):  # (an address binds on its third visit; a few addresses may take turns)
             xb, yb = gather_batch(rows, X, Y)
             e.backward(crit(e(xb), yb))
             e.step()
