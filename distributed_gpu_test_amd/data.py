@@ -87,12 +87,20 @@ def gather_batch(rows: torch.Tensor, *tensors: torch.Tensor) -> Tuple[torch.Tens
     all of them (``csrc/data.hip``), fresh contiguous outputs, instead of one ``index_select`` per
     tensor -- the generic engine's step is host-bound and each launch is ~4-5 us of it.  Indices must
     lie in ``[0, rows)`` (an out-of-range index yields a zero row, as no check may sync the step)."""
-    if (rows.is_cuda and 0 < len(tensors) <= 4 and rows.dtype == torch.long and rows.dim() == 1
-            and all(t.is_cuda and t.dim() >= 1 and t.is_contiguous() and (t.stride(0) * t.element_size()) % 4 == 0
-                    for t in tensors)):
-        from .ops import _ext
-        return tuple(_ext.hot().gather_rows(rows.contiguous(), list(tensors)))  # (checks the devices)
+    if rows.is_cuda and 0 < len(tensors) <= 4 and rows.dtype == torch.long and rows.dim() == 1:
+        for t in tensors:  # (a plain loop: this runs every step of a host-bound loop)
+            if not (t.is_cuda and t.dim() >= 1 and t.is_contiguous() and (t.stride(0) * t.element_size()) % 4 == 0):
+                break
+        else:
+            global _HOT
+            if _HOT is None:
+                from .ops import _ext
+                _HOT = _ext.hot()
+            return tuple(_HOT.gather_rows(rows.contiguous(), list(tensors)))  # (checks the devices)
     return tuple(t.index_select(0, rows) for t in tensors)
+
+
+_HOT = None  # ops._ext.hot(), looked up on the first GPU gather
 
 
 @dataclass

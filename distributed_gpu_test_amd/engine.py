@@ -507,7 +507,7 @@ class Engine:
             with torch.no_grad():
                 runner.static_gout[0].view(-1).copy_(dz.view(-1))
         with tracing.range("dgt.graphed_tail"):
-            runner.bwd_tail.replay()
+            runner.tail_replay()
         runner.finish()
         self._tail_step_host = want + 1
         self._tail_done = True

@@ -173,6 +173,8 @@ class GraphedModule:
             del gs2
         self.single = torch.is_tensor(out) or len(out) == 1
         self.fwd_replay = torch._C._CUDAGraph.replay.__get__(self.fwd)  # (no Python wrapper frame per step)
+        self.tail_replay = (torch._C._CUDAGraph.replay.__get__(self.bwd_tail) if self.bwd_tail is not None
+                            else None)
         self.replays = 0
         self.pending = False  # a replayed forward whose backward has not run yet
         self.held = None  # bound inputs of the pending forward: alive (and unmoved) until its backward
