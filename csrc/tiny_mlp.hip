@@ -498,10 +498,40 @@ DGT_DEVICE void unpack_payload(const float (&sum)[TinyCfg<F, H>::NPAY], float in
 // and the per-pair uniform branches cost ~12 scalar branches per step).
 // One Adam step of the lane's register-resident parameters: two per packed-fp32 update (W2 and b2
 // form the last pair).
+#ifdef DGT_TINY_SCALAR_ADAM
+// A/B: the same update per element with single fp32 ops (the same operations in the same order,
+// so the same bits as the packed form)
+template <bool WD>
+DGT_DEVICE float adam_update_fast1(float p, float g, float& m, float& v, const AdamHyper& h, float step_size_neg,
+                                   float inv_bc2_sqrt) {
+  if (WD && h.weight_decay != 0.f) {
+    if (h.adamw) p = p * h.decay;
+    else g = fmaf(h.weight_decay, p, g);
+  }
+  m = fmaf(h.one_minus_beta1, g - m, m);
+  v = v * h.beta2;
+  v = fmaf(h.one_minus_beta2 * g, g, v);
+  const float r = __builtin_amdgcn_rcpf(fmaf(__builtin_amdgcn_sqrtf(v), inv_bc2_sqrt, h.eps));
+  return fmaf(step_size_neg, m * r, p);
+}
+#endif
+
 template <int F, int H, bool WD>
 DGT_DEVICE void adam_lane(LaneState<F, H>& st, const float (&gw1)[TinyCfg<F, H>::NSP], float gbw, float gb2,
                           const AdamHyper& hp, float step_size_neg, float inv_bc2_sqrt) {
   using C = TinyCfg<F, H>;
+#ifdef DGT_TINY_SCALAR_ADAM
+#pragma unroll
+  for (int i = 0; i < C::NSP; ++i)
+    st.w1[i] = adam_update_fast1<WD>(st.w1[i], gw1[i], st.m1[i], st.v1[i], hp, step_size_neg, inv_bc2_sqrt);
+  float m2x = st.m2.x, v2x = st.v2.x, m2y = st.m2.y, v2y = st.v2.y;
+  const float px = adam_update_fast1<WD>(st.p2.x, gbw, m2x, v2x, hp, step_size_neg, inv_bc2_sqrt);
+  const float py = adam_update_fast1<WD>(st.p2.y, gb2, m2y, v2y, hp, step_size_neg, inv_bc2_sqrt);
+  st.p2 = f32x2{px, py};
+  st.m2 = f32x2{m2x, m2y};
+  st.v2 = f32x2{v2x, v2y};
+  return;
+#endif
 #pragma unroll
   for (int i = 0; i < C::NSP; i += 2) {
     f32x2 m = {st.m1[i], st.m1[i + 1]}, v = {st.v1[i], st.v1[i + 1]};

@@ -65,9 +65,11 @@ PER_FILE_FLAGS = {"tiny_mlp.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form", "-mllvm",
                   **{f"gemm_f32_l{a}{b}.hip": _F32_GEMM for a in "01" for b in "01"}}
 
 
-def build(verbose: bool = False, force: bool = False, jobs: int = 8, variant: str = "", defines=()) -> str:
-    """``variant``: an A/B build of the whole extension with extra ``defines`` (-D) into
-    build/variants/<variant>/_C.so (load it with DGT_EXT_LIB=<path>); the default build is untouched."""
+def build(verbose: bool = False, force: bool = False, jobs: int = 8, variant: str = "", defines=(),
+          file_flags=()) -> str:
+    """``variant``: an A/B build of the whole extension with extra ``defines`` (-D) and per-source
+    ``file_flags`` ("tiny_mlp.hip=-fno-slp-vectorize") into build/variants/<variant>/_C.so (load it
+    with DGT_EXT_LIB=<path>); the default build is untouched."""
     global BUILD, OUT
     if variant:
         BUILD = os.path.join(ROOT, "build", "variants", variant, "obj")
@@ -77,6 +79,10 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 8, variant: st
     headers = glob.glob(os.path.join(CSRC, "*.h"))
     common = ["-O3", "-std=c++17", "-fPIC", f"-I{CSRC}", "-Wno-unused-result", *[f"-D{d}" for d in defines]]
     hip_srcs = sorted(glob.glob(os.path.join(CSRC, "*.hip")))
+    extra = {}
+    for ff in file_flags:
+        name, flag = ff.split("=", 1)
+        extra.setdefault(name, []).append(flag)
     inc, tlib, abi = _torch_paths()
     jobs_list = []
     objs = []
@@ -85,7 +91,7 @@ def build(verbose: bool = False, force: bool = False, jobs: int = 8, variant: st
         objs.append(obj)
         if force or _newer(obj, [src] + headers):
             jobs_list.append([HIPCC, f"--offload-arch={ARCH}", *common, *PER_FILE_FLAGS.get(os.path.basename(src), []),
-                              "-c", src, "-o", obj])
+                              *extra.get(os.path.basename(src), []), "-c", src, "-o", obj])
     # host translation units against the torch headers (op bindings, RCCL communicator)
     for bsrc in sorted(glob.glob(os.path.join(CSRC, "*.cpp"))):
         bobj = os.path.join(BUILD, os.path.basename(bsrc) + ".o")
@@ -140,8 +146,10 @@ def main(argv=None):
                     help="also build host-ASan/UBSan copies of the standalone tools (build/bin/*_asan)")
     ap.add_argument("--variant", default="", help="A/B build into build/variants/<name>/_C.so")
     ap.add_argument("-D", "--define", action="append", default=[], help="extra preprocessor define (variants)")
+    ap.add_argument("--file-flag", action="append", default=[], help="FILE=FLAG: extra flag for one source (variants)")
     a = ap.parse_args(argv)
-    out = build(verbose=a.verbose, force=a.force, jobs=a.jobs, variant=a.variant, defines=a.define)
+    out = build(verbose=a.verbose, force=a.force, jobs=a.jobs, variant=a.variant, defines=a.define,
+                file_flags=a.file_flag)
     print(f"built {out}")
     if a.sanitize:
         for exe in build_sanitized(verbose=a.verbose, force=a.force):
