@@ -26,6 +26,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=3000)
     ap.add_argument("--config", default="configs/ds_graph_module.json")
+    ap.add_argument("--side-stream", action="store_true", help="run the loop on a created stream")
     a = ap.parse_args()
     comm.init_distributed()
     dev = torch.device("cuda", 0)
@@ -48,6 +49,10 @@ def main():
         replay_t[1] += 1
 
     names = ("gather", "forward", "loss", "backward", "step")
+    if a.side_stream:
+        side = torch.cuda.Stream()
+        side.wait_stream(torch.cuda.current_stream())
+        torch.cuda.set_stream(side)
     for phase in ("warm", "timed"):
         acc = [0.0] * 5
         replay_t[0], replay_t[1] = 0.0, 0
@@ -80,7 +85,7 @@ def main():
     torch.cuda.CUDAGraph.replay = orig
     n = a.steps
     us = lambda v: f"{v / n * 1e6:.1f}"  # noqa: E731
-    print(f"[breakdown] impl={b.impl} total {us(t_end - t_start)} us/step, enqueue {us(t_enq - t_start)}; "
+    print(f"[breakdown] {'side stream ' if a.side_stream else ''}impl={b.impl} total {us(t_end - t_start)} us/step, enqueue {us(t_enq - t_start)}; "
           + ", ".join(f"{k} {us(v)}" for k, v in zip(names, acc))
           + f"; graph replays {replay_t[1] / n:.1f}/step {us(replay_t[0])} us/step", flush=True)
     base = min(ptrs)
