@@ -9,6 +9,7 @@
 #include <torch/library.h>
 
 #include <cstdlib>
+#include <memory>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -1234,6 +1235,68 @@ TORCH_LIBRARY(dgt, m) {
 // goes through the boxed dispatcher (an IValue stack per call) -- ~2-3 us of host time per call on
 // the MI355X box, paid several times per step by the host-bound engine paths (gather, Linear chain,
 // loss, Adam).  Only the hot eager-path ops; everything else stays on torch.ops.dgt.
+
+// ---------------------------------------------------------------- captured kernels, launched directly
+// A HIP graph replay costs ~10 us of device time on this stack whatever it holds, against ~4-5 us for
+// one kernel launched directly (profiles/r5_graph_launch_cost.txt).  A graph that captured only a
+// chain of kernels can therefore run cheaper as the same kernels re-launched with the captured
+// arguments, in capture order, on the current stream: the graph keeps owning the argument storage
+// (torch.cuda.CUDAGraph(keep_graph=True)), so the launches read exactly what a replay would.
+struct DirectNode {
+  const void* func;
+  dim3 grid, block;
+  unsigned shmem;
+  void** params;
+};
+
+struct DirectLaunch {
+  std::vector<DirectNode> nodes;
+  int device = 0;
+  void launch() const {
+    hipStream_t st = at::hip::getCurrentHIPStreamMasqueradingAsCUDA(device).stream();
+    for (const DirectNode& n : nodes) DGT_CHECK_HIP(hipLaunchKernel(n.func, n.grid, n.block, n.params, n.shmem, st));
+  }
+};
+
+// The kernels of ``graph`` in dependency order, or nullptr when the graph holds anything else (a copy,
+// memset, event or child-graph node, a fork or join, arguments passed through ``extra``, or a function
+// the runtime does not know as a launchable kernel).
+std::unique_ptr<DirectLaunch> direct_plan(uintptr_t graph_handle, int device) {
+  hipGraph_t g = reinterpret_cast<hipGraph_t>(graph_handle);
+  size_t n = 0;
+  if (hipGraphGetNodes(g, nullptr, &n) != hipSuccess || n == 0 || n > 64) return nullptr;
+  std::vector<hipGraphNode_t> all(n);
+  if (hipGraphGetNodes(g, all.data(), &n) != hipSuccess) return nullptr;
+  // a linear chain: one root, every node at most one dependency and one dependent
+  hipGraphNode_t cur = nullptr;
+  for (hipGraphNode_t node : all) {
+    size_t deps = 0;
+    if (hipGraphNodeGetDependencies(node, nullptr, &deps) != hipSuccess || deps > 1) return nullptr;
+    if (deps == 0) {
+      if (cur != nullptr) return nullptr;
+      cur = node;
+    }
+  }
+  auto plan = std::make_unique<DirectLaunch>();
+  plan->device = device;
+  while (cur != nullptr) {
+    hipGraphNodeType type;
+    if (hipGraphNodeGetType(cur, &type) != hipSuccess || type != hipGraphNodeTypeKernel) return nullptr;
+    hipKernelNodeParams kp{};
+    if (hipGraphKernelNodeGetParams(cur, &kp) != hipSuccess || kp.extra != nullptr || kp.func == nullptr) return nullptr;
+    hipFuncAttributes attr;
+    if (hipFuncGetAttributes(&attr, kp.func) != hipSuccess) return nullptr;
+    plan->nodes.push_back({kp.func, kp.gridDim, kp.blockDim, kp.sharedMemBytes, kp.kernelParams});
+    size_t outs = 0;
+    if (hipGraphNodeGetDependentNodes(cur, nullptr, &outs) != hipSuccess || outs > 1) return nullptr;
+    hipGraphNode_t next = nullptr;
+    if (outs == 1 && hipGraphNodeGetDependentNodes(cur, &next, &outs) != hipSuccess) return nullptr;
+    cur = outs == 1 ? next : nullptr;
+  }
+  if (plan->nodes.size() != n) return nullptr;
+  return plan;
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "dgt hot-path ops without the dispatcher (same C++ functions as torch.ops.dgt)";
   m.def("gather_rows", [](const at::Tensor& idx, const std::vector<at::Tensor>& srcs) { return gather_rows(idx, srcs); });
@@ -1243,4 +1306,12 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear2_fwd", &linear2_fwd);
   m.def("linear2_bwd", &linear2_bwd);
   m.def("adam_flat", &adam_flat);
+  pybind11::class_<DirectLaunch>(m, "DirectLaunch")
+      .def("__call__", &DirectLaunch::launch)
+      .def_property_readonly("kernels", [](const DirectLaunch& d) { return d.nodes.size(); });
+  m.def("graph_direct_plan", [](uintptr_t graph, int device) -> pybind11::object {
+    auto p = direct_plan(graph, device);
+    if (!p) return pybind11::none();
+    return pybind11::cast(std::move(p));
+  });
 }

@@ -42,6 +42,39 @@ def _as_tuple(out) -> Tuple[torch.Tensor, ...]:
 
 _CAPTURE_STREAMS: dict = {}
 
+# A graph replay costs ~10 us of device time on this stack whatever it holds, and in most processes
+# the host blocks on it; one kernel launched directly costs ~4-5 us (profiles/r5_graph_launch_cost.txt).
+# A graph that captured at most this many kernels (in a chain, nothing else: no copy, memset, event
+# or collective) is therefore run as those kernels re-launched with the captured arguments, in one
+# C++ call (``_C.DirectLaunch``): the forward, the graphed tail and the whole-step graph of a small
+# model (profiles/r5_graph_direct_ab.txt: graph_module 17-22k -> 26-30k iters/s, whole-step graph
+# 34-35k -> 38-46k on the reference model).  DGT_GRAPH_DIRECT=0 keeps every replay.
+DIRECT_MAX_KERNELS = 8
+
+
+def direct_launcher(graph: "torch.cuda.CUDAGraph"):
+    """``_C.DirectLaunch`` for a ``keep_graph=True`` graph of at most DIRECT_MAX_KERNELS chained
+    kernels (DGT_GRAPH_DIRECT_MAX overrides the limit), else None (then replay it).  The graph object
+    must outlive the launcher: it owns the captured kernel arguments."""
+    import os
+    if os.environ.get("DGT_GRAPH_DIRECT", "1") == "0":
+        return None
+    limit = int(os.environ.get("DGT_GRAPH_DIRECT_MAX", DIRECT_MAX_KERNELS))
+    if limit > 1 and torch.distributed.is_available() and torch.distributed.is_initialized() \
+            and torch.distributed.get_world_size() > 1:
+        limit = 1  # a captured collective's kernels are only ever replayed (its plan lives in RCCL)
+    from ..ops import _ext
+    try:
+        mod = _ext.fast()
+    except Exception:  # no extension: replay
+        return None
+    if not hasattr(mod, "graph_direct_plan"):
+        return None
+    plan = mod.graph_direct_plan(int(graph.raw_cuda_graph()), torch.cuda.current_device())
+    if plan is None or plan.kernels > limit:
+        return None
+    return plan
+
 
 class _capture:
     """``torch.cuda.graph`` without its ``gc.collect()`` + ``empty_cache()`` on entry: emptying the
@@ -126,7 +159,7 @@ class GraphedModule:
             torch.set_rng_state(cpu_rng)
             torch.cuda.set_rng_state(gpu_rng)
         self.pool = torch.cuda.graph_pool_handle()
-        self.fwd = torch.cuda.CUDAGraph()
+        self.fwd = torch.cuda.CUDAGraph(keep_graph=True)  # (kept: a direct launcher reads its kernel nodes)
         with _capture(self.fwd, self.pool):
             out = run()
             self.grad_out_idx = [i for i, o in enumerate(out) if o.requires_grad]
@@ -134,6 +167,8 @@ class GraphedModule:
             # allocator here would shift the addresses the caller's next batches land at
             self.static_gout = [torch.empty_like(out[i]) for i in self.grad_out_idx]
         self.static_out = out
+        self.fwd.instantiate()
+        self.fwd_direct = direct_launcher(self.fwd)
         self.bwd = torch.cuda.CUDAGraph()
         # The injected HIP Linear kernels (ops/linear.py, ops/mfma_linear.py) add dW / db straight into
         # their parameter's .grad inside an engine backward: with the aliases' .grad bound to the
@@ -161,7 +196,7 @@ class GraphedModule:
         self.bwd_tail = None
         self.tail_lr = getattr(tail, "lr", None)  # baked into the captured Adam launch
         if with_tail:
-            self.bwd_tail = torch.cuda.CUDAGraph()
+            self.bwd_tail = torch.cuda.CUDAGraph(keep_graph=True)
             with _capture(self.bwd_tail, self.pool), engine_backward(False):
                 gs2 = torch.autograd.grad([out[i] for i in self.grad_out_idx], targets[:len(self.params)],
                                           grad_outputs=self.static_gout, allow_unused=True)
@@ -172,9 +207,13 @@ class GraphedModule:
                     tail()
             del gs2
         self.single = torch.is_tensor(out) or len(out) == 1
-        self.fwd_replay = torch._C._CUDAGraph.replay.__get__(self.fwd)  # (no Python wrapper frame per step)
-        self.tail_replay = (torch._C._CUDAGraph.replay.__get__(self.bwd_tail) if self.bwd_tail is not None
-                            else None)
+        # (bound C methods: no Python wrapper frame per step)
+        self.fwd_replay = self.fwd_direct or torch._C._CUDAGraph.replay.__get__(self.fwd)
+        self.tail_replay = None
+        if self.bwd_tail is not None:
+            self.bwd_tail.instantiate()
+            self.tail_direct = direct_launcher(self.bwd_tail)
+            self.tail_replay = self.tail_direct or torch._C._CUDAGraph.replay.__get__(self.bwd_tail)
         self.replays = 0
         self.pending = False  # a replayed forward whose backward has not run yet
         self.held = None  # bound inputs of the pending forward: alive (and unmoved) until its backward

@@ -138,6 +138,7 @@ class GraphedStep:
         self._bce_node = _FusedBCEWithLogits._backward_cls
         self._unit = unit_seed(engine.device)  # (made here, outside any capture)
         self.replays = 0
+        self.launchers = {}  # key -> _C.DirectLaunch of that signature's graph (graph_module.direct_launcher)
         self.eager_steps = 0
         self._last = None  # (shape, dtype, entry, bound replay) of the last replayed one-tensor signature
         self.failed = ""
@@ -218,9 +219,10 @@ class GraphedStep:
         for dst, src in zip(static_in, args):
             if torch.is_tensor(dst):
                 dst.copy_(src, non_blocking=True)
-        graph.replay()
+        run = self.launchers.get(key) or torch._C._CUDAGraph.replay.__get__(graph)
+        run()
         if len(args) == 1 and torch.is_tensor(args[0]):
-            self._last = (args[0].shape, args[0].dtype, entry, torch._C._CUDAGraph.replay.__get__(graph))
+            self._last = (args[0].shape, args[0].dtype, entry, run)
         self.replays += 1
         e._finish_graph_step()
         return static_loss
@@ -228,17 +230,23 @@ class GraphedStep:
     def _capture(self, key, args):
         static_in = tuple(a.detach().clone() if torch.is_tensor(a) else a for a in args)
         torch.cuda.synchronize(self.e.device)
-        graph = torch.cuda.CUDAGraph()
+        graph = torch.cuda.CUDAGraph(keep_graph=True)
         # capture records the launches without running them: the step counter advance is replayed,
         # not double-counted
         with torch.cuda.graph(graph, pool=self.pool):
             static_loss = self._body(*static_in, key=key, capturing=True)
+        graph.instantiate()
+        from .graph_module import direct_launcher  # a short chain of kernels: launched, not replayed
+        launcher = direct_launcher(graph)
+        if launcher is not None:
+            self.launchers[key] = launcher
         entry = (graph, static_in, static_loss)
         self.graphs[key] = entry
         return entry
 
     def close(self) -> None:
         self._last = None
+        self.launchers.clear()
         self.graphs.clear()
         if self.rccl is not None:
             self.rccl.close()

@@ -1,5 +1,6 @@
 """The generic engine on the GPU (fused HIP Adam over flat buffers) vs plain PyTorch fp32."""
 import copy
+import json
 import os
 
 import pytest
@@ -943,3 +944,116 @@ def test_hip_graph_step_with_fused_bce_drops_seed_and_zero_fill(extra):
     torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
     e1.close()
     e2.close()
+
+
+@pytest.mark.gpu
+def test_graph_direct_launch_matches_replay():
+    """A graph that captured a short chain of kernels runs as those kernels re-launched directly
+    (runtime/graph_module.direct_launcher, csrc/bindings.cpp direct_plan): same outputs bit for bit
+    as replaying the graph, on the current stream, reading the captured addresses' current
+    contents; a graph holding a copy node gets no plan."""
+    from distributed_gpu_test_amd.runtime.graph_module import direct_launcher
+    from distributed_gpu_test_amd.ops import _ext
+    dev = torch.device("cuda", 0)
+    x = torch.randn(64, 32, device=dev)
+    w = torch.randn(16, 32, device=dev)
+    out = torch.empty(64, 16, device=dev)
+    g = torch.cuda.CUDAGraph(keep_graph=True)
+    s = torch.cuda.Stream()
+    s.wait_stream(torch.cuda.current_stream())
+    with torch.cuda.stream(s):
+        g.capture_begin()
+        out.copy_(torch.nn.functional.gelu(x @ w.t()))  # several kernels: no plan (over the limit)
+        g.capture_end()
+    torch.cuda.current_stream().wait_stream(s)
+    g.instantiate()
+    d = direct_launcher(g)
+    if d is not None:  # a chain of plain kernels: the launches reproduce the replay
+        out.zero_()
+        g.replay()
+        torch.cuda.synchronize()
+        ref = out.clone()
+        out.zero_()
+        d()
+        torch.cuda.synchronize()
+        assert torch.equal(out, ref)
+    # a graph holding a copy node gets no plan
+    dst, src0 = torch.empty(1 << 20, device=dev), torch.randn(1 << 20, device=dev)
+    gc_ = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.stream(s):
+        s.wait_stream(torch.cuda.current_stream())
+        gc_.capture_begin()
+        dst.copy_(src0)
+        gc_.capture_end()
+    torch.cuda.current_stream().wait_stream(s)
+    gc_.instantiate()
+    plan = _ext.fast().graph_direct_plan(int(gc_.raw_cuda_graph()), 0)
+    assert plan is None or plan.kernels == 1  # (a copy captured as a kernel is a kernel)
+    # one kernel: a plan, and its launches write exactly what the replays write
+    y = torch.zeros(1 << 16, device=dev)
+    src = torch.randn(1 << 16, device=dev)
+    g1 = torch.cuda.CUDAGraph(keep_graph=True)
+    with torch.cuda.stream(s):
+        s.wait_stream(torch.cuda.current_stream())
+        g1.capture_begin()
+        torch.add(src, 1.5, out=y)
+        g1.capture_end()
+    torch.cuda.current_stream().wait_stream(s)
+    g1.instantiate()
+    d = direct_launcher(g1)
+    assert d is not None and d.kernels == 1
+    y.zero_()
+    g1.replay()
+    torch.cuda.synchronize()
+    ref = y.clone()
+    y.zero_()
+    src.mul_(1.0)  # (same values)
+    d()
+    torch.cuda.synchronize()
+    assert torch.equal(y, ref) and torch.equal(ref, src + 1.5)
+    src.add_(1.0)  # the launcher reads the captured addresses' CURRENT contents, as a replay does
+    d()
+    torch.cuda.synchronize()
+    assert torch.equal(y, src + 1.5)
+
+
+@pytest.mark.gpu
+def test_graph_module_forward_uses_direct_launch():
+    """The reference model's graphed forward (one fused-chain kernel) and graphed tail (backward,
+    Adam, zero fill) are launched directly, and the trajectory is bit-identical to replaying every
+    graph (DGT_GRAPH_DIRECT=0)."""
+    import subprocess
+    import sys
+    code = r"""
+import json, torch
+import distributed_gpu_test_amd as dgt
+from distributed_gpu_test_amd.models import SimpleNet
+from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+from distributed_gpu_test_amd.data import gather_batch
+torch.manual_seed(0)
+m = SimpleNet(20, 64)
+cfg = {"train_batch_size": 4, "amd": {"graph_module": True}}
+e, _, _, _ = dgt.initialize(model=m, model_parameters=m.parameters(), config=cfg)
+X = torch.randn(256, 20, device="cuda"); Y = (torch.rand(256, 1, device="cuda") > 0.5).float()
+crit = BCEWithLogitsLoss()
+for s in range(40):
+    rows = torch.arange(4 * (s % 8), 4 * (s % 8) + 4, device="cuda")
+    xb, yb = gather_batch(rows, X, Y)
+    loss = crit(e(xb), yb); e.backward(loss); e.step()
+torch.cuda.synchronize()
+runners = list(e._runners)
+print(json.dumps({"direct": [r.fwd_direct is not None and getattr(r, "tail_direct", None) is not None
+                             for r in runners],
+                  "params": [p.detach().cpu().double().sum().item() for p in m.parameters()],
+                  "bits": [p.detach().cpu().view(torch.int32).sum().item() for p in m.parameters()]}))
+"""
+    outs = {}
+    for flag in ("1", "0"):
+        env = dict(os.environ, DGT_GRAPH_DIRECT=flag, DGT_QUIET="1")
+        r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True, timeout=240,
+                           cwd=os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+        assert r.returncode == 0, r.stderr[-3000:]
+        outs[flag] = json.loads(r.stdout.strip().splitlines()[-1])
+    assert outs["1"]["direct"] and all(outs["1"]["direct"])
+    assert not any(outs["0"]["direct"])
+    assert outs["1"]["bits"] == outs["0"]["bits"]
