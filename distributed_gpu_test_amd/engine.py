@@ -60,6 +60,17 @@ def _direct_node_classes():
     return _DIRECT_KINDS
 
 
+def _torch_mean_bce(node) -> bool:
+    """``node`` is torch's binary_cross_entropy_with_logits backward with reduction='mean' and no
+    weight / pos_weight: its gradient is the framework loss kernel's (sigmoid(z) - y) / n."""
+    if type(node).__name__ != "BinaryCrossEntropyWithLogitsBackward0":
+        return False
+    try:
+        return node._saved_reduction == 1 and node._saved_weight is None and node._saved_pos_weight is None
+    except (AttributeError, RuntimeError):  # (saved tensors already freed)
+        return False
+
+
 def _bce_node_class():
     return _direct_node_classes()[0]
 
@@ -224,6 +235,7 @@ class Engine:
         # graphed tail (runtime/graph_module.py): backward + collective + Adam as one replay when
         # the loss is the framework's own; the step counter Adam reads lives on the device
         self._tail_rccl = None
+        self._tail_scratch: Optional[torch.Tensor] = None  # the loss kernel's unused loss output (torch's BCE)
         self._tail_step_dev: Optional[torch.Tensor] = None
         self._tail_step_host = -1   # what _tail_step_dev holds (host mirror, no sync)
         self._tail_done = False     # backward ran the whole step: step() only does the bookkeeping
@@ -445,9 +457,14 @@ class Engine:
         """(GraphedModule, dL/dout) when ``loss`` is the framework's fused BCE (``ops/loss.py``) of a
         graphed forward's output, through reshapes / a dtype cast only -- a gradient the engine can
         form without autograd: the BCE kernel already wrote it (d loss / d logits), and with no loss
-        scaling and one micro-step the backward seed is 1.  Else None (the autograd path)."""
+        scaling and one micro-step the backward seed is 1.  (GraphedModule, (z, y)) for torch's own
+        mean BCEWithLogitsLoss of fp32 logits (the reference's criterion): the caller forms dL/dz
+        with the framework's loss kernel.  Else None (the autograd path)."""
         node = loss.grad_fn
-        if node is None or type(node) is not _bce_node_class():
+        if node is None:
+            return None
+        torch_bce = type(node) is not _bce_node_class()
+        if torch_bce and not _torch_mean_bce(node):
             return None
         nxt = node.next_functions  # (logits, targets[, sum_into])
         if len(nxt) < 2 or any(e[0] is not None for e in nxt[1:]):
@@ -463,10 +480,18 @@ class Engine:
             return None
         if len(runner.static_out) != 1 or runner.grad_out_idx != [0]:
             return None
+        gout = runner.static_gout[0]
+        if torch_bce:
+            # torch.nn.BCEWithLogitsLoss (the reference's criterion, train.py:96): its dL/dz is formed by
+            # the framework's loss kernel straight into the graph's input (see _try_graphed_tail)
+            z, y = node._saved_self, node._saved_target
+            if (z.dtype != torch.float32 or gout.dtype != torch.float32 or z.numel() != gout.numel()
+                    or y.numel() != z.numel() or z.device != gout.device):
+                return None
+            return runner, (z, y)
         if getattr(node, "freed", True):
             return None
         dz, lp = node.dz, node.lp
-        gout = runner.static_gout[0]
         if lp is not None and gout.dtype == lp.dtype:
             dz = lp  # the kernel's once-rounded bf16 copy: a plain copy into the graph's input
         if dz.numel() != gout.numel() or gout.device != dz.device:
@@ -503,7 +528,15 @@ class Engine:
         want = self.global_steps - self.skipped_steps  # the graph adds 1 before its Adam launch
         if self._tail_step_host != want:
             self._tail_step_dev.fill_(want)
-        if dz.data_ptr() != runner.static_gout[0].data_ptr():  # (else the loss kernel wrote it there)
+        if isinstance(dz, tuple):  # torch's BCE: dL/dz = (sigmoid(z) - y) / n from the fused loss kernel
+            z, y = dz
+            if self._tail_scratch is None:
+                self._tail_scratch = torch.empty((), dtype=torch.float32, device=self.device)
+            from .ops import _ext
+            _ext.hot().bce_logits(z if z.is_contiguous() else z.contiguous(),
+                                  y if (y.dtype == torch.float32 and y.is_contiguous()) else y.float().contiguous(),
+                                  self._tail_scratch, runner.static_gout[0], None, None)
+        elif dz.data_ptr() != runner.static_gout[0].data_ptr():  # (else the loss kernel wrote it there)
             with torch.no_grad():
                 runner.static_gout[0].view(-1).copy_(dz.view(-1))
         with tracing.range("dgt.graphed_tail"):

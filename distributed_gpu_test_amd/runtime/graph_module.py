@@ -52,17 +52,19 @@ _CAPTURE_STREAMS: dict = {}
 DIRECT_MAX_KERNELS = 8
 
 
-def direct_launcher(graph: "torch.cuda.CUDAGraph"):
+def direct_launcher(graph: "torch.cuda.CUDAGraph", may_hold_collective: bool = True):
     """``_C.DirectLaunch`` for a ``keep_graph=True`` graph of at most DIRECT_MAX_KERNELS chained
     kernels (DGT_GRAPH_DIRECT_MAX overrides the limit), else None (then replay it).  The graph object
-    must outlive the launcher: it owns the captured kernel arguments."""
+    must outlive the launcher: it owns the captured kernel arguments.  ``may_hold_collective``: the
+    graph was captured where a collective can run (the graphed tail, the whole-step graph); with
+    more than one rank such a graph is only replayed."""
     import os
     if os.environ.get("DGT_GRAPH_DIRECT", "1") == "0":
         return None
     limit = int(os.environ.get("DGT_GRAPH_DIRECT_MAX", DIRECT_MAX_KERNELS))
-    if limit > 1 and torch.distributed.is_available() and torch.distributed.is_initialized() \
+    if may_hold_collective and torch.distributed.is_available() and torch.distributed.is_initialized() \
             and torch.distributed.get_world_size() > 1:
-        limit = 1  # a captured collective's kernels are only ever replayed (its plan lives in RCCL)
+        return None  # a captured collective's kernels are only ever replayed (its plan lives in RCCL)
     from ..ops import _ext
     try:
         mod = _ext.fast()
@@ -168,8 +170,8 @@ class GraphedModule:
             self.static_gout = [torch.empty_like(out[i]) for i in self.grad_out_idx]
         self.static_out = out
         self.fwd.instantiate()
-        self.fwd_direct = direct_launcher(self.fwd)
-        self.bwd = torch.cuda.CUDAGraph()
+        self.fwd_direct = direct_launcher(self.fwd, may_hold_collective=False)
+        self.bwd = torch.cuda.CUDAGraph(keep_graph=True)
         # The injected HIP Linear kernels (ops/linear.py, ops/mfma_linear.py) add dW / db straight into
         # their parameter's .grad inside an engine backward: with the aliases' .grad bound to the
         # engine's gradient views, the captured backward needs no separate add per parameter (one
@@ -188,6 +190,9 @@ class GraphedModule:
                     if g is not None:
                         gv.add_(g)
         self.static_gin = gs[len(self.params):]
+        self.bwd.instantiate()
+        self.bwd_direct = direct_launcher(self.bwd, may_hold_collective=False)  # (the reducer runs outside)
+        self.bwd_replay = self.bwd_direct or torch._C._CUDAGraph.replay.__get__(self.bwd)
         # The graphed tail: the same backward followed by ``tail()`` (the engine's gradient
         # collective, clip coefficient, fused Adam, ZeRO-1 all-gather and the bucket's zero fill) in
         # ONE graph, replayed by Engine.backward when the loss is one it can differentiate itself
@@ -285,7 +290,7 @@ class _Replay(torch.autograd.Function):
                 dst.zero_()
             elif g.data_ptr() != dst.data_ptr():  # (the fused BCE may have written it in place)
                 dst.copy_(g)
-        r.bwd.replay()
+        r.bwd_replay()
         r.finish()
         grads_in: List = [None] * (len(r.bound_ptrs) if r.bound_ptrs is not None else len(r.static_in))
         for i, g in zip(r.in_rg, r.static_gin):

@@ -27,6 +27,8 @@ def main():
     ap.add_argument("--steps", type=int, default=3000)
     ap.add_argument("--config", default="configs/ds_graph_module.json")
     ap.add_argument("--side-stream", action="store_true", help="run the loop on a created stream")
+    ap.add_argument("--torch-loss", action="store_true",
+                    help="torch.nn.BCEWithLogitsLoss (the reference's criterion: autograd backward, no graphed tail)")
     a = ap.parse_args()
     comm.init_distributed()
     dev = torch.device("cuda", 0)
@@ -34,7 +36,7 @@ def main():
     x, y = make_synthetic_data(2000, 20, 42)
     b = bench.DgtEngineBench(SimpleNet(20, 64), x, y, 4, dev, a.config or None)
     eng = b.engine
-    crit = BCEWithLogitsLoss(sum_into=b.loss_acc)
+    crit = torch.nn.BCEWithLogitsLoss() if a.torch_loss else BCEWithLogitsLoss(sum_into=b.loss_acc)
     plan, counts = b.epoch_plan(0)
     reps = (a.steps + plan.shape[0] - 1) // plan.shape[0]
     plan = plan.repeat(reps, 1)[:a.steps].to(dev).long()
@@ -85,7 +87,7 @@ def main():
     torch.cuda.CUDAGraph.replay = orig
     n = a.steps
     us = lambda v: f"{v / n * 1e6:.1f}"  # noqa: E731
-    print(f"[breakdown] {'side stream ' if a.side_stream else ''}impl={b.impl} total {us(t_end - t_start)} us/step, enqueue {us(t_enq - t_start)}; "
+    print(f"[breakdown] {'side stream ' if a.side_stream else ''}{'torch loss ' if a.torch_loss else ''}impl={b.impl} total {us(t_end - t_start)} us/step, enqueue {us(t_enq - t_start)}; "
           + ", ".join(f"{k} {us(v)}" for k, v in zip(names, acc))
           + f"; graph replays {replay_t[1] / n:.1f}/step {us(replay_t[0])} us/step", flush=True)
     base = min(ptrs)

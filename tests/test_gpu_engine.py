@@ -144,13 +144,13 @@ def test_engine_graph_tail_matches_eager(extra):
 
 
 def test_engine_graph_tail_falls_back_for_other_losses_and_lr_changes():
-    """A loss the engine cannot differentiate itself (torch's BCE, a sum) takes the autograd path;
-    a changed lr disables the captured tail (its lr is baked in) -- results still match eager."""
+    """A loss the engine cannot differentiate itself (here torch's BCE summed instead of averaged)
+    takes the autograd path; a changed lr disables the captured tail (its lr is baked in)."""
     from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
     m = _mlp(3)
     opt = torch.optim.Adam(m.parameters(), lr=1e-3)
     e, _, _, _ = dgt.initialize(model=m, optimizer=opt, config={"train_batch_size": 32, "amd": {"graph_module": True}})
-    fused, torch_bce = BCEWithLogitsLoss(), torch.nn.BCEWithLogitsLoss()
+    fused, torch_bce = BCEWithLogitsLoss(), torch.nn.BCEWithLogitsLoss(reduction="sum")
     for i, (x, y) in enumerate(_batches(6, 9)):
         loss = (fused if i % 2 == 0 else torch_bce)(e(x), y)
         e.backward(loss)
@@ -1057,3 +1057,25 @@ print(json.dumps({"direct": [r.fwd_direct is not None and getattr(r, "tail_direc
     assert outs["1"]["direct"] and all(outs["1"]["direct"])
     assert not any(outs["0"]["direct"])
     assert outs["1"]["bits"] == outs["0"]["bits"]
+
+
+@pytest.mark.gpu
+def test_graph_tail_with_torch_bce():
+    """The reference's own criterion (torch.nn.BCEWithLogitsLoss, mean, reference train.py:96) takes the
+    graphed tail too: dL/dz comes from the framework's loss kernel straight into the backward graph's
+    input, and the trajectory matches the eager engine's autograd backward.  A weighted BCE (not the
+    kernel's gradient) keeps the autograd path."""
+    batches = _batches(10, 5) + _batches(3, 8, bs=8)
+    cfg = {"train_batch_size": 32}
+    e1, l1, p1 = _run_engine(dict(cfg), batches)
+    e2, l2, p2 = _run_engine(dict(cfg, amd={"graph_module": True}), batches)
+    assert e2.tail_steps == len(batches), (e2.tail_steps, e2.tail_reason)
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=1e-5, atol=1e-6)
+    torch.testing.assert_close(p2, p1, rtol=1e-5, atol=1e-6)
+    crit = torch.nn.BCEWithLogitsLoss(pos_weight=torch.tensor([2.0], device="cuda"))
+    e3, l3, p3 = _run_engine(dict(cfg, amd={"graph_module": True}), batches, crit=crit)
+    e4, l4, p4 = _run_engine(dict(cfg), batches, crit=crit)
+    assert e3.tail_steps == 0
+    torch.testing.assert_close(p3, p4, rtol=1e-5, atol=1e-6)
+    for e in (e1, e2, e3, e4):
+        e.close()
