@@ -236,6 +236,7 @@ class Engine:
         # the loss is the framework's own; the step counter Adam reads lives on the device
         self._tail_rccl = None
         self._tail_scratch: Optional[torch.Tensor] = None  # the loss kernel's unused loss output (torch's BCE)
+        self._last_torch_bce = None  # the torch BCE node the last direct backward consumed (no second pass)
         self._tail_step_dev: Optional[torch.Tensor] = None
         self._tail_step_host = -1   # what _tail_step_dev holds (host mirror, no sync)
         self._tail_done = False     # backward ran the whole step: step() only does the bookkeeping
@@ -597,7 +598,9 @@ class Engine:
     def _direct_backward(self, scaled: torch.Tensor, loss: torch.Tensor) -> bool:
         """The backward of the engine's own two-node graph without the autograd engine.
 
-        When the loss is the framework's fused BCE (``ops/loss.py``) of the output of an injected
+        When the loss is the framework's fused BCE (``ops/loss.py``) -- or torch's own mean
+        BCEWithLogitsLoss, whose d loss / d logits the framework's loss kernel then forms -- of the
+        output of an injected
         Linear chain (``ops/linear.py`` FusedChain / FusedLinear), through reshapes only, and the
         chain's input needs no gradient, the whole graph is two Python backward functions: the BCE's
         (d loss / d logits is already computed: one multiply by the seed) and the chain's (one fused
@@ -612,8 +615,20 @@ class Engine:
             return False
         kinds = _direct_node_classes()
         node = loss.grad_fn
-        if node is None or type(node) is not kinds[0]:
+        if node is None:
             return False
+        # torch's own mean BCEWithLogitsLoss (the reference's criterion, train.py:96): d loss / d logits
+        # comes from the framework's loss kernel, (sigmoid(z) - y) / n, instead of autograd's node
+        torch_bce = type(node) is not kinds[0]
+        if torch_bce:
+            if not _torch_mean_bce(node):
+                return False
+            z, y = node._saved_self, node._saved_target
+            if z.dtype != torch.float32 or not z.is_cuda or y.numel() != z.numel():
+                return False
+            if node is self._last_torch_bce:
+                raise RuntimeError("Trying to backward through the graph a second time: the engine's direct "
+                                   "backward already consumed this loss")
         nxt = node.next_functions  # (logits, targets[, sum_into])
         if len(nxt) < 2:
             return False
@@ -656,8 +671,18 @@ class Engine:
                 # the Functions' own backward on their nodes (what BackwardCFunction.apply calls,
                 # without its per-call vjp / backward lookup): the unit seed -> the saved d loss /
                 # d logits itself, no launch
-                g = node._forward_cls.backward(node, seed)
-                g = g[0] if isinstance(g, tuple) else g
+                if torch_bce:
+                    from .ops import _ext
+                    g = torch.empty(z.shape, dtype=torch.float32, device=z.device)
+                    if self._tail_scratch is None:
+                        self._tail_scratch = torch.empty((), dtype=torch.float32, device=self.device)
+                    _ext.hot().bce_logits(z if z.is_contiguous() else z.contiguous(),
+                                          y if (y.dtype == torch.float32 and y.is_contiguous())
+                                          else y.float().contiguous(), self._tail_scratch, g, None, None)
+                    self._last_torch_bce = node
+                else:
+                    g = node._forward_cls.backward(node, seed)
+                    g = g[0] if isinstance(g, tuple) else g
                 for v in views:  # reshapes / casts back to the chain's output
                     g = v(g)
                     g = g[0] if isinstance(g, tuple) else g
@@ -665,7 +690,8 @@ class Engine:
             # what autograd does after a backward that does not retain the graph: the activations and
             # d loss / d logits are freed now (not when the caller drops ``loss``), and a second
             # backward through this graph raises instead of adding the gradients again
-            release(node)
+            if not torch_bce:
+                release(node)
             release(cur)
             # backward outputs -> the tensor inputs the edges belong to (weights, then present biases)
             if chain:

@@ -663,10 +663,10 @@ def test_engine_direct_backward_matches_autograd(extra):
     assert e1.direct_backwards == 0 and e2.direct_backwards == len(batches)
     assert l1 == l2
     assert torch.equal(p1, p2)
-    # torch's own loss keeps the autograd path (its numerics differ from the fused BCE's: no
-    # trajectory comparison here, test_engine_graph_module_matches_eager covers that path)
+    # torch's own mean BCE takes the direct backward too (d loss / d logits from the fused loss
+    # kernel; test_eager_direct_backward_with_torch_bce compares that trajectory with plain torch)
     e3, l3, p3 = _run_engine(dict(cfg), batches)
-    assert e3.direct_backwards == 0 and all(v == v for v in l3)
+    assert e3.direct_backwards == len(batches) and all(v == v for v in l3)
     for e in (e1, e2, e3):
         e.close()
 
@@ -1079,3 +1079,34 @@ def test_graph_tail_with_torch_bce():
     torch.testing.assert_close(p3, p4, rtol=1e-5, atol=1e-6)
     for e in (e1, e2, e3, e4):
         e.close()
+
+
+@pytest.mark.gpu
+def test_eager_direct_backward_with_torch_bce():
+    """The eager engine runs torch's own mean BCEWithLogitsLoss (the reference's criterion) through its
+    direct backward too (d loss / d logits from the framework's loss kernel, no autograd engine): the
+    trajectory matches plain torch; a second backward of the same loss raises, as autograd would."""
+    m = _mlp(6)
+    ref = copy.deepcopy(m).cuda()
+    opt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    crit = torch.nn.BCEWithLogitsLoss()
+    for x, y in _batches(8, 12):
+        opt.zero_grad()
+        crit(ref(x), y).backward()
+        opt.step()
+    engine, _, _, _ = dgt.initialize(model=m, optimizer=torch.optim.Adam(m.parameters(), lr=1e-3),
+                                     config={"train_batch_size": 32})
+    for x, y in _batches(8, 12):
+        loss = crit(engine(x), y)
+        engine.backward(loss)
+        engine.step()
+    assert engine.direct_backwards == 8
+    got = torch.nn.utils.parameters_to_vector(engine.module.parameters())
+    want = torch.nn.utils.parameters_to_vector(ref.parameters())
+    torch.testing.assert_close(got, want, rtol=2e-4, atol=2e-5)
+    x, y = _batches(1, 13)[0]
+    loss = crit(engine(x), y)
+    engine.backward(loss)
+    with pytest.raises(RuntimeError, match="second time"):
+        engine.backward(loss)
+    engine.close()
