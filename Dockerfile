@@ -10,7 +10,12 @@
 # _C.so, scripts/health.py, build/bin/rccl_perf) therefore lives in /opt/dgt, and /workspace only
 # receives logs, checkpoints and job_status.txt.  tests/test_slurm_fake.py builds a fake image from
 # THIS file's ENV / WORKDIR / COPY lines and runs the sbatch against it with the CI's file set.
-ARG BASE_IMAGE=rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.7.1
+#
+# torch: the stack every test ran on is PyTorch 2.10 + ROCm 7.0 (distributed_gpu_test_amd/compat.py
+# MIN_TORCH); the engine's graph and direct-backward paths use torch internals that older releases
+# lack.  The base below carries that torch, and the build fails (compat --strict, below) rather than
+# ship an image whose fast paths would fall back.  tests/test_compat.py pins these lines.
+ARG BASE_IMAGE=rocm/pytorch:rocm7.0_ubuntu22.04_py3.10_pytorch_release_2.10.0
 FROM ${BASE_IMAGE}
 
 ENV DEBIAN_FRONTEND=noninteractive \
@@ -28,7 +33,8 @@ COPY scripts/ /opt/dgt/scripts/
 COPY configs/ /opt/dgt/configs/
 COPY train.py bench.py __graft_entry__.py slurm_train.sbatch /opt/dgt/
 
-RUN cd /opt/dgt && python3 tools/build_ext.py -j 8 && \
+RUN cd /opt/dgt && python3 -m distributed_gpu_test_amd.compat --strict && \
+    python3 tools/build_ext.py -j 8 && \
     test -x /opt/dgt/build/bin/rccl_perf && \
     cd / && python3 -c "import distributed_gpu_test_amd as d, torch; from distributed_gpu_test_amd.ops import _ext; \
 assert _ext.available(); print('dgt ok from', d.__file__, 'torch', torch.__version__)"

@@ -37,6 +37,12 @@ worker thread under a wall-clock budget (``--sweep-budget-s``; it stops growing 
 budget is spent) and a hard deadline: an RCCL error is recorded in ``allreduce_sweep_error`` and a
 hang ends the job after the headline line is printed, so neither can cost the headline.
 
+After everything else, the same guarded runner times the same-run PyTorch baselines ("match or beat",
+SURVEY 6.4(a)): the reference's own loop on the reference model (``baseline``: nn.Module eager,
+autograd, RCCL all-reduce at N > 1, torch.optim.Adam, a per-step ``loss.item()``) -- ``vs_baseline``
+is the headline over it -- and plain PyTorch-ROCm on each secondary block's model (``baselines``;
+each block gets ``torch_baseline_iters_per_s`` and ``speedup``).  ``--no-baselines`` turns them off.
+
 After the headline's timed region, and outside it, the same guarded runner times BASELINE config #2
 (``bf16_mlp``: SyntheticMLP(4096, 4), batch 1024 per GPU, bf16 MFMA GEMMs, MLPTrainer), the fp32
 engine MLP (``fp32_engine_mlp``: SyntheticMLP(1024, 4) through the DeepSpeed-style engine on the
@@ -105,6 +111,12 @@ def parse_args(argv=None):
     # (200 timed steps: 0.06 s of the fp32 block, 0.14 s of the bf16 one -- past the first-steps ramp)
     ap.add_argument("--force-secondary", action="store_true",
                     help="run the secondary blocks also when ranks share a card (a rehearsal of the N > 1 blocks)")
+    ap.add_argument("--no-baselines", action="store_true",
+                    help="skip the same-run PyTorch baselines (the reference-equivalent stack for the headline "
+                         "and for each secondary block)")
+    ap.add_argument("--baseline-steps", type=int, default=200, help="timed steps of the headline's torch baseline")
+    ap.add_argument("--force-baselines", action="store_true",
+                    help="run the baselines on any device (the CPU tests: the headline's, as no secondary block runs)")
     ap.add_argument("--secondary-steps", type=int, default=200)
     ap.add_argument("--secondary-warmup", type=int, default=20)
     ap.add_argument("--secondary-budget-s", type=float, default=90.0,
@@ -297,6 +309,59 @@ def secondary_specs(args, device, world: int):
         specs.append(("bf16_mlp_zero1", "as bf16_mlp with ZeRO-1: reduce-scatter + sharded Adam + all-gather "
                       "(BASELINE config #5)", bf16_mlp(1)))
     return specs
+
+
+def baseline_specs(args, device, world: int):
+    """The same-run PyTorch baselines ("match or beat": SURVEY 6.4(a)), each (key, description, factory,
+    steps, warmup): the headline's is the reference's own loop (``train.py:104-117``: nn.Module eager,
+    autograd, RCCL all-reduce of the gradients at N > 1, torch.optim.Adam, a per-step ``loss.item()``
+    host sync) on the reference model and micro-batch; the secondary blocks' are the same model and
+    batch in plain PyTorch-ROCm (hipBLASLt GEMMs, torch's fused Adam, DDP at N > 1): bf16 autocast
+    for ``bf16_mlp``, fp32 for ``fp32_engine_mlp``."""
+    from distributed_gpu_test_amd.data import make_synthetic_data
+    from distributed_gpu_test_amd.models import SimpleNet
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+
+    def headline():
+        torch.manual_seed(42)
+        x, y = make_synthetic_data(2000, 20, 42)
+        return EngineBench(SimpleNet(20, 64), x, y, 4, device)
+
+    def mlp(width, autocast):
+        def make():
+            torch.manual_seed(1234)
+            return TorchMLPBench(SyntheticMLP(width, 4), 1024, device, autocast=autocast)
+        return make
+
+    return [("headline", "reference loop: PyTorch eager SimpleNet + torch.optim.Adam + RCCL all-reduce + per-step "
+             "loss.item() (train.py:104-117), fp32, micro-batch 4", headline, args.baseline_steps, 20),
+            ("bf16_mlp", "PyTorch-ROCm: SyntheticMLP(4096, 4) bf16 autocast (hipBLASLt) + fused torch Adam"
+             + (" + DDP" if world > 1 else ""), mlp(4096, True), 50, 20),
+            ("fp32_engine_mlp", "PyTorch-ROCm: SyntheticMLP(1024, 4) fp32 (hipBLASLt) + fused torch Adam"
+             + (" + DDP" if world > 1 else ""), mlp(1024, False), 100, 20)]
+
+
+def attach_baselines(secondary: dict, baselines: dict) -> None:
+    """Each secondary block gets its same-run torch baseline's rate and the speedup over it."""
+    for key, b in baselines.items():
+        if key in secondary and "iters_per_s" in b and "iters_per_s" in secondary[key]:
+            secondary[key]["torch_baseline_iters_per_s"] = b["iters_per_s"]
+            secondary[key]["torch_baseline_impl"] = b["impl"]
+            secondary[key]["speedup"] = round(secondary[key]["iters_per_s"] / b["iters_per_s"], 3)
+
+
+def run_baseline(desc: str, make, steps: int, warmup: int, device) -> dict:
+    tr = make()
+    try:
+        elapsed = timed_block(tr, steps, warmup, device)
+        return {"model": desc, "impl": tr.impl, "steps": steps, "warmup": warmup,
+                "ms_per_step": round(elapsed / steps * 1e3, 6), "iters_per_s": round(steps / elapsed, 2)}
+    finally:
+        tr.close()
+        del tr
+        if device.type == "cuda":
+            torch.cuda.synchronize()
+            torch.cuda.empty_cache()
 
 
 def run_secondary(key: str, desc: str, make, args, device, world: int) -> dict:
@@ -587,6 +652,28 @@ def main(argv=None):
                 break
             if bad is None or bad > 0:
                 break
+    # ---- the same-run PyTorch baselines (after everything above, outside every timed region)
+    baselines = {}
+    if (not hung and not args.no_baselines and args.model == "simple" and args.impl == "fused"
+            and ((device.type == "cuda" and (n_devices == world or args.force_secondary)) or args.force_baselines)):
+        for key, desc, make, steps, warm in baseline_specs(args, device, world):
+            if key != "headline" and key not in secondary:
+                continue
+            res, err, h = run_bounded(functools.partial(run_baseline, desc, make, steps, warm, device),
+                                      args.secondary_budget_s, device)
+            baselines[key] = res if res is not None else {"model": desc, "error": err}
+            if err:
+                print(f"[bench] baseline {key} failed: {err}", file=sys.stderr, flush=True)
+            if h:
+                hung = f"baseline_{key}"
+                break
+            bad, _, h = run_bounded(functools.partial(comm.all_reduce_max, float(err is not None)), 60.0, device)
+            if h:
+                hung = f"baseline_{key}:agreement"
+                break
+            if bad is None or bad > 0:
+                break
+    attach_baselines(secondary, baselines)
     small_os = min(oneshot, key=lambda r: abs(r["bytes"] - 5632)) if oneshot else None
     peak_busbw = max((r["busbw_GBps"] for r in sweep), default=None)
     small = min(sweep, key=lambda r: abs(r["bytes"] - 5632)) if sweep else None
@@ -612,7 +699,10 @@ def main(argv=None):
         "ms_per_step": round(ms, 6),
         "higher_is_better": True,
         "scaling": "weak",
-        "vs_baseline": None,
+        # value / the same run's reference-equivalent stack (torch eager + RCCL + torch Adam + per-step
+        # loss.item(), in the same rank-iterations/s unit); null when that baseline did not run
+        "vs_baseline": (round(global_steps_per_s / baselines["headline"]["iters_per_s"], 2)
+                        if "iters_per_s" in baselines.get("headline", {}) else None),
         "dtype": dtype,
         "data": ("synthetic (2000x20 N(0,1), seed 42; random-init SimpleNet)" if args.model == "simple" else
                  "synthetic N(0,1) batches, random-init weights"),
@@ -640,6 +730,9 @@ def main(argv=None):
         "allreduce_sweep_error": sweep_error,
         "hung": hung,
     }
+    if baselines:
+        out["baseline"] = baselines.get("headline")
+        out["baselines"] = {k: v for k, v in baselines.items() if k != "headline"}
     if getattr(trainer, "graph_stats", None) is not None:
         out["engine_graph_replays"] = trainer.graph_stats
     out.update(secondary)

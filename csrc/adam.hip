@@ -97,11 +97,7 @@ DGT_DEVICE void adam_bias_corrections(const AdamFlatArgs& a, float& step_size_ne
   if (a.step_dev) {
     __shared__ float sc[2];
     if (threadIdx.x == 0) {
-#ifndef DGT_ADAM_NO_TICKET
       const double t = (double)(*a.step_dev + (a.step_ticket ? 1 : 0));
-#else
-      const double t = (double)*a.step_dev;
-#endif
       sc[0] = (float)(-(a.lr_d / (1.0 - pow(a.beta1_d, t))));
       sc[1] = (float)sqrt(1.0 - pow(a.beta2_d, t));
     }
@@ -142,9 +138,7 @@ __global__ __launch_bounds__(256) void adam_flat_kernel(AdamFlatArgs a) {
   // MLP's 67M weights (profiles/r3_adam_lp_policy_ab.txt)
   for (long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x; i < n4; i += stride)
     adam_group<GT, LT, true, false>(a, grad, lp, 4 * i, scale, step_size_neg, bc2_sqrt);
-#ifndef DGT_ADAM_NO_TICKET  // (A/B build switch: tools/build_ext.py --variant)
   if (a.step_ticket) advance_step(a);
-#endif
 }
 
 template <typename GT, typename LT>

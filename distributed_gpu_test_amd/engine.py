@@ -29,6 +29,7 @@ from typing import Any, Dict, Iterable, List, Optional, Tuple
 import torch
 import torch.distributed as dist
 
+from . import compat
 from .config import DSConfig, parse_config
 from .ops.adam import adam_flat_
 from .ops.linear import engine_backward
@@ -62,8 +63,9 @@ def _direct_node_classes():
 
 def _torch_mean_bce(node) -> bool:
     """``node`` is torch's binary_cross_entropy_with_logits backward with reduction='mean' and no
-    weight / pos_weight: its gradient is the framework loss kernel's (sigmoid(z) - y) / n."""
-    if type(node).__name__ != "BinaryCrossEntropyWithLogitsBackward0":
+    weight / pos_weight: its gradient is the framework loss kernel's (sigmoid(z) - y) / n.  (Only on a
+    torch whose node exposes that saved state: compat.features()["torch_bce_node"].)"""
+    if type(node).__name__ != "BinaryCrossEntropyWithLogitsBackward0" or not compat.has("torch_bce_node"):
         return False
     try:
         return node._saved_reduction == 1 and node._saved_weight is None and node._saved_pos_weight is None
@@ -146,8 +148,10 @@ class Engine:
         self.params = list(params)
         self.param_names = self._names(self.params)
         bucket_elems = max(int(config.zero.reduce_bucket_size), 1024)
+        # a module's own parameters (a layer's weight and bias) never straddle two buckets: a layer
+        # larger than the bucket size is one bucket, bias included (runtime/flat.py units)
         self.layout = FlatLayout([tuple(p.shape) for p in self.params], bucket_elems, self.world_size,
-                                 shard=self.stage >= 1)
+                                 shard=self.stage >= 1, units=self._layer_units(self.params))
         self.store = FlatParamStore(self.params, self.layout, device, self.dtype)
         comm.broadcast_(self.store.param_buf, 0)  # DeepSpeed _broadcast_model
 
@@ -189,6 +193,8 @@ class Engine:
                                and not self.graph_module)
         self._hooks = []
         self._own_tensor_hooks = set()  # ids of the engine's own tensor hooks (the direct backward runs them)
+        self._pindex = {id(p): i for i, p in enumerate(self.params)}
+        self.layer_notifications = 0  # parameters reported complete from inside a fused chain's backward
         for i, p in enumerate(self.params):
             self._hooks.append(p.register_post_accumulate_grad_hook(
                 lambda _p, i=i: self.reducer.on_grad_ready(i)))
@@ -206,6 +212,11 @@ class Engine:
         self.tput = ThroughputTimer(self.micro_batch * self.world_size, config.steps_per_print)
         self.metrics = MetricsSink.from_env(self.rank)
         self.faults = FaultInjector.from_env(self.rank)
+        # the torch internals the graph paths need (compat.py): a torch without them runs eagerly, loudly
+        if (self.graph_module or config.amd.hip_graph) and not compat.has("hip_graph"):
+            self.graph_module = False
+            self.graph_module_reason = compat.features()["hip_graph"]
+            compat.report_fallback("graph paths", self.graph_module_reason, self.metrics)
         self._timers: Dict[str, float] = {}
         self._seed_one: Optional[torch.Tensor] = None
         self._grads_dirty = False  # the flat gradient buffer holds something since the last zero_grad
@@ -245,6 +256,34 @@ class Engine:
         self.tail_reason = ""       # why the graphed tail is not used (empty: in use or not asked)
 
     # ------------------------------------------------------------------ helpers
+    def _layer_units(self, params):
+        """Parameter-index groups, one per owning module (its direct parameters), in order."""
+        owner = {}
+        for m in self.module.modules():
+            for p in m.parameters(recurse=False):
+                owner.setdefault(id(p), id(m))
+        units, index = [], {}
+        for i, p in enumerate(params):
+            key = owner.get(id(p), ("param", i))
+            if key not in index:
+                index[key] = len(units)
+                units.append([])
+            units[index[key]].append(i)
+        return units
+
+    def _on_layer_ready(self, p) -> None:
+        """A fused chain finished ``p``'s gradient (ops.linear.grad_ready): the reducer may launch its
+        bucket now.  A parameter with a user's hook keeps autograd's timing (the hook may still edit
+        the gradient before it is accumulated / after)."""
+        i = self._pindex.get(id(p))
+        if i is None:
+            return
+        post = p._post_accumulate_grad_hooks
+        if (post is not None and len(post) > 1) or any(k not in self._own_tensor_hooks for k in (p._backward_hooks or ())):
+            return
+        self.layer_notifications += 1
+        self.reducer.on_grad_ready(i)
+
     def _names(self, params):
         lookup = {id(p): n for n, p in self.module.named_parameters()}
         return [lookup.get(id(p), f"param{i}") for i, p in enumerate(params)]
@@ -358,6 +397,8 @@ class Engine:
         fn.calls += 1
         b = fn.bound.get(p)
         if b is not None:
+            if not a.is_contiguous():  # same address, other strides (e.g. a transposed square batch)
+                return None
             b.last_use = fn.calls
             return b
         seen, fn.recent = fn.recent, (p,) + fn.recent[:7]
@@ -415,6 +456,7 @@ class Engine:
         except Exception as e:  # data-dependent control flow, host syncs, ...: stay eager
             self.graph_module = False
             self.graph_module_reason = f"capture failed: {type(e).__name__}: {e}"
+            compat.report_fallback("graph paths", f"graph_module {self.graph_module_reason}", self.metrics)
             return None
         fn.bound, fn.recent, fn.bind_failed, fn.calls, fn.evictions = {}, (), None, 0, 0
         # what one more graph pair of this signature costs (its pool: activations, outputs)
@@ -569,8 +611,10 @@ class Engine:
         from_zero, deferred = not self._grads_dirty, self._zero_deferred
         self._zero_deferred = False
         self._deferred_active, self._hook_zeroed = deferred, 0
+        # per-layer bucket launches from inside the fused chains, when a launch communicates
+        ready = self._on_layer_ready if (self.reducer.armed and self.reducer.launches_collectives) else None
         try:
-            with tracing.range("dgt.backward"), engine_backward(grads_zero=from_zero) as stored:
+            with tracing.range("dgt.backward"), engine_backward(grads_zero=from_zero, on_ready=ready) as stored:
                 if retain_graph or not self._direct_backward(scaled, loss):
                     scaled.backward(self._backward_seed(scaled, loss), retain_graph=retain_graph)
         finally:
@@ -853,10 +897,13 @@ class Engine:
         graph cannot represent the configuration it returns the equivalent eager closure."""
         from .runtime.graph_step import GraphedStep, supported
         ok, why = supported(self)
+        if ok and not compat.has("hip_graph"):
+            ok, why = False, compat.features()["hip_graph"]
         if ok:
             self.graphed = GraphedStep(self, loss_fn, warmup=warmup)
             return self.graphed
         self.graph_fallback_reason = why
+        compat.report_fallback("graph paths", f"whole-step graph: {why}", self.metrics)
 
         def eager(*args):
             loss = loss_fn(*args)

@@ -37,6 +37,9 @@ from . import _ext
 from ..utils.fnapply import fast_apply
 from .loss import FREED, keep_graph, release
 
+MODIFIED = ("one of the variables needed for gradient computation has been modified by an inplace operation: "
+            "the input or a weight of a fused Linear changed between its forward and this backward")
+
 # > 0 while the engine runs a backward (Engine.backward / the graphed step): only then do the
 # in-place kernels add dW / db straight into the parameters' .grad views (the engine's flat
 # gradient buckets).  Autograd runs a HIP Function's backward on its device thread, so this is a
@@ -49,30 +52,55 @@ _ENGINE_BACKWARD = 0
 # backward writes each of its gradients twice: the second write must add)
 _GRADS_ZERO = False
 _WRITTEN: set = set()
+# the engine's per-layer readiness callback (Engine._on_layer_ready) while its backward communicates:
+# the fused chains are ONE autograd node for many layers, so autograd's post-accumulate hooks would
+# fire for every layer only after the whole chain's backward is queued; the chains call grad_ready()
+# right after each layer's dW / db kernels instead, and the bucket reducer launches that layer's
+# collective there -- overlapped with the layers below (parallel/reducer.py)
+_GRAD_READY = None
+
+
+def grad_ready(*params) -> None:
+    """The gradients of ``params`` (written in place into their .grad views) are complete for this
+    backward: their kernels are queued on the current stream."""
+    f = _GRAD_READY
+    if f is not None:
+        for p in params:
+            if p is not None:
+                f(p)
+
+
+def grad_ready_on() -> bool:
+    return _GRAD_READY is not None
 
 
 class engine_backward:
-    """``with engine_backward(grads_zero) as stored``: the engine's backward; ``stored`` is the set of
-    ``(data_ptr, numel)`` gradient views STORED (first-written) in it.  (A class, not a generator-based
-    context manager: entered once per eager step, where the host cost is the step's cost.)"""
+    """``with engine_backward(grads_zero, on_ready) as stored``: the engine's backward; ``stored`` is
+    the set of ``(data_ptr, numel)`` gradient views STORED (first-written) in it; ``on_ready`` (or None)
+    receives each parameter whose in-place gradient a chain has finished (``grad_ready``).  (A class,
+    not a generator-based context manager: entered once per eager step, where the host cost is the
+    step's cost.)"""
 
-    __slots__ = ("grads_zero", "prev", "prev_written")
+    __slots__ = ("grads_zero", "on_ready", "prev", "prev_written", "prev_ready")
 
-    def __init__(self, grads_zero: bool = False):
+    def __init__(self, grads_zero: bool = False, on_ready=None):
         self.grads_zero = bool(grads_zero)
+        self.on_ready = on_ready
 
     def __enter__(self):
-        global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN
+        global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN, _GRAD_READY
         _ENGINE_BACKWARD += 1
         self.prev, _GRADS_ZERO = _GRADS_ZERO, self.grads_zero
         self.prev_written, _WRITTEN = _WRITTEN, set()
+        self.prev_ready, _GRAD_READY = _GRAD_READY, self.on_ready
         return _WRITTEN
 
     def __exit__(self, *exc):
-        global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN
+        global _ENGINE_BACKWARD, _GRADS_ZERO, _WRITTEN, _GRAD_READY
         _ENGINE_BACKWARD -= 1
         _GRADS_ZERO = self.prev
         _WRITTEN = self.prev_written
+        _GRAD_READY = self.prev_ready
         return False
 
 
@@ -201,6 +229,8 @@ class _FusedLinearFn(torch.autograd.Function):
         # the input and the weight as attributes (freed by the direct backward: ops/loss.py
         # release), the output through save_for_backward (an attribute would be a reference cycle)
         ctx.x, ctx.w, ctx.freed, ctx.held = x, weight, False, ("x", "w")
+        # (held as attributes, not saved tensors: autograd's in-place check is done here instead)
+        ctx.vers = (x._version, weight._version)
         ctx.save_for_backward(y if relu else None)
         return y
 
@@ -210,6 +240,8 @@ class _FusedLinearFn(torch.autograd.Function):
             raise RuntimeError(FREED)
         (y,) = ctx.saved_tensors
         x, weight = ctx.x, ctx.w
+        if (x._version, weight._version) != ctx.vers:
+            raise RuntimeError(MODIFIED)
         if not keep_graph():
             release(ctx)
         dy = dy.contiguous()
@@ -224,6 +256,7 @@ class _FusedLinearFn(torch.autograd.Function):
             # (the engine's bucket reducer) after this kernel is queued
             bg = None if b_leaf is None else b_leaf.grad
             _bwd(_ext.hot(), dy, x, weight, y, dx, w_leaf.grad, bg, not _store_both(w_leaf.grad, bg))
+            grad_ready(w_leaf, b_leaf)
             return dx, None, None, None, None
         dw = torch.empty_like(weight)
         db = torch.empty(weight.shape[0], dtype=torch.float32, device=x.device) if ctx.has_bias else None
@@ -324,6 +357,8 @@ class _FusedChainFn(torch.autograd.Function):
         # no reference cycle; freed by the direct backward, ops/loss.py release), the chain's output
         # through save_for_backward
         ctx.acts, ctx.ws, ctx.freed, ctx.held = acts[:-1], wb[0::2], False, ("acts", "ws")
+        # (the hidden activations are the chain's own; the input and the weights are the caller's)
+        ctx.vers = (x._version, *[w._version for w in wb[0::2]])
         ctx.save_for_backward(h)
         return h
 
@@ -334,6 +369,8 @@ class _FusedChainFn(torch.autograd.Function):
             raise RuntimeError(FREED)
         L = len(ctx.relus)
         acts, ws = list(ctx.acts) + list(ctx.saved_tensors), ctx.ws
+        if (acts[0]._version, *[w._version for w in ws]) != ctx.vers:
+            raise RuntimeError(MODIFIED)
         if not keep_graph():
             release(ctx)
         active = ctx.grad_in_place and _in_place_active()
@@ -349,6 +386,7 @@ class _FusedChainFn(torch.autograd.Function):
                 ops.linear2_bwd(dy.contiguous(), acts[0], ws[0], acts[1], ws[1], acts[2] if ctx.relus[1] else None, dx,
                                 W1.grad, None if B1 is None else B1.grad, W2.grad, None if B2 is None else B2.grad,
                                 ctx.relus[0], acc1, acc2)
+                grad_ready(W2, B2, W1, B1)
                 return (dx, None, None, *([None] * (2 * L)))
         grads = [None] * (2 * L)
         dy = dy.contiguous()
@@ -369,6 +407,7 @@ class _FusedChainFn(torch.autograd.Function):
                 bg = None if b_leaf is None else b_leaf.grad
                 masked = _bwd(ops, dy, acts[i], ws[i], y, dx, w_leaf.grad, bg, not _store_both(w_leaf.grad, bg),
                               mask_dx)
+                grad_ready(w_leaf, b_leaf)  # this layer's bucket may go out while the layers below run
             else:
                 dw = torch.empty_like(ws[i])
                 db = torch.empty(ws[i].shape[0], dtype=torch.float32, device=dy.device) if ctx.has_bias[i] else None

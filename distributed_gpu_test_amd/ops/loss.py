@@ -58,7 +58,12 @@ def keep_graph() -> bool:
     backward)."""
     if getattr(_DIRECT, "on", False):
         return False
-    return torch._C._autograd._get_current_graph_task_keep_graph()
+    if _KEEP is None:  # a torch without the query: assume retained (frees nothing early; compat.py)
+        return True
+    return _KEEP()
+
+
+_KEEP = getattr(getattr(torch._C, "_autograd", None), "_get_current_graph_task_keep_graph", None)
 
 
 class direct_backward:
@@ -127,6 +132,7 @@ class _FusedBCEWithLogits(torch.autograd.Function):
         _ext.hot().bce_logits(zc, yc, loss, dz, lp, sum_into)
         ctx.dz, ctx.lp, ctx.freed, ctx.held = dz, lp, False, ("dz", "lp")
         ctx.shape, ctx.dtype = z.shape, z.dtype
+        ctx.claimed = gbuf is not None
         return loss
 
     @staticmethod
@@ -137,6 +143,15 @@ class _FusedBCEWithLogits(torch.autograd.Function):
         keep = keep_graph()
         if not keep:
             release(ctx)
+        elif ctx.claimed:
+            # the claimed buffer is the graphed backward's static input: the replay this backward
+            # feeds copies its (possibly scaled) gradient there, over what a later backward through
+            # this retained graph must read -- keep a private copy for that one
+            if lp is not None:
+                ctx.lp = lp = lp.clone()
+            else:
+                ctx.dz = dz = dz.clone()
+            ctx.claimed = False
         if _is_unit(g):
             out = (lp if lp is not None else dz).view(ctx.shape)
             return (out.clone() if keep else out), None, None

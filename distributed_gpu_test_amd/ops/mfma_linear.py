@@ -39,7 +39,7 @@ import torch.nn as nn
 from ..models.synthetic_mlp import SyntheticMLP
 from .gemm import gemm_nt, partials_reduce_multi, rowsum_bf16, skinny_bwd_bf16, skinny_fwd_bf16, transpose_bf16
 from ..utils.fnapply import fast_apply
-from .linear import _first_write, _grad_view_ok, _in_place_active, count_fallback
+from .linear import _first_write, _grad_view_ok, _in_place_active, count_fallback, grad_ready, grad_ready_on
 
 MAX_HEAD = 4
 BF16 = torch.bfloat16
@@ -146,6 +146,10 @@ class _MfmaChainFn(torch.autograd.Function):
 
         bpart = None  # column-sum partials of the current g (fp32 [row tiles, features]), if formed
         segs = []     # (partials, bias-gradient target, accumulate): reduced together at the end
+        # the engine's backward communicates (ops.linear.grad_ready): each layer's partials are reduced
+        # right after its wgrad and the layer is reported complete there, so its bucket's collective
+        # overlaps the layers below; else every layer's partials go into one launch at the end
+        notify = active and grad_ready_on()
         if head:
             wh = ws[L]
             kh = wh.shape[1]
@@ -174,6 +178,11 @@ class _MfmaChainFn(torch.autograd.Function):
                                 dw_part=hw)
                 if hw is not None:
                     segs.append((hw, pw.grad.view(-1), not store_w))
+                if notify:
+                    if segs:
+                        partials_reduce_multi(segs)
+                        segs = []
+                    grad_ready(pw, pb)
             else:
                 dw = torch.zeros(wh.shape, dtype=torch.float32, device=dev)
                 db = torch.zeros(wh.shape[0], dtype=torch.float32, device=dev)
@@ -204,10 +213,12 @@ class _MfmaChainFn(torch.autograd.Function):
         for i in reversed(range(L)):
             w = ws[i]
             jw, jb = 2 * i, 2 * i + 1
+            done = []  # parameters of this layer written in place (reported to the engine below)
             if need[4 + jw]:
                 p = leaf(jw)
                 if p is not None and _grad_view_ok(p, BF16):
                     gemm_nt(gT, xTs[i], C=p.grad, accumulate=not _first_write(p.grad))
+                    done.append(p)
                 else:
                     grads[jw] = torch.empty_like(w)
                     gemm_nt(gT, xTs[i], C=grads[jw])
@@ -215,6 +226,7 @@ class _MfmaChainFn(torch.autograd.Function):
                 p = leaf(jb)
                 if p is not None and _grad_view_ok(p, BF16) and (bpart is None or p.grad.data_ptr() % 8 == 0):
                     tgt, acc = p.grad, not _first_write(p.grad)
+                    done.append(p)
                 else:
                     tgt = grads[jb] = torch.empty(w.shape[0], dtype=BF16, device=dev)
                     acc = False
@@ -222,6 +234,11 @@ class _MfmaChainFn(torch.autograd.Function):
                     segs.append((bpart, tgt, acc))
                 else:
                     rowsum_bf16(gT, tgt, accumulate=acc)
+            if notify:
+                if segs:
+                    partials_reduce_multi(segs)
+                    segs = []
+                grad_ready(*done)
             if i > 0:
                 k = w.shape[1]
                 g_prev = torch.empty(M, k, dtype=BF16, device=dev)

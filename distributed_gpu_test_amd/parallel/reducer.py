@@ -9,6 +9,13 @@ gradient that belongs to it (``register_post_accumulate_grad_hook``), so RCCL mo
 xGMI while backward computes bucket k-1.  ProcessGroupNCCL runs the collective on its own HIP
 stream, ordered after the producing kernels; ``finish()`` joins all of them before the optimizer.
 
+Readiness comes from two places, whichever is first (a parameter counts once per backward):
+autograd's post-accumulate hooks, and -- for the framework's fused Linear chains, which are ONE
+autograd node for many layers, so their hooks would all fire after the whole chain's backward --
+the chain's own per-layer notification right after that layer's weight / bias gradient kernels are
+queued (``ops.linear.grad_ready``, wired by ``Engine.backward``).  So bucket L's collective is
+queued on the communication stream between layer L's gradient kernels and layer L-1's.
+
 * stage 0: in-place ``all_reduce(SUM)`` of the bucket (or the IPC one-shot kernel for buckets up
   to ``oneshot_max_bytes`` when a validated channel exists: one xGMI hop instead of a ring);
 * stage 1/2: ``reduce_scatter_tensor`` of the bucket into this rank's contiguous shard buffer.
@@ -44,8 +51,11 @@ class GradReducer:
         self._param_count = [len(b.params) for b in layout.buckets]
         self._remaining = list(self._param_count)
         self._launched = [False] * nb
+        self._ready = [False] * len(layout.shapes)
         self._works: List = []
         self.armed = False
+        self._side = None  # the wire-cast stream (comm_buf): the cast runs beside backward, not in it
+        self._side_used = False
         # staging buffer when the wire dtype differs from the gradient dtype (e.g. bf16 grads, fp32 comm);
         # a rank that sends nothing (world size 1, collectives not forced) has no wire: the optimizer
         # reads the gradient buffer as it is (no 6 B/param conversion pass, half the optimizer's reads)
@@ -76,11 +86,18 @@ class GradReducer:
         self.armed = boundary
         self._remaining = list(self._param_count)
         self._launched = [False] * len(self._launched)
+        self._ready = [False] * len(self._ready)
         self._works = []
 
+    @property
+    def launches_collectives(self) -> bool:
+        """Whether a bucket launch does more than account bytes (worth an early notification)."""
+        return self.comm_buf is not None or self.stage >= 1 or comm.collectives_on(self.world_size)
+
     def on_grad_ready(self, param_index: int) -> None:
-        if not self.armed:
+        if not self.armed or self._ready[param_index]:
             return
+        self._ready[param_index] = True
         b = self.layout.param_bucket[param_index]
         self._remaining[b] -= 1
         if self._remaining[b] == 0:
@@ -96,11 +113,30 @@ class GradReducer:
             self.bytes_reduced += b.numel * self.grad_buf.element_size()
             return
         src = self.grad_buf[b.start:b.start + b.numel]
+        side = None
         if self.comm_buf is not None:
             view = self.comm_buf[b.start:b.start + b.numel]
-            view.copy_(src)
+            if src.is_cuda and not torch.cuda.is_current_stream_capturing():
+                # the wire cast on a side stream ordered after the producing kernels: the compute
+                # stream goes on with the next layer; the collective below is ordered after the cast
+                if self._side is None:
+                    self._side = torch.cuda.Stream(device=src.device)
+                side = self._side
+                side.wait_stream(torch.cuda.current_stream(src.device))
+                self._side_used = True
+                with torch.cuda.stream(side):
+                    view.copy_(src)
+            else:
+                view.copy_(src)
         else:
             view = src
+        if side is not None:
+            with torch.cuda.stream(side):
+                self._issue(bi, b, view)
+        else:
+            self._issue(bi, b, view)
+
+    def _issue(self, bi: int, b, view: torch.Tensor) -> None:
         self.bytes_reduced += view.numel() * view.element_size()
         if not comm.collectives_on(self.world_size):
             if self.stage >= 1:
@@ -140,6 +176,9 @@ class GradReducer:
         for w in self._works:
             w.wait()
         self._works = []
+        if self._side_used:  # (the casts, and collectives issued from the side stream)
+            torch.cuda.current_stream(self.grad_buf.device).wait_stream(self._side)
+            self._side_used = False
         if self.debug_sync and self.grad_buf.is_cuda:
             torch.cuda.synchronize()
         self.armed = False

@@ -15,6 +15,10 @@ gradient is a VIEW into one contiguous buffer from the start, so:
 
 Buckets are formed in REVERSE parameter order (backward produces gradients last-layer-first) and
 laid out forward, so the first bucket whose gradients are complete is the tail of the buffer.
+``units`` (the engine passes one per module: a layer's weight and bias) are never split across
+buckets: a layer larger than the bucket size gets a bucket of its own, with its bias in it, so the
+layer's collective starts as soon as that layer's backward has written both (``ops/linear.py``
+grad_ready) -- not one extra bias-sized collective per layer.
 """
 from __future__ import annotations
 
@@ -44,20 +48,27 @@ class Bucket:
 
 class FlatLayout:
     def __init__(self, shapes: Sequence[Tuple[int, ...]], bucket_elems: int, world_size: int = 1,
-                 shard: bool = False):
+                 shard: bool = False, units: "Sequence[Sequence[int]] | None" = None):
         self.shapes = [tuple(int(d) for d in s) for s in shapes]
         self.numels = [int(torch.Size(s).numel()) for s in self.shapes]
         self.world_size = world_size
         bucket_align = ALIGN * (world_size if shard else 1)
+        # the atomic units of bucketing, in parameter order (default: one per parameter)
+        if units is None:
+            units = [[i] for i in range(len(self.shapes))]
+        units = [sorted(int(i) for i in u) for u in units if len(u)]
+        if sorted(i for u in units for i in u) != list(range(len(self.shapes))):
+            raise ValueError("FlatLayout units must partition the parameter indices")
+        units.sort(key=lambda u: u[0])
         groups: List[List[int]] = []
         cur: List[int] = []
         cur_n = 0
-        for i in reversed(range(len(self.shapes))):
-            n = _round_up(self.numels[i], ALIGN)
+        for u in reversed(units):
+            n = sum(_round_up(self.numels[i], ALIGN) for i in u)
             if cur and cur_n + n > bucket_elems:
                 groups.append(cur)
                 cur, cur_n = [], 0
-            cur.append(i)
+            cur.extend(u)
             cur_n += n
         if cur:
             groups.append(cur)

@@ -48,7 +48,8 @@ _CAPTURE_STREAMS: dict = {}
 # or collective) is therefore run as those kernels re-launched with the captured arguments, in one
 # C++ call (``_C.DirectLaunch``): the forward, the graphed tail and the whole-step graph of a small
 # model (profiles/r5_graph_direct_ab.txt: graph_module 17-22k -> 26-30k iters/s, whole-step graph
-# 34-35k -> 38-46k on the reference model).  DGT_GRAPH_DIRECT=0 keeps every replay.
+# 34-35k -> 38-46k on the reference model).  DGT_GRAPH_DIRECT=0 keeps every replay, and a graph
+# that consumes RNG is always replayed (``rng_checked``).
 DIRECT_MAX_KERNELS = 8
 
 
@@ -72,10 +73,32 @@ def direct_launcher(graph: "torch.cuda.CUDAGraph", may_hold_collective: bool = T
         return None
     if not hasattr(mod, "graph_direct_plan"):
         return None
-    plan = mod.graph_direct_plan(int(graph.raw_cuda_graph()), torch.cuda.current_device())
+    raw = getattr(graph, "raw_cuda_graph", None)
+    if raw is None:  # (a torch without it: replay; compat.py reports the missing feature)
+        return None
+    plan = mod.graph_direct_plan(int(raw()), torch.cuda.current_device())
     if plan is None or plan.kernels > limit:
         return None
     return plan
+
+
+def rng_checked(graph: "torch.cuda.CUDAGraph", direct, install: Callable[[Callable[[], None]], None]):
+    """The callable that runs ``graph``: its first call is a real ``replay()``, which also refills the
+    graph's captured Philox seed / offset and advances the CUDA generator (dropout, ``torch.rand``
+    inside the graph).  A direct launcher (``direct_launcher``) re-launches the captured kernels
+    with their captured arguments and does neither, so it would hand a graph that draws random
+    numbers the same numbers on every step.  Only a graph whose first replay left the default
+    generator's state unchanged -- it consumes no RNG -- switches to ``direct``: ``install`` receives
+    the callable every later call should use (the direct launcher or the bound replay)."""
+    replay = torch._C._CUDAGraph.replay.__get__(graph)
+    if direct is None:
+        return replay
+
+    def first() -> None:
+        before = torch.cuda.get_rng_state()
+        replay()
+        install(direct if torch.equal(before, torch.cuda.get_rng_state()) else replay)
+    return first
 
 
 class _capture:
@@ -192,7 +215,7 @@ class GraphedModule:
         self.static_gin = gs[len(self.params):]
         self.bwd.instantiate()
         self.bwd_direct = direct_launcher(self.bwd, may_hold_collective=False)  # (the reducer runs outside)
-        self.bwd_replay = self.bwd_direct or torch._C._CUDAGraph.replay.__get__(self.bwd)
+        self.bwd_replay = rng_checked(self.bwd, self.bwd_direct, lambda f: setattr(self, "bwd_replay", f))
         # The graphed tail: the same backward followed by ``tail()`` (the engine's gradient
         # collective, clip coefficient, fused Adam, ZeRO-1 all-gather and the bucket's zero fill) in
         # ONE graph, replayed by Engine.backward when the loss is one it can differentiate itself
@@ -213,12 +236,14 @@ class GraphedModule:
             del gs2
         self.single = torch.is_tensor(out) or len(out) == 1
         # (bound C methods: no Python wrapper frame per step)
-        self.fwd_replay = self.fwd_direct or torch._C._CUDAGraph.replay.__get__(self.fwd)
+        # (a graph that draws random numbers is always replayed: rng_checked)
+        self.fwd_replay = rng_checked(self.fwd, self.fwd_direct, lambda f: setattr(self, "fwd_replay", f))
         self.tail_replay = None
         if self.bwd_tail is not None:
             self.bwd_tail.instantiate()
             self.tail_direct = direct_launcher(self.bwd_tail)
-            self.tail_replay = self.tail_direct or torch._C._CUDAGraph.replay.__get__(self.bwd_tail)
+            self.tail_replay = rng_checked(self.bwd_tail, self.tail_direct,
+                                           lambda f: setattr(self, "tail_replay", f))
         self.replays = 0
         self.pending = False  # a replayed forward whose backward has not run yet
         self.held = None  # bound inputs of the pending forward: alive (and unmoved) until its backward

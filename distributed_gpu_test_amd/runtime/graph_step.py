@@ -209,6 +209,8 @@ class GraphedStep:
                 entry = self._capture(key, args)
             except Exception as err:  # never lose a step to a capture problem: run it eagerly
                 self.failed = f"{type(err).__name__}: {err}"
+                from .. import compat
+                compat.report_fallback("graph paths", f"whole-step graph capture failed: {self.failed}", e.metrics)
                 self.max_graphs = len(self.graphs)
                 torch.cuda.synchronize(e.device)
                 loss = self._body(*args)
@@ -221,6 +223,7 @@ class GraphedStep:
                 dst.copy_(src, non_blocking=True)
         run = self.launchers.get(key) or torch._C._CUDAGraph.replay.__get__(graph)
         run()
+        run = self.launchers.get(key) or run  # (a first call may have installed the steady-state launcher)
         if len(args) == 1 and torch.is_tensor(args[0]):
             self._last = (args[0].shape, args[0].dtype, entry, run)
         self.replays += 1
@@ -236,13 +239,19 @@ class GraphedStep:
         with torch.cuda.graph(graph, pool=self.pool):
             static_loss = self._body(*static_in, key=key, capturing=True)
         graph.instantiate()
-        from .graph_module import direct_launcher  # a short chain of kernels: launched, not replayed
+        from .graph_module import direct_launcher, rng_checked  # a short chain of kernels: launched, not replayed
         launcher = direct_launcher(graph)
         if launcher is not None:
-            self.launchers[key] = launcher
+            # (first call replays; a graph drawing random numbers stays on replay: rng_checked)
+            self.launchers[key] = rng_checked(graph, launcher, lambda f, key=key: self._install(key, f))
         entry = (graph, static_in, static_loss)
         self.graphs[key] = entry
         return entry
+
+    def _install(self, key, run) -> None:
+        """rng_checked's verdict for ``key``'s graph: ``run`` from now on (the fast path re-reads it)."""
+        self.launchers[key] = run
+        self._last = None
 
     def close(self) -> None:
         self._last = None

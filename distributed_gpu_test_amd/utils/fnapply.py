@@ -16,9 +16,12 @@ import torch
 def fast_apply(cls):
     if cls.setup_context is not torch.autograd.function._SingleLevelFunction.setup_context:
         return cls.apply
-    raw = torch._C._FunctionBase.__dict__["apply"].__get__(None, cls)
+    base = getattr(torch._C, "_FunctionBase", None)
+    active = getattr(torch._C, "_are_functorch_transforms_active", None)
+    if base is None or "apply" not in base.__dict__ or active is None:
+        return cls.apply  # (a torch without these internals: the public entry; compat.py reports it)
+    raw = base.__dict__["apply"].__get__(None, cls)
     slow = cls.apply
-    active = torch._C._are_functorch_transforms_active
 
     def apply(*args):
         if active():

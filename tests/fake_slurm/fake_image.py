@@ -102,7 +102,8 @@ def build_fake_image(dst: str, root: str = ROOT, dockerfile: str = "Dockerfile")
                 _copy(s, d, dst, pats, root)
             roots.append(d.rstrip("/") if d.endswith("/") or len(srcs) > 1 else os.path.dirname(d))
         elif instr == "RUN" and "tools/build_ext.py" in rest:
-            m = re.search(r"cd\s+(\S+)\s*&&\s*python3?\s+tools/build_ext\.py", rest)
+            # (``cd DIR && ... && python3 tools/build_ext.py``: other commands may come between)
+            m = re.search(r"cd\s+(\S+)\s*&&.*?python3?\s+tools/build_ext\.py", rest)
             where = m.group(1) if m else workdir
             so = os.path.join(root, "distributed_gpu_test_amd", "_C.so")
             if os.path.exists(so):

@@ -43,15 +43,18 @@ def forced(flag: bool):
 
 
 def run_pair(fn):
-    out = []
+    out, extra = [], {}
     for flag in (False, True):
         forced(flag)
         CALLS["n"] = 0
         p = fn()
+        if isinstance(p, tuple):  # (params, {key: value}) -- the forced run's extras are reported
+            p, ex = p
+            extra = {f"{k}_{'forced' if flag else 'off'}": v for k, v in ex.items()} | extra
         torch.cuda.synchronize()
         out.append((p.detach().clone(), CALLS["n"]))
     forced(False)
-    return {"equal": bool(torch.equal(out[0][0], out[1][0])), "calls": out[1][1], "calls_off": out[0][1]}
+    return {"equal": bool(torch.equal(out[0][0], out[1][0])), "calls": out[1][1], "calls_off": out[0][1], **extra}
 
 
 def engine_case(stage, graph):
@@ -79,6 +82,38 @@ def engine_case(stage, graph):
         p = engine.store.param_buf.detach().clone()
         engine.close()
         return p
+    return fn
+
+
+def engine_mlp_case(dtype, stage):
+    """The SyntheticMLP through the engine on the fused chains (bf16: the MFMA GEMM chain; fp32: the
+    exact-fp32 GEMM chain), one bucket per layer: every layer's collective is launched from inside
+    the chain's backward (ops.linear.grad_ready), counted as ``layer_notifications``."""
+    import distributed_gpu_test_amd as dgt
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+
+    def fn():
+        torch.manual_seed(6)
+        m = SyntheticMLP(width=256, depth=3)
+        cfg = {"train_micro_batch_size_per_gpu": 128, "gradient_accumulation_steps": 1,
+               "zero_optimization": {"stage": stage, "reduce_bucket_size": 4096},
+               "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}}
+        if dtype == "bf16":
+            cfg.update({"bf16": {"enabled": True}, "communication_data_type": "fp32"})
+        engine, _, _, _ = dgt.initialize(model=m, config=cfg)
+        from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+        crit = BCEWithLogitsLoss()
+        g = torch.Generator().manual_seed(7)
+        for _ in range(6):
+            x = torch.randn(128, 256, generator=g).cuda().to(engine.dtype)
+            y = (torch.rand(128, generator=g) > 0.5).float().cuda()
+            engine.backward(crit(engine(x).view(-1), y))
+            engine.step()
+        p = engine.store.param_buf.detach().float().clone()
+        extra = {"layer_notifications": engine.layer_notifications, "buckets": len(engine.layout.buckets),
+                 "fused_layers": engine.fused_linear_layers}
+        engine.close()
+        return p, extra
     return fn
 
 
@@ -124,6 +159,9 @@ def main():
     for stage in (0, 1):
         for graph in (False, True):
             cases[f"engine_zero{stage}_{'graph' if graph else 'eager'}"] = engine_case(stage, graph)
+    for dtype in ("bf16", "fp32"):
+        for stage in (0, 1):
+            cases[f"engine_mlp_{dtype}_zero{stage}"] = engine_mlp_case(dtype, stage)
     for schedule in ("overlap", "serial", "flat"):
         for stage in (0, 1):
             cases[f"mlp_{schedule}_zero{stage}"] = mlp_case(schedule, stage)

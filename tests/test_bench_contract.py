@@ -42,6 +42,32 @@ def test_bench_single_process_cpu():
     assert lines[0]["config"]["closing_barrier"] == "none (1 rank)"
 
 
+def test_bench_same_run_baseline_cpu():
+    """The headline's same-run baseline (the reference loop on torch) fills ``vs_baseline``."""
+    env = dict(os.environ, DGT_QUIET="1")
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--steps", "40", "--warmup", "5",
+                        "--force-baselines", "--baseline-steps", "30"],
+                       cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = _json_lines(r.stdout)[-1]
+    _check(d, 1, 40, 5)
+    b = d["baseline"]
+    assert b["impl"] == "engine" and b["steps"] == 30 and b["warmup"] == 20 and b["iters_per_s"] > 0
+    assert abs(d["vs_baseline"] - d["global_steps_per_sec"] / b["iters_per_s"]) < 0.02 * d["vs_baseline"] + 0.01
+    assert d["baselines"] == {}  # no secondary block on the CPU, so no secondary baseline either
+
+
+def test_attach_baselines_keys():
+    import bench
+    sec = {"bf16_mlp": {"iters_per_s": 1500.0}, "fp32_engine_mlp": {"error": "x"}}
+    bench.attach_baselines(sec, {"headline": {"iters_per_s": 2.0, "impl": "engine"},
+                                 "bf16_mlp": {"iters_per_s": 750.0, "impl": "torch-autocast-bf16"},
+                                 "fp32_engine_mlp": {"iters_per_s": 10.0, "impl": "torch-fp32"}})
+    assert sec["bf16_mlp"]["torch_baseline_iters_per_s"] == 750.0 and sec["bf16_mlp"]["speedup"] == 2.0
+    assert sec["bf16_mlp"]["torch_baseline_impl"] == "torch-autocast-bf16"
+    assert "speedup" not in sec["fp32_engine_mlp"]
+
+
 def test_bench_two_ranks_gloo_cpu():
     env = dict(os.environ, DGT_QUIET="1", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",

@@ -1110,3 +1110,78 @@ def test_eager_direct_backward_with_torch_bce():
     with pytest.raises(RuntimeError, match="second time"):
         engine.backward(loss)
     engine.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", ["ds_graph.json", "ds_graph_fused.json", "ds_zero1_graph.json", "ds_graph_module.json",
+                                  "ds_zero0.json", "ds_fused_linear.json"])
+def test_shipped_configs_take_their_fast_paths(name):
+    """Each shipped config on the reference loop (bench.py's DgtEngineBench: gather, forward, the
+    framework's BCE, backward, step) engages the path it is for -- a silent eager fallback (e.g. on a
+    torch without the graph internals, compat.py) fails here: whole-step graph replays for
+    ``hip_graph``, graphed-tail steps for ``graph_module``, direct backwards for the eager configs."""
+    import json
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    import bench
+    from distributed_gpu_test_amd.data import make_synthetic_data
+    from distributed_gpu_test_amd.models import SimpleNet
+    cfg = json.load(open(os.path.join(root, "configs", name)))
+    torch.manual_seed(42)
+    x, y = make_synthetic_data(2000, 20, 42)
+    tr = bench.DgtEngineBench(SimpleNet(20, 64), x, y, 4, torch.device("cuda", 0), cfg)
+    plan, counts = tr.epoch_plan(1)
+    tr.run_plan(plan[:30], counts[:30])
+    torch.cuda.synchronize()
+    e = tr.engine
+    amd = cfg.get("amd", {})
+    if amd.get("hip_graph"):
+        assert e.graphed is not None and e.graphed.replays > 0 and not e.graphed.failed, \
+            (e.graph_fallback_reason, getattr(e.graphed, "failed", None))
+    elif amd.get("graph_module"):
+        assert e.graph_module and e.tail_steps > 0, (e.graph_module_reason, e.tail_reason)
+    else:
+        assert e.direct_backwards == 30, e.direct_backwards
+    assert float(tr.loss_acc.item()) > 0
+    tr.close()
+
+
+@pytest.mark.gpu
+def test_graph_module_dropout_draws_fresh_masks():
+    """a graph that consumes RNG (dropout) is replayed, not re-launched with its captured
+    arguments: every step draws a new mask and the generator advances (graph_module.rng_checked)."""
+    torch.manual_seed(0)
+    m = torch.nn.Sequential(torch.nn.Linear(16, 64), torch.nn.Dropout(0.5), torch.nn.Linear(64, 1))
+    e, _, _, _ = dgt.initialize(model=m, config={"train_batch_size": 8, "amd": {"graph_module": True},
+                                                 "optimizer": {"type": "Adam", "params": {"lr": 0.0}}})
+    x = torch.randn(8, 16, device="cuda")
+    y = torch.ones(8, 1, device="cuda")
+    crit = torch.nn.BCEWithLogitsLoss()
+    outs = []
+    for _ in range(6):
+        s0 = torch.cuda.get_rng_state()
+        out = e(x)
+        outs.append(out.detach().clone())
+        e.backward(crit(out, y))
+        e.step()
+        assert not torch.equal(s0, torch.cuda.get_rng_state())  # the generator moved
+    assert e._graphed_fwd, e.graph_module_reason
+    # lr 0: same weights every step, so any change of the output is a new dropout mask
+    assert len({tuple(o.view(-1).tolist()) for o in outs[2:]}) == len(outs[2:])
+    e.close()
+
+
+@pytest.mark.gpu
+def test_fused_linear_refuses_inplace_modified_input():
+    """the fused Linear nodes hold their input and weights as attributes; an in-place
+    change between forward and backward raises, as autograd's saved-tensor check would."""
+    m = _mlp(3)
+    e, _, _, _ = dgt.initialize(model=m, config={"train_batch_size": 32})
+    assert e.fused_linear_layers == 2
+    x, y = _batches(1)[0]
+    out = e(x)
+    x.mul_(2.0)
+    with pytest.raises(RuntimeError, match="modified by an inplace operation"):
+        e.backward(torch.nn.functional.binary_cross_entropy_with_logits(out, y))
+    e.close()

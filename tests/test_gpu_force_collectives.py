@@ -6,7 +6,8 @@ ZeRO knob of the DeepSpeed config (``train.py:82``).  Paths covered (tests/force
 the engine's bucketed async all-reduce / reduce-scatter + all-gather (eager and inside a captured
 HIP graph on the native communicator), the MLP trainer's overlap / serial / flat schedules at
 ZeRO-0 and ZeRO-1 (side comm and optimizer streams, per-layer events), and the tiny trainer's
-graph and stepwise RCCL fallbacks."""
+graph and stepwise RCCL fallbacks, and the engine's fused-chain SyntheticMLP (bf16 MFMA and fp32) with
+per-layer buckets launched from inside the chain's backward (the overlap of VERDICT r5 item 1)."""
 import json
 import os
 import subprocess
@@ -26,7 +27,11 @@ def test_forced_collectives_bit_identical_on_one_gpu():
                        env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-4000:]
     res = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][len("RESULT "):])
-    assert len(res) == 12, sorted(res)
+    assert len(res) == 16, sorted(res)
     for name, v in res.items():
         assert v["equal"], (name, v)
         assert v["calls"] > v["calls_off"], (name, v)  # the forced run really issued its collectives
+        if name.startswith("engine_mlp_"):
+            # one bucket per layer, each launched from inside the fused chain's backward
+            assert v["fused_layers_forced"] == 4 and v["buckets_forced"] == 4, (name, v)
+            assert v["layer_notifications_forced"] >= 6 * 8, (name, v)
