@@ -1297,6 +1297,10 @@ std::unique_ptr<DirectLaunch> direct_plan(uintptr_t graph_handle, int device) {
   return plan;
 }
 
+namespace dgt {
+void bucket_launcher_submit(int64_t h, int64_t bi);  // bucket_launcher.cpp
+}
+
 PYBIND11_MODULE(_C, m) {
   m.doc() = "dgt hot-path ops without the dispatcher (same C++ functions as torch.ops.dgt)";
   m.def("gather_rows", [](const at::Tensor& idx, const std::vector<at::Tensor>& srcs) { return gather_rows(idx, srcs); });
@@ -1306,6 +1310,7 @@ PYBIND11_MODULE(_C, m) {
   m.def("linear2_fwd", &linear2_fwd);
   m.def("linear2_bwd", &linear2_bwd);
   m.def("adam_flat", &adam_flat);
+  m.def("bucket_launcher_submit", &dgt::bucket_launcher_submit);
   pybind11::class_<DirectLaunch>(m, "DirectLaunch")
       .def("__call__", &DirectLaunch::launch)
       .def_property_readonly("kernels", [](const DirectLaunch& d) { return d.nodes.size(); });

@@ -99,4 +99,44 @@ hipError_t oneshot_allreduce(const float* in, float* out, long long n, float sca
   return hipGetLastError();
 }
 
+// ---- bf16 -> fp32 widening of a gradient bucket onto its fp32 wire buffer (bucket_launcher.cpp):
+// 8 elements (16 B in, 32 B out) per lane per iteration, grid-stride; a scalar tail / unaligned path.
+__global__ __launch_bounds__(256) void widen_bf16_kernel(const unsigned short* __restrict__ src,
+                                                          float* __restrict__ dst, long long n, int vec) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  long long i = blockIdx.x * (long long)blockDim.x + threadIdx.x;
+  long long done = 0;
+  if (vec) {
+    const long long n8 = n >> 3;
+    const uint4* s8 = reinterpret_cast<const uint4*>(src);
+    float4* d4 = reinterpret_cast<float4*>(dst);
+    for (long long k = i; k < n8; k += stride) {
+      const uint4 v = s8[k];
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+      float o[8];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[2 * j] = __uint_as_float(w[j] << 16);
+        o[2 * j + 1] = __uint_as_float(w[j] & 0xffff0000u);
+      }
+      d4[2 * k] = make_float4(o[0], o[1], o[2], o[3]);
+      d4[2 * k + 1] = make_float4(o[4], o[5], o[6], o[7]);
+    }
+    done = n8 << 3;
+  }
+  for (long long k = done + i; k < n; k += stride) dst[k] = __uint_as_float((unsigned)src[k] << 16);
+}
+
+hipError_t widen_bf16_f32(const void* src, float* dst, long long n, hipStream_t stream) {
+  if (n <= 0) return hipSuccess;
+  const int vec = ((reinterpret_cast<uintptr_t>(src) | reinterpret_cast<uintptr_t>(dst)) & 31) == 0;
+  const long long work = vec ? (n >> 3) : n;
+  long long blocks = (work + 255) / 256;
+  if (blocks > 4096) blocks = 4096;  // grid-stride beyond 16 blocks per CU
+  if (blocks < 1) blocks = 1;
+  hipLaunchKernelGGL(widen_bf16_kernel, dim3((unsigned)blocks), dim3(256), 0, stream,
+                     static_cast<const unsigned short*>(src), dst, n, vec);
+  return hipGetLastError();
+}
+
 }  // namespace dgt

@@ -292,4 +292,8 @@ struct GatherArgs {
 };
 hipError_t gather_rows(const GatherArgs& a, int n_out, hipStream_t stream);
 
+// comm.hip: dst[i] = float(src[i]) for a bf16 src (the gradient bucket's wire cast to fp32), n
+// elements, 16-byte vectors where both pointers allow.
+hipError_t widen_bf16_f32(const void* src, float* dst, long long n, hipStream_t stream);
+
 }  // namespace dgt

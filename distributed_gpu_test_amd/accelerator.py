@@ -12,6 +12,7 @@ Two implementations: ``hip`` (AMD Instinct through PyTorch-ROCm, whose device na
 from __future__ import annotations
 
 import os
+import threading
 from typing import Optional
 
 import torch
@@ -111,6 +112,93 @@ def set_wait_mode(mode: str) -> bool:
     if rc != 0:
         raise RuntimeError(f"hipSetDeviceFlags({mode}) failed with HIP error {rc}")
     return True
+
+
+def _current_cpu() -> "int | None":
+    """The CPU this thread last ran on (/proc/self/task/<tid>/stat field 39), or None."""
+    try:
+        tid = threading.get_native_id()
+        with open(f"/proc/self/task/{tid}/stat") as f:
+            fields = f.read().rsplit(")", 1)[1].split()
+        return int(fields[36])  # (fields after the comm: state is field 3, processor is field 39)
+    except (OSError, ValueError, IndexError):
+        return None
+
+
+def pin_host_thread(local_rank: int = 0, local_world_size: int = 1) -> "int | None":
+    """Pin the calling thread to ONE CPU of its allowed set (``"amd": {"pin_host_thread": true}`` /
+    ``DGT_PIN_HOST_THREAD=1``).  A host-bound engine step (a whole-step graph: ~18 us of host enqueue
+    per ~19.5 us of device time) runs 19.4-25.7 us/step from process to process unpinned -- the
+    thread's slow steps are scheduler hiccups (host enqueue p90 36-50 us against 18-20) -- and
+    19.5-19.7 pinned (profiles/r6_engine_graph_variance.txt).  One rank: the CPU it runs on now (the
+    scheduler's NUMA placement kept); N ranks per node: spread evenly over the allowed set so no two
+    ranks share a core.  Only this thread is pinned (``sched_setaffinity`` of its own tid): threads
+    that already exist (the HIP runtime's, RCCL's) keep their set, but threads and processes this
+    thread starts LATER inherit the one CPU -- create a multi-worker DataLoader first, or leave the
+    option off.  Returns the CPU, or None if nothing was pinned."""
+    try:
+        allowed = sorted(os.sched_getaffinity(0))
+    except (AttributeError, OSError):
+        return None
+    if not allowed:
+        return None
+    if local_world_size > 1:
+        cpu = allowed[(local_rank * len(allowed)) // local_world_size]
+    else:
+        cpu = _current_cpu()
+        if cpu not in allowed:
+            cpu = allowed[0]
+    try:
+        os.sched_setaffinity(threading.get_native_id(), {cpu})
+    except OSError:
+        return None
+    return cpu
+
+
+_CONCURRENT: dict = {}
+
+
+def concurrent_stream(device, tries: int = 8):
+    """A stream of torch's pool that runs BESIDE the device's current stream: (stream, probed_ok).
+
+    HIP maps a process's streams onto at most GPU_MAX_HW_QUEUES (4 here) hardware queues, round
+    robin; two streams on one queue run strictly in turn, so a side stream that happens to share the
+    compute stream's queue overlaps nothing (profiles/r6_engine_overlap_trace_v3.txt: every kernel of
+    both streams on queue 1).  A stream of its own queue class -- another priority, or a CU mask --
+    does get a queue of its own, but a fifth queue oversubscribes the hardware scheduler, which then
+    time-slices: every kernel of the process ran ~2.5x longer (profiles/r6_reducer_launch_ab.txt).
+    There is no API that names a stream's queue, so this MEASURES it: the current stream is held by
+    a ~4 ms spin kernel and an event is recorded on a candidate stream; a candidate whose event
+    completes while the spin still runs sits on another queue.  The first such candidate is kept
+    (per device, once per process); if none is found, the last candidate comes back with False."""
+    import torch
+    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    hit = _CONCURRENT.get(key)
+    if hit is not None:
+        return hit
+    import time
+    dev = torch.device("cuda", key)
+    cur = torch.cuda.current_stream(dev)
+    cand = None
+    found = False
+    for _ in range(tries):
+        cand = torch.cuda.Stream(device=dev)
+        torch.cuda.synchronize(dev)
+        spin_done = torch.cuda.Event()
+        mark = torch.cuda.Event()
+        with torch.cuda.stream(cur):
+            torch.cuda._sleep(8_000_000)  # ~4 ms at ~2 GHz
+            spin_done.record(cur)
+        mark.record(cand)
+        t0 = time.perf_counter()
+        while not mark.query() and time.perf_counter() - t0 < 0.003:
+            pass
+        found = mark.query() and not spin_done.query()
+        torch.cuda.synchronize(dev)
+        if found:
+            break
+    _CONCURRENT[key] = (cand, found)
+    return cand, found
 
 
 _ACCEL = None

@@ -106,6 +106,10 @@ class AMDConfig:
     # one GPU, injected kernels that STORE their first gradient writes: skip the step's zero fill of
     # the gradient bucket (the next backward overwrites it; engine.py "Deferred zeroing")
     defer_zero_grad: bool = True
+    # pin the engine's host thread to one CPU (accelerator.pin_host_thread): a host-bound graphed step
+    # then keeps its rate from process to process (profiles/r6_engine_graph_variance.txt).  Opt-in:
+    # threads / processes the pinned thread starts later inherit the CPU.  DGT_PIN_HOST_THREAD=1 too
+    pin_host_thread: bool = False
 
 
 @dataclass
@@ -238,7 +242,8 @@ def parse_config(config: Union[str, os.PathLike, Dict[str, Any], None], world_si
                     graph_tail=bool(a.get("graph_tail", True)),
                     graph_bind_inputs=bool(a.get("graph_bind_inputs", True)),
                     direct_backward=bool(a.get("direct_backward", True)),
-                    defer_zero_grad=bool(a.get("defer_zero_grad", True)))
+                    defer_zero_grad=bool(a.get("defer_zero_grad", True)),
+                    pin_host_thread=bool(a.get("pin_host_thread", False)))
     if amd.allreduce not in ("auto", "rccl", "oneshot"):
         raise ConfigError(f"amd.allreduce={amd.allreduce!r}: expected auto|rccl|oneshot")
 

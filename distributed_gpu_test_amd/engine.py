@@ -112,6 +112,12 @@ class Engine:
             device = get_accelerator().device()
         self.device = device
         self.dtype = _DTYPES[config.compute_dtype]
+        self.host_cpu = None  # the CPU the host thread is pinned to (amd.pin_host_thread), if any
+        if device.type == "cuda" and (config.amd.pin_host_thread
+                                      or os.environ.get("DGT_PIN_HOST_THREAD", "0") not in ("", "0")):
+            from .accelerator import pin_host_thread
+            info = comm.rank_info()
+            self.host_cpu = pin_host_thread(info.local_rank, info.local_world_size)
         self.module = model.to(device=device, dtype=self.dtype)
         self.fused_linear_layers = 0
         fused_linear = config.amd.fused_linear
@@ -180,7 +186,8 @@ class Engine:
         self.reducer = GradReducer(self.store.grad_buf, self.layout, self.stage, self.world_size, self.rank,
                                    comm_dtype=comm_dtype, oneshot=self.oneshot,
                                    oneshot_max_bytes=config.amd.oneshot_max_bytes,
-                                   debug_sync=config.amd.debug_sync_streams)
+                                   debug_sync=config.amd.debug_sync_streams,
+                                   native_comm=self._native_reducer_comm(config))
         # ---- module forward/backward from HIP graphs under the eager API (amd.graph_module)
         self.graph_module = bool(config.amd.graph_module and device.type == "cuda")
         # deferred zeroing needs a writer that STORES gradients (the bf16 MFMA chain, the fp32 fused
@@ -234,6 +241,9 @@ class Engine:
         self._deferred_active = False
         self._hook_zeroed = 0  # views zeroed by that hook in the current backward
         self._grad_norm: Optional[torch.Tensor] = None
+        # a whole-step graph (graph_step) ran last and left its gradients in the flat bucket: the next
+        # eager backward zeroes it first (runtime/graph_step.py GraphedStep._done)
+        self._grads_stale = False
         self._boundary_pending = False
         self.training = True
         self.graphed = None
@@ -288,6 +298,18 @@ class Engine:
         lookup = {id(p): n for n, p in self.module.named_parameters()}
         return [lookup.get(id(p), f"param{i}") for i, p in enumerate(params)]
 
+    def _native_reducer_comm(self, config):
+        """A native RCCL communicator for the reducer's C++ bucket launcher (parallel/reducer.py), when
+        the buckets go over RCCL and there is more than one of them.  Every rank takes the same
+        decision (the same config and layout), then all of them bootstrap it together."""
+        from .parallel.reducer import _thread_default
+        if not (self.device.type == "cuda" and comm.collectives_on(self.world_size) and comm.backend_name() == "nccl"
+                and _thread_default() and not config.amd.debug_sync_streams and len(self.layout.buckets) > 1
+                and os.environ.get("DGT_REDUCER_NATIVE", "1") != "0"):
+            return None
+        from .parallel.rccl import RcclComm
+        return RcclComm(self.device)
+
     def _maybe_oneshot(self):
         from .parallel.ipc import IpcChannel, ipc_disabled_by_env
         if ipc_disabled_by_env() or self.world_size > 8:
@@ -325,6 +347,16 @@ class Engine:
         self.store.zero_grad()
         self._grads_dirty = False
         self._zero_deferred = False
+        self._grads_stale = False
+
+    def _sync_client_lr(self) -> float:
+        """The lr of the next update: a client torch optimizer's own param group, which the user (or
+        their scheduler) may change between steps, else the engine's."""
+        g = self.optimizer.param_groups[0]
+        c = self.client_optimizer
+        if c is not None and not isinstance(c, FlatAdamOptimizer):
+            g["lr"] = float(c.param_groups[0]["lr"])
+        return g["lr"]
 
     def _zero_after_step(self) -> None:
         if self._stored_all and self._defer_capable:
@@ -558,8 +590,7 @@ class Engine:
             return False
         runner, dz = found
         g = self.optimizer.param_groups[0]
-        if self.client_optimizer is not None and not isinstance(self.client_optimizer, FlatAdamOptimizer):
-            g["lr"] = float(self.client_optimizer.param_groups[0]["lr"])
+        self._sync_client_lr()
         if g["lr"] != runner.tail_lr:
             self.tail_reason = "the lr changed since the tail was captured"
             return False
@@ -593,6 +624,8 @@ class Engine:
     def backward(self, loss: torch.Tensor, retain_graph: bool = False) -> torch.Tensor:
         if self._tail_done:
             raise RuntimeError("engine.backward called twice without engine.step() after a graphed-tail step")
+        if self._grads_stale:
+            self.zero_grad()
         if self._try_graphed_tail(loss, retain_graph):
             return loss
         loss = self.faults.maybe_corrupt_loss(loss, self.global_steps)
@@ -824,8 +857,7 @@ class Engine:
                 self.skipped_steps += 1
                 self._finish_step(skipped=True)
                 return
-        if self.client_optimizer is not None and not isinstance(self.client_optimizer, FlatAdamOptimizer):
-            self.optimizer.param_groups[0]["lr"] = float(self.client_optimizer.param_groups[0]["lr"])
+        self._sync_client_lr()
         coef = self._clip_coef(grads, scale)
         g = self.optimizer.param_groups[0]
         with tracing.range("dgt.adam"):
@@ -1050,6 +1082,7 @@ class Engine:
         for h in self._hooks:
             h.remove()
         self._hooks = []
+        self.reducer.close()
         if self.oneshot is not None:
             self.oneshot.close()
             self.oneshot = None

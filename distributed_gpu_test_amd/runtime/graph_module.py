@@ -27,6 +27,7 @@ signature before that runs eagerly instead of overwriting the first one's activa
 """
 from __future__ import annotations
 
+import gc
 from typing import Callable, List, Optional, Sequence, Tuple
 
 import torch
@@ -101,13 +102,28 @@ def rng_checked(graph: "torch.cuda.CUDAGraph", direct, install: Callable[[Callab
     return first
 
 
+def _setter(obj, attr: str):
+    """``install`` for rng_checked that holds ``obj`` weakly: a strong reference from the callable
+    stored on ``obj`` back to ``obj`` would be a cycle, and a cycle holding HIP graphs is freed by the
+    garbage collector whenever it runs -- possibly inside another graph's capture, where destroying a
+    graph aborts the process.  Without the cycle the graphs go when their owner does."""
+    import weakref
+    ref = weakref.ref(obj)
+
+    def install(f) -> None:
+        o = ref()
+        if o is not None:
+            setattr(o, attr, f)
+    return install
+
+
 class _capture:
     """``torch.cuda.graph`` without its ``gc.collect()`` + ``empty_cache()`` on entry: emptying the
     caching allocator moves every later allocation, so the addresses bound graphs were captured for
     (``bind_inputs``) would never come back.  Captures on one side stream per device, ordered
     after and before the caller's stream."""
 
-    __slots__ = ("graph", "pool", "stream", "ctx")
+    __slots__ = ("graph", "pool", "stream", "ctx", "gc_was_on")
 
     def __init__(self, graph: "torch.cuda.CUDAGraph", pool):
         self.graph, self.pool = graph, pool
@@ -120,13 +136,24 @@ class _capture:
         self.stream.wait_stream(torch.cuda.current_stream())
         self.ctx = torch.cuda.stream(self.stream)
         self.ctx.__enter__()
-        self.graph.capture_begin(pool=self.pool)
+        # no garbage collection while capturing: a collected cycle that owns HIP graphs, events or
+        # streams (any user object) would destroy them mid-capture, which aborts the process
+        self.gc_was_on = gc.isenabled()
+        gc.disable()
+        try:
+            self.graph.capture_begin(pool=self.pool)
+        except BaseException:
+            if self.gc_was_on:
+                gc.enable()
+            raise
         return self
 
     def __exit__(self, *exc):
         try:
             self.graph.capture_end()
         finally:
+            if self.gc_was_on:
+                gc.enable()
             self.ctx.__exit__(*exc)
             torch.cuda.current_stream().wait_stream(self.stream)
         return False
@@ -215,7 +242,7 @@ class GraphedModule:
         self.static_gin = gs[len(self.params):]
         self.bwd.instantiate()
         self.bwd_direct = direct_launcher(self.bwd, may_hold_collective=False)  # (the reducer runs outside)
-        self.bwd_replay = rng_checked(self.bwd, self.bwd_direct, lambda f: setattr(self, "bwd_replay", f))
+        self.bwd_replay = rng_checked(self.bwd, self.bwd_direct, _setter(self, "bwd_replay"))
         # The graphed tail: the same backward followed by ``tail()`` (the engine's gradient
         # collective, clip coefficient, fused Adam, ZeRO-1 all-gather and the bucket's zero fill) in
         # ONE graph, replayed by Engine.backward when the loss is one it can differentiate itself
@@ -237,13 +264,12 @@ class GraphedModule:
         self.single = torch.is_tensor(out) or len(out) == 1
         # (bound C methods: no Python wrapper frame per step)
         # (a graph that draws random numbers is always replayed: rng_checked)
-        self.fwd_replay = rng_checked(self.fwd, self.fwd_direct, lambda f: setattr(self, "fwd_replay", f))
+        self.fwd_replay = rng_checked(self.fwd, self.fwd_direct, _setter(self, "fwd_replay"))
         self.tail_replay = None
         if self.bwd_tail is not None:
             self.bwd_tail.instantiate()
             self.tail_direct = direct_launcher(self.bwd_tail)
-            self.tail_replay = rng_checked(self.bwd_tail, self.tail_direct,
-                                           lambda f: setattr(self, "tail_replay", f))
+            self.tail_replay = rng_checked(self.bwd_tail, self.tail_direct, _setter(self, "tail_replay"))
         self.replays = 0
         self.pending = False  # a replayed forward whose backward has not run yet
         self.held = None  # bound inputs of the pending forward: alive (and unmoved) until its backward

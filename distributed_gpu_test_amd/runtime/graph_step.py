@@ -26,6 +26,8 @@ steps of the same body (allocator / library warm-up before capture), then is cap
 """
 from __future__ import annotations
 
+import gc
+import weakref
 from typing import Callable, Dict, Optional, Tuple
 
 import torch
@@ -128,6 +130,8 @@ class GraphedStep:
         # the Adam step counter the captured launch reads (the step number of THIS update, 1-based)
         self.step_dev = torch.full((), engine.global_steps - engine.skipped_steps, dtype=torch.int64,
                                    device=engine.device)
+        self._step_host = engine.global_steps - engine.skipped_steps  # what step_dev holds (no sync)
+        self.lr = engine._sync_client_lr()  # the lr the captured Adam launches carry
         self.step_ticket = torch.zeros((), dtype=torch.int32, device=engine.device)  # (Adam advances step_dev)
         self.pool = torch.cuda.graph_pool_handle()
         self.graphs: Dict[tuple, tuple] = {}  # shape key -> (graph, static inputs, static loss)
@@ -183,8 +187,36 @@ class GraphedStep:
         return seed
 
     # ------------------------------------------------------------------ public
+    def _sync(self) -> int:
+        """Before any step of this callable.  Eager steps of the same engine (``engine(x)`` /
+        ``backward`` / ``step``) may have run since the last one: the device step counter the
+        captured Adam reads is re-filled from the engine's count when its host mirror disagrees, and
+        the client optimizer's lr is read (Engine.step does the same) -- a different lr than the one
+        baked into the captured launches drops the graphs (they are recaptured at the new lr).
+        Returns the update number this step performs minus one."""
+        e = self.e
+        want = e.global_steps - e.skipped_steps
+        if want != self._step_host:
+            self.step_dev.fill_(want)
+        lr = e._sync_client_lr()
+        if lr != self.lr:
+            self.lr = lr
+            self._last = None
+            self.launchers.clear()
+            self.graphs.clear()
+        return want
+
+    def _done(self, want: int) -> None:
+        e = self.e
+        self._step_host = want + 1  # the step's Adam advanced the device counter
+        # the flat bucket now holds this step's gradients (the graph leaves them in place): the
+        # engine's next eager backward starts from a zeroed buffer
+        e._grads_stale = True
+        e._finish_graph_step()
+
     def __call__(self, *args) -> torch.Tensor:
         e = self.e
+        want = self._sync()
         last = self._last  # the common case: one tensor argument of last step's signature
         if last is not None and len(args) == 1 and torch.is_tensor(args[0]):
             a = args[0]
@@ -193,7 +225,7 @@ class GraphedStep:
                 static_in[0].copy_(a, non_blocking=True)
                 last[3]()
                 self.replays += 1
-                e._finish_graph_step()
+                self._done(want)
                 return static_loss
         key = tuple((tuple(a.shape), a.dtype) if torch.is_tensor(a) else ("py", a) for a in args)
         entry = self.graphs.get(key)
@@ -203,7 +235,7 @@ class GraphedStep:
                 self.seen[key] = n + 1
                 loss = self._body(*args, key=key)
                 self.eager_steps += 1
-                e._finish_graph_step()
+                self._done(want)
                 return loss
             try:
                 entry = self._capture(key, args)
@@ -215,7 +247,7 @@ class GraphedStep:
                 torch.cuda.synchronize(e.device)
                 loss = self._body(*args)
                 self.eager_steps += 1
-                e._finish_graph_step()
+                self._done(want)
                 return loss
         graph, static_in, static_loss = entry
         for dst, src in zip(static_in, args):
@@ -227,7 +259,7 @@ class GraphedStep:
         if len(args) == 1 and torch.is_tensor(args[0]):
             self._last = (args[0].shape, args[0].dtype, entry, run)
         self.replays += 1
-        e._finish_graph_step()
+        self._done(want)
         return static_loss
 
     def _capture(self, key, args):
@@ -236,14 +268,22 @@ class GraphedStep:
         graph = torch.cuda.CUDAGraph(keep_graph=True)
         # capture records the launches without running them: the step counter advance is replayed,
         # not double-counted
-        with torch.cuda.graph(graph, pool=self.pool):
-            static_loss = self._body(*static_in, key=key, capturing=True)
+        gc_on = gc.isenabled()
+        try:
+            with torch.cuda.graph(graph, pool=self.pool):  # (collects garbage first, then captures)
+                gc.disable()  # nothing collected mid-capture (graph_module._capture)
+                static_loss = self._body(*static_in, key=key, capturing=True)
+        finally:
+            if gc_on:
+                gc.enable()
         graph.instantiate()
         from .graph_module import direct_launcher, rng_checked  # a short chain of kernels: launched, not replayed
         launcher = direct_launcher(graph)
         if launcher is not None:
             # (first call replays; a graph drawing random numbers stays on replay: rng_checked)
-            self.launchers[key] = rng_checked(graph, launcher, lambda f, key=key: self._install(key, f))
+            ref = weakref.ref(self)  # (no cycle through the stored callable: graph_module._setter)
+            self.launchers[key] = rng_checked(graph, launcher,
+                                              lambda f, key=key: ref() is not None and ref()._install(key, f))
         entry = (graph, static_in, static_loss)
         self.graphs[key] = entry
         return entry

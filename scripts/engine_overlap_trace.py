@@ -45,6 +45,9 @@ def run(steps: int = 12) -> None:
     e = tr.engine
     print(json.dumps({"steps": steps, "buckets": [[b.start, b.numel, b.params] for b in e.layout.buckets],
                       "layer_notifications": e.layer_notifications, "fused_layers": e.fused_linear_layers,
+                      "thread_launches": e.reducer.thread_launches, "native_launches": e.reducer.native_launches,
+                      "reducer_thread": e.reducer.launch_thread, "native": e.reducer.native is not None,
+                      "side_concurrent": e.reducer.side_concurrent,
                       "bytes_reduced": e.reducer.bytes_reduced}), flush=True)
     tr.close()
     comm.destroy()
@@ -78,11 +81,14 @@ def analyze(path: str) -> None:
         print(f"  stream {r['Stream_Id']:>3} {(r['t0'] - t_base) / 1e3:8.1f} .. {(r['t1'] - t_base) / 1e3:8.1f}  "
               f"{r['Kernel_Name'][:45]:45s}  during {where}")
     last_bwd_gemm_end = max(r["t1"] for r in bwd) if bwd else None
-    coll = [r for r in other if "rocclr" in r["Kernel_Name"] or "nccl" in r["Kernel_Name"].lower()]
+    # RCCL's kernels (a 1-rank in-place all-reduce launches none) and the wire casts the reducer issues
+    # on the side stream immediately before each bucket's collective (the collective's launch point)
+    coll = [r for r in other if "rocclr" in r["Kernel_Name"] or "nccl" in r["Kernel_Name"].lower()
+            or "elementwise" in r["Kernel_Name"]]
     if coll and last_bwd_gemm_end is not None:
         first = min(r["t0"] for r in coll)
         before = sum(1 for r in coll if r["t0"] < last_bwd_gemm_end)
-        print(f"first collective kernel at {(first - t_base) / 1e3:.1f} us; last backward GEMM ends at "
+        print(f"first collective-stream kernel at {(first - t_base) / 1e3:.1f} us; last backward GEMM ends at "
               f"{(last_bwd_gemm_end - t_base) / 1e3:.1f} us; {before} of {len(coll)} collective kernels start before "
               f"it -> overlap {'YES' if first < last_bwd_gemm_end else 'NO'}")
 

@@ -28,7 +28,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--steps", type=int, default=4000)
     ap.add_argument("--config", default=os.path.join(ROOT, "configs", "ds_graph_fused.json"))
-    ap.add_argument("--pin", type=int, default=None)
+    ap.add_argument("--pin", type=int, default=None, help="pin the process to this CPU before anything else")
+    ap.add_argument("--unpinned", action="store_true", help="the config's amd.pin_host_thread turned off")
     a = ap.parse_args()
     if a.pin is not None:
         os.sched_setaffinity(0, {a.pin})
@@ -41,7 +42,10 @@ def main():
     comm.init_distributed()
     torch.manual_seed(42)
     x, y = make_synthetic_data(2000, 20, 42)
-    tr = bench.DgtEngineBench(SimpleNet(20, 64), x, y, 4, torch.device("cuda", 0), json.load(open(a.config)))
+    cfg = json.load(open(a.config))
+    if a.unpinned:
+        cfg.setdefault("amd", {})["pin_host_thread"] = False
+    tr = bench.DgtEngineBench(SimpleNet(20, 64), x, y, 4, torch.device("cuda", 0), cfg)
     plan, counts = bench.build_plan(tr, a.steps + 200)
     tr.run_plan(plan[:200], counts[:200])
     torch.cuda.synchronize()
@@ -79,7 +83,8 @@ def main():
     f1.record()
     torch.cuda.synchronize()
     dev_only = f0.elapsed_time(f1) / 1e3
-    out = {"config": os.path.basename(a.config), "impl": tr.impl, "pin": a.pin, "steps": n,
+    out = {"config": os.path.basename(a.config), "impl": tr.impl, "pin": a.pin, "engine_pin": tr.engine.host_cpu,
+           "steps": n,
            "iters_per_s": round(n / wall, 1), "us_per_step": round(1e6 * wall / n, 2),
            "host_enqueue_us_mean": round(1e6 * sum(host) / n, 2),
            "host_enqueue_us_p50": round(1e6 * host[n // 2], 2), "host_enqueue_us_p90": round(1e6 * host[int(n * 0.9)], 2),
@@ -87,7 +92,7 @@ def main():
            "device_span_us_per_step": round(1e6 * dev / n, 2),
            "device_only_us_per_step": round(1e6 * dev_only / len(half), 2),
            "enqueue_ahead_us_per_step": round(1e6 * (q1 - q0) / len(half), 2),
-           "cpu": os.sched_getaffinity(0).__len__()}
+           "cpus_allowed": len(os.sched_getaffinity(0))}
     print(json.dumps(out), flush=True)
     tr.close()
     comm.destroy()

@@ -111,7 +111,8 @@ def engine_mlp_case(dtype, stage):
             engine.step()
         p = engine.store.param_buf.detach().float().clone()
         extra = {"layer_notifications": engine.layer_notifications, "buckets": len(engine.layout.buckets),
-                 "fused_layers": engine.fused_linear_layers}
+                 "fused_layers": engine.fused_linear_layers, "thread_launches": engine.reducer.thread_launches + engine.reducer.native_launches,
+                 "native": engine.reducer.native is not None}
         engine.close()
         return p, extra
     return fn

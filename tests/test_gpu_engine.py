@@ -1130,12 +1130,17 @@ def test_shipped_configs_take_their_fast_paths(name):
     cfg = json.load(open(os.path.join(root, "configs", name)))
     torch.manual_seed(42)
     x, y = make_synthetic_data(2000, 20, 42)
-    tr = bench.DgtEngineBench(SimpleNet(20, 64), x, y, 4, torch.device("cuda", 0), cfg)
-    plan, counts = tr.epoch_plan(1)
-    tr.run_plan(plan[:30], counts[:30])
-    torch.cuda.synchronize()
+    mask = os.sched_getaffinity(0)
+    try:
+        tr = bench.DgtEngineBench(SimpleNet(20, 64), x, y, 4, torch.device("cuda", 0), cfg)
+        plan, counts = tr.epoch_plan(1)
+        tr.run_plan(plan[:30], counts[:30])
+        torch.cuda.synchronize()
+    finally:
+        os.sched_setaffinity(0, mask)  # (the graph configs pin the host thread: not the rest of the suite)
     e = tr.engine
     amd = cfg.get("amd", {})
+    assert (e.host_cpu is not None) == bool(amd.get("pin_host_thread")), e.host_cpu
     if amd.get("hip_graph"):
         assert e.graphed is not None and e.graphed.replays > 0 and not e.graphed.failed, \
             (e.graph_fallback_reason, getattr(e.graphed, "failed", None))
@@ -1185,3 +1190,24 @@ def test_fused_linear_refuses_inplace_modified_input():
     with pytest.raises(RuntimeError, match="modified by an inplace operation"):
         e.backward(torch.nn.functional.binary_cross_entropy_with_logits(out, y))
     e.close()
+
+
+@pytest.mark.gpu
+def test_concurrent_stream_runs_beside_the_current_stream():
+    """accelerator.concurrent_stream: a pool stream measured to sit on a hardware queue other than the
+    current stream's -- an event recorded on it completes while a spin kernel holds the current stream."""
+    import time
+    from distributed_gpu_test_amd.accelerator import concurrent_stream
+    s, ok = concurrent_stream(torch.device("cuda", 0))
+    assert ok and s is not None
+    assert concurrent_stream(torch.device("cuda", 0))[0] is s  # cached per device
+    torch.cuda.synchronize()
+    spin, mark = torch.cuda.Event(), torch.cuda.Event()
+    torch.cuda._sleep(8_000_000)
+    spin.record()
+    mark.record(s)
+    t0 = time.perf_counter()
+    while not mark.query() and time.perf_counter() - t0 < 0.003:
+        pass
+    assert mark.query() and not spin.query()
+    torch.cuda.synchronize()

@@ -47,7 +47,7 @@ def _pool(X, Y, sizes, per_size, rnd):
     return pool
 
 
-def _fuzz(seed: int, mode: str, steps: int = STEPS, mutate=None):
+def _fuzz(seed: int, mode: str, steps: int = STEPS, mutate=None, check_every: int = 50):
     """Returns the list of (step, max abs diff, allowed) at each checkpoint; raises on mismatch."""
     from distributed_gpu_test_amd.models import SimpleNet
     from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
@@ -78,6 +78,7 @@ def _fuzz(seed: int, mode: str, steps: int = STEPS, mutate=None):
     micro = 0
     checks = []
     counts = {"whole": 0, "retain": 0, "user_grad": 0, "lr": 0, "torch_bce": 0}
+    hist = []  # (step, what it did): the failure message carries the last few
     for s in range(steps):
         window_start = micro % gas == 0
         if window_start and rnd.random() < 0.05:  # lr change (the client optimizer's, read each step)
@@ -91,10 +92,12 @@ def _fuzz(seed: int, mode: str, steps: int = STEPS, mutate=None):
         if whole is not None and rnd.random() < 0.5:
             whole(x, y)  # forward + backward + Adam as one replay
             counts["whole"] += 1
+            hist.append((s, f"whole B={b}"))
             ref_loss = torch.nn.functional.binary_cross_entropy_with_logits(ref(x), y)
             ref_opt.zero_grad(set_to_none=True)
             ref_loss.backward()
             ref_opt.step()
+            ref_opt.zero_grad(set_to_none=True)
             micro += 1
         else:
             user_grad = window_start and rnd.random() < 0.06
@@ -111,6 +114,7 @@ def _fuzz(seed: int, mode: str, steps: int = STEPS, mutate=None):
             counts["retain"] += int(retain)
             engine.backward(loss, retain_graph=retain)
             engine.step()
+            hist.append((s, f"eager B={b} torch_bce={use_torch} retain={retain} user_grad={user_grad} lr={lr}"))
             ref_loss = torch.nn.functional.binary_cross_entropy_with_logits(ref(x), y)
             (ref_loss / gas).backward(retain_graph=retain)
             micro += 1
@@ -118,7 +122,7 @@ def _fuzz(seed: int, mode: str, steps: int = STEPS, mutate=None):
                 ref_opt.step()
                 ref_opt.zero_grad(set_to_none=True)
             del loss
-        if (s + 1) % 50 == 0 or s + 1 == steps:
+        if (s + 1) % check_every == 0 or s + 1 == steps:
             torch.cuda.synchronize()
             got = torch.cat([p.detach().reshape(-1) for p in model.parameters()])
             want = torch.cat([p.detach().reshape(-1) for p in ref_params])
@@ -128,7 +132,7 @@ def _fuzz(seed: int, mode: str, steps: int = STEPS, mutate=None):
             if not checks[-1][2]:
                 engine.close()
                 raise AssertionError(f"seed {seed} mode {mode}: parameters left torch's trajectory by step {s + 1} "
-                                     f"(max |diff| {checks[-1][1]:.3g}); transitions {counts}")
+                                     f"(max |diff| {checks[-1][1]:.3g}); transitions {counts}; last ops {hist[-6:]}")
     stats = {"counts": counts, "tail_steps": engine.tail_steps, "direct_backwards": engine.direct_backwards,
              "graph_module": engine.graph_module, "evictions": sum(f.evictions for f in engine._graphed_fwd.values()),
              "bound": sum(len(f.bound) for f in engine._graphed_fwd.values()),
@@ -150,8 +154,7 @@ def test_engine_fuzz_matches_torch(mode, seed):
         assert st["evictions"] > 0 or st["bound"] > 0, st
     elif mode == "whole_step":
         assert st["whole_replays"] > 0 and st["direct_backwards"] > 0, st
-    else:
-        assert st["direct_backwards"] > 0, st
+    # (gas2: the 1/gas-scaled loss takes autograd's path, not the direct backward)
 
 
 def test_fuzz_catches_defer_bug():
@@ -167,3 +170,24 @@ def test_fuzz_catches_defer_bug():
         except AssertionError:
             failed += 1
     assert failed > 0, "the fuzz did not notice deferred zeroing under graph_module"
+
+
+def test_fuzz_catches_whole_step_counter_bug(monkeypatch):
+    """Round 6: the whole-step graph's device step counter was never re-synced after eager steps of
+    the same engine (Adam's bias correction then used a stale step).  With the re-sync disabled the
+    fuzz must fail."""
+    from distributed_gpu_test_amd.runtime import graph_step
+    orig = graph_step.GraphedStep._sync
+
+    def stale(self):
+        self._step_host = self.e.global_steps - self.e.skipped_steps  # "in sync": never re-filled
+        return orig(self)
+
+    monkeypatch.setattr(graph_step.GraphedStep, "_sync", stale)
+    failed = 0
+    for seed in SEEDS:
+        try:
+            _fuzz(seed, "whole_step")
+        except AssertionError:
+            failed += 1
+    assert failed > 0, "the fuzz did not notice a stale whole-step step counter"

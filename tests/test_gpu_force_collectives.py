@@ -35,3 +35,5 @@ def test_forced_collectives_bit_identical_on_one_gpu():
             # one bucket per layer, each launched from inside the fused chain's backward
             assert v["fused_layers_forced"] == 4 and v["buckets_forced"] == 4, (name, v)
             assert v["layer_notifications_forced"] >= 6 * 8, (name, v)
+            # every bucket went out from the reducer's native launcher thread (csrc/bucket_launcher.cpp)
+            assert v["native_forced"] and v["thread_launches_forced"] == 6 * 4, (name, v)

@@ -245,3 +245,19 @@ def test_train_py_model_mlp_engine_path(tmp_path):
     l = epoch_losses(r.stdout)
     assert len(l) == 2 and l[1] < l[0]
     assert (tmp_path / "e" / "epoch2" / "global_step8" / "mp_rank_00_model_states.pt").exists()
+
+
+def test_reducer_launcher_thread_matches_inline():
+    """The gradient reducer's launcher thread (parallel/reducer.py) issues every bucket's collective
+    from one side thread in notification order: the reduced gradients are bit-identical to launching
+    on the backward thread, at stage 0 and 1, with and without a wire-dtype cast; buckets follow the
+    layers (a layer's weight and bias share one)."""
+    r = run(2, script="tests/reducer_thread_worker.py")
+    assert r.returncode == 0, r.stderr[-3000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][7:])
+    assert len(res) == 4
+    for k, v in res.items():
+        assert v["equal"], (k, v)
+        assert v["thread_launches"] == 3 * v["buckets"] and v["inline_thread_launches"] == 0, (k, v)
+        assert all(sorted(p) in ([0, 1], [2, 3], [4, 5], [6, 7], [4, 5, 6, 7], [2, 3, 4, 5, 6, 7])
+                   for p in v["bucket_params"]), v["bucket_params"]
