@@ -158,8 +158,10 @@ def pin_host_thread(local_rank: int = 0, local_world_size: int = 1) -> "int | No
 _CONCURRENT: dict = {}
 
 
-def concurrent_stream(device, tries: int = 8):
+def concurrent_stream(device, tries: int = 8, slot: int = 0):
     """A stream of torch's pool that runs BESIDE the device's current stream: (stream, probed_ok).
+    ``slot``: independent users (the engine's reducer 0, the MLP trainer's comm 1 / optimizer 2
+    streams) get streams of their own.
 
     HIP maps a process's streams onto at most GPU_MAX_HW_QUEUES (4 here) hardware queues, round
     robin; two streams on one queue run strictly in turn, so a side stream that happens to share the
@@ -170,14 +172,15 @@ def concurrent_stream(device, tries: int = 8):
     There is no API that names a stream's queue, so this MEASURES it: the current stream is held by
     a ~4 ms spin kernel and an event is recorded on a candidate stream; a candidate whose event
     completes while the spin still runs sits on another queue.  The first such candidate is kept
-    (per device, once per process); if none is found, the last candidate comes back with False."""
+    (per device and slot, once per process); if none is found, the last candidate comes back with False."""
     import torch
-    key = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    idx = torch.device(device).index if torch.device(device).index is not None else torch.cuda.current_device()
+    key = (idx, slot)
     hit = _CONCURRENT.get(key)
     if hit is not None:
         return hit
     import time
-    dev = torch.device("cuda", key)
+    dev = torch.device("cuda", idx)
     cur = torch.cuda.current_stream(dev)
     cand = None
     found = False

@@ -250,8 +250,11 @@ class MLPTrainer:
             self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
             self.ev_opt = [torch.cuda.Event() for _ in range(self.L)]
         if self._overlap:
-            self.s_opt = torch.cuda.Stream(dev)
-            self.s_comm = torch.cuda.Stream(dev)
+            # side streams measured to sit on hardware queues other than the compute stream's (two
+            # streams on one queue run in turn: accelerator.concurrent_stream)
+            from ..accelerator import concurrent_stream
+            self.s_comm = concurrent_stream(dev, slot=1)[0]
+            self.s_opt = concurrent_stream(dev, slot=2)[0]
             self.ev_wgrad = [torch.cuda.Event() for _ in range(self.L)]
             self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
             self.ev_comm = [torch.cuda.Event() for _ in range(self.L)]

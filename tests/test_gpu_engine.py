@@ -1211,3 +1211,38 @@ def test_concurrent_stream_runs_beside_the_current_stream():
         pass
     assert mark.query() and not spin.query()
     torch.cuda.synchronize()
+
+
+@pytest.mark.gpu
+def test_graph_module_retained_fused_bce_backward_twice():
+    """with graph_module the fused BCE writes d loss / d logits into the backward graph's
+    static input; a scaled (gas = 2) backward under retain_graph copies dz * g over it.  A second
+    backward through the retained graph must still read the unscaled dz (the BCE keeps a private copy)."""
+    from distributed_gpu_test_amd.models import SimpleNet
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+    torch.manual_seed(3)
+    m = SimpleNet(20, 64)
+    ref = copy.deepcopy(m).cuda()
+    e, _, _, _ = dgt.initialize(model=m, optimizer=torch.optim.Adam(m.parameters(), lr=1e-3),
+                                config={"train_micro_batch_size_per_gpu": 8, "gradient_accumulation_steps": 2,
+                                        "amd": {"graph_module": True}})
+    ropt = torch.optim.Adam(ref.parameters(), lr=1e-3)
+    x = torch.randn(8, 20, device="cuda")
+    y = (torch.rand(8, 1, device="cuda") > 0.5).float()
+    crit = BCEWithLogitsLoss()
+    for _ in range(3):  # (the first forwards capture; later ones replay and claim the gout buffer)
+        loss = crit(e(x), y)
+        e.backward(loss, retain_graph=True)
+        e.step()
+        e.backward(loss)
+        e.step()
+        rl = torch.nn.functional.binary_cross_entropy_with_logits(ref(x), y)
+        (rl / 2).backward(retain_graph=True)
+        (rl / 2).backward()
+        ropt.step()
+        ropt.zero_grad(set_to_none=True)
+    assert e._graphed_fwd, e.graph_module_reason
+    got = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    want = torch.cat([p.detach().reshape(-1) for p in ref.parameters()])
+    torch.testing.assert_close(got, want, rtol=1e-4, atol=1e-6)
+    e.close()
