@@ -171,6 +171,38 @@ def test_flat_layout_buckets_and_shards():
     assert sum(n for _, n in lay.shard_ranges(2)) == lay.shard_numel()
 
 
+def test_flat_layout_units_keep_layers_whole():
+    """Round 6: a layer's weight and bias never straddle buckets; a layer bigger than the bucket size is
+    a bucket of its own (bias included) -- one collective per layer, launched when the layer is done."""
+    import pytest
+    shapes = [(4096, 4096), (4096,)] * 4 + [(1, 4096), (1,)]
+    units = [[0, 1], [2, 3], [4, 5], [6, 7], [8, 9]]
+    lay = FlatLayout(shapes, bucket_elems=8 << 20, units=units)
+    assert [b.params for b in lay.buckets] == [[0, 1], [2, 3], [4, 5], [6, 7], [8, 9]]
+    per_param = FlatLayout(shapes, bucket_elems=8 << 20)  # (the old per-parameter grouping)
+    assert len(per_param.buckets) > len(lay.buckets)  # biases were singleton buckets
+    # small layers still share a bucket, in backward order
+    small = FlatLayout([(8, 4), (8,), (8, 8), (8,), (1, 8), (1,)], bucket_elems=1 << 20, units=[[0, 1], [2, 3], [4, 5]])
+    assert [b.params for b in small.buckets] == [[0, 1, 2, 3, 4, 5]]
+    with pytest.raises(ValueError):
+        FlatLayout(shapes, 1 << 20, units=[[0, 1], [2, 3]])  # units must cover every parameter
+
+
+def test_engine_layer_units_follow_modules():
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.engine import Engine
+    from distributed_gpu_test_amd.config import parse_config
+    m = SyntheticMLP(64, 3)
+    e = Engine(m, parse_config({"train_batch_size": 4, "zero_optimization": {"reduce_bucket_size": 1024}}, 1),
+               device=torch.device("cpu"))
+    names = dict(enumerate(e.param_names))
+    for b in e.layout.buckets:
+        owners = {names[i].rsplit(".", 1)[0] for i in b.params}
+        for o in owners:  # every bucket holds whole modules: weight and bias together
+            assert all(names[i].rsplit(".", 1)[0] != o or i in b.params for i in names)
+    e.close()
+
+
 def test_schedules_and_loss_scaler():
     s = WarmupLR(warmup_min_lr=0.0, warmup_max_lr=1.0, warmup_num_steps=10, warmup_type="linear")
     vals = [s.step() for _ in range(12)]
