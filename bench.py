@@ -336,9 +336,9 @@ def baseline_specs(args, device, world: int):
     return [("headline", "reference loop: PyTorch eager SimpleNet + torch.optim.Adam + RCCL all-reduce + per-step "
              "loss.item() (train.py:104-117), fp32, micro-batch 4", headline, args.baseline_steps, 20),
             ("bf16_mlp", "PyTorch-ROCm: SyntheticMLP(4096, 4) bf16 autocast (hipBLASLt) + fused torch Adam"
-             + (" + DDP" if world > 1 else ""), mlp(4096, True), 50, 20),
+             + (" + DDP" if world > 1 else ""), mlp(4096, True), 100, 20),
             ("fp32_engine_mlp", "PyTorch-ROCm: SyntheticMLP(1024, 4) fp32 (hipBLASLt) + fused torch Adam"
-             + (" + DDP" if world > 1 else ""), mlp(1024, False), 100, 20)]
+             + (" + DDP" if world > 1 else ""), mlp(1024, False), 200, 20)]
 
 
 def attach_baselines(secondary: dict, baselines: dict) -> None:

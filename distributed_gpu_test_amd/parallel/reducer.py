@@ -278,6 +278,7 @@ class GradReducer:
             torch.cuda.set_device(dev)  # (the current device is per thread)
         while True:
             item = q.get()
+            r = None
             try:
                 if item is None:
                     return
