@@ -246,7 +246,8 @@ class MLPTrainer:
         self._v_fwd = int(os.environ.get("DGT_MLP_FWD_VARIANT", "0") or 0)
         self._v_wgrad = int(os.environ.get("DGT_MLP_WGRAD_VARIANT", "0") or 0)
         if self._wga_side:
-            self.s_opt = torch.cuda.Stream(dev)
+            from ..accelerator import concurrent_stream  # (its own hardware queue: see the overlap schedule)
+            self.s_opt = concurrent_stream(dev, slot=2)[0]
             self.ev_bwd = [torch.cuda.Event() for _ in range(self.L)]
             self.ev_opt = [torch.cuda.Event() for _ in range(self.L)]
         if self._overlap:
