@@ -170,7 +170,7 @@ def concurrent_stream(device, tries: int = 8, slot: int = 0):
     does get a queue of its own, but a fifth queue oversubscribes the hardware scheduler, which then
     time-slices: every kernel of the process ran ~2.5x longer (profiles/r6_reducer_launch_ab.txt).
     There is no API that names a stream's queue, so this MEASURES it: the current stream is held by
-    a ~4 ms spin kernel and an event is recorded on a candidate stream; a candidate whose event
+    a ~8 ms spin kernel and an event is recorded on a candidate stream; a candidate whose event
     completes while the spin still runs sits on another queue.  The first such candidate is kept
     (per device and slot, once per process); if none is found, the last candidate comes back with False."""
     import torch
@@ -190,11 +190,11 @@ def concurrent_stream(device, tries: int = 8, slot: int = 0):
         spin_done = torch.cuda.Event()
         mark = torch.cuda.Event()
         with torch.cuda.stream(cur):
-            torch.cuda._sleep(8_000_000)  # ~4 ms at ~2 GHz
+            torch.cuda._sleep(16_000_000)  # ~8 ms at ~2 GHz
             spin_done.record(cur)
         mark.record(cand)
         t0 = time.perf_counter()
-        while not mark.query() and time.perf_counter() - t0 < 0.003:
+        while not mark.query() and time.perf_counter() - t0 < 0.005:
             pass
         found = mark.query() and not spin_done.query()
         torch.cuda.synchronize(dev)

@@ -11,7 +11,9 @@ tail -2 $O/pytest.log
 timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > $O/smoke.log 2>&1 || { tail -20 $O/smoke.log; exit 1; }
 grep "smoke ok" $O/smoke.log
 for i in 1 2 3; do
+  t0=$(date +%s.%N)
   timeout -k 10 300 python bench.py --gpus 1 --steps 20 --warmup 5 > $O/bench_$i.json 2> $O/bench_$i.err || { tail -20 $O/bench_$i.err; exit 1; }
+  echo "bench wall $(python -c "import time; print(round(time.time() - $t0, 1))") s"
   python - $O/bench_$i.json <<'PY'
 import json, sys
 d = json.loads([l for l in open(sys.argv[1]) if l.startswith("{")][-1])

@@ -1203,11 +1203,11 @@ def test_concurrent_stream_runs_beside_the_current_stream():
     assert concurrent_stream(torch.device("cuda", 0))[0] is s  # cached per device
     torch.cuda.synchronize()
     spin, mark = torch.cuda.Event(), torch.cuda.Event()
-    torch.cuda._sleep(8_000_000)
+    torch.cuda._sleep(16_000_000)
     spin.record()
     mark.record(s)
     t0 = time.perf_counter()
-    while not mark.query() and time.perf_counter() - t0 < 0.003:
+    while not mark.query() and time.perf_counter() - t0 < 0.005:
         pass
     assert mark.query() and not spin.query()
     torch.cuda.synchronize()
