@@ -9,7 +9,9 @@
 #include <torch/library.h>
 
 #include <cstdlib>
+#include <map>
 #include <memory>
+#include <mutex>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -704,17 +706,44 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
   TORCH_CHECK(reinterpret_cast<uintptr_t>(t.data_ptr()) % 16 == 0, "dgt: ", name, " must be 16-byte aligned");
 }
 
+// Workspace of the split-K GEMM (gemm.hip, variant 9): per (device, stream), so launches that may
+// run concurrently never share a partial slab or a ticket.  Tensors from the caching allocator (a
+// first use inside a graph capture allocates from the graph's pool; the map keeps it alive); the
+// ticket words start at zero and every launch leaves them at zero.
+struct SkWorkspace {
+  at::Tensor slab, flags;
+};
+std::mutex g_sk_mu;
+std::map<std::pair<int, hipStream_t>, SkWorkspace> g_sk_ws;
+
+void attach_sk_workspace(dgt::GemmArgs& g, const at::Tensor& like, hipStream_t stream) {
+  const int64_t tiles = (int64_t)(g.M / 256) * (g.N / 128);
+  std::lock_guard<std::mutex> lock(g_sk_mu);
+  SkWorkspace& w = g_sk_ws[{(int)like.device().index(), stream}];
+  if (!w.slab.defined() || w.slab.numel() < tiles * 256 * 128) {
+    w.slab = at::empty({tiles * 256 * 128}, like.options().dtype(at::kFloat));
+    w.flags = at::zeros({tiles * 4}, like.options().dtype(at::kInt));
+  }
+  g.sk_slab = w.slab.data_ptr<float>();
+  g.sk_flags = w.flags.data_ptr<int>();
+  static const int xs = [] {
+    const char* e = std::getenv("DGT_GEMM_SK_XS");
+    return (e && *e) ? std::atoi(e) : 1;
+  }();
+  g.sk_xs = xs;
+}
+
 void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& C,
              const std::optional<at::Tensor>& CT, const std::optional<at::Tensor>& bias,
              const std::optional<at::Tensor>& mask, int64_t epi, double alpha, int64_t variant,
              const std::optional<at::Tensor>& colsum) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || (variant != 2 && variant != 8),
               "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK(variant >= 0 && variant <= 8,
+  TORCH_CHECK(variant >= 0 && variant <= 9,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
               "fragment reads), 4 (128x128, 4 stages, 8 waves), 5 (software-pipelined reads), 6 / 7 (register "
-              "prefetch, 2 / 4 K-tiles) or 8 (256x256 with cross-phase fragment prefetch); the round-2 "
-              "variants live in git history (commit c0371a5)");
+              "prefetch, 2 / 4 K-tiles), 8 (256x256 with cross-phase fragment prefetch) or 9 (256x128 split-K "
+              "2); the round-2 variants live in git history (commit c0371a5)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
@@ -775,7 +804,14 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
   c10::DeviceGuard guard(A.device());
   if (variant == 2 || variant == 8)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
-  DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream_of(A), (int)variant));
+  const hipStream_t stream = stream_of(A);
+  if (dgt::gemm_nt_uses_sk(g, (int)epi, (int)variant)) {
+    TORCH_CHECK(dgt::gemm_nt_sk_fits(g, (int)epi),
+                "dgt: the split-K gemm (variant 9) needs M % 256 == 0, N % 128 == 0, K % 128 == 0, a multiple of 8 "
+                "256x128 tiles and a bf16 (staged) epilogue");
+    attach_sk_workspace(g, A, stream);
+  }
+  DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream, (int)variant));
 }
 
 // wgrad + Adam in one launch: the weight gradient alpha * A . B^T ([M, N], never stored) updates the

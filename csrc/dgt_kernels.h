@@ -189,11 +189,19 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   float alpha;
   GemmAdam adam;       // kEpiAdam only (the gradient is alpha * A . B^T; ldc = row stride of the weight)
   float* colsum;       // kEpiColSum: fp32 [M / 128, N]
-  float* sk_slab;      // diag split-K kernel only (removed; git history c0371a5): fp32 partial tiles
-  int* sk_flags;       // diag split-K kernel only: 2 ints per tile (arrivals, slab ready)
+  float* sk_slab;      // split-K kernel (variant 9): fp32 256 x 128 partial per tile (two 128-row halves)
+  int* sk_flags;       // split-K kernel: 4 ints per tile (ticket, partial ready per 128-row half), zero
+                       // between launches
+  int sk_xs;           // split-K kernel: bit 0 = a tile's two K halves on neighbouring XCDs (else one XCD);
+                       // bits 1-2: timing diagnostics (gemm.hip), wrong results
 };
 
 hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream, int variant = 0);
+// the split-K kernel's shape rule (256 x 128 tiles, a multiple of 8 of them, K % 128 == 0, staged
+// bf16 epilogue); the caller provides sk_slab / sk_flags for (M / 256) * (N / 128) tiles
+bool gemm_nt_sk_fits(const GemmArgs& g, int epilogue);
+// whether gemm_nt(g, epilogue, ., variant) runs the split-K kernel (needs its workspace)
+bool gemm_nt_uses_sk(const GemmArgs& g, int epilogue, int variant);
 hipError_t transpose_bf16(const void* in, void* out, int rows, int cols, hipStream_t stream);
 // out (fp32, or bf16 when out_bf16) [rows] (+)= row sums of a bf16 [rows, cols] matrix
 hipError_t rowsum_bf16(const void* in, void* out, int out_bf16, int rows, int cols, int accumulate,

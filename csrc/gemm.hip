@@ -21,6 +21,7 @@
 #include <hip/hip_bf16.h>
 
 #include <algorithm>
+#include <cstdlib>
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 
@@ -28,6 +29,7 @@ namespace dgt {
 
 typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef unsigned short u16;
+typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
 
 constexpr int GBM = 128, GBN = 128, GBK = 64;
 
@@ -345,27 +347,73 @@ DGT_DEVICE void epilogue_adam(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN 
   }
 }
 
-template <int EPI, int TM, int TN, int WM, int WN, int NT>
-DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN / 16], u16* tile, int m0, int n0,
-                                int wr, int wc, int l, int tid) {
-  __syncthreads();  // every wave has finished reading the operand stages
+// What the staged epilogue reads from memory, loadable ahead: the bias of a wave's WN / 16
+// accumulator columns (nb + 16 j + (l & 15)) and the ReLU-mask chunks of the thread's C-row passes.
+// Read where they are used, each load's latency is exposed in turn (a vmcnt(0) after each: the
+// compiler cannot move a mask load above the previous pass's C store).
+template <int EPI, int TM, int TN, int WN, int NT>
+struct EpiPre {
+  static constexpr int NB = WN / 16, CPR = TN / 8;
+  static constexpr int NMK = (EPI & kEpiMask) ? TM * CPR / NT : 1;
+  float bn[NB];
+  uint4 mk[NMK];
+  DGT_DEVICE void load_bias(const GemmArgs& g, int nb, int l) {
+    if constexpr ((EPI & kEpiBias) != 0) {
+      if (g.bias_bf16) {
+        const u16* b = static_cast<const u16*>(g.bias) + nb + (l & 15);
 #pragma unroll
-  for (int j = 0; j < WN / 16; ++j) {
+        for (int j = 0; j < NB; ++j) bn[j] = bf2f(b[16 * j]);
+      } else {
+        const float* b = static_cast<const float*>(g.bias) + nb + (l & 15);
+#pragma unroll
+        for (int j = 0; j < NB; ++j) bn[j] = b[16 * j];
+      }
+    } else {
+#pragma unroll
+      for (int j = 0; j < NB; ++j) bn[j] = 0.f;
+    }
+  }
+  DGT_DEVICE void load_mask(const GemmArgs& g, int m0, int n0, int tid) {
+    if constexpr ((EPI & kEpiMask) != 0) {
+      const u16* mask = static_cast<const u16*>(g.mask);
+#pragma unroll
+      for (int it = 0; it < NMK; ++it) {
+        const int idx = tid + NT * it, r = idx / CPR, c = (idx % CPR) * 8;
+        mk[it] = *reinterpret_cast<const uint4*>(mask + (long long)(m0 + r) * g.ldmask + n0 + c);
+      }
+    }
+  }
+};
+
+// PRE: the bias and mask come from `pre` (loaded ahead by the split-K kernel); otherwise they are
+// read here, where used (the 128 x 128 / 256 x 256 kernels: issuing them ahead of the K loop, or
+// batched at the epilogue, measured no faster in the MLP step -- 1,406-1,413 vs 1,411-1,417 iters/s,
+// scripts/sessions/gpu_r6_epi.sh)
+template <int EPI, int TM, int TN, int WM, int WN, int NT, bool PRE = false>
+DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][WN / 16], u16* tile, int m0, int n0,
+                                int wr, int wc, int l, int tid, const EpiPre<EPI, TM, TN, WN, NT>& pre,
+                                bool own = true) {
+  __syncthreads();  // every wave has finished reading the operand stages
+  // (own = false: this wave holds none of the tile's accumulators -- the split-K kernel's half
+  // epilogue -- and only joins the store passes)
+#pragma unroll
+  for (int j = 0; j < WN / 16 && own; ++j) {
     const int nl = wc * WN + j * 16 + (l & 15);
-    const float bn = (EPI & kEpiBias) ? bias_at(g, n0 + nl) : 0.f;
+    float bnj;
+    if constexpr (PRE) bnj = pre.bn[j];
+    else bnj = (EPI & kEpiBias) ? bias_at(g, n0 + nl) : 0.f;
 #pragma unroll
     for (int i = 0; i < WM / 16; ++i) {
       const int ml = wr * WM + i * 16 + 4 * (l >> 4);
 #pragma unroll
       for (int rr = 0; rr < 4; ++rr) {
-        float x = acc[i][j][rr] * g.alpha + bn;
+        float x = acc[i][j][rr] * g.alpha + bnj;
         if (EPI & kEpiRelu) x = fmaxf(x, 0.f);
         tile[etile<TN>(ml + rr, nl)] = f2bf(x);
       }
     }
   }
   __syncthreads();
-  const u16* mask = static_cast<const u16*>(g.mask);
   u16* C = static_cast<u16*>(g.C);
   constexpr int CPR = TN / 8;  // 16-byte chunks per row
   if ((EPI & kEpiMask) || C) {
@@ -373,8 +421,10 @@ DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][W
     for (int it = 0; it < TM * CPR / NT; ++it) {
       const int idx = tid + NT * it, r = idx / CPR, c = (idx % CPR) * 8;
       uint4 v = *reinterpret_cast<const uint4*>(tile + etile<TN>(r, c));
-      if (EPI & kEpiMask) {
-        const uint4 mk = *reinterpret_cast<const uint4*>(mask + (long long)(m0 + r) * g.ldmask + n0 + c);
+      if constexpr ((EPI & kEpiMask) != 0) {
+        uint4 mk;
+        if constexpr (PRE) mk = pre.mk[it];
+        else mk = *reinterpret_cast<const uint4*>(static_cast<const u16*>(g.mask) + (long long)(m0 + r) * g.ldmask + n0 + c);
         unsigned* vw = reinterpret_cast<unsigned*>(&v);
         const unsigned* mw = reinterpret_cast<const unsigned*>(&mk);
 #pragma unroll
@@ -407,7 +457,7 @@ DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][W
     u16* CT = static_cast<u16*>(g.CT);
     constexpr int CPC = TM / 8;  // 8-row chunks per column
     static_assert(CPC % 16 == 0 && NT % 64 == 0, "C^T read mapping: 16-chunk blocks per wave");
-    static_assert(!(EPI & kEpiColSum) || CPC == 16, "column sums: one 16-chunk block (128 rows) per column");
+    static_assert(!(EPI & kEpiColSum) || CPC == 16 || CPC == 32, "column sums: per 128-row block of the tile");
 #pragma unroll
     for (int it = 0; it < TN * CPC / NT; ++it) {
       // a wave reads 4 columns x 16 row chunks; each 32-lane half 4 columns x 8 row chunks
@@ -429,7 +479,8 @@ DGT_DEVICE void epilogue_staged(const GemmArgs& g, const f32x4 (&acc)[WM / 16][W
         cs += __shfl_xor(cs, 2);
         cs += __shfl_xor(cs, 4);
         cs += __shfl_xor(cs, 32);
-        if ((q & 0x27) == 0) g.colsum[(long long)(m0 / TM) * g.N + n0 + n] = cs;
+        // (a 256-row tile: sub >> 6 picks the 128-row half, one partial row each)
+        if ((q & 0x27) == 0) g.colsum[(long long)(m0 / 128 + (sub >> 6)) * g.N + n0 + n] = cs;
       }
     }
   }
@@ -709,7 +760,8 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
     epilogue_adam<GBM, GBN, 64, WN, 64 * NW, GBM>(g, acc, reinterpret_cast<float*>(&lds[0][0][0]), m0, n0, wr, wc, l,
                                                   tid);
   } else if constexpr (!(EPI & kEpiOutF32)) {
-    epilogue_staged<EPI, GBM, GBN, 64, WN, 64 * NW>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
+    epilogue_staged<EPI, GBM, GBN, 64, WN, 64 * NW>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid,
+                                                    EpiPre<EPI, GBM, GBN, WN, 64 * NW>{});
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -717,6 +769,199 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       for (int j = 0; j < NJ; ++j)
         epi_store<EPI>(g, acc[i][j], m0 + wr * 64 + i * 16 + 4 * (l >> 4), n0 + wc * WN + j * 16 + (l & 15));
   }
+}
+
+// ------------------------------------------------------------------ 256 x 128 tile, split-K 2 (SK)
+// For products whose 128 x 128 grid is one block per CU (the MLP's M = 1024 forward and dgrad at
+// N = K = 4096): each CU there streams 2 MiB of operands at the chip's ~13 TB/s L2 -> CU rate
+// (profiles/r4_panel_stream.jsonl; the stage depth does not move it), so only fewer bytes per CU
+// help.  Here a block owns a 256 x 128 tile over HALF of K: 1.5 MiB per CU for the same FLOPs, and
+// 64 x 64 wave tiles (4 (M) x 2 (N) waves of 4 x 4 accumulators: 16 fragment reads per 32 MFMAs,
+// against 12 per 16 in the 128 x 128 kernel's 64 x 32 wave tiles).  M = 1024 gives 4 x 32 tiles x
+// 2 halves = 256 blocks.  The loop is the FR kernel's (asm LDS-DMA, front-loaded fragment reads,
+// counted vmcnt + raw barrier), three 48 KiB stages.
+// The halves meet in-launch (cdna_hip_programming.md §5 projection GEMM item 2, §6 Guideline 16),
+// once per 128-row half of the tile, each block taking its own row half first: a per-(tile, row
+// half) ticket says who came first; the first writes its fp32 partial of those rows (64 KiB,
+// write-through sc1 16-byte stores), drains and raises a flag; the second polls the flag (its
+// partner holds ticket 0 and publishes in that same phase: no co-residency is assumed; bounded),
+// re-arms both words for the next launch, adds the partial (sc1 loads; fp32 a + b == b + a: the sum
+// does not depend on which half came first) and runs the staged epilogue of those 128 rows.
+// Arriving together, each block finishes one row half; arriving apart, the later one finishes both.
+// sk_xs = 1 puts a tile's halves on neighbouring XCDs (each XCD's L2 then holds half of K for a
+// 4 x 8-tile region: 8 MiB of unique operands per XCD instead of 12), 0 on one XCD.
+namespace sk {
+constexpr int TM = 256, TN = 128, S = 3, NW = 8;
+constexpr int A_ELEMS = TM * GBK, STAGE = (TM + TN) * GBK;  // u16 per stage (48 KiB)
+constexpr int PER_TILE = 3 * (16 / NW);                      // LDS-DMAs per thread per K-tile (A 4, B 2)
+}  // namespace sk
+
+template <int EPI>
+__global__ __launch_bounds__(512, 1) void gemm_nt_sk_kernel(GemmArgs g) {
+  using namespace sk;
+  constexpr int BK = GBK, NJ = 4;
+  constexpr bool KN = (EPI & kEpiBKN) != 0;
+  static_assert(!(EPI & (kEpiOutF32 | kEpiAccumulate | kEpiAdam)), "SK: staged bf16 epilogues only");
+  // ONE __shared__ array: a second LDS object (even the ticket word) can make the compiler drain
+  // the DMAs before every fragment read
+  __shared__ __attribute__((aligned(16))) u16 lds[S * STAGE];
+  const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int wr = w >> 1, wc = w & 1;
+  const int MT = g.M / TM, T = MT * (g.N / TN);
+  const int xcd = blockIdx.x & 7, slot = blockIdx.x >> 3;
+  int half, t;
+  if (g.sk_xs & 1) {
+    half = xcd & 1;
+    t = (xcd >> 1) * (T / 4) + slot;
+  } else {
+    half = slot & 1;
+    t = xcd * (T / 8) + (slot >> 1);
+  }
+  const int m0 = (t % MT) * TM, n0 = (t / MT) * TN;
+  const int kh = g.K / 2, nk = kh / BK;
+  const u16* A = static_cast<const u16*>(g.A) + (long long)half * kh;
+  const u16* B = static_cast<const u16*>(g.B) + (long long)half * kh * (KN ? g.ldb : 1);
+
+  f32x4 acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  EpiPre<EPI, 128, TN, 64, 512> pre;  // the epilogue's bias, in flight during the K loop (the mask:
+  pre.load_bias(g, n0 + wc * 64, l);   // per row half, when that half's epilogue starts)
+
+  Stager<NW, false, true> sa0(A, g.lda, m0, w, l);
+  Stager<NW, false, true> sa1(A, g.lda, m0 + 128, w, l);
+  Stager<NW, KN, true> sb(B, g.ldb, n0, w, l);
+  const unsigned lds0 = __builtin_amdgcn_readfirstlane(lds_byte_addr(lds));
+  auto issue = [&](int b) {
+    const unsigned base = lds0 + (unsigned)(b * STAGE * 2);
+    sa0.issue_at(base);
+    sa1.issue_at(base + 128 * BK * 2);
+    sb.issue_at(base + A_ELEMS * 2);
+  };
+  auto compute = [&](int buf) {
+    const u16* As = lds + buf * STAGE;
+    const u16* Bs = As + A_ELEMS;
+    bf16x8 af[BK / 32][4], bfr[BK / 32][NJ];
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      const int chunk = kk * 4 + (l >> 4);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if constexpr (KN) bfr[kk][j] = read_frag_kn_fr(Bs, kk * 32, wc * 64 + j * 16, l);
+        else bfr[kk][j] = read_frag<BK>(Bs, wc * 64 + j * 16 + (l & 15), chunk);
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i) af[kk][i] = read_frag<BK>(As, wr * 64 + i * 16 + (l & 15), chunk);
+    }
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk)
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(af[kk][i], bfr[kk][j], acc[i][j], 0, 0, 0);
+    if constexpr (KN) {
+      __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * NJ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, 2, 0);
+      __builtin_amdgcn_sched_group_barrier(0x100, 4 + 2 * NJ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ - 2, 0);
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) __builtin_amdgcn_sched_group_barrier(0x100, 4 + NJ, 0);
+      __builtin_amdgcn_sched_group_barrier(0x008, (BK / 32) * 4 * NJ, 0);
+    }
+  };
+#pragma unroll
+  for (int p = 0; p < S - 1; ++p)
+    if (p < nk) issue(p);
+  int buf = 0, nb = S - 1;
+  for (int kt = 0; kt < nk; ++kt) {
+    // tiles kt and (if any) kt + 1 are in flight: retire tile kt
+    if (kt + 1 < nk) wait_vmcnt<PER_TILE>();
+    else wait_vmcnt<0>();
+    __builtin_amdgcn_sched_barrier(0);
+    __builtin_amdgcn_s_barrier();  // tile kt visible to every wave; the stage of tile kt - 1 is free
+    __builtin_amdgcn_sched_barrier(0);
+    if (kt + S - 1 < nk) issue(nb);
+    nb = (nb + 1 == S) ? 0 : nb + 1;
+    compute(buf);
+    buf = (buf + 1 == S) ? 0 : buf + 1;
+  }
+  __builtin_amdgcn_s_barrier();  // every wave is done with the operand stages
+  const int own_half = w >> 2;     // waves 4r .. 4r + 3 hold rows [128 r, 128 r + 128) of the tile
+  if (g.sk_xs & 6) {  // diag (DGT_GEMM_SK_XS bits, timing only, WRONG results): 2 = the K loop alone,
+    if (g.sk_xs & 2) return;  // 4 = each block runs the epilogue of one row half on its own partial
+    pre.load_mask(g, m0 + 128 * half, n0, tid);
+    epilogue_staged<EPI, 128, TN, 64, 64, 512, true>(g, acc, lds, m0 + 128 * half, n0, wr - 2 * half, wc, l, tid,
+                                                     pre, own_half == half);
+    return;
+  }
+
+  // ---- the halves meet, per 128-row half of the tile, own row half first
+  // (taking both tickets at once measured 8 us slower: the block arriving first then wins both
+  // halves and its partner finishes the whole tile)
+  int* order = reinterpret_cast<int*>(lds + 64 * 1024);  // past the epilogue's 32 KiB tile
+#pragma unroll 1
+  for (int ph = 0; ph < 2; ++ph) {
+    const int r = half ^ ph;
+    int* ticket = g.sk_flags + 4 * t + 2 * r;
+    int* ready = ticket + 1;
+    // the row half's partial: 64 KiB, lane-linear in the owning waves' accumulator order
+    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(g.sk_slab + (long long)(2 * t + r) * (128 * TN), 0,
+                                                         128 * TN * 4, 0x00020000);
+    if (tid == 0) order[ph] = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    const bool mine = own_half == r;
+    if (order[ph] == 0) {
+      if (mine) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
+                                                   ((i * NJ + j) * 256 + (tid & 255)) * 16, 0, 16 /* sc1 */);
+      }
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+      __syncthreads();
+      if (tid == 0) __hip_atomic_store(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      continue;
+    }
+    if (tid == 0) {
+      // the partner holds ticket 0 and publishes this half within that same phase, before it
+      // waits on anything (it can only be second on a half after publishing the other): the wait
+      // is bounded by its store pass; bounded all the same (~seconds): a lost flag yields a wrong
+      // tile, never a hung GPU
+      for (int spin = 0; spin < (1 << 22) && __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+           ++spin)
+        __builtin_amdgcn_s_sleep(1);
+      // both blocks are past their last use of the two words: re-arm them for the next launch
+      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(ready, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    // every load of the partial is an sc1 load (L1 bypassed) after the poll and a barrier: no
+    // acquire fence (MI355X_MICROARCH.md, visibility: valid forms, first row)
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    __syncthreads();
+    if (mine) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] += __builtin_bit_cast(
+              f32x4, __builtin_amdgcn_raw_buffer_load_b128(rsrc, ((i * NJ + j) * 256 + (tid & 255)) * 16, 0, 16));
+    }
+    pre.load_mask(g, m0 + 128 * r, n0, tid);
+    epilogue_staged<EPI, 128, TN, 64, 64, 512, true>(g, acc, lds, m0 + 128 * r, n0, wr - 2 * r, wc, l, tid, pre,
+                                                     mine);
+  }
+}
+
+bool gemm_nt_sk_fits(const GemmArgs& g, int epi) {
+  if (epi & (kEpiOutF32 | kEpiAccumulate | kEpiAdam)) return false;
+  if (g.M <= 0 || g.N <= 0 || g.M % sk::TM || g.N % sk::TN || g.K % (2 * GBK)) return false;
+  return ((g.M / sk::TM) * (g.N / sk::TN)) % 8 == 0;
 }
 
 // ------------------------------------------------------------------ 128 x 128, register prefetch (RP)
@@ -763,7 +1008,6 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_rp_kernel(GemmArgs g) {
     }
   }
   const long long bstep = KN ? (long long)BK * g.ldb : BK;  // elements per K-tile of B
-  typedef unsigned u32x4 __attribute__((ext_vector_type(4)));
   u32x4 rg[D][4];
   auto gload = [&](int kt, u32x4 (&r)[4]) {
 #pragma unroll
@@ -843,7 +1087,8 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_rp_kernel(GemmArgs g) {
   }
 
   if constexpr (!(EPI & kEpiOutF32)) {
-    epilogue_staged<EPI, GBM, GBN, 64, WN, 64 * NW>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid);
+    epilogue_staged<EPI, GBM, GBN, 64, WN, 64 * NW>(g, acc, &lds[0][0][0], m0, n0, wr, wc, l, tid,
+                                                    EpiPre<EPI, GBM, GBN, WN, 64 * NW>{});
   } else {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
@@ -1203,7 +1448,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
     // fp32 256 x 256 tile = 256 KiB: two passes of 128 rows through the 128 KiB of operand LDS
     epilogue_adam<BM, BN, 128, 64, 512, 128>(g, acc, reinterpret_cast<float*>(lds), m0, n0, c.wr, c.wc, c.l, tid);
   } else if constexpr (!(EPI & kEpiOutF32)) {
-    epilogue_staged<EPI, BM, BN, 128, 64, 512>(g, acc, lds, m0, n0, c.wr, c.wc, c.l, tid);
+    epilogue_staged<EPI, BM, BN, 128, 64, 512>(g, acc, lds, m0, n0, c.wr, c.wc, c.l, tid, EpiPre<EPI, BM, BN, 64, 512>{});
   } else {
 #pragma unroll
     for (int i = 0; i < 8; ++i)
@@ -1239,9 +1484,52 @@ bool launch_rp(int grid, const GemmArgs& g, hipStream_t stream, int depth) {
   }
 }
 
+// the shape rule's use of the split-K kernel: DGT_GEMM_SK=1 for one-wave 128 x 128 grids with
+// K >= 2048 and a [N, K] B (the MLP's M = 1024 forwards); the default (0) keeps the 128 x 128
+// kernels: the split-K forward with C^T is 43.5-46.2 us hot against 44.8-45.1, without C^T
+// 40.0-40.4 against 38.6-39.5, and the bf16 MLP step is no faster (profiles/r6_gemm_m1024_splitk.jsonl:
+// its K loop alone takes 32 us, a 128-row half epilogue ~4 us, the halves' meeting ~6.5 us)
+static bool sk_auto() {
+  static const int on = [] {
+    const char* e = std::getenv("DGT_GEMM_SK");
+    return (e && *e) ? std::atoi(e) : 0;
+  }();
+  return on != 0;
+}
+
+bool gemm_nt_uses_sk(const GemmArgs& g, int epi, int variant) {
+  if (variant == 9) return true;
+  // (the [K, N] dgrad stays on the software-pipelined 128 x 128 kernel: 41.9 vs 46.5-47.8 us)
+  if (variant != 0 || !sk_auto() || (epi & kEpiBKN) || !gemm_nt_sk_fits(g, epi)) return false;
+  return (g.M / GBM) * (g.N / GBN) <= 256 && g.K >= 2048;
+}
+
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 8) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 9) return hipErrorInvalidValue;
+  if (gemm_nt_uses_sk(g, epi, variant)) {
+    if (!gemm_nt_sk_fits(g, epi) || !g.sk_slab || !g.sk_flags) return hipErrorInvalidValue;
+    const int grid = 2 * (g.M / sk::TM) * (g.N / sk::TN);
+    switch (epi) {
+#define DGT_SK_CASE(E)                                                                          \
+  case E:                                                                                       \
+    hipLaunchKernelGGL((gemm_nt_sk_kernel<E>), dim3(grid), dim3(512), 0, stream, g);            \
+    return hipGetLastError();
+      DGT_SK_CASE(0)
+      DGT_SK_CASE(kEpiBias | kEpiRelu | kEpiStoreT)
+      DGT_SK_CASE(kEpiBias | kEpiRelu)
+      DGT_SK_CASE(kEpiBias | kEpiStoreT)
+      DGT_SK_CASE(kEpiBias)
+      DGT_SK_CASE(kEpiMask | kEpiStoreT)
+      DGT_SK_CASE(kEpiMask | kEpiStoreT | kEpiBKN)
+      DGT_SK_CASE(kEpiMask | kEpiStoreT | kEpiBKN | kEpiColSum)
+      DGT_SK_CASE(kEpiBKN)
+      DGT_SK_CASE(kEpiStoreT | kEpiBKN)
+#undef DGT_SK_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+  }
   // the 256x256 kernel runs the cross-phase fragment prefetch (g256::phase_x) unless variant 2 asks
   // for the 8-phase pipeline it is bitwise-checked against: 8192^3 1.51-1.52 vs 1.39-1.47 PF, the
   // MLP's wgrad 31.6-31.9 vs 33.0-33.7 us (profiles/r4_gemm256_xp.jsonl)

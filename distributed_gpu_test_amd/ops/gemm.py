@@ -58,12 +58,17 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     forward-type products, bit-identical to 3; other products keep the shape rule),
     8 = the 256x256 kernel with cross-phase fragment prefetch (phase P's MFMAs overlap the LDS
     reads of phase P + 1; bit-identical to 2) -- the kernel the shape rule runs for >= 200 tiles of
-    256x256.
+    256x256,
+    9 = 256x128 tiles with K split in two halves that meet in-launch (per-tile ticket, fp32 partial,
+    deterministic; M % 256 == 0, N % 128 == 0, K % 128 == 0, a multiple of 8 tiles, bf16 epilogues,
+    ``b_kn`` and ``colsum`` included) -- opt-in: ``DGT_GEMM_SK=1`` makes the shape rule use it for
+    one-wave NT grids with K >= 2048; on the MLP's M = 1024 products it is no faster than 3 / 5
+    (``profiles/r6_gemm_m1024_splitk.jsonl``).
     ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
     the shape rule gives to the 128x128 kernels).
 
     ``b_kn=True``: B is given as ``[K, N]`` (N contiguous) and ``C = alpha * A @ B`` — the operand is
-    staged as it lies and read with transposed LDS reads (128x128 kernels only).  ``accumulate``
+    staged as it lies and read with transposed LDS reads (128x128 and split-K kernels).  ``accumulate``
     adds into C (fp32, or bf16 summed in fp32 and rounded once).
 
     ``colsum`` (fp32 ``[M // 128, N]``, the ``[K, N]`` dgrad with ``mask`` and ``CT`` only): each

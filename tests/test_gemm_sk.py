@@ -1,0 +1,130 @@
+"""The 256x128 split-K bf16 GEMM (``csrc/gemm.hip`` gemm_nt_sk_kernel, variant 9) against a plain
+PyTorch fp32 reference of the same product + epilogue, its determinism (the two K halves meet
+through a per-tile ticket: the result must not depend on which half finished first, and every
+launch must leave the ticket words re-armed), its per-stream workspace, and its agreement with the
+unsplit 128x128 kernels it replaces on the MLP's M = 1024 products."""
+import pytest
+import torch
+
+from distributed_gpu_test_amd.ops.gemm import gemm_nt, gemm_nt_reference
+
+pytestmark = pytest.mark.gpu
+
+# (M, N, K): the tile count (M / 256) * (N / 128) must be a multiple of 8
+SHAPES = [(256, 1024, 256), (512, 512, 512), (256, 1024, 2048), (1024, 4096, 4096)]
+EPIS = ["plain", "bias_relu_T", "bias_relu", "bias_T", "bias", "mask_T",
+        "kn_plain", "kn_T", "kn_mask_T", "kn_mask_T_colsum"]
+
+
+def _operands(M, N, K, seed):
+    g = torch.Generator().manual_seed(seed)
+    A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
+    B = torch.randn(N, K, generator=g).to(torch.bfloat16).cuda()
+    Bkn = torch.randn(K, N, generator=g).to(torch.bfloat16).cuda()
+    bias = torch.randn(N, generator=g).cuda()
+    mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).cuda()
+    return A, B, Bkn, bias, mask
+
+
+def _run(epi, A, B, Bkn, bias, mask, variant):
+    M, N = A.shape[0], B.shape[0]
+    kn = epi.startswith("kn_")
+    kw = {}
+    if "bias" in epi:
+        kw["bias"] = bias
+    if "relu" in epi:
+        kw["relu"] = True
+    if "mask" in epi:
+        kw["mask"] = mask
+    C = torch.full((M, N), float("nan"), device="cuda").to(torch.bfloat16)
+    CT = torch.full((N, M), float("nan"), device="cuda").to(torch.bfloat16) if "_T" in epi else None
+    cs = torch.full((M // 128, N), float("nan"), device="cuda") if epi.endswith("colsum") else None
+    gemm_nt(A, Bkn if kn else B, C=C, CT=CT, b_kn=kn, variant=variant, colsum=cs, **kw)
+    return C, CT, cs, kw
+
+
+@pytest.mark.parametrize("M,N,K", SHAPES)
+@pytest.mark.parametrize("epi", EPIS)
+def test_gemm_sk_matches_fp32_reference(M, N, K, epi):
+    A, B, Bkn, bias, mask = _operands(M, N, K, M + N + K)
+    C, CT, cs, kw = _run(epi, A, B, Bkn, bias, mask, 9)
+    kn = epi.startswith("kn_")
+    ref = gemm_nt_reference(A, Bkn if kn else B, b_kn=kn, **kw)  # fp32 on the GPU
+    tol = dict(rtol=2e-2, atol=2e-2 * K ** 0.5)
+    torch.testing.assert_close(C.float(), ref.to(torch.bfloat16).float(), **tol)
+    if CT is not None:
+        assert torch.equal(CT, C.t()), "C^T must hold the same bf16 values as C"
+    if cs is not None:
+        want = C.float().view(M // 128, 128, N).sum(1)  # the kernel sums its own bf16 outputs
+        torch.testing.assert_close(cs, want, rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("epi", ["bias_relu_T", "kn_mask_T_colsum"])
+def test_gemm_sk_deterministic_and_rearmed(epi):
+    """Ten launches on one workspace give the same bits: which half comes first differs from launch
+    to launch, fp32 a + b == b + a, and a ticket left un-armed would make a later launch read a
+    stale partial (or wait on a flag that never rises)."""
+    A, B, Bkn, bias, mask = _operands(1024, 4096, 4096, 7)
+    first = _run(epi, A, B, Bkn, bias, mask, 9)
+    for _ in range(9):
+        again = _run(epi, A, B, Bkn, bias, mask, 9)
+        for x, y in zip(first[:3], again[:3]):
+            if x is not None:
+                assert torch.equal(x, y)
+
+
+@pytest.mark.parametrize("epi", ["bias_relu_T", "bias_relu", "kn_mask_T_colsum"])
+def test_gemm_sk_agrees_with_unsplit_kernels(epi):
+    """On the MLP's M = 1024 products the split-K sum (two fp32 half-K partials, added once) differs
+    from the 128x128 kernels' single K loop only by fp32 summation order: the bf16 outputs agree to
+    one rounding step."""
+    A, B, Bkn, bias, mask = _operands(1024, 4096, 4096, 11)
+    C9 = _run(epi, A, B, Bkn, bias, mask, 9)[0].float()
+    C5 = _run(epi, A, B, Bkn, bias, mask, 5 if epi.startswith("kn_") else 3)[0].float()
+    diff = (C9 - C5).abs()
+    assert float((diff > 0).float().mean()) < 0.05
+    assert float((diff / C5.abs().clamp_min(1.0)).max()) <= 2 ** -7
+
+
+def test_gemm_sk_two_streams_use_separate_workspaces():
+    """Two split-K products in flight on two streams at once must not share tickets or partials."""
+    A, B, Bkn, bias, mask = _operands(1024, 4096, 4096, 3)
+    A2 = torch.flip(A, dims=[0]).contiguous()
+    want1 = _run("bias_relu_T", A, B, Bkn, bias, mask, 9)[0]
+    want2 = _run("bias_relu_T", A2, B, Bkn, bias, mask, 9)[0]
+    s1, s2 = torch.cuda.Stream(), torch.cuda.Stream()
+    torch.cuda.synchronize()
+    outs = []
+    for _ in range(4):
+        with torch.cuda.stream(s1):
+            o1 = _run("bias_relu_T", A, B, Bkn, bias, mask, 9)[0]
+        with torch.cuda.stream(s2):
+            o2 = _run("bias_relu_T", A2, B, Bkn, bias, mask, 9)[0]
+        outs.append((o1, o2))
+    torch.cuda.synchronize()
+    for o1, o2 in outs:
+        assert torch.equal(o1, want1) and torch.equal(o2, want2)
+
+
+def test_gemm_sk_rejects_unfit_shapes_and_epilogues():
+    A = torch.randn(256, 256, device="cuda").bfloat16()
+    B = torch.randn(512, 256, device="cuda").bfloat16()  # 1 x 4 = 4 tiles: not a multiple of 8
+    with pytest.raises(RuntimeError, match="split-K"):
+        gemm_nt(A, B, C=torch.empty(256, 512, device="cuda").bfloat16(), variant=9)
+    B = torch.randn(1024, 256, device="cuda").bfloat16()
+    with pytest.raises(RuntimeError, match="split-K"):  # fp32 output: not a staged bf16 epilogue
+        gemm_nt(A, B, C=torch.empty(256, 1024, device="cuda"), out_f32=True, variant=9)
+
+
+def test_gemm_shape_rule_keeps_the_unsplit_kernels_by_default():
+    """The split-K kernel is opt-in (DGT_GEMM_SK=1): on the MLP's M = 1024 products it measured
+    slower than the 128x128 kernels (profiles/r6_gemm_m1024_splitk.jsonl), so variant 0 gives the
+    unsplit kernels' bits -- and variant 9's under DGT_GEMM_SK=1."""
+    import os
+    if os.environ.get("DGT_GEMM_VARIANT"):
+        pytest.skip("variant forced by the environment")
+    A, B, Bkn, bias, mask = _operands(1024, 4096, 4096, 5)
+    sk = os.environ.get("DGT_GEMM_SK", "0") not in ("", "0")
+    for epi, unsplit in [("bias_relu_T", 3), ("kn_mask_T_colsum", 5)]:
+        want = _run(epi, A, B, Bkn, bias, mask, 9 if sk else unsplit)[0]
+        assert torch.equal(_run(epi, A, B, Bkn, bias, mask, 0)[0], want)
