@@ -41,7 +41,9 @@ After everything else, the same guarded runner times the same-run PyTorch baseli
 SURVEY 6.4(a)): the reference's own loop on the reference model (``baseline``: nn.Module eager,
 autograd, RCCL all-reduce at N > 1, torch.optim.Adam, a per-step ``loss.item()``) -- ``vs_baseline``
 is the headline over it -- and plain PyTorch-ROCm on each secondary block's model (``baselines``;
-each block gets ``torch_baseline_iters_per_s`` and ``speedup``).  ``--no-baselines`` turns them off.
+each block gets ``torch_baseline_iters_per_s`` and ``speedup``).  Each baseline is timed in two
+back-to-back windows and its rate is the faster one (``windows_iters_per_s`` lists both): a host
+hiccup cannot make the baseline look slow.  ``--no-baselines`` turns them off.
 
 After the headline's timed region, and outside it, the same guarded runner times BASELINE config #2
 (``bf16_mlp``: SyntheticMLP(4096, 4), batch 1024 per GPU, bf16 MFMA GEMMs, MLPTrainer), the fp32
@@ -350,12 +352,17 @@ def attach_baselines(secondary: dict, baselines: dict) -> None:
             secondary[key]["speedup"] = round(secondary[key]["iters_per_s"] / b["iters_per_s"], 3)
 
 
-def run_baseline(desc: str, make, steps: int, warmup: int, device) -> dict:
+def run_baseline(desc: str, make, steps: int, warmup: int, device, windows: int = 2) -> dict:
+    """The torch baseline, timed in ``windows`` back-to-back windows of ``steps`` steps; the FASTEST
+    window is its rate (an eager, host-bound loop: one host hiccup in a single window made the
+    baseline 2.5x slower in one of three fresh processes, and so the ratio against it 2x better)."""
     tr = make()
     try:
-        elapsed = timed_block(tr, steps, warmup, device)
+        elapsed = [timed_block(tr, steps, warmup if w == 0 else 0, device) for w in range(windows)]
+        best = min(elapsed)
         return {"model": desc, "impl": tr.impl, "steps": steps, "warmup": warmup,
-                "ms_per_step": round(elapsed / steps * 1e3, 6), "iters_per_s": round(steps / elapsed, 2)}
+                "ms_per_step": round(best / steps * 1e3, 6), "iters_per_s": round(steps / best, 2),
+                "windows_iters_per_s": [round(steps / e, 2) for e in elapsed]}
     finally:
         tr.close()
         del tr

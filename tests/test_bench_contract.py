@@ -53,6 +53,8 @@ def test_bench_same_run_baseline_cpu():
     _check(d, 1, 40, 5)
     b = d["baseline"]
     assert b["impl"] == "engine" and b["steps"] == 30 and b["warmup"] == 20 and b["iters_per_s"] > 0
+    # two windows, the fastest is the baseline's rate
+    assert len(b["windows_iters_per_s"]) == 2 and b["iters_per_s"] == max(b["windows_iters_per_s"])
     assert abs(d["vs_baseline"] - d["global_steps_per_sec"] / b["iters_per_s"]) < 0.02 * d["vs_baseline"] + 0.01
     assert d["baselines"] == {}  # no secondary block on the CPU, so no secondary baseline either
 
