@@ -709,17 +709,18 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
 // Workspace of the split-K GEMM (gemm.hip, variant 9): per (device, stream), so launches that may
 // run concurrently never share a partial slab or a ticket.  Tensors from the caching allocator (a
 // first use inside a graph capture allocates from the graph's pool; the map keeps it alive); the
-// ticket words start at zero and every launch leaves them at zero.
+// ticket words start at zero and every launch leaves them at zero.  The map is never destroyed: its
+// tensors must not be freed into the caching allocator during static destruction at exit.
 struct SkWorkspace {
   at::Tensor slab, flags;
 };
 std::mutex g_sk_mu;
-std::map<std::pair<int, hipStream_t>, SkWorkspace> g_sk_ws;
+auto* g_sk_ws = new std::map<std::pair<int, hipStream_t>, SkWorkspace>();
 
 void attach_sk_workspace(dgt::GemmArgs& g, const at::Tensor& like, hipStream_t stream) {
   const int64_t tiles = (int64_t)(g.M / 256) * (g.N / 128);
   std::lock_guard<std::mutex> lock(g_sk_mu);
-  SkWorkspace& w = g_sk_ws[{(int)like.device().index(), stream}];
+  SkWorkspace& w = (*g_sk_ws)[{(int)like.device().index(), stream}];
   if (!w.slab.defined() || w.slab.numel() < tiles * 256 * 128) {
     w.slab = at::empty({tiles * 256 * 128}, like.options().dtype(at::kFloat));
     w.flags = at::zeros({tiles * 4}, like.options().dtype(at::kInt));
