@@ -118,6 +118,77 @@ def engine_mlp_case(dtype, stage):
     return fn
 
 
+def engine_fuzz_case(dtype, stage, gas, seed, steps=24):
+    """The engine MLP (fused chains, one bucket per layer) through seeded random transitions --
+    batch 128 / 256, the fused or torch's BCE, a no-grad forward in between, a retained graph taken
+    backward twice, lr changes, extra zero_grad calls -- so that the reducer's per-layer launches,
+    its launcher thread and the accumulation across backwards are exercised in orders no listed case
+    has; the forced run must still give the collective-free run's bits."""
+    import random
+
+    import distributed_gpu_test_amd as dgt
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+
+    def fn():
+        torch.manual_seed(100 + seed)
+        rnd = random.Random(seed)
+        m = SyntheticMLP(width=256, depth=3)
+        cfg = {"train_micro_batch_size_per_gpu": 128, "gradient_accumulation_steps": gas,
+               "zero_optimization": {"stage": stage, "reduce_bucket_size": 4096},
+               "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}}
+        if dtype == "bf16":
+            cfg.update({"bf16": {"enabled": True}, "communication_data_type": "fp32"})
+        engine, opt, _, _ = dgt.initialize(model=m, config=cfg)
+        fused, tbce = BCEWithLogitsLoss(), torch.nn.BCEWithLogitsLoss()
+        g = torch.Generator().manual_seed(1000 + seed)
+        counts = {"eval": 0, "retain": 0, "torch_bce": 0, "lr": 0, "zero_grad": 0, "b256": 0}
+        for _ in range(steps * gas):
+            b = rnd.choice([128, 256])
+            counts["b256"] += b == 256
+            x = torch.randn(b, 256, generator=g).cuda().to(engine.dtype)
+            y = (torch.rand(b, generator=g) > 0.5).float().cuda()
+            if rnd.random() < 0.15:
+                counts["eval"] += 1
+                with torch.no_grad():
+                    engine(x)
+            out = engine(x).view(-1)
+            if rnd.random() < 0.5:
+                counts["torch_bce"] += 1
+                loss = tbce(out.float(), y)
+            else:
+                loss = fused(out, y)
+            if rnd.random() < 0.2:
+                counts["retain"] += 1
+                engine.backward(loss, retain_graph=True)
+                engine.backward(loss)
+            else:
+                engine.backward(loss)
+            engine.step()
+            if rnd.random() < 0.1:
+                counts["zero_grad"] += 1
+                engine.zero_grad()
+            if rnd.random() < 0.15:
+                counts["lr"] += 1
+                opt.param_groups[0]["lr"] = rnd.choice([5e-4, 1e-3, 2e-3])
+        p = engine.store.param_buf.detach().float().clone()
+        extra = {"layer_notifications": engine.layer_notifications,
+                 "launches": engine.reducer.thread_launches + engine.reducer.native_launches, **counts}
+        engine.close()
+        return p, extra
+    return fn
+
+
+def fuzz_cases(names):
+    """fuzz_<bf16|fp32>_zero<stage>_gas<gas>_s<seed> -> the case (requested by name only)."""
+    out = {}
+    for n in names:
+        if n.startswith("fuzz_"):
+            _, dtype, z, ga, sd = n.split("_")
+            out[n] = engine_fuzz_case(dtype, int(z[4:]), int(ga[3:]), int(sd[1:]))
+    return out
+
+
 def mlp_case(schedule, stage):
     from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
     from distributed_gpu_test_amd.runtime.mlp_trainer import MLPTrainer
@@ -168,6 +239,7 @@ def main():
             cases[f"mlp_{schedule}_zero{stage}"] = mlp_case(schedule, stage)
     for impl in ("graph", "stepwise"):
         cases[f"tiny_{impl}"] = tiny_case(impl)
+    cases.update(fuzz_cases(only))
     res = {}
     for name, fn in cases.items():
         if only and name not in only:

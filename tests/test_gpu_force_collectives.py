@@ -37,3 +37,28 @@ def test_forced_collectives_bit_identical_on_one_gpu():
             assert v["layer_notifications_forced"] >= 6 * 8, (name, v)
             # every bucket went out from the reducer's native launcher thread (csrc/bucket_launcher.cpp)
             assert v["native_forced"] and v["thread_launches_forced"] == 6 * 4, (name, v)
+
+
+FUZZ = [f"fuzz_{d}_zero{z}_gas{g}_s{s}" for d in ("bf16", "fp32") for z in (0, 1) for g in (1, 2) for s in (0, 1)]
+
+
+def test_forced_collectives_fuzz_bit_identical():
+    """Seeded random transitions on the engine MLP (tests/force_collectives_worker.py
+    engine_fuzz_case): retained graphs taken backward twice, no-grad forwards, batch changes, lr
+    changes, both BCEs, gas 1 / 2, ZeRO-0 / 1, bf16 / fp32 -- the forced-collective run must give the
+    collective-free run's bits, with the per-layer launches really issued."""
+    env = dict(os.environ)
+    env.pop("DGT_BACKEND", None)
+    env.pop("DGT_FORCE_COLLECTIVES", None)
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "tests", "force_collectives_worker.py"), *FUZZ], cwd=ROOT,
+                       env=env, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-4000:]
+    res = json.loads([l for l in r.stdout.splitlines() if l.startswith("RESULT ")][-1][len("RESULT "):])
+    assert sorted(res) == sorted(FUZZ), sorted(res)
+    for name, v in res.items():
+        assert v["equal"], (name, v)
+        assert v["calls"] > v["calls_off"] and v["launches_forced"] > 0, (name, v)
+        assert v["layer_notifications_forced"] > 0, (name, v)
+    # the transitions really happened somewhere in the sweep
+    for k in ("eval", "retain", "torch_bce", "lr", "zero_grad", "b256"):
+        assert sum(v[f"{k}_forced"] for v in res.values()) > 0, k
