@@ -721,8 +721,8 @@ void attach_sk_workspace(dgt::GemmArgs& g, const at::Tensor& like, hipStream_t s
   const int64_t tiles = (int64_t)(g.M / 256) * (g.N / 128);
   std::lock_guard<std::mutex> lock(g_sk_mu);
   SkWorkspace& w = (*g_sk_ws)[{(int)like.device().index(), stream}];
-  if (!w.slab.defined() || w.slab.numel() < tiles * 256 * 128) {
-    w.slab = at::empty({tiles * 256 * 128}, like.options().dtype(at::kFloat));
+  if (!w.slab.defined() || w.slab.numel() < tiles * 512 * 128) {
+    w.slab = at::empty({tiles * 512 * 128}, like.options().dtype(at::kFloat));
     w.flags = at::zeros({tiles * 4}, like.options().dtype(at::kInt));
   }
   g.sk_slab = w.slab.data_ptr<float>();

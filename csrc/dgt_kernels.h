@@ -189,11 +189,13 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
   float alpha;
   GemmAdam adam;       // kEpiAdam only (the gradient is alpha * A . B^T; ldc = row stride of the weight)
   float* colsum;       // kEpiColSum: fp32 [M / 128, N]
-  float* sk_slab;      // split-K kernel (variant 9): fp32 256 x 128 partial per tile (two 128-row halves)
-  int* sk_flags;       // split-K kernel: 4 ints per tile (ticket, partial ready per 128-row half), zero
+  float* sk_slab;      // split-K kernel (variant 9): 4 fp32 128 x 128 partials per tile (per row half:
+                       // the publisher's, a finisher's that gave up)
+  int* sk_flags;       // split-K kernel: 4 ints per tile (a state word per 128-row half, 2 spare), zero
                        // between launches
   int sk_xs;           // split-K kernel: bit 0 = a tile's two K halves on neighbouring XCDs (else one XCD);
-                       // bits 1-2: timing diagnostics (gemm.hip), wrong results
+                       // bits 1-2: timing diagnostics (gemm.hip), wrong results; bit 3: finishers never
+                       // wait (the hand-over paths, for tests)
 };
 
 hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream, int variant = 0);

@@ -780,16 +780,23 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 // against 12 per 16 in the 128 x 128 kernel's 64 x 32 wave tiles).  M = 1024 gives 4 x 32 tiles x
 // 2 halves = 256 blocks.  The loop is the FR kernel's (asm LDS-DMA, front-loaded fragment reads,
 // counted vmcnt + raw barrier), three 48 KiB stages.
-// The halves meet in-launch (cdna_hip_programming.md §5 projection GEMM item 2, §6 Guideline 16),
-// once per 128-row half of the tile, each block taking its own row half first: a per-(tile, row
-// half) ticket says who came first; the first writes its fp32 partial of those rows (64 KiB,
-// write-through sc1 16-byte stores), drains and raises a flag; the second polls the flag (its
-// partner holds ticket 0 and publishes in that same phase: no co-residency is assumed; bounded),
-// re-arms both words for the next launch, adds the partial (sc1 loads; fp32 a + b == b + a: the sum
-// does not depend on which half came first) and runs the staged epilogue of those 128 rows.
-// Arriving together, each block finishes one row half; arriving apart, the later one finishes both.
+// The halves meet in-launch (cdna_hip_programming.md §5 projection GEMM item 2, §6 Guideline 16)
+// per 128-row half of the tile, with static roles: each block publishes its fp32 partial of one row
+// half (64 KiB, write-through sc1 16-byte stores, drained, then a compare-and-swap of that half's
+// state word) and finishes the other (polls its state word, adds the partner's partial with sc1
+// loads -- fp32 a + b == b + a: the sum does not depend on arrival order -- and runs the staged
+// epilogue of those 128 rows).  A finisher whose partner has not published within ~20 us hands its
+// own partial over instead and leaves the row half to the publisher, so no block waits on a partner
+// that is not running (no co-residency is assumed).  Every state word is back at zero after a launch.
 // sk_xs = 1 puts a tile's halves on neighbouring XCDs (each XCD's L2 then holds half of K for a
 // 4 x 8-tile region: 8 MiB of unique operands per XCD instead of 12), 0 on one XCD.
+// agent-scope compare-and-swap (relaxed), returning the value found
+DGT_DEVICE int cas_agent(int* p, int expected, int desired) {
+  __hip_atomic_compare_exchange_strong(p, &expected, desired, __ATOMIC_RELAXED, __ATOMIC_RELAXED,
+                                       __HIP_MEMORY_SCOPE_AGENT);
+  return expected;
+}
+
 namespace sk {
 constexpr int TM = 256, TN = 128, S = 3, NW = 8;
 constexpr int A_ELEMS = TM * GBK, STAGE = (TM + TN) * GBK;  // u16 per stage (48 KiB)
@@ -899,52 +906,44 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_sk_kernel(GemmArgs g) {
     return;
   }
 
-  // ---- the halves meet, per 128-row half of the tile, own row half first
-  // (taking both tickets at once measured 8 us slower: the block arriving first then wins both
-  // halves and its partner finishes the whole tile)
-  int* order = reinterpret_cast<int*>(lds + 64 * 1024);  // past the epilogue's 32 KiB tile
-#pragma unroll 1
-  for (int ph = 0; ph < 2; ++ph) {
-    const int r = half ^ ph;
-    int* ticket = g.sk_flags + 4 * t + 2 * r;
-    int* ready = ticket + 1;
-    // the row half's partial: 64 KiB, lane-linear in the owning waves' accumulator order
-    const auto rsrc = __builtin_amdgcn_make_buffer_rsrc(g.sk_slab + (long long)(2 * t + r) * (128 * TN), 0,
-                                                         128 * TN * 4, 0x00020000);
-    if (tid == 0) order[ph] = __hip_atomic_fetch_add(ticket, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  // ---- the halves meet.  Roles are static: the block of K half h FINISHES row half h (adds the
+  // partner's partial, runs its epilogue) and PUBLISHES its partial of row half 1 - h.  Publishing
+  // never waits; finishing waits for the partner's publish only up to a time limit, after which the
+  // finisher hands its own partial over and leaves the row half to the publisher (a per-row-half
+  // state word, compare-and-swap: 0 -> kPub by the publisher, 0 -> kGaveUp by a finisher that timed
+  // out; exactly one of the two succeeds).  So no block waits on a partner that is not running,
+  // and arriving together each block finishes half the tile.
+  // (v2, tickets per row half taken in order: the ticket round trips sat on the critical path,
+  // 42.4 vs 35.7 us without the meeting; v2b, both tickets at once: the first arriver won both.)
+  constexpr int kPub = 1, kGaveUp = 2;
+  int* words = reinterpret_cast<int*>(lds + 64 * 1024);  // LDS broadcast words, past the epilogue tile
+  const int pr = half ^ 1;                                 // the row half this block publishes
+  int* st_pub = g.sk_flags + 4 * t + pr;
+  int* st_fin = g.sk_flags + 4 * t + half;
+  // 4 partials of 64 KiB per tile: [row half][0 = the publisher's, 1 = a finisher's that gave up]
+  auto slab_of = [&](int r, int which) {
+    return __builtin_amdgcn_make_buffer_rsrc(g.sk_slab + (long long)(4 * t + 2 * r + which) * (128 * TN), 0,
+                                             128 * TN * 4, 0x00020000);
+  };
+  auto store_rows = [&](int r, int which) {  // the owning waves' accumulators of row half r, sc1
+    if (own_half == r) {
+      const auto rsrc = slab_of(r, which);
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
+                                                 ((i * NJ + j) * 256 + (tid & 255)) * 16, 0, 16 /* sc1 */);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
     __syncthreads();
-    const bool mine = own_half == r;
-    if (order[ph] == 0) {
-      if (mine) {
-#pragma unroll
-        for (int i = 0; i < 4; ++i)
-#pragma unroll
-          for (int j = 0; j < NJ; ++j)
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), rsrc,
-                                                   ((i * NJ + j) * 256 + (tid & 255)) * 16, 0, 16 /* sc1 */);
-      }
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
-      __syncthreads();
-      if (tid == 0) __hip_atomic_store(ready, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      continue;
-    }
-    if (tid == 0) {
-      // the partner holds ticket 0 and publishes this half within that same phase, before it
-      // waits on anything (it can only be second on a half after publishing the other): the wait
-      // is bounded by its store pass; bounded all the same (~seconds): a lost flag yields a wrong
-      // tile, never a hung GPU
-      for (int spin = 0; spin < (1 << 22) && __hip_atomic_load(ready, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
-           ++spin)
-        __builtin_amdgcn_s_sleep(1);
-      // both blocks are past their last use of the two words: re-arm them for the next launch
-      __hip_atomic_store(ticket, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-      __hip_atomic_store(ready, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    }
-    // every load of the partial is an sc1 load (L1 bypassed) after the poll and a barrier: no
-    // acquire fence (MI355X_MICROARCH.md, visibility: valid forms, first row)
+  };
+  auto finish_rows = [&](int r, int which) {  // add the other block's partial of row half r, epilogue
+    // every load of a partial is an sc1 load (L1 bypassed) behind the state word's sc1 poll or
+    // compare-and-swap and a barrier: no acquire fence (MI355X_MICROARCH.md, visibility: valid forms)
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    __syncthreads();
-    if (mine) {
+    if (own_half == r) {
+      const auto rsrc = slab_of(r, which);
 #pragma unroll
       for (int i = 0; i < 4; ++i)
 #pragma unroll
@@ -954,7 +953,42 @@ __global__ __launch_bounds__(512, 1) void gemm_nt_sk_kernel(GemmArgs g) {
     }
     pre.load_mask(g, m0 + 128 * r, n0, tid);
     epilogue_staged<EPI, 128, TN, 64, 64, 512, true>(g, acc, lds, m0 + 128 * r, n0, wr - 2 * r, wc, l, tid, pre,
-                                                     mine);
+                                                     own_half == r);
+  };
+  // 1. publish row half pr (the compare-and-swap's answer is only needed at step 3)
+  store_rows(pr, 0);
+  int pub_old = 0;
+  if (tid == 0) pub_old = cas_agent(st_pub, 0, kPub);
+  // 2. finish row half `half`: wait for the partner's publish, at most ~20 us (sk_xs bit 3, a test
+  // knob: not at all, so the hand-over paths run)
+  if (tid == 0) {
+    const unsigned long long t0 = wall_clock64(), limit = (g.sk_xs & 8) ? 0 : 2000;  // 100 MHz: 20 us
+    int st;
+    while ((st = __hip_atomic_load(st_fin, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) == 0 &&
+           wall_clock64() - t0 < limit)
+      __builtin_amdgcn_s_sleep(1);
+    words[0] = st;
+  }
+  __syncthreads();
+  int fin = words[0];
+  if (fin != kPub) {
+    // the partner has not published: hand this block's partial over and give the row half up,
+    // unless the partner's publish lands first
+    store_rows(half, 1);
+    if (tid == 0) words[1] = cas_agent(st_fin, 0, kGaveUp);
+    __syncthreads();
+    fin = words[1] == kPub ? kPub : kGaveUp;
+  }
+  if (fin == kPub) {
+    if (tid == 0) __hip_atomic_store(st_fin, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    finish_rows(half, 0);
+  }
+  // 3. the finisher of row half pr gave up: finish it here from its handed-over partial
+  if (tid == 0) words[2] = pub_old;
+  __syncthreads();
+  if (words[2] == kGaveUp) {
+    if (tid == 0) __hip_atomic_store(st_pub, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    finish_rows(pr, 1);
   }
 }
 

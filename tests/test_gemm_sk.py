@@ -128,3 +128,40 @@ def test_gemm_shape_rule_keeps_the_unsplit_kernels_by_default():
     for epi, unsplit in [("bias_relu_T", 3), ("kn_mask_T_colsum", 5)]:
         want = _run(epi, A, B, Bkn, bias, mask, 9 if sk else unsplit)[0]
         assert torch.equal(_run(epi, A, B, Bkn, bias, mask, 0)[0], want)
+
+
+_HANDOVER = r"""
+import sys, torch
+sys.path.insert(0, {root!r})
+from tests.test_gemm_sk import _operands, _run
+A, B, Bkn, bias, mask = _operands(1024, 4096, 4096, 13)
+outs = {{}}
+for epi in ("bias_relu_T", "kn_mask_T_colsum"):
+    for rep in range(3):
+        C, CT, cs, _ = _run(epi, A, B, Bkn, bias, mask, 9)
+        outs[f"{{epi}}_{{rep}}"] = [t.cpu() for t in (C, CT, cs) if t is not None]
+torch.save(outs, {path!r})
+"""
+
+
+def test_gemm_sk_handover_paths_give_the_same_bits(tmp_path):
+    """DGT_GEMM_SK_XS=9 (bit 3: a finisher never waits for its partner's publish) drives the
+    hand-over paths -- the finisher gives its row half up and the publisher finishes it, or the
+    publish lands first and the give-up loses the compare-and-swap -- which a normal launch takes
+    only when a partner is late by ~20 us.  Every launch must still give the normal launch's bits."""
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    path = str(tmp_path / "handover.pt")
+    env = dict(os.environ, DGT_GEMM_SK_XS="9")
+    r = subprocess.run([sys.executable, "-c", _HANDOVER.format(root=root, path=path)], cwd=root, env=env,
+                       capture_output=True, text=True, timeout=240)
+    assert r.returncode == 0, r.stderr[-3000:]
+    got = torch.load(path, weights_only=True)
+    A, B, Bkn, bias, mask = _operands(1024, 4096, 4096, 13)
+    for epi in ("bias_relu_T", "kn_mask_T_colsum"):
+        want = [t.cpu() for t in _run(epi, A, B, Bkn, bias, mask, 9)[:3] if t is not None]
+        for rep in range(3):
+            for x, y in zip(got[f"{epi}_{rep}"], want):
+                assert torch.equal(x, y), (epi, rep)
