@@ -1520,9 +1520,9 @@ bool launch_rp(int grid, const GemmArgs& g, hipStream_t stream, int depth) {
 
 // the shape rule's use of the split-K kernel: DGT_GEMM_SK=1 for one-wave 128 x 128 grids with
 // K >= 2048 and a [N, K] B (the MLP's M = 1024 forwards); the default (0) keeps the 128 x 128
-// kernels: the split-K forward with C^T is 43.5-46.2 us hot against 44.8-45.1, without C^T
-// 40.0-40.4 against 38.6-39.5, and the bf16 MLP step is no faster (profiles/r6_gemm_m1024_splitk.jsonl:
-// its K loop alone takes 32 us, a 128-row half epilogue ~4 us, the halves' meeting ~6.5 us)
+// kernels: hot the split-K forward is level with them (45.3-45.7 vs 45.4-46.9 us with C^T), in the
+// bf16 MLP step it times the same (41.5 vs 41.5 us) (profiles/r6_gemm_m1024_splitk.jsonl: its K loop
+// alone takes 32-33 us, a 128-row half epilogue ~4 us, the halves' meeting ~5 us)
 static bool sk_auto() {
   static const int on = [] {
     const char* e = std::getenv("DGT_GEMM_SK");

@@ -59,8 +59,8 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     8 = the 256x256 kernel with cross-phase fragment prefetch (phase P's MFMAs overlap the LDS
     reads of phase P + 1; bit-identical to 2) -- the kernel the shape rule runs for >= 200 tiles of
     256x256,
-    9 = 256x128 tiles with K split in two halves that meet in-launch (per-tile ticket, fp32 partial,
-    deterministic; M % 256 == 0, N % 128 == 0, K % 128 == 0, a multiple of 8 tiles, bf16 epilogues,
+    9 = 256x128 tiles with K split in two halves that meet in-launch (per 128-row half: one block
+    publishes its fp32 partial, the other finishes; deterministic; M % 256 == 0, N % 128 == 0, K % 128 == 0, a multiple of 8 tiles, bf16 epilogues,
     ``b_kn`` and ``colsum`` included) -- opt-in: ``DGT_GEMM_SK=1`` makes the shape rule use it for
     one-wave NT grids with K >= 2048; on the MLP's M = 1024 products it is no faster than 3 / 5
     (``profiles/r6_gemm_m1024_splitk.jsonl``).
