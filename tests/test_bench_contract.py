@@ -74,7 +74,7 @@ def test_bench_two_ranks_gloo_cpu():
     env = dict(os.environ, DGT_QUIET="1", OMP_NUM_THREADS="1")
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node=2", "--master-addr=127.0.0.1",
            f"--master-port={free_port()}", os.path.join(ROOT, "bench.py"), "--gpus", "2", "--steps", "30",
-           "--warmup", "3"]
+           "--warmup", "3", "--force-baselines", "--baseline-steps", "20"]
     r = subprocess.run(cmd, cwd=ROOT, env=env, capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-3000:]
     lines = _json_lines(r.stdout)
@@ -82,6 +82,9 @@ def test_bench_two_ranks_gloo_cpu():
     _check(lines[0], 2, 30, 3)
     # no IPC mailboxes on the CPU: the process group's barrier brackets the timed region
     assert lines[0]["config"]["closing_barrier"] == "process-group"
+    # the same-run baseline at N = 2 (its all-reduce on the process group), two windows, max over ranks
+    b = lines[0]["baseline"]
+    assert b["steps"] == 20 and len(b["windows_iters_per_s"]) == 2 and lines[0]["vs_baseline"] > 0, b
 
 
 def test_bench_self_launches_n_ranks_cpu():
