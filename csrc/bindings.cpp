@@ -8,6 +8,7 @@
 #include <torch/extension.h>
 #include <torch/library.h>
 
+#include <algorithm>
 #include <cstdlib>
 #include <map>
 #include <memory>
@@ -717,13 +718,15 @@ struct SkWorkspace {
 std::mutex g_sk_mu;
 auto* g_sk_ws = new std::map<std::pair<int, hipStream_t>, SkWorkspace>();
 
-void attach_sk_workspace(dgt::GemmArgs& g, const at::Tensor& like, hipStream_t stream) {
-  const int64_t tiles = (int64_t)(g.M / 256) * (g.N / 128);
+void attach_sk_workspace(dgt::GemmArgs& g, const at::Tensor& like, hipStream_t stream, int64_t slab_floats,
+                         int64_t flag_ints) {
   std::lock_guard<std::mutex> lock(g_sk_mu);
   SkWorkspace& w = (*g_sk_ws)[{(int)like.device().index(), stream}];
-  if (!w.slab.defined() || w.slab.numel() < tiles * 512 * 128) {
-    w.slab = at::empty({tiles * 512 * 128}, like.options().dtype(at::kFloat));
-    w.flags = at::zeros({tiles * 4}, like.options().dtype(at::kInt));
+  if (!w.slab.defined() || w.slab.numel() < slab_floats || w.flags.numel() < flag_ints) {
+    const int64_t sf = std::max<int64_t>(slab_floats, w.slab.defined() ? w.slab.numel() : 0);
+    const int64_t fi = std::max<int64_t>(flag_ints, w.flags.defined() ? w.flags.numel() : 0);
+    w.slab = at::empty({sf}, like.options().dtype(at::kFloat));
+    w.flags = at::zeros({fi}, like.options().dtype(at::kInt));
   }
   g.sk_slab = w.slab.data_ptr<float>();
   g.sk_flags = w.flags.data_ptr<int>();
@@ -740,11 +743,11 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
              const std::optional<at::Tensor>& colsum) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || (variant != 2 && variant != 8),
               "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK(variant >= 0 && variant <= 9,
+  TORCH_CHECK(variant >= 0 && variant <= 10,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
               "fragment reads), 4 (128x128, 4 stages, 8 waves), 5 (software-pipelined reads), 6 / 7 (register "
-              "prefetch, 2 / 4 K-tiles), 8 (256x256 with cross-phase fragment prefetch) or 9 (256x128 split-K "
-              "2); the round-2 variants live in git history (commit c0371a5)");
+              "prefetch, 2 / 4 K-tiles), 8 (256x256 with cross-phase fragment prefetch), 9 (256x128 split-K 2) or "
+              "10 (128x128 split-K for small grids); the round-2 variants live in git history (commit c0371a5)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
@@ -806,11 +809,20 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
   if (variant == 2 || variant == 8)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
   const hipStream_t stream = stream_of(A);
-  if (dgt::gemm_nt_uses_sk(g, (int)epi, (int)variant)) {
+  const int skn = dgt::gemm_nt_uses_skn(g, (int)epi, (int)variant);
+  TORCH_CHECK(variant != 10 || skn > 0,
+              "dgt: the 128x128 split-K mode (variant 10) needs a bf16 (staged) epilogue and a grid of at most 128 "
+              "tiles with at least 16 K-tiles");
+  if (skn > 0) {
+    g.skn_split = skn;
+    const int64_t tiles = (int64_t)(M / 128) * (N / 128);
+    attach_sk_workspace(g, A, stream, tiles * skn * 128 * 128, tiles);
+  } else if (dgt::gemm_nt_uses_sk(g, (int)epi, (int)variant)) {
     TORCH_CHECK(dgt::gemm_nt_sk_fits(g, (int)epi),
                 "dgt: the split-K gemm (variant 9) needs M % 256 == 0, N % 128 == 0, K % 128 == 0, a multiple of 8 "
                 "256x128 tiles and a bf16 (staged) epilogue");
-    attach_sk_workspace(g, A, stream);
+    const int64_t tiles = (int64_t)(M / 256) * (N / 128);
+    attach_sk_workspace(g, A, stream, tiles * 512 * 128, tiles * 4);
   }
   DGT_CHECK_HIP(dgt::gemm_nt(g, (int)epi, stream, (int)variant));
 }

@@ -193,12 +193,18 @@ struct GemmArgs {      // C[M,N] = alpha * A[M,K] . B[N,K]^T (+ epilogue); bf16 
                        // the publisher's, a finisher's that gave up)
   int* sk_flags;       // split-K kernel: 4 ints per tile (a state word per 128-row half, 2 spare), zero
                        // between launches
+  int skn_split;       // 128 x 128 split-K mode (variant 10): blocks per tile
   int sk_xs;           // split-K kernel: bit 0 = a tile's two K halves on neighbouring XCDs (else one XCD);
                        // bits 1-2: timing diagnostics (gemm.hip), wrong results; bit 3: finishers never
                        // wait (the hand-over paths, for tests)
 };
 
 hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream, int variant = 0);
+// the 128 x 128 split-K mode (variant 10; the shape rule's choice for grids of <= 128 tiles): its
+// split for these arguments (0: does not apply); the caller sets skn_split to it and provides
+// sk_slab (tiles x split x 128 x 128 fp32) and sk_flags (tiles ints, zero between launches)
+int gemm_nt_skn_split(const GemmArgs& g, int epilogue);
+int gemm_nt_uses_skn(const GemmArgs& g, int epilogue, int variant);
 // the split-K kernel's shape rule (256 x 128 tiles, a multiple of 8 of them, K % 128 == 0, staged
 // bf16 epilogue); the caller provides sk_slab / sk_flags for (M / 256) * (N / 128) tiles
 bool gemm_nt_sk_fits(const GemmArgs& g, int epilogue);

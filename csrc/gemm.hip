@@ -512,9 +512,15 @@ DGT_DEVICE void wait_vmcnt() {
 // into a second register set while tile kt's MFMAs run, so no MFMA waits on an LDS round trip of
 // its own K-tile; the barrier of step kt publishes tile kt+1 (one K-tile earlier than FR = 1), and
 // five stages keep the same two to three K-tiles of staging in flight.
-template <int EPI, int S, int NW = 4, int FR = 0>
+// SPK (split-K, small grids): g.skn_split blocks per tile, block s taking K-slice s; the slices meet
+// in-launch -- each block writes its fp32 partial (64 KiB, write-through sc1 stores), drains and
+// adds to the tile's counter; the block whose add comes last sums every partial in slice order
+// (fixed, so the bits do not depend on arrival order), re-arms the counter and runs the epilogue
+// (MI355X_MICROARCH.md visibility, valid forms, first row: the last adder is told by its add).
+template <int EPI, int S, int NW = 4, int FR = 0, bool SPK = false>
 __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmArgs g) {
   static_assert(S == 2 || S == 4 || (S == 5 && FR == 3), "two stages (2 blocks / CU), four (1 block / CU), or SP");
+  static_assert(!SPK || (S == 4 && NW == 8 && FR == 1), "split-K: the FR kernel");
   constexpr int BK = GBK;
   constexpr bool KN = (EPI & kEpiBKN) != 0;      // B is [K, N]: staged as is, transposed reads
   constexpr int WN = NW == 8 ? 32 : 64;          // wave tile columns
@@ -522,12 +528,15 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
   constexpr int NJ = WN / 16;                    // accumulator columns per wave
   __shared__ __attribute__((aligned(16))) u16 lds[S][2][GBM * BK];  // [stage][A|B], 32 KiB per stage
   const int tid = threadIdx.x, w = tid >> 6, l = tid & 63;
+  const int split = SPK ? g.skn_split : 1;
+  const int tile = SPK ? (int)blockIdx.x / split : (int)blockIdx.x, slice = SPK ? (int)blockIdx.x % split : 0;
   int tm, tn;
-  tile_of_block(blockIdx.x, g.M / GBM, g.N / GBN, tm, tn);
+  tile_of_block(tile, g.M / GBM, g.N / GBN, tm, tn);
   const int m0 = tm * GBM, n0 = tn * GBN;
   const int wr = w / WCOLS, wc = w % WCOLS;
-  const u16* A = static_cast<const u16*>(g.A);
-  const u16* B = static_cast<const u16*>(g.B);
+  const long long kbase = (long long)slice * (g.K / split);
+  const u16* A = static_cast<const u16*>(g.A) + kbase;
+  const u16* B = static_cast<const u16*>(g.B) + kbase * (KN ? g.ldb : 1);
 
   f32x4 acc[4][NJ];
 #pragma unroll
@@ -535,7 +544,7 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
 #pragma unroll
     for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
 
-  const int nk = g.K / BK;
+  const int nk = g.K / BK / split;
   auto compute = [&](int buf) {
     const u16* As = lds[buf][0];
     const u16* Bs = lds[buf][1];
@@ -752,6 +761,61 @@ __global__ __launch_bounds__(64 * NW, S == 2 ? 2 : 1) void gemm_nt_kernel(GemmAr
       buf = (buf + 1 == S) ? 0 : buf + 1;
     }
     __builtin_amdgcn_s_barrier();
+  }
+
+  if constexpr (SPK) {
+    const int t = blockIdx.x / split;  // the tile's index for its partials and counter
+    auto part = [&](int q) {
+      return __builtin_amdgcn_make_buffer_rsrc(g.sk_slab + ((long long)t * split + q) * (GBM * GBN), 0, GBM * GBN * 4,
+                                               0x00020000);
+    };
+    const auto mine = part(slice);
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), mine,
+                                               ((i * NJ + j) * 512 + tid) * 16, 0, 16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+    __syncthreads();
+    int* word = reinterpret_cast<int*>(&lds[0][0][0]);  // the stages are idle
+    if (tid == 0) *word = __hip_atomic_fetch_add(g.sk_flags + t, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*word != split - 1) return;  // not the last slice to arrive
+    if (tid == 0) __hip_atomic_store(g.sk_flags + t, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    // every load of a partial is an sc1 load behind the counter's add and the barrier above
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f32x4 sum[4][NJ];
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) sum[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int q = 0; q < split; ++q) {  // slice order: the same sum whoever arrived last
+      f32x4 p[4][NJ];
+      if (q == slice) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j) p[i][j] = acc[i][j];
+      } else {
+        const auto rs = part(q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            p[i][j] = __builtin_bit_cast(
+                f32x4, __builtin_amdgcn_raw_buffer_load_b128(rs, ((i * NJ + j) * 512 + tid) * 16, 0, 16));
+      }
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) sum[i][j] += p[i][j];
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = sum[i][j];
   }
 
   // ---- epilogue: D col = l&15 (n), row = 4*(l>>4) + r (m)
@@ -1538,9 +1602,58 @@ bool gemm_nt_uses_sk(const GemmArgs& g, int epi, int variant) {
   return (g.M / GBM) * (g.N / GBN) <= 256 && g.K >= 2048;
 }
 
+// The split of the 128 x 128 split-K mode (variant 10) for a grid that leaves CUs idle: the largest
+// of 8 / 4 / 2 with tiles x split <= 256 blocks and at least 8 K-tiles per slice (0: none fits).
+// DGT_GEMM_SKN (default 1) lets the shape rule use it for grids of at most 128 tiles.
+int gemm_nt_skn_split(const GemmArgs& g, int epi) {
+  if (epi & (kEpiOutF32 | kEpiAccumulate | kEpiAdam)) return 0;
+  const int tiles = (g.M / GBM) * (g.N / GBN), nk = g.K / GBK;
+  for (int sp = 8; sp >= 2; sp /= 2)
+    if (tiles * sp <= 256 && nk % sp == 0 && nk / sp >= 8) return sp;
+  return 0;
+}
+
+static bool skn_auto() {
+  static const int on = [] {
+    const char* e = std::getenv("DGT_GEMM_SKN");
+    return (e && *e) ? std::atoi(e) : 1;
+  }();
+  return on != 0;
+}
+
+int gemm_nt_uses_skn(const GemmArgs& g, int epi, int variant) {
+  if (variant == 10) return gemm_nt_skn_split(g, epi);
+  if (variant != 0 || !skn_auto() || (g.M / GBM) * (g.N / GBN) > 128) return 0;
+  return gemm_nt_skn_split(g, epi);
+}
+
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 9) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 10) return hipErrorInvalidValue;
+  if (variant == 10 || (variant == 0 && gemm_nt_uses_skn(g, epi, 0))) {
+    const int split = gemm_nt_skn_split(g, epi);
+    if (!split || g.skn_split != split || !g.sk_slab || !g.sk_flags) return hipErrorInvalidValue;
+    const int grid = (g.M / GBM) * (g.N / GBN) * split;
+    switch (epi) {
+#define DGT_SKN_CASE(E)                                                                         \
+  case E:                                                                                       \
+    hipLaunchKernelGGL((gemm_nt_kernel<E, 4, 8, 1, true>), dim3(grid), dim3(512), 0, stream, g); \
+    return hipGetLastError();
+      DGT_SKN_CASE(0)
+      DGT_SKN_CASE(kEpiBias | kEpiRelu | kEpiStoreT)
+      DGT_SKN_CASE(kEpiBias | kEpiRelu)
+      DGT_SKN_CASE(kEpiBias | kEpiStoreT)
+      DGT_SKN_CASE(kEpiBias)
+      DGT_SKN_CASE(kEpiMask | kEpiStoreT)
+      DGT_SKN_CASE(kEpiMask | kEpiStoreT | kEpiBKN)
+      DGT_SKN_CASE(kEpiMask | kEpiStoreT | kEpiBKN | kEpiColSum)
+      DGT_SKN_CASE(kEpiBKN)
+      DGT_SKN_CASE(kEpiStoreT | kEpiBKN)
+#undef DGT_SKN_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+  }
   if (gemm_nt_uses_sk(g, epi, variant)) {
     if (!gemm_nt_sk_fits(g, epi) || !g.sk_slab || !g.sk_flags) return hipErrorInvalidValue;
     const int grid = 2 * (g.M / sk::TM) * (g.N / sk::TN);

@@ -63,7 +63,10 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     publishes its fp32 partial, the other finishes; deterministic; M % 256 == 0, N % 128 == 0, K % 128 == 0, a multiple of 8 tiles, bf16 epilogues,
     ``b_kn`` and ``colsum`` included) -- opt-in: ``DGT_GEMM_SK=1`` makes the shape rule use it for
     one-wave NT grids with K >= 2048; on the MLP's M = 1024 products it is no faster than 3 / 5
-    (``profiles/r6_gemm_m1024_splitk.jsonl``).
+    (``profiles/r6_gemm_m1024_splitk.jsonl``),
+    10 = the 128x128 kernel with K split 2 / 4 / 8 ways for grids of at most 128 tiles (small M): the
+    slices meet in-launch, the last to arrive sums them in slice order (deterministic) -- the shape
+    rule's choice there (``DGT_GEMM_SKN=0`` turns it off).
     ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
     the shape rule gives to the 128x128 kernels).
 

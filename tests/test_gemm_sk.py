@@ -165,3 +165,51 @@ def test_gemm_sk_handover_paths_give_the_same_bits(tmp_path):
         for rep in range(3):
             for x, y in zip(got[f"{epi}_{rep}"], want):
                 assert torch.equal(x, y), (epi, rep)
+
+
+# ---- the 128x128 kernel's split-K mode (variant 10): small grids, K split 2 / 4 / 8 ways
+SKN_SHAPES = [(128, 4096, 4096), (256, 4096, 4096), (512, 4096, 4096), (128, 512, 1024), (256, 1024, 2048)]
+
+
+@pytest.mark.parametrize("M,N,K", SKN_SHAPES)
+@pytest.mark.parametrize("epi", EPIS)
+def test_gemm_skn_matches_fp32_reference(M, N, K, epi):
+    A, B, Bkn, bias, mask = _operands(M, N, K, 3 * M + N + K)
+    C, CT, cs, kw = _run(epi, A, B, Bkn, bias, mask, 10)
+    kn = epi.startswith("kn_")
+    ref = gemm_nt_reference(A, Bkn if kn else B, b_kn=kn, **kw)
+    torch.testing.assert_close(C.float(), ref.to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2 * K ** 0.5)
+    if CT is not None:
+        assert torch.equal(CT, C.t())
+    if cs is not None:
+        torch.testing.assert_close(cs, C.float().view(M // 128, 128, N).sum(1), rtol=1e-5, atol=1e-3)
+
+
+@pytest.mark.parametrize("epi", ["bias_relu_T", "kn_mask_T_colsum"])
+@pytest.mark.parametrize("M", [128, 256, 512])
+def test_gemm_skn_deterministic_close_to_unsplit_and_picked_by_the_shape_rule(epi, M):
+    """The slices are summed in slice order by whichever block arrives last: ten launches give the
+    same bits; against the unsplit kernel only fp32 summation order differs (one bf16 rounding step
+    at most); variant 0 runs this mode for grids of at most 128 tiles (DGT_GEMM_SKN=1, default)."""
+    import os
+    A, B, Bkn, bias, mask = _operands(M, 4096, 4096, 17 + M)
+    first = _run(epi, A, B, Bkn, bias, mask, 10)
+    for _ in range(9):
+        again = _run(epi, A, B, Bkn, bias, mask, 10)
+        for x, y in zip(first[:3], again[:3]):
+            if x is not None:
+                assert torch.equal(x, y)
+    C10 = first[0].float()
+    C3 = _run(epi, A, B, Bkn, bias, mask, 3)[0].float()
+    d = (C10 - C3).abs()
+    assert float((d > 0).float().mean()) < 0.05
+    assert float((d / C3.abs().clamp_min(1.0)).max()) <= 2 ** -7
+    if os.environ.get("DGT_GEMM_SKN", "1") != "0" and not os.environ.get("DGT_GEMM_VARIANT"):
+        assert torch.equal(_run(epi, A, B, Bkn, bias, mask, 0)[0], first[0])
+
+
+def test_gemm_skn_rejects_grids_it_does_not_fit():
+    A = torch.randn(1024, 4096, device="cuda").bfloat16()
+    B = torch.randn(4096, 4096, device="cuda").bfloat16()  # 256 tiles: the grid already fills the chip
+    with pytest.raises(RuntimeError, match="split-K mode"):
+        gemm_nt(A, B, C=torch.empty(1024, 4096, device="cuda").bfloat16(), variant=10)
