@@ -29,10 +29,12 @@ def main():
         d = sorted(dur.get(k, [0.0]))
         us = d[len(d) // 2]
         rows.append((us * len(v.get("FETCH_SIZE", [])), k, fe / 1024, wr / 1024, us))
-    print("# kernel | fetched MB / dispatch | written MB / dispatch | median us (counter runs) | GB/s")
+    print("# kernel | fetched MB / dispatch | written MB / dispatch | median us (counter runs) | TB/s")
+    print("# (FETCH_SIZE as rocprofv3 derives it: on gfx950 it read ~half the flat Adam's expected 0.94 GB")
+    print("#  -- treat the fetch column as a lower bound)")
     for _, k, fe, wr, us in sorted(rows, reverse=True)[:14]:
-        gbs = (fe + wr) * 1e6 / 1e9 / (us * 1e-6) / 1e3 if us else 0.0
-        print(f"{k[:70]:70s} | {fe:9.1f} | {wr:9.1f} | {us:8.1f} | {gbs:7.0f}")
+        tbs = (fe + wr) * 1e6 / (us * 1e-6) / 1e12 if us else 0.0
+        print(f"{k[:70]:70s} | {fe:9.1f} | {wr:9.1f} | {us:8.1f} | {tbs:6.2f}")
 
 
 if __name__ == "__main__":
