@@ -252,7 +252,8 @@ def test_gemm_register_prefetch_is_bitwise_variant3(rp, epi):
     """The register-prefetch kernels (6: 2 K-tiles in VGPRs, 7: 4) stage the same LDS image and run
     variant 3's fragment reads and MFMAs: every epilogue output equals variant 3's bit for bit, and
     a [K, N] product (the dgrad, plain and with the mask + C^T + column-sum epilogue) equals the
-    shape rule's (variant 5, itself bitwise variant 4)."""
+    unsplit kernels' (variant 5, itself bitwise variant 4; for this small grid the shape rule would
+    pick the split-K mode, variant 10)."""
     g = torch.Generator().manual_seed(rp)
     M, N, K = 512, 384, 1024
     A = torch.randn(M, K, generator=g).to(torch.bfloat16).cuda()
@@ -277,7 +278,7 @@ def test_gemm_register_prefetch_is_bitwise_variant3(rp, epi):
     Bkn = torch.randn(K, N, generator=g).to(torch.bfloat16).cuda()
     C0 = torch.empty(M, N, dtype=torch.bfloat16).cuda()
     C1 = torch.empty(M, N, dtype=torch.bfloat16).cuda()
-    gemm_nt(A, Bkn, C=C0, b_kn=True, variant=0)
+    gemm_nt(A, Bkn, C=C0, b_kn=True, variant=5)
     gemm_nt(A, Bkn, C=C1, b_kn=True, variant=rp)
     assert torch.equal(C0, C1)
     mask = (torch.randn(M, N, generator=g) > 0).to(torch.bfloat16).cuda()
