@@ -213,3 +213,48 @@ def test_gemm_skn_rejects_grids_it_does_not_fit():
     B = torch.randn(4096, 4096, device="cuda").bfloat16()  # 256 tiles: the grid already fills the chip
     with pytest.raises(RuntimeError, match="split-K mode"):
         gemm_nt(A, B, C=torch.empty(1024, 4096, device="cuda").bfloat16(), variant=10)
+
+
+@pytest.mark.parametrize("mode", ["graph_module", "hip_graph"])
+def test_engine_bf16_small_batch_split_k_under_graph_capture(mode):
+    """The engine's bf16 chain at batch 128 on 1024-wide layers runs its products on the split-K
+    mode (8 tiles -> split 2); under graph_module / the whole-step graph its per-stream workspace is
+    first allocated inside a capture.  Both graphed trajectories follow the eager engine's."""
+    import distributed_gpu_test_amd as dgt
+    from distributed_gpu_test_amd.models.synthetic_mlp import SyntheticMLP
+    from distributed_gpu_test_amd.ops import BCEWithLogitsLoss
+
+    def run(amd):
+        torch.manual_seed(9)
+        m = SyntheticMLP(width=1024, depth=2)
+        cfg = {"train_micro_batch_size_per_gpu": 128, "bf16": {"enabled": True},
+               "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}, "amd": amd}
+        engine, _, _, _ = dgt.initialize(model=m, config=cfg)
+        crit = BCEWithLogitsLoss()
+        g = torch.Generator().manual_seed(10)
+        batches = [(torch.randn(128, 1024, generator=g).cuda().bfloat16(), (torch.rand(128, generator=g) > 0.5).float().cuda())
+                   for _ in range(8)]
+        losses = []
+        if amd.get("hip_graph"):
+            step = engine.graph_step(lambda bx, by: crit(engine(bx).view(-1), by))
+            assert engine.graphed is not None, engine.graph_fallback_reason
+            for x, y in batches:
+                losses.append(float(step(x, y)))
+        else:
+            for x, y in batches:
+                loss = crit(engine(x).view(-1), y)
+                engine.backward(loss)
+                engine.step()
+                losses.append(float(loss))
+        return engine, losses, engine.store.param_buf.detach().float().clone()
+
+    e1, l1, p1 = run({})
+    e2, l2, p2 = run({mode: True})
+    if mode == "graph_module":
+        assert e2.graph_module, e2.graph_module_reason
+    else:
+        assert e2.graphed.replays >= 6 and not e2.graphed.failed, (e2.graphed.replays, e2.graphed.failed)
+    torch.testing.assert_close(torch.tensor(l2), torch.tensor(l1), rtol=2e-2, atol=2e-3)
+    torch.testing.assert_close(p2, p1, rtol=2e-2, atol=2e-3)
+    e1.close()
+    e2.close()
