@@ -743,11 +743,12 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
              const std::optional<at::Tensor>& colsum) {
   TORCH_CHECK(!(epi & dgt::kEpiBKN) || (variant != 2 && variant != 8),
               "dgt: a [K, N] B operand runs on the 128x128 kernels only");
-  TORCH_CHECK(variant >= 0 && variant <= 10,
+  TORCH_CHECK(variant >= 0 && variant <= 11,
               "dgt: gemm_nt variant must be 0 (auto), 1 (128x128, 2 stages), 2 (256x256), 3 (4 with front-loaded "
               "fragment reads), 4 (128x128, 4 stages, 8 waves), 5 (software-pipelined reads), 6 / 7 (register "
               "prefetch, 2 / 4 K-tiles), 8 (256x256 with cross-phase fragment prefetch), 9 (256x128 split-K 2) or "
-              "10 (128x128 split-K for small grids); the round-2 variants live in git history (commit c0371a5)");
+              "10 (128x128 split-K for small grids) or 11 (256x256 split-K 2); the round-2 variants live in git history "
+              "(commit c0371a5)");
   const bool b_kn = (epi & dgt::kEpiBKN) != 0;
   TORCH_CHECK(A.dim() == 2 && B.dim() == 2 && A.size(1) == B.size(b_kn ? 0 : 1),
               b_kn ? "dgt: gemm_nt with kEpiBKN needs A[M,K], B[K,N]" : "dgt: gemm_nt needs A[M,K], B[N,K]");
@@ -809,11 +810,17 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
   if (variant == 2 || variant == 8)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
   const hipStream_t stream = stream_of(A);
-  const int skn = dgt::gemm_nt_uses_skn(g, (int)epi, (int)variant);
+  const int spk256 = dgt::gemm_nt_uses_spk256(g, (int)epi, (int)variant);
+  TORCH_CHECK(variant != 11 || spk256, "dgt: the 256x256 split-K mode (variant 11) needs M, N % 256 == 0, K % 256 == 0, "
+              "an [N, K] B and a bf16 (staged) epilogue without column sums");
+  const int skn = spk256 ? 0 : dgt::gemm_nt_uses_skn(g, (int)epi, (int)variant);
   TORCH_CHECK(variant != 10 || skn > 0,
               "dgt: the 128x128 split-K mode (variant 10) needs a bf16 (staged) epilogue and a grid of at most 128 "
               "tiles with at least 16 K-tiles");
-  if (skn > 0) {
+  if (spk256) {
+    const int64_t tiles = (int64_t)(M / 256) * (N / 256);
+    attach_sk_workspace(g, A, stream, tiles * 2 * 256 * 256, tiles);
+  } else if (skn > 0) {
     g.skn_split = skn;
     const int64_t tiles = (int64_t)(M / 128) * (N / 128);
     attach_sk_workspace(g, A, stream, tiles * skn * 128 * 128, tiles);

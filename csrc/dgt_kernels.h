@@ -205,6 +205,10 @@ hipError_t gemm_nt(const GemmArgs& g, int epilogue, hipStream_t stream, int vari
 // sk_slab (tiles x split x 128 x 128 fp32) and sk_flags (tiles ints, zero between launches)
 int gemm_nt_skn_split(const GemmArgs& g, int epilogue);
 int gemm_nt_uses_skn(const GemmArgs& g, int epilogue, int variant);
+// the 256 x 256 kernel's split-K 2 mode (variant 11; the shape rule's for 100-128 tiles of 256 x 256):
+// 1 if it runs for these arguments (the caller provides sk_slab: tiles x 2 x 256 x 256 fp32, sk_flags:
+// tiles ints)
+int gemm_nt_uses_spk256(const GemmArgs& g, int epilogue, int variant);
 // the split-K kernel's shape rule (256 x 128 tiles, a multiple of 8 of them, K % 128 == 0, staged
 // bf16 epilogue); the caller provides sk_slab / sk_flags for (M / 256) * (N / 128) tiles
 bool gemm_nt_sk_fits(const GemmArgs& g, int epilogue);

@@ -1485,17 +1485,24 @@ DGT_DEVICE void iteration_x(const Ctx& c, int it, FragsX& f, f32x4 (&acc)[8][4])
 }
 }  // namespace g256
 
-template <int EPI, bool XP = false>
+// SPK (split-K 2, grids of 100-128 tiles, e.g. M = 1024 x N = 8192): two blocks per tile, each over
+// half of K -- half the operand bytes per CU of the 128 x 128 kernel's two waves of blocks.  Each
+// writes its fp32 partial (256 KiB, write-through sc1), drains and adds to the tile's counter; the
+// second to add sums the other's partial into its accumulators (fp32 a + b == b + a: the bits do not
+// depend on the order), re-arms the counter and runs the epilogue.
+template <int EPI, bool XP = false, bool SPK = false>
 __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   using namespace g256;
   __shared__ __attribute__((aligned(16))) u16 lds[2 * 4 * UNIT];
   const int tid = threadIdx.x;
+  const int tile = SPK ? (int)blockIdx.x >> 1 : (int)blockIdx.x, slice = SPK ? (int)blockIdx.x & 1 : 0;
   int tm, tn;
-  tile_of_block(blockIdx.x, g.M / BM, g.N / BN, tm, tn);
+  tile_of_block(tile, g.M / BM, g.N / BN, tm, tn);
   const int m0 = tm * BM, n0 = tn * BN;
+  const int kslice = SPK ? g.K / 2 : g.K;
   Ctx c;
-  c.A = static_cast<const u16*>(g.A) + (long long)m0 * g.lda;
-  c.B = static_cast<const u16*>(g.B) + (long long)n0 * g.ldb;
+  c.A = static_cast<const u16*>(g.A) + (long long)m0 * g.lda + (long long)slice * kslice;
+  c.B = static_cast<const u16*>(g.B) + (long long)n0 * g.ldb + (long long)slice * kslice;
   c.lda = g.lda;
   c.ldb = g.ldb;
   c.w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1528,7 +1535,7 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   wait_vm<8>();
   __builtin_amdgcn_s_barrier();
 
-  const int nit = g.K / (2 * BK);
+  const int nit = kslice / (2 * BK);
   if constexpr (XP) {
     // phase 1's fragments (tile 0's A_lo and B_lo, retired by the wait above)
     FragsX fx;
@@ -1540,6 +1547,41 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
   } else {
     for (int it = 0; it + 1 < nit; ++it) iteration<false>(c, it, f, acc);
     iteration<true>(c, nit - 1, f, acc);
+  }
+
+  if constexpr (SPK) {
+    auto part = [&](int q) {
+      return __builtin_amdgcn_make_buffer_rsrc(g.sk_slab + ((long long)tile * 2 + q) * (BM * BN), 0, BM * BN * 4,
+                                               0x00020000);
+    };
+    const auto mine = part(slice);
+#pragma unroll
+    for (int i = 0; i < 8; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4, acc[i][j]), mine,
+                                               ((i * 4 + j) * 512 + tid) * 16, 0, 16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+    __syncthreads();                                  // (and every wave is past its last LDS read)
+    int* word = reinterpret_cast<int*>(lds);
+    if (tid == 0) *word = __hip_atomic_fetch_add(g.sk_flags + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*word == 0) return;  // the other half finishes the tile
+    if (tid == 0) __hip_atomic_store(g.sk_flags + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // re-arm
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");  // sc1 loads behind the counter's add + barrier
+    const auto other = part(slice ^ 1);
+    // one accumulator row at a time: the accumulators hold 128 VGPRs, so all 32 loads in flight at
+    // once would spill
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      f32x4 p[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        p[j] = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(other, ((i * 4 + j) * 512 + tid) * 16, 0, 16));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) acc[i][j] += p[j];
+      __builtin_amdgcn_sched_barrier(0);
+    }
   }
 
   if constexpr ((EPI & kEpiAdam) != 0) {
@@ -1621,6 +1663,18 @@ static bool skn_auto() {
   return on != 0;
 }
 
+// The 256 x 256 kernel's split-K 2 mode (variant 11; the shape rule's choice, DGT_GEMM_SKN=1, for
+// 100-128 tiles of 256 x 256 with an [N, K] B, a staged bf16 epilogue and K / 2 a multiple of 128, at
+// least 1024): M = 1024 x N = 8192 or M = 2048 x N = 4096.
+int gemm_nt_uses_spk256(const GemmArgs& g, int epi, int variant) {
+  if (variant != 11 && (variant != 0 || !skn_auto())) return 0;
+  if (epi & (kEpiOutF32 | kEpiAccumulate | kEpiAdam | kEpiBKN | kEpiColSum)) return 0;
+  if (g.M % 256 || g.N % 256 || g.K % 256 || g.lda > (1 << 22) || g.ldb > (1 << 22)) return 0;
+  const int tiles = (g.M / 256) * (g.N / 256);
+  if (variant == 11) return tiles * 2 <= 1024 ? 1 : 0;
+  return (tiles >= 100 && tiles <= 128 && g.K / 2 >= 1024) ? 1 : 0;
+}
+
 int gemm_nt_uses_skn(const GemmArgs& g, int epi, int variant) {
   if (variant == 10) return gemm_nt_skn_split(g, epi);
   if (variant != 0 || !skn_auto() || (g.M / GBM) * (g.N / GBN) > 128) return 0;
@@ -1629,7 +1683,27 @@ int gemm_nt_uses_skn(const GemmArgs& g, int epi, int variant) {
 
 hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) {
   if (g.M % GBM || g.N % GBN || g.K % GBK || g.M <= 0 || g.N <= 0 || g.K <= 0) return hipErrorInvalidValue;
-  if (variant < 0 || variant > 10) return hipErrorInvalidValue;
+  if (variant < 0 || variant > 11) return hipErrorInvalidValue;
+  if (gemm_nt_uses_spk256(g, epi, variant)) {
+    if (!g.sk_slab || !g.sk_flags) return hipErrorInvalidValue;
+    const int grid = (g.M / 256) * (g.N / 256) * 2;
+    switch (epi) {
+#define DGT_SPK256_CASE(E)                                                                             \
+  case E:                                                                                              \
+    hipLaunchKernelGGL((gemm_nt_256_kernel<E, true, true>), dim3(grid), dim3(512), 0, stream, g);      \
+    return hipGetLastError();
+      DGT_SPK256_CASE(0)
+      DGT_SPK256_CASE(kEpiBias | kEpiRelu | kEpiStoreT)
+      DGT_SPK256_CASE(kEpiBias | kEpiRelu)
+      DGT_SPK256_CASE(kEpiBias | kEpiStoreT)
+      DGT_SPK256_CASE(kEpiBias)
+      DGT_SPK256_CASE(kEpiMask | kEpiStoreT)
+#undef DGT_SPK256_CASE
+      default:
+        return hipErrorInvalidValue;
+    }
+  }
+  if (variant == 11) return hipErrorInvalidValue;
   if (variant == 10 || (variant == 0 && gemm_nt_uses_skn(g, epi, 0))) {
     const int split = gemm_nt_skn_split(g, epi);
     if (!split || g.skn_split != split || !g.sk_slab || !g.sk_flags) return hipErrorInvalidValue;

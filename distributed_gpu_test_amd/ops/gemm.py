@@ -66,7 +66,10 @@ def gemm_nt(A: torch.Tensor, B: torch.Tensor, C: Optional[torch.Tensor] = None, 
     (``profiles/r6_gemm_m1024_splitk.jsonl``),
     10 = the 128x128 kernel with K split 2 / 4 / 8 ways for grids of at most 128 tiles (small M): the
     slices meet in-launch, the last to arrive sums them in slice order (deterministic) -- the shape
-    rule's choice there (``DGT_GEMM_SKN=0`` turns it off).
+    rule's choice there (``DGT_GEMM_SKN=0`` turns it off),
+    11 = the 256x256 kernel with K split in two (NT, staged bf16 epilogues without column sums; the
+    second block to finish adds the first's fp32 partial): the shape rule's choice for 100-128 tiles
+    of 256x256, e.g. 1024 x 8192 (``profiles/r6_gemm_wide_8192.jsonl``).
     ``DGT_GEMM_VARIANT`` (A/B runs) replaces variant 0 for grids of at most 256 tiles (the shapes
     the shape rule gives to the 128x128 kernels).
 

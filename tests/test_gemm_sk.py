@@ -258,3 +258,40 @@ def test_engine_bf16_small_batch_split_k_under_graph_capture(mode):
     torch.testing.assert_close(p2, p1, rtol=2e-2, atol=2e-3)
     e1.close()
     e2.close()
+
+
+# ---- the 256x256 kernel's split-K 2 mode (variant 11): 100-128 tiles of 256x256 (M = 1024 x N = 8192)
+SPK256_EPIS = ["plain", "bias_relu_T", "bias_relu", "bias_T", "bias", "mask_T"]
+
+
+@pytest.mark.parametrize("M,N,K", [(512, 1024, 1024), (1024, 8192, 2048), (2048, 4096, 4096)])
+@pytest.mark.parametrize("epi", SPK256_EPIS)
+def test_gemm_spk256_matches_fp32_reference(M, N, K, epi):
+    A, B, Bkn, bias, mask = _operands(M, N, K, 5 * M + N + K)
+    C, CT, _, kw = _run(epi, A, B, Bkn, bias, mask, 11)
+    ref = gemm_nt_reference(A, B, **kw)
+    torch.testing.assert_close(C.float(), ref.to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2 * K ** 0.5)
+    if CT is not None:
+        assert torch.equal(CT, C.t())
+
+
+def test_gemm_spk256_deterministic_close_to_unsplit_and_picked_by_the_shape_rule():
+    import os
+    A, B, Bkn, bias, mask = _operands(1024, 8192, 4096, 23)
+    first = _run("bias_relu_T", A, B, Bkn, bias, mask, 11)
+    for _ in range(5):
+        again = _run("bias_relu_T", A, B, Bkn, bias, mask, 11)
+        assert torch.equal(first[0], again[0]) and torch.equal(first[1], again[1])
+    C8 = _run("bias_relu_T", A, B, Bkn, bias, mask, 8)[0].float()
+    d = (first[0].float() - C8).abs()
+    assert float((d > 0).float().mean()) < 0.05
+    assert float((d / C8.abs().clamp_min(1.0)).max()) <= 2 ** -7
+    if os.environ.get("DGT_GEMM_SKN", "1") != "0" and not os.environ.get("DGT_GEMM_VARIANT"):
+        assert torch.equal(_run("bias_relu_T", A, B, Bkn, bias, mask, 0)[0], first[0])
+
+
+def test_gemm_spk256_rejects_a_kn_operand():
+    A = torch.randn(1024, 2048, device="cuda").bfloat16()
+    Bkn = torch.randn(2048, 8192, device="cuda").bfloat16()
+    with pytest.raises(RuntimeError):
+        gemm_nt(A, Bkn, C=torch.empty(1024, 8192, device="cuda").bfloat16(), b_kn=True, variant=11)
