@@ -118,7 +118,7 @@ def engine_mlp_case(dtype, stage):
     return fn
 
 
-def engine_fuzz_case(dtype, stage, gas, seed, steps=24):
+def engine_fuzz_case(dtype, stage, gas, seed, steps=24, width=256):
     """The engine MLP (fused chains, one bucket per layer) through seeded random transitions --
     batch 128 / 256, the fused or torch's BCE, a no-grad forward in between, a retained graph taken
     backward twice, lr changes, extra zero_grad calls -- so that the reducer's per-layer launches,
@@ -133,7 +133,7 @@ def engine_fuzz_case(dtype, stage, gas, seed, steps=24):
     def fn():
         torch.manual_seed(100 + seed)
         rnd = random.Random(seed)
-        m = SyntheticMLP(width=256, depth=3)
+        m = SyntheticMLP(width=width, depth=3)
         cfg = {"train_micro_batch_size_per_gpu": 128, "gradient_accumulation_steps": gas,
                "zero_optimization": {"stage": stage, "reduce_bucket_size": 4096},
                "optimizer": {"type": "Adam", "params": {"lr": 1e-3}}}
@@ -146,7 +146,7 @@ def engine_fuzz_case(dtype, stage, gas, seed, steps=24):
         for _ in range(steps * gas):
             b = rnd.choice([128, 256])
             counts["b256"] += b == 256
-            x = torch.randn(b, 256, generator=g).cuda().to(engine.dtype)
+            x = torch.randn(b, width, generator=g).cuda().to(engine.dtype)
             y = (torch.rand(b, generator=g) > 0.5).float().cuda()
             if rnd.random() < 0.15:
                 counts["eval"] += 1
@@ -180,12 +180,15 @@ def engine_fuzz_case(dtype, stage, gas, seed, steps=24):
 
 
 def fuzz_cases(names):
-    """fuzz_<bf16|fp32>_zero<stage>_gas<gas>_s<seed> -> the case (requested by name only)."""
+    """fuzz_<bf16|fp32>_zero<stage>_gas<gas>_s<seed>[_w<width>] -> the case (requested by name only;
+    width 1024 puts the bf16 chain's products on the GEMM's small-grid split-K mode)."""
     out = {}
     for n in names:
         if n.startswith("fuzz_"):
-            _, dtype, z, ga, sd = n.split("_")
-            out[n] = engine_fuzz_case(dtype, int(z[4:]), int(ga[3:]), int(sd[1:]))
+            parts = n.split("_")
+            _, dtype, z, ga, sd = parts[:5]
+            width = int(parts[5][1:]) if len(parts) > 5 else 256
+            out[n] = engine_fuzz_case(dtype, int(z[4:]), int(ga[3:]), int(sd[1:]), width=width)
     return out
 
 

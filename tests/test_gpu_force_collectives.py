@@ -40,6 +40,8 @@ def test_forced_collectives_bit_identical_on_one_gpu():
 
 
 FUZZ = [f"fuzz_{d}_zero{z}_gas{g}_s{s}" for d in ("bf16", "fp32") for z in (0, 1) for g in (1, 2) for s in (0, 1)]
+# the bf16 chain on 1024-wide layers: its products run on the GEMM's small-grid split-K mode
+FUZZ += [f"fuzz_bf16_zero{z}_gas{g}_s2_w1024" for z in (0, 1) for g in (1, 2)]
 
 
 def test_forced_collectives_fuzz_bit_identical():
