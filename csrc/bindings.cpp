@@ -714,6 +714,7 @@ void check_2d(const at::Tensor& t, const char* name, at::ScalarType dt, int64_t 
 // tensors must not be freed into the caching allocator during static destruction at exit.
 struct SkWorkspace {
   at::Tensor slab, flags;
+  at::Tensor bt;  // B^T of a [K, N] operand run as NT (gemm_nt_kn_transposes)
 };
 std::mutex g_sk_mu;
 auto* g_sk_ws = new std::map<std::pair<int, hipStream_t>, SkWorkspace>();
@@ -810,6 +811,20 @@ void gemm_nt(const at::Tensor& A, const at::Tensor& B, const std::optional<at::T
   if (variant == 2 || variant == 8)
     TORCH_CHECK(M % 256 == 0 && N % 256 == 0 && K % 128 == 0, "dgt: the 256x256 gemm needs M, N % 256 == 0, K % 128 == 0");
   const hipStream_t stream = stream_of(A);
+  if (dgt::gemm_nt_kn_transposes(g, (int)epi, (int)variant)) {
+    // B [K, N] -> B^T [N, K] in this stream's workspace, then the NT product (256 x 256 kernels)
+    void* bt = nullptr;
+    {
+      std::lock_guard<std::mutex> lock(g_sk_mu);
+      SkWorkspace& w = (*g_sk_ws)[{(int)A.device().index(), stream}];
+      if (!w.bt.defined() || w.bt.numel() < K * N) w.bt = at::empty({K * N}, A.options());
+      bt = w.bt.data_ptr();
+    }
+    DGT_CHECK_HIP(dgt::transpose_bf16(g.B, bt, (int)K, (int)N, stream));
+    g.B = bt;
+    g.ldb = (int)K;
+    epi &= ~(int64_t)dgt::kEpiBKN;
+  }
   const int spk256 = dgt::gemm_nt_uses_spk256(g, (int)epi, (int)variant);
   TORCH_CHECK(variant != 11 || spk256, "dgt: the 256x256 split-K mode (variant 11) needs M, N % 256 == 0, K % 256 == 0, "
               "an [N, K] B and a bf16 (staged) epilogue without column sums");

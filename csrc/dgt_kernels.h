@@ -209,6 +209,9 @@ int gemm_nt_uses_skn(const GemmArgs& g, int epilogue, int variant);
 // 1 if it runs for these arguments (the caller provides sk_slab: tiles x 2 x 256 x 256 fp32, sk_flags:
 // tiles ints)
 int gemm_nt_uses_spk256(const GemmArgs& g, int epilogue, int variant);
+// whether a [K, N]-B product should be run as NT on B^T (a grid larger than the chip; the caller
+// transposes B into a [N, K] workspace with transpose_bf16 and calls gemm_nt without kEpiBKN)
+bool gemm_nt_kn_transposes(const GemmArgs& g, int epilogue, int variant);
 // the split-K kernel's shape rule (256 x 128 tiles, a multiple of 8 of them, K % 128 == 0, staged
 // bf16 epilogue); the caller provides sk_slab / sk_flags for (M / 256) * (N / 128) tiles
 bool gemm_nt_sk_fits(const GemmArgs& g, int epilogue);

@@ -1675,6 +1675,22 @@ int gemm_nt_uses_spk256(const GemmArgs& g, int epi, int variant) {
   return (tiles >= 100 && tiles <= 128 && g.K / 2 >= 1024) ? 1 : 0;
 }
 
+// A [K, N] B operand on a grid of at least 200 tiles of 256 x 256 (batch 4096 on 4096-wide layers,
+// 2048 on 8192-wide ones) is transposed once (transpose_bf16, into the caller's workspace) and the product
+// runs as NT on the 256 x 256 kernels: 4096^3 dgrad 167-172 -> ~110 us (hipBLASLt 107), 2048 x 8192
+// 279-283 -> ~235.  DGT_GEMM_KN_T=0 keeps the 128 x 128 [K, N] kernels.  (variant 0, B contiguous.)
+bool gemm_nt_kn_transposes(const GemmArgs& g, int epi, int variant) {
+  static const int on = [] {
+    const char* e = std::getenv("DGT_GEMM_KN_T");
+    return (e && *e) ? std::atoi(e) : 1;
+  }();
+  if (!on || variant != 0 || !(epi & kEpiBKN) || (epi & (kEpiOutF32 | kEpiAccumulate | kEpiAdam))) return false;
+  if (g.M % 256 || g.N % 256 || g.K % 256 || g.ldb != g.N || g.K > (1 << 22)) return false;
+  // the NT product must land on the 256 x 256 kernel's full grid (>= 200 tiles); at 100-128 tiles
+  // (2048 x 4096) transpose + split-K 2 measured level with the [K, N] 128 x 128 kernel
+  return (g.M / 256) * (g.N / 256) >= 200;
+}
+
 int gemm_nt_uses_skn(const GemmArgs& g, int epi, int variant) {
   if (variant == 10) return gemm_nt_skn_split(g, epi);
   if (variant != 0 || !skn_auto() || (g.M / GBM) * (g.N / GBN) > 128) return 0;
@@ -1756,8 +1772,8 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
   // MLP's wgrad 31.6-31.9 vs 33.0-33.7 us (profiles/r4_gemm256_xp.jsonl)
   const bool xp = variant != 2;
   if (variant == 8) variant = 2;
-  // only the 128x128 kernels read a [K, N] B operand or form column sums
-  const bool kn = (epi & (kEpiBKN | kEpiColSum)) != 0;
+  // only the 128x128 kernels read a [K, N] B operand (column sums: both tile sizes)
+  const bool kn = (epi & kEpiBKN) != 0;
   if ((epi & kEpiColSum) && (!(epi & kEpiStoreT) || !g.colsum)) return hipErrorInvalidValue;
   // variants 6 / 7: the register-prefetch 128x128 kernel (2 / 4 K-tiles in VGPRs) for NT products
   // with forward-type epilogues and K a multiple of 2 / 4 K-tiles; any other product asked for it
@@ -1816,6 +1832,8 @@ hipError_t gemm_nt(const GemmArgs& g, int epi, hipStream_t stream, int variant) 
     DGT_EPI_CASE(kEpiBias | kEpiStoreT)                            // linear forward (no ReLU)
     DGT_EPI_CASE(kEpiBias)
     DGT_EPI_CASE(kEpiMask | kEpiStoreT)                            // dgrad through ReLU
+    DGT_EPI_CASE(kEpiMask | kEpiStoreT | kEpiColSum)               // + bias-gradient partials (W^T given)
+    DGT_EPI_CASE(kEpiStoreT)                                       // product + C^T (a transposed [K, N] dgrad)
     DGT_EPI_CASE(kEpiOutF32)                                       // wgrad into fp32 grads
     DGT_EPI_CASE(kEpiOutF32 | kEpiAccumulate)                      // wgrad, gradient accumulation
     DGT_EPI_CASE(kEpiOutF32 | kEpiBias)                            // generic fp32 out

@@ -295,3 +295,24 @@ def test_gemm_spk256_rejects_a_kn_operand():
     Bkn = torch.randn(2048, 8192, device="cuda").bfloat16()
     with pytest.raises(RuntimeError):
         gemm_nt(A, Bkn, C=torch.empty(1024, 8192, device="cuda").bfloat16(), b_kn=True, variant=11)
+
+
+# ---- a [K, N] operand on a 256x256-sized grid: transposed once, then the NT 256x256 kernel
+@pytest.mark.parametrize("M,N,K", [(4096, 4096, 1024), (2048, 8192, 512)])
+@pytest.mark.parametrize("epi", ["kn_plain", "kn_T", "kn_mask_T", "kn_mask_T_colsum"])
+def test_gemm_kn_large_grid_runs_transposed_and_matches_reference(M, N, K, epi):
+    import os
+    A, B, Bkn, bias, mask = _operands(M, N, K, 7 * M + N + K)
+    C, CT, cs, kw = _run(epi, A, B, Bkn, bias, mask, 0)
+    ref = gemm_nt_reference(A, Bkn, b_kn=True, **kw)
+    torch.testing.assert_close(C.float(), ref.to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2 * K ** 0.5)
+    if CT is not None:
+        assert torch.equal(CT, C.t())
+    if cs is not None:
+        torch.testing.assert_close(cs, C.float().view(M // 128, 128, N).sum(1), rtol=1e-5, atol=1e-3)
+    if cs is None and os.environ.get("DGT_GEMM_KN_T", "1") != "0" and not os.environ.get("DGT_GEMM_VARIANT"):
+        # the same bits as the NT product on an explicit B^T (the 256x256 kernel)
+        C2 = torch.empty_like(C)
+        CT2 = torch.empty_like(CT) if CT is not None else None
+        gemm_nt(A, Bkn.t().contiguous(), C=C2, CT=CT2, variant=8, **kw)
+        assert torch.equal(C, C2)
