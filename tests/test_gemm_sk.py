@@ -316,3 +316,31 @@ def test_gemm_kn_large_grid_runs_transposed_and_matches_reference(M, N, K, epi):
         CT2 = torch.empty_like(CT) if CT is not None else None
         gemm_nt(A, Bkn.t().contiguous(), C=C2, CT=CT2, variant=8, **kw)
         assert torch.equal(C, C2)
+
+
+@pytest.mark.parametrize("path", ["skn", "spk256", "kn_large"])
+def test_gemm_split_paths_read_strided_operands(path):
+    """Row-strided operands (column blocks of a wider matrix) on every split / transposed path: the
+    K-slice offsets and the staging use the row strides, and a strided [K, N] operand keeps the
+    [K, N] kernels (the transposition needs a contiguous one)."""
+    g = torch.Generator().manual_seed(31)
+    if path == "skn":
+        M, N, K = 256, 4096, 4096
+    elif path == "spk256":
+        M, N, K = 1024, 8192, 2048
+    else:
+        M, N, K = 4096, 4096, 1024
+    Aw = torch.randn(M, K + 256, generator=g).to(torch.bfloat16).cuda()
+    A = Aw[:, 128:128 + K]
+    C = torch.empty(M, N, device="cuda", dtype=torch.bfloat16)
+    if path == "kn_large":
+        Bw = torch.randn(K, N + 256, generator=g).to(torch.bfloat16).cuda()
+        B = Bw[:, 64:64 + N]
+        gemm_nt(A, B, C=C, b_kn=True)
+        ref = A.float() @ B.float()
+    else:
+        Bw = torch.randn(N, K + 128, generator=g).to(torch.bfloat16).cuda()
+        B = Bw[:, 64:64 + K]
+        gemm_nt(A, B, C=C)
+        ref = A.float() @ B.float().t()
+    torch.testing.assert_close(C.float(), ref.to(torch.bfloat16).float(), rtol=2e-2, atol=2e-2 * K ** 0.5)
