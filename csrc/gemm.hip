@@ -1588,6 +1588,8 @@ __global__ __launch_bounds__(512) void gemm_nt_256_kernel(GemmArgs g) {
     // fp32 256 x 256 tile = 256 KiB: two passes of 128 rows through the 128 KiB of operand LDS
     epilogue_adam<BM, BN, 128, 64, 512, 128>(g, acc, reinterpret_cast<float*>(lds), m0, n0, c.wr, c.wc, c.l, tid);
   } else if constexpr (!(EPI & kEpiOutF32)) {
+    // (bias and mask loaded together ahead of the epilogue (EpiPre, PRE = true): 1.5-2 % on the
+    // large transposed dgrads, with 4-13 more spilled VGPRs -- not kept)
     epilogue_staged<EPI, BM, BN, 128, 64, 512>(g, acc, lds, m0, n0, c.wr, c.wc, c.l, tid, EpiPre<EPI, BM, BN, 64, 512>{});
   } else {
 #pragma unroll
