@@ -163,8 +163,10 @@ def _small(x: torch.Tensor, weight: torch.Tensor) -> bool:
 
 
 def _skinny(x: torch.Tensor, weight: torch.Tensor) -> bool:
-    """A head Linear(K, N <= 4) beyond the small-batch kernels: two bandwidth passes over x
-    (``csrc/head.hip`` skinny_f32), not 64 x 64 MFMA tiles with one useful column."""
+    """A head Linear(K, N <= 4) with whole 64-row blocks: two bandwidth passes over x (``csrc/head.hip``
+    skinny_f32), not 64 x 64 MFMA tiles with one useful column.  Checked before ``_small``: the
+    small-batch kernels walk K serially per output, 55-75 us for Linear(1024, 1) at M = 256 against
+    a few us here (profiles/r6_fp32_head_batch256.txt)."""
     return (weight.shape[0] <= 4 and x.shape[0] % 64 == 0 and x.shape[1] % 32 == 0
             and x.data_ptr() % 16 == 0 and weight.data_ptr() % 16 == 0)
 
@@ -182,10 +184,10 @@ def _fwd(ops, x, weight, bias, relu: bool) -> torch.Tensor:
     """y = act(x W^T + b): the small-batch kernel, the skinny head kernel or the tiled fp32 MFMA GEMM
     (bias/ReLU epilogue)."""
     y = torch.empty(x.shape[0], weight.shape[0], dtype=torch.float32, device=x.device)
-    if _small(x, weight):
-        ops.linear_fwd(x, weight, bias, y, relu)
-    elif _skinny(x, weight):
+    if _skinny(x, weight):
         ops.skinny_f32_fwd(x, weight, bias, y, relu)
+    elif _small(x, weight):
+        ops.linear_fwd(x, weight, bias, y, relu)
     else:
         ops.gemm_f32(x, weight, None, bias, y, 0, 0, relu, False)
     return y
@@ -199,12 +201,12 @@ def _bwd(ops, dy, x, weight, y, dx, dW, db, accumulate: bool = False, mask_dx=No
     ``mask_dx`` (the layer below's ReLU output): the tiled dgrad stores dx * 1[mask_dx > 0], the
     gradient the layer below needs, so that layer reads no mask.  Returns whether it did (the
     small-batch kernel does not)."""
-    if _small(x, weight):
-        ops.linear_bwd(dy, x, weight, y, dx, dW, db, accumulate)
-        return False
     if _skinny(x, weight) and dW.data_ptr() % 16 == 0 and (mask_dx is None or mask_dx is x):
         ops.skinny_f32_bwd(dy, y, x, weight, mask_dx is not None, dx, dW, db, accumulate)
         return dx is not None and mask_dx is not None
+    if _small(x, weight):
+        ops.linear_bwd(dy, x, weight, y, dx, dW, db, accumulate)
+        return False
     if dx is not None:
         ops.gemm_f32(dy, weight, y, None, dx, 0, 1, False, False, None, mask_dx)
     if _FUSED_ROWSUM:
