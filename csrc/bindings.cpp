@@ -15,6 +15,7 @@
 #include <mutex>
 #include <cstring>
 #include <string>
+#include <tuple>
 #include <vector>
 
 #include "dgt_kernels.h"
@@ -419,6 +420,9 @@ void linear_bwd(const at::Tensor& dy, const at::Tensor& x, const at::Tensor& W, 
                                 stream_of(x)));
 }
 
+std::pair<float*, int*> sk_workspace(const at::Tensor& like, hipStream_t stream, int64_t slab_floats,
+                                     int64_t flag_ints);  // (below, with the bf16 split-K's)
+
 // Exact-fp32 MFMA GEMM (gemm_f32.hip): C[M, N] (+)= epi(A . B) with A [M, K] (la 0) or [K, M] (la 1),
 // B [N, K] (lb 0) or [K, N] (lb 1), all contiguous; one launch (K splits inside the workgroup).
 void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::Tensor>& maskA,
@@ -482,8 +486,19 @@ void gemm_f32(const at::Tensor& A, const at::Tensor& B, const std::optional<at::
     const char* e = std::getenv("DGT_F32_CFG");
     return e && *e ? std::atoi(e) : -1;
   }();
+  // DGT_F32_SPLIT (A/B knob, read once): 0 / 1 = no cross-workgroup split-K, n > 1 = at most n
+  static const int force_split = [] {
+    const char* e = std::getenv("DGT_F32_SPLIT");
+    return e && *e ? std::atoi(e) : -1;
+  }();
   const dgt::GemmF32Plan plan = dgt::gemm_f32_plan(a.M, a.N, a.K, force_cfg);
-  DGT_CHECK_HIP(dgt::gemm_f32(a, (int)la, (int)lb, plan, stream_of(A)));
+  const hipStream_t stream = stream_of(A);
+  a.split = a.rowsum ? 1 : dgt::gemm_f32_split(a.M, a.N, a.K, plan, force_split);
+  if (a.split > 1) {
+    const int64_t tiles = ((M + 63) / 64) * ((N + 63) / 64);
+    std::tie(a.sk_slab, a.sk_flags) = sk_workspace(A, stream, tiles * a.split * 64 * 64, tiles);
+  }
+  DGT_CHECK_HIP(dgt::gemm_f32(a, (int)la, (int)lb, plan, stream));
 }
 
 // db[n] (+)= sum_m dy[m][n] (* 1[y[m][n] > 0]), deterministic two-pass column sum
@@ -719,8 +734,8 @@ struct SkWorkspace {
 std::mutex g_sk_mu;
 auto* g_sk_ws = new std::map<std::pair<int, hipStream_t>, SkWorkspace>();
 
-void attach_sk_workspace(dgt::GemmArgs& g, const at::Tensor& like, hipStream_t stream, int64_t slab_floats,
-                         int64_t flag_ints) {
+std::pair<float*, int*> sk_workspace(const at::Tensor& like, hipStream_t stream, int64_t slab_floats,
+                                     int64_t flag_ints) {
   std::lock_guard<std::mutex> lock(g_sk_mu);
   SkWorkspace& w = (*g_sk_ws)[{(int)like.device().index(), stream}];
   if (!w.slab.defined() || w.slab.numel() < slab_floats || w.flags.numel() < flag_ints) {
@@ -729,8 +744,12 @@ void attach_sk_workspace(dgt::GemmArgs& g, const at::Tensor& like, hipStream_t s
     w.slab = at::empty({sf}, like.options().dtype(at::kFloat));
     w.flags = at::zeros({fi}, like.options().dtype(at::kInt));
   }
-  g.sk_slab = w.slab.data_ptr<float>();
-  g.sk_flags = w.flags.data_ptr<int>();
+  return {w.slab.data_ptr<float>(), w.flags.data_ptr<int>()};
+}
+
+void attach_sk_workspace(dgt::GemmArgs& g, const at::Tensor& like, hipStream_t stream, int64_t slab_floats,
+                         int64_t flag_ints) {
+  std::tie(g.sk_slab, g.sk_flags) = sk_workspace(like, stream, slab_floats, flag_ints);
   static const int xs = [] {
     const char* e = std::getenv("DGT_GEMM_SK_XS");
     return (e && *e) ? std::atoi(e) : 1;

@@ -127,6 +127,14 @@ struct GemmF32Args {
   // optional: the product masked by 1[maskC > 0] ([M, N], row stride N) before it is stored or
   // accumulated -- a dgrad writing the ReLU-masked gradient of the layer below directly
   const float* maskC;
+  // optional split-K across workgroups (gemm_f32_split; the 64x64 K-split-4 tile, no rowsum):
+  // `split` workgroups per output tile, each over 1/split of K; partial tiles go to sk_slab
+  // (tiles * split * 4096 floats) and the last of a tile's workgroups to arrive (counter
+  // sk_flags[tile], zero before and after every launch) sums them in slice order, then runs the
+  // epilogue.  split <= 1: off.
+  float* sk_slab;
+  int* sk_flags;
+  int split;
 };
 // wave tile / workgroup shape: 128x64 waves in 2x2 (256x128 tiles), 64x64 waves in 2x2 (128x128),
 // 64x64 waves 1x2 with K split 2 (64x128), 64x64 waves with K split 4 (64x64)
@@ -137,6 +145,9 @@ struct GemmF32Plan {
 // force_cfg >= 0: that configuration (A/B knob); else the largest wave tile that still gives every
 // SIMD a wave
 GemmF32Plan gemm_f32_plan(int M, int N, int K, int force_cfg = -1);
+// workgroups per output tile for the cross-workgroup split-K of a small grid under `plan` (1: none);
+// force >= 1 caps it (1 = off), force < 0 = the shape rule
+int gemm_f32_split(int M, int N, int K, const GemmF32Plan& plan, int force = -1);
 hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& plan, hipStream_t stream);
 // db[n] (+)= sum_m dy[m][n] * (y ? 1[y[m][n] > 0] : 1) over row slices (part: slices * N floats)
 int colsum_f32_slices(int M, int N);

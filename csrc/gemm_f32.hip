@@ -37,6 +37,8 @@
 //    tiles are summed once at the end through LDS in wave order (deterministic), each wave then
 //    finishing 1/WGK of the tile's rows -- a small grid (1024^3: 64x64 tiles = 256 workgroups =
 //    1,024 waves, one per SIMD) fills the chip without a split-K launch or a reduce kernel;
+//  * smaller grids (fewer than 256 64x64 tiles) also split K across workgroups in the same launch
+//    (gemm_f32_split; the last workgroup of a tile to arrive sums the partials in slice order);
 //  * workgroup ids go through the XCD-aware remap (T1) so an XCD's workgroups share panels in L2.
 // Reference: the fp32 nn.Linear layers of train.py:29-33 (forward train.py:107, backward :113).
 #include "dgt_common.h"
@@ -116,6 +118,20 @@ GemmF32Plan gemm_f32_plan(int M, int N, int K, int force_cfg) {
   return p;
 }
 
+int gemm_f32_split(int M, int N, int K, const GemmF32Plan& p, int force) {
+  // the 64x64 tile with its K split 4 ways inside the workgroup is the small-grid configuration;
+  // when even it leaves SIMDs idle (tiles < 256: e.g. M = 256, N = 1024 is 64 tiles = 256 waves on
+  // 1,024 SIMDs), split K across workgroups too, while every wave keeps >= 4 16-deep chunks.  At
+  // most one workgroup per CU: two (the 64 KiB reduce buffer allows it) measured 1.5-1.9x slower
+  // (profiles/r6_gemm_f32_split_k.jsonl)
+  if (p.cfg != kF32Wave64Split4 || force == 0 || force == 1) return 1;
+  const long long tiles = (long long)((M + 63) / 64) * ((N + 63) / 64);
+  const int cap = force > 1 ? force : 8;
+  int s = 1;
+  while (s < cap && tiles * s * 2 <= 256 && K / (16 * 4 * s * 2) >= 4) s *= 2;
+  return s;
+}
+
 hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& p, hipStream_t stream) {
   if (a.M <= 0 || a.N <= 0 || a.K <= 0 || la < 0 || la > 1 || lb < 0 || lb > 1) return hipErrorInvalidValue;
   // 16-byte loads need the contiguous extent, the leading dims and the bases aligned to 4 floats
@@ -125,6 +141,7 @@ hipError_t gemm_f32(const GemmF32Args& a, int la, int lb, const GemmF32Plan& p, 
                    (a.maskA == nullptr || (uintptr_t)a.maskA % 16 == 0) && ((uintptr_t)a.C % 16 == 0) &&
                    (a.bias == nullptr || (uintptr_t)a.bias % 16 == 0) &&
                    (a.maskC == nullptr || (uintptr_t)a.maskC % 16 == 0);
+  if (a.split > 1 && (p.cfg != kF32Wave64Split4 || a.rowsum || !a.sk_slab || !a.sk_flags)) return hipErrorInvalidValue;
   switch (la * 2 + lb) {
     case 0: return gemm_f32_l00(a, p, vec, stream);
     case 1: return gemm_f32_l01(a, p, vec, stream);

@@ -8,6 +8,7 @@ namespace dgt {
 namespace f32g {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
+typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
 
 // XCD-aware bijective remap (T1): blocks b and b + 8 run on one XCD; each XCD gets a contiguous run
 // of tile ids, walked in groups of GROUP block-rows so neighbours reuse B panels in the XCD's L2.
@@ -122,24 +123,33 @@ DGT_DEVICE int row_of(int r0, int t, int x) {
 // The wave tile is WTM x WTN (16-row tiles TM x TN); the workgroup's 4 waves are WGM x WGN wave
 // tiles x WGK K-slices.  acc[t][u] = the 16x16 output tile of A-tile t and B-tile u; its C/D layout
 // (16x16x4 f32): register r of lane l is row 4 (l >> 4) + r, column l & 15 of the tile.
-template <int LA, int LB, int WTM, int WTN, int WGM, int WGN, int WGK, int H, bool VEC, bool MASKED, bool ROWSUM>
+// SPK: a.split workgroups per tile (blocks tile * split + slice), K cut into split * WGK wave slices;
+// after the in-workgroup sum each workgroup parks its 64x64 partial (16 KiB) in a.sk_slab with
+// write-through (sc1) stores and bumps the tile's counter; the last to arrive sums the partials in
+// slice order (the same bits whoever arrives last), re-arms the counter and runs the epilogue --
+// the pattern of the bf16 small-grid split-K (gemm.hip gemm_nt_kernel SPK).
+template <int LA, int LB, int WTM, int WTN, int WGM, int WGN, int WGK, int H, bool VEC, bool MASKED, bool ROWSUM,
+          bool SPK = false>
 __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32Args a) {
   constexpr int TM = WTM / 16, TN = WTN / 16, BM = WGM * WTM, BN = WGN * WTN;
   constexpr bool AK = LA == 1, BK = LB == 1;  // row-contiguous operands
   static_assert(WGM * WGN * WGK == 4, "4 waves per workgroup");
   static_assert((!AK || TM % 4 == 0) && (!BK || TN % 4 == 0), "row-contiguous tiles come in 64-row groups");
+  static_assert(!SPK || (WTM == 64 && WTN == 64 && WGK == 4 && VEC && !ROWSUM), "split-K: the 64x64 K-split-4 tile");
   // (the wave index through readfirstlane: every per-wave quantity below is a scalar)
   const int lane = threadIdx.x & 63, wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
   const int wk = wave % WGK, wmn = wave / WGK, wm = wmn / WGN, wn = wmn % WGN;
   const int nbm = (a.M + BM - 1) / BM, nbn = (a.N + BN - 1) / BN;
+  const int split = SPK ? a.split : 1;
+  const int tile = SPK ? (int)blockIdx.x / split : (int)blockIdx.x, slice = SPK ? (int)blockIdx.x % split : 0;
   int tm, tn;
-  tile_of(blockIdx.x, nbm, nbn, tm, tn);
+  tile_of(tile, nbm, nbn, tm, tn);
   const int m0 = tm * BM + wm * WTM, n0 = tn * BN + wn * WTN;
   // this wave's K slice, in whole KC-deep chunks; a partial last chunk (K % KC) is peeled below
   constexpr int KC = 16 * H;
   const int nfull = a.K / KC, ntot = (a.K + KC - 1) / KC;
-  const int per = (ntot + WGK - 1) / WGK;
-  const int c0 = wk * per, c1 = min(ntot, c0 + per);
+  const int per = (ntot + WGK * split - 1) / (WGK * split);
+  const int c0 = (slice * WGK + wk) * per, c1 = min(ntot, c0 + per);
   const int f1 = max(c0, min(c1, nfull));  // [c0, f1): full chunks; [f1, c1): at most the partial chunk
 
   f32x4v acc[TM][TN];
@@ -238,6 +248,61 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32Args a) {
         acc[t][u] = v;
       }
     }
+  }
+
+  if constexpr (SPK) {
+    // wave wk holds row tile t = wk of the workgroup's partial: [wave][u][lane] x float4 (picked out
+    // with compile-time indices: acc[wk] would put the whole accumulator array in scratch)
+    f32x4v own[TN];
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+      if (t == wk) {
+#pragma unroll
+        for (int u = 0; u < TN; ++u) own[u] = acc[t][u];
+      }
+    auto part = [&](int z) {
+      return __builtin_amdgcn_make_buffer_rsrc(a.sk_slab + ((long long)tile * split + z) * (WTM * WTN), 0,
+                                               WTM * WTN * 4, 0x00020000);
+    };
+    const auto mine = part(slice);
+#pragma unroll
+    for (int u = 0; u < TN; ++u)
+      __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u32x4v, own[u]), mine,
+                                             ((wave * TN + u) * 64 + lane) * 16, 0, 16 /* sc1 */);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every storing wave drains its stores
+    __syncthreads();                                   // (and every wave is done reading `red`)
+    int* word = reinterpret_cast<int*>(red);
+    if (threadIdx.x == 0) *word = __hip_atomic_fetch_add(a.sk_flags + tile, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __syncthreads();
+    if (*word != split - 1) return;  // not the last slice to arrive
+    if (threadIdx.x == 0) __hip_atomic_store(a.sk_flags + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    // every load of a partial is an sc1 load behind the counter's add and the barrier above
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    f32x4v sum[TN];
+#pragma unroll
+    for (int u = 0; u < TN; ++u) sum[u] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll 1
+    for (int z = 0; z < split; ++z) {  // slice order
+      f32x4v p[TN];
+      if (z == slice) {
+#pragma unroll
+        for (int u = 0; u < TN; ++u) p[u] = own[u];
+      } else {
+        const auto rs = part(z);
+#pragma unroll
+        for (int u = 0; u < TN; ++u)
+          p[u] = __builtin_bit_cast(
+              f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((wave * TN + u) * 64 + lane) * 16, 0, 16));
+      }
+#pragma unroll
+      for (int u = 0; u < TN; ++u) sum[u] += p[u];
+    }
+#pragma unroll
+    for (int t = 0; t < TM; ++t)
+      if (t == wk) {
+#pragma unroll
+        for (int u = 0; u < TN; ++u) acc[t][u] = sum[u];
+      }
   }
 
   // ---- row sums (the wgrad's bias gradient): lanes of one row sum over k quads q, then slices
@@ -389,6 +454,18 @@ hipError_t launch(const GemmF32Args& a, bool vec, hipStream_t stream) {
 #define DGT_F32_LAUNCH(V, MK, RS)                                                                          \
   {                                                                                                    \
     hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, WTM, WTN, WGM, WGN, WGK, H, V, MK, RS>), grid, block, 0, stream, a); \
+  }
+  if constexpr (SCALAR_OK) {  // the small-grid split-K (gemm_f32_split)
+    if (vec && a.split > 1 && a.rowsum == nullptr) {
+      const dim3 sgrid((unsigned)(tiles * a.split));
+      if (a.maskA)
+        hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, WTM, WTN, WGM, WGN, WGK, H, true, true, false, true>), sgrid, block,
+                           0, stream, a);
+      else
+        hipLaunchKernelGGL((gemm_f32_kernel<LA, LB, WTM, WTN, WGM, WGN, WGK, H, true, false, false, true>), sgrid, block,
+                           0, stream, a);
+      return hipGetLastError();
+    }
   }
   // (the ReLU-masked A and the fused row sums come together in a wgrad: MASKED and ROWSUM share
   // one instantiation pair)

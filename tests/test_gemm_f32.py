@@ -281,3 +281,98 @@ def test_engine_fp32_mlp_runs_no_vendor_gemm():
     # differs between two fp32 summation orders moves apart by up to 2 lr per step
     torch.testing.assert_close(got, want, rtol=0, atol=1e-3)
     engine.close()
+
+
+# Small grids that the 64x64 K-split-4 tile still leaves under-filled (tiles < 256): the GEMM splits
+# K across workgroups too (gemm_f32_split) and the last workgroup of a tile to arrive sums the
+# partials in slice order.  Aligned, ragged M / N, a K tail that is not a whole 16-deep chunk.
+SPLIT_SHAPES = [(256, 1024, 1024), (128, 512, 4096), (192, 320, 2004), (100, 200, 3000), (64, 64, 8192)]
+
+
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 1), (1, 0)])
+@pytest.mark.parametrize("M,N,K", SPLIT_SHAPES)
+def test_gemm_f32_split_k_layouts(M, N, K, la, lb):
+    ops = _ops()
+    a, b, A, B = _operands(M, N, K, la, lb, seed=N)
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm_f32(A, B, None, None, C, la, lb, False, False)
+    _close(C, _ref(a, b), a, b)
+
+
+@pytest.mark.parametrize("M,N,K", SPLIT_SHAPES)
+def test_gemm_f32_split_k_epilogues(M, N, K):
+    """Bias + ReLU, accumulate, the ReLU mask on A and the output mask run once per tile, by the
+    workgroup that sums the partials."""
+    ops = _ops()
+    a, b, A, B = _operands(M, N, K, 0, 0, seed=7)
+    bias = torch.randn(N, device="cuda")
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm_f32(A, B, None, bias, C, 0, 0, True, False)
+    _close(C, _ref(a, b, bias, relu=True), a, b)
+    C0 = torch.randn(M, N, device="cuda")
+    C = C0.clone()
+    ops.gemm_f32(A, B, None, None, C, 0, 0, False, True)
+    _close(C, C0.double() + _ref(a, b), a, b)
+    mask = torch.randn(M, K, device="cuda")
+    mk = torch.randn(M, N, device="cuda")
+    Bt = b.t().contiguous()
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm_f32(A, Bt, mask, None, C, 0, 1, False, False, None, mk)  # the dgrad form
+    _close(C, torch.where(mk > 0, _ref(a, b, mask=mask), torch.zeros((), dtype=torch.float64, device="cuda")), a, b)
+
+
+@pytest.mark.parametrize("M,N,K", [(256, 1024, 1024), (192, 320, 2004)])
+def test_gemm_f32_split_k_deterministic_and_rearmed(M, N, K):
+    """The slice-order sum gives the same bits on every call whichever workgroup arrives last, and
+    each launch leaves the tile counters at zero (a stale counter would skip the epilogue: C keeps
+    its NaN fill); also across a second stream (its own workspace)."""
+    ops = _ops()
+    a, b, A, B = _operands(M, N, K, 0, 0, seed=3)
+    first = None
+    side = torch.cuda.Stream()
+    for i in range(6):
+        C = torch.full((M, N), float("nan"), device="cuda")
+        if i % 2:
+            side.wait_stream(torch.cuda.current_stream())
+            with torch.cuda.stream(side):
+                ops.gemm_f32(A, B, None, None, C, 0, 0, False, False)
+            torch.cuda.current_stream().wait_stream(side)
+        else:
+            ops.gemm_f32(A, B, None, None, C, 0, 0, False, False)
+        assert not C.isnan().any()
+        if first is None:
+            first = C
+            _close(C, _ref(a, b), a, b)
+        else:
+            assert torch.equal(C, first)
+
+
+def test_gemm_f32_split_k_knob_off_matches_reference(tmp_path):
+    """DGT_F32_SPLIT=1 turns the cross-workgroup split off (read once per process): a subprocess
+    computes the same product without it; both agree with the fp64 reference and differ only by
+    summation order."""
+    import os
+    import subprocess
+    import sys
+    M, N, K = 256, 1024, 1024
+    ops = _ops()
+    a, b, A, B = _operands(M, N, K, 0, 0, seed=11)
+    C = torch.empty(M, N, device="cuda")
+    ops.gemm_f32(A, B, None, None, C, 0, 0, False, False)
+    src = (
+        "import torch\n"
+        "from distributed_gpu_test_amd.ops import _ext\n"
+        "ops = _ext.require()\n"
+        f"g = torch.Generator(device='cuda').manual_seed(11)\n"
+        f"a = torch.randn({M}, {K}, device='cuda', generator=g); b = torch.randn({N}, {K}, device='cuda', generator=g)\n"
+        f"C = torch.empty({M}, {N}, device='cuda')\n"
+        "ops.gemm_f32(a, b, None, None, C, 0, 0, False, False)\n"
+        f"torch.save(C.cpu(), {str(tmp_path / 'c.pt')!r})\n")
+    env = dict(os.environ, DGT_F32_SPLIT="1")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, "-c", src], env=env, cwd=root, capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    off = torch.load(tmp_path / "c.pt", weights_only=True).cuda()
+    _close(off, _ref(a, b), a, b)
+    _close(C, _ref(a, b), a, b)
+    assert not torch.equal(off, C)  # a different summation order: the split path did run
