@@ -41,6 +41,8 @@
 //    (gemm_f32_split; the last workgroup of a tile to arrive sums the partials in slice order);
 //  * workgroup ids go through the XCD-aware remap (T1) so an XCD's workgroups share panels in L2.
 // Reference: the fp32 nn.Linear layers of train.py:29-33 (forward train.py:107, backward :113).
+#include <algorithm>
+
 #include "dgt_common.h"
 #include "dgt_kernels.h"
 
@@ -126,7 +128,7 @@ int gemm_f32_split(int M, int N, int K, const GemmF32Plan& p, int force) {
   // (profiles/r6_gemm_f32_split_k.jsonl)
   if (p.cfg != kF32Wave64Split4 || force == 0 || force == 1) return 1;
   const long long tiles = (long long)((M + 63) / 64) * ((N + 63) / 64);
-  const int cap = force > 1 ? force : 8;
+  const int cap = force > 1 ? std::min(force, 8) : 8;  // (f32g::kF32MaxSplit)
   int s = 1;
   while (s < cap && tiles * s * 2 <= 256 && K / (16 * 4 * s * 2) >= 4) s *= 2;
   return s;

@@ -9,6 +9,7 @@ namespace f32g {
 
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef unsigned int u32x4v __attribute__((ext_vector_type(4)));
+constexpr int kF32MaxSplit = 8;  // gemm_f32_split's cap
 
 // XCD-aware bijective remap (T1): blocks b and b + 8 run on one XCD; each XCD gets a contiguous run
 // of tile ids, walked in groups of GROUP block-rows so neighbours reuse B panels in the XCD's L2.
@@ -278,25 +279,27 @@ __global__ __launch_bounds__(256, 1) void gemm_f32_kernel(GemmF32Args a) {
     if (threadIdx.x == 0) __hip_atomic_store(a.sk_flags + tile, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     // every load of a partial is an sc1 load behind the counter's add and the barrier above
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    f32x4v sum[TN];
+    // every partial's loads are issued before the first add (own slot included: this workgroup's
+    // stores drained above), so the cross-XCD round trips overlap instead of running one per slice
+    f32x4v p[kF32MaxSplit][TN];
 #pragma unroll
-    for (int u = 0; u < TN; ++u) sum[u] = f32x4v{0.f, 0.f, 0.f, 0.f};
-#pragma unroll 1
-    for (int z = 0; z < split; ++z) {  // slice order
-      f32x4v p[TN];
-      if (z == slice) {
-#pragma unroll
-        for (int u = 0; u < TN; ++u) p[u] = own[u];
-      } else {
+    for (int z = 0; z < kF32MaxSplit; ++z)
+      if (z < split) {
         const auto rs = part(z);
 #pragma unroll
         for (int u = 0; u < TN; ++u)
-          p[u] = __builtin_bit_cast(
+          p[z][u] = __builtin_bit_cast(
               f32x4v, __builtin_amdgcn_raw_buffer_load_b128(rs, ((wave * TN + u) * 64 + lane) * 16, 0, 16));
       }
+    f32x4v sum[TN];
 #pragma unroll
-      for (int u = 0; u < TN; ++u) sum[u] += p[u];
-    }
+    for (int u = 0; u < TN; ++u) sum[u] = f32x4v{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int z = 0; z < kF32MaxSplit; ++z)  // slice order: the same bits whoever arrived last
+      if (z < split) {
+#pragma unroll
+        for (int u = 0; u < TN; ++u) sum[u] += p[z][u];
+      }
 #pragma unroll
     for (int t = 0; t < TM; ++t)
       if (t == wk) {
