@@ -5,7 +5,7 @@ set -o pipefail
 O=gpurun_out/r6fp32b; mkdir -p gpurun_out/r6fp32p
 mkdir -p $O
 export TMPDIR=/tmp
-for B in 256 1024; do
+for B in ${BATCHES:-256 1024}; do
   timeout -k 10 200 python bench.py --model mlp --impl dgt-engine --width 1024 --batch $B --deepspeed-config configs/ds_bench_mlp_fp32.json \
     --steps 200 --warmup 20 --no-sweep --no-secondary --no-baselines > $O/ours_$B.json 2> $O/ours_$B.err || { tail -20 $O/ours_$B.err; exit 1; }
   timeout -k 10 200 python bench.py --model mlp --impl engine --torch-dtype fp32 --width 1024 --batch $B \
